@@ -1,0 +1,151 @@
+/*
+ * openr_spf.h — the C ABI of the MI355X SPF engine (the ONLY entry point to
+ * the HIP kernels).  Plain pointers and sizes, no C++ or torch types.
+ *
+ * What it replaces.  Open/R has no FFI for this path: the boundary is the C++
+ * class API of LinkState / SpfSolver.  Every function below replaces the inner
+ * arithmetic of one reference member function; the re-implemented LinkState
+ * (openr_amd/csrc/host/LinkState.cpp) is the only caller:
+ *
+ *   spf_graph_create / spf_graph_destroy
+ *       replaces the adjacency graph the reference walks in place:
+ *       LinkState::linkMap_ / nodeOverloads_   (openr/decision/LinkState.h:457-463)
+ *       and Link::isUp / getMetricFromNode     (openr/decision/LinkState.cpp:195-236)
+ *   spf_graph_set_transit
+ *       replaces LinkState::isNodeOverloaded as read by runSpf
+ *                                               (openr/decision/LinkState.cpp:829-836)
+ *   spf_query_create / spf_query_run / spf_query_sync
+ *       replaces LinkState::runSpf(src, useLinkMetric, linksToIgnore)
+ *                                               (openr/decision/LinkState.cpp:806-880)
+ *       batched over many sources (getSpfResult memo fill, LFA neighbours,
+ *       all-sources views, KSP2 second passes, what-if link failures).
+ *   spf_query_dist / spf_query_nexthops / spf_query_order
+ *       replace the reads of NodeSpfResult::metric / nextHops / pathLinks
+ *       order                                   (openr/decision/LinkState.h:203-257)
+ *
+ * Conventions
+ *   - Status: 0 = OK, negative = error (SPF_E_*).  No exceptions cross the ABI.
+ *   - Ownership: every device buffer is owned by the handle that allocated it.
+ *     Host buffers passed in are read during the call only; host output
+ *     buffers are caller-allocated and filled synchronously.
+ *   - Threading: a graph and its queries are used from one host thread.  All
+ *     work of a graph is enqueued on one HIP stream (spf_graph_set_stream).
+ *   - Node ids are 0..V-1 and MUST equal the lexicographic rank of the node
+ *     name (the reference breaks Dijkstra ties by name, LinkState.h:488-498).
+ *   - There is no CPU fallback: without a usable gfx950 device every call that
+ *     needs one returns SPF_E_DEVICE.
+ */
+#ifndef OPENR_SPF_H
+#define OPENR_SPF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPF_OK 0
+#define SPF_E_INVALID (-1)     /* bad argument / shape */
+#define SPF_E_NOMEM (-2)       /* device or host allocation failed */
+#define SPF_E_DEVICE (-3)      /* HIP runtime error / no device */
+#define SPF_E_UNSUPPORTED (-4) /* shape outside what the kernels handle */
+
+#define SPF_UNREACHABLE UINT64_MAX
+
+/* query flags */
+#define SPF_F_UNIT_METRIC 0x1u /* useLinkMetric == false: every hop costs 1 */
+#define SPF_F_NEXTHOPS 0x2u    /* compute ECMP next-hop sets */
+#define SPF_F_ORDER 0x4u       /* keep the settle order (pathLinks ordering) */
+
+/* Directed CSR of the UP links of one area (Link::isUp, LinkState.cpp:233).
+ * Every undirected link contributes two half-edges e (u->v) and rev[e]
+ * (v->u) that share link_id.  metric[e] is the metric advertised by the row
+ * node u (Link::getMetricFromNode(u)), as the reference's uint64
+ * LinkStateMetric (an i32 adjacency metric sign-extended, LinkState.h:22). */
+typedef struct spf_graph_desc {
+  uint32_t num_nodes;             /* V */
+  uint32_t num_edges;             /* E (directed half-edges) */
+  const uint32_t* row_ptr;        /* [V+1] */
+  const uint32_t* col;            /* [E] other endpoint */
+  const uint64_t* metric;         /* [E] metric advertised by the row node */
+  const uint32_t* link_id;        /* [E] undirected link id (< num_links) */
+  const uint32_t* rev;            /* [E] index of the reverse half-edge */
+  const uint8_t* node_overloaded; /* [V] 1 = no transit (isNodeOverloaded) */
+  uint32_t num_links;             /* number of distinct link ids */
+  int device;                     /* HIP device ordinal */
+} spf_graph_desc;
+
+typedef struct spf_graph spf_graph;
+typedef struct spf_query spf_query;
+
+/* One batch of single-source SPF runs.  Query i runs from sources[i]; when
+ * ignore_offsets is non-NULL query i skips the links
+ * ignore_links[ignore_offsets[i] .. ignore_offsets[i+1]) (sorted ascending,
+ * the linksToIgnore set of LinkState::runSpf / getKthPaths k>=2). */
+typedef struct spf_query_desc {
+  uint32_t num_queries;
+  const uint32_t* sources;        /* [num_queries] */
+  const uint32_t* ignore_offsets; /* [num_queries+1] or NULL */
+  const uint32_t* ignore_links;   /* sorted per query, or NULL */
+  uint32_t flags;                 /* SPF_F_* */
+} spf_query_desc;
+
+/* ---- device ---- */
+int spf_device_count(void);
+const char* spf_error_string(int status);
+const char* spf_last_error_detail(void); /* thread-local text of last error */
+
+/* ---- graph ---- */
+int spf_graph_create(const spf_graph_desc* desc, spf_graph** out);
+int spf_graph_destroy(spf_graph* g);
+/* Replace the per-node transit bits (overload/drain) in place: node
+ * overload toggles are the common churn (DecisionBenchmark.cpp:600-626). */
+int spf_graph_set_transit(spf_graph* g, const uint8_t* node_overloaded);
+/* Patch metrics of existing half-edges in place (metric churn, a7 deltas). */
+int spf_graph_patch_metrics(
+    spf_graph* g, uint32_t n, const uint32_t* edge_idx, const uint64_t* metric);
+/* Work of this graph is enqueued on `stream` (a hipStream_t, NULL = the
+ * graph's own stream). */
+int spf_graph_set_stream(spf_graph* g, void* stream);
+void* spf_graph_get_stream(spf_graph* g);
+/* 1 if metric runs on this graph need the exact (metric-0 / 64-bit) kernel. */
+int spf_graph_needs_exact(const spf_graph* g);
+/* Number of distinct neighbours of `node` = bits in its next-hop masks. */
+int spf_graph_num_nbrs(const spf_graph* g, uint32_t node);
+/* The distinct neighbours of `node`, ascending by id; bit b of a next-hop
+ * mask of a query from `node` stands for out[b]. */
+int spf_graph_nbrs(const spf_graph* g, uint32_t node, uint32_t* out);
+
+/* ---- queries ---- */
+int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out);
+int spf_query_destroy(spf_query* q);
+/* Enqueue the batch on the graph stream (asynchronous). */
+int spf_query_run(spf_query* q);
+/* Wait for the last run to finish. */
+int spf_query_sync(spf_query* q);
+/* Device time of the last run's kernels (HIP events), milliseconds. */
+int spf_query_elapsed_ms(spf_query* q, float* ms);
+/* Name of the kernel the last run used ("lds", "gmem", "exact"). */
+const char* spf_query_kernel_name(const spf_query* q);
+
+/* Distances of query i, one per node; SPF_UNREACHABLE = not reached. */
+int spf_query_dist(spf_query* q, uint32_t i, uint64_t* out /*[V]*/);
+/* Words per next-hop mask of query i (ceil(nbrs(src)/64), at least 1). */
+int spf_query_nh_words(const spf_query* q, uint32_t i);
+/* Next-hop masks of query i: out[v*W + w], W = spf_query_nh_words. */
+int spf_query_nexthops(spf_query* q, uint32_t i, uint64_t* out /*[V*W]*/);
+/* Settle rank of every node for query i (SPF_F_ORDER): the order in which the
+ * reference's DijkstraQ extracts nodes; UINT32_MAX = not reached. */
+int spf_query_order(spf_query* q, uint32_t i, uint32_t* out /*[V]*/);
+/* Device pointers of the result rows (for RCCL gathers): dist rows are
+ * uint32 (fast kernels) or uint64 (exact kernel) of V entries per query. */
+int spf_query_device_rows(
+    spf_query* q, void** dist_rows, uint32_t* dist_elem_bytes,
+    void** nh_rows, uint64_t* nh_total_words);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OPENR_SPF_H */

@@ -1,0 +1,376 @@
+"""ctypes view of the C ABI in include/openr_spf.h.
+
+This is how Python (tests, bench.py) reaches the HIP engine directly; the C++
+LinkState/SpfSolver re-implementation (openr_amd/csrc/host) links the same
+shared library.  There is deliberately no fallback: if libopenr_spf.so is
+missing or the device is unusable, the calls raise.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libopenr_spf.so")
+
+SPF_OK = 0
+SPF_UNREACHABLE = (1 << 64) - 1
+SPF_F_UNIT_METRIC = 0x1
+SPF_F_NEXTHOPS = 0x2
+SPF_F_ORDER = 0x4
+
+# every symbol include/openr_spf.h declares (tests check the .so exports them)
+EXPORTED_SYMBOLS = (
+    "spf_device_count",
+    "spf_error_string",
+    "spf_last_error_detail",
+    "spf_graph_create",
+    "spf_graph_destroy",
+    "spf_graph_set_transit",
+    "spf_graph_patch_metrics",
+    "spf_graph_set_stream",
+    "spf_graph_get_stream",
+    "spf_graph_needs_exact",
+    "spf_graph_num_nbrs",
+    "spf_graph_nbrs",
+    "spf_query_create",
+    "spf_query_destroy",
+    "spf_query_run",
+    "spf_query_sync",
+    "spf_query_elapsed_ms",
+    "spf_query_kernel_name",
+    "spf_query_dist",
+    "spf_query_nh_words",
+    "spf_query_nexthops",
+    "spf_query_order",
+    "spf_query_device_rows",
+)
+
+
+class SpfError(RuntimeError):
+    pass
+
+
+class _GraphDesc(C.Structure):
+    _fields_ = [
+        ("num_nodes", C.c_uint32),
+        ("num_edges", C.c_uint32),
+        ("row_ptr", C.POINTER(C.c_uint32)),
+        ("col", C.POINTER(C.c_uint32)),
+        ("metric", C.POINTER(C.c_uint64)),
+        ("link_id", C.POINTER(C.c_uint32)),
+        ("rev", C.POINTER(C.c_uint32)),
+        ("node_overloaded", C.POINTER(C.c_uint8)),
+        ("num_links", C.c_uint32),
+        ("device", C.c_int),
+    ]
+
+
+class _QueryDesc(C.Structure):
+    _fields_ = [
+        ("num_queries", C.c_uint32),
+        ("sources", C.POINTER(C.c_uint32)),
+        ("ignore_offsets", C.POINTER(C.c_uint32)),
+        ("ignore_links", C.POINTER(C.c_uint32)),
+        ("flags", C.c_uint32),
+    ]
+
+
+_lib = None
+
+
+def load():
+    """Load libopenr_spf.so (raises OSError if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OSError(
+            f"{LIB_PATH} missing: run `python -m openr_amd.build` "
+            "(the HIP engine has no CPU fallback)"
+        )
+    lib = C.CDLL(LIB_PATH)
+    vp = C.c_void_p
+    u32 = C.c_uint32
+    pu32 = C.POINTER(C.c_uint32)
+    pu64 = C.POINTER(C.c_uint64)
+    sig = {
+        "spf_device_count": (C.c_int, []),
+        "spf_error_string": (C.c_char_p, [C.c_int]),
+        "spf_last_error_detail": (C.c_char_p, []),
+        "spf_graph_create": (C.c_int, [C.POINTER(_GraphDesc), C.POINTER(vp)]),
+        "spf_graph_destroy": (C.c_int, [vp]),
+        "spf_graph_set_transit": (C.c_int, [vp, C.POINTER(C.c_uint8)]),
+        "spf_graph_patch_metrics": (C.c_int, [vp, u32, pu32, pu64]),
+        "spf_graph_set_stream": (C.c_int, [vp, vp]),
+        "spf_graph_get_stream": (vp, [vp]),
+        "spf_graph_needs_exact": (C.c_int, [vp]),
+        "spf_graph_num_nbrs": (C.c_int, [vp, u32]),
+        "spf_graph_nbrs": (C.c_int, [vp, u32, pu32]),
+        "spf_query_create": (C.c_int, [vp, C.POINTER(_QueryDesc), C.POINTER(vp)]),
+        "spf_query_destroy": (C.c_int, [vp]),
+        "spf_query_run": (C.c_int, [vp]),
+        "spf_query_sync": (C.c_int, [vp]),
+        "spf_query_elapsed_ms": (C.c_int, [vp, C.POINTER(C.c_float)]),
+        "spf_query_kernel_name": (C.c_char_p, [vp]),
+        "spf_query_dist": (C.c_int, [vp, u32, pu64]),
+        "spf_query_nh_words": (C.c_int, [vp, u32]),
+        "spf_query_nexthops": (C.c_int, [vp, u32, pu64]),
+        "spf_query_order": (C.c_int, [vp, u32, pu32]),
+        "spf_query_device_rows": (
+            C.c_int,
+            [vp, C.POINTER(vp), pu32, C.POINTER(vp), pu64],
+        ),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(status: int, what: str):
+    if status != SPF_OK:
+        lib = load()
+        raise SpfError(
+            f"{what}: {lib.spf_error_string(status).decode()} "
+            f"({lib.spf_last_error_detail().decode()})"
+        )
+
+
+def _p(arr, ctype):
+    return arr.ctypes.data_as(C.POINTER(ctype))
+
+
+def device_count() -> int:
+    return load().spf_device_count()
+
+
+@dataclass
+class Csr:
+    """Directed CSR of the up links of one area (see spf_graph_desc)."""
+
+    num_nodes: int
+    row_ptr: np.ndarray  # uint32 [V+1]
+    col: np.ndarray  # uint32 [E]
+    metric: np.ndarray  # uint64 [E]
+    link_id: np.ndarray  # uint32 [E]
+    rev: np.ndarray  # uint32 [E]
+    overloaded: np.ndarray  # uint8 [V]
+    num_links: int
+
+    @staticmethod
+    def from_links(num_nodes, links, overloaded=None):
+        """links: iterable of (u, v, metric_u_to_v, metric_v_to_u).
+
+        Half-edges of one row keep the input order of `links`.
+        """
+        links = list(links)
+        V = int(num_nodes)
+        deg = np.zeros(V + 1, dtype=np.int64)
+        for (u, v, _, _) in links:
+            deg[u + 1] += 1
+            deg[v + 1] += 1
+        row = np.cumsum(deg).astype(np.uint32)
+        E = int(row[-1])
+        fill = row[:-1].astype(np.int64).copy()
+        col = np.zeros(E, dtype=np.uint32)
+        met = np.zeros(E, dtype=np.uint64)
+        lid = np.zeros(E, dtype=np.uint32)
+        rev = np.zeros(E, dtype=np.uint32)
+        for i, (u, v, muv, mvu) in enumerate(links):
+            eu = fill[u]
+            fill[u] += 1
+            ev = fill[v]
+            fill[v] += 1
+            col[eu], met[eu], lid[eu], rev[eu] = v, np.uint64(muv % (1 << 64)), i, ev
+            col[ev], met[ev], lid[ev], rev[ev] = u, np.uint64(mvu % (1 << 64)), i, eu
+        ov = (
+            np.zeros(V, dtype=np.uint8)
+            if overloaded is None
+            else np.asarray(overloaded, dtype=np.uint8)
+        )
+        return Csr(V, row, col, met, lid, rev, ov, len(links))
+
+
+class Graph:
+    def __init__(self, csr: Csr, device: int = 0):
+        lib = load()
+        self.csr = csr
+        self._keep = [
+            np.ascontiguousarray(csr.row_ptr, dtype=np.uint32),
+            np.ascontiguousarray(csr.col, dtype=np.uint32),
+            np.ascontiguousarray(csr.metric, dtype=np.uint64),
+            np.ascontiguousarray(csr.link_id, dtype=np.uint32),
+            np.ascontiguousarray(csr.rev, dtype=np.uint32),
+            np.ascontiguousarray(csr.overloaded, dtype=np.uint8),
+        ]
+        row, col, met, lid, rev, ov = self._keep
+        d = _GraphDesc(
+            csr.num_nodes,
+            len(col),
+            _p(row, C.c_uint32),
+            _p(col, C.c_uint32),
+            _p(met, C.c_uint64),
+            _p(lid, C.c_uint32),
+            _p(rev, C.c_uint32),
+            _p(ov, C.c_uint8),
+            csr.num_links,
+            device,
+        )
+        h = C.c_void_p()
+        _check(lib.spf_graph_create(C.byref(d), C.byref(h)), "spf_graph_create")
+        self.h = h
+        self.V = csr.num_nodes
+
+    def close(self):
+        if self.h:
+            load().spf_graph_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def needs_exact(self) -> bool:
+        return bool(load().spf_graph_needs_exact(self.h))
+
+    def nbrs(self, node: int) -> np.ndarray:
+        lib = load()
+        n = lib.spf_graph_num_nbrs(self.h, node)
+        if n < 0:
+            _check(n, "spf_graph_num_nbrs")
+        out = np.zeros(max(n, 1), dtype=np.uint32)
+        _check(lib.spf_graph_nbrs(self.h, node, _p(out, C.c_uint32)), "nbrs")
+        return out[:n]
+
+    def set_transit(self, overloaded):
+        ov = np.ascontiguousarray(overloaded, dtype=np.uint8)
+        _check(load().spf_graph_set_transit(self.h, _p(ov, C.c_uint8)), "transit")
+
+    def set_stream(self, stream_ptr: int | None):
+        _check(load().spf_graph_set_stream(self.h, stream_ptr), "set_stream")
+
+    def query(self, sources, flags=SPF_F_NEXTHOPS, ignore=None) -> "Query":
+        return Query(self, sources, flags, ignore)
+
+
+class Query:
+    def __init__(self, graph: Graph, sources, flags, ignore=None):
+        lib = load()
+        self.graph = graph
+        src = np.ascontiguousarray(sources, dtype=np.uint32)
+        keep = [src]
+        ioff = ilinks = None
+        if ignore is not None:
+            offs = [0]
+            flat = []
+            for lst in ignore:
+                s = sorted(set(int(x) for x in lst))
+                flat.extend(s)
+                offs.append(len(flat))
+            ioff = np.asarray(offs, dtype=np.uint32)
+            ilinks = np.asarray(flat if flat else [0], dtype=np.uint32)
+            keep += [ioff, ilinks]
+        d = _QueryDesc(
+            len(src),
+            _p(src, C.c_uint32),
+            _p(ioff, C.c_uint32) if ioff is not None else None,
+            _p(ilinks, C.c_uint32) if ilinks is not None else None,
+            flags,
+        )
+        h = C.c_void_p()
+        _check(lib.spf_query_create(graph.h, C.byref(d), C.byref(h)), "spf_query_create")
+        self.h = h
+        self._keep = keep
+        self.n = len(src)
+        self.flags = flags
+
+    def close(self):
+        if self.h:
+            load().spf_query_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def run(self, sync=True):
+        lib = load()
+        _check(lib.spf_query_run(self.h), "spf_query_run")
+        if sync:
+            _check(lib.spf_query_sync(self.h), "spf_query_sync")
+        return self
+
+    def sync(self):
+        _check(load().spf_query_sync(self.h), "spf_query_sync")
+
+    def elapsed_ms(self) -> float:
+        ms = C.c_float()
+        _check(load().spf_query_elapsed_ms(self.h, C.byref(ms)), "elapsed")
+        return float(ms.value)
+
+    @property
+    def kernel(self) -> str:
+        return load().spf_query_kernel_name(self.h).decode()
+
+    def dist(self, i: int) -> np.ndarray:
+        out = np.zeros(self.graph.V, dtype=np.uint64)
+        _check(load().spf_query_dist(self.h, i, _p(out, C.c_uint64)), "dist")
+        return out
+
+    def nh_words(self, i: int) -> int:
+        return load().spf_query_nh_words(self.h, i)
+
+    def nexthops(self, i: int) -> np.ndarray:
+        W = self.nh_words(i)
+        out = np.zeros(self.graph.V * W, dtype=np.uint64)
+        _check(load().spf_query_nexthops(self.h, i, _p(out, C.c_uint64)), "nexthops")
+        return out.reshape(self.graph.V, W)
+
+    def nexthop_sets(self, i: int, src: int):
+        """{node: frozenset(first-hop node ids)} for reached nodes."""
+        d = self.dist(i)
+        masks = self.nexthops(i)
+        nb = self.graph.nbrs(src)
+        out = {}
+        for v in range(self.graph.V):
+            if d[v] == np.uint64(SPF_UNREACHABLE):
+                continue
+            s = set()
+            for w in range(masks.shape[1]):
+                m = int(masks[v, w])
+                while m:
+                    b = (m & -m).bit_length() - 1
+                    s.add(int(nb[w * 64 + b]))
+                    m &= m - 1
+            out[v] = frozenset(s)
+        return out
+
+    def order(self, i: int) -> np.ndarray:
+        out = np.zeros(self.graph.V, dtype=np.uint32)
+        _check(load().spf_query_order(self.h, i, _p(out, C.c_uint32)), "order")
+        return out
+
+    def device_rows(self):
+        dp = C.c_void_p()
+        eb = C.c_uint32()
+        np_ = C.c_void_p()
+        nt = C.c_uint64()
+        _check(
+            load().spf_query_device_rows(
+                self.h, C.byref(dp), C.byref(eb), C.byref(np_), C.byref(nt)
+            ),
+            "device_rows",
+        )
+        return dp.value, eb.value, np_.value, nt.value

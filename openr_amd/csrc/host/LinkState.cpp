@@ -1,0 +1,1131 @@
+// LinkState.cpp — graph bookkeeping of the reference LinkState
+// (openr/decision/LinkState.cpp) on top of the MI355X SPF engine.
+//
+// Graph maintenance (links exist only when both ends advertise each other,
+// HoldableValue holds, change flags) follows the reference semantics line by
+// line because its outputs are asserted by the reference tests.  Shortest
+// paths come from libopenr_spf (include/openr_spf.h): the up-link graph is
+// flattened once per topology version into a device CSR whose node ids are
+// name ranks and whose rows list links in linksFromNode() iteration order.
+
+#include "LinkState.h"
+
+#include <chrono>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+
+#include "openr_spf.h"
+
+namespace openr {
+
+// ------------------------------------------------------------------ counters
+
+namespace {
+std::mutex& counterMutex() {
+  static std::mutex m;
+  return m;
+}
+std::unordered_map<std::string, int64_t>& counterMap() {
+  static std::unordered_map<std::string, int64_t> m;
+  return m;
+}
+int& spfDevice() {
+  static int d = 0;
+  return d;
+}
+} // namespace
+
+void Counters::add(const std::string& key, int64_t v) {
+  std::lock_guard<std::mutex> g(counterMutex());
+  counterMap()[key] += v;
+}
+int64_t Counters::get(const std::string& key) {
+  std::lock_guard<std::mutex> g(counterMutex());
+  auto it = counterMap().find(key);
+  return it == counterMap().end() ? 0 : it->second;
+}
+std::unordered_map<std::string, int64_t> Counters::snapshot() {
+  std::lock_guard<std::mutex> g(counterMutex());
+  return counterMap();
+}
+void Counters::reset() {
+  std::lock_guard<std::mutex> g(counterMutex());
+  counterMap().clear();
+}
+
+void setSpfDevice(int device) { spfDevice() = device; }
+int getSpfDevice() { return spfDevice(); }
+
+// --------------------------------------------------------------- hashing
+
+namespace {
+// folly::hash::hash_128_to_64 — folly's std::hash<std::pair> combines the two
+// member hashes with it (folly/hash/Hash.h @ ab8339ea).  Link::hash feeds
+// Link::operator< and the bucket order of every LinkSet, and that order picks
+// the parallel link a KSP2 trace takes (DecisionTest.cpp:3276-3279).
+inline uint64_t hash128to64(uint64_t upper, uint64_t lower) {
+  const uint64_t kMul = 0x9ddfea08eb382d69ULL;
+  uint64_t a = (lower ^ upper) * kMul;
+  a ^= (a >> 47);
+  uint64_t b = (upper ^ a) * kMul;
+  b ^= (b >> 47);
+  b *= kMul;
+  return b;
+}
+inline size_t hashStrPair(const std::pair<std::string, std::string>& p) {
+  return hash128to64(
+      std::hash<std::string>()(p.first), std::hash<std::string>()(p.second));
+}
+} // namespace
+
+size_t LinkState::KthKeyHash::operator()(const KthKey& key) const {
+  return hash128to64(
+      hash128to64(std::hash<std::string>()(key.src), std::hash<std::string>()(key.dst)),
+      key.k);
+}
+
+// ---------------------------------------------------------- HoldableValue
+
+template <class T>
+HoldableValue<T>::HoldableValue(T val) : val_(val) {}
+
+template <class T>
+void HoldableValue<T>::operator=(T val) {
+  val_ = val;
+  heldVal_.reset();
+  holdTtl_ = 0;
+}
+
+template <class T>
+const T& HoldableValue<T>::value() const {
+  if (heldVal_) {
+    return *heldVal_;
+  }
+  return val_;
+}
+
+template <class T>
+bool HoldableValue<T>::hasHold() const {
+  return heldVal_.has_value();
+}
+
+template <class T>
+bool HoldableValue<T>::decrementTtl() {
+  if (!heldVal_) {
+    return false;
+  }
+  if (--holdTtl_ != 0) {
+    return false;
+  }
+  heldVal_.reset();
+  return true;
+}
+
+template <class T>
+bool HoldableValue<T>::updateValue(
+    T val, LinkStateMetric holdUpTtl, LinkStateMetric holdDownTtl) {
+  if (val == val_) {
+    return false; // same value: no-op
+  }
+  if (heldVal_) {
+    // a second change while holding falls back to an immediate update
+    heldVal_.reset();
+    holdTtl_ = 0;
+  } else {
+    holdTtl_ = isChangeBringingUp(val) ? holdUpTtl : holdDownTtl;
+    if (holdTtl_ != 0) {
+      heldVal_ = val_;
+    }
+  }
+  val_ = val;
+  return !heldVal_.has_value();
+}
+
+template <>
+bool HoldableValue<bool>::isChangeBringingUp(bool val) {
+  // clearing an overload brings the element up
+  return val_ && !val;
+}
+
+template <>
+bool HoldableValue<LinkStateMetric>::isChangeBringingUp(LinkStateMetric val) {
+  // a metric decrease attracts traffic
+  return val < val_;
+}
+
+template class HoldableValue<LinkStateMetric>;
+template class HoldableValue<bool>;
+
+// --------------------------------------------------------------------- Link
+
+Link::Link(
+    const std::string& area,
+    const std::string& nodeName1,
+    const std::string& if1,
+    const std::string& nodeName2,
+    const std::string& if2)
+    : area_(area),
+      n1_(nodeName1),
+      n2_(nodeName2),
+      if1_(if1),
+      if2_(if2),
+      orderedNames_(std::minmax(std::make_pair(n1_, if1_), std::make_pair(n2_, if2_))),
+      hash(hash128to64(hashStrPair(orderedNames_.first), hashStrPair(orderedNames_.second))) {}
+
+Link::Link(
+    const std::string& area,
+    const std::string& nodeName1,
+    const thrift::Adjacency& adj1,
+    const std::string& nodeName2,
+    const thrift::Adjacency& adj2)
+    : Link(area, nodeName1, adj1.ifName, nodeName2, adj2.ifName) {
+  // an i32 metric widens to the uint64 LinkStateMetric (negative -> huge)
+  metric1_ = static_cast<LinkStateMetric>(static_cast<int64_t>(adj1.metric));
+  metric2_ = static_cast<LinkStateMetric>(static_cast<int64_t>(adj2.metric));
+  overload1_ = adj1.isOverloaded;
+  overload2_ = adj2.isOverloaded;
+  adjLabel1_ = adj1.adjLabel;
+  adjLabel2_ = adj2.adjLabel;
+  nhV41_ = adj1.nextHopV4;
+  nhV42_ = adj2.nextHopV4;
+  nhV61_ = adj1.nextHopV6;
+  nhV62_ = adj2.nextHopV6;
+}
+
+namespace {
+[[noreturn]] void badNode(const std::string& nodeName) {
+  throw std::invalid_argument(nodeName);
+}
+} // namespace
+
+#define LINK_SIDE(nodeName, a, b) \
+  ((nodeName) == n1_ ? (a) : ((nodeName) == n2_ ? (b) : (badNode(nodeName), (a))))
+
+const std::string& Link::getOtherNodeName(const std::string& nodeName) const {
+  return LINK_SIDE(nodeName, n2_, n1_);
+}
+const std::string& Link::firstNodeName() const { return orderedNames_.first.first; }
+const std::string& Link::secondNodeName() const { return orderedNames_.second.first; }
+const std::string& Link::getIfaceFromNode(const std::string& nodeName) const {
+  return LINK_SIDE(nodeName, if1_, if2_);
+}
+LinkStateMetric Link::getMetricFromNode(const std::string& nodeName) const {
+  return LINK_SIDE(nodeName, metric1_, metric2_).value();
+}
+int32_t Link::getAdjLabelFromNode(const std::string& nodeName) const {
+  return LINK_SIDE(nodeName, adjLabel1_, adjLabel2_);
+}
+bool Link::getOverloadFromNode(const std::string& nodeName) const {
+  return LINK_SIDE(nodeName, overload1_, overload2_).value();
+}
+const thrift::BinaryAddress& Link::getNhV4FromNode(const std::string& nodeName) const {
+  return LINK_SIDE(nodeName, nhV41_, nhV42_);
+}
+const thrift::BinaryAddress& Link::getNhV6FromNode(const std::string& nodeName) const {
+  return LINK_SIDE(nodeName, nhV61_, nhV62_);
+}
+void Link::setNhV4FromNode(const std::string& nodeName, const thrift::BinaryAddress& nhV4) {
+  LINK_SIDE(nodeName, nhV41_, nhV42_) = nhV4;
+}
+void Link::setNhV6FromNode(const std::string& nodeName, const thrift::BinaryAddress& nhV6) {
+  LINK_SIDE(nodeName, nhV61_, nhV62_) = nhV6;
+}
+bool Link::setMetricFromNode(
+    const std::string& nodeName,
+    LinkStateMetric d,
+    LinkStateMetric holdUpTtl,
+    LinkStateMetric holdDownTtl) {
+  return LINK_SIDE(nodeName, metric1_, metric2_).updateValue(d, holdUpTtl, holdDownTtl);
+}
+void Link::setAdjLabelFromNode(const std::string& nodeName, int32_t adjLabel) {
+  LINK_SIDE(nodeName, adjLabel1_, adjLabel2_) = adjLabel;
+}
+bool Link::setOverloadFromNode(
+    const std::string& nodeName,
+    bool overload,
+    LinkStateMetric holdUpTtl,
+    LinkStateMetric holdDownTtl) {
+  const bool upBefore = isUp();
+  LINK_SIDE(nodeName, overload1_, overload2_).updateValue(overload, holdUpTtl, holdDownTtl);
+  // only a change of isUp() is a topology change (no simplex overloads)
+  return upBefore != isUp();
+}
+#undef LINK_SIDE
+
+void Link::setHoldUpTtl(LinkStateMetric ttl) { holdUpTtl_ = ttl; }
+
+bool Link::isUp() const {
+  return holdUpTtl_ == 0 && !overload1_.value() && !overload2_.value();
+}
+
+bool Link::decrementHolds() {
+  bool expired = false;
+  if (holdUpTtl_ != 0) {
+    --holdUpTtl_;
+    expired |= holdUpTtl_ == 0;
+  }
+  expired |= metric1_.decrementTtl();
+  expired |= metric2_.decrementTtl();
+  expired |= overload1_.decrementTtl();
+  expired |= overload2_.decrementTtl();
+  return expired;
+}
+
+bool Link::hasHolds() const {
+  return holdUpTtl_ != 0 || metric1_.hasHold() || metric2_.hasHold() ||
+      overload1_.hasHold() || overload2_.hasHold();
+}
+
+bool Link::operator<(const Link& other) const {
+  // hash first, then names (LinkState.cpp:347-353)
+  if (hash != other.hash) {
+    return hash < other.hash;
+  }
+  return orderedNames_ < other.orderedNames_;
+}
+
+bool Link::operator==(const Link& other) const {
+  return hash == other.hash && orderedNames_ == other.orderedNames_;
+}
+
+std::string Link::toString() const {
+  return area_ + " - " + n1_ + "%" + if1_ + " <---> " + n2_ + "%" + if2_;
+}
+
+std::string Link::directionalToString(const std::string& fromNode) const {
+  const auto& to = getOtherNodeName(fromNode);
+  return area_ + " - " + fromNode + "%" + getIfaceFromNode(fromNode) + " ---> " +
+      to + "%" + getIfaceFromNode(to);
+}
+
+// ------------------------------------------------------------------ engine
+
+struct LinkState::Engine {
+  bool built{false};
+  std::vector<std::string> names; // id -> name, ascending
+  std::unordered_map<std::string, uint32_t> ids;
+  std::vector<uint32_t> row, col, linkId, rev;
+  std::vector<uint64_t> metric;
+  std::vector<uint8_t> overloaded;
+  std::vector<std::shared_ptr<Link>> links; // link id -> Link
+  std::unordered_map<const Link*, uint32_t> linkIndex;
+  spf_graph* graph{nullptr};
+  bool exact{false};
+  float lastMs{0};
+  std::unordered_map<uint32_t, std::unique_ptr<SpfView>> memo[2];
+  std::unordered_map<uint32_t, std::unique_ptr<SpfView>> prefetched[2];
+  std::map<std::pair<uint32_t, uint32_t>, std::unique_ptr<SpfView>> kthPrefetch;
+  std::unordered_map<std::string, std::unique_ptr<SpfView>> isolated;
+
+  ~Engine() {
+    if (graph) {
+      spf_graph_destroy(graph);
+    }
+  }
+};
+
+namespace {
+
+[[noreturn]] void engineFailure(const char* what, int status) {
+  throw std::runtime_error(
+      std::string("openr_spf: ") + what + ": " + spf_error_string(status) + " (" +
+      spf_last_error_detail() + ")");
+}
+
+// Flatten the up links into the device CSR.  Rows follow linksFromNode()
+// iteration order (the reference's relaxation order).
+void buildGraph(
+    LinkState::Engine& eng,
+    const std::unordered_map<std::string, LinkState::LinkSet>& linkMap,
+    const std::unordered_map<std::string, thrift::AdjacencyDatabase>& adjDbs,
+    const LinkState& ls) {
+  eng.names.clear();
+  eng.names.reserve(adjDbs.size() + linkMap.size());
+  for (const auto& kv : adjDbs) {
+    eng.names.push_back(kv.first);
+  }
+  for (const auto& kv : linkMap) {
+    if (!adjDbs.count(kv.first)) {
+      eng.names.push_back(kv.first);
+    }
+  }
+  std::sort(eng.names.begin(), eng.names.end());
+  const uint32_t V = (uint32_t)eng.names.size();
+  eng.ids.clear();
+  eng.ids.reserve(V * 2);
+  for (uint32_t i = 0; i < V; ++i) {
+    eng.ids.emplace(eng.names[i], i);
+  }
+  eng.row.assign(V + 1, 0);
+  eng.col.clear();
+  eng.linkId.clear();
+  eng.metric.clear();
+  eng.links.clear();
+  eng.linkIndex.clear();
+  eng.overloaded.assign(V, 0);
+  // half-edge slots per link: [0] = from firstNodeName, [1] = from second
+  std::vector<std::array<uint32_t, 2>> halves;
+  for (uint32_t u = 0; u < V; ++u) {
+    const std::string& name = eng.names[u];
+    eng.overloaded[u] = ls.isNodeOverloaded(name) ? 1 : 0;
+    auto it = linkMap.find(name);
+    if (it != linkMap.end()) {
+      for (const auto& link : it->second) {
+        if (!link->isUp()) {
+          continue;
+        }
+        auto [pos, inserted] =
+            eng.linkIndex.emplace(link.get(), (uint32_t)eng.links.size());
+        if (inserted) {
+          eng.links.push_back(link);
+          halves.push_back({~0u, ~0u});
+        }
+        const uint32_t lid = pos->second;
+        const std::string& other = link->getOtherNodeName(name);
+        const uint32_t e = (uint32_t)eng.col.size();
+        eng.col.push_back(eng.ids.at(other));
+        eng.linkId.push_back(lid);
+        eng.metric.push_back(link->getMetricFromNode(name));
+        halves[lid][name == link->firstNodeName() ? 0 : 1] = e;
+      }
+    }
+    eng.row[u + 1] = (uint32_t)eng.col.size();
+  }
+  const uint32_t E = (uint32_t)eng.col.size();
+  eng.rev.assign(E, 0);
+  for (uint32_t e = 0; e < E; ++e) {
+    const auto& h = halves[eng.linkId[e]];
+    eng.rev[e] = h[0] == e ? h[1] : h[0];
+  }
+  spf_graph_desc d{};
+  d.num_nodes = V;
+  d.num_edges = E;
+  d.row_ptr = eng.row.data();
+  d.col = eng.col.data();
+  d.metric = eng.metric.data();
+  d.link_id = eng.linkId.data();
+  d.rev = eng.rev.data();
+  d.node_overloaded = eng.overloaded.data();
+  d.num_links = (uint32_t)eng.links.size();
+  d.device = getSpfDevice();
+  if (eng.graph) {
+    spf_graph_destroy(eng.graph);
+    eng.graph = nullptr;
+  }
+  if (V > 0) {
+    const int s = spf_graph_create(&d, &eng.graph);
+    if (s != SPF_OK) {
+      engineFailure("spf_graph_create", s);
+    }
+    eng.exact = spf_graph_needs_exact(eng.graph) != 0;
+  }
+  eng.built = true;
+}
+
+// One device batch; returns one SpfView per source.
+std::vector<std::unique_ptr<SpfView>> runBatch(
+    LinkState::Engine& eng,
+    const std::vector<uint32_t>& sources,
+    bool useLinkMetric,
+    bool wantNextHops,
+    const std::vector<std::vector<uint32_t>>* ignore) {
+  std::vector<std::unique_ptr<SpfView>> out;
+  if (sources.empty()) {
+    return out;
+  }
+  const bool exact = eng.exact && useLinkMetric;
+  uint32_t flags = 0;
+  if (!useLinkMetric) {
+    flags |= SPF_F_UNIT_METRIC;
+  }
+  if (wantNextHops) {
+    flags |= SPF_F_NEXTHOPS;
+  }
+  if (exact) {
+    flags |= SPF_F_ORDER;
+  }
+  std::vector<uint32_t> ioff, ilinks;
+  spf_query_desc qd{};
+  qd.num_queries = (uint32_t)sources.size();
+  qd.sources = sources.data();
+  qd.flags = flags;
+  if (ignore) {
+    ioff.push_back(0);
+    for (const auto& l : *ignore) {
+      ilinks.insert(ilinks.end(), l.begin(), l.end());
+      ioff.push_back((uint32_t)ilinks.size());
+    }
+    qd.ignore_offsets = ioff.data();
+    qd.ignore_links = ilinks.data();
+  }
+  spf_query* q = nullptr;
+  int s = spf_query_create(eng.graph, &qd, &q);
+  if (s != SPF_OK) {
+    engineFailure("spf_query_create", s);
+  }
+  struct Guard {
+    spf_query* q;
+    ~Guard() { spf_query_destroy(q); }
+  } guard{q};
+  if ((s = spf_query_run(q)) != SPF_OK || (s = spf_query_sync(q)) != SPF_OK) {
+    engineFailure("spf_query_run", s);
+  }
+  spf_query_elapsed_ms(q, &eng.lastMs);
+  Counters::add("decision.spf_device_us", (int64_t)(eng.lastMs * 1000.0f));
+  const uint32_t V = (uint32_t)eng.names.size();
+  out.reserve(sources.size());
+  for (uint32_t i = 0; i < sources.size(); ++i) {
+    auto view = std::make_unique<SpfView>();
+    view->src = sources[i];
+    view->useLinkMetric = useLinkMetric;
+    view->exact = exact;
+    view->dist.resize(V);
+    if ((s = spf_query_dist(q, i, view->dist.data())) != SPF_OK) {
+      engineFailure("spf_query_dist", s);
+    }
+    if (wantNextHops) {
+      view->words = (uint32_t)spf_query_nh_words(q, i);
+      view->nh.resize((size_t)V * view->words);
+      if ((s = spf_query_nexthops(q, i, view->nh.data())) != SPF_OK) {
+        engineFailure("spf_query_nexthops", s);
+      }
+      const int nn = spf_graph_num_nbrs(eng.graph, sources[i]);
+      view->nbrs.resize(std::max(nn, 0));
+      if (nn > 0) {
+        spf_graph_nbrs(eng.graph, sources[i], view->nbrs.data());
+      }
+    }
+    if (exact) {
+      view->order.resize(V);
+      if ((s = spf_query_order(q, i, view->order.data())) != SPF_OK) {
+        engineFailure("spf_query_order", s);
+      }
+    }
+    if (ignore) {
+      view->ignored = (*ignore)[i];
+    }
+    out.push_back(std::move(view));
+  }
+  return out;
+}
+
+// Predecessors of v in the reference's pathLinks order: usable in-links whose
+// tail is the source or transit, is settled before v and is tight; sorted by
+// the tail's settle rank, then by the tail's linksFromNode() order.
+void pathLinksOf(
+    const LinkState::Engine& eng,
+    const SpfView& view,
+    uint32_t v,
+    std::vector<std::pair<uint32_t /* half-edge u->v */, uint32_t /* u */>>& out) {
+  out.clear();
+  if (!view.reached(v) || v == view.src) {
+    return;
+  }
+  const uint64_t dv = view.dist[v];
+  for (uint32_t e = eng.row[v]; e < eng.row[v + 1]; ++e) {
+    const uint32_t u = eng.col[e];
+    if (!view.reached(u)) {
+      continue;
+    }
+    if (u != view.src && eng.overloaded[u]) {
+      continue;
+    }
+    if (!view.ignored.empty() &&
+        std::binary_search(view.ignored.begin(), view.ignored.end(), eng.linkId[e])) {
+      continue;
+    }
+    const uint32_t eu = eng.rev[e]; // the half-edge u->v
+    const uint64_t w = view.useLinkMetric ? eng.metric[eu] : 1ull;
+    if (view.dist[u] + w != dv) {
+      continue;
+    }
+    if (view.exact ? !(view.order[u] < view.order[v])
+                   : !(view.dist[u] < dv)) {
+      continue;
+    }
+    out.emplace_back(eu, u);
+  }
+  std::sort(out.begin(), out.end(), [&](const auto& a, const auto& b) {
+    const uint32_t ua = a.second, ub = b.second;
+    if (ua != ub) {
+      if (view.exact) {
+        return view.order[ua] < view.order[ub];
+      }
+      if (view.dist[ua] != view.dist[ub]) {
+        return view.dist[ua] < view.dist[ub];
+      }
+      return ua < ub;
+    }
+    return a.first < b.first; // row-u position = linksFromNode(u) order
+  });
+}
+
+} // namespace
+
+LinkState::Engine& LinkState::engine() const {
+  if (!engine_) {
+    engine_ = std::make_unique<Engine>();
+  }
+  if (!engine_->built) {
+    buildGraph(*engine_, linkMap_, adjacencyDatabases_, *this);
+  }
+  return *engine_;
+}
+
+// ---------------------------------------------------------------- LinkState
+
+LinkState::LinkState(const std::string& area) : area_(area) {}
+LinkState::~LinkState() = default;
+LinkState::LinkState(LinkState&& o) noexcept
+    : area_(o.area_),
+      linkMap_(std::move(o.linkMap_)),
+      allLinks_(std::move(o.allLinks_)),
+      nodeOverloads_(std::move(o.nodeOverloads_)),
+      adjacencyDatabases_(std::move(o.adjacencyDatabases_)),
+      spfResultsMetric_(std::move(o.spfResultsMetric_)),
+      spfResultsHops_(std::move(o.spfResultsHops_)),
+      kthPathResults_(std::move(o.kthPathResults_)),
+      engine_(std::move(o.engine_)) {}
+
+size_t LinkState::LinkPtrHash::operator()(const std::shared_ptr<Link>& l) const {
+  return l->hash;
+}
+bool LinkState::LinkPtrLess::operator()(
+    const std::shared_ptr<Link>& lhs, const std::shared_ptr<Link>& rhs) const {
+  return *lhs < *rhs;
+}
+bool LinkState::LinkPtrEqual::operator()(
+    const std::shared_ptr<Link>& lhs, const std::shared_ptr<Link>& rhs) const {
+  return *lhs == *rhs;
+}
+
+void LinkState::clearMemo() const {
+  spfResultsMetric_.clear();
+  spfResultsHops_.clear();
+  kthPathResults_.clear();
+  if (engine_) {
+    engine_.reset(); // drop the device graph: the topology changed
+  }
+}
+
+void LinkState::invalidate() const { clearMemo(); }
+
+void LinkState::addLink(std::shared_ptr<Link> link) {
+  if (!linkMap_[link->firstNodeName()].insert(link).second ||
+      !linkMap_[link->secondNodeName()].insert(link).second ||
+      !allLinks_.insert(link).second) {
+    throw std::logic_error("addLink: duplicate link " + link->toString());
+  }
+}
+
+void LinkState::removeLink(std::shared_ptr<Link> link) {
+  if (!linkMap_.at(link->firstNodeName()).erase(link) ||
+      !linkMap_.at(link->secondNodeName()).erase(link) || !allLinks_.erase(link)) {
+    throw std::logic_error("removeLink: missing link " + link->toString());
+  }
+}
+
+void LinkState::removeNode(const std::string& nodeName) {
+  auto it = linkMap_.find(nodeName);
+  if (it == linkMap_.end()) {
+    return; // an empty adjacency database created no links
+  }
+  for (const auto& link : it->second) {
+    if (!linkMap_.at(link->getOtherNodeName(nodeName)).erase(link) ||
+        !allLinks_.erase(link)) {
+      throw std::logic_error("removeNode: inconsistent link set");
+    }
+  }
+  linkMap_.erase(it);
+  nodeOverloads_.erase(nodeName);
+}
+
+const LinkState::LinkSet& LinkState::linksFromNode(const std::string& nodeName) const {
+  static const LinkSet kEmpty;
+  auto it = linkMap_.find(nodeName);
+  return it == linkMap_.end() ? kEmpty : it->second;
+}
+
+std::vector<std::shared_ptr<Link>> LinkState::orderedLinksFromNode(
+    const std::string& nodeName) const {
+  const auto& set = linksFromNode(nodeName);
+  std::vector<std::shared_ptr<Link>> links(set.begin(), set.end());
+  std::sort(links.begin(), links.end(), LinkPtrLess{});
+  return links;
+}
+
+bool LinkState::updateNodeOverloaded(
+    const std::string& nodeName,
+    bool isOverloaded,
+    LinkStateMetric holdUpTtl,
+    LinkStateMetric holdDownTtl) {
+  auto it = nodeOverloads_.find(nodeName);
+  if (it == nodeOverloads_.end()) {
+    // a new node is not a topology change by itself
+    nodeOverloads_.emplace(nodeName, HoldableValue<bool>{isOverloaded});
+    return false;
+  }
+  return it->second.updateValue(isOverloaded, holdUpTtl, holdDownTtl);
+}
+
+bool LinkState::isNodeOverloaded(const std::string& nodeName) const {
+  auto it = nodeOverloads_.find(nodeName);
+  return it != nodeOverloads_.end() && it->second.value();
+}
+
+LinkState::LinkStateChange LinkState::decrementHolds() {
+  LinkStateChange change;
+  for (const auto& link : allLinks_) {
+    change.topologyChanged |= link->decrementHolds();
+  }
+  for (auto& kv : nodeOverloads_) {
+    change.topologyChanged |= kv.second.decrementTtl();
+  }
+  if (change.topologyChanged) {
+    clearMemo();
+  }
+  return change;
+}
+
+bool LinkState::hasHolds() const {
+  for (const auto& link : allLinks_) {
+    if (link->hasHolds()) {
+      return true;
+    }
+  }
+  for (const auto& kv : nodeOverloads_) {
+    if (kv.second.hasHold()) {
+      return true;
+    }
+  }
+  return false;
+}
+
+std::shared_ptr<Link> LinkState::maybeMakeLink(
+    const std::string& nodeName, const thrift::Adjacency& adj) const {
+  // bidirectional only: the neighbour must advertise the mirror adjacency
+  auto it = adjacencyDatabases_.find(adj.otherNodeName);
+  if (it == adjacencyDatabases_.end()) {
+    return nullptr;
+  }
+  for (const auto& mirror : it->second.adjacencies) {
+    if (mirror.otherNodeName == nodeName && mirror.ifName == adj.otherIfName &&
+        mirror.otherIfName == adj.ifName) {
+      return std::make_shared<Link>(area_, nodeName, adj, adj.otherNodeName, mirror);
+    }
+  }
+  return nullptr;
+}
+
+std::vector<std::shared_ptr<Link>> LinkState::getOrderedLinkSet(
+    const thrift::AdjacencyDatabase& adjDb) const {
+  std::vector<std::shared_ptr<Link>> links;
+  links.reserve(adjDb.adjacencies.size());
+  for (const auto& adj : adjDb.adjacencies) {
+    if (auto link = maybeMakeLink(adjDb.thisNodeName, adj)) {
+      links.push_back(std::move(link));
+    }
+  }
+  std::sort(links.begin(), links.end(), LinkPtrLess{});
+  return links;
+}
+
+LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
+    thrift::AdjacencyDatabase const& newDb,
+    LinkStateMetric holdUpTtl,
+    LinkStateMetric holdDownTtl) {
+  LinkStateChange change;
+  const std::string& nodeName = newDb.thisNodeName;
+
+  thrift::AdjacencyDatabase priorDb(std::move(adjacencyDatabases_[nodeName]));
+  adjacencyDatabases_[nodeName] = newDb;
+
+  // both sides sorted by Link::operator< so one merge pass finds the diff
+  const auto oldLinks = orderedLinksFromNode(nodeName);
+  const auto newLinks = getOrderedLinkSet(newDb);
+
+  change.topologyChanged |=
+      updateNodeOverloaded(nodeName, newDb.isOverloaded, holdUpTtl, holdDownTtl);
+  change.nodeLabelChanged = priorDb.nodeLabel != newDb.nodeLabel;
+
+  size_t ni = 0, oi = 0;
+  while (ni < newLinks.size() || oi < oldLinks.size()) {
+    const bool haveNew = ni < newLinks.size(), haveOld = oi < oldLinks.size();
+    if (haveNew && (!haveOld || *newLinks[ni] < *oldLinks[oi])) {
+      // link appears: keep it held down for holdUpTtl
+      newLinks[ni]->setHoldUpTtl(holdUpTtl);
+      change.topologyChanged |= newLinks[ni]->isUp();
+      addLink(newLinks[ni]);
+      ++ni;
+      continue;
+    }
+    if (haveOld && (!haveNew || *oldLinks[oi] < *newLinks[ni])) {
+      // link disappears (a held or overloaded link was not carrying traffic)
+      change.topologyChanged |= oldLinks[oi]->isUp();
+      removeLink(oldLinks[oi]);
+      ++oi;
+      continue;
+    }
+    // same link: fold attribute changes into the existing Link object
+    const Link& fresh = *newLinks[ni];
+    Link& cur = *oldLinks[oi];
+    if (fresh.getMetricFromNode(nodeName) != cur.getMetricFromNode(nodeName)) {
+      change.topologyChanged |= cur.setMetricFromNode(
+          nodeName, fresh.getMetricFromNode(nodeName), holdUpTtl, holdDownTtl);
+    }
+    if (fresh.getOverloadFromNode(nodeName) != cur.getOverloadFromNode(nodeName)) {
+      change.topologyChanged |= cur.setOverloadFromNode(
+          nodeName, fresh.getOverloadFromNode(nodeName), holdUpTtl, holdDownTtl);
+    }
+    if (fresh.getAdjLabelFromNode(nodeName) != cur.getAdjLabelFromNode(nodeName)) {
+      change.linkAttributesChanged = true;
+      cur.setAdjLabelFromNode(nodeName, fresh.getAdjLabelFromNode(nodeName));
+    }
+    if (fresh.getNhV4FromNode(nodeName) != cur.getNhV4FromNode(nodeName)) {
+      change.linkAttributesChanged = true;
+      cur.setNhV4FromNode(nodeName, fresh.getNhV4FromNode(nodeName));
+    }
+    if (fresh.getNhV6FromNode(nodeName) != cur.getNhV6FromNode(nodeName)) {
+      change.linkAttributesChanged = true;
+      cur.setNhV6FromNode(nodeName, fresh.getNhV6FromNode(nodeName));
+    }
+    ++ni;
+    ++oi;
+  }
+  if (change.topologyChanged) {
+    clearMemo();
+  }
+  return change;
+}
+
+LinkState::LinkStateChange LinkState::deleteAdjacencyDatabase(const std::string& nodeName) {
+  LinkStateChange change;
+  auto it = adjacencyDatabases_.find(nodeName);
+  if (it != adjacencyDatabases_.end()) {
+    removeNode(nodeName);
+    adjacencyDatabases_.erase(it);
+    clearMemo();
+    change.topologyChanged = true;
+  }
+  return change;
+}
+
+bool LinkState::pathAInPathB(Path const& a, Path const& b) {
+  if (a.size() > b.size()) {
+    return false;
+  }
+  for (size_t start = 0; start + a.size() <= b.size(); ++start) {
+    size_t k = 0;
+    while (k < a.size() && *a[k] == *b[start + k]) {
+      ++k;
+    }
+    if (k == a.size()) {
+      return true;
+    }
+  }
+  return false;
+}
+
+// ---------------------------------------------------------- SPF accessors
+
+std::optional<uint32_t> LinkState::nodeId(const std::string& name) const {
+  auto& eng = engine();
+  auto it = eng.ids.find(name);
+  if (it == eng.ids.end()) {
+    return std::nullopt;
+  }
+  return it->second;
+}
+
+const std::string& LinkState::nodeNameOf(uint32_t id) const {
+  return engine().names.at(id);
+}
+
+uint32_t LinkState::numGraphNodes() const {
+  return (uint32_t)engine().names.size();
+}
+
+float LinkState::lastDeviceMs() const {
+  return engine_ ? engine_->lastMs : 0.0f;
+}
+
+const SpfView& LinkState::spfView(const std::string& node, bool useLinkMetric) const {
+  auto& eng = engine();
+  auto idIt = eng.ids.find(node);
+  if (idIt == eng.ids.end()) {
+    // unknown source: the reference result holds only the source itself
+    auto& slot = eng.isolated[node];
+    if (!slot) {
+      slot = std::make_unique<SpfView>();
+      slot->src = ~0u;
+      slot->useLinkMetric = useLinkMetric;
+      Counters::add("decision.spf_runs", 1);
+    }
+    return *slot;
+  }
+  const uint32_t id = idIt->second;
+  auto& memo = eng.memo[useLinkMetric ? 1 : 0];
+  auto it = memo.find(id);
+  if (it != memo.end()) {
+    return *it->second;
+  }
+  auto& pre = eng.prefetched[useLinkMetric ? 1 : 0];
+  std::unique_ptr<SpfView> view;
+  auto pit = pre.find(id);
+  if (pit != pre.end()) {
+    view = std::move(pit->second);
+    pre.erase(pit);
+  } else {
+    const auto t0 = std::chrono::steady_clock::now();
+    auto batch = runBatch(eng, {id}, useLinkMetric, true, nullptr);
+    view = std::move(batch.front());
+    Counters::add(
+        "decision.spf_us",
+        std::chrono::duration_cast<std::chrono::microseconds>(
+            std::chrono::steady_clock::now() - t0)
+            .count());
+  }
+  Counters::add("decision.spf_runs", 1);
+  return *memo.emplace(id, std::move(view)).first->second;
+}
+
+void LinkState::prefetchSpf(const std::vector<std::string>& nodes, bool useLinkMetric) const {
+  auto& eng = engine();
+  auto& memo = eng.memo[useLinkMetric ? 1 : 0];
+  auto& pre = eng.prefetched[useLinkMetric ? 1 : 0];
+  std::vector<uint32_t> todo;
+  std::unordered_set<uint32_t> seen;
+  for (const auto& n : nodes) {
+    auto it = eng.ids.find(n);
+    if (it == eng.ids.end()) {
+      continue;
+    }
+    const uint32_t id = it->second;
+    if (memo.count(id) || pre.count(id) || !seen.insert(id).second) {
+      continue;
+    }
+    todo.push_back(id);
+  }
+  if (todo.empty()) {
+    return;
+  }
+  auto views = runBatch(eng, todo, useLinkMetric, true, nullptr);
+  for (size_t i = 0; i < todo.size(); ++i) {
+    pre.emplace(todo[i], std::move(views[i]));
+  }
+}
+
+LinkState::SpfResult const& LinkState::getSpfResult(
+    const std::string& nodeName, bool useLinkMetric) const {
+  auto& cache = useLinkMetric ? spfResultsMetric_ : spfResultsHops_;
+  auto it = cache.find(nodeName);
+  if (it != cache.end()) {
+    return it->second;
+  }
+  const SpfView& view = spfView(nodeName, useLinkMetric);
+  const auto& eng = *engine_;
+  SpfResult res;
+  if (view.src == ~0u) {
+    res.emplace(nodeName, NodeSpfResult(0));
+  } else {
+    std::vector<std::pair<uint32_t, uint32_t>> preds;
+    const uint32_t V = (uint32_t)eng.names.size();
+    res.reserve(V);
+    for (uint32_t v = 0; v < V; ++v) {
+      if (!view.reached(v)) {
+        continue;
+      }
+      NodeSpfResult r(view.dist[v]);
+      pathLinksOf(eng, view, v, preds);
+      for (const auto& [eu, u] : preds) {
+        r.addPath(eng.links[eng.linkId[eu]], eng.names[u]);
+      }
+      view.forEachNextHop(v, [&](uint32_t h) { r.addNextHop(eng.names[h]); });
+      res.emplace(eng.names[v], std::move(r));
+    }
+  }
+  return cache.emplace(nodeName, std::move(res)).first->second;
+}
+
+std::optional<LinkStateMetric> LinkState::getMetricFromAToB(
+    std::string const& a, std::string const& b, bool useLinkMetric) const {
+  if (a == b) {
+    return 0;
+  }
+  const SpfView& view = spfView(a, useLinkMetric);
+  if (view.src == ~0u) {
+    return std::nullopt;
+  }
+  auto it = engine_->ids.find(b);
+  if (it == engine_->ids.end() || !view.reached(it->second)) {
+    return std::nullopt;
+  }
+  return view.dist[it->second];
+}
+
+LinkStateMetric LinkState::getMaxHopsToNode(const std::string& nodeName) const {
+  const SpfView& view = spfView(nodeName, false);
+  LinkStateMetric best = 0;
+  for (uint64_t d : view.dist) {
+    if (d != SpfView::kUnreachable) {
+      best = std::max(best, d);
+    }
+  }
+  return best;
+}
+
+std::optional<LinkState::Path> LinkState::traceOnePath(
+    uint32_t src, uint32_t dest, const SpfView& result, LinkSet& linksToIgnore) const {
+  if (src == dest) {
+    return Path{};
+  }
+  const auto& eng = *engine_;
+  std::vector<std::pair<uint32_t, uint32_t>> preds;
+  pathLinksOf(eng, result, dest, preds);
+  for (const auto& [eu, u] : preds) {
+    const auto& link = eng.links[eng.linkId[eu]];
+    if (linksToIgnore.insert(link).second) {
+      if (auto path = traceOnePath(src, u, result, linksToIgnore)) {
+        path->push_back(link);
+        return path;
+      }
+    }
+  }
+  return std::nullopt;
+}
+
+std::vector<LinkState::Path> const& LinkState::getKthPaths(
+    const std::string& src, const std::string& dest, size_t k) const {
+  if (k < 1) {
+    throw std::invalid_argument("getKthPaths: k must be >= 1");
+  }
+  KthKey key{src, dest, k};
+  auto found = kthPathResults_.find(key);
+  if (found != kthPathResults_.end()) {
+    return found->second;
+  }
+  LinkSet linksToIgnore;
+  for (size_t i = 1; i < k; ++i) {
+    for (const auto& path : getKthPaths(src, dest, i)) {
+      for (const auto& link : path) {
+        linksToIgnore.insert(link);
+      }
+    }
+  }
+  std::vector<Path> paths;
+  auto& eng = engine();
+  const SpfView* res = nullptr;
+  std::unique_ptr<SpfView> second;
+  if (linksToIgnore.empty()) {
+    res = &spfView(src, true);
+  } else {
+    auto sid = eng.ids.find(src);
+    if (sid != eng.ids.end()) {
+      auto did = eng.ids.find(dest);
+      auto pit = did == eng.ids.end()
+          ? eng.kthPrefetch.end()
+          : eng.kthPrefetch.find({sid->second, did->second});
+      std::vector<uint32_t> ign;
+      for (const auto& link : linksToIgnore) {
+        auto li = eng.linkIndex.find(link.get());
+        if (li != eng.linkIndex.end()) {
+          ign.push_back(li->second);
+        }
+      }
+      std::sort(ign.begin(), ign.end());
+      if (pit != eng.kthPrefetch.end() && pit->second->ignored == ign) {
+        second = std::move(pit->second);
+        eng.kthPrefetch.erase(pit);
+      } else {
+        std::vector<std::vector<uint32_t>> lists{ign};
+        second = std::move(runBatch(eng, {sid->second}, true, false, &lists).front());
+      }
+      res = second.get();
+    }
+    Counters::add("decision.spf_runs", 1);
+  }
+  if (res && res->src != ~0u) {
+    auto did = eng.ids.find(dest);
+    if (did != eng.ids.end() && res->reached(did->second)) {
+      LinkSet visited;
+      auto path = traceOnePath(res->src, did->second, *res, visited);
+      while (path && !path->empty()) {
+        paths.push_back(std::move(*path));
+        path = traceOnePath(res->src, did->second, *res, visited);
+      }
+    }
+  }
+  return kthPathResults_.emplace(std::move(key), std::move(paths)).first->second;
+}
+
+void LinkState::prefetchKthPaths(
+    const std::string& src, const std::vector<std::string>& dests) const {
+  auto& eng = engine();
+  auto sid = eng.ids.find(src);
+  if (sid == eng.ids.end()) {
+    return;
+  }
+  std::vector<uint32_t> sources;
+  std::vector<uint32_t> dstIds;
+  std::vector<std::vector<uint32_t>> lists;
+  std::unordered_set<uint32_t> seen;
+  for (const auto& d : dests) {
+    auto did = eng.ids.find(d);
+    if (did == eng.ids.end() || !seen.insert(did->second).second) {
+      continue;
+    }
+    if (kthPathResults_.count(KthKey{src, d, 2}) ||
+        eng.kthPrefetch.count({sid->second, did->second})) {
+      continue;
+    }
+    std::vector<uint32_t> ign;
+    for (const auto& path : getKthPaths(src, d, 1)) {
+      for (const auto& link : path) {
+        auto li = eng.linkIndex.find(link.get());
+        if (li != eng.linkIndex.end()) {
+          ign.push_back(li->second);
+        }
+      }
+    }
+    if (ign.empty()) {
+      continue;
+    }
+    std::sort(ign.begin(), ign.end());
+    ign.erase(std::unique(ign.begin(), ign.end()), ign.end());
+    sources.push_back(sid->second);
+    dstIds.push_back(did->second);
+    lists.push_back(std::move(ign));
+  }
+  if (sources.empty()) {
+    return;
+  }
+  auto views = runBatch(eng, sources, true, false, &lists);
+  for (size_t i = 0; i < views.size(); ++i) {
+    eng.kthPrefetch[{sid->second, dstIds[i]}] = std::move(views[i]);
+  }
+}
+
+} // namespace openr
+
+size_t std::hash<openr::LinkState::LinkSet>::operator()(
+    openr::LinkState::LinkSet const& set) const {
+  size_t h = 0;
+  for (const auto& link : set) {
+    h ^= link->hash; // order independent
+  }
+  return h;
+}
+
+bool std::equal_to<openr::LinkState::LinkSet>::operator()(
+    openr::LinkState::LinkSet const& a, openr::LinkState::LinkSet const& b) const {
+  if (a.size() != b.size()) {
+    return false;
+  }
+  for (const auto& l : a) {
+    if (!b.count(l)) {
+      return false;
+    }
+  }
+  return true;
+}

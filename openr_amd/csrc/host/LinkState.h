@@ -1,0 +1,355 @@
+// LinkState.h — drop-in replacement of openr/decision/LinkState.h whose SPF
+// runs on MI355X through the C ABI in include/openr_spf.h.
+//
+// Public surface kept identical to the reference (LinkState.h:36-469):
+// HoldableValue, Link, LinkState (getSpfResult, getKthPaths,
+// updateAdjacencyDatabase, deleteAdjacencyDatabase, decrementHolds, hop/metric
+// queries, linksFromNode, ...), nested NodeSpfResult / PathLink / LinkSet /
+// Path / LinkStateChange, std::hash<Link>.  The graph bookkeeping uses the same
+// container types as the reference because their iteration orders are
+// observable (parallel-link choice in KSP2 traces, duplicate adj labels).
+//
+// What changes is where the shortest paths come from: instead of a
+// string-keyed DijkstraQ on the Decision thread (LinkState.cpp:806-880) the
+// up-link graph is flattened into a device CSR (node id = name rank) and each
+// SPF is a row of a batched GPU query.  `SpfView` is the flat per-source
+// result (distances + next-hop masks); getSpfResult() materialises the
+// reference's map form from it on demand.  Extensions beyond the reference API
+// (prefetchSpf, spfView, prefetchKthPaths) let SpfSolver batch many sources
+// into one launch.
+#pragma once
+
+#include <algorithm>
+#include <memory>
+#include <optional>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "Types.h"
+
+namespace openr {
+
+using LinkStateMetric = uint64_t;
+
+// RFC 6976 ordered-FIB hold (reference: LinkState.h:36-58, .cpp:54-125).
+template <class T>
+class HoldableValue {
+ public:
+  explicit HoldableValue(T val);
+  void operator=(T val);
+  const T& value() const;
+  bool hasHold() const;
+  // return true if the call changes value()
+  bool decrementTtl();
+  bool updateValue(T val, LinkStateMetric holdUpTtl, LinkStateMetric holdDownTtl);
+
+ private:
+  bool isChangeBringingUp(T val);
+  T val_;
+  std::optional<T> heldVal_;
+  LinkStateMetric holdTtl_{0};
+};
+
+class Link {
+ public:
+  Link(
+      const std::string& area,
+      const std::string& nodeName1,
+      const std::string& if1,
+      const std::string& nodeName2,
+      const std::string& if2);
+  Link(
+      const std::string& area,
+      const std::string& nodeName1,
+      const thrift::Adjacency& adj1,
+      const std::string& nodeName2,
+      const thrift::Adjacency& adj2);
+
+ private:
+  const std::string area_;
+  const std::string n1_, n2_, if1_, if2_;
+  HoldableValue<LinkStateMetric> metric1_{1}, metric2_{1};
+  HoldableValue<bool> overload1_{false}, overload2_{false};
+  int32_t adjLabel1_{0}, adjLabel2_{0};
+  thrift::BinaryAddress nhV41_, nhV42_, nhV61_, nhV62_;
+  LinkStateMetric holdUpTtl_{0};
+  const std::pair<
+      std::pair<std::string, std::string>,
+      std::pair<std::string, std::string>>
+      orderedNames_;
+
+ public:
+  const size_t hash{0};
+
+  void setHoldUpTtl(LinkStateMetric ttl);
+  bool isUp() const;
+  bool decrementHolds();
+  bool hasHolds() const;
+  const std::string& getArea() const { return area_; }
+  const std::string& getOtherNodeName(const std::string& nodeName) const;
+  const std::string& firstNodeName() const;
+  const std::string& secondNodeName() const;
+  const std::string& getIfaceFromNode(const std::string& nodeName) const;
+  LinkStateMetric getMetricFromNode(const std::string& nodeName) const;
+  int32_t getAdjLabelFromNode(const std::string& nodeName) const;
+  bool getOverloadFromNode(const std::string& nodeName) const;
+  const thrift::BinaryAddress& getNhV4FromNode(const std::string& nodeName) const;
+  const thrift::BinaryAddress& getNhV6FromNode(const std::string& nodeName) const;
+  void setNhV4FromNode(const std::string& nodeName, const thrift::BinaryAddress& nhV4);
+  void setNhV6FromNode(const std::string& nodeName, const thrift::BinaryAddress& nhV6);
+  bool setMetricFromNode(
+      const std::string& nodeName,
+      LinkStateMetric d,
+      LinkStateMetric holdUpTtl,
+      LinkStateMetric holdDownTtl);
+  void setAdjLabelFromNode(const std::string& nodeName, int32_t adjLabel);
+  bool setOverloadFromNode(
+      const std::string& nodeName,
+      bool overload,
+      LinkStateMetric holdUpTtl,
+      LinkStateMetric holdDownTtl);
+  const std::pair<
+      std::pair<std::string, std::string>,
+      std::pair<std::string, std::string>>&
+  orderedNames() const {
+    return orderedNames_;
+  }
+  bool operator<(const Link& other) const;
+  bool operator==(const Link& other) const;
+  std::string toString() const;
+  std::string directionalToString(const std::string& fromNode) const;
+};
+
+// Flat single-source SPF result as produced by the device (one batch row).
+struct SpfView {
+  uint32_t src{0};            // node id (name rank) of the source
+  bool useLinkMetric{true};
+  bool exact{false};          // settle order came from the exact kernel
+  std::vector<uint64_t> dist; // per node id; kUnreachable = not reached
+  uint32_t words{1};          // words per next-hop mask
+  std::vector<uint64_t> nh;   // [V * words]
+  std::vector<uint32_t> nbrs; // mask bit -> node id
+  std::vector<uint32_t> order; // exact kernel: settle rank per node id
+  std::vector<uint32_t> ignored; // sorted link ids this run skipped
+  static constexpr uint64_t kUnreachable = ~0ull;
+
+  bool reached(uint32_t v) const { return v < dist.size() && dist[v] != kUnreachable; }
+  template <class Fn>
+  void forEachNextHop(uint32_t v, Fn&& fn) const {
+    const uint64_t* m = nh.data() + (size_t)v * words;
+    for (uint32_t w = 0; w < words; ++w) {
+      uint64_t b = m[w];
+      while (b) {
+        const int k = __builtin_ctzll(b);
+        b &= b - 1;
+        fn(nbrs[w * 64 + k]);
+      }
+    }
+  }
+};
+
+class LinkState {
+ public:
+  explicit LinkState(const std::string& area);
+  ~LinkState();
+  LinkState(LinkState&&) noexcept;
+  LinkState& operator=(LinkState&&) = delete;
+  LinkState(const LinkState&) = delete;
+  LinkState& operator=(const LinkState&) = delete;
+
+  struct LinkPtrHash {
+    size_t operator()(const std::shared_ptr<Link>& l) const;
+  };
+  struct LinkPtrLess {
+    bool operator()(const std::shared_ptr<Link>& lhs, const std::shared_ptr<Link>& rhs) const;
+  };
+  struct LinkPtrEqual {
+    bool operator()(const std::shared_ptr<Link>& lhs, const std::shared_ptr<Link>& rhs) const;
+  };
+
+  using LinkSet = std::unordered_set<std::shared_ptr<Link>, LinkPtrHash, LinkPtrEqual>;
+
+  class NodeSpfResult {
+   public:
+    class PathLink {
+     public:
+      PathLink(std::shared_ptr<Link> const& l, std::string const& n)
+          : link(l), prevNode(n) {}
+      std::shared_ptr<Link> const link;
+      std::string const prevNode;
+    };
+    explicit NodeSpfResult(LinkStateMetric m) : metric_(m) {}
+    void reset(LinkStateMetric newMetric) {
+      metric_ = newMetric;
+      pathLinks_.clear();
+      nextHops_.clear();
+    }
+    std::vector<PathLink> const& pathLinks() const { return pathLinks_; }
+    std::unordered_set<std::string> const& nextHops() const { return nextHops_; }
+    LinkStateMetric metric() const { return metric_; }
+    void addPath(std::shared_ptr<Link> const& link, std::string const& prevNode) {
+      pathLinks_.emplace_back(link, prevNode);
+    }
+    void addNextHops(std::unordered_set<std::string> const& toInsert) {
+      nextHops_.insert(toInsert.begin(), toInsert.end());
+    }
+    void addNextHop(std::string const& toInsert) { nextHops_.insert(toInsert); }
+
+   private:
+    LinkStateMetric metric_{std::numeric_limits<LinkStateMetric>::max()};
+    std::vector<PathLink> pathLinks_;
+    std::unordered_set<std::string> nextHops_;
+  };
+
+  using SpfResult = std::unordered_map<std::string, NodeSpfResult>;
+  using Path = std::vector<std::shared_ptr<Link>>;
+
+  // memoized until the next topology change (reference: LinkState.cpp:791)
+  SpfResult const& getSpfResult(const std::string& nodeName, bool useLinkMetric = true) const;
+
+  // edge-disjoint path tracing (reference: LinkState.cpp:760-789)
+  std::vector<Path> const& getKthPaths(
+      const std::string& src, const std::string& dest, size_t k) const;
+
+  class LinkStateChange {
+   public:
+    LinkStateChange() = default;
+    LinkStateChange(bool topo, bool link, bool node)
+        : topologyChanged(topo), linkAttributesChanged(link), nodeLabelChanged(node) {}
+    bool operator==(LinkStateChange const& other) const {
+      return topologyChanged == other.topologyChanged &&
+          linkAttributesChanged == other.linkAttributesChanged &&
+          nodeLabelChanged == other.nodeLabelChanged;
+    }
+    bool topologyChanged{false};
+    bool linkAttributesChanged{false};
+    bool nodeLabelChanged{false};
+  };
+
+  LinkStateChange decrementHolds();
+  LinkStateChange updateAdjacencyDatabase(
+      thrift::AdjacencyDatabase const& adjacencyDb,
+      LinkStateMetric holdUpTtl = 0,
+      LinkStateMetric holdDownTtl = 0);
+  LinkStateChange deleteAdjacencyDatabase(const std::string& nodeName);
+
+  std::optional<LinkStateMetric> getMetricFromAToB(
+      std::string const& a, std::string const& b, bool useLinkMetric = true) const;
+  std::optional<LinkStateMetric> getHopsFromAToB(std::string const& a, std::string const& b) const {
+    return getMetricFromAToB(a, b, false);
+  }
+  LinkStateMetric getMaxHopsToNode(const std::string& nodeName) const;
+
+  const std::string& getArea() const { return area_; }
+  bool hasNode(const std::string& nodeName) const {
+    return 0 != adjacencyDatabases_.count(nodeName);
+  }
+  const LinkSet& linksFromNode(const std::string& nodeName) const;
+  bool isNodeOverloaded(const std::string& nodeName) const;
+  bool hasHolds() const;
+  size_t numLinks() const { return allLinks_.size(); }
+  size_t numNodes() const { return linkMap_.size(); }
+  std::unordered_map<std::string, thrift::AdjacencyDatabase> const&
+  getAdjacencyDatabases() const {
+    return adjacencyDatabases_;
+  }
+
+  // path A is a contiguous sub-path of B (reference: LinkState.h:395-410)
+  static bool pathAInPathB(Path const& a, Path const& b);
+
+  // ---- MI355X engine extensions (not part of the reference API) ----
+
+  // Flat SPF of `node`, memoized like getSpfResult (shares its spf_runs
+  // accounting: the first access of a (node, useLinkMetric) counts one run).
+  const SpfView& spfView(const std::string& node, bool useLinkMetric = true) const;
+  // Compute the SPFs of many sources in one device batch (no counting until
+  // they are first accessed through spfView/getSpfResult).
+  void prefetchSpf(const std::vector<std::string>& nodes, bool useLinkMetric = true) const;
+  // Run every second-pass (k = 2) SPF that getKthPaths(src, d, 2) would need
+  // for d in dests, as one device batch.
+  void prefetchKthPaths(const std::string& src, const std::vector<std::string>& dests) const;
+  // node id (name rank) in the current device graph
+  std::optional<uint32_t> nodeId(const std::string& name) const;
+  const std::string& nodeNameOf(uint32_t id) const;
+  uint32_t numGraphNodes() const;
+  // device time of the last batch, ms (HIP events)
+  float lastDeviceMs() const;
+  // release the device graph and every memoized result
+  void invalidate() const;
+
+  struct Engine; // device graph + flat memo (LinkState.cpp)
+
+ private:
+  void clearMemo() const;
+  Engine& engine() const;
+  std::optional<Path> traceOnePath(
+      uint32_t src, uint32_t dest, const SpfView& result, LinkSet& linksToIgnore) const;
+  void addLink(std::shared_ptr<Link> link);
+  void removeLink(std::shared_ptr<Link> link);
+  void removeNode(const std::string& nodeName);
+  bool updateNodeOverloaded(
+      const std::string& nodeName,
+      bool isOverloaded,
+      LinkStateMetric holdUpTtl,
+      LinkStateMetric holdDownTtl);
+  std::shared_ptr<Link> maybeMakeLink(
+      const std::string& nodeName, const thrift::Adjacency& adj) const;
+  std::vector<std::shared_ptr<Link>> getOrderedLinkSet(
+      const thrift::AdjacencyDatabase& adjDb) const;
+  std::vector<std::shared_ptr<Link>> orderedLinksFromNode(const std::string& nodeName) const;
+
+  const std::string area_;
+  std::unordered_map<std::string, LinkSet> linkMap_;
+  LinkSet allLinks_;
+  std::unordered_map<std::string, HoldableValue<bool>> nodeOverloads_;
+  std::unordered_map<std::string, thrift::AdjacencyDatabase> adjacencyDatabases_;
+
+  // reference-form memo (materialised lazily from the flat results)
+  mutable std::unordered_map<std::string, SpfResult> spfResultsMetric_;
+  mutable std::unordered_map<std::string, SpfResult> spfResultsHops_;
+  struct KthKey {
+    std::string src, dst;
+    size_t k;
+    bool operator==(const KthKey& o) const {
+      return k == o.k && src == o.src && dst == o.dst;
+    }
+  };
+  struct KthKeyHash {
+    size_t operator()(const KthKey& key) const;
+  };
+  mutable std::unordered_map<KthKey, std::vector<Path>, KthKeyHash> kthPathResults_;
+  mutable std::unique_ptr<Engine> engine_;
+};
+
+// Process-wide counters mirroring the fb303 keys the reference bumps
+// (decision.spf_runs, decision.spf_ms, ...).  Tests assert exact spf_runs.
+struct Counters {
+  static void add(const std::string& key, int64_t v);
+  static int64_t get(const std::string& key);
+  static std::unordered_map<std::string, int64_t> snapshot();
+  static void reset();
+};
+
+// Which HIP device new LinkStates bind to (one process per GPU).
+void setSpfDevice(int device);
+int getSpfDevice();
+
+} // namespace openr
+
+namespace std {
+template <>
+struct hash<openr::Link> {
+  size_t operator()(openr::Link const& link) const { return link.hash; }
+};
+template <>
+struct hash<openr::LinkState::LinkSet> {
+  size_t operator()(openr::LinkState::LinkSet const& set) const;
+};
+template <>
+struct equal_to<openr::LinkState::LinkSet> {
+  bool operator()(
+      openr::LinkState::LinkSet const& a, openr::LinkState::LinkSet const& b) const;
+};
+} // namespace std

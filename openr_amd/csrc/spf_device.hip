@@ -1,0 +1,1313 @@
+// spf_device.hip — MI355X (gfx950) kernels and the C ABI of include/openr_spf.h
+//
+// The reference runs one Dijkstra per source on the Decision thread, walking a
+// string-keyed graph (openr/decision/LinkState.cpp:806-880).  Here a batch of
+// sources is solved at once, one workgroup per source, against a device CSR
+// that every workgroup shares through L2:
+//
+//  * spf_sssp_kernel  (fast path, every usable metric in [1, 2^31)):
+//      the per-source state (distance row, frontier bitmaps, node queue) lives
+//      in LDS (or, for graphs too large for LDS, in a global scratch slab).
+//      Rounds alternate
+//        PUSH  — every node whose (dist, next-hops) changed marks the
+//                neighbours it could still improve or tie (ds_or on an LDS
+//                bitmap), and
+//        PULL  — every marked node recomputes its distance and ECMP next-hop
+//                mask from ALL its in-edges (min over d[u]+w, OR of the
+//                predecessors' masks at the minimum).
+//      A node is written only by the group that owns it in PULL, so no
+//      distance atomics are needed and the fixpoint is deterministic.  With
+//      unit metrics every node is pulled exactly once (level-synchronous
+//      BFS); with weights it is a frontier Bellman-Ford.
+//      This is the order-free restatement of runSpf validated in SURVEY §8(a):
+//        d = Dijkstra where u relaxes only if u==src or !overloaded(u);
+//        NH(v) = OR over usable u->v with d[u]+w==d[v] and (u==src ||
+//                !overloaded(u)) of (u==src ? {v} : NH(u)).
+//  * spf_exact_kernel (metric 0 or 64-bit metric sums): one thread per query
+//      replays the reference DijkstraQ literally — (metric, name) ordered
+//      extraction of DISCOVERED nodes, >= relaxation into unsettled nodes,
+//      union of next hops, "directly connected" rule — with uint64 wrap-around
+//      arithmetic, and records the settle order (pathLinks ordering).
+//
+// Node ids are name ranks, so "ties settle by name" is "ties settle by id".
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "openr_spf.h"
+
+namespace {
+
+constexpr uint32_t kBlock = 512;           // threads per workgroup (8 waves)
+constexpr uint32_t kWaves = kBlock / 64;
+constexpr uint32_t kInf32 = 0xFFFFFFFFu;
+constexpr uint32_t kCtlWords = 16;         // qlen + scan scratch
+constexpr size_t kLdsLimit = 160 * 1024;   // gfx950 LDS per CU
+constexpr uint32_t kIgnLdsMax = 2048;      // ignore-list entries staged in LDS
+constexpr uint32_t kNotSeen = 0xFFFFFFFFu; // exact kernel heap states
+constexpr uint32_t kSettled = 0xFFFFFFFEu;
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& what) {
+  g_last_error = what;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                       \
+  do {                                                                      \
+    hipError_t e_ = (expr);                                                 \
+    if (e_ != hipSuccess) {                                                 \
+      return fail(                                                          \
+          e_ == hipErrorOutOfMemory ? SPF_E_NOMEM : SPF_E_DEVICE,           \
+          std::string(#expr) + ": " + hipGetErrorString(e_));               \
+    }                                                                       \
+  } while (0)
+
+// ---------------------------------------------------------------- device utils
+
+__device__ __forceinline__ uint32_t grp_min(uint32_t x, int G) {
+  for (int o = G >> 1; o > 0; o >>= 1) {
+    x = min(x, (uint32_t)__shfl_xor((int)x, o, G));
+  }
+  return x;
+}
+
+__device__ __forceinline__ uint64_t grp_or(uint64_t x, int G) {
+  for (int o = G >> 1; o > 0; o >>= 1) {
+    x |= (uint64_t)__shfl_xor((unsigned long long)x, o, G);
+  }
+  return x;
+}
+
+__device__ __forceinline__ bool in_sorted(
+    const uint32_t* a, uint32_t n, uint32_t x) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    uint32_t m = a[mid];
+    if (m == x) {
+      return true;
+    }
+    if (m < x) {
+      lo = mid + 1;
+    } else {
+      hi = mid;
+    }
+  }
+  return false;
+}
+
+// Exclusive scan of one value per thread over the workgroup.  `scan` holds
+// kWaves+1 LDS words.  Returns the thread's offset; *total = block sum.
+__device__ __forceinline__ uint32_t block_excl_scan(
+    uint32_t x, uint32_t* scan, uint32_t* total) {
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  uint32_t inc = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = (uint32_t)__shfl_up((int)inc, o, 64);
+    if (lane >= (uint32_t)o) {
+      inc += y;
+    }
+  }
+  if (lane == 63) {
+    scan[wid] = inc;
+  }
+  __syncthreads();
+  if (wid == 0) {
+    uint32_t w = lane < kWaves ? scan[lane] : 0;
+#pragma unroll
+    for (int o = 1; o < (int)kWaves; o <<= 1) {
+      uint32_t y = (uint32_t)__shfl_up((int)w, o, 64);
+      if (lane >= (uint32_t)o) {
+        w += y;
+      }
+    }
+    if (lane < kWaves) {
+      scan[lane] = w;
+    }
+  }
+  __syncthreads();
+  uint32_t base = wid ? scan[wid - 1] : 0;
+  *total = scan[kWaves - 1];
+  return base + inc - x;
+}
+
+// Turn a node bitmap into a queue of node ids (ascending), clearing the bitmap.
+template <typename QT>
+__device__ __forceinline__ uint32_t compact_bits(
+    uint32_t* bits, uint32_t nbw, QT* queue, uint32_t* scan) {
+  const uint32_t chunk = (nbw + kBlock - 1) / kBlock;
+  const uint32_t w0 = min(threadIdx.x * chunk, nbw);
+  const uint32_t w1 = min(w0 + chunk, nbw);
+  uint32_t cnt = 0;
+  for (uint32_t w = w0; w < w1; ++w) {
+    cnt += __popc(bits[w]);
+  }
+  uint32_t total;
+  uint32_t off = block_excl_scan(cnt, scan, &total);
+  for (uint32_t w = w0; w < w1; ++w) {
+    uint32_t b = bits[w];
+    if (b) {
+      bits[w] = 0;
+      do {
+        uint32_t k = __ffs(b) - 1;
+        b &= b - 1;
+        queue[off++] = (QT)(w * 32 + k);
+      } while (b);
+    }
+  }
+  return total;
+}
+
+struct SsspArgs {
+  // graph
+  const uint32_t* row;
+  const uint32_t* col;
+  const uint32_t* wout; // metric of u->v advertised by the row node u
+  const uint32_t* win;  // metric of v->u for the entry (u, v): w_out[rev[e]]
+  const uint32_t* link;
+  const uint32_t* rev;
+  const uint32_t* slot; // slot of col[e] among the row node's distinct nbrs
+  const uint32_t* trbits;
+  // batch
+  const uint32_t* src;
+  const uint32_t* ign_off;
+  const uint32_t* ign;
+  const uint64_t* nh_off;
+  const uint32_t* nh_w;
+  uint32_t* dist_out;
+  uint64_t* nh_out;
+  uint32_t* gscratch; // GMEM: per-workgroup node queue (V u32)
+  uint32_t V;
+  uint32_t nbw;
+  uint32_t nq;
+  uint32_t G;       // lanes per node (power of two, <= 64)
+  uint32_t ign_cap; // LDS words reserved for the ignore list
+};
+
+// WMAX: max next-hop words (0 = distances only).  UNIT: every hop costs 1.
+// IGN: per-query ignored links.  GMEM: distances / queue in global memory.
+template <int WMAX, bool UNIT, bool IGN, bool GMEM>
+__global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
+  extern __shared__ __align__(16) uint32_t smem[];
+  using QT = typename std::conditional<GMEM, uint32_t, uint16_t>::type;
+
+  const uint32_t V = a.V, nbw = a.nbw, G = a.G;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lg = tid & (G - 1);
+  const uint32_t grp = tid / G, ngrp = kBlock / G;
+
+  uint32_t* act = smem;
+  uint32_t* chg = act + nbw;
+  uint32_t* tr = chg + nbw;
+  uint32_t* ctl = tr + nbw;
+  uint32_t* ignl = ctl + kCtlWords;
+  QT* queue;
+  uint32_t* dist;
+  if constexpr (GMEM) {
+    queue = a.gscratch + (size_t)blockIdx.x * V;
+    dist = nullptr;
+  } else {
+    queue = reinterpret_cast<QT*>(ignl + a.ign_cap);
+    dist = reinterpret_cast<uint32_t*>(queue + ((V + 1) & ~1u));
+  }
+
+  for (uint32_t i = tid; i < nbw; i += kBlock) {
+    act[i] = 0;
+    chg[i] = 0;
+    tr[i] = a.trbits[i];
+  }
+
+  for (uint32_t q = blockIdx.x; q < a.nq; q += gridDim.x) {
+    const uint32_t src = a.src[q];
+    if constexpr (GMEM) {
+      dist = a.dist_out + (size_t)q * V;
+    }
+    uint32_t nign = 0;
+    const uint32_t* ignp = ignl;
+    if constexpr (IGN) {
+      const uint32_t lo = a.ign_off[q];
+      nign = a.ign_off[q + 1] - lo;
+      if (nign <= a.ign_cap) {
+        for (uint32_t i = tid; i < nign; i += kBlock) {
+          ignl[i] = a.ign[lo + i];
+        }
+      } else {
+        ignp = a.ign + lo;
+      }
+    }
+    uint32_t Wm = 0;
+    uint64_t* nhrow = nullptr;
+    if constexpr (WMAX > 0) {
+      Wm = a.nh_w[q];
+      nhrow = a.nh_out + a.nh_off[q];
+    }
+    for (uint32_t v = tid; v < V; v += kBlock) {
+      dist[v] = kInf32;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      dist[src] = 0;
+      queue[0] = (QT)src;
+      ctl[0] = 1;
+    }
+    if constexpr (WMAX > 0) {
+      if (tid < Wm) {
+        nhrow[(size_t)src * Wm + tid] = 0; // the source has no next hop
+      }
+    }
+    __syncthreads();
+    uint32_t qlen = ctl[0];
+
+    while (qlen) {
+      // ---- PUSH: changed nodes mark the neighbours they can improve or tie
+      for (uint32_t i = grp; i < qlen; i += ngrp) {
+        const uint32_t u = queue[i];
+        if (u != src && !((tr[u >> 5] >> (u & 31)) & 1u)) {
+          continue; // overloaded: recorded but never transited
+        }
+        const uint32_t du = dist[u];
+        const uint32_t beg = a.row[u], end = a.row[u + 1];
+        for (uint32_t e = beg + lg; e < end; e += G) {
+          if constexpr (IGN) {
+            if (nign && in_sorted(ignp, nign, a.link[e])) {
+              continue;
+            }
+          }
+          const uint32_t v = a.col[e];
+          const uint32_t c = du + (UNIT ? 1u : a.wout[e]);
+          if (c <= dist[v]) {
+            const uint32_t bit = 1u << (v & 31);
+            if (!(act[v >> 5] & bit)) {
+              atomicOr(&act[v >> 5], bit);
+            }
+          }
+        }
+      }
+      __syncthreads();
+      qlen = compact_bits<QT>(act, nbw, queue, ctl + 1);
+      __syncthreads();
+
+      // ---- PULL: marked nodes recompute (dist, next hops) from all in-edges
+      for (uint32_t i = grp; i < qlen; i += ngrp) {
+        const uint32_t v = queue[i];
+        const uint32_t beg = a.row[v], end = a.row[v + 1];
+        uint32_t best = kInf32;
+        uint64_t nh[WMAX > 0 ? WMAX : 1];
+#pragma unroll
+        for (int j = 0; j < (WMAX > 0 ? WMAX : 1); ++j) {
+          nh[j] = 0;
+        }
+        for (uint32_t e = beg + lg; e < end; e += G) {
+          if constexpr (IGN) {
+            if (nign && in_sorted(ignp, nign, a.link[e])) {
+              continue;
+            }
+          }
+          const uint32_t u = a.col[e];
+          const bool isSrc = (u == src);
+          if (!isSrc && !((tr[u >> 5] >> (u & 31)) & 1u)) {
+            continue;
+          }
+          const uint32_t du = dist[u];
+          if (du == kInf32) {
+            continue;
+          }
+          const uint32_t c = du + (UNIT ? 1u : a.win[e]);
+          if (c < best) {
+            best = c;
+#pragma unroll
+            for (int j = 0; j < (WMAX > 0 ? WMAX : 1); ++j) {
+              nh[j] = 0;
+            }
+          }
+          if constexpr (WMAX > 0) {
+            if (c == best) {
+              if (isSrc) {
+                // directly connected: the first hop is v itself
+                const uint32_t s = a.slot[a.rev[e]];
+#pragma unroll
+                for (int j = 0; j < WMAX; ++j) {
+                  if ((uint32_t)j == (s >> 6)) {
+                    nh[j] |= 1ull << (s & 63);
+                  }
+                }
+              } else {
+                const uint64_t* p = nhrow + (size_t)u * Wm;
+#pragma unroll
+                for (int j = 0; j < WMAX; ++j) {
+                  if ((uint32_t)j < Wm) {
+                    nh[j] |= p[j];
+                  }
+                }
+              }
+            }
+          }
+        }
+        const uint32_t gbest = grp_min(best, (int)G);
+        if constexpr (WMAX > 0) {
+#pragma unroll
+          for (int j = 0; j < WMAX; ++j) {
+            nh[j] = grp_or(best == gbest ? nh[j] : 0ull, (int)G);
+          }
+        }
+        if (lg == 0 && gbest != kInf32) {
+          const uint32_t old = dist[v];
+          bool changed = gbest < old;
+          uint64_t* row = nullptr;
+          if constexpr (WMAX > 0) {
+            row = nhrow + (size_t)v * Wm;
+            if (!changed && gbest == old) {
+#pragma unroll
+              for (int j = 0; j < WMAX; ++j) {
+                if ((uint32_t)j < Wm && row[j] != nh[j]) {
+                  changed = true;
+                }
+              }
+            }
+          }
+          if (changed) {
+            dist[v] = gbest;
+            if constexpr (WMAX > 0) {
+#pragma unroll
+              for (int j = 0; j < WMAX; ++j) {
+                if ((uint32_t)j < Wm) {
+                  row[j] = nh[j];
+                }
+              }
+            }
+            atomicOr(&chg[v >> 5], 1u << (v & 31));
+          }
+        }
+      }
+      __syncthreads();
+      qlen = compact_bits<QT>(chg, nbw, queue, ctl + 1);
+      __syncthreads();
+    }
+
+    if constexpr (!GMEM) {
+      uint32_t* out = a.dist_out + (size_t)q * V;
+      for (uint32_t v = tid; v < V; v += kBlock) {
+        out[v] = dist[v];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------- exact kernel
+
+struct ExactArgs {
+  const uint32_t* row;
+  const uint32_t* col;
+  const uint64_t* w64;
+  const uint32_t* link;
+  const uint32_t* slot;
+  const uint32_t* trbits;
+  const uint32_t* src;
+  const uint32_t* ign_off;
+  const uint32_t* ign;
+  const uint64_t* nh_off;
+  const uint32_t* nh_w;
+  uint64_t* dist_out;
+  uint64_t* nh_out;
+  uint32_t* order_out;
+  uint32_t* scratch; // per query: pos[V] + heap[V]
+  uint32_t V;
+  uint32_t nq;
+  uint32_t unit;
+  uint32_t want_nh;
+};
+
+__device__ __forceinline__ bool ex_less(
+    const uint64_t* d, uint32_t a, uint32_t b) {
+  return d[a] < d[b] || (d[a] == d[b] && a < b);
+}
+
+__device__ void ex_sift_up(
+    uint32_t* heap, uint32_t* pos, const uint64_t* d, uint32_t i) {
+  const uint32_t x = heap[i];
+  while (i > 0) {
+    const uint32_t p = (i - 1) >> 1;
+    if (!ex_less(d, x, heap[p])) {
+      break;
+    }
+    heap[i] = heap[p];
+    pos[heap[i]] = i;
+    i = p;
+  }
+  heap[i] = x;
+  pos[x] = i;
+}
+
+__device__ void ex_sift_down(
+    uint32_t* heap, uint32_t* pos, const uint64_t* d, uint32_t n, uint32_t i) {
+  const uint32_t x = heap[i];
+  for (;;) {
+    uint32_t c = 2 * i + 1;
+    if (c >= n) {
+      break;
+    }
+    if (c + 1 < n && ex_less(d, heap[c + 1], heap[c])) {
+      ++c;
+    }
+    if (!ex_less(d, heap[c], x)) {
+      break;
+    }
+    heap[i] = heap[c];
+    pos[heap[i]] = i;
+    i = c;
+  }
+  heap[i] = x;
+  pos[x] = i;
+}
+
+// One thread per query: the literal DijkstraQ replay (LinkState.cpp:816-873).
+__global__ __launch_bounds__(64) void spf_exact_kernel(ExactArgs a) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= a.nq) {
+    return;
+  }
+  const uint32_t V = a.V;
+  const uint32_t src = a.src[q];
+  uint64_t* d = a.dist_out + (size_t)q * V;
+  uint32_t* order = a.order_out + (size_t)q * V;
+  uint32_t* pos = a.scratch + (size_t)q * 2 * V;
+  uint32_t* heap = pos + V;
+  const uint32_t Wm = a.want_nh ? a.nh_w[q] : 0;
+  uint64_t* nhrow = a.want_nh ? a.nh_out + a.nh_off[q] : nullptr;
+  const uint32_t ilo = a.ign_off ? a.ign_off[q] : 0;
+  const uint32_t nign = a.ign_off ? a.ign_off[q + 1] - ilo : 0;
+  const uint32_t* ignp = a.ign ? a.ign + ilo : nullptr;
+
+  for (uint32_t v = 0; v < V; ++v) {
+    pos[v] = kNotSeen;
+    order[v] = kInf32;
+    d[v] = SPF_UNREACHABLE;
+  }
+  uint32_t n = 0, settled = 0;
+  d[src] = 0;
+  heap[n++] = src;
+  pos[src] = 0;
+  while (n) {
+    const uint32_t u = heap[0];
+    --n;
+    if (n) {
+      heap[0] = heap[n];
+      pos[heap[0]] = 0;
+      ex_sift_down(heap, pos, d, n, 0);
+    }
+    pos[u] = kSettled;
+    order[u] = settled++;
+    if (u != src && !((a.trbits[u >> 5] >> (u & 31)) & 1u)) {
+      continue;
+    }
+    const uint64_t du = d[u];
+    for (uint32_t e = a.row[u]; e < a.row[u + 1]; ++e) {
+      const uint32_t v = a.col[e];
+      if (pos[v] == kSettled) {
+        continue;
+      }
+      if (nign && in_sorted(ignp, nign, a.link[e])) {
+        continue;
+      }
+      const uint64_t c = du + (a.unit ? 1ull : a.w64[e]);
+      if (pos[v] == kNotSeen) {
+        d[v] = c;
+        heap[n] = v;
+        pos[v] = n;
+        ex_sift_up(heap, pos, d, n);
+        ++n;
+      }
+      if (d[v] >= c) {
+        if (d[v] > c) {
+          d[v] = c;
+          for (uint32_t j = 0; j < Wm; ++j) {
+            nhrow[(size_t)v * Wm + j] = 0;
+          }
+          ex_sift_up(heap, pos, d, pos[v]);
+        }
+        if (Wm) {
+          uint64_t any = 0;
+          for (uint32_t j = 0; j < Wm; ++j) {
+            uint64_t m = (u == src) ? 0ull : nhrow[(size_t)u * Wm + j];
+            m |= nhrow[(size_t)v * Wm + j];
+            nhrow[(size_t)v * Wm + j] = m;
+            any |= m;
+          }
+          if (!any && u == src) {
+            const uint32_t s = a.slot[e];
+            nhrow[(size_t)v * Wm + (s >> 6)] |= 1ull << (s & 63);
+          }
+        }
+      }
+    }
+  }
+}
+
+__global__ void fill_u32_kernel(uint32_t* p, size_t n, uint32_t v) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) {
+    p[i] = v;
+  }
+}
+
+} // namespace
+
+// ==================================================================== host side
+
+struct spf_graph {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  uint32_t V = 0, E = 0, L = 0, nbw = 0;
+  bool exact = false;
+  uint32_t G = 8;
+  int num_cus = 256;
+  // host copies
+  std::vector<uint32_t> row, col, link, rev, slot, nbr_off, nbrs, trbits;
+  std::vector<uint64_t> w64;
+  // device copies
+  uint32_t *d_row = nullptr, *d_col = nullptr, *d_wout = nullptr,
+           *d_win = nullptr, *d_link = nullptr, *d_rev = nullptr,
+           *d_slot = nullptr, *d_tr = nullptr;
+  uint64_t* d_w64 = nullptr;
+};
+
+struct spf_query {
+  spf_graph* g = nullptr;
+  uint32_t nq = 0, flags = 0;
+  int kind = 0; // 0 lds, 1 gmem, 2 exact
+  int wmax = 0;
+  uint32_t ign_cap = 0, grid = 0;
+  size_t lds_bytes = 0;
+  bool has_ign = false;
+  std::vector<uint64_t> nh_off;
+  std::vector<uint32_t> nh_w;
+  uint64_t nh_total = 0;
+  uint32_t *d_src = nullptr, *d_ign_off = nullptr, *d_ign = nullptr,
+           *d_nh_w = nullptr, *d_order = nullptr, *d_scratch = nullptr;
+  uint64_t* d_nh_off = nullptr;
+  void* d_dist = nullptr;
+  uint64_t* d_nh = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool ran = false;
+};
+
+namespace {
+
+template <typename T>
+int dev_upload(T** dst, const T* src, size_t n) {
+  *dst = nullptr;
+  if (n == 0) {
+    return SPF_OK;
+  }
+  HIP_TRY(hipMalloc((void**)dst, n * sizeof(T)));
+  HIP_TRY(hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice));
+  return SPF_OK;
+}
+
+#define SPF_TRY(expr)   \
+  do {                  \
+    int s_ = (expr);    \
+    if (s_ != SPF_OK) { \
+      return s_;        \
+    }                   \
+  } while (0)
+
+void free_graph(spf_graph* g) {
+  if (!g) {
+    return;
+  }
+  (void)hipSetDevice(g->device);
+  for (void* p :
+       {(void*)g->d_row, (void*)g->d_col, (void*)g->d_wout, (void*)g->d_win,
+        (void*)g->d_link, (void*)g->d_rev, (void*)g->d_slot, (void*)g->d_tr,
+        (void*)g->d_w64}) {
+    if (p) {
+      (void)hipFree(p);
+    }
+  }
+  if (g->own_stream) {
+    (void)hipStreamDestroy(g->own_stream);
+  }
+  delete g;
+}
+
+void free_query(spf_query* q) {
+  if (!q) {
+    return;
+  }
+  (void)hipSetDevice(q->g->device);
+  for (void* p :
+       {(void*)q->d_src, (void*)q->d_ign_off, (void*)q->d_ign,
+        (void*)q->d_nh_w, (void*)q->d_order, (void*)q->d_scratch,
+        (void*)q->d_nh_off, q->d_dist, (void*)q->d_nh}) {
+    if (p) {
+      (void)hipFree(p);
+    }
+  }
+  if (q->ev0) {
+    (void)hipEventDestroy(q->ev0);
+  }
+  if (q->ev1) {
+    (void)hipEventDestroy(q->ev1);
+  }
+  delete q;
+}
+
+// fast-path weights and exactness from the 64-bit metrics
+int upload_weights(spf_graph* g) {
+  const uint32_t E = g->E;
+  uint64_t maxw = 0;
+  bool exact = false;
+  for (uint32_t e = 0; e < E; ++e) {
+    const uint64_t m = g->w64[e];
+    if (m == 0 || m > 0x7FFFFFFFull) {
+      exact = true;
+    }
+    maxw = std::max(maxw, m);
+  }
+  if (!exact && g->V > 1 && maxw > 0 &&
+      (unsigned __int128)maxw * (g->V - 1) >= 0xFFFFFFFFull) {
+    exact = true;
+  }
+  g->exact = exact;
+  std::vector<uint32_t> wout(E), win(E);
+  for (uint32_t e = 0; e < E; ++e) {
+    wout[e] = (uint32_t)std::min<uint64_t>(g->w64[e], 0xFFFFFFFFull);
+  }
+  for (uint32_t e = 0; e < E; ++e) {
+    win[e] = wout[g->rev[e]];
+  }
+  if (E) {
+    if (!g->d_wout) {
+      HIP_TRY(hipMalloc((void**)&g->d_wout, E * 4));
+      HIP_TRY(hipMalloc((void**)&g->d_win, E * 4));
+      HIP_TRY(hipMalloc((void**)&g->d_w64, E * 8));
+    }
+    HIP_TRY(hipMemcpy(g->d_wout, wout.data(), E * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(g->d_win, win.data(), E * 4, hipMemcpyHostToDevice));
+    HIP_TRY(
+        hipMemcpy(g->d_w64, g->w64.data(), E * 8, hipMemcpyHostToDevice));
+  }
+  return SPF_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int spf_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    return 0;
+  }
+  return n;
+}
+
+const char* spf_error_string(int status) {
+  switch (status) {
+  case SPF_OK:
+    return "ok";
+  case SPF_E_INVALID:
+    return "invalid argument";
+  case SPF_E_NOMEM:
+    return "out of memory";
+  case SPF_E_DEVICE:
+    return "device error";
+  case SPF_E_UNSUPPORTED:
+    return "unsupported shape";
+  default:
+    return "unknown status";
+  }
+}
+
+const char* spf_last_error_detail(void) {
+  return g_last_error.c_str();
+}
+
+int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
+  if (!desc || !out) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  *out = nullptr;
+  const uint32_t V = desc->num_nodes, E = desc->num_edges;
+  if (!desc->row_ptr || (E && (!desc->col || !desc->metric ||
+                               !desc->link_id || !desc->rev)) ||
+      (V && !desc->node_overloaded)) {
+    return fail(SPF_E_INVALID, "missing graph array");
+  }
+  if (desc->row_ptr[0] != 0 || desc->row_ptr[V] != E) {
+    return fail(SPF_E_INVALID, "row_ptr does not span [0, E]");
+  }
+  for (uint32_t u = 0; u < V; ++u) {
+    if (desc->row_ptr[u + 1] < desc->row_ptr[u]) {
+      return fail(SPF_E_INVALID, "row_ptr not monotone");
+    }
+  }
+  for (uint32_t u = 0; u < V; ++u) {
+    for (uint32_t e = desc->row_ptr[u]; e < desc->row_ptr[u + 1]; ++e) {
+      const uint32_t v = desc->col[e], r = desc->rev[e];
+      if (v >= V || r >= E || desc->rev[r] != e || desc->col[r] != u ||
+          desc->link_id[e] >= desc->num_links ||
+          desc->link_id[r] != desc->link_id[e]) {
+        return fail(SPF_E_INVALID, "inconsistent half-edge at " +
+                                       std::to_string(e));
+      }
+    }
+  }
+  int ndev = spf_device_count();
+  if (ndev <= 0) {
+    return fail(SPF_E_DEVICE, "no HIP device visible");
+  }
+  if (desc->device < 0 || desc->device >= ndev) {
+    return fail(SPF_E_INVALID, "bad device ordinal");
+  }
+
+  spf_graph* g = new spf_graph();
+  g->device = desc->device;
+  g->V = V;
+  g->E = E;
+  g->L = desc->num_links;
+  g->nbw = (V + 31) / 32;
+  g->row.assign(desc->row_ptr, desc->row_ptr + V + 1);
+  g->col.assign(desc->col, desc->col + E);
+  g->link.assign(desc->link_id, desc->link_id + E);
+  g->rev.assign(desc->rev, desc->rev + E);
+  g->w64.assign(desc->metric, desc->metric + E);
+  g->trbits.assign(std::max<uint32_t>(g->nbw, 1), 0);
+  for (uint32_t v = 0; v < V; ++v) {
+    if (!desc->node_overloaded[v]) {
+      g->trbits[v >> 5] |= 1u << (v & 31);
+    }
+  }
+  // distinct neighbours per node (ascending id = name order) and edge slots
+  g->nbr_off.assign(V + 1, 0);
+  g->slot.assign(E, 0);
+  std::vector<uint32_t> tmp;
+  for (uint32_t u = 0; u < V; ++u) {
+    tmp.assign(g->col.begin() + g->row[u], g->col.begin() + g->row[u + 1]);
+    std::sort(tmp.begin(), tmp.end());
+    tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
+    g->nbr_off[u + 1] = g->nbr_off[u] + (uint32_t)tmp.size();
+    g->nbrs.insert(g->nbrs.end(), tmp.begin(), tmp.end());
+    for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
+      g->slot[e] = (uint32_t)(std::lower_bound(tmp.begin(), tmp.end(),
+                                               g->col[e]) -
+                              tmp.begin());
+    }
+  }
+  // lanes per node: the median degree, rounded to a power of two in [4, 64]
+  {
+    std::vector<uint32_t> deg(V);
+    for (uint32_t u = 0; u < V; ++u) {
+      deg[u] = g->row[u + 1] - g->row[u];
+    }
+    uint32_t med = 4;
+    if (V) {
+      std::nth_element(deg.begin(), deg.begin() + V / 2, deg.end());
+      med = deg[V / 2];
+    }
+    uint32_t G = 4;
+    while (G < med && G < 64) {
+      G <<= 1;
+    }
+    g->G = G;
+  }
+
+  auto bail = [&](int s) {
+    free_graph(g);
+    return s;
+  };
+  if (hipSetDevice(g->device) != hipSuccess) {
+    return bail(fail(SPF_E_DEVICE, "hipSetDevice failed"));
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, g->device) == hipSuccess &&
+      prop.multiProcessorCount > 0) {
+    g->num_cus = prop.multiProcessorCount;
+  }
+  if (hipStreamCreateWithFlags(&g->own_stream, hipStreamNonBlocking) !=
+      hipSuccess) {
+    return bail(fail(SPF_E_DEVICE, "hipStreamCreate failed"));
+  }
+  g->stream = g->own_stream;
+  int s = SPF_OK;
+  if ((s = dev_upload(&g->d_row, g->row.data(), V + 1)) ||
+      (s = dev_upload(&g->d_col, g->col.data(), E)) ||
+      (s = dev_upload(&g->d_link, g->link.data(), E)) ||
+      (s = dev_upload(&g->d_rev, g->rev.data(), E)) ||
+      (s = dev_upload(&g->d_slot, g->slot.data(), E)) ||
+      (s = dev_upload(&g->d_tr, g->trbits.data(), g->trbits.size())) ||
+      (s = upload_weights(g))) {
+    return bail(s);
+  }
+  *out = g;
+  return SPF_OK;
+}
+
+int spf_graph_destroy(spf_graph* g) {
+  free_graph(g);
+  return SPF_OK;
+}
+
+int spf_graph_set_transit(spf_graph* g, const uint8_t* node_overloaded) {
+  if (!g || (g->V && !node_overloaded)) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  std::fill(g->trbits.begin(), g->trbits.end(), 0u);
+  for (uint32_t v = 0; v < g->V; ++v) {
+    if (!node_overloaded[v]) {
+      g->trbits[v >> 5] |= 1u << (v & 31);
+    }
+  }
+  HIP_TRY(hipSetDevice(g->device));
+  HIP_TRY(hipStreamSynchronize(g->stream));
+  HIP_TRY(hipMemcpy(g->d_tr, g->trbits.data(), g->trbits.size() * 4,
+                    hipMemcpyHostToDevice));
+  return SPF_OK;
+}
+
+int spf_graph_patch_metrics(
+    spf_graph* g, uint32_t n, const uint32_t* edge_idx, const uint64_t* m) {
+  if (!g || (n && (!edge_idx || !m))) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    if (edge_idx[i] >= g->E) {
+      return fail(SPF_E_INVALID, "edge index out of range");
+    }
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    g->w64[edge_idx[i]] = m[i];
+  }
+  HIP_TRY(hipSetDevice(g->device));
+  HIP_TRY(hipStreamSynchronize(g->stream));
+  return upload_weights(g);
+}
+
+int spf_graph_set_stream(spf_graph* g, void* stream) {
+  if (!g) {
+    return fail(SPF_E_INVALID, "null graph");
+  }
+  g->stream = stream ? (hipStream_t)stream : g->own_stream;
+  return SPF_OK;
+}
+
+void* spf_graph_get_stream(spf_graph* g) {
+  return g ? (void*)g->stream : nullptr;
+}
+
+int spf_graph_needs_exact(const spf_graph* g) {
+  return g && g->exact ? 1 : 0;
+}
+
+int spf_graph_num_nbrs(const spf_graph* g, uint32_t node) {
+  if (!g || node >= g->V) {
+    return fail(SPF_E_INVALID, "bad node");
+  }
+  return (int)(g->nbr_off[node + 1] - g->nbr_off[node]);
+}
+
+int spf_graph_nbrs(const spf_graph* g, uint32_t node, uint32_t* out) {
+  if (!g || node >= g->V || !out) {
+    return fail(SPF_E_INVALID, "bad node");
+  }
+  std::copy(g->nbrs.begin() + g->nbr_off[node],
+            g->nbrs.begin() + g->nbr_off[node + 1], out);
+  return SPF_OK;
+}
+
+int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) {
+  if (!g || !desc || !out) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  *out = nullptr;
+  const uint32_t nq = desc->num_queries, V = g->V;
+  if (nq && !desc->sources) {
+    return fail(SPF_E_INVALID, "null sources");
+  }
+  for (uint32_t i = 0; i < nq; ++i) {
+    if (desc->sources[i] >= V) {
+      return fail(SPF_E_INVALID, "source out of range");
+    }
+  }
+  const bool has_ign = desc->ignore_offsets != nullptr;
+  uint32_t max_ign = 0;
+  if (has_ign) {
+    if (desc->ignore_offsets[0] != 0) {
+      return fail(SPF_E_INVALID, "ignore_offsets[0] != 0");
+    }
+    for (uint32_t i = 0; i < nq; ++i) {
+      const uint32_t lo = desc->ignore_offsets[i],
+                     hi = desc->ignore_offsets[i + 1];
+      if (hi < lo || (hi > lo && !desc->ignore_links)) {
+        return fail(SPF_E_INVALID, "bad ignore_offsets");
+      }
+      for (uint32_t k = lo + 1; k < hi; ++k) {
+        if (desc->ignore_links[k - 1] >= desc->ignore_links[k]) {
+          return fail(SPF_E_INVALID, "ignore list not strictly sorted");
+        }
+      }
+      max_ign = std::max(max_ign, hi - lo);
+    }
+  }
+
+  spf_query* q = new spf_query();
+  q->g = g;
+  q->nq = nq;
+  q->flags = desc->flags;
+  q->has_ign = has_ign;
+  auto bail = [&](int s) {
+    free_query(q);
+    return s;
+  };
+  const bool unit = desc->flags & SPF_F_UNIT_METRIC;
+  const bool want_nh = desc->flags & SPF_F_NEXTHOPS;
+  const bool want_order = desc->flags & SPF_F_ORDER;
+
+  // next-hop mask geometry
+  uint32_t maxw = 0;
+  q->nh_off.assign(nq, 0);
+  q->nh_w.assign(nq, 0);
+  if (want_nh) {
+    uint64_t off = 0;
+    for (uint32_t i = 0; i < nq; ++i) {
+      const uint32_t s = desc->sources[i];
+      const uint32_t nn = g->nbr_off[s + 1] - g->nbr_off[s];
+      const uint32_t w = std::max<uint32_t>(1, (nn + 63) / 64);
+      q->nh_off[i] = off;
+      q->nh_w[i] = w;
+      off += (uint64_t)w * V;
+      maxw = std::max(maxw, w);
+    }
+    q->nh_total = off;
+  }
+
+  // kernel choice
+  if ((g->exact && !unit) || want_order || maxw > 16) {
+    q->kind = 2;
+  } else {
+    q->wmax = !want_nh ? 0 : (maxw <= 1 ? 1 : (maxw <= 4 ? 4 : 16));
+    q->ign_cap = has_ign ? std::min(max_ign, kIgnLdsMax) : 0;
+    const size_t ctl =
+        (3 * (size_t)g->nbw + kCtlWords + q->ign_cap) * sizeof(uint32_t);
+    const size_t lds =
+        ctl + (size_t)((V + 1) & ~1u) * 2 + (size_t)V * 4; // u16 queue + dist
+    if (V <= 65535 && lds <= kLdsLimit) {
+      q->kind = 0;
+      q->lds_bytes = lds;
+      const uint32_t per_cu =
+          std::max<uint32_t>(1, std::min<uint32_t>(4, kLdsLimit / lds));
+      q->grid = std::min<uint32_t>(std::max<uint32_t>(nq, 1),
+                                   (uint32_t)g->num_cus * per_cu);
+    } else if (ctl <= kLdsLimit) {
+      q->kind = 1;
+      q->lds_bytes = ctl;
+      q->grid = std::min<uint32_t>(std::max<uint32_t>(nq, 1),
+                                   (uint32_t)g->num_cus * 2);
+    } else {
+      return bail(fail(SPF_E_UNSUPPORTED, "graph too large for one device"));
+    }
+  }
+
+  if (hipSetDevice(g->device) != hipSuccess) {
+    return bail(fail(SPF_E_DEVICE, "hipSetDevice failed"));
+  }
+  int s = SPF_OK;
+  if ((s = dev_upload(&q->d_src, desc->sources, nq))) {
+    return bail(s);
+  }
+  if (has_ign) {
+    const uint32_t total = desc->ignore_offsets[nq];
+    if ((s = dev_upload(&q->d_ign_off, desc->ignore_offsets, nq + 1)) ||
+        (s = dev_upload(&q->d_ign, desc->ignore_links, total))) {
+      return bail(s);
+    }
+  }
+  if (want_nh) {
+    if ((s = dev_upload(&q->d_nh_off, q->nh_off.data(), nq)) ||
+        (s = dev_upload(&q->d_nh_w, q->nh_w.data(), nq))) {
+      return bail(s);
+    }
+    if (q->nh_total &&
+        hipMalloc((void**)&q->d_nh, q->nh_total * 8) != hipSuccess) {
+      return bail(fail(SPF_E_NOMEM, "next-hop rows"));
+    }
+  }
+  const size_t elem = q->kind == 2 ? 8 : 4;
+  if ((size_t)nq * V &&
+      hipMalloc(&q->d_dist, (size_t)nq * V * elem) != hipSuccess) {
+    return bail(fail(SPF_E_NOMEM, "distance rows"));
+  }
+  if (q->kind == 1 &&
+      hipMalloc((void**)&q->d_scratch, (size_t)q->grid * V * 4) !=
+          hipSuccess) {
+    return bail(fail(SPF_E_NOMEM, "queue scratch"));
+  }
+  if (q->kind == 2 && (size_t)nq * V) {
+    if (hipMalloc((void**)&q->d_scratch, (size_t)nq * V * 8) != hipSuccess ||
+        hipMalloc((void**)&q->d_order, (size_t)nq * V * 4) != hipSuccess) {
+      return bail(fail(SPF_E_NOMEM, "exact-kernel scratch"));
+    }
+  }
+  if (hipEventCreate(&q->ev0) != hipSuccess ||
+      hipEventCreate(&q->ev1) != hipSuccess) {
+    return bail(fail(SPF_E_DEVICE, "hipEventCreate failed"));
+  }
+  *out = q;
+  return SPF_OK;
+}
+
+int spf_query_destroy(spf_query* q) {
+  free_query(q);
+  return SPF_OK;
+}
+
+} // extern "C"
+
+namespace {
+
+template <int WMAX, bool UNIT, bool IGN, bool GMEM>
+int launch_sssp(spf_query* q) {
+  spf_graph* g = q->g;
+  SsspArgs a;
+  a.row = g->d_row;
+  a.col = g->d_col;
+  a.wout = g->d_wout;
+  a.win = g->d_win;
+  a.link = g->d_link;
+  a.rev = g->d_rev;
+  a.slot = g->d_slot;
+  a.trbits = g->d_tr;
+  a.src = q->d_src;
+  a.ign_off = q->d_ign_off;
+  a.ign = q->d_ign;
+  a.nh_off = q->d_nh_off;
+  a.nh_w = q->d_nh_w;
+  a.dist_out = (uint32_t*)q->d_dist;
+  a.nh_out = q->d_nh;
+  a.gscratch = q->d_scratch;
+  a.V = g->V;
+  a.nbw = g->nbw;
+  a.nq = q->nq;
+  a.G = g->G;
+  a.ign_cap = q->ign_cap;
+  auto kern = spf_sssp_kernel<WMAX, UNIT, IGN, GMEM>;
+  HIP_TRY(hipFuncSetAttribute(
+      (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (int)q->lds_bytes));
+  hipLaunchKernelGGL(
+      kern, dim3(q->grid), dim3(kBlock), q->lds_bytes, g->stream, a);
+  HIP_TRY(hipGetLastError());
+  return SPF_OK;
+}
+
+template <int WMAX>
+int dispatch_flags(spf_query* q, bool unit, bool ign, bool gmem) {
+  if (unit) {
+    if (ign) {
+      return gmem ? launch_sssp<WMAX, true, true, true>(q)
+                  : launch_sssp<WMAX, true, true, false>(q);
+    }
+    return gmem ? launch_sssp<WMAX, true, false, true>(q)
+                : launch_sssp<WMAX, true, false, false>(q);
+  }
+  if (ign) {
+    return gmem ? launch_sssp<WMAX, false, true, true>(q)
+                : launch_sssp<WMAX, false, true, false>(q);
+  }
+  return gmem ? launch_sssp<WMAX, false, false, true>(q)
+              : launch_sssp<WMAX, false, false, false>(q);
+}
+
+int launch_exact(spf_query* q) {
+  spf_graph* g = q->g;
+  ExactArgs a;
+  a.row = g->d_row;
+  a.col = g->d_col;
+  a.w64 = g->d_w64;
+  a.link = g->d_link;
+  a.slot = g->d_slot;
+  a.trbits = g->d_tr;
+  a.src = q->d_src;
+  a.ign_off = q->d_ign_off;
+  a.ign = q->d_ign;
+  a.nh_off = q->d_nh_off;
+  a.nh_w = q->d_nh_w;
+  a.dist_out = (uint64_t*)q->d_dist;
+  a.nh_out = q->d_nh;
+  a.order_out = q->d_order;
+  a.scratch = q->d_scratch;
+  a.V = g->V;
+  a.nq = q->nq;
+  a.unit = (q->flags & SPF_F_UNIT_METRIC) ? 1 : 0;
+  a.want_nh = (q->flags & SPF_F_NEXTHOPS) ? 1 : 0;
+  if (q->d_nh && q->nh_total) {
+    HIP_TRY(hipMemsetAsync(q->d_nh, 0, q->nh_total * 8, g->stream));
+  }
+  const uint32_t threads = 64;
+  hipLaunchKernelGGL(
+      spf_exact_kernel, dim3((q->nq + threads - 1) / threads), dim3(threads),
+      0, g->stream, a);
+  HIP_TRY(hipGetLastError());
+  return SPF_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int spf_query_run(spf_query* q) {
+  if (!q) {
+    return fail(SPF_E_INVALID, "null query");
+  }
+  spf_graph* g = q->g;
+  HIP_TRY(hipSetDevice(g->device));
+  HIP_TRY(hipEventRecord(q->ev0, g->stream));
+  int s = SPF_OK;
+  if (q->nq && g->V) {
+    if (q->kind == 2) {
+      s = launch_exact(q);
+    } else {
+      const bool unit = q->flags & SPF_F_UNIT_METRIC;
+      const bool gmem = q->kind == 1;
+      switch (q->wmax) {
+      case 0:
+        s = dispatch_flags<0>(q, unit, q->has_ign, gmem);
+        break;
+      case 1:
+        s = dispatch_flags<1>(q, unit, q->has_ign, gmem);
+        break;
+      case 4:
+        s = dispatch_flags<4>(q, unit, q->has_ign, gmem);
+        break;
+      default:
+        s = dispatch_flags<16>(q, unit, q->has_ign, gmem);
+        break;
+      }
+    }
+  }
+  HIP_TRY(hipEventRecord(q->ev1, g->stream));
+  q->ran = true;
+  return s;
+}
+
+int spf_query_sync(spf_query* q) {
+  if (!q) {
+    return fail(SPF_E_INVALID, "null query");
+  }
+  HIP_TRY(hipSetDevice(q->g->device));
+  HIP_TRY(hipStreamSynchronize(q->g->stream));
+  return SPF_OK;
+}
+
+int spf_query_elapsed_ms(spf_query* q, float* ms) {
+  if (!q || !ms || !q->ran) {
+    return fail(SPF_E_INVALID, "query has not run");
+  }
+  HIP_TRY(hipEventSynchronize(q->ev1));
+  HIP_TRY(hipEventElapsedTime(ms, q->ev0, q->ev1));
+  return SPF_OK;
+}
+
+const char* spf_query_kernel_name(const spf_query* q) {
+  if (!q) {
+    return "none";
+  }
+  return q->kind == 0 ? "lds" : (q->kind == 1 ? "gmem" : "exact");
+}
+
+int spf_query_dist(spf_query* q, uint32_t i, uint64_t* out) {
+  if (!q || !out || i >= q->nq) {
+    return fail(SPF_E_INVALID, "bad query row");
+  }
+  const uint32_t V = q->g->V;
+  HIP_TRY(hipSetDevice(q->g->device));
+  HIP_TRY(hipStreamSynchronize(q->g->stream));
+  if (q->kind == 2) {
+    HIP_TRY(hipMemcpy(out, (uint64_t*)q->d_dist + (size_t)i * V, V * 8ull,
+                      hipMemcpyDeviceToHost));
+    std::vector<uint32_t> order(V);
+    HIP_TRY(hipMemcpy(order.data(), q->d_order + (size_t)i * V, V * 4ull,
+                      hipMemcpyDeviceToHost));
+    for (uint32_t v = 0; v < V; ++v) {
+      if (order[v] == kInf32) {
+        out[v] = SPF_UNREACHABLE;
+      }
+    }
+    return SPF_OK;
+  }
+  std::vector<uint32_t> d(V);
+  HIP_TRY(hipMemcpy(d.data(), (uint32_t*)q->d_dist + (size_t)i * V, V * 4ull,
+                    hipMemcpyDeviceToHost));
+  for (uint32_t v = 0; v < V; ++v) {
+    out[v] = d[v] == kInf32 ? SPF_UNREACHABLE : (uint64_t)d[v];
+  }
+  return SPF_OK;
+}
+
+int spf_query_nh_words(const spf_query* q, uint32_t i) {
+  if (!q || i >= q->nq) {
+    return fail(SPF_E_INVALID, "bad query row");
+  }
+  return (int)q->nh_w[i];
+}
+
+int spf_query_nexthops(spf_query* q, uint32_t i, uint64_t* out) {
+  if (!q || !out || i >= q->nq || !(q->flags & SPF_F_NEXTHOPS)) {
+    return fail(SPF_E_INVALID, "no next hops for this row");
+  }
+  HIP_TRY(hipSetDevice(q->g->device));
+  HIP_TRY(hipStreamSynchronize(q->g->stream));
+  const size_t n = (size_t)q->nh_w[i] * q->g->V;
+  if (n) {
+    HIP_TRY(hipMemcpy(out, q->d_nh + q->nh_off[i], n * 8,
+                      hipMemcpyDeviceToHost));
+  }
+  return SPF_OK;
+}
+
+int spf_query_order(spf_query* q, uint32_t i, uint32_t* out) {
+  if (!q || !out || i >= q->nq || q->kind != 2) {
+    return fail(SPF_E_INVALID, "no settle order for this row");
+  }
+  HIP_TRY(hipSetDevice(q->g->device));
+  HIP_TRY(hipStreamSynchronize(q->g->stream));
+  HIP_TRY(hipMemcpy(out, q->d_order + (size_t)i * q->g->V, q->g->V * 4ull,
+                    hipMemcpyDeviceToHost));
+  return SPF_OK;
+}
+
+int spf_query_device_rows(
+    spf_query* q, void** dist_rows, uint32_t* dist_elem_bytes,
+    void** nh_rows, uint64_t* nh_total_words) {
+  if (!q) {
+    return fail(SPF_E_INVALID, "null query");
+  }
+  if (dist_rows) {
+    *dist_rows = q->d_dist;
+  }
+  if (dist_elem_bytes) {
+    *dist_elem_bytes = q->kind == 2 ? 8 : 4;
+  }
+  if (nh_rows) {
+    *nh_rows = q->d_nh;
+  }
+  if (nh_total_words) {
+    *nh_total_words = q->nh_total;
+  }
+  return SPF_OK;
+}
+
+} // extern "C"

@@ -1,0 +1,169 @@
+"""GPU parity of the raw C ABI (spf_query_*) against the literal DijkstraQ
+replay in oracle/spf_py.py, on seeded random graphs.
+
+Covers: positive / unit / zero / negative (uint64 wrap) metrics, overloaded
+(drained) nodes, parallel links, per-query ignored links, the LDS, global
+memory and exact kernels.  Bit-exact distances and next-hop sets.
+"""
+
+import random
+
+import numpy as np
+import pytest
+
+from openr_amd import abi
+from oracle import spf_py
+
+pytestmark = pytest.mark.gpu
+
+UNREACH = np.uint64(abi.SPF_UNREACHABLE)
+
+
+def random_links(rng, V, L, wmin=1, wmax=20, parallel=0.05, asym=True):
+    links = []
+    # spanning-ish backbone so most nodes are reachable
+    for v in range(1, V):
+        u = rng.randrange(v)
+        a = rng.randint(wmin, wmax)
+        b = rng.randint(wmin, wmax) if asym else a
+        links.append((u, v, a, b))
+    while len(links) < L:
+        u, v = rng.randrange(V), rng.randrange(V)
+        if u == v:
+            continue
+        a = rng.randint(wmin, wmax)
+        b = rng.randint(wmin, wmax) if asym else a
+        links.append((u, v, a, b))
+        if rng.random() < parallel:
+            links.append((u, v, rng.randint(wmin, wmax), rng.randint(wmin, wmax)))
+    rng.shuffle(links)
+    return links
+
+
+def check_query(csr, q, sources, use_metric, ignore=None):
+    for i, s in enumerate(sources):
+        ref = spf_py.run_spf(
+            csr, s, use_metric, frozenset(ignore[i]) if ignore else frozenset()
+        )
+        d = q.dist(i)
+        for v in range(csr.num_nodes):
+            if v in ref:
+                assert int(d[v]) == ref[v][0], (s, v)
+            else:
+                assert d[v] == UNREACH, (s, v)
+        if q.flags & abi.SPF_F_NEXTHOPS:
+            got = q.nexthop_sets(i, s)
+            for v, (m, nhs, _, _) in ref.items():
+                if v == s:
+                    assert got[v] == frozenset()
+                else:
+                    assert got[v] == nhs, (s, v, got[v], nhs)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_weighted_random(gpu_ready, seed):
+    rng = random.Random(seed)
+    V = 300
+    links = random_links(rng, V, 1200)
+    ov = [1 if rng.random() < 0.03 else 0 for _ in range(V)]
+    csr = abi.Csr.from_links(V, links, ov)
+    g = abi.Graph(csr)
+    assert not g.needs_exact
+    sources = list(range(0, V, 7))
+    q = g.query(sources, abi.SPF_F_NEXTHOPS).run()
+    assert q.kernel == "lds"
+    check_query(csr, q, sources, True)
+    qu = g.query(sources, abi.SPF_F_NEXTHOPS | abi.SPF_F_UNIT_METRIC).run()
+    check_query(csr, qu, sources, False)
+    qd = g.query(sources, 0).run()
+    check_query(csr, qd, sources, True)
+
+
+def test_ignore_lists(gpu_ready):
+    rng = random.Random(11)
+    V = 200
+    links = random_links(rng, V, 700)
+    csr = abi.Csr.from_links(V, links)
+    g = abi.Graph(csr)
+    sources = [rng.randrange(V) for _ in range(40)]
+    ignore = [rng.sample(range(len(links)), rng.randint(0, 30)) for _ in sources]
+    q = g.query(sources, abi.SPF_F_NEXTHOPS, ignore=ignore).run()
+    check_query(csr, q, sources, True, ignore)
+
+
+def test_high_degree_masks(gpu_ready):
+    # a hub with 300 neighbours -> 5 mask words (WMAX 16 kernel)
+    V = 400
+    links = [(0, v, 1, 1) for v in range(1, 301)]
+    links += [(v, 300 + (v % 99) + 1, 2, 3) for v in range(1, 301)]
+    csr = abi.Csr.from_links(V, links)
+    g = abi.Graph(csr)
+    q = g.query([0, 5, 350], abi.SPF_F_NEXTHOPS).run()
+    assert q.nh_words(0) == 5
+    check_query(csr, q, [0, 5, 350], True)
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_zero_metric_exact(gpu_ready, seed):
+    rng = random.Random(seed)
+    V = 150
+    links = random_links(rng, V, 500, wmin=0, wmax=5)
+    ov = [1 if rng.random() < 0.05 else 0 for _ in range(V)]
+    csr = abi.Csr.from_links(V, links, ov)
+    g = abi.Graph(csr)
+    assert g.needs_exact
+    sources = list(range(0, V, 5))
+    q = g.query(sources, abi.SPF_F_NEXTHOPS | abi.SPF_F_ORDER).run()
+    assert q.kernel == "exact"
+    check_query(csr, q, sources, True)
+    for i, s in enumerate(sources):
+        ref = spf_py.run_spf(csr, s, True)
+        order = q.order(i)
+        for v, (_, _, _, rank) in ref.items():
+            assert int(order[v]) == rank
+
+
+def test_zero_metric_triangle_name_order(gpu_ready):
+    # SURVEY §8(a) probe: all-zero triangle from "1": nh(2)={2}, nh(3)={2,3}
+    # with node ids = name ranks 0:"1", 1:"2", 2:"3"
+    csr = abi.Csr.from_links(3, [(0, 1, 0, 0), (0, 2, 0, 0), (1, 2, 0, 0)])
+    g = abi.Graph(csr)
+    q = g.query([0], abi.SPF_F_NEXTHOPS).run()
+    sets = q.nexthop_sets(0, 0)
+    assert sets[1] == frozenset({1})
+    assert sets[2] == frozenset({1, 2})
+
+
+def test_negative_metric_wraps(gpu_ready):
+    # an i32 metric of -5 is the uint64 2^64-5 (LinkStateMetric)
+    m = (1 << 64) - 5
+    csr = abi.Csr.from_links(4, [(0, 1, m, 1), (1, 2, 10, 10), (0, 2, 3, 3), (2, 3, 1, 1)])
+    g = abi.Graph(csr)
+    assert g.needs_exact
+    q = g.query([0, 1, 2, 3], abi.SPF_F_NEXTHOPS).run()
+    check_query(csr, q, [0, 1, 2, 3], True)
+
+
+def test_gmem_kernel_large_graph(gpu_ready):
+    rng = random.Random(21)
+    V = 70000
+    links = random_links(rng, V, 150000, wmin=1, wmax=50, parallel=0.0)
+    csr = abi.Csr.from_links(V, links)
+    g = abi.Graph(csr)
+    q = g.query([0, 12345], abi.SPF_F_NEXTHOPS).run()
+    assert q.kernel == "gmem"
+    check_query(csr, q, [0, 12345], True)
+
+
+def test_transit_update(gpu_ready):
+    rng = random.Random(8)
+    V = 120
+    links = random_links(rng, V, 400)
+    csr = abi.Csr.from_links(V, links)
+    g = abi.Graph(csr)
+    ov = np.zeros(V, dtype=np.uint8)
+    ov[rng.sample(range(V), 10)] = 1
+    g.set_transit(ov)
+    csr.overloaded = ov
+    q = g.query(list(range(V)), abi.SPF_F_NEXTHOPS).run()
+    check_query(csr, q, list(range(V)), True)

@@ -1,0 +1,954 @@
+// SpfSolver.cpp — RouteDb generation (reference: openr/decision/Decision.cpp
+// :47-1321) over the MI355X LinkState.
+//
+// The selection rules (announcer choice, drain filtering, ECMP across areas,
+// RFC 5286 LFA, next-hop expansion to links, MPLS actions, KSP2 label
+// stacks, BGP metric vectors) are restated rule for rule.  What differs is
+// how shortest paths are fetched: instead of one lazily computed string-keyed
+// SpfResult per source, buildRouteDb first asks each area's LinkState for all
+// the SPFs it is going to read (myNode, and with LFA every up neighbour; the
+// KSP2 second passes of every SR_MPLS prefix) as one device batch, then reads
+// distances / next-hop masks by node id (SpfView).
+
+#include "SpfSolver.h"
+
+#include <chrono>
+#include <list>
+
+#include "Util.h"
+
+namespace openr {
+
+using Metric = LinkStateMetric;
+namespace mvu = MetricVectorUtils;
+
+// ---------------------------------------------------------------- RouteDb
+
+thrift::UnicastRoute RibUnicastEntry::toThrift() const {
+  thrift::UnicastRoute r;
+  r.dest = prefix;
+  r.nextHops.assign(nexthops.begin(), nexthops.end());
+  r.doNotInstall = doNotInstall;
+  if (bestPrefixEntry.type == thrift::PrefixType::BGP) {
+    r.prefixType = thrift::PrefixType::BGP;
+    r.data = bestPrefixEntry.data;
+    r.bestNexthop = bestNexthop.value();
+  }
+  return r;
+}
+
+thrift::MplsRoute RibMplsEntry::toThrift() const {
+  thrift::MplsRoute r;
+  r.topLabel = label;
+  r.nextHops.assign(nexthops.begin(), nexthops.end());
+  return r;
+}
+
+thrift::RouteDatabase DecisionRouteDb::toThrift() const {
+  thrift::RouteDatabase db;
+  for (const auto& [_, e] : unicastEntries) {
+    db.unicastRoutes.push_back(e.toThrift());
+  }
+  for (const auto& [_, e] : mplsEntries) {
+    db.mplsRoutes.push_back(e.toThrift());
+  }
+  return db;
+}
+
+DecisionRouteUpdate getRouteDelta(const DecisionRouteDb& newDb, const DecisionRouteDb& oldDb) {
+  DecisionRouteUpdate delta;
+  for (const auto& [prefix, entry] : newDb.unicastEntries) {
+    auto it = oldDb.unicastEntries.find(prefix);
+    if (it == oldDb.unicastEntries.end() || !(it->second == entry)) {
+      delta.unicastRoutesToUpdate.push_back(entry);
+    }
+  }
+  for (const auto& [prefix, _] : oldDb.unicastEntries) {
+    if (!newDb.unicastEntries.count(prefix)) {
+      delta.unicastRoutesToDelete.push_back(prefix);
+    }
+  }
+  for (const auto& [label, entry] : newDb.mplsEntries) {
+    auto it = oldDb.mplsEntries.find(label);
+    if (it == oldDb.mplsEntries.end() || !(it->second == entry)) {
+      delta.mplsRoutesToUpdate.push_back(entry);
+    }
+  }
+  for (const auto& [label, _] : oldDb.mplsEntries) {
+    if (!newDb.mplsEntries.count(label)) {
+      delta.mplsRoutesToDelete.push_back(label);
+    }
+  }
+  return delta;
+}
+
+// ------------------------------------------------------------ SPF reads
+
+namespace {
+
+using AreaLinkStates = std::unordered_map<std::string, LinkState>;
+
+struct PairHash {
+  size_t operator()(const std::pair<std::string, std::string>& p) const {
+    return detail::mix(std::hash<std::string>()(p.first), std::hash<std::string>()(p.second));
+  }
+};
+using NextHopNodes = std::unordered_map<std::pair<std::string, std::string>, Metric, PairHash>;
+
+// Name-keyed reads of one SPF row (what the reference does with
+// SpfResult::find / at(...).metric() / nextHops()).
+class SpfRead {
+ public:
+  SpfRead(const LinkState& ls, const std::string& src, bool useLinkMetric = true)
+      : ls_(ls), src_(src), view_(ls.spfView(src, useLinkMetric)) {}
+
+  std::optional<Metric> metric(const std::string& node) const {
+    if (view_.src == ~0u) {
+      return node == src_ ? std::optional<Metric>(0) : std::nullopt;
+    }
+    auto id = ls_.nodeId(node);
+    if (!id || !view_.reached(*id)) {
+      return std::nullopt;
+    }
+    return view_.dist[*id];
+  }
+
+  template <class Fn>
+  void forEachNextHop(const std::string& node, Fn&& fn) const {
+    if (view_.src == ~0u) {
+      return;
+    }
+    auto id = ls_.nodeId(node);
+    if (!id || !view_.reached(*id)) {
+      return;
+    }
+    view_.forEachNextHop(*id, [&](uint32_t h) { fn(ls_.nodeNameOf(h)); });
+  }
+
+ private:
+  const LinkState& ls_;
+  const std::string& src_;
+  const SpfView& view_;
+};
+
+} // namespace
+
+// ------------------------------------------------------------------- impl
+
+class SpfSolver::SpfSolverImpl {
+ public:
+  SpfSolverImpl(
+      const std::string& myNodeName,
+      bool enableV4,
+      bool computeLfaPaths,
+      bool enableOrderedFib,
+      bool bgpDryRun,
+      bool bgpUseIgpMetric)
+      : myNodeName_(myNodeName),
+        enableV4_(enableV4),
+        computeLfaPaths_(computeLfaPaths),
+        enableOrderedFib_(enableOrderedFib),
+        bgpDryRun_(bgpDryRun),
+        bgpUseIgpMetric_(bgpUseIgpMetric) {}
+
+  bool staticRoutesUpdated() const { return !staticRoutesUpdates_.empty(); }
+  void pushRoutesDeltaUpdates(thrift::RouteDatabaseDelta& d) {
+    staticRoutesUpdates_.push_back(std::move(d));
+  }
+  std::optional<DecisionRouteUpdate> processStaticRouteUpdates();
+  thrift::StaticRoutes const& getStaticRoutes() const { return staticRoutes_; }
+
+  std::optional<DecisionRouteDb> buildRouteDb(
+      const std::string& myNodeName,
+      AreaLinkStates const& areaLinkStates,
+      PrefixState const& prefixState);
+
+ private:
+  void prefetch(
+      const std::string& myNodeName,
+      AreaLinkStates const& areaLinkStates,
+      PrefixState const& prefixState) const;
+
+  BestPathCalResult getBestAnnouncingNodes(
+      const std::string& myNodeName,
+      const thrift::IpPrefix& prefix,
+      const thrift::PrefixEntries& prefixEntries,
+      bool hasBgp,
+      bool useKsp2EdAlgo,
+      AreaLinkStates const& areaLinkStates);
+
+  BestPathCalResult runBestPathSelectionBgp(
+      const std::string& myNodeName,
+      const thrift::IpPrefix& prefix,
+      const thrift::PrefixEntries& prefixEntries,
+      AreaLinkStates const& areaLinkStates);
+
+  BestPathCalResult maybeFilterDrainedNodes(
+      BestPathCalResult&& result, AreaLinkStates const& areaLinkStates) const;
+
+  std::optional<int64_t> getMinNextHopThreshold(
+      const BestPathCalResult& nodes, const thrift::PrefixEntries& prefixEntries) const;
+
+  void selectEcmpOpenr(
+      std::unordered_map<thrift::IpPrefix, RibUnicastEntry>& unicastEntries,
+      const std::string& myNodeName,
+      const thrift::IpPrefix& prefix,
+      const thrift::PrefixEntries& prefixEntries,
+      bool isV4,
+      AreaLinkStates const& areaLinkStates);
+
+  void selectEcmpBgp(
+      std::unordered_map<thrift::IpPrefix, RibUnicastEntry>& unicastEntries,
+      const std::string& myNodeName,
+      const thrift::IpPrefix& prefix,
+      const thrift::PrefixEntries& prefixEntries,
+      bool isV4,
+      AreaLinkStates const& areaLinkStates,
+      PrefixState const& prefixState);
+
+  void selectKsp2(
+      std::unordered_map<thrift::IpPrefix, RibUnicastEntry>& unicastEntries,
+      const thrift::IpPrefix& prefix,
+      const std::string& myNodeName,
+      const BestPathCalResult& best,
+      const thrift::PrefixEntries& prefixEntries,
+      bool hasBgp,
+      AreaLinkStates const& areaLinkStates,
+      PrefixState const& prefixState,
+      thrift::PrefixForwardingAlgorithm algo);
+
+  std::pair<Metric, NextHopNodes> getNextHopsWithMetric(
+      const std::string& myNodeName,
+      const std::set<std::string>& dstNodeNames,
+      bool perDestination,
+      AreaLinkStates const& areaLinkStates);
+
+  std::unordered_set<thrift::NextHopThrift> getNextHopsThrift(
+      const std::string& myNodeName,
+      const std::set<std::string>& dstNodeNames,
+      bool isV4,
+      bool perDestination,
+      Metric minMetric,
+      const NextHopNodes& nextHopNodes,
+      std::optional<int32_t> swapLabel,
+      AreaLinkStates const& areaLinkStates,
+      const std::set<std::string>& prefixAreas) const;
+
+  thrift::StaticRoutes staticRoutes_;
+  std::vector<thrift::RouteDatabaseDelta> staticRoutesUpdates_;
+  const std::string myNodeName_;
+  const bool enableV4_;
+  const bool computeLfaPaths_;
+  const bool enableOrderedFib_;
+  const bool bgpDryRun_;
+  const bool bgpUseIgpMetric_;
+};
+
+std::optional<DecisionRouteUpdate> SpfSolver::SpfSolverImpl::processStaticRouteUpdates() {
+  std::unordered_map<int32_t, thrift::MplsRoute> toUpdate;
+  std::unordered_set<int32_t> toDelete;
+  for (const auto& delta : staticRoutesUpdates_) {
+    for (const auto& r : delta.mplsRoutesToUpdate) {
+      toUpdate[r.topLabel] = r;
+      toDelete.erase(r.topLabel);
+    }
+    for (const auto label : delta.mplsRoutesToDelete) {
+      toDelete.insert(label);
+      toUpdate.erase(label);
+    }
+  }
+  staticRoutesUpdates_.clear();
+  if (toUpdate.empty() && toDelete.empty()) {
+    return std::nullopt;
+  }
+  DecisionRouteUpdate ret;
+  for (const auto& [label, route] : toUpdate) {
+    staticRoutes_.mplsRoutes[label] = route.nextHops;
+    ret.mplsRoutesToUpdate.push_back(RibMplsEntry::fromThrift(route));
+  }
+  for (const auto label : toDelete) {
+    staticRoutes_.mplsRoutes.erase(label);
+    ret.mplsRoutesToDelete.push_back(label);
+  }
+  return ret;
+}
+
+// Ask every area for the SPF rows this build will read, one batch per area.
+void SpfSolver::SpfSolverImpl::prefetch(
+    const std::string& myNodeName,
+    AreaLinkStates const& areaLinkStates,
+    PrefixState const& prefixState) const {
+  std::vector<std::string> ksp2Dests;
+  bool anyPrefix = false;
+  for (const auto& [prefix, entries] : prefixState.prefixes()) {
+    anyPrefix = true;
+    if (getPrefixForwardingType(entries) == thrift::PrefixForwardingType::SR_MPLS &&
+        getPrefixForwardingAlgorithm(entries) ==
+            thrift::PrefixForwardingAlgorithm::KSP2_ED_ECMP) {
+      for (const auto& [node, _] : entries) {
+        if (node != myNodeName) {
+          ksp2Dests.push_back(node);
+        }
+      }
+    }
+  }
+  std::sort(ksp2Dests.begin(), ksp2Dests.end());
+  ksp2Dests.erase(std::unique(ksp2Dests.begin(), ksp2Dests.end()), ksp2Dests.end());
+  for (const auto& [area, ls] : areaLinkStates) {
+    std::vector<std::string> sources{myNodeName};
+    if (computeLfaPaths_ && anyPrefix) {
+      for (const auto& link : ls.linksFromNode(myNodeName)) {
+        if (link->isUp()) {
+          sources.push_back(link->getOtherNodeName(myNodeName));
+        }
+      }
+    }
+    ls.prefetchSpf(sources, true);
+    if (!ksp2Dests.empty()) {
+      ls.prefetchKthPaths(myNodeName, ksp2Dests);
+    }
+  }
+}
+
+std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
+    const std::string& myNodeName,
+    AreaLinkStates const& areaLinkStates,
+    PrefixState const& prefixState) {
+  bool known = false;
+  for (const auto& [_, ls] : areaLinkStates) {
+    known |= ls.hasNode(myNodeName);
+  }
+  if (!known) {
+    return std::nullopt;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  Counters::add("decision.route_build_runs", 1);
+  prefetch(myNodeName, areaLinkStates, prefixState);
+
+  DecisionRouteDb routeDb;
+
+  // unicast routes: IP and IP->MPLS
+  for (const auto& [prefix, prefixEntries] : prefixState.prefixes()) {
+    bool hasBGP = false, hasNonBGP = false, missingMv = false;
+    for (const auto& [node, byArea] : prefixEntries) {
+      for (const auto& [area, entry] : byArea) {
+        const bool isBGP = entry.type == thrift::PrefixType::BGP;
+        hasBGP |= isBGP;
+        hasNonBGP |= !isBGP;
+        missingMv |= isBGP && !entry.mv.has_value();
+      }
+    }
+    if (hasBGP && (hasNonBGP || missingMv)) {
+      Counters::add("decision.skipped_unicast_route", 1);
+      continue;
+    }
+    if (prefixEntries.count(myNodeName) && !hasBGP) {
+      continue; // we advertise it ourselves
+    }
+    const bool isV4Prefix = prefix.prefixAddress.addr.size() == 4;
+    if (isV4Prefix && !enableV4_) {
+      Counters::add("decision.skipped_unicast_route", 1);
+      continue;
+    }
+    const auto algo = getPrefixForwardingAlgorithm(prefixEntries);
+    const auto type = getPrefixForwardingType(prefixEntries);
+    if (type == thrift::PrefixForwardingType::SR_MPLS) {
+      const auto nodes = getBestAnnouncingNodes(
+          myNodeName, prefix, prefixEntries, hasBGP, true, areaLinkStates);
+      if (!nodes.success || nodes.nodes.empty()) {
+        continue;
+      }
+      selectKsp2(
+          routeDb.unicastEntries, prefix, myNodeName, nodes, prefixEntries, hasBGP,
+          areaLinkStates, prefixState, algo);
+    } else if (algo == thrift::PrefixForwardingAlgorithm::SP_ECMP) {
+      if (hasBGP) {
+        selectEcmpBgp(
+            routeDb.unicastEntries, myNodeName, prefix, prefixEntries, isV4Prefix,
+            areaLinkStates, prefixState);
+      } else {
+        selectEcmpOpenr(
+            routeDb.unicastEntries, myNodeName, prefix, prefixEntries, isV4Prefix,
+            areaLinkStates);
+      }
+    } else {
+      // KSP2 is not supported for plain IP routing
+      Counters::add("decision.incompatible_forwarding_type", 1);
+    }
+  }
+
+  // node-label MPLS routes: on a label collision the smaller node name wins
+  std::unordered_map<int32_t, std::pair<std::string, RibMplsEntry>> labelToNode;
+  for (const auto& [area, ls] : areaLinkStates) {
+    for (const auto& [_, adjDb] : ls.getAdjacencyDatabases()) {
+      const int32_t topLabel = adjDb.nodeLabel;
+      if (topLabel == 0) {
+        continue; // not SR
+      }
+      if (!isMplsLabelValid(topLabel)) {
+        Counters::add("decision.skipped_mpls_route", 1);
+        continue;
+      }
+      auto it = labelToNode.find(topLabel);
+      if (it != labelToNode.end()) {
+        Counters::add("decision.duplicate_node_label", 1);
+        if (it->second.first < adjDb.thisNodeName) {
+          continue;
+        }
+      }
+      if (adjDb.thisNodeName == myNodeName) {
+        thrift::NextHopThrift nh;
+        nh.address.addr = std::string(16, '\0'); // "::"
+        nh.area = area;
+        nh.mplsAction = createMplsAction(thrift::MplsActionCode::POP_AND_LOOKUP);
+        labelToNode.erase(topLabel);
+        labelToNode.emplace(
+            topLabel, std::make_pair(adjDb.thisNodeName, RibMplsEntry(topLabel, {nh})));
+        continue;
+      }
+      const auto metricNhs =
+          getNextHopsWithMetric(myNodeName, {adjDb.thisNodeName}, false, areaLinkStates);
+      if (metricNhs.second.empty()) {
+        Counters::add("decision.no_route_to_label", 1);
+        continue;
+      }
+      labelToNode.erase(topLabel);
+      labelToNode.emplace(
+          topLabel,
+          std::make_pair(
+              adjDb.thisNodeName,
+              RibMplsEntry(
+                  topLabel,
+                  getNextHopsThrift(
+                      myNodeName, {adjDb.thisNodeName}, false, false, metricNhs.first,
+                      metricNhs.second, topLabel, areaLinkStates, {area}))));
+    }
+  }
+  for (auto& [label, nodeAndEntry] : labelToNode) {
+    routeDb.mplsEntries.emplace(label, std::move(nodeAndEntry.second));
+  }
+
+  // adjacency-label PHP routes of our own links
+  for (const auto& [_, ls] : areaLinkStates) {
+    for (const auto& link : ls.linksFromNode(myNodeName)) {
+      const int32_t topLabel = link->getAdjLabelFromNode(myNodeName);
+      if (topLabel == 0) {
+        continue;
+      }
+      if (!isMplsLabelValid(topLabel)) {
+        Counters::add("decision.skipped_mpls_route", 1);
+        continue;
+      }
+      routeDb.mplsEntries.emplace(
+          topLabel,
+          RibMplsEntry(
+              topLabel,
+              {createNextHop(
+                  link->getNhV6FromNode(myNodeName), link->getIfaceFromNode(myNodeName),
+                  (int32_t)link->getMetricFromNode(myNodeName),
+                  createMplsAction(thrift::MplsActionCode::PHP), false, link->getArea())}));
+    }
+  }
+
+  Counters::add(
+      "decision.route_build_us",
+      std::chrono::duration_cast<std::chrono::microseconds>(
+          std::chrono::steady_clock::now() - t0)
+          .count());
+  return routeDb;
+}
+
+BestPathCalResult SpfSolver::SpfSolverImpl::getBestAnnouncingNodes(
+    const std::string& myNodeName,
+    const thrift::IpPrefix& prefix,
+    const thrift::PrefixEntries& prefixEntries,
+    bool hasBgp,
+    bool useKsp2EdAlgo,
+    AreaLinkStates const& areaLinkStates) {
+  BestPathCalResult ret;
+  if (!hasBgp) {
+    // every reachable announcer is a best node; the smallest name is "best"
+    if (prefixEntries.count(myNodeName)) {
+      return BestPathCalResult{};
+    }
+    for (const auto& [node, byArea] : prefixEntries) {
+      for (const auto& [area, entry] : byArea) {
+        SpfRead mine(areaLinkStates.at(area), myNodeName);
+        if (!mine.metric(node)) {
+          continue; // unreachable announcer
+        }
+        if (ret.bestNode.empty() || node < ret.bestNode) {
+          ret.bestNode = node;
+          ret.bestArea = area;
+        }
+        ret.nodes.insert(node);
+        ret.areas.insert(area);
+      }
+    }
+    ret.success = true;
+    return maybeFilterDrainedNodes(std::move(ret), areaLinkStates);
+  }
+
+  ret = runBestPathSelectionBgp(myNodeName, prefix, prefixEntries, areaLinkStates);
+  if (!ret.success) {
+    Counters::add("decision.no_route_to_prefix", 1);
+    return BestPathCalResult{};
+  }
+  if (!useKsp2EdAlgo) {
+    if (ret.nodes.count(myNodeName)) {
+      return BestPathCalResult{}; // best path originated by ourselves
+    }
+    return maybeFilterDrainedNodes(std::move(ret), areaLinkStates);
+  }
+  // KSP2: program our own prefix only when others announce it too and we
+  // carry a prepend label
+  bool myLabel = false;
+  auto mine = prefixEntries.find(myNodeName);
+  if (mine != prefixEntries.end()) {
+    for (const auto& [_, entry] : mine->second) {
+      myLabel |= entry.prependLabel.has_value();
+    }
+  }
+  if (!ret.nodes.count(myNodeName) || (ret.nodes.size() > 1 && myLabel)) {
+    return maybeFilterDrainedNodes(std::move(ret), areaLinkStates);
+  }
+  return BestPathCalResult{};
+}
+
+BestPathCalResult SpfSolver::SpfSolverImpl::runBestPathSelectionBgp(
+    const std::string& myNodeName,
+    const thrift::IpPrefix& /* prefix */,
+    const thrift::PrefixEntries& prefixEntries,
+    AreaLinkStates const& areaLinkStates) {
+  BestPathCalResult ret;
+  for (const auto& [nodeName, byArea] : prefixEntries) {
+    for (const auto& [area, entry] : byArea) {
+      SpfRead mine(areaLinkStates.at(area), myNodeName);
+      const auto igp = mine.metric(nodeName);
+      if (!igp) {
+        continue;
+      }
+      const thrift::MetricVector& mvIn = entry.mv.value();
+      if (mvu::getMetricEntityByType(mvIn, mvu::kOpenrIgpCostType)) {
+        continue; // OPENR_IGP_COST must not be advertised
+      }
+      thrift::MetricVector metricVector = mvIn;
+      if (bgpUseIgpMetric_) {
+        const int64_t igpMetric = (int64_t)*igp;
+        if (!ret.bestIgpMetric || *ret.bestIgpMetric > igpMetric) {
+          ret.bestIgpMetric = igpMetric;
+        }
+        metricVector.metrics.push_back(mvu::createMetricEntity(
+            mvu::kOpenrIgpCostType, mvu::kOpenrIgpCostPriority,
+            thrift::CompareType::WIN_IF_NOT_PRESENT, false, {-1 * igpMetric}));
+      }
+      mvu::CompareResult cmp = mvu::CompareResult::WINNER;
+      if (ret.bestVector) {
+        cmp = mvu::compareMetricVectors(metricVector, *ret.bestVector);
+      }
+      switch (cmp) {
+      case mvu::CompareResult::WINNER:
+        ret.nodes.clear();
+        [[fallthrough]];
+      case mvu::CompareResult::TIE_WINNER:
+        ret.bestVector = std::move(metricVector);
+        ret.bestNode = nodeName;
+        ret.bestArea = area;
+        [[fallthrough]];
+      case mvu::CompareResult::TIE_LOOSER:
+        ret.nodes.insert(nodeName);
+        ret.areas.insert(area);
+        break;
+      case mvu::CompareResult::TIE:
+      case mvu::CompareResult::ERROR:
+        return ret; // cannot order: no route (success stays false)
+      default:
+        break;
+      }
+    }
+  }
+  ret.success = true;
+  return maybeFilterDrainedNodes(std::move(ret), areaLinkStates);
+}
+
+BestPathCalResult SpfSolver::SpfSolverImpl::maybeFilterDrainedNodes(
+    BestPathCalResult&& result, AreaLinkStates const& areaLinkStates) const {
+  BestPathCalResult filtered = result;
+  for (const auto& [_, ls] : areaLinkStates) {
+    for (auto it = filtered.nodes.begin(); it != filtered.nodes.end();) {
+      it = ls.isNodeOverloaded(*it) ? filtered.nodes.erase(it) : std::next(it);
+    }
+  }
+  // drained announcers are used only when every announcer is drained
+  return filtered.nodes.empty() ? result : filtered;
+}
+
+std::optional<int64_t> SpfSolver::SpfSolverImpl::getMinNextHopThreshold(
+    const BestPathCalResult& nodes, const thrift::PrefixEntries& prefixEntries) const {
+  std::optional<int64_t> threshold;
+  for (const auto& node : nodes.nodes) {
+    auto it = prefixEntries.find(node);
+    if (it == prefixEntries.end()) {
+      continue;
+    }
+    for (const auto& [_, entry] : it->second) {
+      if (entry.minNexthop && (!threshold || *entry.minNexthop > *threshold)) {
+        threshold = entry.minNexthop;
+      }
+    }
+  }
+  return threshold;
+}
+
+void SpfSolver::SpfSolverImpl::selectEcmpOpenr(
+    std::unordered_map<thrift::IpPrefix, RibUnicastEntry>& unicastEntries,
+    const std::string& myNodeName,
+    const thrift::IpPrefix& prefix,
+    const thrift::PrefixEntries& prefixEntries,
+    bool isV4,
+    AreaLinkStates const& areaLinkStates) {
+  const auto ret =
+      getBestAnnouncingNodes(myNodeName, prefix, prefixEntries, false, false, areaLinkStates);
+  if (!ret.success) {
+    return;
+  }
+  const bool perDestination =
+      getPrefixForwardingType(prefixEntries) == thrift::PrefixForwardingType::SR_MPLS;
+  const auto metricNhs =
+      getNextHopsWithMetric(myNodeName, ret.nodes, perDestination, areaLinkStates);
+  if (metricNhs.second.empty()) {
+    Counters::add("decision.no_route_to_prefix", 1);
+    return;
+  }
+  RibUnicastEntry entry(
+      prefix,
+      getNextHopsThrift(
+          myNodeName, ret.nodes, isV4, perDestination, metricNhs.first, metricNhs.second,
+          std::nullopt, areaLinkStates, ret.areas),
+      prefixEntries.at(ret.bestNode).at(ret.bestArea),
+      ret.bestArea);
+  unicastEntries.emplace(prefix, std::move(entry));
+}
+
+void SpfSolver::SpfSolverImpl::selectEcmpBgp(
+    std::unordered_map<thrift::IpPrefix, RibUnicastEntry>& unicastEntries,
+    const std::string& myNodeName,
+    const thrift::IpPrefix& prefix,
+    const thrift::PrefixEntries& prefixEntries,
+    bool isV4,
+    AreaLinkStates const& areaLinkStates,
+    PrefixState const& prefixState) {
+  const auto dst =
+      getBestAnnouncingNodes(myNodeName, prefix, prefixEntries, true, false, areaLinkStates);
+  if (!dst.success) {
+    return;
+  }
+  if (dst.nodes.empty() || dst.nodes.count(myNodeName)) {
+    if (!dst.nodes.count(myNodeName)) {
+      Counters::add("decision.no_route_to_prefix", 1);
+    }
+    return;
+  }
+  auto bestNextHop = prefixState.getLoopbackVias({dst.bestNode}, isV4, dst.bestIgpMetric);
+  if (bestNextHop.size() != 1) {
+    Counters::add("decision.missing_loopback_addr", 1);
+    return;
+  }
+  const auto nhs = getNextHopsWithMetric(myNodeName, dst.nodes, false, areaLinkStates);
+  RibUnicastEntry entry(
+      prefix,
+      getNextHopsThrift(
+          myNodeName, dst.nodes, isV4, false, nhs.first, nhs.second, std::nullopt,
+          areaLinkStates, dst.areas),
+      prefixEntries.at(dst.bestNode).at(dst.bestArea),
+      dst.bestArea,
+      bgpDryRun_,
+      bestNextHop.at(0));
+  unicastEntries.emplace(prefix, std::move(entry));
+}
+
+void SpfSolver::SpfSolverImpl::selectKsp2(
+    std::unordered_map<thrift::IpPrefix, RibUnicastEntry>& unicastEntries,
+    const thrift::IpPrefix& prefix,
+    const std::string& myNodeName,
+    const BestPathCalResult& best,
+    const thrift::PrefixEntries& prefixEntries,
+    bool hasBgp,
+    AreaLinkStates const& areaLinkStates,
+    PrefixState const& prefixState,
+    thrift::PrefixForwardingAlgorithm algo) {
+  RibUnicastEntry entry(prefix);
+  bool selfNodeContained = false;
+  std::vector<LinkState::Path> paths;
+
+  for (const auto& [_, ls] : areaLinkStates) {
+    for (const auto& node : best.nodes) {
+      if (node == myNodeName) {
+        selfNodeContained = true;
+        continue;
+      }
+      for (const auto& path : ls.getKthPaths(myNodeName, node, 1)) {
+        paths.push_back(path);
+      }
+    }
+    if (algo == thrift::PrefixForwardingAlgorithm::KSP2_ED_ECMP) {
+      // drop second paths that contain a first path (anycast double spray)
+      const size_t firstPaths = paths.size();
+      for (const auto& node : best.nodes) {
+        for (const auto& secPath : ls.getKthPaths(myNodeName, node, 2)) {
+          bool contained = false;
+          for (size_t i = 0; i < firstPaths && !contained; ++i) {
+            contained = LinkState::pathAInPathB(paths[i], secPath);
+          }
+          if (!contained) {
+            paths.push_back(secPath);
+          }
+        }
+      }
+    }
+  }
+  if (paths.empty()) {
+    return;
+  }
+
+  const bool isV4Prefix = prefix.prefixAddress.addr.size() == 4;
+  for (const auto& path : paths) {
+    for (const auto& [area, ls] : areaLinkStates) {
+      Metric cost = 0;
+      std::list<int32_t> labels;
+      std::string nextNode = myNodeName;
+      for (const auto& link : path) {
+        cost += link->getMetricFromNode(nextNode);
+        nextNode = link->getOtherNodeName(nextNode);
+        labels.push_front(ls.getAdjacencyDatabases().at(nextNode).nodeLabel);
+      }
+      labels.pop_back(); // PHP: the first hop's label is not pushed
+      const auto& destEntry = prefixEntries.at(nextNode).at(area);
+      if (destEntry.prependLabel) {
+        labels.push_front(*destEntry.prependLabel); // bottom of stack
+      }
+      if (path.empty()) {
+        throw std::logic_error("selectKsp2: empty path");
+      }
+      const auto& firstLink = path.front();
+      std::optional<thrift::MplsAction> action;
+      if (!labels.empty()) {
+        action = createMplsAction(
+            thrift::MplsActionCode::PUSH, std::nullopt,
+            std::vector<int32_t>(labels.begin(), labels.end()));
+      }
+      entry.nexthops.insert(createNextHop(
+          isV4Prefix ? firstLink->getNhV4FromNode(myNodeName)
+                     : firstLink->getNhV6FromNode(myNodeName),
+          firstLink->getIfaceFromNode(myNodeName), (int32_t)cost, action, true,
+          firstLink->getArea()));
+    }
+  }
+
+  int staticNexthops = 0;
+  if (selfNodeContained) {
+    const auto& mine = prefixEntries.at(myNodeName);
+    if (mine.size() != 1) {
+      throw std::logic_error("selectKsp2: MPLS can only be originated to one area");
+    }
+    const int32_t label = mine.begin()->second.prependLabel.value();
+    auto it = staticRoutes_.mplsRoutes.find(label);
+    if (it != staticRoutes_.mplsRoutes.end()) {
+      for (const auto& nh : it->second) {
+        ++staticNexthops;
+        entry.nexthops.insert(
+            createNextHop(nh.address, std::nullopt, 0, std::nullopt, true, mine.begin()->first));
+      }
+    }
+  }
+
+  const auto minNextHop = getMinNextHopThreshold(best, prefixEntries);
+  const int64_t dynamicNextHops = (int64_t)entry.nexthops.size() - staticNexthops;
+  if (minNextHop && *minNextHop > dynamicNextHops) {
+    return; // not enough next hops for this prefix
+  }
+  if (hasBgp) {
+    auto bestNextHop = prefixState.getLoopbackVias(
+        {best.bestNode}, prefix.prefixAddress.addr.size() == 4, best.bestIgpMetric);
+    if (bestNextHop.size() == 1) {
+      entry.bestNexthop = bestNextHop.at(0);
+      entry.bestPrefixEntry = prefixEntries.at(best.bestNode).at(best.bestArea);
+      entry.doNotInstall = bgpDryRun_;
+    }
+  }
+  unicastEntries.emplace(prefix, std::move(entry));
+}
+
+std::pair<Metric, NextHopNodes> SpfSolver::SpfSolverImpl::getNextHopsWithMetric(
+    const std::string& myNodeName,
+    const std::set<std::string>& dstNodeNames,
+    bool perDestination,
+    AreaLinkStates const& areaLinkStates) {
+  NextHopNodes nextHopNodes;
+  Metric shortestMetric = std::numeric_limits<Metric>::max();
+
+  for (const auto& [_, ls] : areaLinkStates) {
+    SpfRead mine(ls, myNodeName);
+    // closest announcers in this area
+    Metric areaMin = std::numeric_limits<Metric>::max();
+    std::vector<const std::string*> minCostNodes;
+    for (const auto& dst : dstNodeNames) {
+      const auto d = mine.metric(dst);
+      if (!d) {
+        continue;
+      }
+      if (areaMin >= *d) {
+        if (areaMin > *d) {
+          areaMin = *d;
+          minCostNodes.clear();
+        }
+        minCostNodes.push_back(&dst);
+      }
+    }
+    if (shortestMetric < areaMin) {
+      continue;
+    }
+    if (shortestMetric > areaMin) {
+      shortestMetric = areaMin;
+      nextHopNodes.clear();
+    }
+    if (minCostNodes.empty()) {
+      continue;
+    }
+    for (const std::string* dst : minCostNodes) {
+      const std::string dstRef = perDestination ? *dst : std::string();
+      mine.forEachNextHop(*dst, [&](const std::string& nh) {
+        nextHopNodes[std::make_pair(nh, dstRef)] =
+            shortestMetric - ls.getMetricFromAToB(myNodeName, nh).value();
+      });
+    }
+    if (computeLfaPaths_) {
+      // RFC 5286 loop-free alternates through every up neighbour
+      for (const auto& link : ls.linksFromNode(myNodeName)) {
+        if (!link->isUp()) {
+          continue;
+        }
+        const std::string& nbr = link->getOtherNodeName(myNodeName);
+        SpfRead fromNbr(ls, nbr);
+        const auto nbrToHere = fromNbr.metric(myNodeName);
+        if (!nbrToHere) {
+          throw std::out_of_range("LFA: neighbour cannot reach " + myNodeName);
+        }
+        for (const auto& dst : dstNodeNames) {
+          const auto dNbr = fromNbr.metric(dst);
+          if (!dNbr) {
+            continue;
+          }
+          if (*dNbr < shortestMetric + *nbrToHere) {
+            auto key = std::make_pair(nbr, perDestination ? dst : std::string());
+            auto it = nextHopNodes.find(key);
+            if (it == nextHopNodes.end()) {
+              nextHopNodes.emplace(std::move(key), *dNbr);
+            } else if (it->second > *dNbr) {
+              it->second = *dNbr;
+            }
+          }
+        }
+      }
+    }
+  }
+  return {shortestMetric, std::move(nextHopNodes)};
+}
+
+std::unordered_set<thrift::NextHopThrift> SpfSolver::SpfSolverImpl::getNextHopsThrift(
+    const std::string& myNodeName,
+    const std::set<std::string>& dstNodeNames,
+    bool isV4,
+    bool perDestination,
+    Metric minMetric,
+    const NextHopNodes& nextHopNodes,
+    std::optional<int32_t> swapLabel,
+    AreaLinkStates const& areaLinkStates,
+    const std::set<std::string>& prefixAreas) const {
+  if (nextHopNodes.empty()) {
+    throw std::logic_error("getNextHopsThrift: no next-hop nodes");
+  }
+  static const std::set<std::string> kNoDest{std::string()};
+  std::unordered_set<thrift::NextHopThrift> nextHops;
+  for (const auto& [area, ls] : areaLinkStates) {
+    if (!prefixAreas.count(area)) {
+      continue;
+    }
+    for (const auto& link : ls.linksFromNode(myNodeName)) {
+      for (const auto& dstNode : perDestination ? dstNodeNames : kNoDest) {
+        const std::string& nbr = link->getOtherNodeName(myNodeName);
+        auto search = nextHopNodes.find(std::make_pair(nbr, dstNode));
+        if (search == nextHopNodes.end() || !link->isUp()) {
+          continue;
+        }
+        // do not reach dstNode through another destination
+        if (!dstNode.empty() && dstNodeNames.count(nbr) && nbr != dstNode) {
+          continue;
+        }
+        const Metric distOverLink = link->getMetricFromNode(myNodeName) + search->second;
+        if (!computeLfaPaths_ && distOverLink != minMetric) {
+          continue; // only shortest paths without LFA
+        }
+        std::optional<thrift::MplsAction> action;
+        if (swapLabel) {
+          const bool nbrIsDst = dstNodeNames.count(nbr) > 0;
+          action = createMplsAction(
+              nbrIsDst ? thrift::MplsActionCode::PHP : thrift::MplsActionCode::SWAP,
+              nbrIsDst ? std::nullopt : swapLabel);
+        }
+        if (!dstNode.empty() && dstNode != nbr) {
+          const int32_t dstLabel = ls.getAdjacencyDatabases().at(dstNode).nodeLabel;
+          if (!isMplsLabelValid(dstLabel)) {
+            continue;
+          }
+          if (action) {
+            throw std::logic_error("getNextHopsThrift: conflicting MPLS actions");
+          }
+          action = createMplsAction(
+              thrift::MplsActionCode::PUSH, std::nullopt, std::vector<int32_t>{dstLabel});
+        }
+        nextHops.insert(createNextHop(
+            isV4 ? link->getNhV4FromNode(myNodeName) : link->getNhV6FromNode(myNodeName),
+            link->getIfaceFromNode(myNodeName), (int32_t)distOverLink, action, false,
+            link->getArea()));
+      }
+    }
+  }
+  return nextHops;
+}
+
+// ------------------------------------------------------------- SpfSolver
+
+SpfSolver::SpfSolver(
+    const std::string& myNodeName,
+    bool enableV4,
+    bool computeLfaPaths,
+    bool enableOrderedFib,
+    bool bgpDryRun,
+    bool bgpUseIgpMetric)
+    : impl_(std::make_unique<SpfSolverImpl>(
+          myNodeName, enableV4, computeLfaPaths, enableOrderedFib, bgpDryRun,
+          bgpUseIgpMetric)) {}
+
+SpfSolver::~SpfSolver() = default;
+
+bool SpfSolver::staticRoutesUpdated() { return impl_->staticRoutesUpdated(); }
+
+void SpfSolver::pushRoutesDeltaUpdates(thrift::RouteDatabaseDelta& d) {
+  impl_->pushRoutesDeltaUpdates(d);
+}
+
+std::optional<DecisionRouteUpdate> SpfSolver::processStaticRouteUpdates() {
+  return impl_->processStaticRouteUpdates();
+}
+
+thrift::StaticRoutes const& SpfSolver::getStaticRoutes() { return impl_->getStaticRoutes(); }
+
+std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
+    const std::string& myNodeName,
+    std::unordered_map<std::string, LinkState> const& areaLinkStates,
+    PrefixState const& prefixState) {
+  return impl_->buildRouteDb(myNodeName, areaLinkStates, prefixState);
+}
+
+} // namespace openr

@@ -1,0 +1,313 @@
+"""Python mirror of the thrift structs on the Decision SPF path plus the
+openr/common/Util helpers the reference tests build fixtures with
+(createAdjacency, createAdjDb, createPrefixEntry, createNextHop, ...).
+
+Field names, defaults and enum values follow openr/if/{Lsdb,Network,
+OpenrConfig}.thrift so the parity tests read like DecisionTest.cpp /
+LinkStateTest.cpp.  Both the product module (openr_amd._openr_spf) and the
+oracle read these objects by attribute.
+"""
+
+from __future__ import annotations
+
+import ipaddress
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+# enums (openr/if/Network.thrift, OpenrConfig.thrift, Lsdb.thrift)
+class PrefixType:
+    LOOPBACK = 1
+    DEFAULT = 2
+    BGP = 3
+    PREFIX_ALLOCATOR = 4
+    BREEZE = 5
+    RIB = 6
+
+
+class PrefixForwardingType:
+    IP = 0
+    SR_MPLS = 1
+
+
+class PrefixForwardingAlgorithm:
+    SP_ECMP = 0
+    KSP2_ED_ECMP = 1
+
+
+class MplsActionCode:
+    PUSH = 0
+    SWAP = 1
+    PHP = 2
+    POP_AND_LOOKUP = 3
+    NOOP = 4
+
+
+class CompareType:
+    WIN_IF_PRESENT = 1
+    WIN_IF_NOT_PRESENT = 2
+    IGNORE_IF_NOT_PRESENT = 3
+
+
+kDefaultArea = "0"
+
+
+@dataclass
+class BinaryAddress:
+    addr: bytes = b""
+    ifName: Optional[str] = None
+
+    def key(self):
+        return (self.addr, self.ifName)
+
+
+@dataclass
+class IpPrefix:
+    prefixAddress: BinaryAddress = field(default_factory=BinaryAddress)
+    prefixLength: int = 0
+
+    def key(self):
+        return (self.prefixAddress.addr, self.prefixLength)
+
+
+@dataclass
+class MplsAction:
+    action: int = MplsActionCode.PUSH
+    swapLabel: Optional[int] = None
+    pushLabels: Optional[List[int]] = None
+
+    def key(self):
+        return (
+            self.action,
+            self.swapLabel,
+            None if self.pushLabels is None else tuple(self.pushLabels),
+        )
+
+
+@dataclass
+class NextHopThrift:
+    address: BinaryAddress = field(default_factory=BinaryAddress)
+    weight: int = 0
+    mplsAction: Optional[MplsAction] = None
+    metric: int = 0
+    useNonShortestRoute: bool = False
+    area: Optional[str] = None
+
+    def key(self):
+        """Canonical hashable form; the C++ modules return the same tuples."""
+        return (
+            self.address.addr,
+            self.address.ifName,
+            self.weight,
+            None if self.mplsAction is None else self.mplsAction.key(),
+            self.metric,
+            self.useNonShortestRoute,
+            self.area,
+        )
+
+
+@dataclass
+class Adjacency:
+    otherNodeName: str = ""
+    ifName: str = ""
+    nextHopV6: BinaryAddress = field(default_factory=BinaryAddress)
+    nextHopV4: BinaryAddress = field(default_factory=BinaryAddress)
+    metric: int = 0
+    adjLabel: int = 0
+    isOverloaded: bool = False
+    rtt: int = 0
+    timestamp: int = 0
+    weight: int = 1
+    otherIfName: str = ""
+
+
+@dataclass
+class AdjacencyDatabase:
+    thisNodeName: str = ""
+    isOverloaded: bool = False
+    adjacencies: List[Adjacency] = field(default_factory=list)
+    nodeLabel: int = 0
+    area: str = kDefaultArea
+
+
+@dataclass
+class MetricEntity:
+    type: int = 0
+    priority: int = 0
+    op: int = CompareType.WIN_IF_PRESENT
+    isBestPathTieBreaker: bool = False
+    metric: List[int] = field(default_factory=list)
+
+
+@dataclass
+class MetricVector:
+    version: int = 0
+    metrics: List[MetricEntity] = field(default_factory=list)
+
+
+@dataclass
+class PrefixEntry:
+    prefix: IpPrefix = field(default_factory=IpPrefix)
+    type: int = PrefixType.LOOPBACK
+    data: Optional[bytes] = None
+    forwardingType: int = PrefixForwardingType.IP
+    forwardingAlgorithm: int = PrefixForwardingAlgorithm.SP_ECMP
+    ephemeral: Optional[bool] = None
+    mv: Optional[MetricVector] = None
+    minNexthop: Optional[int] = None
+    prependLabel: Optional[int] = None
+
+
+@dataclass
+class PrefixDatabase:
+    thisNodeName: str = ""
+    prefixEntries: List[PrefixEntry] = field(default_factory=list)
+    deletePrefix: bool = False
+    area: str = kDefaultArea
+
+
+@dataclass
+class MplsRoute:
+    topLabel: int = 0
+    nextHops: List[NextHopThrift] = field(default_factory=list)
+
+
+# ------------------------------------------------------------ Util helpers
+
+
+def toBinaryAddress(addr: str) -> BinaryAddress:
+    return BinaryAddress(ipaddress.ip_address(addr).packed)
+
+
+def toIpPrefix(prefix: str) -> IpPrefix:
+    net = ipaddress.ip_network(prefix, strict=False)
+    addr = ipaddress.ip_address(prefix.split("/")[0])
+    return IpPrefix(BinaryAddress(addr.packed), net.prefixlen)
+
+
+def prefixToString(key) -> str:
+    """(addr bytes, length) -> 'a.b.c.d/len' in folly's networkToString form."""
+    addr, plen = key
+    return f"{ipaddress.ip_address(addr)}/{plen}"
+
+
+def createAdjacency(
+    nodeName,
+    ifName,
+    remoteIfName,
+    nextHopV6,
+    nextHopV4,
+    metric,
+    adjLabel,
+    weight=1,
+):
+    # Util.cpp:786-808 (rtt = metric * 100; the timestamp is not on the path)
+    return Adjacency(
+        otherNodeName=nodeName,
+        ifName=ifName,
+        nextHopV6=toBinaryAddress(nextHopV6),
+        nextHopV4=toBinaryAddress(nextHopV4),
+        metric=metric,
+        adjLabel=adjLabel,
+        isOverloaded=False,
+        rtt=metric * 100,
+        timestamp=0,
+        weight=weight,
+        otherIfName=remoteIfName,
+    )
+
+
+def createThriftAdjacency(
+    nodeName,
+    ifName,
+    nextHopV6,
+    nextHopV4,
+    metric,
+    adjLabel,
+    isOverloaded,
+    rtt,
+    timestamp,
+    weight,
+    remoteIfName,
+):
+    return Adjacency(
+        nodeName,
+        ifName,
+        toBinaryAddress(nextHopV6),
+        toBinaryAddress(nextHopV4),
+        metric,
+        adjLabel,
+        isOverloaded,
+        rtt,
+        timestamp,
+        weight,
+        remoteIfName,
+    )
+
+
+def createAdjDb(nodeName, adjs, nodeLabel, overLoadBit=False, area=kDefaultArea):
+    return AdjacencyDatabase(nodeName, overLoadBit, list(adjs), nodeLabel, area)
+
+
+def createPrefixEntry(
+    prefix,
+    type=PrefixType.LOOPBACK,
+    data="",
+    forwardingType=PrefixForwardingType.IP,
+    forwardingAlgorithm=PrefixForwardingAlgorithm.SP_ECMP,
+    ephemeral=None,
+    mv=None,
+    minNexthop=None,
+):
+    return PrefixEntry(
+        prefix=prefix,
+        type=type,
+        data=data.encode() if data else None,
+        forwardingType=forwardingType,
+        forwardingAlgorithm=forwardingAlgorithm,
+        ephemeral=ephemeral,
+        mv=mv,
+        minNexthop=minNexthop,
+    )
+
+
+def createPrefixDb(nodeName, prefixEntries=(), area=kDefaultArea):
+    return PrefixDatabase(nodeName, list(prefixEntries), False, area)
+
+
+def createMplsAction(action, swapLabel=None, pushLabels=None):
+    return MplsAction(action, swapLabel, None if pushLabels is None else list(pushLabels))
+
+
+def createNextHop(
+    addr: BinaryAddress,
+    ifName=None,
+    metric=0,
+    mplsAction=None,
+    useNonShortestRoute=False,
+    area=kDefaultArea,
+):
+    return NextHopThrift(
+        BinaryAddress(addr.addr, ifName),
+        0,
+        mplsAction,
+        metric,
+        useNonShortestRoute,
+        area,
+    )
+
+
+def createNextHopFromAdj(
+    adj, isV4, metric, mplsAction=None, useNonShortestRoute=False, area=kDefaultArea
+):
+    return createNextHop(
+        adj.nextHopV4 if isV4 else adj.nextHopV6,
+        adj.ifName,
+        metric,
+        mplsAction,
+        useNonShortestRoute,
+        area,
+    )
+
+
+def createMetricEntity(type, priority, op, isBestPathTieBreaker, metric):
+    return MetricEntity(type, priority, op, isBestPathTieBreaker, list(metric))

@@ -1,0 +1,1215 @@
+// ref_decision.cpp — CPU ORACLE for the Decision SPF path.
+//
+// TEST INFRASTRUCTURE ONLY.  Imported (as oracle/_oracle_ref*.so) by tests/,
+// __graft_entry__.smoke() and the cpu_baseline leg of bench.py, and only as
+// the checker / the timed CPU baseline.  The product (openr_amd) never links
+// or imports it.
+//
+// This is a restatement of the reference algorithms with the reference's own
+// data-structure semantics (string-keyed maps, shared_ptr links in hash sets,
+// a binary-heap Dijkstra queue rebuilt with make_heap on every strict
+// improvement), so that (a) its outputs can be pinned to the known answers of
+// the reference's tests and (b) its run time is representative of the
+// reference CPU path.  Every function cites the reference lines it follows
+// (paths relative to the reference repo root).
+//
+// Reference build status: the reference itself needs folly / fbthrift / fb303 /
+// glog, none of which is in this image, so it is not built here.
+// folly's std::hash<std::pair> formula (hash_128_to_64 over libstdc++
+// std::hash<std::string>, folly @ ab8339ea) is restated below because link
+// iteration order depends on it.
+
+#include <algorithm>
+#include <chrono>
+#include <list>
+#include <map>
+#include <memory>
+#include <optional>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "../openr_amd/csrc/host/Types.h"
+#include "../openr_amd/csrc/py/convert.h"
+
+namespace oracle {
+
+using openr::thrift::Adjacency;
+using openr::thrift::AdjacencyDatabase;
+using openr::thrift::BinaryAddress;
+using openr::thrift::IpPrefix;
+using openr::thrift::MetricEntity;
+using openr::thrift::MetricVector;
+using openr::thrift::MplsAction;
+using openr::thrift::MplsActionCode;
+using openr::thrift::NextHopThrift;
+using openr::thrift::PrefixEntries;
+using openr::thrift::PrefixEntry;
+using openr::thrift::PrefixForwardingAlgorithm;
+using openr::thrift::PrefixForwardingType;
+using openr::thrift::PrefixType;
+using Metric = uint64_t;
+
+std::unordered_map<std::string, int64_t> g_counters;
+
+// ------------------------------------------------ folly hash (see header)
+static uint64_t h128(uint64_t upper, uint64_t lower) {
+  const uint64_t kMul = 0x9ddfea08eb382d69ULL;
+  uint64_t a = (lower ^ upper) * kMul;
+  a ^= (a >> 47);
+  uint64_t b = (upper ^ a) * kMul;
+  b ^= (b >> 47);
+  b *= kMul;
+  return b;
+}
+
+// ------------------------------------- HoldableValue (LinkState.cpp:54-125)
+template <class T>
+struct Held {
+  T cur;
+  std::optional<T> held;
+  Metric ttl = 0;
+  explicit Held(T v) : cur(v) {}
+  void set(T v) { cur = v; held.reset(); ttl = 0; }
+  const T& value() const { return held ? *held : cur; }
+  bool hasHold() const { return held.has_value(); }
+  bool decrementTtl() {
+    if (held && --ttl == 0) { held.reset(); return true; }
+    return false;
+  }
+  bool bringsUp(T v) const;
+  bool update(T v, Metric up, Metric down) {
+    if (v == cur) return false;
+    if (held) { held.reset(); ttl = 0; }
+    else { ttl = bringsUp(v) ? up : down; if (ttl) held = cur; }
+    cur = v;
+    return !held.has_value();
+  }
+};
+template <> bool Held<bool>::bringsUp(bool v) const { return cur && !v; }
+template <> bool Held<Metric>::bringsUp(Metric v) const { return v < cur; }
+
+// ------------------------------------------------- Link (LinkState.cpp:127-377)
+struct OLink {
+  std::string area, n1, n2, if1, if2;
+  Held<Metric> m1{1}, m2{1};
+  Held<bool> o1{false}, o2{false};
+  int32_t lab1 = 0, lab2 = 0;
+  BinaryAddress v41, v42, v61, v62;
+  Metric holdUp = 0;
+  std::pair<std::pair<std::string, std::string>, std::pair<std::string, std::string>> names;
+  size_t hash = 0;
+
+  OLink(const std::string& a, const std::string& x, const std::string& ix,
+        const std::string& y, const std::string& iy)
+      : area(a), n1(x), n2(y), if1(ix), if2(iy) {
+    names = std::minmax(std::make_pair(n1, if1), std::make_pair(n2, if2));
+    auto ph = [](const std::pair<std::string, std::string>& p) {
+      return h128(std::hash<std::string>()(p.first), std::hash<std::string>()(p.second));
+    };
+    hash = h128(ph(names.first), ph(names.second));
+  }
+  bool side1(const std::string& n) const {
+    if (n == n1) return true;
+    if (n == n2) return false;
+    throw std::invalid_argument(n);
+  }
+  const std::string& other(const std::string& n) const { return side1(n) ? n2 : n1; }
+  const std::string& iface(const std::string& n) const { return side1(n) ? if1 : if2; }
+  Metric metric(const std::string& n) const { return side1(n) ? m1.value() : m2.value(); }
+  bool overload(const std::string& n) const { return side1(n) ? o1.value() : o2.value(); }
+  int32_t adjLabel(const std::string& n) const { return side1(n) ? lab1 : lab2; }
+  const BinaryAddress& nhV4(const std::string& n) const { return side1(n) ? v41 : v42; }
+  const BinaryAddress& nhV6(const std::string& n) const { return side1(n) ? v61 : v62; }
+  bool isUp() const { return holdUp == 0 && !o1.value() && !o2.value(); }
+  bool decrementHolds() {
+    bool x = false;
+    if (holdUp != 0) x |= (--holdUp == 0);
+    x |= m1.decrementTtl();
+    x |= m2.decrementTtl();
+    x |= o1.decrementTtl();
+    x |= o2.decrementTtl();
+    return x;
+  }
+  bool hasHolds() const {
+    return holdUp != 0 || m1.hasHold() || m2.hasHold() || o1.hasHold() || o2.hasHold();
+  }
+  bool setOverload(const std::string& n, bool v, Metric up, Metric down) {
+    bool was = isUp();
+    (side1(n) ? o1 : o2).update(v, up, down);
+    return was != isUp();
+  }
+  bool operator<(const OLink& o) const { return hash != o.hash ? hash < o.hash : names < o.names; }
+  bool operator==(const OLink& o) const { return hash == o.hash && names == o.names; }
+};
+using LinkP = std::shared_ptr<OLink>;
+struct LH { size_t operator()(const LinkP& l) const { return l->hash; } };
+struct LE { bool operator()(const LinkP& a, const LinkP& b) const { return *a == *b; } };
+using LinkSet = std::unordered_set<LinkP, LH, LE>;
+
+// ------------------------------------------ SPF result (LinkState.h:203-260)
+struct NodeSpf {
+  Metric metric;
+  std::vector<std::pair<LinkP, std::string>> paths;
+  std::unordered_set<std::string> nhs;
+  explicit NodeSpf(Metric m) : metric(m) {}
+};
+using SpfResult = std::unordered_map<std::string, NodeSpf>;
+using Path = std::vector<LinkP>;
+
+// ------------------------------------------- DijkstraQ (LinkState.h:475-535)
+struct QNode {
+  std::string name;
+  NodeSpf res;
+  QNode(const std::string& n, Metric m) : name(n), res(m) {}
+};
+class DijkstraQ {
+  std::vector<std::shared_ptr<QNode>> heap_;
+  std::unordered_map<std::string, std::shared_ptr<QNode>> byName_;
+  static bool greater(const std::shared_ptr<QNode>& a, const std::shared_ptr<QNode>& b) {
+    if (a->res.metric != b->res.metric) return a->res.metric > b->res.metric;
+    return a->name > b->name;
+  }
+ public:
+  void insert(const std::string& n, Metric d) {
+    heap_.push_back(std::make_shared<QNode>(n, d));
+    byName_[n] = heap_.back();
+    std::push_heap(heap_.begin(), heap_.end(), greater);
+  }
+  std::shared_ptr<QNode> get(const std::string& n) {
+    auto it = byName_.find(n);
+    return it == byName_.end() ? nullptr : it->second;
+  }
+  std::shared_ptr<QNode> extractMin() {
+    if (heap_.empty()) return nullptr;
+    auto top = heap_.front();
+    byName_.erase(top->name);
+    std::pop_heap(heap_.begin(), heap_.end(), greater);
+    heap_.pop_back();
+    return top;
+  }
+  void reMake() { std::make_heap(heap_.begin(), heap_.end(), greater); }
+};
+
+// --------------------------------------------- LinkState (LinkState.cpp:379-880)
+class Graph {
+ public:
+  explicit Graph(const std::string& area) : area_(area) {}
+  const std::string& area() const { return area_; }
+
+  // LinkState.cpp:421-455
+  void addLink(const LinkP& l) {
+    if (!linkMap_[l->names.first.first].insert(l).second ||
+        !linkMap_[l->names.second.first].insert(l).second || !all_.insert(l).second)
+      throw std::logic_error("dup link");
+  }
+  void removeLink(const LinkP& l) {
+    if (!linkMap_.at(l->names.first.first).erase(l) ||
+        !linkMap_.at(l->names.second.first).erase(l) || !all_.erase(l))
+      throw std::logic_error("missing link");
+  }
+  void removeNode(const std::string& n) {
+    auto it = linkMap_.find(n);
+    if (it == linkMap_.end()) return;
+    for (const auto& l : it->second) {
+      if (!linkMap_.at(l->other(n)).erase(l) || !all_.erase(l)) throw std::logic_error("rm");
+    }
+    linkMap_.erase(it);
+    nodeOv_.erase(n);
+  }
+  const LinkSet& links(const std::string& n) const {
+    static const LinkSet empty;
+    auto it = linkMap_.find(n);
+    return it == linkMap_.end() ? empty : it->second;
+  }
+  bool overloaded(const std::string& n) const {
+    auto it = nodeOv_.find(n);
+    return it != nodeOv_.end() && it->second.value();
+  }
+  bool hasNode(const std::string& n) const { return dbs_.count(n) > 0; }
+  const std::unordered_map<std::string, AdjacencyDatabase>& dbs() const { return dbs_; }
+  size_t numLinks() const { return all_.size(); }
+
+  void clearMemo() { spf_.clear(); kth_.clear(); }
+
+  // LinkState.cpp:500-514
+  std::tuple<bool, bool, bool> decrementHolds() {
+    bool topo = false;
+    for (auto& l : all_) topo |= l->decrementHolds();
+    for (auto& kv : nodeOv_) topo |= kv.second.decrementTtl();
+    if (topo) clearMemo();
+    return {topo, false, false};
+  }
+  bool hasHolds() const {
+    for (auto& l : all_) if (l->hasHolds()) return true;
+    for (auto& kv : nodeOv_) if (kv.second.hasHold()) return true;
+    return false;
+  }
+
+  // LinkState.cpp:531-547
+  LinkP makeLink(const std::string& n, const Adjacency& adj) const {
+    auto it = dbs_.find(adj.otherNodeName);
+    if (it == dbs_.end()) return nullptr;
+    for (const auto& o : it->second.adjacencies) {
+      if (n == o.otherNodeName && adj.otherIfName == o.ifName && adj.ifName == o.otherIfName) {
+        auto l = std::make_shared<OLink>(area_, n, adj.ifName, adj.otherNodeName, o.ifName);
+        l->m1.set((Metric)(int64_t)adj.metric);
+        l->m2.set((Metric)(int64_t)o.metric);
+        l->o1.set(adj.isOverloaded);
+        l->o2.set(o.isOverloaded);
+        l->lab1 = adj.adjLabel;
+        l->lab2 = o.adjLabel;
+        l->v41 = adj.nextHopV4;
+        l->v42 = o.nextHopV4;
+        l->v61 = adj.nextHopV6;
+        l->v62 = o.nextHopV6;
+        return l;
+      }
+    }
+    return nullptr;
+  }
+
+  // LinkState.cpp:564-717
+  std::tuple<bool, bool, bool> update(const AdjacencyDatabase& db, Metric up, Metric down) {
+    bool topo = false, attrs = false, label = false;
+    const std::string n = db.thisNodeName;
+    AdjacencyDatabase prior(std::move(dbs_[n]));
+    dbs_[n] = db;
+    std::vector<LinkP> olds(links(n).begin(), links(n).end());
+    std::sort(olds.begin(), olds.end(), [](const LinkP& a, const LinkP& b) { return *a < *b; });
+    std::vector<LinkP> news;
+    for (const auto& adj : db.adjacencies) {
+      if (auto l = makeLink(n, adj)) news.push_back(l);
+    }
+    std::sort(news.begin(), news.end(), [](const LinkP& a, const LinkP& b) { return *a < *b; });
+    // LinkState.cpp:480-493
+    auto ov = nodeOv_.find(n);
+    if (ov != nodeOv_.end()) topo |= ov->second.update(db.isOverloaded, up, down);
+    else nodeOv_.emplace(n, Held<bool>(db.isOverloaded));
+    label = prior.nodeLabel != db.nodeLabel;
+    auto ni = news.begin();
+    auto oi = olds.begin();
+    while (ni != news.end() || oi != olds.end()) {
+      if (ni != news.end() && (oi == olds.end() || **ni < **oi)) {
+        (*ni)->holdUp = up;
+        topo |= (*ni)->isUp();
+        addLink(*ni);
+        ++ni;
+      } else if (oi != olds.end() && (ni == news.end() || **oi < **ni)) {
+        topo |= (*oi)->isUp();
+        removeLink(*oi);
+        ++oi;
+      } else {
+        OLink& nw = **ni;
+        OLink& od = **oi;
+        if (nw.metric(n) != od.metric(n))
+          topo |= (od.side1(n) ? od.m1 : od.m2).update(nw.metric(n), up, down);
+        if (nw.overload(n) != od.overload(n)) topo |= od.setOverload(n, nw.overload(n), up, down);
+        if (nw.adjLabel(n) != od.adjLabel(n)) {
+          attrs = true;
+          (od.side1(n) ? od.lab1 : od.lab2) = nw.adjLabel(n);
+        }
+        if (nw.nhV4(n) != od.nhV4(n)) {
+          attrs = true;
+          (od.side1(n) ? od.v41 : od.v42) = nw.nhV4(n);
+        }
+        if (nw.nhV6(n) != od.nhV6(n)) {
+          attrs = true;
+          (od.side1(n) ? od.v61 : od.v62) = nw.nhV6(n);
+        }
+        ++ni;
+        ++oi;
+      }
+    }
+    if (topo) clearMemo();
+    return {topo, attrs, label};
+  }
+
+  // LinkState.cpp:719-736
+  std::tuple<bool, bool, bool> remove(const std::string& n) {
+    auto it = dbs_.find(n);
+    if (it == dbs_.end()) return {false, false, false};
+    removeNode(n);
+    dbs_.erase(it);
+    clearMemo();
+    return {true, false, false};
+  }
+
+  // LinkState.cpp:806-880
+  SpfResult runSpf(const std::string& src, bool useMetric, const LinkSet& ignore) const {
+    SpfResult result;
+    g_counters["decision.spf_runs"] += 1;
+    DijkstraQ q;
+    q.insert(src, 0);
+    while (auto node = q.extractMin()) {
+      auto ins = result.emplace(node->name, std::move(node->res));
+      const std::string& un = ins.first->first;
+      const Metric um = ins.first->second.metric;
+      const auto& unh = ins.first->second.nhs;
+      if (overloaded(un) && un != src) continue; // recorded, never transited
+      for (const auto& l : links(un)) {
+        const std::string& vn = l->other(un);
+        if (!l->isUp() || result.count(vn) || ignore.count(l)) continue;
+        const Metric w = useMetric ? l->metric(un) : 1;
+        auto v = q.get(vn);
+        if (!v) {
+          q.insert(vn, um + w);
+          v = q.get(vn);
+        }
+        if (v->res.metric >= um + w) {
+          if (v->res.metric > um + w) {
+            v->res.metric = um + w;
+            v->res.paths.clear();
+            v->res.nhs.clear();
+            q.reMake();
+          }
+          v->res.paths.emplace_back(l, un);
+          v->res.nhs.insert(unh.begin(), unh.end());
+          if (v->res.nhs.empty()) v->res.nhs.insert(vn);
+        }
+      }
+    }
+    return result;
+  }
+
+  // LinkState.cpp:791-801
+  const SpfResult& getSpf(const std::string& n, bool useMetric) const {
+    auto key = std::make_pair(n, useMetric);
+    auto it = spf_.find(key);
+    if (it == spf_.end()) it = spf_.emplace(key, runSpf(n, useMetric, {})).first;
+    return it->second;
+  }
+
+  // LinkState.cpp:398-419
+  std::optional<Path> trace(const std::string& s, const std::string& d, const SpfResult& r,
+                            LinkSet& seen) const {
+    if (s == d) return Path{};
+    for (const auto& [l, prev] : r.at(d).paths) {
+      if (seen.insert(l).second) {
+        if (auto p = trace(s, prev, r, seen)) {
+          p->push_back(l);
+          return p;
+        }
+      }
+    }
+    return std::nullopt;
+  }
+
+  // LinkState.cpp:760-789
+  const std::vector<Path>& kth(const std::string& s, const std::string& d, size_t k) const {
+    if (k < 1) throw std::invalid_argument("k");
+    auto key = std::make_tuple(s, d, k);
+    auto it = kth_.find(key);
+    if (it != kth_.end()) return it->second;
+    LinkSet ignore;
+    for (size_t i = 1; i < k; ++i)
+      for (const auto& p : kth(s, d, i))
+        for (const auto& l : p) ignore.insert(l);
+    std::vector<Path> paths;
+    SpfResult tmp;
+    const SpfResult* res;
+    if (ignore.empty()) res = &getSpf(s, true);
+    else { tmp = runSpf(s, true, ignore); res = &tmp; }
+    if (res->count(d)) {
+      LinkSet seen;
+      auto p = trace(s, d, *res, seen);
+      while (p && !p->empty()) {
+        paths.push_back(std::move(*p));
+        p = trace(s, d, *res, seen);
+      }
+    }
+    return kth_.emplace(key, std::move(paths)).first->second;
+  }
+
+  std::optional<Metric> metricAB(const std::string& a, const std::string& b, bool m) const {
+    if (a == b) return 0;
+    const auto& r = getSpf(a, m);
+    auto it = r.find(b);
+    if (it == r.end()) return std::nullopt;
+    return it->second.metric;
+  }
+  Metric maxHops(const std::string& n) const {
+    Metric best = 0;
+    for (const auto& kv : getSpf(n, false)) best = std::max(best, kv.second.metric);
+    return best;
+  }
+
+ private:
+  std::string area_;
+  std::unordered_map<std::string, LinkSet> linkMap_;
+  LinkSet all_;
+  std::unordered_map<std::string, Held<bool>> nodeOv_;
+  std::unordered_map<std::string, AdjacencyDatabase> dbs_;
+  struct PH {
+    size_t operator()(const std::pair<std::string, bool>& p) const {
+      return std::hash<std::string>()(p.first) * 2 + p.second;
+    }
+  };
+  struct TH {
+    size_t operator()(const std::tuple<std::string, std::string, size_t>& t) const {
+      return h128(std::hash<std::string>()(std::get<0>(t)),
+                  h128(std::hash<std::string>()(std::get<1>(t)), std::get<2>(t)));
+    }
+  };
+  mutable std::unordered_map<std::pair<std::string, bool>, SpfResult, PH> spf_;
+  mutable std::unordered_map<std::tuple<std::string, std::string, size_t>, std::vector<Path>, TH>
+      kth_;
+};
+
+// LinkState.h:395-410
+bool pathAInPathB(const Path& a, const Path& b) {
+  if (a.size() > b.size()) return false;
+  for (size_t i = 0; i + a.size() <= b.size(); ++i) {
+    size_t j = 0;
+    while (j < a.size() && *a[j] == *b[i + j]) ++j;
+    if (j == a.size()) return true;
+  }
+  return false;
+}
+
+// ----------------------------------------------- PrefixState (PrefixState.cpp)
+class Prefixes {
+ public:
+  std::unordered_map<IpPrefix, PrefixEntries> byPrefix;
+  std::unordered_map<std::string, std::unordered_map<std::string, std::set<IpPrefix>>> byNode;
+  std::unordered_map<std::string, BinaryAddress> lo4, lo6;
+
+  // PrefixState.cpp:36-125
+  std::set<IpPrefix> update(const openr::thrift::PrefixDatabase& db) {
+    std::set<IpPrefix> changed;
+    const auto& n = db.thisNodeName;
+    const auto& a = db.area;
+    const std::set<IpPrefix> old = byNode[n][a];
+    auto& now = byNode[n][a];
+    now.clear();
+    for (const auto& e : db.prefixEntries) now.insert(e.prefix);
+    for (const auto& p : old) {
+      if (now.count(p)) continue;
+      auto& byOrig = byPrefix.at(p);
+      if (!byOrig.count(n)) continue;
+      byOrig.at(n).erase(a);
+      if (byOrig.at(n).empty()) byOrig.erase(n);
+      if (byOrig.empty()) byPrefix.erase(p);
+      // PrefixState.cpp:12-34
+      if (p.prefixAddress.addr.size() == 4 && p.prefixLength == 32 && lo4.count(n) &&
+          lo4.at(n) == p.prefixAddress)
+        lo4.erase(n);
+      if (p.prefixAddress.addr.size() == 16 && p.prefixLength == 128 && lo6.count(n) &&
+          lo6.at(n) == p.prefixAddress)
+        lo6.erase(n);
+      changed.insert(p);
+    }
+    for (const auto& e : db.prefixEntries) {
+      auto& byOrig = byPrefix[e.prefix];
+      if (byOrig.count(n) && byOrig.at(n).count(a) && byOrig.at(n).at(a) == e) continue;
+      byOrig[n][a] = e;
+      changed.insert(e.prefix);
+      if (e.type == PrefixType::LOOPBACK) {
+        if (e.prefix.prefixAddress.addr.size() == 4 && e.prefix.prefixLength == 32)
+          lo4[n] = e.prefix.prefixAddress;
+        if (e.prefix.prefixAddress.addr.size() == 16 && e.prefix.prefixLength == 128)
+          lo6[n] = e.prefix.prefixAddress;
+      }
+    }
+    if (now.empty()) byNode.erase(n);
+    return changed;
+  }
+};
+
+// --------------------------------------------------- Util helpers (Util.cpp)
+bool labelOk(int32_t l) { return (l & 0xfff00000) == 0; } // Util.h:303-306
+
+MplsAction mkAction(MplsActionCode c, std::optional<int32_t> swap = std::nullopt,
+                    std::optional<std::vector<int32_t>> push = std::nullopt) {
+  // Util.cpp:673-703 checks (a CHECK failure aborts the reference)
+  if (c == MplsActionCode::PUSH) {
+    if (swap || !push || push->empty()) throw std::logic_error("PUSH");
+    for (auto l : *push) if (!labelOk(l)) throw std::logic_error("PUSH label");
+  } else if (c == MplsActionCode::SWAP) {
+    if (!swap || !labelOk(*swap) || push) throw std::logic_error("SWAP");
+  } else if (swap || push) {
+    throw std::logic_error("PHP/POP");
+  }
+  MplsAction a;
+  a.action = c;
+  a.swapLabel = swap;
+  a.pushLabels = push;
+  return a;
+}
+
+NextHopThrift mkNextHop(BinaryAddress addr, std::optional<std::string> ifName, int32_t metric,
+                        std::optional<MplsAction> act, bool nonShortest, const std::string& area) {
+  // Util.cpp:914-930
+  NextHopThrift nh;
+  nh.address = std::move(addr);
+  nh.address.ifName = std::move(ifName);
+  nh.metric = metric;
+  nh.mplsAction = std::move(act);
+  nh.useNonShortestRoute = nonShortest;
+  nh.area = area;
+  return nh;
+}
+
+PrefixForwardingType fwdType(const PrefixEntries& es) { // Util.cpp:635-652
+  if (es.empty()) return PrefixForwardingType::IP;
+  for (const auto& [_, m] : es)
+    for (const auto& [__, e] : m)
+      if (e.forwardingType == PrefixForwardingType::IP) return PrefixForwardingType::IP;
+  return PrefixForwardingType::SR_MPLS;
+}
+PrefixForwardingAlgorithm fwdAlgo(const PrefixEntries& es) { // Util.cpp:654-671
+  if (es.empty()) return PrefixForwardingAlgorithm::SP_ECMP;
+  for (const auto& [_, m] : es)
+    for (const auto& [__, e] : m)
+      if (e.forwardingAlgorithm == PrefixForwardingAlgorithm::SP_ECMP)
+        return PrefixForwardingAlgorithm::SP_ECMP;
+  return PrefixForwardingAlgorithm::KSP2_ED_ECMP;
+}
+
+// Util.cpp:1051-1228 (MetricVectorUtils)
+enum class Cmp { WINNER, TIE_WINNER, TIE, TIE_LOOSER, LOOSER, ERROR };
+Cmp negate(Cmp c) {
+  switch (c) {
+    case Cmp::WINNER: return Cmp::LOOSER;
+    case Cmp::TIE_WINNER: return Cmp::TIE_LOOSER;
+    case Cmp::TIE_LOOSER: return Cmp::TIE_WINNER;
+    case Cmp::LOOSER: return Cmp::WINNER;
+    default: return c;
+  }
+}
+bool decisive(Cmp c) { return c == Cmp::WINNER || c == Cmp::LOOSER || c == Cmp::ERROR; }
+Cmp loner(const MetricEntity& e) {
+  using CT = openr::thrift::CompareType;
+  if (e.op == CT::WIN_IF_PRESENT) return e.isBestPathTieBreaker ? Cmp::TIE_WINNER : Cmp::WINNER;
+  if (e.op == CT::WIN_IF_NOT_PRESENT) return e.isBestPathTieBreaker ? Cmp::TIE_LOOSER : Cmp::LOOSER;
+  return Cmp::TIE;
+}
+void upd(Cmp& t, Cmp u) { if (decisive(u) || t == Cmp::TIE) t = u; }
+void sortMv(MetricVector& mv) {
+  bool ok = true;
+  for (size_t i = 1; i < mv.metrics.size(); ++i) ok &= mv.metrics[i].priority <= mv.metrics[i - 1].priority;
+  if (!ok)
+    std::sort(mv.metrics.begin(), mv.metrics.end(),
+              [](const MetricEntity& a, const MetricEntity& b) { return a.priority > b.priority; });
+}
+Cmp cmpVals(const std::vector<int64_t>& l, const std::vector<int64_t>& r, bool tb) {
+  if (l.size() != r.size()) return Cmp::ERROR;
+  for (size_t i = 0; i < l.size(); ++i) {
+    if (l[i] > r[i]) return tb ? Cmp::TIE_WINNER : Cmp::WINNER;
+    if (l[i] < r[i]) return tb ? Cmp::TIE_LOOSER : Cmp::LOOSER;
+  }
+  return Cmp::TIE;
+}
+Cmp compareMv(MetricVector& l, MetricVector& r) {
+  if (l.version != r.version) return Cmp::ERROR;
+  sortMv(l);
+  sortMv(r);
+  Cmp res = Cmp::TIE;
+  auto a = l.metrics.begin(), b = r.metrics.begin();
+  while (!decisive(res) && a != l.metrics.end() && b != r.metrics.end()) {
+    if (a->type == b->type) {
+      if (a->isBestPathTieBreaker != b->isBestPathTieBreaker) upd(res, Cmp::ERROR);
+      else upd(res, cmpVals(a->metric, b->metric, a->isBestPathTieBreaker));
+      ++a;
+      ++b;
+    } else if (a->priority > b->priority) {
+      upd(res, loner(*a++));
+    } else if (a->priority < b->priority) {
+      upd(res, negate(loner(*b++)));
+    } else {
+      upd(res, Cmp::ERROR);
+    }
+  }
+  while (!decisive(res) && a != l.metrics.end()) upd(res, loner(*a++));
+  while (!decisive(res) && b != r.metrics.end()) upd(res, negate(loner(*b++)));
+  return res;
+}
+
+// ------------------------------------------------ SpfSolver (Decision.cpp:90-1271)
+struct Best {
+  bool success = false;
+  std::string bestNode, bestArea;
+  std::set<std::string> nodes, areas;
+  std::optional<int64_t> bestIgp;
+  std::optional<MetricVector> bestVector;
+};
+struct UEntry {
+  std::unordered_set<NextHopThrift> nhs;
+  PrefixEntry best;
+  std::string bestArea;
+  bool dni = false;
+  std::optional<NextHopThrift> bestNh;
+};
+struct RouteDb {
+  std::unordered_map<IpPrefix, UEntry> unicast;
+  std::unordered_map<int32_t, std::unordered_set<NextHopThrift>> mpls;
+};
+using Areas = std::unordered_map<std::string, Graph>;
+struct SPH {
+  size_t operator()(const std::pair<std::string, std::string>& p) const {
+    return h128(std::hash<std::string>()(p.first), std::hash<std::string>()(p.second));
+  }
+};
+using NhNodes = std::unordered_map<std::pair<std::string, std::string>, Metric, SPH>;
+
+class Solver {
+ public:
+  Solver(bool v4, bool lfa, bool dryRun, bool useIgp)
+      : v4_(v4), lfa_(lfa), dryRun_(dryRun), useIgp_(useIgp) {}
+  std::unordered_map<int32_t, std::vector<NextHopThrift>> staticMpls;
+
+  // Decision.cpp:544-630
+  Best announcers(const std::string& me, const PrefixEntries& es, bool bgp, bool ksp2,
+                  const Areas& areas) {
+    Best r;
+    if (!bgp) {
+      if (es.count(me)) return Best{};
+      for (const auto& [node, byArea] : es) {
+        for (const auto& [area, e] : byArea) {
+          const auto& spf = areas.at(area).getSpf(me, true);
+          if (!spf.count(node)) continue;
+          if (r.bestNode.empty() || node.compare(r.bestNode) < 0) {
+            r.bestNode = node;
+            r.bestArea = area;
+          }
+          r.nodes.insert(node);
+          r.areas.insert(area);
+        }
+      }
+      r.success = true;
+      return filterDrained(std::move(r), areas);
+    }
+    r = bgpBest(me, es, areas);
+    if (!r.success) return Best{};
+    if (!ksp2) {
+      if (r.nodes.count(me)) return Best{};
+      return filterDrained(std::move(r), areas);
+    }
+    bool myLabel = false;
+    if (es.count(me))
+      for (const auto& [_, e] : es.at(me)) myLabel |= e.prependLabel.has_value();
+    if (!r.nodes.count(me) || (r.nodes.size() > 1 && myLabel)) return filterDrained(std::move(r), areas);
+    return Best{};
+  }
+
+  // Decision.cpp:714-800
+  Best bgpBest(const std::string& me, const PrefixEntries& es, const Areas& areas) {
+    Best r;
+    for (const auto& [node, byArea] : es) {
+      for (const auto& [area, e] : byArea) {
+        const auto& spf = areas.at(area).getSpf(me, true);
+        auto it = spf.find(node);
+        if (it == spf.end()) continue;
+        bool hasIgp = false;
+        for (const auto& m : e.mv.value().metrics) hasIgp |= m.type == 9;
+        if (hasIgp) continue;
+        MetricVector mv = *e.mv;
+        if (useIgp_) {
+          const int64_t igp = (int64_t)it->second.metric;
+          if (!r.bestIgp || *r.bestIgp > igp) r.bestIgp = igp;
+          MetricEntity me2;
+          me2.type = 9;
+          me2.priority = 3500;
+          me2.op = openr::thrift::CompareType::WIN_IF_NOT_PRESENT;
+          me2.isBestPathTieBreaker = false;
+          me2.metric = {-1 * igp};
+          mv.metrics.push_back(me2);
+        }
+        Cmp c = r.bestVector ? compareMv(mv, *r.bestVector) : Cmp::WINNER;
+        if (c == Cmp::TIE || c == Cmp::ERROR) return r;
+        if (c == Cmp::WINNER) r.nodes.clear();
+        if (c == Cmp::WINNER || c == Cmp::TIE_WINNER) {
+          r.bestVector = std::move(mv);
+          r.bestNode = node;
+          r.bestArea = area;
+        }
+        if (c == Cmp::WINNER || c == Cmp::TIE_WINNER || c == Cmp::TIE_LOOSER) {
+          r.nodes.insert(node);
+          r.areas.insert(area);
+        }
+      }
+    }
+    r.success = true;
+    return filterDrained(std::move(r), areas);
+  }
+
+  // Decision.cpp:651-666
+  Best filterDrained(Best&& r, const Areas& areas) const {
+    Best f = r;
+    for (const auto& [_, g] : areas)
+      for (auto it = f.nodes.begin(); it != f.nodes.end();)
+        it = g.overloaded(*it) ? f.nodes.erase(it) : std::next(it);
+    return f.nodes.empty() ? r : f;
+  }
+
+  // Decision.cpp:1093-1179
+  std::pair<Metric, NhNodes> nextHopsWithMetric(const std::string& me,
+                                                const std::set<std::string>& dsts, bool perDst,
+                                                const Areas& areas) {
+    NhNodes out;
+    Metric shortest = std::numeric_limits<Metric>::max();
+    for (const auto& [_, g] : areas) {
+      const auto& mine = g.getSpf(me, true);
+      // Decision.cpp:1068-1091
+      Metric aMin = std::numeric_limits<Metric>::max();
+      std::unordered_set<std::string> minNodes;
+      for (const auto& d : dsts) {
+        auto it = mine.find(d);
+        if (it == mine.end()) continue;
+        if (aMin >= it->second.metric) {
+          if (aMin > it->second.metric) {
+            aMin = it->second.metric;
+            minNodes.clear();
+          }
+          minNodes.insert(d);
+        }
+      }
+      if (shortest < aMin) continue;
+      if (shortest > aMin) {
+        shortest = aMin;
+        out.clear();
+      }
+      if (minNodes.empty()) continue;
+      for (const auto& d : minNodes)
+        for (const auto& nh : mine.at(d).nhs)
+          out[{nh, perDst ? d : ""}] = shortest - g.metricAB(me, nh, true).value();
+      if (lfa_) {
+        for (const auto& l : g.links(me)) {
+          if (!l->isUp()) continue;
+          const auto& nbr = l->other(me);
+          const auto& theirs = g.getSpf(nbr, true);
+          const Metric back = theirs.at(me).metric;
+          for (const auto& d : dsts) {
+            auto it = theirs.find(d);
+            if (it == theirs.end()) continue;
+            if (it->second.metric < shortest + back) {
+              auto key = std::make_pair(nbr, perDst ? d : std::string());
+              auto f = out.find(key);
+              if (f == out.end()) out.emplace(key, it->second.metric);
+              else if (f->second > it->second.metric) f->second = it->second.metric;
+            }
+          }
+        }
+      }
+    }
+    return {shortest, out};
+  }
+
+  // Decision.cpp:1181-1271
+  std::unordered_set<NextHopThrift> nextHopsThrift(const std::string& me,
+                                                  const std::set<std::string>& dsts, bool isV4,
+                                                  bool perDst, Metric minMetric, const NhNodes& nhn,
+                                                  std::optional<int32_t> swap, const Areas& areas,
+                                                  const std::set<std::string>& pAreas) const {
+    if (nhn.empty()) throw std::logic_error("no next hops");
+    std::unordered_set<NextHopThrift> out;
+    const std::set<std::string> blank{""};
+    for (const auto& [area, g] : areas) {
+      if (!pAreas.count(area)) continue;
+      for (const auto& l : g.links(me)) {
+        for (const auto& d : perDst ? dsts : blank) {
+          const std::string nbr = l->other(me);
+          auto it = nhn.find({nbr, d});
+          if (it == nhn.end() || !l->isUp()) continue;
+          if (!d.empty() && dsts.count(nbr) && nbr != d) continue;
+          const Metric over = l->metric(me) + it->second;
+          if (!lfa_ && over != minMetric) continue;
+          std::optional<MplsAction> act;
+          if (swap) {
+            const bool alsoDst = dsts.count(nbr) > 0;
+            act = mkAction(alsoDst ? MplsActionCode::PHP : MplsActionCode::SWAP,
+                           alsoDst ? std::nullopt : swap);
+          }
+          if (!d.empty() && d != nbr) {
+            const int32_t lab = g.dbs().at(d).nodeLabel;
+            if (!labelOk(lab)) continue;
+            if (act) throw std::logic_error("double action");
+            act = mkAction(MplsActionCode::PUSH, std::nullopt, std::vector<int32_t>{lab});
+          }
+          out.insert(mkNextHop(isV4 ? l->nhV4(me) : l->nhV6(me), l->iface(me), (int32_t)over, act,
+                               false, l->area));
+        }
+      }
+    }
+    return out;
+  }
+
+  // Decision.cpp:632-649
+  std::optional<int64_t> minNh(const Best& b, const PrefixEntries& es) const {
+    std::optional<int64_t> r;
+    for (const auto& n : b.nodes) {
+      if (!es.count(n)) continue;
+      for (const auto& [_, e] : es.at(n))
+        r = e.minNexthop && (!r || *e.minNexthop > *r) ? e.minNexthop : r;
+    }
+    return r;
+  }
+
+  // Decision.cpp:909-1066
+  void ksp2(RouteDb& db, const IpPrefix& prefix, const std::string& me, const Best& b,
+            const PrefixEntries& es, bool bgp, const Areas& areas, const Prefixes& ps,
+            PrefixForwardingAlgorithm algo) {
+    UEntry entry;
+    bool self = false;
+    std::vector<Path> paths;
+    for (const auto& [_, g] : areas) {
+      for (const auto& n : b.nodes) {
+        if (n == me) {
+          self = true;
+          continue;
+        }
+        for (const auto& p : g.kth(me, n, 1)) paths.push_back(p);
+      }
+      if (algo == PrefixForwardingAlgorithm::KSP2_ED_ECMP) {
+        const size_t first = paths.size();
+        for (const auto& n : b.nodes) {
+          for (const auto& sp : g.kth(me, n, 2)) {
+            bool add = true;
+            for (size_t i = 0; i < first; ++i)
+              if (pathAInPathB(paths[i], sp)) { add = false; break; }
+            if (add) paths.push_back(sp);
+          }
+        }
+      }
+    }
+    if (paths.empty()) return;
+    for (const auto& path : paths) {
+      for (const auto& [area, g] : areas) {
+        Metric cost = 0;
+        std::list<int32_t> labels;
+        std::string next = me;
+        for (const auto& l : path) {
+          cost += l->metric(next);
+          next = l->other(next);
+          labels.push_front(g.dbs().at(next).nodeLabel);
+        }
+        labels.pop_back();
+        if (es.at(next).at(area).prependLabel) labels.push_front(*es.at(next).at(area).prependLabel);
+        if (path.empty()) throw std::logic_error("empty path");
+        const auto& first = path.front();
+        std::optional<MplsAction> act;
+        if (!labels.empty())
+          act = mkAction(MplsActionCode::PUSH, std::nullopt,
+                         std::vector<int32_t>(labels.begin(), labels.end()));
+        const bool v4 = prefix.prefixAddress.addr.size() == 4;
+        entry.nhs.insert(mkNextHop(v4 ? first->nhV4(me) : first->nhV6(me), first->iface(me),
+                                   (int32_t)cost, act, true, first->area));
+      }
+    }
+    int statics = 0;
+    if (self) {
+      if (es.at(me).size() != 1) throw std::logic_error("one area");
+      const int32_t lab = es.at(me).begin()->second.prependLabel.value();
+      auto it = staticMpls.find(lab);
+      if (it != staticMpls.end()) {
+        for (const auto& nh : it->second) {
+          ++statics;
+          entry.nhs.insert(mkNextHop(nh.address, std::nullopt, 0, std::nullopt, true,
+                                     es.at(me).begin()->first));
+        }
+      }
+    }
+    auto mn = minNh(b, es);
+    if (mn && *mn > (int64_t)entry.nhs.size() - statics) return;
+    if (bgp) {
+      auto via = loopbackVias(ps, {b.bestNode}, prefix.prefixAddress.addr.size() == 4, b.bestIgp);
+      if (via.size() == 1) {
+        entry.bestNh = via.at(0);
+        entry.best = es.at(b.bestNode).at(b.bestArea);
+        entry.dni = dryRun_;
+      }
+    }
+    db.unicast.emplace(prefix, std::move(entry));
+  }
+
+  // PrefixState.cpp:145-163
+  static std::vector<NextHopThrift> loopbackVias(const Prefixes& ps,
+                                                 const std::unordered_set<std::string>& nodes,
+                                                 bool v4, std::optional<int64_t> igp) {
+    std::vector<NextHopThrift> out;
+    const auto& lo = v4 ? ps.lo4 : ps.lo6;
+    for (const auto& n : nodes)
+      if (lo.count(n))
+        out.push_back(mkNextHop(lo.at(n), std::nullopt, (int32_t)igp.value_or(0), std::nullopt,
+                                false, "0"));
+    return out;
+  }
+
+  // Decision.cpp:291-542
+  std::optional<RouteDb> build(const std::string& me, const Areas& areas, const Prefixes& ps) {
+    bool exists = false;
+    for (const auto& [_, g] : areas) exists |= g.hasNode(me);
+    if (!exists) return std::nullopt;
+    RouteDb db;
+    for (const auto& [prefix, es] : ps.byPrefix) {
+      bool bgp = false, nonBgp = false, noMv = false;
+      for (const auto& [_, m] : es)
+        for (const auto& [__, e] : m) {
+          const bool isB = e.type == PrefixType::BGP;
+          bgp |= isB;
+          nonBgp |= !isB;
+          if (isB && !e.mv) noMv = true;
+        }
+      if (bgp && (nonBgp || noMv)) continue;
+      if (es.count(me) && !bgp) continue;
+      const bool isV4 = prefix.prefixAddress.addr.size() == 4;
+      if (isV4 && !v4_) continue;
+      const auto algo = fwdAlgo(es);
+      if (fwdType(es) == PrefixForwardingType::SR_MPLS) {
+        auto b = announcers(me, es, bgp, true, areas);
+        if (!b.success || b.nodes.empty()) continue;
+        ksp2(db, prefix, me, b, es, bgp, areas, ps, algo);
+      } else if (algo == PrefixForwardingAlgorithm::SP_ECMP) {
+        if (bgp) ecmpBgp(db, me, prefix, es, isV4, areas, ps);
+        else ecmpOpenr(db, me, prefix, es, isV4, areas);
+      }
+    }
+    // node labels (Decision.cpp:415-501)
+    std::unordered_map<int32_t, std::pair<std::string, std::unordered_set<NextHopThrift>>> l2n;
+    for (const auto& [area, g] : areas) {
+      for (const auto& [_, adb] : g.dbs()) {
+        const int32_t top = adb.nodeLabel;
+        if (top == 0 || !labelOk(top)) continue;
+        auto it = l2n.find(top);
+        if (it != l2n.end() && it->second.first < adb.thisNodeName) continue;
+        if (adb.thisNodeName == me) {
+          NextHopThrift nh;
+          nh.address.addr = std::string(16, '\0');
+          nh.area = area;
+          nh.mplsAction = mkAction(MplsActionCode::POP_AND_LOOKUP);
+          l2n.erase(top);
+          l2n.emplace(top, std::make_pair(adb.thisNodeName, std::unordered_set<NextHopThrift>{nh}));
+          continue;
+        }
+        auto mn = nextHopsWithMetric(me, {adb.thisNodeName}, false, areas);
+        if (mn.second.empty()) continue;
+        l2n.erase(top);
+        l2n.emplace(top, std::make_pair(adb.thisNodeName,
+                                        nextHopsThrift(me, {adb.thisNodeName}, false, false,
+                                                       mn.first, mn.second, top, areas, {area})));
+      }
+    }
+    for (auto& [lab, p] : l2n) db.mpls.emplace(lab, std::move(p.second));
+    // adjacency labels (Decision.cpp:503-534)
+    for (const auto& [_, g] : areas) {
+      for (const auto& l : g.links(me)) {
+        const int32_t top = l->adjLabel(me);
+        if (top == 0 || !labelOk(top)) continue;
+        db.mpls.emplace(top, std::unordered_set<NextHopThrift>{
+                                 mkNextHop(l->nhV6(me), l->iface(me), (int32_t)l->metric(me),
+                                           mkAction(MplsActionCode::PHP), false, l->area)});
+      }
+    }
+    return db;
+  }
+
+  // Decision.cpp:668-712
+  void ecmpOpenr(RouteDb& db, const std::string& me, const IpPrefix& prefix,
+                 const PrefixEntries& es, bool isV4, const Areas& areas) {
+    auto b = announcers(me, es, false, false, areas);
+    if (!b.success) return;
+    const bool perDst = fwdType(es) == PrefixForwardingType::SR_MPLS;
+    auto mn = nextHopsWithMetric(me, b.nodes, perDst, areas);
+    if (mn.second.empty()) return;
+    UEntry e;
+    e.nhs = nextHopsThrift(me, b.nodes, isV4, perDst, mn.first, mn.second, std::nullopt, areas, b.areas);
+    e.best = es.at(b.bestNode).at(b.bestArea);
+    e.bestArea = b.bestArea;
+    db.unicast.emplace(prefix, std::move(e));
+  }
+
+  // Decision.cpp:802-866
+  void ecmpBgp(RouteDb& db, const std::string& me, const IpPrefix& prefix, const PrefixEntries& es,
+               bool isV4, const Areas& areas, const Prefixes& ps) {
+    auto b = announcers(me, es, true, false, areas);
+    if (!b.success) return;
+    if (b.nodes.empty() || b.nodes.count(me)) return;
+    auto via = loopbackVias(ps, {b.bestNode}, isV4, b.bestIgp);
+    if (via.size() != 1) return;
+    auto mn = nextHopsWithMetric(me, b.nodes, false, areas);
+    UEntry e;
+    e.nhs = nextHopsThrift(me, b.nodes, isV4, false, mn.first, mn.second, std::nullopt, areas, b.areas);
+    e.best = es.at(b.bestNode).at(b.bestArea);
+    e.bestArea = b.bestArea;
+    e.dni = dryRun_;
+    e.bestNh = via.at(0);
+    db.unicast.emplace(prefix, std::move(e));
+  }
+
+ private:
+  bool v4_, lfa_, dryRun_, useIgp_;
+};
+
+} // namespace oracle
+
+// =================================================================== python
+
+namespace {
+using namespace oracle;
+using namespace openr_py;
+
+py::tuple linkKey(const OLink& l) {
+  return py::make_tuple(py::make_tuple(l.names.first.first, l.names.first.second),
+                        py::make_tuple(l.names.second.first, l.names.second.second));
+}
+py::tuple chg(const std::tuple<bool, bool, bool>& t) {
+  return py::make_tuple(std::get<0>(t), std::get<1>(t), std::get<2>(t));
+}
+struct AreaHolder {
+  Areas map;
+  AreaHolder() = default;
+  AreaHolder(const AreaHolder&) = delete;
+};
+} // namespace
+
+PYBIND11_MODULE(_oracle_ref, m) {
+  m.doc() = "CPU oracle (test infrastructure): restated reference LinkState / SpfSolver";
+  m.def("get_counters", [] {
+    py::dict d;
+    for (const auto& [k, v] : g_counters) d[py::str(k)] = v;
+    return d;
+  });
+  m.def("reset_counters", [] { g_counters.clear(); });
+
+  // iteration order of a libstdc++ std::unordered_map<int, ...> built from an
+  // initializer list in `keys` order (DecisionTestUtils.cpp:16-43 iterates one)
+  m.def("cxx_unordered_int_order", [](std::vector<int> keys) {
+    std::vector<std::pair<const int, int>> init;
+    for (int k : keys) init.emplace_back(k, 0);
+    std::unordered_map<int, int> um(init.begin(), init.end());
+    std::vector<int> out;
+    for (const auto& kv : um) out.push_back(kv.first);
+    return out;
+  });
+
+  py::class_<OLink, std::shared_ptr<OLink>>(m, "Link")
+      .def(py::init<std::string, std::string, std::string, std::string, std::string>())
+      .def("key", [](const OLink& l) { return linkKey(l); })
+      .def("getMetricFromNode", &OLink::metric)
+      .def("getOtherNodeName", &OLink::other)
+      .def("getIfaceFromNode", &OLink::iface)
+      .def("isUp", &OLink::isUp)
+      .def("__eq__", [](const OLink& a, const OLink& b) { return a == b; })
+      .def("__hash__", [](const OLink& l) { return l.hash; });
+
+  py::class_<Graph>(m, "LinkState")
+      .def(py::init<std::string>())
+      .def("getArea", &Graph::area)
+      .def("updateAdjacencyDatabase",
+           [](Graph& g, py::handle db, uint64_t up, uint64_t down) {
+             return chg(g.update(toAdjDb(db), up, down));
+           },
+           py::arg("adjDb"), py::arg("holdUpTtl") = 0, py::arg("holdDownTtl") = 0)
+      .def("deleteAdjacencyDatabase", [](Graph& g, const std::string& n) { return chg(g.remove(n)); })
+      .def("decrementHolds", [](Graph& g) { return chg(g.decrementHolds()); })
+      .def("hasHolds", &Graph::hasHolds)
+      .def("hasNode", &Graph::hasNode)
+      .def("numLinks", &Graph::numLinks)
+      .def("isNodeOverloaded", &Graph::overloaded)
+      .def("linksFromNode",
+           [](const Graph& g, const std::string& n) {
+             py::list out;
+             for (const auto& l : g.links(n)) out.append(py::cast(l));
+             return out;
+           })
+      .def("getSpfResult",
+           [](const Graph& g, const std::string& n, bool useMetric) {
+             py::dict out;
+             for (const auto& [name, r] : g.getSpf(n, useMetric)) {
+               py::list paths;
+               for (const auto& [l, prev] : r.paths) paths.append(py::make_tuple(linkKey(*l), prev));
+               py::set nhs;
+               for (const auto& h : r.nhs) nhs.add(py::str(h));
+               out[py::str(name)] = py::make_tuple(r.metric, py::frozenset(nhs), paths);
+             }
+             return out;
+           },
+           py::arg("node"), py::arg("useLinkMetric") = true)
+      .def("runSpfTimed",
+           [](const Graph& g, std::vector<std::string> srcs, bool useMetric) {
+             // the cpu_baseline leg: uncached runSpf per source
+             const auto t0 = std::chrono::steady_clock::now();
+             size_t reached = 0;
+             for (const auto& s : srcs) reached += g.runSpf(s, useMetric, {}).size();
+             const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+             return py::make_tuple(sec, reached);
+           })
+      .def("getKthPaths",
+           [](const Graph& g, const std::string& s, const std::string& d, size_t k) {
+             py::list out;
+             for (const auto& p : g.kth(s, d, k)) {
+               py::list pl;
+               for (const auto& l : p) pl.append(py::cast(l));
+               out.append(pl);
+             }
+             return out;
+           })
+      .def("getMetricFromAToB", &Graph::metricAB, py::arg("a"), py::arg("b"),
+           py::arg("useLinkMetric") = true)
+      .def("getHopsFromAToB", [](const Graph& g, const std::string& a, const std::string& b) {
+        return g.metricAB(a, b, false);
+      })
+      .def("getMaxHopsToNode", &Graph::maxHops)
+      .def_static("pathAInPathB", [](py::list a, py::list b) {
+        Path pa, pb;
+        for (auto x : a) pa.push_back(x.cast<LinkP>());
+        for (auto x : b) pb.push_back(x.cast<LinkP>());
+        return pathAInPathB(pa, pb);
+      });
+
+  py::class_<AreaHolder>(m, "AreaLinkStates")
+      .def(py::init<>())
+      .def("add",
+           [](AreaHolder& h, const std::string& area) -> Graph& {
+             return h.map.emplace(area, Graph(area)).first->second;
+           },
+           py::return_value_policy::reference_internal)
+      .def("__getitem__", [](AreaHolder& h, const std::string& a) -> Graph& { return h.map.at(a); },
+           py::return_value_policy::reference_internal);
+
+  py::class_<Prefixes>(m, "PrefixState")
+      .def(py::init<>())
+      .def("updatePrefixDatabase", [](Prefixes& p, py::handle db) {
+        py::set out;
+        for (const auto& x : p.update(toPrefixDb(db))) out.add(prefixKey(x));
+        return out;
+      });
+
+  py::class_<Solver>(m, "SpfSolver")
+      .def(py::init([](std::string /*me*/, bool v4, bool lfa, bool /*ofib*/, bool dry, bool igp) {
+             return std::make_unique<Solver>(v4, lfa, dry, igp);
+           }),
+           py::arg("myNodeName"), py::arg("enableV4"), py::arg("computeLfaPaths"),
+           py::arg("enableOrderedFib") = false, py::arg("bgpDryRun") = false,
+           py::arg("bgpUseIgpMetric") = false)
+      .def("setStaticMplsRoute",
+           [](Solver& s, int32_t label, py::list nhs) {
+             std::vector<NextHopThrift> v;
+             for (auto nh : nhs) v.push_back(toNextHop(nh));
+             s.staticMpls[label] = v;
+           })
+      .def("buildRouteDb",
+           [](Solver& s, const std::string& me, const AreaHolder& areas,
+              const Prefixes& ps) -> py::object {
+             auto db = s.build(me, areas.map, ps);
+             if (!db) return py::none();
+             py::dict uni, mpls;
+             for (const auto& [p, e] : db->unicast) {
+               py::dict d;
+               d["nexthops"] = nextHopSet(e.nhs);
+               d["bestArea"] = e.bestArea;
+               d["doNotInstall"] = e.dni;
+               d["bestNexthop"] = e.bestNh ? py::object(nextHopKey(*e.bestNh)) : py::none();
+               d["bestPrefixEntry"] = prefixEntryKey(e.best);
+               uni[prefixKey(p)] = d;
+             }
+             for (const auto& [l, s2] : db->mpls) mpls[py::int_(l)] = nextHopSet(s2);
+             py::dict out;
+             out["unicast"] = uni;
+             out["mpls"] = mpls;
+             return out;
+           });
+}

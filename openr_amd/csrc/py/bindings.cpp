@@ -5,6 +5,8 @@
 // and the reference's known answers.
 
 #include <pybind11/pybind11.h>
+
+#include <chrono>
 #include <pybind11/stl.h>
 
 #include "../host/LinkState.h"
@@ -239,6 +241,20 @@ PYBIND11_MODULE(_openr_spf, m) {
                return py::none();
              }
              return routeDbToPy(*db);
+           })
+      .def("buildRouteDbTimed",
+           [](SpfSolver& s, const std::string& node, const AreaMapHolder& areas,
+              const PrefixState& ps) {
+             // RouteDb build timed in C++ (no Python conversion of the routes)
+             const auto t0 = std::chrono::steady_clock::now();
+             auto db = s.buildRouteDb(node, areas.map, ps);
+             const double us = std::chrono::duration<double, std::micro>(
+                                   std::chrono::steady_clock::now() - t0)
+                                   .count();
+             if (!db) {
+               return py::make_tuple((long)-1, (long)-1, us);
+             }
+             return py::make_tuple((long)db->unicastEntries.size(), (long)db->mplsEntries.size(), us);
            })
       .def("staticRoutesUpdated", &SpfSolver::staticRoutesUpdated)
       .def("pushRoutesDeltaUpdates",

@@ -139,10 +139,14 @@ int spf_query_nexthops(spf_query* q, uint32_t i, uint64_t* out /*[V*W]*/);
  * reference's DijkstraQ extracts nodes; UINT32_MAX = not reached. */
 int spf_query_order(spf_query* q, uint32_t i, uint32_t* out /*[V]*/);
 /* Device pointers of the result rows (for RCCL gathers): dist rows are
- * uint32 (fast kernels) or uint64 (exact kernel) of V entries per query. */
+ * uint32 (fast kernels) or uint64 (exact kernel), spf_query_row_stride
+ * elements apart (V entries used per row).  Next-hop rows are packed:
+ * query i starts at word sum_{j<i} V * nh_words(j). */
 int spf_query_device_rows(
     spf_query* q, void** dist_rows, uint32_t* dist_elem_bytes,
     void** nh_rows, uint64_t* nh_total_words);
+/* Elements between consecutive distance rows (>= V). */
+uint32_t spf_query_row_stride(const spf_query* q);
 
 #ifdef __cplusplus
 }

@@ -48,6 +48,7 @@ EXPORTED_SYMBOLS = (
     "spf_query_nexthops",
     "spf_query_order",
     "spf_query_device_rows",
+    "spf_query_row_stride",
 )
 
 
@@ -121,6 +122,7 @@ def load():
         "spf_query_nh_words": (C.c_int, [vp, u32]),
         "spf_query_nexthops": (C.c_int, [vp, u32, pu64]),
         "spf_query_order": (C.c_int, [vp, u32, pu32]),
+        "spf_query_row_stride": (u32, [vp]),
         "spf_query_device_rows": (
             C.c_int,
             [vp, C.POINTER(vp), pu32, C.POINTER(vp), pu64],

@@ -187,6 +187,7 @@ struct SsspArgs {
   uint64_t* nh_out;
   uint32_t* gscratch; // GMEM: per-workgroup node queue (V u32)
   uint32_t V;
+  uint32_t Vp; // row stride of dist_out
   uint32_t nbw;
   uint32_t nq;
   uint32_t G;       // lanes per node (power of two, <= 64)
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
   for (uint32_t q = blockIdx.x; q < a.nq; q += gridDim.x) {
     const uint32_t src = a.src[q];
     if constexpr (GMEM) {
-      dist = a.dist_out + (size_t)q * V;
+      dist = a.dist_out + (size_t)q * a.Vp;
     }
     uint32_t nign = 0;
     const uint32_t* ignp = ignl;
@@ -394,12 +395,261 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
     }
 
     if constexpr (!GMEM) {
-      uint32_t* out = a.dist_out + (size_t)q * V;
+      uint32_t* out = a.dist_out + (size_t)q * a.Vp;
       for (uint32_t v = tid; v < V; v += kBlock) {
         out[v] = dist[v];
       }
     }
     __syncthreads();
+  }
+}
+
+// ------------------------------------------- uniform-metric distance kernel
+//
+// Every usable link has the same metric c (the fabric and grid benchmarks,
+// and every useLinkMetric=false run): distances are c * BFS levels.  One
+// workgroup per source, direction-optimizing level-synchronous BFS in LDS:
+// top-down (frontier rows pushed, first writer wins with an identical value)
+// while the frontier is small, bottom-up (each unvisited node scans its own
+// row and stops at the first transit frontier neighbour) once the frontier's
+// edges outnumber the unvisited edges / 14.  Overloaded nodes are reached
+// but never expanded, exactly as the reference (LinkState.cpp:829-836).
+
+struct BfsArgs {
+  const uint32_t* row;
+  const uint32_t* col;
+  const uint32_t* trbits;
+  const uint32_t* src;
+  uint32_t* dist_out;
+  uint32_t* gscratch;
+  uint32_t V;
+  uint32_t Vp; // row stride of dist_out
+  uint32_t nbw;
+  uint32_t nq;
+  uint32_t E;
+  uint32_t G;
+  uint32_t scale; // the uniform metric c
+};
+
+// next-frontier bitmap -> queue; cur = next; next = 0; returns the queue
+// length, *degsum = sum of out-degrees of the queued nodes.
+template <typename QT>
+__device__ __forceinline__ uint32_t compact_frontier(
+    uint32_t* nxt, uint32_t* cur, uint32_t nbw, QT* queue, uint32_t* scan,
+    const uint32_t* row, uint32_t* degsum) {
+  const uint32_t chunk = (nbw + kBlock - 1) / kBlock;
+  const uint32_t w0 = min(threadIdx.x * chunk, nbw);
+  const uint32_t w1 = min(w0 + chunk, nbw);
+  uint32_t cnt = 0;
+  for (uint32_t w = w0; w < w1; ++w) {
+    cnt += __popc(nxt[w]);
+  }
+  uint32_t total;
+  uint32_t off = block_excl_scan(cnt, scan, &total);
+  uint32_t deg = 0;
+  for (uint32_t w = w0; w < w1; ++w) {
+    uint32_t b = nxt[w];
+    cur[w] = b;
+    nxt[w] = 0;
+    while (b) {
+      const uint32_t k = __ffs(b) - 1;
+      b &= b - 1;
+      const uint32_t v = w * 32 + k;
+      queue[off++] = (QT)v;
+      deg += row[v + 1] - row[v];
+    }
+  }
+  __syncthreads();
+  uint32_t dtot;
+  block_excl_scan(deg, scan, &dtot);
+  *degsum = dtot;
+  return total;
+}
+
+template <bool GMEM>
+__global__ __launch_bounds__(kBlock) void spf_bfs_kernel(BfsArgs a) {
+  extern __shared__ __align__(16) uint32_t smem[];
+  using QT = typename std::conditional<GMEM, uint32_t, uint16_t>::type;
+  const uint32_t V = a.V, nbw = a.nbw, G = a.G;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lg = tid & (G - 1);
+  const uint32_t grp = tid / G, ngrp = kBlock / G;
+
+  uint32_t* cur = smem;
+  uint32_t* nxt = cur + nbw;
+  uint32_t* tr = nxt + nbw;
+  uint32_t* ctl = tr + nbw;
+  QT* queue;
+  uint32_t* dist;
+  if constexpr (GMEM) {
+    queue = a.gscratch + (size_t)blockIdx.x * V;
+    dist = nullptr;
+  } else {
+    queue = reinterpret_cast<QT*>(ctl + kCtlWords);
+    dist = reinterpret_cast<uint32_t*>(queue + ((V + 1) & ~1u));
+  }
+  for (uint32_t i = tid; i < nbw; i += kBlock) {
+    cur[i] = 0;
+    nxt[i] = 0;
+    tr[i] = a.trbits[i];
+  }
+
+  for (uint32_t q = blockIdx.x; q < a.nq; q += gridDim.x) {
+    const uint32_t src = a.src[q];
+    if constexpr (GMEM) {
+      dist = a.dist_out + (size_t)q * a.Vp;
+    }
+    for (uint32_t v = tid; v < V; v += kBlock) {
+      dist[v] = kInf32;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      dist[src] = 0;
+      queue[0] = (QT)src;
+      cur[src >> 5] |= 1u << (src & 31);
+    }
+    __syncthreads();
+    uint32_t qlen = 1;
+    uint64_t frontierEdges = a.row[src + 1] - a.row[src];
+    uint64_t unvisitedEdges = a.E - frontierEdges;
+    uint32_t level = 0;
+
+    while (qlen) {
+      const uint32_t L1 = level + 1;
+      const bool bottomUp = frontierEdges * 14 > unvisitedEdges;
+      if (!bottomUp) {
+        for (uint32_t i = grp; i < qlen; i += ngrp) {
+          const uint32_t u = queue[i];
+          if (u != src && !((tr[u >> 5] >> (u & 31)) & 1u)) {
+            continue;
+          }
+          const uint32_t end = a.row[u + 1];
+          for (uint32_t e = a.row[u] + lg; e < end; e += G) {
+            const uint32_t v = a.col[e];
+            if (dist[v] == kInf32) {
+              dist[v] = L1; // every writer stores the same level
+              atomicOr(&nxt[v >> 5], 1u << (v & 31));
+            }
+          }
+        }
+      } else {
+        for (uint32_t v = tid; v < V; v += kBlock) {
+          if (dist[v] != kInf32) {
+            continue;
+          }
+          const uint32_t end = a.row[v + 1];
+          for (uint32_t e = a.row[v]; e < end; ++e) {
+            const uint32_t u = a.col[e];
+            const uint32_t ub = 1u << (u & 31);
+            if ((cur[u >> 5] & ub) &&
+                (u == src || (tr[u >> 5] & ub))) {
+              dist[v] = L1;
+              atomicOr(&nxt[v >> 5], 1u << (v & 31));
+              break;
+            }
+          }
+        }
+      }
+      __syncthreads();
+      uint32_t degsum;
+      qlen = compact_frontier<QT>(nxt, cur, nbw, queue, ctl + 1, a.row, &degsum);
+      __syncthreads();
+      frontierEdges = degsum;
+      unvisitedEdges = unvisitedEdges > degsum ? unvisitedEdges - degsum : 0;
+      level = L1;
+    }
+
+    if constexpr (!GMEM) {
+      uint32_t* out = a.dist_out + (size_t)q * a.Vp;
+      for (uint32_t v = tid; v < V; v += kBlock) {
+        const uint32_t d = dist[v];
+        out[v] = d == kInf32 ? kInf32 : d * a.scale;
+      }
+    } else if (a.scale != 1) {
+      for (uint32_t v = tid; v < V; v += kBlock) {
+        const uint32_t d = dist[v];
+        dist[v] = d == kInf32 ? kInf32 : d * a.scale;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------- next hops from distance rows
+//
+// For positive metrics the reference's next-hop union (LinkState.cpp:855-871)
+// equals a first-hop test on distance rows:
+//   f in NH_s(v)  <=>  f is a distinct neighbour of s, (f transit or v == f)
+//                      and w(s,f) + D_f[v] == D_s[v]
+// (w(s,f) = cheapest usable s->f link; D_f is f's own SPF, in which f — the
+// source — may transit).  When a batch holds the distance rows of every
+// neighbour of its sources (all-sources, LFA neighbourhoods) the masks are
+// one streaming pass over those rows: coalesced 16-byte loads, no gathers,
+// no atomics.  Grid is chunk-major so that blocks sharing an XCD (b, b+8, ...)
+// work on neighbouring sources of the same vertex chunk and share the
+// neighbours' row chunks in that XCD's L2.
+
+struct NhRowsArgs {
+  const uint32_t* nbr_off;
+  const uint32_t* nbrs;
+  const uint32_t* nbr_w; // cheapest metric to that neighbour
+  const uint32_t* trbits;
+  const uint32_t* src;
+  const int32_t* row_of; // node -> batch row holding its distances
+  const uint32_t* dist;  // [nq][Vp]
+  const uint64_t* nh_off;
+  const uint32_t* nh_w;
+  uint64_t* nh_out;
+  uint32_t V;
+  uint32_t Vp;
+  uint32_t nq;
+  uint32_t nchunks;
+  uint32_t unit;
+};
+
+constexpr uint32_t kNhThreads = 256;
+constexpr uint32_t kNhPerThread = 4;
+constexpr uint32_t kNhChunk = kNhThreads * kNhPerThread;
+
+__global__ __launch_bounds__(kNhThreads) void spf_nh_rows_kernel(NhRowsArgs a) {
+  const uint32_t chunk = blockIdx.x / a.nq;
+  const uint32_t q = blockIdx.x - chunk * a.nq;
+  const uint32_t s = a.src[q];
+  const uint32_t v0 = chunk * kNhChunk + threadIdx.x * kNhPerThread;
+  if (v0 >= a.V) {
+    return;
+  }
+  const uint32_t Wm = a.nh_w[q];
+  uint64_t* nhrow = a.nh_out + a.nh_off[q];
+  const uint4 ds = *reinterpret_cast<const uint4*>(a.dist + (size_t)q * a.Vp + v0);
+  const uint32_t dsv[4] = {ds.x, ds.y, ds.z, ds.w};
+  const uint32_t beg = a.nbr_off[s], n = a.nbr_off[s + 1] - beg;
+  for (uint32_t w = 0; w < Wm; ++w) {
+    uint64_t acc[4] = {0, 0, 0, 0};
+    const uint32_t jend = min(n, (w + 1) * 64);
+    for (uint32_t j = w * 64; j < jend; ++j) {
+      const uint32_t f = a.nbrs[beg + j];
+      const uint64_t wf = a.unit ? 1ull : (uint64_t)a.nbr_w[beg + j];
+      const bool tf = (a.trbits[f >> 5] >> (f & 31)) & 1u;
+      const int32_t r = a.row_of[f];
+      const uint4 df = *reinterpret_cast<const uint4*>(a.dist + (size_t)r * a.Vp + v0);
+      const uint32_t dfv[4] = {df.x, df.y, df.z, df.w};
+      const uint64_t bit = 1ull << (j & 63);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t v = v0 + k;
+        if (dsv[k] != kInf32 && dfv[k] != kInf32 && wf + dfv[k] == (uint64_t)dsv[k] &&
+            (tf || v == f)) {
+          acc[k] |= bit;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (v0 + k < a.V) {
+        nhrow[(size_t)(v0 + k) * Wm + w] = acc[k];
+      }
+    }
   }
 }
 
@@ -570,25 +820,32 @@ struct spf_graph {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   uint32_t V = 0, E = 0, L = 0, nbw = 0;
-  bool exact = false;
+  bool exact = false;     // metric runs need the exact kernel
+  uint32_t uniform = 0;   // every metric equals this value (0 = mixed)
   uint32_t G = 8;
   int num_cus = 256;
   // host copies
-  std::vector<uint32_t> row, col, link, rev, slot, nbr_off, nbrs, trbits;
+  std::vector<uint32_t> row, col, link, rev, slot, nbr_off, nbrs, nbr_w, trbits;
   std::vector<uint64_t> w64;
   // device copies
   uint32_t *d_row = nullptr, *d_col = nullptr, *d_wout = nullptr,
            *d_win = nullptr, *d_link = nullptr, *d_rev = nullptr,
-           *d_slot = nullptr, *d_tr = nullptr;
+           *d_slot = nullptr, *d_tr = nullptr, *d_nbr_off = nullptr,
+           *d_nbrs = nullptr, *d_nbr_w = nullptr;
   uint64_t* d_w64 = nullptr;
 };
+
+// How a batch is computed.
+enum class DistPlan { SsspLds, SsspGmem, BfsLds, BfsGmem, Exact };
+enum class NhPlan { None, Inline, Rows };
 
 struct spf_query {
   spf_graph* g = nullptr;
   uint32_t nq = 0, flags = 0;
-  int kind = 0; // 0 lds, 1 gmem, 2 exact
+  DistPlan dist = DistPlan::SsspLds;
+  NhPlan nh = NhPlan::None;
   int wmax = 0;
-  uint32_t ign_cap = 0, grid = 0;
+  uint32_t ign_cap = 0, grid = 0, Vp = 0;
   size_t lds_bytes = 0;
   bool has_ign = false;
   std::vector<uint64_t> nh_off;
@@ -596,6 +853,7 @@ struct spf_query {
   uint64_t nh_total = 0;
   uint32_t *d_src = nullptr, *d_ign_off = nullptr, *d_ign = nullptr,
            *d_nh_w = nullptr, *d_order = nullptr, *d_scratch = nullptr;
+  int32_t* d_row_of = nullptr;
   uint64_t* d_nh_off = nullptr;
   void* d_dist = nullptr;
   uint64_t* d_nh = nullptr;
@@ -616,14 +874,6 @@ int dev_upload(T** dst, const T* src, size_t n) {
   return SPF_OK;
 }
 
-#define SPF_TRY(expr)   \
-  do {                  \
-    int s_ = (expr);    \
-    if (s_ != SPF_OK) { \
-      return s_;        \
-    }                   \
-  } while (0)
-
 void free_graph(spf_graph* g) {
   if (!g) {
     return;
@@ -632,7 +882,8 @@ void free_graph(spf_graph* g) {
   for (void* p :
        {(void*)g->d_row, (void*)g->d_col, (void*)g->d_wout, (void*)g->d_win,
         (void*)g->d_link, (void*)g->d_rev, (void*)g->d_slot, (void*)g->d_tr,
-        (void*)g->d_w64}) {
+        (void*)g->d_w64, (void*)g->d_nbr_off, (void*)g->d_nbrs,
+        (void*)g->d_nbr_w}) {
     if (p) {
       (void)hipFree(p);
     }
@@ -651,7 +902,7 @@ void free_query(spf_query* q) {
   for (void* p :
        {(void*)q->d_src, (void*)q->d_ign_off, (void*)q->d_ign,
         (void*)q->d_nh_w, (void*)q->d_order, (void*)q->d_scratch,
-        (void*)q->d_nh_off, q->d_dist, (void*)q->d_nh}) {
+        (void*)q->d_nh_off, q->d_dist, (void*)q->d_nh, (void*)q->d_row_of}) {
     if (p) {
       (void)hipFree(p);
     }
@@ -665,9 +916,9 @@ void free_query(spf_query* q) {
   delete q;
 }
 
-// fast-path weights and exactness from the 64-bit metrics
+// fast-path weights, exactness, uniformity and per-neighbour cheapest metric
 int upload_weights(spf_graph* g) {
-  const uint32_t E = g->E;
+  const uint32_t E = g->E, V = g->V;
   uint64_t maxw = 0;
   bool exact = false;
   for (uint32_t e = 0; e < E; ++e) {
@@ -677,11 +928,20 @@ int upload_weights(spf_graph* g) {
     }
     maxw = std::max(maxw, m);
   }
-  if (!exact && g->V > 1 && maxw > 0 &&
-      (unsigned __int128)maxw * (g->V - 1) >= 0xFFFFFFFFull) {
+  if (!exact && V > 1 && maxw > 0 &&
+      (unsigned __int128)maxw * (V - 1) >= 0xFFFFFFFFull) {
     exact = true;
   }
   g->exact = exact;
+  g->uniform = 0;
+  if (!exact && E) {
+    const uint64_t c = g->w64[0];
+    bool same = true;
+    for (uint32_t e = 1; e < E && same; ++e) {
+      same = g->w64[e] == c;
+    }
+    g->uniform = same ? (uint32_t)c : 0;
+  }
   std::vector<uint32_t> wout(E), win(E);
   for (uint32_t e = 0; e < E; ++e) {
     wout[e] = (uint32_t)std::min<uint64_t>(g->w64[e], 0xFFFFFFFFull);
@@ -689,18 +949,36 @@ int upload_weights(spf_graph* g) {
   for (uint32_t e = 0; e < E; ++e) {
     win[e] = wout[g->rev[e]];
   }
+  // cheapest usable link to each distinct neighbour (parallel links)
+  g->nbr_w.assign(g->nbrs.size(), 0xFFFFFFFFu);
+  for (uint32_t u = 0; u < V; ++u) {
+    for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
+      uint32_t& w = g->nbr_w[g->nbr_off[u] + g->slot[e]];
+      w = std::min(w, wout[e]);
+    }
+  }
   if (E) {
     if (!g->d_wout) {
       HIP_TRY(hipMalloc((void**)&g->d_wout, E * 4));
       HIP_TRY(hipMalloc((void**)&g->d_win, E * 4));
       HIP_TRY(hipMalloc((void**)&g->d_w64, E * 8));
+      HIP_TRY(hipMalloc((void**)&g->d_nbr_w, g->nbr_w.size() * 4));
     }
     HIP_TRY(hipMemcpy(g->d_wout, wout.data(), E * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(g->d_win, win.data(), E * 4, hipMemcpyHostToDevice));
-    HIP_TRY(
-        hipMemcpy(g->d_w64, g->w64.data(), E * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(g->d_w64, g->w64.data(), E * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(g->d_nbr_w, g->nbr_w.data(), g->nbr_w.size() * 4,
+                      hipMemcpyHostToDevice));
   }
   return SPF_OK;
+}
+
+inline size_t lds_ctl_bytes(const spf_graph* g, uint32_t ign_cap) {
+  return (3 * (size_t)g->nbw + kCtlWords + ign_cap) * sizeof(uint32_t);
+}
+
+inline size_t lds_state_bytes(uint32_t V) {
+  return (size_t)((V + 1) & ~1u) * 2 + (size_t)V * 4; // u16 queue + u32 dist
 }
 
 } // namespace
@@ -758,15 +1036,15 @@ int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
   for (uint32_t u = 0; u < V; ++u) {
     for (uint32_t e = desc->row_ptr[u]; e < desc->row_ptr[u + 1]; ++e) {
       const uint32_t v = desc->col[e], r = desc->rev[e];
-      if (v >= V || r >= E || desc->rev[r] != e || desc->col[r] != u ||
-          desc->link_id[e] >= desc->num_links ||
+      if (v >= V || v == u || r >= E || desc->rev[r] != e ||
+          desc->col[r] != u || desc->link_id[e] >= desc->num_links ||
           desc->link_id[r] != desc->link_id[e]) {
         return fail(SPF_E_INVALID, "inconsistent half-edge at " +
                                        std::to_string(e));
       }
     }
   }
-  int ndev = spf_device_count();
+  const int ndev = spf_device_count();
   if (ndev <= 0) {
     return fail(SPF_E_DEVICE, "no HIP device visible");
   }
@@ -849,6 +1127,8 @@ int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
       (s = dev_upload(&g->d_rev, g->rev.data(), E)) ||
       (s = dev_upload(&g->d_slot, g->slot.data(), E)) ||
       (s = dev_upload(&g->d_tr, g->trbits.data(), g->trbits.size())) ||
+      (s = dev_upload(&g->d_nbr_off, g->nbr_off.data(), V + 1)) ||
+      (s = dev_upload(&g->d_nbrs, g->nbrs.data(), g->nbrs.size())) ||
       (s = upload_weights(g))) {
     return bail(s);
   }
@@ -942,9 +1222,9 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       return fail(SPF_E_INVALID, "source out of range");
     }
   }
-  const bool has_ign = desc->ignore_offsets != nullptr;
+  bool has_ign = false;
   uint32_t max_ign = 0;
-  if (has_ign) {
+  if (desc->ignore_offsets) {
     if (desc->ignore_offsets[0] != 0) {
       return fail(SPF_E_INVALID, "ignore_offsets[0] != 0");
     }
@@ -961,6 +1241,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       }
       max_ign = std::max(max_ign, hi - lo);
     }
+    has_ign = max_ign > 0;
   }
 
   spf_query* q = new spf_query();
@@ -968,6 +1249,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
   q->nq = nq;
   q->flags = desc->flags;
   q->has_ign = has_ign;
+  q->Vp = (V + 15) & ~15u;
   auto bail = [&](int s) {
     free_query(q);
     return s;
@@ -994,25 +1276,50 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     q->nh_total = off;
   }
 
-  // kernel choice
-  if ((g->exact && !unit) || want_order || maxw > 16) {
-    q->kind = 2;
+  // ---- plan: which kernels compute this batch
+  std::vector<int32_t> row_of;
+  const bool exact = (g->exact && !unit) || want_order;
+  const bool uniform = unit || g->uniform != 0;
+  bool rows_ok = false;
+  if (want_nh && !exact && !has_ign) {
+    // next hops from distance rows need every neighbour's row in the batch
+    row_of.assign(V, -1);
+    for (uint32_t i = nq; i-- > 0;) {
+      row_of[desc->sources[i]] = (int32_t)i;
+    }
+    rows_ok = true;
+    for (uint32_t i = 0; i < nq && rows_ok; ++i) {
+      const uint32_t s = desc->sources[i];
+      for (uint32_t k = g->nbr_off[s]; k < g->nbr_off[s + 1]; ++k) {
+        if (row_of[g->nbrs[k]] < 0) {
+          rows_ok = false;
+          break;
+        }
+      }
+    }
+    if (!rows_ok) {
+      row_of.clear();
+    }
+  }
+  if (exact || (want_nh && !rows_ok && maxw > 16)) {
+    q->dist = DistPlan::Exact;
+    q->nh = want_nh ? NhPlan::Inline : NhPlan::None;
   } else {
-    q->wmax = !want_nh ? 0 : (maxw <= 1 ? 1 : (maxw <= 4 ? 4 : 16));
+    q->nh = !want_nh ? NhPlan::None : (rows_ok ? NhPlan::Rows : NhPlan::Inline);
+    const bool bfs = uniform && !has_ign && q->nh != NhPlan::Inline;
+    q->wmax = q->nh != NhPlan::Inline ? 0 : (maxw <= 1 ? 1 : (maxw <= 4 ? 4 : 16));
     q->ign_cap = has_ign ? std::min(max_ign, kIgnLdsMax) : 0;
-    const size_t ctl =
-        (3 * (size_t)g->nbw + kCtlWords + q->ign_cap) * sizeof(uint32_t);
-    const size_t lds =
-        ctl + (size_t)((V + 1) & ~1u) * 2 + (size_t)V * 4; // u16 queue + dist
+    const size_t ctl = lds_ctl_bytes(g, q->ign_cap);
+    const size_t lds = ctl + lds_state_bytes(V);
     if (V <= 65535 && lds <= kLdsLimit) {
-      q->kind = 0;
+      q->dist = bfs ? DistPlan::BfsLds : DistPlan::SsspLds;
       q->lds_bytes = lds;
       const uint32_t per_cu =
           std::max<uint32_t>(1, std::min<uint32_t>(4, kLdsLimit / lds));
       q->grid = std::min<uint32_t>(std::max<uint32_t>(nq, 1),
                                    (uint32_t)g->num_cus * per_cu);
     } else if (ctl <= kLdsLimit) {
-      q->kind = 1;
+      q->dist = bfs ? DistPlan::BfsGmem : DistPlan::SsspGmem;
       q->lds_bytes = ctl;
       q->grid = std::min<uint32_t>(std::max<uint32_t>(nq, 1),
                                    (uint32_t)g->num_cus * 2);
@@ -1045,17 +1352,20 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       return bail(fail(SPF_E_NOMEM, "next-hop rows"));
     }
   }
-  const size_t elem = q->kind == 2 ? 8 : 4;
-  if ((size_t)nq * V &&
-      hipMalloc(&q->d_dist, (size_t)nq * V * elem) != hipSuccess) {
+  if (!row_of.empty() && (s = dev_upload(&q->d_row_of, row_of.data(), V))) {
+    return bail(s);
+  }
+  const bool ex = q->dist == DistPlan::Exact;
+  const size_t dist_bytes = ex ? (size_t)nq * V * 8 : (size_t)nq * q->Vp * 4;
+  if (dist_bytes && hipMalloc(&q->d_dist, dist_bytes) != hipSuccess) {
     return bail(fail(SPF_E_NOMEM, "distance rows"));
   }
-  if (q->kind == 1 &&
+  if ((q->dist == DistPlan::SsspGmem || q->dist == DistPlan::BfsGmem) &&
       hipMalloc((void**)&q->d_scratch, (size_t)q->grid * V * 4) !=
           hipSuccess) {
     return bail(fail(SPF_E_NOMEM, "queue scratch"));
   }
-  if (q->kind == 2 && (size_t)nq * V) {
+  if (ex && (size_t)nq * V) {
     if (hipMalloc((void**)&q->d_scratch, (size_t)nq * V * 8) != hipSuccess ||
         hipMalloc((void**)&q->d_order, (size_t)nq * V * 4) != hipSuccess) {
       return bail(fail(SPF_E_NOMEM, "exact-kernel scratch"));
@@ -1099,6 +1409,7 @@ int launch_sssp(spf_query* q) {
   a.nh_out = q->d_nh;
   a.gscratch = q->d_scratch;
   a.V = g->V;
+  a.Vp = q->Vp;
   a.nbw = g->nbw;
   a.nq = q->nq;
   a.G = g->G;
@@ -1129,6 +1440,62 @@ int dispatch_flags(spf_query* q, bool unit, bool ign, bool gmem) {
   }
   return gmem ? launch_sssp<WMAX, false, false, true>(q)
               : launch_sssp<WMAX, false, false, false>(q);
+}
+
+int launch_bfs(spf_query* q, bool unit) {
+  spf_graph* g = q->g;
+  BfsArgs a;
+  a.row = g->d_row;
+  a.col = g->d_col;
+  a.trbits = g->d_tr;
+  a.src = q->d_src;
+  a.dist_out = (uint32_t*)q->d_dist;
+  a.gscratch = q->d_scratch;
+  a.V = g->V;
+  a.Vp = q->Vp;
+  a.nbw = g->nbw;
+  a.nq = q->nq;
+  a.E = g->E;
+  a.G = g->G;
+  a.scale = unit ? 1u : g->uniform;
+  const bool gmem = q->dist == DistPlan::BfsGmem;
+  auto kern = gmem ? spf_bfs_kernel<true> : spf_bfs_kernel<false>;
+  HIP_TRY(hipFuncSetAttribute(
+      (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (int)q->lds_bytes));
+  hipLaunchKernelGGL(
+      kern, dim3(q->grid), dim3(kBlock), q->lds_bytes, g->stream, a);
+  HIP_TRY(hipGetLastError());
+  return SPF_OK;
+}
+
+int launch_nh_rows(spf_query* q, bool unit) {
+  spf_graph* g = q->g;
+  NhRowsArgs a;
+  a.nbr_off = g->d_nbr_off;
+  a.nbrs = g->d_nbrs;
+  a.nbr_w = g->d_nbr_w;
+  a.trbits = g->d_tr;
+  a.src = q->d_src;
+  a.row_of = q->d_row_of;
+  a.dist = (const uint32_t*)q->d_dist;
+  a.nh_off = q->d_nh_off;
+  a.nh_w = q->d_nh_w;
+  a.nh_out = q->d_nh;
+  a.V = g->V;
+  a.Vp = q->Vp;
+  a.nq = q->nq;
+  a.nchunks = (g->V + kNhChunk - 1) / kNhChunk;
+  a.unit = unit ? 1 : 0;
+  const uint64_t blocks = (uint64_t)a.nchunks * q->nq;
+  if (blocks > 0x7FFFFFFFull) {
+    return fail(SPF_E_UNSUPPORTED, "batch too large for the next-hop pass");
+  }
+  hipLaunchKernelGGL(
+      spf_nh_rows_kernel, dim3((uint32_t)blocks), dim3(kNhThreads), 0,
+      g->stream, a);
+  HIP_TRY(hipGetLastError());
+  return SPF_OK;
 }
 
 int launch_exact(spf_query* q) {
@@ -1164,6 +1531,44 @@ int launch_exact(spf_query* q) {
   return SPF_OK;
 }
 
+int run_plan(spf_query* q) {
+  const bool unit = q->flags & SPF_F_UNIT_METRIC;
+  switch (q->dist) {
+  case DistPlan::Exact:
+    return launch_exact(q);
+  case DistPlan::BfsLds:
+  case DistPlan::BfsGmem: {
+    int s = launch_bfs(q, unit);
+    if (s == SPF_OK && q->nh == NhPlan::Rows) {
+      s = launch_nh_rows(q, unit);
+    }
+    return s;
+  }
+  default: {
+    const bool gmem = q->dist == DistPlan::SsspGmem;
+    int s = SPF_OK;
+    switch (q->wmax) {
+    case 0:
+      s = dispatch_flags<0>(q, unit, q->has_ign, gmem);
+      break;
+    case 1:
+      s = dispatch_flags<1>(q, unit, q->has_ign, gmem);
+      break;
+    case 4:
+      s = dispatch_flags<4>(q, unit, q->has_ign, gmem);
+      break;
+    default:
+      s = dispatch_flags<16>(q, unit, q->has_ign, gmem);
+      break;
+    }
+    if (s == SPF_OK && q->nh == NhPlan::Rows) {
+      s = launch_nh_rows(q, unit);
+    }
+    return s;
+  }
+  }
+}
+
 } // namespace
 
 extern "C" {
@@ -1177,26 +1582,7 @@ int spf_query_run(spf_query* q) {
   HIP_TRY(hipEventRecord(q->ev0, g->stream));
   int s = SPF_OK;
   if (q->nq && g->V) {
-    if (q->kind == 2) {
-      s = launch_exact(q);
-    } else {
-      const bool unit = q->flags & SPF_F_UNIT_METRIC;
-      const bool gmem = q->kind == 1;
-      switch (q->wmax) {
-      case 0:
-        s = dispatch_flags<0>(q, unit, q->has_ign, gmem);
-        break;
-      case 1:
-        s = dispatch_flags<1>(q, unit, q->has_ign, gmem);
-        break;
-      case 4:
-        s = dispatch_flags<4>(q, unit, q->has_ign, gmem);
-        break;
-      default:
-        s = dispatch_flags<16>(q, unit, q->has_ign, gmem);
-        break;
-      }
-    }
+    s = run_plan(q);
   }
   HIP_TRY(hipEventRecord(q->ev1, g->stream));
   q->ran = true;
@@ -1225,7 +1611,18 @@ const char* spf_query_kernel_name(const spf_query* q) {
   if (!q) {
     return "none";
   }
-  return q->kind == 0 ? "lds" : (q->kind == 1 ? "gmem" : "exact");
+  switch (q->dist) {
+  case DistPlan::SsspLds:
+    return q->nh == NhPlan::Rows ? "lds+rows" : "lds";
+  case DistPlan::SsspGmem:
+    return q->nh == NhPlan::Rows ? "gmem+rows" : "gmem";
+  case DistPlan::BfsLds:
+    return q->nh == NhPlan::Rows ? "bfs+rows" : "bfs";
+  case DistPlan::BfsGmem:
+    return q->nh == NhPlan::Rows ? "bfs-gmem+rows" : "bfs-gmem";
+  default:
+    return "exact";
+  }
 }
 
 int spf_query_dist(spf_query* q, uint32_t i, uint64_t* out) {
@@ -1235,7 +1632,7 @@ int spf_query_dist(spf_query* q, uint32_t i, uint64_t* out) {
   const uint32_t V = q->g->V;
   HIP_TRY(hipSetDevice(q->g->device));
   HIP_TRY(hipStreamSynchronize(q->g->stream));
-  if (q->kind == 2) {
+  if (q->dist == DistPlan::Exact) {
     HIP_TRY(hipMemcpy(out, (uint64_t*)q->d_dist + (size_t)i * V, V * 8ull,
                       hipMemcpyDeviceToHost));
     std::vector<uint32_t> order(V);
@@ -1249,8 +1646,8 @@ int spf_query_dist(spf_query* q, uint32_t i, uint64_t* out) {
     return SPF_OK;
   }
   std::vector<uint32_t> d(V);
-  HIP_TRY(hipMemcpy(d.data(), (uint32_t*)q->d_dist + (size_t)i * V, V * 4ull,
-                    hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(d.data(), (uint32_t*)q->d_dist + (size_t)i * q->Vp,
+                    V * 4ull, hipMemcpyDeviceToHost));
   for (uint32_t v = 0; v < V; ++v) {
     out[v] = d[v] == kInf32 ? SPF_UNREACHABLE : (uint64_t)d[v];
   }
@@ -1279,7 +1676,7 @@ int spf_query_nexthops(spf_query* q, uint32_t i, uint64_t* out) {
 }
 
 int spf_query_order(spf_query* q, uint32_t i, uint32_t* out) {
-  if (!q || !out || i >= q->nq || q->kind != 2) {
+  if (!q || !out || i >= q->nq || q->dist != DistPlan::Exact) {
     return fail(SPF_E_INVALID, "no settle order for this row");
   }
   HIP_TRY(hipSetDevice(q->g->device));
@@ -1299,7 +1696,7 @@ int spf_query_device_rows(
     *dist_rows = q->d_dist;
   }
   if (dist_elem_bytes) {
-    *dist_elem_bytes = q->kind == 2 ? 8 : 4;
+    *dist_elem_bytes = q->dist == DistPlan::Exact ? 8 : 4;
   }
   if (nh_rows) {
     *nh_rows = q->d_nh;
@@ -1308,6 +1705,13 @@ int spf_query_device_rows(
     *nh_total_words = q->nh_total;
   }
   return SPF_OK;
+}
+
+uint32_t spf_query_row_stride(const spf_query* q) {
+  if (!q) {
+    return 0;
+  }
+  return q->dist == DistPlan::Exact ? q->g->V : q->Vp;
 }
 
 } // extern "C"

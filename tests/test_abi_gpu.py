@@ -167,3 +167,84 @@ def test_transit_update(gpu_ready):
     csr.overloaded = ov
     q = g.query(list(range(V)), abi.SPF_F_NEXTHOPS).run()
     check_query(csr, q, list(range(V)), True)
+
+
+# ---- batch plans: distance rows + next hops from rows (neighbour-closed batches)
+
+
+@pytest.mark.parametrize("seed", [31, 32])
+def test_all_sources_rows_plan_weighted(gpu_ready, seed):
+    rng = random.Random(seed)
+    V = 250
+    links = random_links(rng, V, 900)
+    ov = [1 if rng.random() < 0.05 else 0 for _ in range(V)]
+    csr = abi.Csr.from_links(V, links, ov)
+    g = abi.Graph(csr)
+    sources = list(range(V))
+    q = g.query(sources, abi.SPF_F_NEXTHOPS).run()
+    assert q.kernel == "lds+rows"
+    check_query(csr, q, sources, True)
+
+
+@pytest.mark.parametrize("seed", [41, 42])
+def test_all_sources_bfs_plan(gpu_ready, seed):
+    rng = random.Random(seed)
+    V = 300
+    links = random_links(rng, V, 1000)
+    ov = [1 if rng.random() < 0.05 else 0 for _ in range(V)]
+    csr = abi.Csr.from_links(V, links, ov)
+    g = abi.Graph(csr)
+    sources = list(range(V))
+    q = g.query(sources, abi.SPF_F_NEXTHOPS | abi.SPF_F_UNIT_METRIC).run()
+    assert q.kernel == "bfs+rows"
+    check_query(csr, q, sources, False)
+    qd = g.query(sources[::3], abi.SPF_F_UNIT_METRIC).run()
+    assert qd.kernel == "bfs"
+    check_query(csr, qd, sources[::3], False)
+
+
+def test_uniform_metric_scaled_bfs(gpu_ready):
+    rng = random.Random(5)
+    V = 200
+    links = [(u, v, 7, 7) for (u, v, _, _) in random_links(rng, V, 600)]
+    csr = abi.Csr.from_links(V, links)
+    g = abi.Graph(csr)
+    sources = list(range(V))
+    q = g.query(sources, abi.SPF_F_NEXTHOPS).run()
+    assert q.kernel == "bfs+rows"
+    check_query(csr, q, sources, True)
+
+
+def test_fabric_all_sources_sampled(gpu_ready):
+    from openr_amd import topologies as TP
+
+    topo = TP.fabric(2000)  # 29 pods, same structure as the 10k fabric
+    rsw = [i for i, n in enumerate(topo.names) if n.startswith("3-")]
+    csr = topo.csr(overloaded=[rsw[3], rsw[77]])
+    g = abi.Graph(csr)
+    sources = list(range(csr.num_nodes))
+    q = g.query(sources, abi.SPF_F_NEXTHOPS).run()
+    assert q.kernel == "bfs+rows"
+    check_query_sample = sources[:: max(1, len(sources) // 25)]
+    for i in check_query_sample:
+        ref = spf_py.run_spf(csr, i, True)
+        d = q.dist(i)
+        got = q.nexthop_sets(i, i)
+        for v in range(csr.num_nodes):
+            if v in ref:
+                assert int(d[v]) == ref[v][0]
+                if v != i:
+                    assert got[v] == ref[v][1], (i, v)
+            else:
+                assert d[v] == UNREACH
+
+
+def test_gmem_bfs_plan_large(gpu_ready):
+    rng = random.Random(22)
+    V = 70000
+    links = random_links(rng, V, 140000, wmin=1, wmax=1, parallel=0.0)
+    csr = abi.Csr.from_links(V, links)
+    g = abi.Graph(csr)
+    q = g.query([0, 4321, 69999], abi.SPF_F_UNIT_METRIC).run()
+    assert q.kernel == "bfs-gmem"
+    check_query(csr, q, [0, 4321, 69999], False)

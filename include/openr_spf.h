@@ -141,7 +141,7 @@ int spf_query_order(spf_query* q, uint32_t i, uint32_t* out /*[V]*/);
 /* Device pointers of the result rows (for RCCL gathers): dist rows are
  * uint32 (fast kernels) or uint64 (exact kernel), spf_query_row_stride
  * elements apart (V entries used per row).  Next-hop rows are packed:
- * query i starts at word sum_{j<i} V * nh_words(j). */
+ * query i starts at word sum_{j<i} roundup4(V * nh_words(j)). */
 int spf_query_device_rows(
     spf_query* q, void** dist_rows, uint32_t* dist_elem_bytes,
     void** nh_rows, uint64_t* nh_total_words);

@@ -36,6 +36,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -653,6 +654,312 @@ __global__ __launch_bounds__(kNhThreads) void spf_nh_rows_kernel(NhRowsArgs a) {
   }
 }
 
+// ------------------------------------- multi-source bit-parallel BFS (MS-BFS)
+//
+// Uniform metric, many sources: one workgroup advances the BFS of a whole
+// batch of B = bits(MT) sources at once.  The frontier is one B-bit mask per
+// node in LDS (bit s = "node is on source s's frontier"); each thread owns
+// K nodes and keeps their visited masks in registers.  One level is a single
+// pull pass over the CSR:
+//     new(v) = OR_{u in N(v)} F(u)  &  ~visited(v)
+// so every CSR row is read once per level for B sources (the per-source BFS
+// reads it once per source).  Transit: a node's frontier bits are published
+// only if it may be transited, except at level 0 where each source's own bit
+// is always published (LinkState.cpp:829-836 exempts the source).
+// Distance rows are written as the bits appear (predicated stores: for a
+// fixed source the active lanes hold consecutive nodes), plus an 8-bit level
+// row that the next-hop pass streams instead of the 32-bit distances.
+
+constexpr uint32_t kMsThreads = 1024;
+constexpr uint32_t kMsMaxK = 16; // nodes per thread -> V <= 16384
+
+struct MsBfsArgs {
+  const uint32_t* row;
+  const uint32_t* col;
+  const uint32_t* trbits;
+  const uint32_t* src;
+  uint32_t* dist_out; // [nq][Vp]
+  uint8_t* lvl_out;   // [nq][Vp8]
+  uint32_t* flags;    // [0] |= 1 when a level >= 255 occurred
+  uint32_t V;
+  uint32_t Vp;
+  uint32_t Vp8;
+  uint32_t nq;
+  uint32_t scale;
+};
+
+template <typename MT>
+__device__ __forceinline__ void ms_record(
+    const MsBfsArgs& a, uint32_t q0, uint32_t v, MT bits, uint32_t level) {
+  const uint32_t d = level * a.scale;
+  const uint8_t l8 = level < 255 ? (uint8_t)level : (uint8_t)255;
+  while (bits) {
+    const uint32_t s = (uint32_t)__builtin_ctzll((unsigned long long)bits);
+    bits &= bits - 1;
+    a.dist_out[(size_t)(q0 + s) * a.Vp + v] = d;
+    a.lvl_out[(size_t)(q0 + s) * a.Vp8 + v] = l8;
+  }
+}
+
+template <typename MT>
+__global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
+  extern __shared__ __align__(16) unsigned char ms_smem[];
+  MT* F = reinterpret_cast<MT*>(ms_smem);
+  constexpr uint32_t B = sizeof(MT) * 8;
+  const uint32_t V = a.V, tid = threadIdx.x;
+  const uint32_t K = (V + kMsThreads - 1) / kMsThreads;
+  const uint32_t nbatch = (a.nq + B - 1) / B;
+
+  for (uint32_t b = blockIdx.x; b < nbatch; b += gridDim.x) {
+    const uint32_t q0 = b * B;
+    const uint32_t nb = min(B, a.nq - q0);
+    const MT full = nb == B ? ~(MT)0 : (((MT)1 << nb) - 1);
+    for (uint32_t v = tid; v < V; v += kMsThreads) {
+      F[v] = 0;
+    }
+    __syncthreads();
+    if (tid < nb) {
+      const uint32_t s = a.src[q0 + tid];
+      if constexpr (sizeof(MT) == 8) {
+        atomicOr(reinterpret_cast<unsigned long long*>(&F[s]), 1ull << tid);
+      } else {
+        atomicOr(reinterpret_cast<unsigned int*>(&F[s]), 1u << tid);
+      }
+    }
+    __syncthreads();
+    MT vis[kMsMaxK];
+    MT nw[kMsMaxK];
+#pragma unroll
+    for (uint32_t k = 0; k < kMsMaxK; ++k) {
+      const uint32_t v = tid + k * kMsThreads;
+      vis[k] = (k < K && v < V) ? F[v] : (MT)0;
+      nw[k] = 0;
+      if (k < K && v < V && vis[k]) {
+        ms_record<MT>(a, q0, v, vis[k], 0);
+      }
+    }
+    uint32_t level = 0;
+    for (;;) {
+      const uint32_t L = level + 1;
+      MT any = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < kMsMaxK; ++k) {
+        const uint32_t v = tid + k * kMsThreads;
+        nw[k] = 0;
+        if (k < K && v < V && vis[k] != full) {
+          const uint32_t beg = a.row[v], end = a.row[v + 1];
+          MT acc = 0;
+          uint32_t e = beg;
+          for (; e + 4 <= end; e += 4) {
+            const uint32_t u0 = a.col[e], u1 = a.col[e + 1], u2 = a.col[e + 2],
+                           u3 = a.col[e + 3];
+            acc |= F[u0] | F[u1] | F[u2] | F[u3];
+          }
+          for (; e < end; ++e) {
+            acc |= F[a.col[e]];
+          }
+          nw[k] = acc & ~vis[k];
+          vis[k] |= nw[k];
+          any |= nw[k];
+        }
+      }
+      __syncthreads(); // every read of this level's frontier is done
+#pragma unroll
+      for (uint32_t k = 0; k < kMsMaxK; ++k) {
+        const uint32_t v = tid + k * kMsThreads;
+        if (k < K && v < V) {
+          const bool transit = (a.trbits[v >> 5] >> (v & 31)) & 1u;
+          F[v] = transit ? nw[k] : (MT)0;
+          if (nw[k]) {
+            ms_record<MT>(a, q0, v, nw[k], L);
+          }
+        }
+      }
+      if (L >= 255 && any) {
+        atomicOr(a.flags, 1u);
+      }
+      if (!__syncthreads_or(any != 0)) {
+        break;
+      }
+      level = L;
+    }
+    // unreached (source, node) pairs
+#pragma unroll
+    for (uint32_t k = 0; k < kMsMaxK; ++k) {
+      const uint32_t v = tid + k * kMsThreads;
+      if (k < K && v < V) {
+        MT miss = full & ~vis[k];
+        while (miss) {
+          const uint32_t s = (uint32_t)__builtin_ctzll((unsigned long long)miss);
+          miss &= miss - 1;
+          a.dist_out[(size_t)(q0 + s) * a.Vp + v] = kInf32;
+          a.lvl_out[(size_t)(q0 + s) * a.Vp8 + v] = 255;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Next hops from 8-bit level rows (uniform metric c: w + D_f == D_s is
+// lf + 1 == ls).  16 nodes per thread per 16-byte load.  Falls back to the
+// 32-bit rows when the BFS saw a level >= 255 (flags[0]).
+struct NhLevelsArgs {
+  const uint32_t* nbr_off;
+  const uint32_t* nbrs;
+  const uint32_t* trbits;
+  const uint32_t* src;
+  const int32_t* row_of;
+  const uint8_t* lvl; // [nq][Vp8]
+  const uint32_t* dist; // [nq][Vp]
+  const uint32_t* flags;
+  const uint64_t* nh_off;
+  const uint32_t* nh_w;
+  uint64_t* nh_out;
+  uint32_t V;
+  uint32_t Vp;
+  uint32_t Vp8;
+  uint32_t nq;
+  uint32_t scale;
+};
+
+constexpr uint32_t kNlThreads = 256;
+constexpr uint32_t kNlPer = 4;
+constexpr uint32_t kNlChunk = kNlThreads * kNlPer;
+
+// 4 nodes per thread: one 4-byte load of a level row (or one 16-byte load of
+// a 32-bit row), four compares, and the four next-hop words leave as two
+// 16-byte stores, so a wave writes 2 KB of contiguous mask row.  The
+// source's neighbour list (row index + transit bit) is staged in LDS first
+// and the neighbour rows are loaded kNlUnroll at a time, so a block keeps
+// several independent row loads in flight instead of one dependent chain
+// (nbrs -> row_of -> trbits -> row) per neighbour.
+constexpr uint32_t kNlUnroll = 8;
+constexpr uint32_t kNlStage = 1024; // neighbours staged per pass
+
+template <bool WIDE>
+__device__ __forceinline__ void nl_load(
+    const NhLevelsArgs& a, uint32_t r, uint32_t v0, uint32_t (&o)[4]) {
+  if constexpr (!WIDE) {
+    const uint32_t x = *reinterpret_cast<const uint32_t*>(a.lvl + (size_t)r * a.Vp8 + v0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[i] = (x >> (8 * i)) & 0xFFu;
+    }
+  } else {
+    const uint4 x = *reinterpret_cast<const uint4*>(a.dist + (size_t)r * a.Vp + v0);
+    o[0] = x.x;
+    o[1] = x.y;
+    o[2] = x.z;
+    o[3] = x.w;
+  }
+}
+
+template <bool WIDE>
+__device__ __forceinline__ void nl_body(
+    const NhLevelsArgs& a, uint32_t q, uint32_t s, uint32_t v0, uint32_t* st_row,
+    uint32_t* st_node) {
+  const uint32_t Wm = a.nh_w[q];
+  uint64_t* nhrow = a.nh_out + a.nh_off[q];
+  const bool active = v0 < a.V;
+  uint32_t ls[4] = {0, 0, 0, 0};
+  if (active) {
+    nl_load<WIDE>(a, q, v0, ls);
+  }
+  const uint32_t none = WIDE ? kInf32 : 255u;
+  const uint64_t step = WIDE ? (uint64_t)a.scale : 1ull;
+  bool live[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    live[i] = active && ls[i] != none && ls[i] != 0;
+  }
+  const uint32_t beg = a.nbr_off[s], n = a.nbr_off[s + 1] - beg;
+  for (uint32_t w = 0; w < Wm; ++w) {
+    uint64_t acc[4] = {0, 0, 0, 0};
+    const uint32_t jlo = w * 64, jhi = min(n, jlo + 64);
+    for (uint32_t base = jlo; base < jhi; base += kNlStage) {
+      const uint32_t cnt = min(kNlStage, jhi - base);
+      __syncthreads();
+      for (uint32_t t = threadIdx.x; t < cnt; t += kNlThreads) {
+        const uint32_t f = a.nbrs[beg + base + t];
+        const uint32_t tf = (a.trbits[f >> 5] >> (f & 31)) & 1u;
+        st_row[t] = (uint32_t)a.row_of[f];
+        st_node[t] = f | (tf << 31);
+      }
+      __syncthreads();
+      if (!active) {
+        continue;
+      }
+      uint32_t t = 0;
+      for (; t + kNlUnroll <= cnt; t += kNlUnroll) {
+        uint32_t lf[kNlUnroll][4];
+#pragma unroll
+        for (uint32_t u = 0; u < kNlUnroll; ++u) {
+          nl_load<WIDE>(a, st_row[t + u], v0, lf[u]);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kNlUnroll; ++u) {
+          const uint32_t nd = st_node[t + u];
+          const uint32_t f = nd & 0x7FFFFFFFu;
+          const bool tf = nd >> 31;
+          const uint64_t bit = 1ull << ((base + t + u) & 63);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (live[i] && lf[u][i] != none && (uint64_t)lf[u][i] + step == (uint64_t)ls[i] &&
+                (tf || v0 + i == f)) {
+              acc[i] |= bit;
+            }
+          }
+        }
+      }
+      for (; t < cnt; ++t) {
+        uint32_t lf[4];
+        nl_load<WIDE>(a, st_row[t], v0, lf);
+        const uint32_t nd = st_node[t];
+        const uint32_t f = nd & 0x7FFFFFFFu;
+        const bool tf = nd >> 31;
+        const uint64_t bit = 1ull << ((base + t) & 63);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (live[i] && lf[i] != none && (uint64_t)lf[i] + step == (uint64_t)ls[i] &&
+              (tf || v0 + i == f)) {
+            acc[i] |= bit;
+          }
+        }
+      }
+    }
+    if (!active) {
+      continue;
+    }
+    if (Wm == 1 && v0 + 4 <= a.V) {
+      ulonglong2* o = reinterpret_cast<ulonglong2*>(nhrow + v0);
+      o[0] = make_ulonglong2(acc[0], acc[1]);
+      o[1] = make_ulonglong2(acc[2], acc[3]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (v0 + i < a.V) {
+          nhrow[(size_t)(v0 + i) * Wm + w] = acc[i];
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kNlThreads) void spf_nh_levels_kernel(NhLevelsArgs a) {
+  __shared__ uint32_t st_row[kNlStage];
+  __shared__ uint32_t st_node[kNlStage];
+  const uint32_t chunk = blockIdx.x / a.nq;
+  const uint32_t q = blockIdx.x - chunk * a.nq;
+  const uint32_t s = a.src[q];
+  const uint32_t v0 = chunk * kNlChunk + threadIdx.x * kNlPer;
+  if (a.flags[0] != 0) {
+    nl_body<true>(a, q, s, v0, st_row, st_node);
+  } else {
+    nl_body<false>(a, q, s, v0, st_row, st_node);
+  }
+}
+
 // ------------------------------------------------------------- exact kernel
 
 struct ExactArgs {
@@ -836,8 +1143,8 @@ struct spf_graph {
 };
 
 // How a batch is computed.
-enum class DistPlan { SsspLds, SsspGmem, BfsLds, BfsGmem, Exact };
-enum class NhPlan { None, Inline, Rows };
+enum class DistPlan { SsspLds, SsspGmem, BfsLds, BfsGmem, MsBfs, Exact };
+enum class NhPlan { None, Inline, Rows, Levels };
 
 struct spf_query {
   spf_graph* g = nullptr;
@@ -845,7 +1152,10 @@ struct spf_query {
   DistPlan dist = DistPlan::SsspLds;
   NhPlan nh = NhPlan::None;
   int wmax = 0;
-  uint32_t ign_cap = 0, grid = 0, Vp = 0;
+  int ms_bits = 64; // MS-BFS batch width (32 or 64 sources per workgroup)
+  uint32_t ign_cap = 0, grid = 0, Vp = 0, Vp8 = 0;
+  uint8_t* d_lvl = nullptr;
+  uint32_t* d_flags = nullptr;
   size_t lds_bytes = 0;
   bool has_ign = false;
   std::vector<uint64_t> nh_off;
@@ -902,7 +1212,8 @@ void free_query(spf_query* q) {
   for (void* p :
        {(void*)q->d_src, (void*)q->d_ign_off, (void*)q->d_ign,
         (void*)q->d_nh_w, (void*)q->d_order, (void*)q->d_scratch,
-        (void*)q->d_nh_off, q->d_dist, (void*)q->d_nh, (void*)q->d_row_of}) {
+        (void*)q->d_nh_off, q->d_dist, (void*)q->d_nh, (void*)q->d_row_of,
+        (void*)q->d_lvl, (void*)q->d_flags}) {
     if (p) {
       (void)hipFree(p);
     }
@@ -1250,6 +1561,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
   q->flags = desc->flags;
   q->has_ign = has_ign;
   q->Vp = (V + 15) & ~15u;
+  q->Vp8 = (V + 15) & ~15u;
   auto bail = [&](int s) {
     free_query(q);
     return s;
@@ -1270,7 +1582,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       const uint32_t w = std::max<uint32_t>(1, (nn + 63) / 64);
       q->nh_off[i] = off;
       q->nh_w[i] = w;
-      off += (uint64_t)w * V;
+      off += ((uint64_t)w * V + 3) & ~3ull; // 32-byte aligned rows
       maxw = std::max(maxw, w);
     }
     q->nh_total = off;
@@ -1328,12 +1640,38 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     }
   }
 
+  // many sources on a uniform metric: bit-parallel multi-source BFS
+  // (OPENR_SPF_MSBFS=0 disables, =32 / =64 picks the batch width)
+  if ((q->dist == DistPlan::BfsLds || q->dist == DistPlan::BfsGmem) &&
+      V <= kMsThreads * kMsMaxK && nq >= 32) {
+    const char* env = getenv("OPENR_SPF_MSBFS");
+    const int width = env ? atoi(env) : 64;
+    if (width == 32 || width == 64) {
+      q->dist = DistPlan::MsBfs;
+      q->ms_bits = width;
+      q->lds_bytes = (size_t)V * (width / 8);
+      const uint32_t nbatch = (nq + width - 1) / width;
+      const uint32_t per_cu = (uint32_t)std::max<size_t>(
+          1, std::min<size_t>(2048 / kMsThreads, kLdsLimit / std::max<size_t>(q->lds_bytes, 1)));
+      q->grid = std::min<uint32_t>(nbatch, (uint32_t)g->num_cus * per_cu);
+      if (q->nh == NhPlan::Rows) {
+        q->nh = NhPlan::Levels;
+      }
+    }
+  }
+
   if (hipSetDevice(g->device) != hipSuccess) {
     return bail(fail(SPF_E_DEVICE, "hipSetDevice failed"));
   }
   int s = SPF_OK;
   if ((s = dev_upload(&q->d_src, desc->sources, nq))) {
     return bail(s);
+  }
+  if (q->dist == DistPlan::MsBfs) {
+    if (hipMalloc((void**)&q->d_lvl, (size_t)nq * q->Vp8) != hipSuccess ||
+        hipMalloc((void**)&q->d_flags, 16) != hipSuccess) {
+      return bail(fail(SPF_E_NOMEM, "level rows"));
+    }
   }
   if (has_ign) {
     const uint32_t total = desc->ignore_offsets[nq];
@@ -1498,6 +1836,70 @@ int launch_nh_rows(spf_query* q, bool unit) {
   return SPF_OK;
 }
 
+int launch_msbfs(spf_query* q, bool unit) {
+  spf_graph* g = q->g;
+  MsBfsArgs a;
+  a.row = g->d_row;
+  a.col = g->d_col;
+  a.trbits = g->d_tr;
+  a.src = q->d_src;
+  a.dist_out = (uint32_t*)q->d_dist;
+  a.lvl_out = q->d_lvl;
+  a.flags = q->d_flags;
+  a.V = g->V;
+  a.Vp = q->Vp;
+  a.Vp8 = q->Vp8;
+  a.nq = q->nq;
+  a.scale = unit ? 1u : g->uniform;
+  HIP_TRY(hipMemsetAsync(q->d_flags, 0, 16, g->stream));
+  if (q->ms_bits == 64) {
+    auto kern = spf_msbfs_kernel<uint64_t>;
+    HIP_TRY(hipFuncSetAttribute((const void*)kern,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)q->lds_bytes));
+    hipLaunchKernelGGL(kern, dim3(q->grid), dim3(kMsThreads), q->lds_bytes,
+                       g->stream, a);
+  } else {
+    auto kern = spf_msbfs_kernel<uint32_t>;
+    HIP_TRY(hipFuncSetAttribute((const void*)kern,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)q->lds_bytes));
+    hipLaunchKernelGGL(kern, dim3(q->grid), dim3(kMsThreads), q->lds_bytes,
+                       g->stream, a);
+  }
+  HIP_TRY(hipGetLastError());
+  return SPF_OK;
+}
+
+int launch_nh_levels(spf_query* q, bool unit) {
+  spf_graph* g = q->g;
+  NhLevelsArgs a;
+  a.nbr_off = g->d_nbr_off;
+  a.nbrs = g->d_nbrs;
+  a.trbits = g->d_tr;
+  a.src = q->d_src;
+  a.row_of = q->d_row_of;
+  a.lvl = q->d_lvl;
+  a.dist = (const uint32_t*)q->d_dist;
+  a.flags = q->d_flags;
+  a.nh_off = q->d_nh_off;
+  a.nh_w = q->d_nh_w;
+  a.nh_out = q->d_nh;
+  a.V = g->V;
+  a.Vp = q->Vp;
+  a.Vp8 = q->Vp8;
+  a.nq = q->nq;
+  a.scale = unit ? 1u : g->uniform;
+  const uint64_t blocks = (uint64_t)((g->V + kNlChunk - 1) / kNlChunk) * q->nq;
+  if (blocks > 0x7FFFFFFFull) {
+    return fail(SPF_E_UNSUPPORTED, "batch too large for the next-hop pass");
+  }
+  hipLaunchKernelGGL(spf_nh_levels_kernel, dim3((uint32_t)blocks),
+                     dim3(kNlThreads), 0, g->stream, a);
+  HIP_TRY(hipGetLastError());
+  return SPF_OK;
+}
+
 int launch_exact(spf_query* q) {
   spf_graph* g = q->g;
   ExactArgs a;
@@ -1536,6 +1938,13 @@ int run_plan(spf_query* q) {
   switch (q->dist) {
   case DistPlan::Exact:
     return launch_exact(q);
+  case DistPlan::MsBfs: {
+    int s = launch_msbfs(q, unit);
+    if (s == SPF_OK && q->nh == NhPlan::Levels) {
+      s = launch_nh_levels(q, unit);
+    }
+    return s;
+  }
   case DistPlan::BfsLds:
   case DistPlan::BfsGmem: {
     int s = launch_bfs(q, unit);
@@ -1620,6 +2029,8 @@ const char* spf_query_kernel_name(const spf_query* q) {
     return q->nh == NhPlan::Rows ? "bfs+rows" : "bfs";
   case DistPlan::BfsGmem:
     return q->nh == NhPlan::Rows ? "bfs-gmem+rows" : "bfs-gmem";
+  case DistPlan::MsBfs:
+    return q->nh == NhPlan::Levels ? "msbfs+levels" : "msbfs";
   default:
     return "exact";
   }

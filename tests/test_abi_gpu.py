@@ -40,8 +40,10 @@ def random_links(rng, V, L, wmin=1, wmax=20, parallel=0.05, asym=True):
     return links
 
 
-def check_query(csr, q, sources, use_metric, ignore=None):
+def check_query(csr, q, sources, use_metric, ignore=None, rows=None):
     for i, s in enumerate(sources):
+        if rows is not None and i not in rows:
+            continue
         ref = spf_py.run_spf(
             csr, s, use_metric, frozenset(ignore[i]) if ignore else frozenset()
         )
@@ -186,8 +188,20 @@ def test_all_sources_rows_plan_weighted(gpu_ready, seed):
     check_query(csr, q, sources, True)
 
 
+@pytest.fixture(params=["0", "32", "64"])
+def msbfs(request, monkeypatch):
+    monkeypatch.setenv("OPENR_SPF_MSBFS", request.param)
+    return request.param
+
+
+def _bfs_kernel(msbfs, nh=True):
+    if msbfs == "0":
+        return "bfs+rows" if nh else "bfs"
+    return "msbfs+levels" if nh else "msbfs"
+
+
 @pytest.mark.parametrize("seed", [41, 42])
-def test_all_sources_bfs_plan(gpu_ready, seed):
+def test_all_sources_bfs_plan(gpu_ready, seed, msbfs):
     rng = random.Random(seed)
     V = 300
     links = random_links(rng, V, 1000)
@@ -196,14 +210,14 @@ def test_all_sources_bfs_plan(gpu_ready, seed):
     g = abi.Graph(csr)
     sources = list(range(V))
     q = g.query(sources, abi.SPF_F_NEXTHOPS | abi.SPF_F_UNIT_METRIC).run()
-    assert q.kernel == "bfs+rows"
+    assert q.kernel == _bfs_kernel(msbfs)
     check_query(csr, q, sources, False)
     qd = g.query(sources[::3], abi.SPF_F_UNIT_METRIC).run()
-    assert qd.kernel == "bfs"
+    assert qd.kernel == _bfs_kernel(msbfs, nh=False)
     check_query(csr, qd, sources[::3], False)
 
 
-def test_uniform_metric_scaled_bfs(gpu_ready):
+def test_uniform_metric_scaled_bfs(gpu_ready, msbfs):
     rng = random.Random(5)
     V = 200
     links = [(u, v, 7, 7) for (u, v, _, _) in random_links(rng, V, 600)]
@@ -211,11 +225,24 @@ def test_uniform_metric_scaled_bfs(gpu_ready):
     g = abi.Graph(csr)
     sources = list(range(V))
     q = g.query(sources, abi.SPF_F_NEXTHOPS).run()
-    assert q.kernel == "bfs+rows"
+    assert q.kernel == _bfs_kernel(msbfs)
     check_query(csr, q, sources, True)
 
 
-def test_fabric_all_sources_sampled(gpu_ready):
+def test_deep_graph_many_levels(gpu_ready, msbfs):
+    # a 300-node path: BFS depth 299 > 255 exercises the 32-bit fallback of
+    # the level rows and long MS-BFS level loops
+    V = 300
+    links = [(i, i + 1, 1, 1) for i in range(V - 1)]
+    csr = abi.Csr.from_links(V, links)
+    g = abi.Graph(csr)
+    sources = list(range(V))
+    q = g.query(sources, abi.SPF_F_NEXTHOPS).run()
+    assert q.kernel == _bfs_kernel(msbfs)
+    check_query(csr, q, sources, True, rows=set(range(0, V, 37)) | {V - 1})
+
+
+def test_fabric_all_sources_sampled(gpu_ready, msbfs):
     from openr_amd import topologies as TP
 
     topo = TP.fabric(2000)  # 29 pods, same structure as the 10k fabric
@@ -224,7 +251,7 @@ def test_fabric_all_sources_sampled(gpu_ready):
     g = abi.Graph(csr)
     sources = list(range(csr.num_nodes))
     q = g.query(sources, abi.SPF_F_NEXTHOPS).run()
-    assert q.kernel == "bfs+rows"
+    assert q.kernel == _bfs_kernel(msbfs)
     check_query_sample = sources[:: max(1, len(sources) // 25)]
     for i in check_query_sample:
         ref = spf_py.run_spf(csr, i, True)

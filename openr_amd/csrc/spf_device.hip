@@ -666,9 +666,10 @@ __global__ __launch_bounds__(kNhThreads) void spf_nh_rows_kernel(NhRowsArgs a) {
 // reads it once per source).  Transit: a node's frontier bits are published
 // only if it may be transited, except at level 0 where each source's own bit
 // is always published (LinkState.cpp:829-836 exempts the source).
-// Distance rows are written as the bits appear (predicated stores: for a
-// fixed source the active lanes hold consecutive nodes), plus an 8-bit level
-// row that the next-hop pass streams instead of the 32-bit distances.
+// The frontier is double-buffered in LDS (read cur, write nxt, one barrier
+// per level), so only the visited masks live in registers.  Distances go out
+// as 32-bit rows plus an 8-bit level row that the next-hop pass streams
+// instead of the 32-bit distances.
 
 constexpr uint32_t kMsThreads = 1024;
 constexpr uint32_t kMsMaxK = 16; // nodes per thread -> V <= 16384
@@ -688,11 +689,19 @@ struct MsBfsArgs {
   uint32_t scale;
 };
 
+// Write each (source, node) distance the moment its bit appears (one store
+// per bit).  These stores overlap the latency-bound row scans of the later
+// levels; writing the rows source-by-source at the end instead (fully
+// coalesced, from a per-level history) measured slower on the fabric because
+// the write burst then serialises behind the last level.
 template <typename MT>
 __device__ __forceinline__ void ms_record(
     const MsBfsArgs& a, uint32_t q0, uint32_t v, MT bits, uint32_t level) {
   const uint32_t d = level * a.scale;
   const uint8_t l8 = level < 255 ? (uint8_t)level : (uint8_t)255;
+  if (level >= 255 && bits) {
+    atomicOr(a.flags, 1u);
+  }
   while (bits) {
     const uint32_t s = (uint32_t)__builtin_ctzll((unsigned long long)bits);
     bits &= bits - 1;
@@ -701,91 +710,91 @@ __device__ __forceinline__ void ms_record(
   }
 }
 
-template <typename MT>
+template <typename MT, uint32_t KMAX>
 __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
   extern __shared__ __align__(16) unsigned char ms_smem[];
-  MT* F = reinterpret_cast<MT*>(ms_smem);
   constexpr uint32_t B = sizeof(MT) * 8;
   const uint32_t V = a.V, tid = threadIdx.x;
-  const uint32_t K = (V + kMsThreads - 1) / kMsThreads;
+  const uint32_t K = (V + kMsThreads - 1) / kMsThreads; // <= KMAX
   const uint32_t nbatch = (a.nq + B - 1) / B;
 
   for (uint32_t b = blockIdx.x; b < nbatch; b += gridDim.x) {
+    // frontier double buffer: cur is read during a level, nxt written
+    MT* cur = reinterpret_cast<MT*>(ms_smem);
+    MT* nxt = cur + V;
     const uint32_t q0 = b * B;
     const uint32_t nb = min(B, a.nq - q0);
     const MT full = nb == B ? ~(MT)0 : (((MT)1 << nb) - 1);
     for (uint32_t v = tid; v < V; v += kMsThreads) {
-      F[v] = 0;
+      cur[v] = 0;
     }
     __syncthreads();
     if (tid < nb) {
       const uint32_t s = a.src[q0 + tid];
       if constexpr (sizeof(MT) == 8) {
-        atomicOr(reinterpret_cast<unsigned long long*>(&F[s]), 1ull << tid);
+        atomicOr(reinterpret_cast<unsigned long long*>(&cur[s]), 1ull << tid);
       } else {
-        atomicOr(reinterpret_cast<unsigned int*>(&F[s]), 1u << tid);
+        atomicOr(reinterpret_cast<unsigned int*>(&cur[s]), 1u << tid);
       }
     }
     __syncthreads();
-    MT vis[kMsMaxK];
-    MT nw[kMsMaxK];
+    MT vis[KMAX];
 #pragma unroll
-    for (uint32_t k = 0; k < kMsMaxK; ++k) {
+    for (uint32_t k = 0; k < KMAX; ++k) {
       const uint32_t v = tid + k * kMsThreads;
-      vis[k] = (k < K && v < V) ? F[v] : (MT)0;
-      nw[k] = 0;
+      vis[k] = (k < K && v < V) ? cur[v] : (MT)0;
       if (k < K && v < V && vis[k]) {
-        ms_record<MT>(a, q0, v, vis[k], 0);
+        ms_record<MT>(a, q0, v, vis[k], 0); // level 0 = the sources
       }
     }
     uint32_t level = 0;
     for (;;) {
       const uint32_t L = level + 1;
-      MT any = 0;
+      bool any = false;
 #pragma unroll
-      for (uint32_t k = 0; k < kMsMaxK; ++k) {
-        const uint32_t v = tid + k * kMsThreads;
-        nw[k] = 0;
-        if (k < K && v < V && vis[k] != full) {
+      for (uint32_t k = 0; k < KMAX; ++k) {
+        uint32_t v = tid + k * kMsThreads;
+        // opaque to the optimizer: keeps per-node addressing from being
+        // hoisted out of the level loop (KMAX copies of it spill VGPRs)
+        asm volatile("" : "+v"(v));
+        if (k >= K || v >= V) {
+          continue;
+        }
+        MT nw = 0;
+        if (vis[k] != full) {
           const uint32_t beg = a.row[v], end = a.row[v + 1];
           MT acc = 0;
           uint32_t e = beg;
           for (; e + 4 <= end; e += 4) {
             const uint32_t u0 = a.col[e], u1 = a.col[e + 1], u2 = a.col[e + 2],
                            u3 = a.col[e + 3];
-            acc |= F[u0] | F[u1] | F[u2] | F[u3];
+            acc |= cur[u0] | cur[u1] | cur[u2] | cur[u3];
           }
           for (; e < end; ++e) {
-            acc |= F[a.col[e]];
+            acc |= cur[a.col[e]];
           }
-          nw[k] = acc & ~vis[k];
-          vis[k] |= nw[k];
-          any |= nw[k];
+          nw = acc & ~vis[k];
+          vis[k] |= nw;
+        }
+        any |= nw != 0;
+        const bool transit = (a.trbits[v >> 5] >> (v & 31)) & 1u;
+        nxt[v] = transit ? nw : (MT)0;
+        if (nw) {
+          ms_record<MT>(a, q0, v, nw, L);
         }
       }
-      __syncthreads(); // every read of this level's frontier is done
-#pragma unroll
-      for (uint32_t k = 0; k < kMsMaxK; ++k) {
-        const uint32_t v = tid + k * kMsThreads;
-        if (k < K && v < V) {
-          const bool transit = (a.trbits[v >> 5] >> (v & 31)) & 1u;
-          F[v] = transit ? nw[k] : (MT)0;
-          if (nw[k]) {
-            ms_record<MT>(a, q0, v, nw[k], L);
-          }
-        }
-      }
-      if (L >= 255 && any) {
-        atomicOr(a.flags, 1u);
-      }
-      if (!__syncthreads_or(any != 0)) {
+      const bool more = __syncthreads_or(any);
+      if (!more) {
         break;
       }
+      MT* t = cur;
+      cur = nxt;
+      nxt = t;
       level = L;
     }
     // unreached (source, node) pairs
 #pragma unroll
-    for (uint32_t k = 0; k < kMsMaxK; ++k) {
+    for (uint32_t k = 0; k < KMAX; ++k) {
       const uint32_t v = tid + k * kMsThreads;
       if (k < K && v < V) {
         MT miss = full & ~vis[k];
@@ -1645,11 +1654,14 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
   if ((q->dist == DistPlan::BfsLds || q->dist == DistPlan::BfsGmem) &&
       V <= kMsThreads * kMsMaxK && nq >= 32) {
     const char* env = getenv("OPENR_SPF_MSBFS");
-    const int width = env ? atoi(env) : 64;
-    if (width == 32 || width == 64) {
+    int width = env ? atoi(env) : 64;
+    if (width == 64 && 2 * (size_t)V * 8 > kLdsLimit) {
+      width = 32; // the 64-bit frontier double buffer does not fit LDS
+    }
+    if ((width == 32 || width == 64) && 2 * (size_t)V * (width / 8) <= kLdsLimit) {
       q->dist = DistPlan::MsBfs;
       q->ms_bits = width;
-      q->lds_bytes = (size_t)V * (width / 8);
+      q->lds_bytes = 2 * (size_t)V * (width / 8); // frontier double buffer
       const uint32_t nbatch = (nq + width - 1) / width;
       const uint32_t per_cu = (uint32_t)std::max<size_t>(
           1, std::min<size_t>(2048 / kMsThreads, kLdsLimit / std::max<size_t>(q->lds_bytes, 1)));
@@ -1852,21 +1864,36 @@ int launch_msbfs(spf_query* q, bool unit) {
   a.nq = q->nq;
   a.scale = unit ? 1u : g->uniform;
   HIP_TRY(hipMemsetAsync(q->d_flags, 0, 16, g->stream));
+  const uint32_t K = (g->V + kMsThreads - 1) / kMsThreads;
+  const void* kern = nullptr;
+#define MS_PICK(MT, KM) kern = (const void*)spf_msbfs_kernel<MT, KM>
   if (q->ms_bits == 64) {
-    auto kern = spf_msbfs_kernel<uint64_t>;
-    HIP_TRY(hipFuncSetAttribute((const void*)kern,
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)q->lds_bytes));
-    hipLaunchKernelGGL(kern, dim3(q->grid), dim3(kMsThreads), q->lds_bytes,
-                       g->stream, a);
+    if (K <= 4) {
+      MS_PICK(uint64_t, 4);
+    } else if (K <= 8) {
+      MS_PICK(uint64_t, 8);
+    } else if (K <= 12) {
+      MS_PICK(uint64_t, 12);
+    } else {
+      MS_PICK(uint64_t, 16);
+    }
   } else {
-    auto kern = spf_msbfs_kernel<uint32_t>;
-    HIP_TRY(hipFuncSetAttribute((const void*)kern,
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)q->lds_bytes));
-    hipLaunchKernelGGL(kern, dim3(q->grid), dim3(kMsThreads), q->lds_bytes,
-                       g->stream, a);
+    if (K <= 4) {
+      MS_PICK(uint32_t, 4);
+    } else if (K <= 8) {
+      MS_PICK(uint32_t, 8);
+    } else if (K <= 12) {
+      MS_PICK(uint32_t, 12);
+    } else {
+      MS_PICK(uint32_t, 16);
+    }
   }
+#undef MS_PICK
+  HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)q->lds_bytes));
+  void* args[] = {&a};
+  HIP_TRY(hipLaunchKernel(kern, dim3(q->grid), dim3(kMsThreads), args,
+                          q->lds_bytes, g->stream));
   HIP_TRY(hipGetLastError());
   return SPF_OK;
 }

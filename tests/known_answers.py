@@ -512,3 +512,419 @@ def sc_compatibility_node(M):
     assert not ls.updateAdjacencyDatabase(db3)[0]
     db1 = T.createAdjDb("1", [adj12_old_2, adj13_old], 0)
     assert not ls.updateAdjacencyDatabase(db1)[0]
+
+
+# ------------------------------------------- SimpleRing (DecisionTest.cpp)
+#
+#   1 --10-- 2
+#   |        |
+#   10       10
+#   |        |
+#   3 --10-- 4
+#
+# DecisionTest.cpp:1522-1640 (SimpleRingTopologyFixture::CustomSetUp)
+
+bgpAddr1 = T.toIpPrefix("2401:1::10.1.1.1/32")  # DecisionTest.cpp:100
+
+
+def kspf_db(pdb, minNexthop=None):
+    """DecisionTest.cpp:147-180 (createPrefixDbWithKspfAlgo, non-BGP)."""
+    entries = []
+    for e in pdb.prefixEntries:
+        entries.append(
+            T.createPrefixEntry(
+                e.prefix,
+                forwardingType=T.PrefixForwardingType.SR_MPLS,
+                forwardingAlgorithm=T.PrefixForwardingAlgorithm.KSP2_ED_ECMP,
+                minNexthop=minNexthop,
+            )
+        )
+    return T.createPrefixDb(pdb.thisNodeName, entries)
+
+
+def ring_setup(M, v4, lfa, ksp2):
+    s = M.SpfSolver("1", v4, lfa)
+    dbs = {
+        "1": T.createAdjDb("1", [adj12, adj13], 1),
+        "2": T.createAdjDb("2", [adj21, adj24], 2),
+        "3": T.createAdjDb("3", [adj31, adj34], 3),
+        "4": T.createAdjDb("4", [adj42, adj43], 4),
+    }
+    areas, ls = single_area(M)
+    assert ls.updateAdjacencyDatabase(dbs["1"]) == (False, False, True)
+    for n in ("2", "3", "4"):
+        assert ls.updateAdjacencyDatabase(dbs[n]) == (True, False, True)
+    ps = M.PrefixState()
+    pdbs = (
+        (prefixDb1V4, prefixDb2V4, prefixDb3V4, prefixDb4V4)
+        if v4
+        else (prefixDb1, prefixDb2, prefixDb3, prefixDb4)
+    )
+    for pdb in pdbs:
+        ps.updatePrefixDatabase(kspf_db(pdb) if ksp2 else pdb)
+    return s, areas, ls, ps, dbs
+
+
+def _ring_addr(v4, i):
+    return P((addr1V4, addr2V4, addr3V4, addr4V4)[i - 1] if v4 else (addr1, addr2, addr3, addr4)[i - 1])
+
+
+def _check_ring_ecmp(rm, v4, dbs):
+    """DecisionTest.cpp:1642-1765 / 1827-1951: expected routes of every node
+    (ShortestPathTest and MultiPathTest expect the same sets on this ring)."""
+    a = lambda i: _ring_addr(v4, i)  # noqa: E731
+    exp = {
+        # node: {dst: [(adj, metric)], ...}
+        "1": {4: [(adj12, 20), (adj13, 20)], 3: [(adj13, 10)], 2: [(adj12, 10)]},
+        "2": {4: [(adj24, 10)], 3: [(adj21, 20), (adj24, 20)], 1: [(adj21, 10)]},
+        "3": {4: [(adj34, 10)], 2: [(adj31, 20), (adj34, 20)], 1: [(adj31, 10)]},
+        "4": {3: [(adj43, 10)], 2: [(adj42, 10)], 1: [(adj42, 20), (adj43, 20)]},
+    }
+    for node, dsts in exp.items():
+        for d, hops in dsts.items():
+            assert R(rm, node, a(d)) == NH(*[nh(x, v4, m) for x, m in hops]), (node, d)
+            act = (lambda m: labelPhpAction) if len(hops) == 1 and hops[0][1] == 10 else (
+                lambda m: swap(d)
+            )
+            assert R(rm, node, L(d)) == NH(
+                *[nh(x, False, m, act(m)) for x, m in hops]
+            ), (node, "label", d)
+        validate_pop_label_route(rm, node, int(node))
+        validate_adj_label_routes(rm, node, dbs[node].adjacencies)
+
+
+def sc_ring_shortest_path(M):
+    """DecisionTest.cpp:1642-1765 (ShortestPathTest): 36 routes, spf_runs 4."""
+    for v4 in (True, False):
+        M.reset_counters()
+        s, areas, ls, ps, dbs = ring_setup(M, v4, False, False)
+        rm = get_route_map(s, ["1", "2", "3", "4"], areas, ps)
+        assert len(rm) == 36
+        assert counters(M)["decision.spf_runs"] == 4
+        _check_ring_ecmp(rm, v4, dbs)
+
+
+def sc_ring_multipath_lfa(M):
+    """DecisionTest.cpp:1827-1951 (MultiPathTest, LFA on): 36 routes."""
+    for v4 in (True, False):
+        s, areas, ls, ps, dbs = ring_setup(M, v4, True, False)
+        rm = get_route_map(s, ["1", "2", "3", "4"], areas, ps)
+        assert len(rm) == 36
+        _check_ring_ecmp(rm, v4, dbs)
+
+
+def sc_ring_ksp2_ed_ecmp(M):
+    """DecisionTest.cpp:1953-2138 (Ksp2EdEcmp): 36 routes, spf_runs 16,
+    second edge-disjoint paths with PUSH label stacks, then overloads."""
+    for v4 in (True, False):
+        M.reset_counters()
+        s, areas, ls, ps, dbs = ring_setup(M, v4, True, True)
+        rm = get_route_map(s, ["1", "2", "3", "4"], areas, ps)
+        assert len(rm) == 36
+        assert counters(M)["decision.spf_runs"] == 16
+        a = lambda i: _ring_addr(v4, i)  # noqa: E731
+        n = lambda adj, m, act=None: nh(adj, v4, m, act, True)  # noqa: E731
+        exp = {
+            ("1", 4): [n(adj12, 20, push(4)), n(adj13, 20, push(4))],
+            ("1", 3): [n(adj13, 10), n(adj12, 30, push(3, 4))],
+            ("1", 2): [n(adj12, 10), n(adj13, 30, push(2, 4))],
+            ("2", 4): [n(adj24, 10), n(adj21, 30, push(4, 3))],
+            ("2", 3): [n(adj21, 20, push(3)), n(adj24, 20, push(3))],
+            ("2", 1): [n(adj21, 10), n(adj24, 30, push(1, 3))],
+            ("3", 4): [n(adj34, 10), n(adj31, 30, push(4, 2))],
+            ("3", 2): [n(adj31, 20, push(2)), n(adj34, 20, push(2))],
+            ("3", 1): [n(adj31, 10), n(adj34, 30, push(1, 2))],
+            ("4", 3): [n(adj43, 10), n(adj42, 30, push(3, 1))],
+            ("4", 2): [n(adj42, 10), n(adj43, 30, push(2, 1))],
+            ("4", 1): [n(adj42, 20, push(1)), n(adj43, 20, push(1))],
+        }
+        for (node, d), hops in exp.items():
+            assert R(rm, node, a(d)) == NH(*hops), (v4, node, d)
+        # node-label routes stay shortest-path (DecisionTest.cpp:1996-2008 ...)
+        assert R(rm, "1", L(4)) == NH(
+            nh(adj12, False, 20, swap(4)), nh(adj13, False, 20, swap(4))
+        )
+        assert R(rm, "1", L(3)) == NH(nh(adj13, False, 10, labelPhpAction))
+        for node in ("1", "2", "3", "4"):
+            validate_pop_label_route(rm, node, int(node))
+            validate_adj_label_routes(rm, node, dbs[node].adjacencies)
+        # overload link 1->2 and node 3 (DecisionTest.cpp:2116-2138)
+        db1 = dbs["1"]
+        db1.adjacencies[0].isOverloaded = True
+        dbs["3"].isOverloaded = True
+        assert ls.updateAdjacencyDatabase(db1)[0]
+        assert ls.updateAdjacencyDatabase(dbs["3"])[0]
+        db1.adjacencies[0].isOverloaded = False  # module-level adj objects are shared
+        rm = get_route_map(s, ["1"], areas, ps)
+        assert ("1",) + a(4) not in rm
+        assert R(rm, "1", a(3)) == NH(n(adj13, 10))
+        assert ("1",) + a(2) not in rm
+
+
+def sc_ring_overload_node(M):
+    """DecisionTest.cpp:2510-2623 (OverloadNodeTest): nodes 2 and 3 drained,
+    LFA on: 32 routes."""
+    for v4 in (True, False):
+        s, areas, ls, ps, dbs = ring_setup(M, v4, True, False)
+        dbs["2"].isOverloaded = True
+        dbs["3"].isOverloaded = True
+        assert ls.updateAdjacencyDatabase(dbs["2"])[0]
+        assert ls.updateAdjacencyDatabase(dbs["3"])[0]
+        rm = get_route_map(s, ["1", "2", "3", "4"], areas, ps)
+        assert len(rm) == 32
+        a = lambda i: _ring_addr(v4, i)  # noqa: E731
+        assert R(rm, "1", a(3)) == NH(nh(adj13, v4, 10))
+        assert R(rm, "1", L(3)) == NH(nh(adj13, False, 10, labelPhpAction))
+        assert R(rm, "1", a(2)) == NH(nh(adj12, v4, 10))
+        assert ("1",) + a(4) not in rm
+        assert R(rm, "2", a(4)) == NH(nh(adj24, v4, 10))
+        assert R(rm, "2", a(3)) == NH(nh(adj21, v4, 20), nh(adj24, v4, 20))
+        assert R(rm, "2", L(3)) == NH(
+            nh(adj21, False, 20, swap(3)), nh(adj24, False, 20, swap(3))
+        )
+        assert R(rm, "2", a(1)) == NH(nh(adj21, v4, 10))
+        assert R(rm, "3", a(4)) == NH(nh(adj34, v4, 10))
+        assert R(rm, "3", a(2)) == NH(nh(adj31, v4, 20), nh(adj34, v4, 20))
+        assert R(rm, "3", a(1)) == NH(nh(adj31, v4, 10))
+        assert R(rm, "4", a(3)) == NH(nh(adj43, v4, 10))
+        assert R(rm, "4", a(2)) == NH(nh(adj42, v4, 10))
+        assert ("4",) + a(1) not in rm
+        for node in ("1", "2", "3", "4"):
+            validate_pop_label_route(rm, node, int(node))
+            validate_adj_label_routes(rm, node, dbs[node].adjacencies)
+
+
+# ------------------------------------------------ Grid (DecisionTest.cpp)
+
+
+def _grid(M, n):
+    """DecisionTest.cpp:3862-3918 (addAdj / createGrid)."""
+    areas, ls = single_area(M)
+    ps = M.PrefixState()
+
+    def pfx(node):
+        return T.toIpPrefix(f"::ffff:10.1.{node // 256}.{node % 256}/128")
+
+    for i in range(n):
+        for j in range(n):
+            node = i * n + j
+            adjs = []
+            for (ii, jj, ifn, oifn) in (
+                (i, j + 1, "0/1", "0/3"),
+                (i - 1, j, "0/2", "0/4"),
+                (i, j - 1, "0/3", "0/1"),
+                (i + 1, j, "0/4", "0/2"),
+            ):
+                if 0 <= ii < n and 0 <= jj < n:
+                    nb = ii * n + jj
+                    adjs.append(
+                        T.createThriftAdjacency(
+                            str(nb), ifn, f"fe80::{nb}",
+                            f"192.168.{nb // 256}.{nb % 256}",
+                            1, 100001 + nb, False, 100, 10000, 1, oifn,
+                        )
+                    )
+            ls.updateAdjacencyDatabase(T.createAdjDb(str(node), adjs, node + 1))
+            ps.updatePrefixDatabase(
+                T.createPrefixDb(str(node), [T.createPrefixEntry(pfx(node))])
+            )
+    return areas, ps, pfx
+
+
+def sc_grid_shortest_path(M):
+    """DecisionTest.cpp:3920-4010 (GridTopologyFixture, n = 2..8 of the
+    reference's 2..16): route count 2n^4+3n^2-4n and Manhattan metrics."""
+    import random
+
+    rnd = random.Random(5)
+    for n in (2, 4, 6, 8):
+        areas, ps, pfx = _grid(M, n)
+        s = M.SpfSolver("1", False, False)
+        nodes = [str(i) for i in range(n * n)]
+        rm = get_route_map(s, nodes, areas, ps)
+        assert len(rm) == 2 * n**4 + 3 * n**2 - 4 * n, n
+
+        def dist(a, b):
+            return abs(a % n - b % n) + abs(a // n - b // n)
+
+        pairs = [(0, n * n - 1), (n - 1, n * (n - 1))]
+        pairs += [(rnd.randrange(n * n), rnd.randrange(n * n)) for _ in range(6)]
+        for a, b in pairs:
+            if a == b:
+                continue
+            hops = R(rm, str(a), P(pfx(b)))
+            assert hops and all(h[4] == dist(a, b) for h in hops), (n, a, b)
+
+
+# ------------------------------------- ParallelAdjRing (DecisionTest.cpp)
+
+adj12_1 = T.createAdjacency("2", "2/1", "1/1", "fe80::2:1", "192.168.2.1", 11, 201)
+adj12_2 = T.createAdjacency("2", "2/2", "1/2", "fe80::2:2", "192.168.2.2", 11, 202)
+adj12_3 = T.createAdjacency("2", "2/3", "1/3", "fe80::2:3", "192.168.2.3", 20, 203)
+adj13_1 = T.createAdjacency("3", "3/1", "1/1", "fe80::3:1", "192.168.3.1", 11, 301)
+adj21_1 = T.createAdjacency("1", "1/1", "2/1", "fe80::1:1", "192.168.1.1", 11, 101)
+adj21_2 = T.createAdjacency("1", "1/2", "2/2", "fe80::1:2", "192.168.1.2", 11, 102)
+adj21_3 = T.createAdjacency("1", "1/3", "2/3", "fe80::1:3", "192.168.1.3", 20, 103)
+adj24_1 = T.createAdjacency("4", "4/1", "2/1", "fe80::4:1", "192.168.4.1", 11, 401)
+adj31_1 = T.createAdjacency("1", "1/1", "3/1", "fe80::1:1", "192.168.1.1", 11, 101)
+adj34_1 = T.createAdjacency("4", "4/1", "3/1", "fe80::4:1", "192.168.4.1", 11, 401)
+adj34_2 = T.createAdjacency("4", "4/2", "3/2", "fe80::4:2", "192.168.4.2", 20, 402)
+adj34_3 = T.createAdjacency("4", "4/3", "3/3", "fe80::4:3", "192.168.4.3", 20, 403)
+adj42_1 = T.createAdjacency("2", "2/1", "4/1", "fe80::2:1", "192.168.2.1", 11, 201)
+adj43_1 = T.createAdjacency("3", "3/1", "4/1", "fe80::3:1", "192.168.3.1", 11, 301)
+adj43_2 = T.createAdjacency("3", "3/2", "4/2", "fe80::3:2", "192.168.3.2", 20, 302)
+adj43_3 = T.createAdjacency("3", "3/3", "4/3", "fe80::3:3", "192.168.3.3", 20, 303)
+
+
+def par_setup(M, lfa, ksp2):
+    """DecisionTest.cpp:2824-2925 (ParallelAdjRingTopologyFixture)."""
+    import copy
+
+    s = M.SpfSolver("1", False, lfa)
+    dbs = {
+        "1": T.createAdjDb("1", copy.deepcopy([adj12_1, adj12_2, adj12_3, adj13_1]), 1),
+        "2": T.createAdjDb("2", copy.deepcopy([adj21_1, adj21_2, adj21_3, adj24_1]), 2),
+        "3": T.createAdjDb("3", copy.deepcopy([adj31_1, adj34_1, adj34_2, adj34_3]), 3),
+        "4": T.createAdjDb("4", copy.deepcopy([adj42_1, adj43_1, adj43_2, adj43_3]), 4),
+    }
+    areas, ls = single_area(M)
+    assert not ls.updateAdjacencyDatabase(dbs["1"])[0]
+    for n in ("2", "3", "4"):
+        assert ls.updateAdjacencyDatabase(dbs[n])[0]
+    ps = M.PrefixState()
+    for pdb in (prefixDb1, prefixDb2, prefixDb3, prefixDb4):
+        ps.updatePrefixDatabase(kspf_db(pdb) if ksp2 else pdb)
+    return s, areas, ls, ps, dbs
+
+
+def sc_parallel_ring_shortest_path(M):
+    """DecisionTest.cpp:2932-3052 (ShortestPathTest): 44 routes, ECMP over
+    parallel links."""
+    s, areas, ls, ps, dbs = par_setup(M, False, False)
+    rm = get_route_map(s, ["1", "2", "3", "4"], areas, ps)
+    assert len(rm) == 44
+    exp = {
+        ("1", 4): [(adj12_2, 22), (adj13_1, 22), (adj12_1, 22)],
+        ("1", 3): [(adj13_1, 11)],
+        ("1", 2): [(adj12_2, 11), (adj12_1, 11)],
+        ("2", 4): [(adj24_1, 11)],
+        ("2", 3): [(adj21_2, 22), (adj21_1, 22), (adj24_1, 22)],
+        ("2", 1): [(adj21_2, 11), (adj21_1, 11)],
+        ("3", 4): [(adj34_1, 11)],
+        ("3", 2): [(adj31_1, 22), (adj34_1, 22)],
+        ("3", 1): [(adj31_1, 11)],
+        ("4", 3): [(adj43_1, 11)],
+        ("4", 2): [(adj42_1, 11)],
+        ("4", 1): [(adj42_1, 22), (adj43_1, 22)],
+    }
+    addrs = {1: addr1, 2: addr2, 3: addr3, 4: addr4}
+    for (node, d), hops in exp.items():
+        assert R(rm, node, P(addrs[d])) == NH(*[nh(x, False, m) for x, m in hops])
+        act = labelPhpAction if hops[0][1] == 11 else swap(d)
+        assert R(rm, node, L(d)) == NH(*[nh(x, False, m, act) for x, m in hops])
+    for node in ("1", "2", "3", "4"):
+        validate_pop_label_route(rm, node, int(node))
+        validate_adj_label_routes(rm, node, dbs[node].adjacencies)
+
+
+def sc_parallel_ring_ksp2(M):
+    """DecisionTest.cpp:3213-3385 (Ksp2EdEcmp, non-BGP instance): parallel
+    links in KSP2 traces, minNexthop thresholds, then link overloads (the
+    adj12_1-vs-adj12_2 choice there depends on folly's pair hash)."""
+    s, areas, ls, ps, dbs = par_setup(M, True, True)
+    rm = get_route_map(s, ["1"], areas, ps)
+    n = lambda adj, m, act=None: nh(adj, False, m, act, True)  # noqa: E731
+    assert R(rm, "1", P(addr2)) == NH(n(adj12_1, 11), n(adj12_2, 11), n(adj12_3, 20))
+    # extra prefix from node 4 with minNexthop 4 -> dropped
+    base4 = kspf_db(prefixDb4)
+
+    def with_bgp(db, mnh):
+        e = T.createPrefixEntry(
+            bgpAddr1, T.PrefixType.LOOPBACK, "", T.PrefixForwardingType.SR_MPLS,
+            T.PrefixForwardingAlgorithm.KSP2_ED_ECMP, None, None, mnh,
+        )
+        return T.createPrefixDb(db.thisNodeName, list(db.prefixEntries) + [e])
+
+    ps.updatePrefixDatabase(with_bgp(base4, 4))
+    rm = get_route_map(s, ["1"], areas, ps)
+    assert ("1",) + P(bgpAddr1) not in rm
+    ps.updatePrefixDatabase(with_bgp(base4, 2))
+    rm = get_route_map(s, ["1"], areas, ps)
+    assert R(rm, "1", P(bgpAddr1)) == NH(n(adj12_2, 22, push(4)), n(adj13_1, 22, push(4)))
+    base3 = kspf_db(prefixDb3)
+    ps.updatePrefixDatabase(with_bgp(base3, 4))
+    rm = get_route_map(s, ["1"], areas, ps)
+    assert ("1",) + P(bgpAddr1) not in rm
+    ps.updatePrefixDatabase(base4)
+    ps.updatePrefixDatabase(base3)
+    # overload adj12_2 and adj34_2 (DecisionTest.cpp:3322-3330)
+    dbs["1"].adjacencies[1].isOverloaded = True
+    dbs["3"].adjacencies[2].isOverloaded = True
+    assert ls.updateAdjacencyDatabase(dbs["1"])[0]
+    assert ls.updateAdjacencyDatabase(dbs["3"])[0]
+    rm = get_route_map(s, ["1", "2", "3", "4"], areas, ps)
+    assert len(rm) == 44
+    exp = {
+        ("1", 4): [n(adj12_1, 22, push(4)), n(adj13_1, 22, push(4))],
+        ("1", 3): [n(adj13_1, 11), n(adj12_1, 33, push(3, 4))],
+        ("1", 2): [n(adj12_1, 11), n(adj12_3, 20)],
+        ("2", 4): [n(adj24_1, 11), n(adj21_1, 33, push(4, 3))],
+        ("2", 3): [n(adj21_1, 22, push(3)), n(adj24_1, 22, push(3))],
+        ("2", 1): [n(adj21_1, 11), n(adj21_3, 20)],
+        ("3", 4): [n(adj34_1, 11), n(adj34_3, 20)],
+        ("3", 2): [n(adj31_1, 22, push(2)), n(adj34_1, 22, push(2))],
+        ("3", 1): [n(adj31_1, 11), n(adj34_1, 33, push(1, 2))],
+        ("4", 3): [n(adj43_1, 11), n(adj43_3, 20)],
+        ("4", 2): [n(adj42_1, 11), n(adj43_1, 33, push(2, 1))],
+        ("4", 1): [n(adj42_1, 22, push(1)), n(adj43_1, 22, push(1))],
+    }
+    addrs = {1: addr1, 2: addr2, 3: addr3, 4: addr4}
+    for (node, d), hops in exp.items():
+        assert R(rm, node, P(addrs[d])) == NH(*hops), (node, d)
+
+
+# ------------------------------------------------- LFA (DecisionTest.cpp)
+
+
+def sc_loop_free_alternates(M):
+    """DecisionTest.cpp:5222-5357 (LoopFreeAlternatePaths), run through
+    SpfSolver directly with computeLfaPaths=true (the fixture's Decision
+    is built with LFA on): triangle 1-2 (10), 1-3 (8), 2-3 (9)."""
+    import copy
+
+    a12 = T.createAdjacency("2", "1/2", "2/1", "fe80::2", "192.168.0.2", 10, 0)
+    a13 = T.createAdjacency("3", "1/3", "3/1", "fe80::3", "192.168.0.3", 8, 0)
+    a21 = T.createAdjacency("1", "2/1", "1/2", "fe80::1", "192.168.0.1", 10, 0)
+    a23 = T.createAdjacency("3", "2/3", "3/2", "fe80::3", "192.168.0.3", 9, 0)
+    a31 = T.createAdjacency("1", "3/1", "1/3", "fe80::1", "192.168.0.1", 8, 0)
+    a32 = T.createAdjacency("2", "3/2", "2/3", "fe80::2", "192.168.0.2", 9, 0)
+    areas, ls = single_area(M)
+    ps = M.PrefixState()
+    ls.updateAdjacencyDatabase(T.createAdjDb("1", [a12, a13], 0))
+    ls.updateAdjacencyDatabase(T.createAdjDb("2", [a21, a23], 0))
+    ls.updateAdjacencyDatabase(T.createAdjDb("3", [a31, a32], 0))
+    for pdb in (prefixDb1, prefixDb2, prefixDb3):
+        ps.updatePrefixDatabase(pdb)
+    s = M.SpfSolver("1", False, True)
+    rm = get_route_map(s, ["1", "2", "3"], areas, ps)
+    f = lambda adj, m: nh(adj, False, m)  # noqa: E731
+    assert R(rm, "1", P(addr2)) == NH(f(a12, 10), f(a13, 17))
+    assert R(rm, "1", P(addr3)) == NH(f(a12, 19), f(a13, 8))
+    assert R(rm, "2", P(addr1)) == NH(f(a21, 10), f(a23, 17))
+    assert R(rm, "2", P(addr3)) == NH(f(a21, 18), f(a23, 9))
+    assert R(rm, "3", P(addr1)) == NH(f(a31, 8), f(a32, 19))
+    assert R(rm, "3", P(addr2)) == NH(f(a31, 18), f(a32, 9))
+    # raise 1-2 to 100: no LFA from node 3 any more
+    a12 = copy.deepcopy(a12)
+    a21 = copy.deepcopy(a21)
+    a12.metric = 100
+    a21.metric = 100
+    ls.updateAdjacencyDatabase(T.createAdjDb("1", [a12, a13], 0))
+    ls.updateAdjacencyDatabase(T.createAdjDb("2", [a21, a23], 0))
+    rm = get_route_map(s, ["1", "2", "3"], areas, ps)
+    assert R(rm, "1", P(addr2)) == NH(f(a12, 100), f(a13, 17))
+    assert R(rm, "1", P(addr3)) == NH(f(a12, 109), f(a13, 8))
+    assert R(rm, "2", P(addr1)) == NH(f(a21, 100), f(a23, 17))
+    assert R(rm, "2", P(addr3)) == NH(f(a21, 108), f(a23, 9))
+    assert R(rm, "3", P(addr1)) == NH(f(a31, 8))
+    assert R(rm, "3", P(addr2)) == NH(f(a32, 9))

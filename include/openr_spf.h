@@ -126,6 +126,14 @@ int spf_query_run(spf_query* q);
 int spf_query_sync(spf_query* q);
 /* Device time of the last run's kernels (HIP events), milliseconds. */
 int spf_query_elapsed_ms(spf_query* q, float* ms);
+/* Device time of the last run split per stage: the distance kernel (plus
+ * its small setup memset) and the next-hop kernel of two-stage plans
+ * (nh_ms = 0 for single-kernel plans). */
+int spf_query_stage_ms(spf_query* q, float* dist_ms, float* nh_ms);
+/* The same split for each of the last min(n, runs, 64) runs, oldest first
+ * (lets a caller time a loop of asynchronous runs per kernel). */
+int spf_query_stage_history(
+    spf_query* q, uint32_t n, float* dist_ms, float* nh_ms, uint32_t* got);
 /* Name of the kernel the last run used ("lds", "gmem", "exact"). */
 const char* spf_query_kernel_name(const spf_query* q);
 

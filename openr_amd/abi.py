@@ -42,6 +42,8 @@ EXPORTED_SYMBOLS = (
     "spf_query_run",
     "spf_query_sync",
     "spf_query_elapsed_ms",
+    "spf_query_stage_ms",
+    "spf_query_stage_history",
     "spf_query_kernel_name",
     "spf_query_dist",
     "spf_query_nh_words",
@@ -117,6 +119,14 @@ def load():
         "spf_query_run": (C.c_int, [vp]),
         "spf_query_sync": (C.c_int, [vp]),
         "spf_query_elapsed_ms": (C.c_int, [vp, C.POINTER(C.c_float)]),
+        "spf_query_stage_ms": (
+            C.c_int,
+            [vp, C.POINTER(C.c_float), C.POINTER(C.c_float)],
+        ),
+        "spf_query_stage_history": (
+            C.c_int,
+            [vp, u32, C.POINTER(C.c_float), C.POINTER(C.c_float), pu32],
+        ),
         "spf_query_kernel_name": (C.c_char_p, [vp]),
         "spf_query_dist": (C.c_int, [vp, u32, pu64]),
         "spf_query_nh_words": (C.c_int, [vp, u32]),
@@ -321,6 +331,20 @@ class Query:
         ms = C.c_float()
         _check(load().spf_query_elapsed_ms(self.h, C.byref(ms)), "elapsed")
         return float(ms.value)
+
+    def stage_ms(self):
+        """(distance-kernel ms, next-hop-kernel ms) of the last run."""
+        a, b = C.c_float(), C.c_float()
+        _check(load().spf_query_stage_ms(self.h, C.byref(a), C.byref(b)), "stage_ms")
+        return float(a.value), float(b.value)
+
+    def stage_history(self, n: int):
+        """[(distance ms, next-hop ms)] of the last min(n, 64) runs."""
+        d = (C.c_float * max(n, 1))()
+        h = (C.c_float * max(n, 1))()
+        got = C.c_uint32()
+        _check(load().spf_query_stage_history(self.h, n, d, h, C.byref(got)), "stage_history")
+        return [(float(d[i]), float(h[i])) for i in range(got.value)]
 
     @property
     def kernel(self) -> str:

@@ -1177,7 +1177,15 @@ struct spf_query {
   void* d_dist = nullptr;
   uint64_t* d_nh = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t evm = nullptr; // after the distance stage, before next hops
   bool ran = false;
+  bool two_stage = false; // evm recorded between two kernels
+  // per-run event triples (start, after distance stage, end) of the last
+  // kHist runs, for per-kernel averages over a timed loop without syncs
+  static constexpr uint32_t kHist = 64;
+  hipEvent_t hist[kHist][3] = {};
+  bool hist_two[kHist] = {};
+  uint64_t runs = 0;
 };
 
 namespace {
@@ -1232,6 +1240,16 @@ void free_query(spf_query* q) {
   }
   if (q->ev1) {
     (void)hipEventDestroy(q->ev1);
+  }
+  if (q->evm) {
+    (void)hipEventDestroy(q->evm);
+  }
+  for (auto& h : q->hist) {
+    for (hipEvent_t e : h) {
+      if (e) {
+        (void)hipEventDestroy(e);
+      }
+    }
   }
   delete q;
 }
@@ -1722,7 +1740,8 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     }
   }
   if (hipEventCreate(&q->ev0) != hipSuccess ||
-      hipEventCreate(&q->ev1) != hipSuccess) {
+      hipEventCreate(&q->ev1) != hipSuccess ||
+      hipEventCreate(&q->evm) != hipSuccess) {
     return bail(fail(SPF_E_DEVICE, "hipEventCreate failed"));
   }
   *out = q;
@@ -1960,6 +1979,15 @@ int launch_exact(spf_query* q) {
   return SPF_OK;
 }
 
+// Event between the distance kernel and the next-hop kernel of a two-stage
+// plan, so spf_query_stage_ms can split the device time per kernel.
+int mark_stage(spf_query* q) {
+  HIP_TRY(hipEventRecord(q->evm, q->g->stream));
+  HIP_TRY(hipEventRecord(q->hist[q->runs % spf_query::kHist][1], q->g->stream));
+  q->two_stage = true;
+  return SPF_OK;
+}
+
 int run_plan(spf_query* q) {
   const bool unit = q->flags & SPF_F_UNIT_METRIC;
   switch (q->dist) {
@@ -1968,7 +1996,10 @@ int run_plan(spf_query* q) {
   case DistPlan::MsBfs: {
     int s = launch_msbfs(q, unit);
     if (s == SPF_OK && q->nh == NhPlan::Levels) {
-      s = launch_nh_levels(q, unit);
+      s = mark_stage(q);
+      if (s == SPF_OK) {
+        s = launch_nh_levels(q, unit);
+      }
     }
     return s;
   }
@@ -1976,7 +2007,10 @@ int run_plan(spf_query* q) {
   case DistPlan::BfsGmem: {
     int s = launch_bfs(q, unit);
     if (s == SPF_OK && q->nh == NhPlan::Rows) {
-      s = launch_nh_rows(q, unit);
+      s = mark_stage(q);
+      if (s == SPF_OK) {
+        s = launch_nh_rows(q, unit);
+      }
     }
     return s;
   }
@@ -1998,7 +2032,10 @@ int run_plan(spf_query* q) {
       break;
     }
     if (s == SPF_OK && q->nh == NhPlan::Rows) {
-      s = launch_nh_rows(q, unit);
+      s = mark_stage(q);
+      if (s == SPF_OK) {
+        s = launch_nh_rows(q, unit);
+      }
     }
     return s;
   }
@@ -2015,12 +2052,23 @@ int spf_query_run(spf_query* q) {
   }
   spf_graph* g = q->g;
   HIP_TRY(hipSetDevice(g->device));
+  const uint32_t h = q->runs % spf_query::kHist;
+  if (!q->hist[h][0]) {
+    for (auto& e : q->hist[h]) {
+      HIP_TRY(hipEventCreate(&e));
+    }
+  }
   HIP_TRY(hipEventRecord(q->ev0, g->stream));
+  HIP_TRY(hipEventRecord(q->hist[h][0], g->stream));
+  q->two_stage = false;
   int s = SPF_OK;
   if (q->nq && g->V) {
     s = run_plan(q);
   }
   HIP_TRY(hipEventRecord(q->ev1, g->stream));
+  HIP_TRY(hipEventRecord(q->hist[h][2], g->stream));
+  q->hist_two[h] = q->two_stage;
+  ++q->runs;
   q->ran = true;
   return s;
 }
@@ -2040,6 +2088,44 @@ int spf_query_elapsed_ms(spf_query* q, float* ms) {
   }
   HIP_TRY(hipEventSynchronize(q->ev1));
   HIP_TRY(hipEventElapsedTime(ms, q->ev0, q->ev1));
+  return SPF_OK;
+}
+
+int spf_query_stage_ms(spf_query* q, float* dist_ms, float* nh_ms) {
+  if (!q || !dist_ms || !nh_ms || !q->ran) {
+    return fail(SPF_E_INVALID, "query has not run");
+  }
+  HIP_TRY(hipEventSynchronize(q->ev1));
+  if (q->two_stage) {
+    HIP_TRY(hipEventElapsedTime(dist_ms, q->ev0, q->evm));
+    HIP_TRY(hipEventElapsedTime(nh_ms, q->evm, q->ev1));
+  } else {
+    HIP_TRY(hipEventElapsedTime(dist_ms, q->ev0, q->ev1));
+    *nh_ms = 0.0f;
+  }
+  return SPF_OK;
+}
+
+int spf_query_stage_history(
+    spf_query* q, uint32_t n, float* dist_ms, float* nh_ms, uint32_t* got) {
+  if (!q || !got || (n && (!dist_ms || !nh_ms))) {
+    return fail(SPF_E_INVALID, "bad arguments");
+  }
+  const uint64_t avail = std::min<uint64_t>(q->runs, spf_query::kHist);
+  const uint32_t m = (uint32_t)std::min<uint64_t>(n, avail);
+  for (uint32_t i = 0; i < m; ++i) {
+    // oldest of the last m runs first
+    const uint32_t h = (uint32_t)((q->runs - m + i) % spf_query::kHist);
+    HIP_TRY(hipEventSynchronize(q->hist[h][2]));
+    if (q->hist_two[h]) {
+      HIP_TRY(hipEventElapsedTime(&dist_ms[i], q->hist[h][0], q->hist[h][1]));
+      HIP_TRY(hipEventElapsedTime(&nh_ms[i], q->hist[h][1], q->hist[h][2]));
+    } else {
+      HIP_TRY(hipEventElapsedTime(&dist_ms[i], q->hist[h][0], q->hist[h][2]));
+      nh_ms[i] = 0.0f;
+    }
+  }
+  *got = m;
   return SPF_OK;
 }
 

@@ -1,0 +1,195 @@
+"""Golden fixtures (tests/golden/, made by tests/golden/make_golden.py).
+
+CPU ("not gpu"): the WAN generator + an independent scipy Dijkstra and the
+CPU oracle reproduce the checksums the REFERENCE's runSpf produced
+(wan_anchors.json); the oracle reproduces its own config-1
+and fabric goldens (regression guard for the checker).
+GPU: the MI355X engine — through the C ABI and through the engine-backed
+LinkState / SpfSolver — reproduces every golden bit-exactly.
+"""
+
+import json
+import os
+
+import numpy as np
+import pytest
+
+from tests.golden.make_golden import (
+    FABRIC_SOURCES,
+    KSP2_DESTS,
+    canon,
+    digest,
+    load,
+    spf_canon,
+)
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _gold(name):
+    return json.load(open(os.path.join(GOLD, name)))
+
+
+def _wan_sources(topo, S):
+    r, _ = topo.rank()
+    V = topo.num_nodes
+    return [int(r[(s * 7919) % V]) for s in range(S)]
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    from oracle import build
+
+    build.build()
+    from oracle import _oracle_ref
+
+    return _oracle_ref
+
+
+@pytest.mark.parametrize("idx", [0, 1, 2])
+def test_wan_generator_matches_reference_checksums(idx):
+    import scipy.sparse as sp
+    import scipy.sparse.csgraph as cg
+
+    from openr_amd import topologies as TP
+
+    a = _gold("wan_anchors.json")["anchors"][idx]
+    topo = TP.wan(a["V"], a["L"])
+    csr = topo.csr()
+    V = csr.num_nodes
+    A = sp.csr_matrix((csr.metric.astype(np.float64), csr.col, csr.row_ptr), shape=(V, V))
+    D = cg.dijkstra(A, indices=_wan_sources(topo, a["S"]))
+    assert np.isfinite(D).all()
+    assert int(D.sum()) == a["sum_dist"]
+
+
+def test_oracle_matches_reference_wan_checksum(oracle):
+    """The C++ oracle's runSpf (reference data structures) on the 10k WAN
+    reproduces the reference checksum (5 of the 20 sources + scipy for the
+    rest would not pin anything: all 20 are run, ~2 s each)."""
+    from openr_amd import topologies as TP
+
+    a = _gold("wan_anchors.json")["anchors"][0]
+    topo = TP.wan(a["V"], a["L"])
+    areas, ls, ps = load(oracle, topo)
+    V = topo.num_nodes
+    total = 0
+    for s in range(a["S"]):
+        res = ls.getSpfResult(topo.names[(s * 7919) % V], True)
+        assert len(res) == V
+        total += sum(v[0] for v in res.values())
+    assert total == a["sum_dist"]
+
+
+def test_oracle_grid10_golden(oracle):
+    from openr_amd import thrift as T
+    from openr_amd import topologies as TP
+
+    gold = _gold("grid10.json")
+    g = TP.grid(10)
+    for tag, ft, fa in (
+        ("sp_ecmp_lfa", 0, 0),
+        ("ksp2_ed_ecmp", T.PrefixForwardingType.SR_MPLS, T.PrefixForwardingAlgorithm.KSP2_ED_ECMP),
+    ):
+        areas, ls, ps = load(oracle, g, "0", ft, fa)
+        db = oracle.SpfSolver("1", False, gold[tag]["lfa"]).buildRouteDb("1", areas, ps)
+        assert len(db["unicast"]) == gold[tag]["num_unicast"] == 99
+        assert digest(db) == gold[tag]["digest"]
+
+
+def test_oracle_fabric_golden(oracle):
+    from openr_amd import topologies as TP
+
+    gold = _gold("fabric_sampled.json")
+    areas, ls, ps = load(oracle, TP.fabric(10000))
+    for src in FABRIC_SOURCES[:3]:
+        assert digest(spf_canon(ls.getSpfResult(src, True))) == gold["spf"][src]["digest"]
+    for d in KSP2_DESTS[:2]:
+        for k in (1, 2):
+            got = [[list(l.key()) for l in p] for p in ls.getKthPaths("2-0-0", d, k)]
+            assert canon(got) == gold["ksp2"][d][str(k)]
+
+
+# ------------------------------------------------------------------ GPU
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("idx", [0, 1, 2])
+def test_engine_wan_reference_checksums(gpu_ready, idx):
+    from openr_amd import abi
+    from openr_amd import topologies as TP
+
+    a = _gold("wan_anchors.json")["anchors"][idx]
+    topo = TP.wan(a["V"], a["L"])
+    g = abi.Graph(topo.csr())
+    srcs = _wan_sources(topo, a["S"])
+    q = g.query(np.asarray(srcs, dtype=np.uint32), abi.SPF_F_NEXTHOPS).run()
+    total = 0
+    for i in range(len(srcs)):
+        d = q.dist(i)
+        assert (d != np.uint64(abi.SPF_UNREACHABLE)).all()
+        total += int(d.sum())
+    assert total == a["sum_dist"]
+
+
+@pytest.mark.gpu
+def test_engine_grid10_golden(gpu_ready):
+    import openr_amd._openr_spf as E
+    from openr_amd import thrift as T
+    from openr_amd import topologies as TP
+
+    gold = _gold("grid10.json")
+    g = TP.grid(10)
+    for tag, ft, fa in (
+        ("sp_ecmp_lfa", 0, 0),
+        ("ksp2_ed_ecmp", T.PrefixForwardingType.SR_MPLS, T.PrefixForwardingAlgorithm.KSP2_ED_ECMP),
+    ):
+        areas, ls, ps = load(E, g, "0", ft, fa)
+        db = E.SpfSolver("1", False, gold[tag]["lfa"]).buildRouteDb("1", areas, ps)
+        assert digest(db) == gold[tag]["digest"], tag
+
+
+@pytest.mark.gpu
+def test_engine_fabric_golden(gpu_ready):
+    import openr_amd._openr_spf as E
+    from openr_amd import topologies as TP
+
+    gold = _gold("fabric_sampled.json")
+    areas, ls, ps = load(E, TP.fabric(10000))
+    ls.prefetchSpf(FABRIC_SOURCES)
+    for src in FABRIC_SOURCES:
+        c = spf_canon(ls.getSpfResult(src, True))
+        assert len(c) == gold["spf"][src]["reached"]
+        assert digest(c) == gold["spf"][src]["digest"], src
+    ls.prefetchKthPaths("2-0-0", KSP2_DESTS)
+    for d in KSP2_DESTS:
+        for k in (1, 2):
+            got = [[list(l.key()) for l in p] for p in ls.getKthPaths("2-0-0", d, k)]
+            assert canon(got) == gold["ksp2"][d][str(k)], (d, k)
+
+
+@pytest.mark.gpu
+def test_engine_whatif_golden(gpu_ready):
+    """Single-link-failure SPFs (config 5 semantics) as one ignore-list batch."""
+    from openr_amd import abi
+    from openr_amd import topologies as TP
+
+    gold = _gold("whatif_fabric.json")
+    f = TP.fabric(10000)
+    csr = f.csr()
+    r, names_by_rank = f.rank()
+    lid_of = {(f.names[a], f.names[b]): i for i, (a, b, _, _) in enumerate(f.links)}
+    qs = gold["queries"]
+    srcs = np.asarray([int(r[f.names.index(x["src"])]) for x in qs], dtype=np.uint32)
+    ign = [[lid_of[tuple(x["link"])]] for x in qs]
+    g = abi.Graph(csr)
+    q = g.query(srcs, abi.SPF_F_NEXTHOPS, ignore=ign).run()
+    for i, x in enumerate(qs):
+        d = q.dist(i)
+        nh = q.nexthop_sets(i, int(srcs[i]))
+        c = {
+            names_by_rank[v]: (int(d[v]), sorted(names_by_rank[h] for h in nh[v]))
+            for v in nh
+        }
+        assert len(c) == x["reached"]
+        assert digest(c) == x["digest"], x

@@ -12,12 +12,26 @@ of drain scenario r (rank 0: no drain; rank r > 0: one RSW drained), no
 collective on the data path.  `value` = SPFs of all ranks / max-over-ranks
 step time.
 
+Roofline: the dominant kernel of the step (the one with the larger average
+device time over the timed launches, HIP events on the engine's stream) is
+priced by its ALGORITHMIC bytes per launch:
+  spf_nh_levels_kernel  sum_q [ V*(1 + nbrs(q)) * b + 8*V*W_q ]
+                         (own level row + one row per distinct neighbour of
+                          the source, b = 1 byte per 8-bit level, 4 if the
+                          32-bit rows are used; next-hop mask row written)
+  spf_msbfs_kernel      sum_q 5*V + levels * (4*E + 4*(V+1)) per 64-source
+                         batch (dist u32 + level u8 rows written; CSR scanned
+                         once per BFS level)
+`traffic` comes from the rocprofv3 PMC passes committed under profiles/
+(profiles/<round>/pmc_traffic.json, written by profiles/collect_pmc.py).
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
 """
 
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -26,7 +40,15 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+
+KERNELS = {
+    "msbfs+levels": ("spf_msbfs_kernel", "spf_nh_levels_kernel"),
+    "bfs+rows": ("spf_bfs_kernel", "spf_nh_rows_kernel"),
+    "bfs-gmem+rows": ("spf_bfs_kernel", "spf_nh_rows_kernel"),
+    "lds+rows": ("spf_sssp_kernel", "spf_nh_rows_kernel"),
+    "gmem+rows": ("spf_sssp_kernel", "spf_nh_rows_kernel"),
+}
 
 
 def parse():
@@ -41,13 +63,44 @@ def parse():
     return p.parse_args()
 
 
-def algorithmic_bytes(csr, nh_words):
-    """SURVEY §8(d) per-SSSP bytes: 8E + 4(V+1) + 4V + 8V*Wm, summed over
-    the batch (Wm = next-hop mask words of each source)."""
+def distinct_nbrs(csr):
+    """Distinct neighbours per node (= bits of its next-hop masks)."""
+    import numpy as np
+
+    V = csr.num_nodes
+    row = csr.row_ptr.astype(np.int64)
+    src = np.repeat(np.arange(V, dtype=np.int64), np.diff(row))
+    key = np.unique(src * V + csr.col.astype(np.int64))
+    return np.bincount(key // V, minlength=V)
+
+
+def nh_levels_bytes(csr, nbrs, nh_words, level_bytes=1):
+    import numpy as np
+
+    V = csr.num_nodes
+    w = np.asarray(nh_words, dtype=np.int64)
+    return int(V * level_bytes * (len(w) + int(nbrs.sum())) + 8 * V * int(w.sum()))
+
+
+def msbfs_bytes(csr, nsrc, levels_per_batch):
     V = csr.num_nodes
     E = len(csr.col)
-    per = 8 * E + 4 * (V + 1) + 4 * V
-    return per * len(nh_words) + 8 * V * int(sum(nh_words))
+    return int(5 * V * nsrc + sum(levels_per_batch) * (4 * E + 4 * (V + 1)))
+
+
+def pmc_traffic(kernel_name):
+    """Per-launch HBM bytes of `kernel_name` from the committed PMC passes
+    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        k = d.get("kernels", {}).get(kernel_name)
+        if k and "hbm_bytes_per_launch" in k:
+            return int(k["hbm_bytes_per_launch"]), os.path.relpath(f, ROOT)
+    return None, None
 
 
 def cpu_baseline(topo, sample):
@@ -82,27 +135,21 @@ def cpu_baseline(topo, sample):
     }
 
 
-def route_db_rebuild_ms(topo, device, iters=5):
-    """Full RouteDb rebuild of the benchmark node "2-0-0" after an RSW
-    overload toggle (the DecisionBenchmark BM_DecisionFabric loop,
-    DecisionBenchmark.cpp:600-626): LinkState update + device graph rebuild
-    + SPF (LFA off, as the benchmark's Decision) + RouteDb."""
-    import openr_amd._openr_spf as E
-    from openr_amd import thrift as T
-
-    E.set_spf_device(device)
-    areas = E.AreaLinkStates()
+def _rebuild_loop(M, topo, iters, timed):
+    """DecisionBenchmark BM_DecisionFabric loop (DecisionBenchmark.cpp:
+    600-626): toggle an RSW's overload bit, rebuild the RouteDb of "2-0-0"."""
+    areas = M.AreaLinkStates()
     ls = areas.add("0")
     dbs = topo.adj_dbs()
     for db in dbs:
         ls.updateAdjacencyDatabase(db)
-    ps = E.PrefixState()
+    ps = M.PrefixState()
     for pdb in topo.prefix_dbs():
         ps.updatePrefixDatabase(pdb)
-    solver = E.SpfSolver("2-0-0", False, False)
-    solver.buildRouteDbTimed("2-0-0", areas, ps)  # cold: builds the device graph
+    solver = M.SpfSolver("2-0-0", False, False)
+    timed(solver, areas, ps)  # cold build (device graph for the engine)
     rsw = [i for i, n in enumerate(topo.names) if n.startswith("3-")]
-    times, builds = [], []
+    tot, upd, bld = [], [], []
     routes = 0
     for it in range(iters):
         db = dbs[rsw[(it * 7919) % len(rsw)]]
@@ -110,16 +157,59 @@ def route_db_rebuild_ms(topo, device, iters=5):
             db.isOverloaded = overloaded
             t0 = time.perf_counter()
             ls.updateAdjacencyDatabase(db)
-            nu, nm, us = solver.buildRouteDbTimed("2-0-0", areas, ps)
-            times.append((time.perf_counter() - t0) * 1000.0)
-            builds.append(us / 1000.0)
-            routes = nu + nm
-    times.sort()
-    builds.sort()
-    return {"ms_median": round(times[len(times) // 2], 3),
-            "build_ms_median": round(builds[len(builds) // 2], 3),
-            "routes": routes, "node": "2-0-0", "samples": len(times),
-            "what": "adj-db update (RSW overload toggle) + buildRouteDb, LFA off"}
+            t1 = time.perf_counter()
+            routes, us = timed(solver, areas, ps)
+            t2 = time.perf_counter()
+            tot.append((t2 - t0) * 1e3)
+            upd.append((t1 - t0) * 1e3)
+            bld.append(us / 1e3)
+    med = lambda x: round(sorted(x)[len(x) // 2], 3)  # noqa: E731
+    return {"ms_median": med(tot), "update_ms_median": med(upd),
+            "build_ms_median": med(bld), "routes": routes, "samples": len(tot)}
+
+
+def route_db_rebuild_ms(topo, device, iters=5):
+    """Full RouteDb rebuild of the benchmark node "2-0-0" after an RSW
+    overload toggle: LinkState update + SPF on the engine (LFA off, as the
+    benchmark's Decision) + RouteDb."""
+    import openr_amd._openr_spf as E
+
+    E.set_spf_device(device)
+
+    def timed(solver, areas, ps):
+        nu, nm, us = solver.buildRouteDbTimed("2-0-0", areas, ps)
+        return nu + nm, us
+
+    E.reset_counters()
+    out = _rebuild_loop(E, topo, iters, timed)
+    c = E.get_counters()
+    n = max(1, c.get("decision.route_build_runs", 1))
+    out["per_build_us"] = {
+        k.split(".", 1)[1]: round(c.get(k, 0) / n, 1)
+        for k in ("decision.graph_build_us", "decision.graph_upload_us",
+                  "decision.spf_batch_us", "decision.spf_device_us",
+                  "decision.route_prefetch_us")
+    }
+    out["node"] = "2-0-0"
+    out["what"] = "adj-db update (RSW overload toggle) + buildRouteDb, LFA off"
+    return out
+
+
+def route_db_rebuild_cpu(topo, iters=2):
+    """The same loop on the oracle (reference data structures), 1 thread."""
+    from oracle import build as obuild
+
+    obuild.build()
+    from oracle import _oracle_ref as O
+
+    def timed(solver, areas, ps):
+        nu, nm, us = solver.buildRouteDbTimed("2-0-0", areas, ps)
+        return nu + nm, us
+
+    out = _rebuild_loop(O, topo, iters, timed)
+    out["cores"] = 1
+    out["kind"] = "port"
+    return out
 
 
 def main():
@@ -138,10 +228,9 @@ def main():
         dist.init_process_group("nccl")
     else:
         torch.cuda.set_device(0)
-    from openr_amd import abi, build
+    from openr_amd import abi
     from openr_amd import topologies as TP
 
-    build.build()
     topo = TP.fabric(args.num_sws)
     # drain scenario of this rank (weak scaling: one all-sources table each)
     rsw = [i for i, n in enumerate(topo.names) if n.startswith("3-")]
@@ -173,6 +262,11 @@ def main():
         dist.barrier()
     wall = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    # per-kernel device time of the timed launches (engine-side HIP events on
+    # the same stream, recorded around each kernel)
+    hist = q.stage_history(args.steps)
+    d_ms = sum(h[0] for h in hist) / max(1, len(hist))
+    n_ms = sum(h[1] for h in hist) / max(1, len(hist))
     step_ms = wall * 1000.0 / args.steps
     if dist:
         t = torch.tensor([step_ms, kernel_ms], device="cuda", dtype=torch.float64)
@@ -182,8 +276,35 @@ def main():
     nsrc = len(sources)
     E = len(csr.col)
     value = world * nsrc / (step_ms / 1000.0)
-    abytes = algorithmic_bytes(csr, nh_words)
-    achieved = abytes / (kernel_ms / 1000.0) / 1e9
+    kname = q.kernel
+    dist_k, nh_k = KERNELS.get(kname, (kname, None))
+    nbrs = distinct_nbrs(csr)
+    # BFS levels per 64-source batch, from the distance rows (unit metric)
+    levels = []
+    if kname.startswith("msbfs"):
+        ecc = np.zeros(nsrc, dtype=np.int64)
+        for i in range(0, nsrc, 97):  # sampled eccentricities (fabric: 4-6)
+            d = q.dist(i)
+            ecc[i] = int(d[d != np.uint64(abi.SPF_UNREACHABLE)].max())
+        lv = int(ecc.max()) + 2  # +1 level discovering nothing, +1 source level
+        levels = [lv] * ((nsrc + 63) // 64)
+    stages = {}
+    if nh_k:
+        b = nh_levels_bytes(csr, nbrs, nh_words) if "levels" in kname else None
+        stages[nh_k] = {"avg_ms": round(n_ms, 4), "algorithmic_bytes": b}
+    stages[dist_k] = {
+        "avg_ms": round(d_ms, 4),
+        "algorithmic_bytes": msbfs_bytes(csr, nsrc, levels) if levels else None,
+    }
+    dom = max(stages, key=lambda k: stages[k]["avg_ms"])
+    dom_bytes = stages[dom]["algorithmic_bytes"]
+    dom_ms = stages[dom]["avg_ms"]
+    achieved = dom_bytes / (dom_ms / 1e3) / 1e9 if dom_bytes and dom_ms else None
+    for k, s in stages.items():
+        if s["algorithmic_bytes"] and s["avg_ms"]:
+            s["achieved_gbs"] = round(s["algorithmic_bytes"] / (s["avg_ms"] / 1e3) / 1e9, 1)
+    traffic, traffic_src = pmc_traffic(dom)
+
     # spot-check this run against the oracle restatement (3 sources, rank 0)
     check = None
     if rank == 0:
@@ -215,27 +336,33 @@ def main():
         "dtype": "u32",
         "data": "synthetic fabric (DecisionBenchmark createFabric, SSW bug fixed), metric 1",
         "config": {
-            "workload": "fabric_full all-sources SPF + ECMP next-hop sets",
+            "workload": "fabric_full all-sources SPF + ECMP next-hop sets (BASELINE configs[1])",
             "nodes": csr.num_nodes,
             "links": int(csr.num_links),
             "directed_edges": E,
             "sources_per_gpu": nsrc,
-            "kernel": q.kernel,
+            "kernel": kname,
             "parallelism": f"source-batch per GPU, drain scenario per rank (x{world})",
         },
         "gteps": round(world * nsrc * E / (step_ms / 1000.0) / 1e9, 2),
         "kernel_ms": round(kernel_ms, 4),
+        "kernels": stages,
         "parity_spot_check": check,
         "roofline": {
             "bound": "hbm",
-            "achieved": round(achieved, 1),
+            "kernel": dom,
+            "achieved": round(achieved, 1) if achieved else None,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
-            "algorithmic_bytes_per_launch": abytes,
+            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": dom_bytes,
+            "avg_launch_ms": dom_ms,
         },
     }
+    q.close()
+    g.close()
     if rank == 0 and world == 1 and not args.no_route_db:
         try:
             out["route_db_rebuild"] = route_db_rebuild_ms(topo, local)
@@ -243,10 +370,12 @@ def main():
             out["route_db_rebuild"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(topo, args.cpu_sample)
+        try:
+            out["cpu_baseline"]["route_db_rebuild"] = route_db_rebuild_cpu(topo)
+        except Exception as e:
+            out["cpu_baseline"]["route_db_rebuild"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    q.close()
-    g.close()
     if dist:
         dist.destroy_process_group()
 

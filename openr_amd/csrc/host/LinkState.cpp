@@ -414,7 +414,13 @@ void buildGraph(
     eng.graph = nullptr;
   }
   if (V > 0) {
+    const auto tc = std::chrono::steady_clock::now();
     const int s = spf_graph_create(&d, &eng.graph);
+    Counters::add(
+        "decision.graph_upload_us",
+        std::chrono::duration_cast<std::chrono::microseconds>(
+            std::chrono::steady_clock::now() - tc)
+            .count());
     if (s != SPF_OK) {
       engineFailure("spf_graph_create", s);
     }
@@ -434,6 +440,17 @@ std::vector<std::unique_ptr<SpfView>> runBatch(
   if (sources.empty()) {
     return out;
   }
+  const auto tBatch = std::chrono::steady_clock::now();
+  struct BatchTimer {
+    std::chrono::steady_clock::time_point t0;
+    ~BatchTimer() {
+      Counters::add(
+          "decision.spf_batch_us",
+          std::chrono::duration_cast<std::chrono::microseconds>(
+              std::chrono::steady_clock::now() - t0)
+              .count());
+    }
+  } batchTimer{tBatch};
   const bool exact = eng.exact && useLinkMetric;
   uint32_t flags = 0;
   if (!useLinkMetric) {
@@ -568,7 +585,13 @@ LinkState::Engine& LinkState::engine() const {
     engine_ = std::make_unique<Engine>();
   }
   if (!engine_->built) {
+    const auto t0 = std::chrono::steady_clock::now();
     buildGraph(*engine_, linkMap_, adjacencyDatabases_, *this);
+    Counters::add(
+        "decision.graph_build_us",
+        std::chrono::duration_cast<std::chrono::microseconds>(
+            std::chrono::steady_clock::now() - t0)
+            .count());
   }
   return *engine_;
 }

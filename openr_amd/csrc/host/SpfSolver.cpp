@@ -324,6 +324,11 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
   const auto t0 = std::chrono::steady_clock::now();
   Counters::add("decision.route_build_runs", 1);
   prefetch(myNodeName, areaLinkStates, prefixState);
+  Counters::add(
+      "decision.route_prefetch_us",
+      std::chrono::duration_cast<std::chrono::microseconds>(
+          std::chrono::steady_clock::now() - t0)
+          .count());
 
   DecisionRouteDb routeDb;
 

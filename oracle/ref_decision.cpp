@@ -1191,6 +1191,16 @@ PYBIND11_MODULE(_oracle_ref, m) {
              for (auto nh : nhs) v.push_back(toNextHop(nh));
              s.staticMpls[label] = v;
            })
+      .def("buildRouteDbTimed",
+           [](Solver& s, const std::string& me, const AreaHolder& areas, const Prefixes& ps) {
+             // the cpu_baseline leg: RouteDb build timed in C++ (no Python conversion)
+             const auto t0 = std::chrono::steady_clock::now();
+             auto db = s.build(me, areas.map, ps);
+             const double us = std::chrono::duration<double, std::micro>(
+                                   std::chrono::steady_clock::now() - t0).count();
+             if (!db) return py::make_tuple((long)-1, (long)-1, us);
+             return py::make_tuple((long)db->unicast.size(), (long)db->mpls.size(), us);
+           })
       .def("buildRouteDb",
            [](Solver& s, const std::string& me, const AreaHolder& areas,
               const Prefixes& ps) -> py::object {

@@ -310,6 +310,7 @@ struct LinkState::Engine {
   std::vector<uint8_t> overloaded;
   std::vector<std::shared_ptr<Link>> links; // link id -> Link
   std::unordered_map<const Link*, uint32_t> linkIndex;
+  std::vector<std::array<uint32_t, 2>> halves; // link id -> half-edge from first/second node
   spf_graph* graph{nullptr};
   bool exact{false};
   float lastMs{0};
@@ -365,7 +366,8 @@ void buildGraph(
   eng.linkIndex.clear();
   eng.overloaded.assign(V, 0);
   // half-edge slots per link: [0] = from firstNodeName, [1] = from second
-  std::vector<std::array<uint32_t, 2>> halves;
+  auto& halves = eng.halves;
+  halves.clear();
   for (uint32_t u = 0; u < V; ++u) {
     const std::string& name = eng.names[u];
     eng.overloaded[u] = ls.isNodeOverloaded(name) ? 1 : 0;
@@ -634,6 +636,81 @@ void LinkState::clearMemo() const {
 
 void LinkState::invalidate() const { clearMemo(); }
 
+// Topology change that keeps the set of up links: drop every SPF memo but
+// keep the device graph, patching node transit bits / link metrics in place
+// (incremental CSR deltas instead of a full rebuild).
+void LinkState::patchMemo(
+    const std::vector<std::string>& transitNodes,
+    const std::vector<std::pair<std::shared_ptr<Link>, std::string>>& metricPatches) const {
+  if (!engine_ || !engine_->built || !engine_->graph) {
+    clearMemo();
+    return;
+  }
+  auto& eng = *engine_;
+  std::vector<uint32_t> edges;
+  std::vector<uint64_t> metrics;
+  for (const auto& [link, from] : metricPatches) {
+    auto li = eng.linkIndex.find(link.get());
+    if (li == eng.linkIndex.end()) {
+      clearMemo(); // not an up link of the device graph: rebuild
+      return;
+    }
+    const auto& h = eng.halves[li->second];
+    const uint32_t e = from == link->firstNodeName() ? h[0] : h[1];
+    if (e == ~0u) {
+      clearMemo();
+      return;
+    }
+    edges.push_back(e);
+    metrics.push_back(link->getMetricFromNode(from));
+  }
+  bool transit = false;
+  for (const auto& n : transitNodes) {
+    auto it = eng.ids.find(n);
+    if (it == eng.ids.end()) {
+      continue; // not in the graph: no transit bit to flip
+    }
+    const uint8_t ov = isNodeOverloaded(n) ? 1 : 0;
+    transit |= eng.overloaded[it->second] != ov;
+    eng.overloaded[it->second] = ov;
+  }
+  spfResultsMetric_.clear();
+  spfResultsHops_.clear();
+  kthPathResults_.clear();
+  for (auto& m : eng.memo) {
+    m.clear();
+  }
+  for (auto& m : eng.prefetched) {
+    m.clear();
+  }
+  eng.kthPrefetch.clear();
+  eng.isolated.clear();
+  const auto t0 = std::chrono::steady_clock::now();
+  if (transit) {
+    const int s = spf_graph_set_transit(eng.graph, eng.overloaded.data());
+    if (s != SPF_OK) {
+      engineFailure("spf_graph_set_transit", s);
+    }
+  }
+  if (!edges.empty()) {
+    for (size_t i = 0; i < edges.size(); ++i) {
+      eng.metric[edges[i]] = metrics[i];
+    }
+    const int s = spf_graph_patch_metrics(
+        eng.graph, (uint32_t)edges.size(), edges.data(), metrics.data());
+    if (s != SPF_OK) {
+      engineFailure("spf_graph_patch_metrics", s);
+    }
+    eng.exact = spf_graph_needs_exact(eng.graph) != 0;
+  }
+  Counters::add("decision.graph_patches", 1);
+  Counters::add(
+      "decision.graph_patch_us",
+      std::chrono::duration_cast<std::chrono::microseconds>(
+          std::chrono::steady_clock::now() - t0)
+          .count());
+}
+
 void LinkState::addLink(std::shared_ptr<Link> link) {
   if (!linkMap_[link->firstNodeName()].insert(link).second ||
       !linkMap_[link->secondNodeName()].insert(link).second ||
@@ -768,9 +845,14 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
   const auto oldLinks = orderedLinksFromNode(nodeName);
   const auto newLinks = getOrderedLinkSet(newDb);
 
-  change.topologyChanged |=
+  const bool transitChanged =
       updateNodeOverloaded(nodeName, newDb.isOverloaded, holdUpTtl, holdDownTtl);
+  change.topologyChanged |= transitChanged;
   change.nodeLabelChanged = priorDb.nodeLabel != newDb.nodeLabel;
+  // what the device graph needs: a rebuild when the set of up links changes,
+  // else in-place transit / metric patches
+  bool structural = false;
+  std::vector<std::pair<std::shared_ptr<Link>, std::string>> metricPatches;
 
   size_t ni = 0, oi = 0;
   while (ni < newLinks.size() || oi < oldLinks.size()) {
@@ -779,6 +861,7 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
       // link appears: keep it held down for holdUpTtl
       newLinks[ni]->setHoldUpTtl(holdUpTtl);
       change.topologyChanged |= newLinks[ni]->isUp();
+      structural |= newLinks[ni]->isUp();
       addLink(newLinks[ni]);
       ++ni;
       continue;
@@ -786,6 +869,7 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
     if (haveOld && (!haveNew || *oldLinks[oi] < *newLinks[ni])) {
       // link disappears (a held or overloaded link was not carrying traffic)
       change.topologyChanged |= oldLinks[oi]->isUp();
+      structural |= oldLinks[oi]->isUp();
       removeLink(oldLinks[oi]);
       ++oi;
       continue;
@@ -793,6 +877,8 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
     // same link: fold attribute changes into the existing Link object
     const Link& fresh = *newLinks[ni];
     Link& cur = *oldLinks[oi];
+    const bool wasUp = cur.isUp();
+    const LinkStateMetric oldMetric = cur.getMetricFromNode(nodeName);
     if (fresh.getMetricFromNode(nodeName) != cur.getMetricFromNode(nodeName)) {
       change.topologyChanged |= cur.setMetricFromNode(
           nodeName, fresh.getMetricFromNode(nodeName), holdUpTtl, holdDownTtl);
@@ -800,6 +886,11 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
     if (fresh.getOverloadFromNode(nodeName) != cur.getOverloadFromNode(nodeName)) {
       change.topologyChanged |= cur.setOverloadFromNode(
           nodeName, fresh.getOverloadFromNode(nodeName), holdUpTtl, holdDownTtl);
+    }
+    if (cur.isUp() != wasUp) {
+      structural = true;
+    } else if (wasUp && cur.getMetricFromNode(nodeName) != oldMetric) {
+      metricPatches.emplace_back(oldLinks[oi], nodeName);
     }
     if (fresh.getAdjLabelFromNode(nodeName) != cur.getAdjLabelFromNode(nodeName)) {
       change.linkAttributesChanged = true;
@@ -817,7 +908,13 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
     ++oi;
   }
   if (change.topologyChanged) {
-    clearMemo();
+    if (structural) {
+      clearMemo();
+    } else {
+      patchMemo(
+          transitChanged ? std::vector<std::string>{nodeName} : std::vector<std::string>{},
+          metricPatches);
+    }
   }
   return change;
 }
@@ -863,6 +960,10 @@ std::optional<uint32_t> LinkState::nodeId(const std::string& name) const {
 
 const std::string& LinkState::nodeNameOf(uint32_t id) const {
   return engine().names.at(id);
+}
+
+const std::vector<std::string>& LinkState::nodeNames() const {
+  return engine().names;
 }
 
 uint32_t LinkState::numGraphNodes() const {

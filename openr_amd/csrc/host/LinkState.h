@@ -274,6 +274,8 @@ class LinkState {
   // node id (name rank) in the current device graph
   std::optional<uint32_t> nodeId(const std::string& name) const;
   const std::string& nodeNameOf(uint32_t id) const;
+  // id -> name of the device graph (valid until the next topology change)
+  const std::vector<std::string>& nodeNames() const;
   uint32_t numGraphNodes() const;
   // device time of the last batch, ms (HIP events)
   float lastDeviceMs() const;
@@ -284,6 +286,9 @@ class LinkState {
 
  private:
   void clearMemo() const;
+  void patchMemo(
+      const std::vector<std::string>& transitNodes,
+      const std::vector<std::pair<std::shared_ptr<Link>, std::string>>& metricPatches) const;
   Engine& engine() const;
   std::optional<Path> traceOnePath(
       uint32_t src, uint32_t dest, const SpfView& result, LinkSet& linksToIgnore) const;

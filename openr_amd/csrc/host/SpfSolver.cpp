@@ -13,6 +13,7 @@
 #include "SpfSolver.h"
 
 #include <chrono>
+#include <string_view>
 #include <list>
 
 #include "Util.h"
@@ -89,18 +90,24 @@ namespace {
 using AreaLinkStates = std::unordered_map<std::string, LinkState>;
 
 struct PairHash {
-  size_t operator()(const std::pair<std::string, std::string>& p) const {
-    return detail::mix(std::hash<std::string>()(p.first), std::hash<std::string>()(p.second));
+  size_t operator()(const std::pair<std::string_view, std::string_view>& p) const {
+    return detail::mix(
+        std::hash<std::string_view>()(p.first), std::hash<std::string_view>()(p.second));
   }
 };
-using NextHopNodes = std::unordered_map<std::pair<std::string, std::string>, Metric, PairHash>;
+// (next-hop node, destination or "") -> metric beyond the next hop.  The
+// views point at names owned by the LinkState engine / the Link objects /
+// the caller's destination set, all alive for the whole RouteDb build.
+using NextHopNodes =
+    std::unordered_map<std::pair<std::string_view, std::string_view>, Metric, PairHash>;
+const std::string kNoDestName;
 
 // Name-keyed reads of one SPF row (what the reference does with
 // SpfResult::find / at(...).metric() / nextHops()).
 class SpfRead {
  public:
   SpfRead(const LinkState& ls, const std::string& src, bool useLinkMetric = true)
-      : ls_(ls), src_(src), view_(ls.spfView(src, useLinkMetric)) {}
+      : ls_(ls), src_(src), view_(ls.spfView(src, useLinkMetric)), names_(ls.nodeNames()) {}
 
   std::optional<Metric> metric(const std::string& node) const {
     if (view_.src == ~0u) {
@@ -122,13 +129,27 @@ class SpfRead {
     if (!id || !view_.reached(*id)) {
       return;
     }
-    view_.forEachNextHop(*id, [&](uint32_t h) { fn(ls_.nodeNameOf(h)); });
+    view_.forEachNextHop(*id, [&](uint32_t h) { fn(names_[h]); });
+  }
+
+  // fn(name, metric to that next hop) — metric = getMetricFromAToB(src, nh)
+  template <class Fn>
+  void forEachNextHopWithMetric(const std::string& node, Fn&& fn) const {
+    if (view_.src == ~0u) {
+      return;
+    }
+    auto id = ls_.nodeId(node);
+    if (!id || !view_.reached(*id)) {
+      return;
+    }
+    view_.forEachNextHop(*id, [&](uint32_t h) { fn(names_[h], view_.dist[h]); });
   }
 
  private:
   const LinkState& ls_;
   const std::string& src_;
   const SpfView& view_;
+  const std::vector<std::string>& names_;
 };
 
 } // namespace
@@ -234,6 +255,41 @@ class SpfSolver::SpfSolverImpl {
       AreaLinkStates const& areaLinkStates,
       const std::set<std::string>& prefixAreas) const;
 
+  // myNode's links of one area in linksFromNode() order with the per-link
+  // values every prefix reads (computed once per RouteDb build)
+  struct MyLink {
+    const Link* link;
+    const std::string* nbr;
+    std::string_view nbrView;
+    bool up;
+    Metric metric;
+    const thrift::BinaryAddress* nhV4;
+    const thrift::BinaryAddress* nhV6;
+    const std::string* iface;
+  };
+  struct MyLinks {
+    std::vector<MyLink> links;
+    std::unordered_map<std::string_view, std::vector<uint32_t>> byNbr;
+  };
+  const MyLinks& myLinks(
+      const std::string& myNodeName, const std::string& area, const LinkState& ls) const {
+    auto it = myLinks_.find(area);
+    if (it != myLinks_.end()) {
+      return it->second;
+    }
+    MyLinks v;
+    for (const auto& link : ls.linksFromNode(myNodeName)) {
+      const std::string& nbr = link->getOtherNodeName(myNodeName);
+      v.byNbr[std::string_view(nbr)].push_back((uint32_t)v.links.size());
+      v.links.push_back(MyLink{
+          link.get(), &nbr, std::string_view(nbr), link->isUp(),
+          link->getMetricFromNode(myNodeName), &link->getNhV4FromNode(myNodeName),
+          &link->getNhV6FromNode(myNodeName), &link->getIfaceFromNode(myNodeName)});
+    }
+    return myLinks_.emplace(area, std::move(v)).first->second;
+  }
+  mutable std::unordered_map<std::string, MyLinks> myLinks_;
+
   thrift::StaticRoutes staticRoutes_;
   std::vector<thrift::RouteDatabaseDelta> staticRoutesUpdates_;
   const std::string myNodeName_;
@@ -323,6 +379,7 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
   }
   const auto t0 = std::chrono::steady_clock::now();
   Counters::add("decision.route_build_runs", 1);
+  myLinks_.clear();
   prefetch(myNodeName, areaLinkStates, prefixState);
   Counters::add(
       "decision.route_prefetch_us",
@@ -821,10 +878,9 @@ std::pair<Metric, NextHopNodes> SpfSolver::SpfSolverImpl::getNextHopsWithMetric(
       continue;
     }
     for (const std::string* dst : minCostNodes) {
-      const std::string dstRef = perDestination ? *dst : std::string();
-      mine.forEachNextHop(*dst, [&](const std::string& nh) {
-        nextHopNodes[std::make_pair(nh, dstRef)] =
-            shortestMetric - ls.getMetricFromAToB(myNodeName, nh).value();
+      const std::string_view dstRef = perDestination ? std::string_view(*dst) : kNoDestName;
+      mine.forEachNextHopWithMetric(*dst, [&](const std::string& nh, Metric toNh) {
+        nextHopNodes[std::make_pair(std::string_view(nh), dstRef)] = shortestMetric - toNh;
       });
     }
     if (computeLfaPaths_) {
@@ -845,7 +901,9 @@ std::pair<Metric, NextHopNodes> SpfSolver::SpfSolverImpl::getNextHopsWithMetric(
             continue;
           }
           if (*dNbr < shortestMetric + *nbrToHere) {
-            auto key = std::make_pair(nbr, perDestination ? dst : std::string());
+            auto key = std::make_pair(
+                std::string_view(nbr),
+                perDestination ? std::string_view(dst) : std::string_view(kNoDestName));
             auto it = nextHopNodes.find(key);
             if (it == nextHopNodes.end()) {
               nextHopNodes.emplace(std::move(key), *dNbr);
@@ -875,22 +933,38 @@ std::unordered_set<thrift::NextHopThrift> SpfSolver::SpfSolverImpl::getNextHopsT
   }
   static const std::set<std::string> kNoDest{std::string()};
   std::unordered_set<thrift::NextHopThrift> nextHops;
+  nextHops.reserve(nextHopNodes.size() * 2);
   for (const auto& [area, ls] : areaLinkStates) {
     if (!prefixAreas.count(area)) {
       continue;
     }
-    for (const auto& link : ls.linksFromNode(myNodeName)) {
-      for (const auto& dstNode : perDestination ? dstNodeNames : kNoDest) {
-        const std::string& nbr = link->getOtherNodeName(myNodeName);
-        auto search = nextHopNodes.find(std::make_pair(nbr, dstNode));
-        if (search == nextHopNodes.end() || !link->isUp()) {
+    // every (up link of myNode, destination) pair whose (neighbour, destination)
+    // is a next-hop node: walk the next-hop nodes and the links to each
+    const MyLinks& mls = myLinks(myNodeName, area, ls);
+    const auto& dests = perDestination ? dstNodeNames : kNoDest;
+    for (auto search = nextHopNodes.begin(); search != nextHopNodes.end(); ++search) {
+      const std::string_view dstView = search->first.second;
+      auto dIt = dests.find(std::string(dstView));
+      if (dIt == dests.end()) {
+        continue;
+      }
+      const std::string& dstNode = *dIt;
+      auto byNbr = mls.byNbr.find(search->first.first);
+      if (byNbr == mls.byNbr.end()) {
+        continue;
+      }
+      for (const uint32_t li : byNbr->second) {
+        const MyLink& ml = mls.links[li];
+        if (!ml.up) {
           continue;
         }
+        const Link* link = ml.link;
+        const std::string& nbr = *ml.nbr;
         // do not reach dstNode through another destination
         if (!dstNode.empty() && dstNodeNames.count(nbr) && nbr != dstNode) {
           continue;
         }
-        const Metric distOverLink = link->getMetricFromNode(myNodeName) + search->second;
+        const Metric distOverLink = ml.metric + search->second;
         if (!computeLfaPaths_ && distOverLink != minMetric) {
           continue; // only shortest paths without LFA
         }
@@ -913,8 +987,7 @@ std::unordered_set<thrift::NextHopThrift> SpfSolver::SpfSolverImpl::getNextHopsT
               thrift::MplsActionCode::PUSH, std::nullopt, std::vector<int32_t>{dstLabel});
         }
         nextHops.insert(createNextHop(
-            isV4 ? link->getNhV4FromNode(myNodeName) : link->getNhV6FromNode(myNodeName),
-            link->getIfaceFromNode(myNodeName), (int32_t)distOverLink, action, false,
+            isV4 ? *ml.nhV4 : *ml.nhV6, *ml.iface, (int32_t)distOverLink, action, false,
             link->getArea()));
       }
     }

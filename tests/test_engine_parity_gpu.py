@@ -131,3 +131,42 @@ def test_spf_runs_counter_matches_oracle(mods):
             E.get_counters().get("decision.spf_runs", 0)
             == O.get_counters()["decision.spf_runs"]
         )
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_incremental_updates(mods, seed):
+    """Churn that keeps the set of up links (node drain toggles, metric
+    changes of up links) patches the device graph in place instead of
+    rebuilding it (LinkState::patchMemo); churn that changes it (link
+    overloads) rebuilds.  After every step the engine's SPF rows, KSP2 paths
+    and RouteDb equal the oracle's, and the change flags match."""
+    import random
+
+    E, O = mods
+    names, adj_dbs, prefix_dbs = RZ.random_network(500 + seed, n_nodes=30, n_links=70)
+    ea, ep = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    oa, op = RZ.load(O, adj_dbs, prefix_dbs, seed)
+    es = E.SpfSolver(names[0], True, True)
+    os_ = O.SpfSolver(names[0], True, True)
+    rng = random.Random(seed)
+    dbs = [copy.deepcopy(d) for d in adj_dbs["0"]]
+    E.reset_counters()
+    for step in range(12):
+        db = rng.choice(dbs)
+        kind = rng.random()
+        if kind < 0.45 or not db.adjacencies:
+            db.isOverloaded = not db.isOverloaded
+        elif kind < 0.85:
+            adj = rng.choice(db.adjacencies)
+            adj.metric = rng.randint(1, 20)
+        else:
+            adj = rng.choice(db.adjacencies)
+            adj.isOverloaded = not adj.isOverloaded
+        assert ea["0"].updateAdjacencyDatabase(db) == oa["0"].updateAdjacencyDatabase(db)
+        node = rng.choice(names)
+        if ea["0"].hasNode(node):
+            _spf_equal(ea["0"], oa["0"], node, True)
+            _spf_equal(ea["0"], oa["0"], node, False)
+        me = names[step % len(names)]
+        assert es.buildRouteDb(me, ea, ep) == os_.buildRouteDb(me, oa, op), (step, me)
+    assert E.get_counters().get("decision.graph_patches", 0) > 0

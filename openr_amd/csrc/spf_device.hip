@@ -48,7 +48,7 @@ namespace {
 constexpr uint32_t kBlock = 512;           // threads per workgroup (8 waves)
 constexpr uint32_t kWaves = kBlock / 64;
 constexpr uint32_t kInf32 = 0xFFFFFFFFu;
-constexpr uint32_t kCtlWords = 16;         // qlen + scan scratch
+constexpr uint32_t kCtlWords = 32;         // qlen + scan scratch (<= 16 waves + 1)
 constexpr size_t kLdsLimit = 160 * 1024;   // gfx950 LDS per CU
 constexpr uint32_t kIgnLdsMax = 2048;      // ignore-list entries staged in LDS
 constexpr uint32_t kNotSeen = 0xFFFFFFFFu; // exact kernel heap states
@@ -107,8 +107,10 @@ __device__ __forceinline__ bool in_sorted(
 
 // Exclusive scan of one value per thread over the workgroup.  `scan` holds
 // kWaves+1 LDS words.  Returns the thread's offset; *total = block sum.
+template <uint32_t BS = kBlock>
 __device__ __forceinline__ uint32_t block_excl_scan(
     uint32_t x, uint32_t* scan, uint32_t* total) {
+  constexpr uint32_t kWaves = BS / 64;
   const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
   uint32_t inc = x;
 #pragma unroll
@@ -142,10 +144,10 @@ __device__ __forceinline__ uint32_t block_excl_scan(
 }
 
 // Turn a node bitmap into a queue of node ids (ascending), clearing the bitmap.
-template <typename QT>
+template <typename QT, uint32_t BS = kBlock>
 __device__ __forceinline__ uint32_t compact_bits(
     uint32_t* bits, uint32_t nbw, QT* queue, uint32_t* scan) {
-  const uint32_t chunk = (nbw + kBlock - 1) / kBlock;
+  const uint32_t chunk = (nbw + BS - 1) / BS;
   const uint32_t w0 = min(threadIdx.x * chunk, nbw);
   const uint32_t w1 = min(w0 + chunk, nbw);
   uint32_t cnt = 0;
@@ -153,7 +155,7 @@ __device__ __forceinline__ uint32_t compact_bits(
     cnt += __popc(bits[w]);
   }
   uint32_t total;
-  uint32_t off = block_excl_scan(cnt, scan, &total);
+  uint32_t off = block_excl_scan<BS>(cnt, scan, &total);
   for (uint32_t w = w0; w < w1; ++w) {
     uint32_t b = bits[w];
     if (b) {
@@ -400,6 +402,286 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
       for (uint32_t v = tid; v < V; v += kBlock) {
         out[v] = dist[v];
       }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------ delta-stepping (large graphs)
+//
+// Weighted graphs whose per-source distance row does not fit LDS (the 100k
+// WAN): the row stays in HBM (it is the output row), and the work is
+// ordered by distance buckets of width 2^shift ("delta-stepping"): only
+// PENDING nodes (improved, not yet pushed) whose bucket <= the current one
+// push their out-edges; the marked heads PULL (min, next-hop union) from
+// all their in-edges exactly as in spf_sssp_kernel.  A frontier
+// Bellman-Ford re-relaxes every node each time a longer-hop but shorter
+// path reaches it; bucket order pushes most nodes once.  LDS holds the
+// per-node bucket byte (V B) and the pending / marked bitmaps, so 100k
+// nodes take ~137 KB.  Any processing order reaches the same fixpoint, so
+// the result is the order-free restatement of runSpf.
+struct DstepArgs {
+  SsspArgs s;
+  uint32_t shift; // bucket width 2^shift
+};
+
+// pending nodes with bucket <= cur -> queue (ascending), clearing their bits
+template <uint32_t BS>
+__device__ __forceinline__ uint32_t compact_bucket(
+    uint32_t* pend, const uint8_t* bkt, uint32_t cur, uint32_t nbw,
+    uint32_t* queue, uint32_t* scan) {
+  const uint32_t chunk = (nbw + BS - 1) / BS;
+  const uint32_t w0 = min(threadIdx.x * chunk, nbw);
+  const uint32_t w1 = min(w0 + chunk, nbw);
+  uint32_t cnt = 0;
+  for (uint32_t w = w0; w < w1; ++w) {
+    uint32_t b = pend[w];
+    while (b) {
+      const uint32_t k = __ffs(b) - 1;
+      b &= b - 1;
+      cnt += bkt[w * 32 + k] <= cur;
+    }
+  }
+  uint32_t total;
+  uint32_t off = block_excl_scan<BS>(cnt, scan, &total);
+  for (uint32_t w = w0; w < w1; ++w) {
+    uint32_t b = pend[w], sel = 0;
+    while (b) {
+      const uint32_t k = __ffs(b) - 1;
+      b &= b - 1;
+      if (bkt[w * 32 + k] <= cur) {
+        sel |= 1u << k;
+        queue[off++] = w * 32 + k;
+      }
+    }
+    if (sel) {
+      pend[w] &= ~sel;
+    }
+  }
+  return total;
+}
+
+// smallest bucket among pending nodes (255 = none pending)
+template <uint32_t BS>
+__device__ __forceinline__ uint32_t min_pending_bucket(
+    const uint32_t* pend, const uint8_t* bkt, uint32_t nbw, uint32_t* scan) {
+  constexpr uint32_t kWaves = BS / 64;
+  uint32_t m = 255;
+  for (uint32_t w = threadIdx.x; w < nbw; w += BS) {
+    uint32_t b = pend[w];
+    while (b) {
+      const uint32_t k = __ffs(b) - 1;
+      b &= b - 1;
+      m = min(m, (uint32_t)bkt[w * 32 + k]);
+    }
+  }
+  m = grp_min(m, 64);
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    scan[wid] = m;
+  }
+  __syncthreads();
+  uint32_t r = 255;
+  for (uint32_t i = 0; i < kWaves; ++i) {
+    r = min(r, scan[i]);
+  }
+  __syncthreads();
+  return r;
+}
+
+template <int WMAX, bool IGN, uint32_t BS>
+__global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
+  extern __shared__ __align__(16) uint32_t smem[];
+  const SsspArgs& a = da.s;
+  const uint32_t V = a.V, nbw = a.nbw, G = a.G, shift = da.shift;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lg = tid & (G - 1);
+  const uint32_t grp = tid / G, ngrp = BS / G;
+
+  uint32_t* act = smem;        // marked heads (PULL)
+  uint32_t* pend = act + nbw;  // improved, not yet pushed
+  uint32_t* ctl = pend + nbw;
+  uint32_t* ignl = ctl + kCtlWords;
+  uint8_t* bkt = reinterpret_cast<uint8_t*>(ignl + a.ign_cap);
+  uint32_t* queue = a.gscratch + (size_t)blockIdx.x * V;
+
+  for (uint32_t i = tid; i < nbw; i += BS) {
+    act[i] = 0;
+    pend[i] = 0;
+  }
+
+  for (uint32_t q = blockIdx.x; q < a.nq; q += gridDim.x) {
+    const uint32_t src = a.src[q];
+    uint32_t* dist = a.dist_out + (size_t)q * a.Vp;
+    uint32_t nign = 0;
+    const uint32_t* ignp = ignl;
+    if constexpr (IGN) {
+      const uint32_t lo = a.ign_off[q];
+      nign = a.ign_off[q + 1] - lo;
+      if (nign <= a.ign_cap) {
+        for (uint32_t i = tid; i < nign; i += BS) {
+          ignl[i] = a.ign[lo + i];
+        }
+      } else {
+        ignp = a.ign + lo;
+      }
+    }
+    uint32_t Wm = 0;
+    uint64_t* nhrow = nullptr;
+    if constexpr (WMAX > 0) {
+      Wm = a.nh_w[q];
+      nhrow = a.nh_out + a.nh_off[q];
+    }
+    for (uint32_t v = tid; v < V; v += BS) {
+      dist[v] = kInf32;
+      bkt[v] = 255;
+    }
+    if constexpr (WMAX > 0) {
+      for (uint32_t i = tid; i < V * Wm; i += BS) {
+        nhrow[i] = 0;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      dist[src] = 0;
+      bkt[src] = 0;
+      pend[src >> 5] |= 1u << (src & 31);
+    }
+    __syncthreads();
+    uint32_t cur = 0;
+
+    for (;;) {
+      uint32_t qlen = compact_bucket<BS>(pend, bkt, cur, nbw, queue, ctl + 1);
+      __syncthreads();
+      if (qlen == 0) {
+        const uint32_t m = min_pending_bucket<BS>(pend, bkt, nbw, ctl + 1);
+        if (m >= 255) {
+          break;
+        }
+        cur = m;
+        continue;
+      }
+      // ---- PUSH from the selected bucket
+      for (uint32_t i = grp; i < qlen; i += ngrp) {
+        const uint32_t u = queue[i];
+        if (u != src && !((a.trbits[u >> 5] >> (u & 31)) & 1u)) {
+          continue; // overloaded: recorded but never transited
+        }
+        const uint32_t du = dist[u];
+        const uint32_t beg = a.row[u], end = a.row[u + 1];
+        for (uint32_t e = beg + lg; e < end; e += G) {
+          if constexpr (IGN) {
+            if (nign && in_sorted(ignp, nign, a.link[e])) {
+              continue;
+            }
+          }
+          const uint32_t v = a.col[e];
+          const uint32_t c = du + a.wout[e];
+          if (c <= dist[v]) {
+            const uint32_t bit = 1u << (v & 31);
+            if (!(act[v >> 5] & bit)) {
+              atomicOr(&act[v >> 5], bit);
+            }
+          }
+        }
+      }
+      __syncthreads();
+      qlen = compact_bits<uint32_t, BS>(act, nbw, queue, ctl + 1);
+      __syncthreads();
+
+      // ---- PULL: marked heads recompute (dist, next hops) from all in-edges
+      for (uint32_t i = grp; i < qlen; i += ngrp) {
+        const uint32_t v = queue[i];
+        const uint32_t beg = a.row[v], end = a.row[v + 1];
+        uint32_t best = kInf32;
+        uint64_t nh[WMAX > 0 ? WMAX : 1];
+#pragma unroll
+        for (int j = 0; j < (WMAX > 0 ? WMAX : 1); ++j) {
+          nh[j] = 0;
+        }
+        for (uint32_t e = beg + lg; e < end; e += G) {
+          if constexpr (IGN) {
+            if (nign && in_sorted(ignp, nign, a.link[e])) {
+              continue;
+            }
+          }
+          const uint32_t u = a.col[e];
+          const bool isSrc = (u == src);
+          if (!isSrc && !((a.trbits[u >> 5] >> (u & 31)) & 1u)) {
+            continue;
+          }
+          const uint32_t du = dist[u];
+          if (du == kInf32) {
+            continue;
+          }
+          const uint32_t c = du + a.win[e];
+          if (c < best) {
+            best = c;
+#pragma unroll
+            for (int j = 0; j < (WMAX > 0 ? WMAX : 1); ++j) {
+              nh[j] = 0;
+            }
+          }
+          if constexpr (WMAX > 0) {
+            if (c == best) {
+              if (isSrc) {
+                const uint32_t s = a.slot[a.rev[e]];
+#pragma unroll
+                for (int j = 0; j < WMAX; ++j) {
+                  if ((uint32_t)j == (s >> 6)) {
+                    nh[j] |= 1ull << (s & 63);
+                  }
+                }
+              } else {
+                const uint64_t* p = nhrow + (size_t)u * Wm;
+#pragma unroll
+                for (int j = 0; j < WMAX; ++j) {
+                  if ((uint32_t)j < Wm) {
+                    nh[j] |= p[j];
+                  }
+                }
+              }
+            }
+          }
+        }
+        const uint32_t gbest = grp_min(best, (int)G);
+        if constexpr (WMAX > 0) {
+#pragma unroll
+          for (int j = 0; j < WMAX; ++j) {
+            nh[j] = grp_or(best == gbest ? nh[j] : 0ull, (int)G);
+          }
+        }
+        if (lg == 0 && gbest != kInf32) {
+          const uint32_t old = dist[v];
+          bool changed = gbest < old;
+          uint64_t* row = nullptr;
+          if constexpr (WMAX > 0) {
+            row = nhrow + (size_t)v * Wm;
+            if (!changed && gbest == old) {
+#pragma unroll
+              for (int j = 0; j < WMAX; ++j) {
+                if ((uint32_t)j < Wm && row[j] != nh[j]) {
+                  changed = true;
+                }
+              }
+            }
+          }
+          if (changed) {
+            dist[v] = gbest;
+            bkt[v] = (uint8_t)min(gbest >> shift, 254u);
+            if constexpr (WMAX > 0) {
+#pragma unroll
+              for (int j = 0; j < WMAX; ++j) {
+                if ((uint32_t)j < Wm) {
+                  row[j] = nh[j];
+                }
+              }
+            }
+            atomicOr(&pend[v >> 5], 1u << (v & 31));
+          }
+        }
+      }
+      __syncthreads();
     }
     __syncthreads();
   }
@@ -1152,7 +1434,7 @@ struct spf_graph {
 };
 
 // How a batch is computed.
-enum class DistPlan { SsspLds, SsspGmem, BfsLds, BfsGmem, MsBfs, Exact };
+enum class DistPlan { SsspLds, SsspGmem, BfsLds, BfsGmem, MsBfs, Dstep, Exact };
 enum class NhPlan { None, Inline, Rows, Levels };
 
 struct spf_query {
@@ -1162,6 +1444,7 @@ struct spf_query {
   NhPlan nh = NhPlan::None;
   int wmax = 0;
   int ms_bits = 64; // MS-BFS batch width (32 or 64 sources per workgroup)
+  uint32_t dstep_shift = 5; // delta-stepping bucket width 2^shift
   uint32_t ign_cap = 0, grid = 0, Vp = 0, Vp8 = 0;
   uint8_t* d_lvl = nullptr;
   uint32_t* d_flags = nullptr;
@@ -1645,6 +1928,18 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     q->nh = want_nh ? NhPlan::Inline : NhPlan::None;
   } else {
     q->nh = !want_nh ? NhPlan::None : (rows_ok ? NhPlan::Rows : NhPlan::Inline);
+    // weighted graph whose distance row does not fit LDS: delta-stepping
+    // with next hops inline (the rows plan would read every neighbour's
+    // 4V-byte row per source: 8E*V bytes per all-sources pass)
+    const bool big = lds_ctl_bytes(g, 0) + lds_state_bytes(V) > kLdsLimit || V > 65535;
+    const size_t dstep_lds =
+        (2 * (size_t)g->nbw + kCtlWords + (has_ign ? std::min(max_ign, kIgnLdsMax) : 0)) * 4 +
+        (((size_t)V + 15) & ~(size_t)15);
+    const bool dstep = big && !uniform && dstep_lds <= kLdsLimit && maxw <= 16 &&
+                       getenv("OPENR_SPF_DSTEP") == nullptr;
+    if (dstep && q->nh == NhPlan::Rows) {
+      q->nh = NhPlan::Inline;
+    }
     const bool bfs = uniform && !has_ign && q->nh != NhPlan::Inline;
     q->wmax = q->nh != NhPlan::Inline ? 0 : (maxw <= 1 ? 1 : (maxw <= 4 ? 4 : 16));
     q->ign_cap = has_ign ? std::min(max_ign, kIgnLdsMax) : 0;
@@ -1657,6 +1952,26 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
           std::max<uint32_t>(1, std::min<uint32_t>(4, kLdsLimit / lds));
       q->grid = std::min<uint32_t>(std::max<uint32_t>(nq, 1),
                                    (uint32_t)g->num_cus * per_cu);
+    } else if (dstep) {
+      q->dist = DistPlan::Dstep;
+      q->lds_bytes = dstep_lds;
+      // bucket width ~ mean metric / mean degree (delta-stepping's
+      // Delta = Theta(w/d)), a power of two; OPENR_SPF_DSTEP_SHIFT overrides
+      uint64_t wsum = 0;
+      for (uint32_t e = 0; e < g->E; ++e) {
+        wsum += std::min<uint64_t>(g->w64[e], 0xFFFFFFFFull);
+      }
+      const double meanw = g->E ? (double)wsum / g->E : 1.0;
+      const double meandeg = V ? (double)g->E / V : 1.0;
+      uint32_t shift = 0;
+      while (shift < 20 && (double)(2u << shift) <= meanw / std::max(meandeg, 1.0)) {
+        ++shift;
+      }
+      if (const char* env = getenv("OPENR_SPF_DSTEP_SHIFT")) {
+        shift = (uint32_t)std::min(24, std::max(0, atoi(env)));
+      }
+      q->dstep_shift = shift;
+      q->grid = std::min<uint32_t>(std::max<uint32_t>(nq, 1), (uint32_t)g->num_cus);
     } else if (ctl <= kLdsLimit) {
       q->dist = bfs ? DistPlan::BfsGmem : DistPlan::SsspGmem;
       q->lds_bytes = ctl;
@@ -1728,7 +2043,8 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
   if (dist_bytes && hipMalloc(&q->d_dist, dist_bytes) != hipSuccess) {
     return bail(fail(SPF_E_NOMEM, "distance rows"));
   }
-  if ((q->dist == DistPlan::SsspGmem || q->dist == DistPlan::BfsGmem) &&
+  if ((q->dist == DistPlan::SsspGmem || q->dist == DistPlan::BfsGmem ||
+       q->dist == DistPlan::Dstep) &&
       hipMalloc((void**)&q->d_scratch, (size_t)q->grid * V * 4) !=
           hipSuccess) {
     return bail(fail(SPF_E_NOMEM, "queue scratch"));
@@ -1809,6 +2125,75 @@ int dispatch_flags(spf_query* q, bool unit, bool ign, bool gmem) {
   }
   return gmem ? launch_sssp<WMAX, false, false, true>(q)
               : launch_sssp<WMAX, false, false, false>(q);
+}
+
+template <int WMAX, bool IGN, uint32_t BS>
+int launch_dstep_t(spf_query* q) {
+  spf_graph* g = q->g;
+  DstepArgs d;
+  SsspArgs& a = d.s;
+  a.row = g->d_row;
+  a.col = g->d_col;
+  a.wout = g->d_wout;
+  a.win = g->d_win;
+  a.link = g->d_link;
+  a.rev = g->d_rev;
+  a.slot = g->d_slot;
+  a.trbits = g->d_tr;
+  a.src = q->d_src;
+  a.ign_off = q->d_ign_off;
+  a.ign = q->d_ign;
+  a.nh_off = q->d_nh_off;
+  a.nh_w = q->d_nh_w;
+  a.dist_out = (uint32_t*)q->d_dist;
+  a.nh_out = q->d_nh;
+  a.gscratch = q->d_scratch;
+  a.V = g->V;
+  a.Vp = q->Vp;
+  a.nbw = g->nbw;
+  a.nq = q->nq;
+  a.G = g->G;
+  a.ign_cap = q->ign_cap;
+  // lanes per node: fewer than the median degree, so more nodes (and more
+  // independent HBM gathers) are in flight per CU; OPENR_SPF_DSTEP_G overrides
+  uint32_t G = 8;
+  if (const char* env = getenv("OPENR_SPF_DSTEP_G")) {
+    const int x = atoi(env);
+    if (x == 1 || x == 2 || x == 4 || x == 8 || x == 16 || x == 32 || x == 64) {
+      G = (uint32_t)x;
+    }
+  }
+  a.G = G;
+  d.shift = q->dstep_shift;
+  auto kern = spf_dstep_kernel<WMAX, IGN, BS>;
+  HIP_TRY(hipFuncSetAttribute(
+      (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (int)q->lds_bytes));
+  hipLaunchKernelGGL(kern, dim3(q->grid), dim3(BS), q->lds_bytes, g->stream, d);
+  HIP_TRY(hipGetLastError());
+  return SPF_OK;
+}
+
+template <uint32_t BS>
+int launch_dstep_bs(spf_query* q) {
+  const bool ign = q->has_ign;
+  switch (q->wmax) {
+  case 0:
+    return ign ? launch_dstep_t<0, true, BS>(q) : launch_dstep_t<0, false, BS>(q);
+  case 1:
+    return ign ? launch_dstep_t<1, true, BS>(q) : launch_dstep_t<1, false, BS>(q);
+  case 4:
+    return ign ? launch_dstep_t<4, true, BS>(q) : launch_dstep_t<4, false, BS>(q);
+  default:
+    return ign ? launch_dstep_t<16, true, BS>(q) : launch_dstep_t<16, false, BS>(q);
+  }
+}
+
+// 1024-thread workgroups: the LDS image allows one workgroup per CU, so the
+// block size sets how many waves (and gathers) a CU keeps in flight
+int launch_dstep(spf_query* q) {
+  const char* env = getenv("OPENR_SPF_DSTEP_BS");
+  return (env && atoi(env) == 512) ? launch_dstep_bs<512>(q) : launch_dstep_bs<1024>(q);
 }
 
 int launch_bfs(spf_query* q, bool unit) {
@@ -1993,6 +2378,8 @@ int run_plan(spf_query* q) {
   switch (q->dist) {
   case DistPlan::Exact:
     return launch_exact(q);
+  case DistPlan::Dstep:
+    return launch_dstep(q);
   case DistPlan::MsBfs: {
     int s = launch_msbfs(q, unit);
     if (s == SPF_OK && q->nh == NhPlan::Levels) {
@@ -2144,6 +2531,8 @@ const char* spf_query_kernel_name(const spf_query* q) {
     return q->nh == NhPlan::Rows ? "bfs-gmem+rows" : "bfs-gmem";
   case DistPlan::MsBfs:
     return q->nh == NhPlan::Levels ? "msbfs+levels" : "msbfs";
+  case DistPlan::Dstep:
+    return "dstep";
   default:
     return "exact";
   }

@@ -153,8 +153,38 @@ def test_gmem_kernel_large_graph(gpu_ready):
     csr = abi.Csr.from_links(V, links)
     g = abi.Graph(csr)
     q = g.query([0, 12345], abi.SPF_F_NEXTHOPS).run()
-    assert q.kernel == "gmem"
+    assert q.kernel == "dstep"
     check_query(csr, q, [0, 12345], True)
+
+
+@pytest.mark.parametrize("seed", [31, 32])
+def test_dstep_vs_frontier_gmem(gpu_ready, seed, monkeypatch):
+    """Delta-stepping (large weighted graphs) against the literal replay
+    and against the frontier Bellman-Ford gmem kernel on the same batch:
+    drained nodes, parallel links, asymmetric metrics, ignore lists, several
+    bucket widths (incl. the saturated last bucket)."""
+    rng = random.Random(seed)
+    V = 40000
+    links = random_links(rng, V, 120000, wmin=1, wmax=300, parallel=0.02)
+    ov = np.zeros(V, dtype=np.uint8)
+    ov[rng.sample(range(V), 400)] = 1
+    csr = abi.Csr.from_links(V, links, overloaded=ov)
+    g = abi.Graph(csr)
+    srcs = [0, 777, 39999]
+    ign = [[], sorted(rng.sample(range(len(links)), 50)), [int(csr.link_id[csr.row_ptr[39999]])]]
+    for shift in ("0", "3", "9", "20"):
+        monkeypatch.setenv("OPENR_SPF_DSTEP_SHIFT", shift)
+        q = g.query(srcs, abi.SPF_F_NEXTHOPS, ignore=ign).run()
+        assert q.kernel == "dstep"
+        check_query(csr, q, srcs, True, ignore=ign, rows={0, 1, 2} if shift == "3" else {1})
+        if shift == "9":
+            monkeypatch.setenv("OPENR_SPF_DSTEP", "0")
+            r = g.query(srcs, abi.SPF_F_NEXTHOPS, ignore=ign).run()
+            monkeypatch.delenv("OPENR_SPF_DSTEP")
+            assert r.kernel == "gmem"
+            for i in range(len(srcs)):
+                assert (q.dist(i) == r.dist(i)).all()
+                assert (q.nexthops(i) == r.nexthops(i)).all()
 
 
 def test_transit_update(gpu_ready):

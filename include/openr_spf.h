@@ -153,6 +153,15 @@ int spf_query_order(spf_query* q, uint32_t i, uint32_t* out /*[V]*/);
 int spf_query_device_rows(
     spf_query* q, void** dist_rows, uint32_t* dist_elem_bytes,
     void** nh_rows, uint64_t* nh_total_words);
+/* Copy distance rows [first, first+count) as uint32 (V entries each,
+ * SPF_UNREACHABLE -> 0xFFFFFFFF) into dst, dst_pitch bytes apart: device
+ * memory (asynchronous, on the graph stream — e.g. a slice of a tensor an
+ * RCCL all-gather then exchanges) or host memory (synchronous).  The
+ * all-sources counterpart of reading NodeSpfResult::metric() per node
+ * (LinkState.h:203-257).  SPF_E_UNSUPPORTED for 64-bit (exact) rows. */
+int spf_query_fetch_rows(
+    spf_query* q, uint32_t first, uint32_t count, void* dst, size_t dst_pitch,
+    int dst_on_device);
 /* Elements between consecutive distance rows (>= V). */
 uint32_t spf_query_row_stride(const spf_query* q);
 

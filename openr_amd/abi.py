@@ -51,6 +51,7 @@ EXPORTED_SYMBOLS = (
     "spf_query_order",
     "spf_query_device_rows",
     "spf_query_row_stride",
+    "spf_query_fetch_rows",
 )
 
 
@@ -133,6 +134,7 @@ def load():
         "spf_query_nexthops": (C.c_int, [vp, u32, pu64]),
         "spf_query_order": (C.c_int, [vp, u32, pu32]),
         "spf_query_row_stride": (u32, [vp]),
+        "spf_query_fetch_rows": (C.c_int, [vp, u32, u32, vp, C.c_size_t, C.c_int]),
         "spf_query_device_rows": (
             C.c_int,
             [vp, C.POINTER(vp), pu32, C.POINTER(vp), pu64],
@@ -387,6 +389,14 @@ class Query:
         out = np.zeros(self.graph.V, dtype=np.uint32)
         _check(load().spf_query_order(self.h, i, _p(out, C.c_uint32)), "order")
         return out
+
+    def fetch_rows(self, first: int, count: int, dst_ptr: int, pitch: int, on_device=True):
+        """Copy uint32 distance rows into caller memory (device: async on
+        the graph stream)."""
+        _check(
+            load().spf_query_fetch_rows(self.h, first, count, dst_ptr, pitch, 1 if on_device else 0),
+            "fetch_rows",
+        )
 
     def device_rows(self):
         dp = C.c_void_p()

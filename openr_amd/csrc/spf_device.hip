@@ -38,6 +38,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <queue>
 #include <string>
 #include <vector>
 
@@ -684,6 +686,291 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
       __syncthreads();
     }
     __syncthreads();
+  }
+}
+
+// ------------------------- multi-source delta-stepping (distance rows only)
+//
+// Many-source distance rows on weighted graphs whose row does not fit LDS
+// (the 100k WAN all-sources pass).  One workgroup solves a BATCH of
+// kMsdK = 32 sources at once over a node-major slab D[v][32] in HBM — one
+// 128-byte line per node — so relaxing an edge u->x fetches ONE line of x
+// and serves every source of the batch whose (u, s) is being expanded, where
+// a per-source kernel fetches a whole line per (edge, source) and uses 4 B of
+// it.  The host groups graph-near sources into a batch (spf_query_create),
+// which keeps their bucket fronts aligned so most lanes of a line do work.
+//
+// State per batch: D (global slab), pend[v] (global, bit s = D[v][s] dropped
+// and not yet expanded), bmin[v] (LDS byte: smallest bucket d >> shift among
+// v's pending lanes, 255 = none) and a dirty bitmap (LDS).  Loop over
+// buckets `cur`:
+//   CLAIM  for each candidate node (nodes dirtied by the last RELAX, or — when
+//          that leaves nothing in bucket cur — every node whose bmin is the
+//          next smallest bucket): pending lanes whose bucket <= cur are
+//          claimed (bits cleared) and queued with their lane mask (overloaded
+//          nodes keep only the lanes they are the source of), bmin is
+//          recomputed over the remaining lanes;
+//   RELAX  every queued (v, mask) relaxes v's out-edges for the lanes of the
+//          mask: c = D[v][s] + w; atomicMin(D[x][s], c); a drop sets
+//          pend[x] bit s and dirty[x].
+// The two phases are barrier-separated, so a pend bit is never set and
+// cleared concurrently; every drop of D[v][s] is followed by its pend bit and
+// every claimed lane is expanded with its CURRENT D[v][s] (<= the claimed
+// value).  The loop therefore ends at the unique fixpoint: Dijkstra distances
+// in which only the source or non-overloaded nodes relax (LinkState.cpp:
+// 806-880).  Reads of D / pend whose value decides a claim or
+// an expansion bypass the (non-coherent) vector L1 (agent-scope atomic loads).
+constexpr uint32_t kMsdK = 32;     // sources per batch = lanes per node line
+constexpr uint32_t kMsdTile = 128; // nodes per LDS transpose tile (row write)
+
+struct MsdArgs {
+  const uint32_t* row;
+  const uint32_t* col;
+  const uint32_t* wout;
+  const uint32_t* trbits;
+  const uint32_t* src;  // [nq] source node of query i
+  const uint32_t* perm; // [nbatch * 32] query of each batch lane (~0 = none)
+  uint32_t* dist_out;   // [nq][Vp]
+  uint32_t* slab;       // [grid][V][32]
+  uint32_t* pend;       // [grid][V]
+  uint32_t* qa;         // [grid][V] candidate nodes
+  uint32_t* qb;         // [grid][V] claimed nodes
+  uint32_t* qm;         // [grid][V] claimed lane masks
+  uint32_t V;
+  uint32_t Vp;
+  uint32_t nbw;
+  uint32_t nbatch;
+  uint32_t shift; // bucket width 2^shift
+};
+
+__device__ __forceinline__ uint32_t ld_coh(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint32_t min4b(uint32_t x) {
+  return min(min(x & 255u, (x >> 8) & 255u), min((x >> 16) & 255u, x >> 24));
+}
+
+// smallest bmin byte over the (255-padded) array
+template <uint32_t BS>
+__device__ __forceinline__ uint32_t msd_min_bucket(
+    const uint32_t* bw, uint32_t nw, uint32_t* scan) {
+  constexpr uint32_t kW = BS / 64;
+  uint32_t m = 255;
+  for (uint32_t i = threadIdx.x; i < nw; i += BS) {
+    m = min(m, min4b(bw[i]));
+  }
+  m = grp_min(m, 64);
+  if ((threadIdx.x & 63u) == 0) {
+    scan[threadIdx.x >> 6] = m;
+  }
+  __syncthreads();
+  uint32_t r = 255;
+#pragma unroll
+  for (uint32_t i = 0; i < kW; ++i) {
+    r = min(r, scan[i]);
+  }
+  __syncthreads();
+  return r;
+}
+
+// nodes whose bmin byte is <= cur -> queue (ascending)
+template <uint32_t BS>
+__device__ __forceinline__ uint32_t msd_compact_le(
+    const uint32_t* bw, uint32_t nw, uint32_t cur, uint32_t* queue,
+    uint32_t* scan) {
+  const uint32_t chunk = (nw + BS - 1) / BS;
+  const uint32_t w0 = min(threadIdx.x * chunk, nw);
+  const uint32_t w1 = min(w0 + chunk, nw);
+  uint32_t cnt = 0;
+  for (uint32_t w = w0; w < w1; ++w) {
+    const uint32_t x = bw[w];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      cnt += ((x >> (8 * k)) & 255u) <= cur;
+    }
+  }
+  uint32_t total;
+  uint32_t off = block_excl_scan<BS>(cnt, scan, &total);
+  for (uint32_t w = w0; w < w1; ++w) {
+    const uint32_t x = bw[w];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      if (((x >> (8 * k)) & 255u) <= cur) {
+        queue[off++] = w * 4 + k;
+      }
+    }
+  }
+  return total;
+}
+
+template <uint32_t BS>
+__global__ __launch_bounds__(BS) void spf_msdstep_kernel(MsdArgs a) {
+  extern __shared__ __align__(16) uint32_t smem[];
+  constexpr uint32_t kW = BS / 64;
+  const uint32_t V = a.V, nbw = a.nbw, shift = a.shift, tid = threadIdx.x;
+  const uint32_t lane = tid & 63u, wid = tid >> 6, s = tid & 31u;
+  const uint32_t half = lane >> 5;
+  const uint32_t nw = (V + 3) / 4; // bmin words
+  uint32_t* ctl = smem;              // [0] claimed count, [1..] scan scratch
+  uint32_t* dirty = ctl + kCtlWords; // [nbw]
+  uint32_t* tile = dirty + nbw;      // [32][kMsdTile + 1]
+  uint32_t* bw = tile + kMsdK * (kMsdTile + 1);
+  uint8_t* bmin = reinterpret_cast<uint8_t*>(bw);
+  uint32_t* D = a.slab + (size_t)blockIdx.x * V * kMsdK;
+  uint32_t* pend = a.pend + (size_t)blockIdx.x * V;
+  uint32_t* qa = a.qa + (size_t)blockIdx.x * V;
+  uint32_t* qb = a.qb + (size_t)blockIdx.x * V;
+  uint32_t* qm = a.qm + (size_t)blockIdx.x * V;
+
+  for (uint32_t i = tid; i < nbw; i += BS) {
+    dirty[i] = 0;
+  }
+  if (tid == 0) {
+    ctl[0] = 0;
+  }
+
+  for (uint32_t b = blockIdx.x; b < a.nbatch; b += gridDim.x) {
+    const uint32_t myq = a.perm[b * kMsdK + s];
+    const uint32_t mysrc = myq != kInf32 ? a.src[myq] : kInf32;
+    // reset the slab, the pending masks and the buckets
+    {
+      uint4* D4 = reinterpret_cast<uint4*>(D);
+      const uint4 inf4 = make_uint4(kInf32, kInf32, kInf32, kInf32);
+      const size_t n4 = (size_t)V * (kMsdK / 4);
+      for (size_t i = tid; i < n4; i += BS) {
+        D4[i] = inf4;
+      }
+      for (uint32_t v = tid; v < V; v += BS) {
+        pend[v] = 0;
+      }
+      for (uint32_t i = tid; i < nw; i += BS) {
+        bw[i] = 0xFFFFFFFFu;
+      }
+    }
+    __threadfence();
+    __syncthreads();
+    if (tid < kMsdK && mysrc != kInf32) {
+      atomicMin(&D[(size_t)mysrc * kMsdK + s], 0u);
+      atomicOr(&pend[mysrc], 1u << s);
+      bmin[mysrc] = 0;
+    }
+    __threadfence();
+    __syncthreads();
+
+    uint32_t cur = 0;
+    bool from_scan = true;
+    for (;;) {
+      // ---- candidates
+      uint32_t na;
+      if (from_scan) {
+        const uint32_t m = msd_min_bucket<BS>(bw, nw, ctl + 1);
+        if (m >= 255) {
+          break;
+        }
+        cur = m;
+        na = msd_compact_le<BS>(bw, nw, cur, qa, ctl + 1);
+      } else {
+        na = compact_bits<uint32_t, BS>(dirty, nbw, qa, ctl + 1);
+      }
+      __threadfence();
+      __syncthreads();
+      // ---- CLAIM: one half-wave per candidate node, lane = source slot
+      for (uint32_t i = wid * 2 + half; i < na; i += kW * 2) {
+        const uint32_t v = qa[i];
+        const uint32_t pm = ld_coh(&pend[v]);
+        const bool pl = (pm >> s) & 1u;
+        uint32_t bk = 255;
+        if (pl) {
+          bk = min(ld_coh(&D[(size_t)v * kMsdK + s]) >> shift, 254u);
+        }
+        const bool el = pl && bk <= cur;
+        const uint32_t em = (uint32_t)(__ballot(el) >> (half * 32));
+        const uint32_t eqm = (uint32_t)(__ballot(mysrc == v) >> (half * 32));
+        const uint32_t rest = grp_min((pl && !el) ? bk : 255u, 32);
+        if (s == 0) {
+          bmin[v] = (uint8_t)rest;
+          if (em) {
+            atomicAnd(&pend[v], ~em);
+            const bool transit = (a.trbits[v >> 5] >> (v & 31)) & 1u;
+            const uint32_t xm = transit ? em : (em & eqm);
+            if (xm) {
+              const uint32_t k = atomicAdd(&ctl[0], 1u);
+              qb[k] = v;
+              qm[k] = xm;
+            }
+          }
+        }
+      }
+      __threadfence();
+      __syncthreads();
+      const uint32_t nb = ctl[0];
+      __syncthreads();
+      if (nb == 0) {
+        from_scan = true;
+        continue;
+      }
+      if (tid == 0) {
+        ctl[0] = 0; // next CLAIM starts after the barrier closing RELAX
+      }
+      // ---- RELAX: one wave per claimed node, half-waves take alternate
+      // edges, 4 edges per half-wave in flight
+      for (uint32_t i = wid; i < nb; i += kW) {
+        const uint32_t v = qb[i], m = qm[i];
+        const bool act = (m >> s) & 1u;
+        const uint32_t dv = act ? ld_coh(&D[(size_t)v * kMsdK + s]) : kInf32;
+        const uint32_t beg = a.row[v], end = a.row[v + 1];
+        for (uint32_t e0 = beg; e0 < end; e0 += 8) {
+          uint32_t x[4], w[4], old[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t e = e0 + half + 2 * j;
+            x[j] = e < end ? a.col[e] : kInf32;
+            w[j] = e < end ? a.wout[e] : 0u;
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            old[j] = (act && x[j] != kInf32) ? D[(size_t)x[j] * kMsdK + s] : 0u;
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            bool imp = false;
+            if (act && x[j] != kInf32) {
+              const uint32_t c = dv + w[j];
+              if (c < old[j]) {
+                imp = atomicMin(&D[(size_t)x[j] * kMsdK + s], c) > c;
+              }
+            }
+            const uint32_t im = (uint32_t)(__ballot(imp) >> (half * 32));
+            if (im && s == 0) {
+              atomicOr(&pend[x[j]], im);
+              atomicOr(&dirty[x[j] >> 5], 1u << (x[j] & 31));
+            }
+          }
+        }
+      }
+      __threadfence();
+      __syncthreads();
+      from_scan = false;
+    }
+
+    // ---- rows out: D[v][s] -> dist_out[query of s][v], via LDS tiles
+    for (uint32_t v0 = 0; v0 < V; v0 += kMsdTile) {
+      for (uint32_t i = tid; i < kMsdTile * kMsdK; i += BS) {
+        const uint32_t vv = i / kMsdK, ss = i % kMsdK, v = v0 + vv;
+        tile[ss * (kMsdTile + 1) + vv] =
+            v < V ? ld_coh(&D[(size_t)v * kMsdK + ss]) : kInf32;
+      }
+      __syncthreads();
+      for (uint32_t i = tid; i < kMsdTile * kMsdK; i += BS) {
+        const uint32_t ss = i / kMsdTile, vv = i % kMsdTile, v = v0 + vv;
+        const uint32_t q = a.perm[b * kMsdK + ss];
+        if (q != kInf32 && v < V) {
+          a.dist_out[(size_t)q * a.Vp + v] = tile[ss * (kMsdTile + 1) + vv];
+        }
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -1434,7 +1721,7 @@ struct spf_graph {
 };
 
 // How a batch is computed.
-enum class DistPlan { SsspLds, SsspGmem, BfsLds, BfsGmem, MsBfs, Dstep, Exact };
+enum class DistPlan { SsspLds, SsspGmem, BfsLds, BfsGmem, MsBfs, Dstep, MsDstep, Exact };
 enum class NhPlan { None, Inline, Rows, Levels };
 
 struct spf_query {
@@ -1456,6 +1743,10 @@ struct spf_query {
   uint32_t *d_src = nullptr, *d_ign_off = nullptr, *d_ign = nullptr,
            *d_nh_w = nullptr, *d_order = nullptr, *d_scratch = nullptr;
   int32_t* d_row_of = nullptr;
+  // multi-source delta-stepping: lane -> query map, node-major slab and
+  // per-workgroup pend / candidate / claimed / mask arrays
+  uint32_t msd_nbatch = 0;
+  uint32_t *d_perm = nullptr, *d_slab = nullptr, *d_msd = nullptr;
   uint64_t* d_nh_off = nullptr;
   void* d_dist = nullptr;
   uint64_t* d_nh = nullptr;
@@ -1513,7 +1804,8 @@ void free_query(spf_query* q) {
        {(void*)q->d_src, (void*)q->d_ign_off, (void*)q->d_ign,
         (void*)q->d_nh_w, (void*)q->d_order, (void*)q->d_scratch,
         (void*)q->d_nh_off, q->d_dist, (void*)q->d_nh, (void*)q->d_row_of,
-        (void*)q->d_lvl, (void*)q->d_flags}) {
+        (void*)q->d_lvl, (void*)q->d_flags, (void*)q->d_perm,
+        (void*)q->d_slab, (void*)q->d_msd}) {
     if (p) {
       (void)hipFree(p);
     }
@@ -1600,6 +1892,135 @@ inline size_t lds_ctl_bytes(const spf_graph* g, uint32_t ign_cap) {
 
 inline size_t lds_state_bytes(uint32_t V) {
   return (size_t)((V + 1) & ~1u) * 2 + (size_t)V * 4; // u16 queue + u32 dist
+}
+
+inline size_t msd_lds_bytes(const spf_graph* g) {
+  return ((size_t)kCtlWords + g->nbw + kMsdK * (kMsdTile + 1) + (g->V + 3) / 4) * 4;
+}
+
+// Batches of kMsdK queries for spf_msdstep_kernel, graph-near sources
+// together: from each unassigned seed, a Dijkstra truncated at `cap` settled
+// nodes collects the nearest sources of unassigned queries.  Seeds whose
+// search cannot fill a batch leave their queries to a tail that is packed in
+// query order.  Any grouping gives the same rows; this one keeps the bucket
+// fronts of a batch aligned (more useful lanes per fetched line).
+std::vector<uint32_t> msd_batches(
+    const spf_graph* g, const uint32_t* srcs, uint32_t nq, bool cluster) {
+  std::vector<uint32_t> perm;
+  perm.reserve(((size_t)nq + kMsdK - 1) / kMsdK * kMsdK);
+  if (!cluster) {
+    for (uint32_t i = 0; i < nq; ++i) {
+      perm.push_back(i);
+    }
+  } else {
+    const uint32_t V = g->V;
+    std::vector<uint32_t> head(V + 1, 0), at(nq);
+    for (uint32_t i = 0; i < nq; ++i) {
+      ++head[srcs[i] + 1];
+    }
+    for (uint32_t v = 0; v < V; ++v) {
+      head[v + 1] += head[v];
+    }
+    {
+      std::vector<uint32_t> fill(head.begin(), head.end() - 1);
+      for (uint32_t i = 0; i < nq; ++i) {
+        at[fill[srcs[i]]++] = i;
+      }
+    }
+    std::vector<uint32_t> taken(V, 0); // queries of node v already assigned
+    std::vector<uint32_t> stamp(V, 0), dist(V, 0);
+    std::vector<uint32_t> tail, batch;
+    uint32_t epoch = 0;
+    const uint32_t cap = (uint32_t)std::min<uint64_t>(
+        8192, std::max<uint64_t>(256, 8ull * kMsdK * V / std::max(nq, 1u)));
+    using HE = std::pair<uint64_t, uint32_t>;
+    std::vector<HE> heap;
+    for (uint32_t i = 0; i < nq; ++i) {
+      const uint32_t s0 = srcs[i];
+      if (taken[s0] == head[s0 + 1] - head[s0]) {
+        continue; // every query of this source is placed
+      }
+      ++epoch;
+      batch.clear();
+      heap.clear();
+      heap.push_back({0, s0});
+      stamp[s0] = epoch;
+      dist[s0] = 0;
+      uint32_t settled = 0;
+      while (!heap.empty() && batch.size() < kMsdK && settled < cap) {
+        std::pop_heap(heap.begin(), heap.end(), std::greater<HE>());
+        const HE top = heap.back();
+        heap.pop_back();
+        const uint32_t u = top.second;
+        if (top.first != dist[u]) {
+          continue;
+        }
+        ++settled;
+        while (taken[u] < head[u + 1] - head[u] && batch.size() < kMsdK) {
+          batch.push_back(at[head[u] + taken[u]++]);
+        }
+        for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
+          const uint32_t x = g->col[e];
+          const uint32_t c = (uint32_t)std::min<uint64_t>(
+              (uint64_t)dist[u] + std::max<uint64_t>(g->w64[e], 1), 0xFFFFFFFEull);
+          if (stamp[x] != epoch || c < dist[x]) {
+            stamp[x] = epoch;
+            dist[x] = c;
+            heap.push_back({c, x});
+            std::push_heap(heap.begin(), heap.end(), std::greater<HE>());
+          }
+        }
+      }
+      auto& dst = batch.size() == kMsdK ? perm : tail;
+      dst.insert(dst.end(), batch.begin(), batch.end());
+    }
+    perm.insert(perm.end(), tail.begin(), tail.end());
+  }
+  while (perm.size() % kMsdK) {
+    perm.push_back(kInf32);
+  }
+  return perm;
+}
+
+// bucket width for spf_msdstep_kernel: the eccentricity of one source (host
+// Dijkstra) spread over ~200 of the 255 bucket bytes; at least the
+// delta-stepping Delta ~ mean metric / mean degree.
+uint32_t msd_shift(const spf_graph* g, uint32_t s0) {
+  const uint32_t V = g->V;
+  std::vector<uint64_t> dist(V, UINT64_MAX);
+  using HE = std::pair<uint64_t, uint32_t>;
+  std::priority_queue<HE, std::vector<HE>, std::greater<HE>> pq;
+  dist[s0] = 0;
+  pq.push({0, s0});
+  uint64_t ecc = 0, wsum = 0;
+  while (!pq.empty()) {
+    const HE t = pq.top();
+    pq.pop();
+    if (t.first != dist[t.second]) {
+      continue;
+    }
+    ecc = std::max(ecc, t.first);
+    const uint32_t u = t.second;
+    for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
+      const uint64_t c = t.first + g->w64[e];
+      if (c < dist[g->col[e]]) {
+        dist[g->col[e]] = c;
+        pq.push({c, g->col[e]});
+      }
+    }
+  }
+  for (uint32_t e = 0; e < g->E; ++e) {
+    wsum += g->w64[e];
+  }
+  const double delta = g->E && V ? ((double)wsum / g->E) / ((double)g->E / V) : 1.0;
+  uint32_t shift = 0;
+  while (shift < 24 && ((ecc >> shift) > 200 || (double)(2u << shift) <= delta)) {
+    ++shift;
+  }
+  if (const char* env = getenv("OPENR_SPF_MSD_SHIFT")) {
+    shift = (uint32_t)std::min(24, std::max(0, atoi(env)));
+  }
+  return shift;
 }
 
 } // namespace
@@ -1900,7 +2321,8 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
 
   // ---- plan: which kernels compute this batch
   std::vector<int32_t> row_of;
-  const bool exact = (g->exact && !unit) || want_order;
+  std::vector<uint32_t> msd_perm;
+  const bool exact =(g->exact && !unit) || want_order;
   const bool uniform = unit || g->uniform != 0;
   bool rows_ok = false;
   if (want_nh && !exact && !has_ign) {
@@ -1937,6 +2359,11 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
         (((size_t)V + 15) & ~(size_t)15);
     const bool dstep = big && !uniform && dstep_lds <= kLdsLimit && maxw <= 16 &&
                        getenv("OPENR_SPF_DSTEP") == nullptr;
+    // many distance-only rows of such a graph: 32 sources per workgroup over
+    // a node-major slab (OPENR_SPF_MSD=0 disables)
+    const char* msd_env = getenv("OPENR_SPF_MSD");
+    const bool msd = big && !uniform && !want_nh && !has_ign && nq >= 2 * kMsdK &&
+                     msd_lds_bytes(g) <= kLdsLimit && !(msd_env && atoi(msd_env) == 0);
     if (dstep && q->nh == NhPlan::Rows) {
       q->nh = NhPlan::Inline;
     }
@@ -1945,7 +2372,17 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     q->ign_cap = has_ign ? std::min(max_ign, kIgnLdsMax) : 0;
     const size_t ctl = lds_ctl_bytes(g, q->ign_cap);
     const size_t lds = ctl + lds_state_bytes(V);
-    if (V <= 65535 && lds <= kLdsLimit) {
+    if (msd) {
+      q->dist = DistPlan::MsDstep;
+      q->nh = NhPlan::None;
+      q->wmax = 0;
+      q->lds_bytes = msd_lds_bytes(g);
+      q->dstep_shift = msd_shift(g, desc->sources[0]);
+      const char* cl = getenv("OPENR_SPF_MSD_CLUSTER");
+      msd_perm = msd_batches(g, desc->sources, nq, !(cl && atoi(cl) == 0));
+      q->msd_nbatch = (uint32_t)(msd_perm.size() / kMsdK);
+      q->grid = std::min<uint32_t>(q->msd_nbatch, (uint32_t)g->num_cus);
+    } else if (V <= 65535 && lds <= kLdsLimit) {
       q->dist = bfs ? DistPlan::BfsLds : DistPlan::SsspLds;
       q->lds_bytes = lds;
       const uint32_t per_cu =
@@ -2048,6 +2485,16 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       hipMalloc((void**)&q->d_scratch, (size_t)q->grid * V * 4) !=
           hipSuccess) {
     return bail(fail(SPF_E_NOMEM, "queue scratch"));
+  }
+  if (q->dist == DistPlan::MsDstep) {
+    const size_t gv = (size_t)q->grid * V;
+    if ((s = dev_upload(&q->d_perm, msd_perm.data(), msd_perm.size()))) {
+      return bail(s);
+    }
+    if (hipMalloc((void**)&q->d_slab, gv * kMsdK * 4) != hipSuccess ||
+        hipMalloc((void**)&q->d_msd, gv * 4 * 4) != hipSuccess) {
+      return bail(fail(SPF_E_NOMEM, "multi-source slab"));
+    }
   }
   if (ex && (size_t)nq * V) {
     if (hipMalloc((void**)&q->d_scratch, (size_t)nq * V * 8) != hipSuccess ||
@@ -2156,7 +2603,7 @@ int launch_dstep_t(spf_query* q) {
   a.ign_cap = q->ign_cap;
   // lanes per node: fewer than the median degree, so more nodes (and more
   // independent HBM gathers) are in flight per CU; OPENR_SPF_DSTEP_G overrides
-  uint32_t G = 8;
+  uint32_t G = 4;
   if (const char* env = getenv("OPENR_SPF_DSTEP_G")) {
     const int x = atoi(env);
     if (x == 1 || x == 2 || x == 4 || x == 8 || x == 16 || x == 32 || x == 64) {
@@ -2194,6 +2641,36 @@ int launch_dstep_bs(spf_query* q) {
 int launch_dstep(spf_query* q) {
   const char* env = getenv("OPENR_SPF_DSTEP_BS");
   return (env && atoi(env) == 512) ? launch_dstep_bs<512>(q) : launch_dstep_bs<1024>(q);
+}
+
+int launch_msdstep(spf_query* q) {
+  spf_graph* g = q->g;
+  MsdArgs a;
+  a.row = g->d_row;
+  a.col = g->d_col;
+  a.wout = g->d_wout;
+  a.trbits = g->d_tr;
+  a.src = q->d_src;
+  a.perm = q->d_perm;
+  a.dist_out = (uint32_t*)q->d_dist;
+  a.slab = q->d_slab;
+  const size_t gv = (size_t)q->grid * g->V;
+  a.pend = q->d_msd;
+  a.qa = q->d_msd + gv;
+  a.qb = q->d_msd + 2 * gv;
+  a.qm = q->d_msd + 3 * gv;
+  a.V = g->V;
+  a.Vp = q->Vp;
+  a.nbw = g->nbw;
+  a.nbatch = q->msd_nbatch;
+  a.shift = q->dstep_shift;
+  auto kern = spf_msdstep_kernel<1024>;
+  HIP_TRY(hipFuncSetAttribute(
+      (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (int)q->lds_bytes));
+  hipLaunchKernelGGL(kern, dim3(q->grid), dim3(1024), q->lds_bytes, g->stream, a);
+  HIP_TRY(hipGetLastError());
+  return SPF_OK;
 }
 
 int launch_bfs(spf_query* q, bool unit) {
@@ -2380,6 +2857,8 @@ int run_plan(spf_query* q) {
     return launch_exact(q);
   case DistPlan::Dstep:
     return launch_dstep(q);
+  case DistPlan::MsDstep:
+    return launch_msdstep(q);
   case DistPlan::MsBfs: {
     int s = launch_msbfs(q, unit);
     if (s == SPF_OK && q->nh == NhPlan::Levels) {
@@ -2533,6 +3012,8 @@ const char* spf_query_kernel_name(const spf_query* q) {
     return q->nh == NhPlan::Levels ? "msbfs+levels" : "msbfs";
   case DistPlan::Dstep:
     return "dstep";
+  case DistPlan::MsDstep:
+    return "msdstep";
   default:
     return "exact";
   }
@@ -2616,6 +3097,39 @@ int spf_query_device_rows(
   }
   if (nh_total_words) {
     *nh_total_words = q->nh_total;
+  }
+  return SPF_OK;
+}
+
+int spf_query_fetch_rows(
+    spf_query* q, uint32_t first, uint32_t count, void* dst, size_t dst_pitch,
+    int dst_on_device) {
+  if (!q || (count && !dst)) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  if (!q->ran) {
+    return fail(SPF_E_INVALID, "query has not run");
+  }
+  if ((uint64_t)first + count > q->nq) {
+    return fail(SPF_E_INVALID, "row range out of bounds");
+  }
+  if (q->dist == DistPlan::Exact) {
+    return fail(SPF_E_UNSUPPORTED, "64-bit distance rows: use spf_query_dist");
+  }
+  const size_t V = q->g->V;
+  if (dst_pitch < V * 4) {
+    return fail(SPF_E_INVALID, "destination pitch < 4*V");
+  }
+  if (count == 0 || V == 0) {
+    return SPF_OK;
+  }
+  HIP_TRY(hipSetDevice(q->g->device));
+  const char* srcp = (const char*)q->d_dist + (size_t)first * q->Vp * 4;
+  HIP_TRY(hipMemcpy2DAsync(
+      dst, dst_pitch, srcp, (size_t)q->Vp * 4, V * 4, count,
+      dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, q->g->stream));
+  if (!dst_on_device) {
+    HIP_TRY(hipStreamSynchronize(q->g->stream));
   }
   return SPF_OK;
 }

@@ -187,6 +187,69 @@ def test_dstep_vs_frontier_gmem(gpu_ready, seed, monkeypatch):
                 assert (q.nexthops(i) == r.nexthops(i)).all()
 
 
+@pytest.mark.parametrize("seed", [41, 42])
+def test_msdstep_vs_dstep_and_replay(gpu_ready, seed, monkeypatch):
+    """Multi-source delta-stepping (32 sources per workgroup, node-major
+    slab) against the per-source delta-stepping kernel on every row and the
+    literal replay on two rows: drained nodes (also as sources), parallel
+    links, duplicate sources, a partial last batch, bucket widths from
+    'everything saturates into the last bucket' to 'one bucket', clustered
+    and unclustered batches."""
+    rng = random.Random(seed)
+    V = 70000
+    links = random_links(rng, V, 200000, wmin=1, wmax=300, parallel=0.02)
+    ov = np.zeros(V, dtype=np.uint8)
+    ov[rng.sample(range(V), 700)] = 1
+    csr = abi.Csr.from_links(V, links, overloaded=ov)
+    g = abi.Graph(csr)
+    drained = [int(v) for v in np.flatnonzero(ov)[:3]]
+    srcs = [rng.randrange(V) for _ in range(150)] + drained + [5, 5, 77]
+    monkeypatch.setenv("OPENR_SPF_MSD", "0")
+    ref = g.query(srcs, 0).run()
+    monkeypatch.delenv("OPENR_SPF_MSD")
+    assert ref.kernel == "dstep"
+    want = [ref.dist(i) for i in range(len(srcs))]
+    for shift, cluster in (("0", "1"), ("4", "0"), (None, "1"), ("30", "1")):
+        if shift is None:
+            monkeypatch.delenv("OPENR_SPF_MSD_SHIFT", raising=False)
+        else:
+            monkeypatch.setenv("OPENR_SPF_MSD_SHIFT", shift)
+        monkeypatch.setenv("OPENR_SPF_MSD_CLUSTER", cluster)
+        q = g.query(srcs, 0).run()
+        assert q.kernel == "msdstep"
+        for i in range(len(srcs)):
+            assert (q.dist(i) == want[i]).all(), (shift, cluster, i)
+    check_query(csr, q, srcs, True, rows={0, len(srcs) - 4})
+
+
+def test_msdstep_wan_anchor(gpu_ready):
+    """100k-node WAN (SURVEY §8(d) generator): the row of source 0 from the
+    multi-source kernel reproduces the reference runSpf checksum, and 16
+    sampled rows equal the per-source kernel's."""
+    import json
+    import os
+
+    from openr_amd import topologies as TP
+
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "wan_anchors.json")))
+    a = [x for x in gold["anchors"] if x["V"] == 100000][0]
+    topo = TP.wan(a["V"], a["L"])
+    csr = topo.csr()
+    g = abi.Graph(csr)
+    srcs = np.arange(0, a["V"], 397, dtype=np.uint32)[:256]
+    assert srcs[0] == 0
+    q = g.query(srcs, 0).run()
+    assert q.kernel == "msdstep"
+    d0 = q.dist(0)
+    assert (d0 != UNREACH).all()
+    assert int(d0.sum()) == a["sum_dist"]
+    rows = list(range(0, 256, 16))
+    r = g.query(srcs[rows], 0).run()  # 16 sources: per-source kernel
+    assert r.kernel == "dstep"
+    for k, i in enumerate(rows):
+        assert (q.dist(i) == r.dist(k)).all(), i
+
+
 def test_transit_update(gpu_ready):
     rng = random.Random(8)
     V = 120

@@ -405,6 +405,17 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
         out[v] = dist[v];
       }
     }
+    if constexpr (WMAX > 0) {
+      // rows are written when a node is reached: unreached nodes get the
+      // empty set here (the buffer is not cleared between runs)
+      for (uint32_t v = tid; v < V; v += kBlock) {
+        if (dist[v] == kInf32) {
+          for (uint32_t j = 0; j < Wm; ++j) {
+            nhrow[(size_t)v * Wm + j] = 0;
+          }
+        }
+      }
+    }
     __syncthreads();
   }
 }
@@ -427,10 +438,31 @@ struct DstepArgs {
   uint32_t shift; // bucket width 2^shift
 };
 
+// Load that bypasses the (non-coherent) vector L1: values other lanes change
+// with atomics in L2 during the same phase.
+__device__ __forceinline__ uint32_t ld_coh(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Bucket of a node: the LDS byte image (LDS-resident plan) or the node's
+// current distance in the HBM row (d >> shift, saturated at 254; the row is
+// written by this workgroup only, and every read follows a barrier).
+struct BktLds {
+  const uint8_t* b;
+  __device__ __forceinline__ uint32_t operator()(uint32_t v) const { return b[v]; }
+};
+struct BktDist {
+  const uint32_t* d;
+  uint32_t shift;
+  __device__ __forceinline__ uint32_t operator()(uint32_t v) const {
+    return min(ld_coh(d + v) >> shift, 254u);
+  }
+};
+
 // pending nodes with bucket <= cur -> queue (ascending), clearing their bits
-template <uint32_t BS>
+template <uint32_t BS, class BK>
 __device__ __forceinline__ uint32_t compact_bucket(
-    uint32_t* pend, const uint8_t* bkt, uint32_t cur, uint32_t nbw,
+    uint32_t* pend, BK bkt, uint32_t cur, uint32_t nbw,
     uint32_t* queue, uint32_t* scan) {
   const uint32_t chunk = (nbw + BS - 1) / BS;
   const uint32_t w0 = min(threadIdx.x * chunk, nbw);
@@ -441,7 +473,7 @@ __device__ __forceinline__ uint32_t compact_bucket(
     while (b) {
       const uint32_t k = __ffs(b) - 1;
       b &= b - 1;
-      cnt += bkt[w * 32 + k] <= cur;
+      cnt += bkt(w * 32 + k) <= cur;
     }
   }
   uint32_t total;
@@ -451,7 +483,7 @@ __device__ __forceinline__ uint32_t compact_bucket(
     while (b) {
       const uint32_t k = __ffs(b) - 1;
       b &= b - 1;
-      if (bkt[w * 32 + k] <= cur) {
+      if (bkt(w * 32 + k) <= cur) {
         sel |= 1u << k;
         queue[off++] = w * 32 + k;
       }
@@ -464,9 +496,9 @@ __device__ __forceinline__ uint32_t compact_bucket(
 }
 
 // smallest bucket among pending nodes (255 = none pending)
-template <uint32_t BS>
+template <uint32_t BS, class BK>
 __device__ __forceinline__ uint32_t min_pending_bucket(
-    const uint32_t* pend, const uint8_t* bkt, uint32_t nbw, uint32_t* scan) {
+    const uint32_t* pend, BK bkt, uint32_t nbw, uint32_t* scan) {
   constexpr uint32_t kWaves = BS / 64;
   uint32_t m = 255;
   for (uint32_t w = threadIdx.x; w < nbw; w += BS) {
@@ -474,7 +506,7 @@ __device__ __forceinline__ uint32_t min_pending_bucket(
     while (b) {
       const uint32_t k = __ffs(b) - 1;
       b &= b - 1;
-      m = min(m, (uint32_t)bkt[w * 32 + k]);
+      m = min(m, bkt(w * 32 + k));
     }
   }
   m = grp_min(m, 64);
@@ -491,7 +523,10 @@ __device__ __forceinline__ uint32_t min_pending_bucket(
   return r;
 }
 
-template <int WMAX, bool IGN, uint32_t BS>
+// LBK: bucket bytes in LDS (V B: one workgroup per CU on the 100k WAN);
+// otherwise buckets are read from the distance row and the LDS image is the
+// two bitmaps only, so several workgroups (sources) share a CU.
+template <int WMAX, bool IGN, uint32_t BS, bool LBK>
 __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
   extern __shared__ __align__(16) uint32_t smem[];
   const SsspArgs& a = da.s;
@@ -504,7 +539,7 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
   uint32_t* pend = act + nbw;  // improved, not yet pushed
   uint32_t* ctl = pend + nbw;
   uint32_t* ignl = ctl + kCtlWords;
-  uint8_t* bkt = reinterpret_cast<uint8_t*>(ignl + a.ign_cap);
+  uint8_t* bkt = reinterpret_cast<uint8_t*>(ignl + a.ign_cap); // LBK only
   uint32_t* queue = a.gscratch + (size_t)blockIdx.x * V;
 
   for (uint32_t i = tid; i < nbw; i += BS) {
@@ -536,7 +571,9 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
     }
     for (uint32_t v = tid; v < V; v += BS) {
       dist[v] = kInf32;
-      bkt[v] = 255;
+      if constexpr (LBK) {
+        bkt[v] = 255;
+      }
     }
     if constexpr (WMAX > 0) {
       for (uint32_t i = tid; i < V * Wm; i += BS) {
@@ -546,21 +583,75 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
     __syncthreads();
     if (tid == 0) {
       dist[src] = 0;
-      bkt[src] = 0;
+      if constexpr (LBK) {
+        bkt[src] = 0;
+      }
       pend[src >> 5] |= 1u << (src & 31);
     }
     __syncthreads();
     uint32_t cur = 0;
 
     for (;;) {
-      uint32_t qlen = compact_bucket<BS>(pend, bkt, cur, nbw, queue, ctl + 1);
+      uint32_t qlen;
+      if constexpr (LBK) {
+        qlen = compact_bucket<BS>(pend, BktLds{bkt}, cur, nbw, queue, ctl + 1);
+      } else {
+        qlen = compact_bucket<BS>(pend, BktDist{dist, shift}, cur, nbw, queue, ctl + 1);
+      }
       __syncthreads();
       if (qlen == 0) {
-        const uint32_t m = min_pending_bucket<BS>(pend, bkt, nbw, ctl + 1);
+        uint32_t m;
+        if constexpr (LBK) {
+          m = min_pending_bucket<BS>(pend, BktLds{bkt}, nbw, ctl + 1);
+        } else {
+          m = min_pending_bucket<BS>(pend, BktDist{dist, shift}, nbw, ctl + 1);
+        }
         if (m >= 255) {
           break;
         }
         cur = m;
+        continue;
+      }
+      if constexpr (WMAX == 0) {
+        // ---- distances only: push relaxation, atomicMin into the HBM row.
+        // One random access per improving edge instead of the PULL pass
+        // over every in-edge of every marked head.  An improved node is
+        // marked (LBK: in `act`, and its bucket byte is refreshed from one
+        // coherent read of its final distance after the phase; otherwise
+        // its pending bit is set and the bucket is derived from the row).
+        // du is re-read coherently: a drop of dist[u] that landed before u
+        // was claimed has already cleared its pending bit.
+        for (uint32_t i = grp; i < qlen; i += ngrp) {
+          const uint32_t u = queue[i];
+          if (u != src && !((a.trbits[u >> 5] >> (u & 31)) & 1u)) {
+            continue; // overloaded: recorded but never transited
+          }
+          const uint32_t du = ld_coh(dist + u);
+          const uint32_t beg = a.row[u], end = a.row[u + 1];
+          for (uint32_t e = beg + lg; e < end; e += G) {
+            if constexpr (IGN) {
+              if (nign && in_sorted(ignp, nign, a.link[e])) {
+                continue;
+              }
+            }
+            const uint32_t v = a.col[e];
+            const uint32_t c = du + a.wout[e];
+            if (c < dist[v] && atomicMin(&dist[v], c) > c) {
+              atomicOr(LBK ? &act[v >> 5] : &pend[v >> 5], 1u << (v & 31));
+            }
+          }
+        }
+        __syncthreads();
+        if constexpr (LBK) {
+          const uint32_t nimp = compact_bits<uint32_t, BS>(act, nbw, queue, ctl + 1);
+          __syncthreads(); // queue entries come from every wave
+          for (uint32_t i = tid; i < nimp; i += BS) {
+            const uint32_t v = queue[i];
+            bkt[v] = (uint8_t)min(ld_coh(dist + v) >> shift, 254u);
+            atomicOr(&pend[v >> 5], 1u << (v & 31));
+          }
+          __syncthreads();
+        }
         continue;
       }
       // ---- PUSH from the selected bucket
@@ -670,7 +761,9 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
           }
           if (changed) {
             dist[v] = gbest;
-            bkt[v] = (uint8_t)min(gbest >> shift, 254u);
+            if constexpr (LBK) {
+              bkt[v] = (uint8_t)min(gbest >> shift, 254u);
+            }
             if constexpr (WMAX > 0) {
 #pragma unroll
               for (int j = 0; j < WMAX; ++j) {
@@ -743,9 +836,6 @@ struct MsdArgs {
   uint32_t shift; // bucket width 2^shift
 };
 
-__device__ __forceinline__ uint32_t ld_coh(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 __device__ __forceinline__ uint32_t min4b(uint32_t x) {
   return min(min(x & 255u, (x >> 8) & 255u), min((x >> 16) & 255u, x >> 24));
@@ -1732,6 +1822,8 @@ struct spf_query {
   int wmax = 0;
   int ms_bits = 64; // MS-BFS batch width (32 or 64 sources per workgroup)
   uint32_t dstep_shift = 5; // delta-stepping bucket width 2^shift
+  bool dstep_lbk = false;    // bucket bytes in LDS (else from the dist row)
+  uint32_t dstep_bs = 1024;  // delta-stepping workgroup size
   uint32_t ign_cap = 0, grid = 0, Vp = 0, Vp8 = 0;
   uint8_t* d_lvl = nullptr;
   uint32_t* d_flags = nullptr;
@@ -2354,16 +2446,25 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     // with next hops inline (the rows plan would read every neighbour's
     // 4V-byte row per source: 8E*V bytes per all-sources pass)
     const bool big = lds_ctl_bytes(g, 0) + lds_state_bytes(V) > kLdsLimit || V > 65535;
+    // delta-stepping LDS image: pending + marked bitmaps + the bucket bytes
+    // (OPENR_SPF_DSTEP_LDSBKT=0: buckets derived from the distance row, a
+    // 25 KB image, 2 workgroups per CU — measured slower on the 100k WAN:
+    // the second 400 KB row per CU and the per-phase row reads of pending
+    // nodes cost more than the extra waves hide)
+    const char* lbk_env = getenv("OPENR_SPF_DSTEP_LDSBKT");
+    q->dstep_lbk = !(lbk_env && atoi(lbk_env) == 0);
     const size_t dstep_lds =
         (2 * (size_t)g->nbw + kCtlWords + (has_ign ? std::min(max_ign, kIgnLdsMax) : 0)) * 4 +
-        (((size_t)V + 15) & ~(size_t)15);
+        (q->dstep_lbk ? (((size_t)V + 15) & ~(size_t)15) : 0);
     const bool dstep = big && !uniform && dstep_lds <= kLdsLimit && maxw <= 16 &&
                        getenv("OPENR_SPF_DSTEP") == nullptr;
     // many distance-only rows of such a graph: 32 sources per workgroup over
-    // a node-major slab (OPENR_SPF_MSD=0 disables)
+    // a node-major slab.  Measured slower than per-source delta-stepping on
+    // the 100k WAN (0.145 vs 0.100 ms/SPF at 8192 sources: the 12.8 MB slab
+    // per workgroup does not stay on chip), so opt-in: OPENR_SPF_MSD=1.
     const char* msd_env = getenv("OPENR_SPF_MSD");
     const bool msd = big && !uniform && !want_nh && !has_ign && nq >= 2 * kMsdK &&
-                     msd_lds_bytes(g) <= kLdsLimit && !(msd_env && atoi(msd_env) == 0);
+                     msd_lds_bytes(g) <= kLdsLimit && msd_env && atoi(msd_env) == 1;
     if (dstep && q->nh == NhPlan::Rows) {
       q->nh = NhPlan::Inline;
     }
@@ -2408,7 +2509,15 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
         shift = (uint32_t)std::min(24, std::max(0, atoi(env)));
       }
       q->dstep_shift = shift;
-      q->grid = std::min<uint32_t>(std::max<uint32_t>(nq, 1), (uint32_t)g->num_cus);
+      const char* bs_env = getenv("OPENR_SPF_DSTEP_BS");
+      q->dstep_bs = (bs_env && atoi(bs_env) == 512) ? 512 : 1024;
+      // workgroups per CU: 2048 threads per CU, LDS permitting
+      uint32_t per_cu = (uint32_t)std::max<size_t>(
+          1, std::min<size_t>(2048 / q->dstep_bs, kLdsLimit / std::max<size_t>(dstep_lds, 1)));
+      if (const char* pc = getenv("OPENR_SPF_DSTEP_PERCU")) {
+        per_cu = std::max<uint32_t>(1, std::min<uint32_t>(per_cu, (uint32_t)atoi(pc)));
+      }
+      q->grid = std::min<uint32_t>(std::max<uint32_t>(nq, 1), (uint32_t)g->num_cus * per_cu);
     } else if (ctl <= kLdsLimit) {
       q->dist = bfs ? DistPlan::BfsGmem : DistPlan::SsspGmem;
       q->lds_bytes = ctl;
@@ -2602,8 +2711,10 @@ int launch_dstep_t(spf_query* q) {
   a.G = g->G;
   a.ign_cap = q->ign_cap;
   // lanes per node: fewer than the median degree, so more nodes (and more
-  // independent HBM gathers) are in flight per CU; OPENR_SPF_DSTEP_G overrides
-  uint32_t G = 4;
+  // independent HBM gathers) are in flight per CU (4 with the PULL pass of
+  // next-hop runs, 8 for the push-only distance runs: measured on the 100k
+  // WAN); OPENR_SPF_DSTEP_G overrides
+  uint32_t G = WMAX == 0 ? 8 : 4;
   if (const char* env = getenv("OPENR_SPF_DSTEP_G")) {
     const int x = atoi(env);
     if (x == 1 || x == 2 || x == 4 || x == 8 || x == 16 || x == 32 || x == 64) {
@@ -2612,7 +2723,8 @@ int launch_dstep_t(spf_query* q) {
   }
   a.G = G;
   d.shift = q->dstep_shift;
-  auto kern = spf_dstep_kernel<WMAX, IGN, BS>;
+  auto kern = q->dstep_lbk ? spf_dstep_kernel<WMAX, IGN, BS, true>
+                           : spf_dstep_kernel<WMAX, IGN, BS, false>;
   HIP_TRY(hipFuncSetAttribute(
       (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
       (int)q->lds_bytes));
@@ -2636,11 +2748,10 @@ int launch_dstep_bs(spf_query* q) {
   }
 }
 
-// 1024-thread workgroups: the LDS image allows one workgroup per CU, so the
-// block size sets how many waves (and gathers) a CU keeps in flight
+// 1024-thread workgroups: one per CU with the LDS bucket image (2 when the
+// buckets come from the distance row)
 int launch_dstep(spf_query* q) {
-  const char* env = getenv("OPENR_SPF_DSTEP_BS");
-  return (env && atoi(env) == 512) ? launch_dstep_bs<512>(q) : launch_dstep_bs<1024>(q);
+  return q->dstep_bs == 512 ? launch_dstep_bs<512>(q) : launch_dstep_bs<1024>(q);
 }
 
 int launch_msdstep(spf_query* q) {

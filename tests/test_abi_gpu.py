@@ -54,6 +54,9 @@ def check_query(csr, q, sources, use_metric, ignore=None, rows=None):
             else:
                 assert d[v] == UNREACH, (s, v)
         if q.flags & abi.SPF_F_NEXTHOPS:
+            # unreached nodes: the empty next-hop set
+            assert not q.nexthops(i)[d == UNREACH].any(), s
+        if q.flags & abi.SPF_F_NEXTHOPS:
             got = q.nexthop_sets(i, s)
             for v, (m, nhs, _, _) in ref.items():
                 if v == s:
@@ -157,12 +160,14 @@ def test_gmem_kernel_large_graph(gpu_ready):
     check_query(csr, q, [0, 12345], True)
 
 
-@pytest.mark.parametrize("seed", [31, 32])
-def test_dstep_vs_frontier_gmem(gpu_ready, seed, monkeypatch):
+@pytest.mark.parametrize("seed,ldsbkt", [(31, "1"), (32, "1"), (33, "0")])
+def test_dstep_vs_frontier_gmem(gpu_ready, seed, ldsbkt, monkeypatch):
     """Delta-stepping (large weighted graphs) against the literal replay
     and against the frontier Bellman-Ford gmem kernel on the same batch:
     drained nodes, parallel links, asymmetric metrics, ignore lists, several
-    bucket widths (incl. the saturated last bucket)."""
+    bucket widths (incl. the saturated last bucket), bucket bytes read from
+    the distance row (default) or kept in LDS."""
+    monkeypatch.setenv("OPENR_SPF_DSTEP_LDSBKT", ldsbkt)
     rng = random.Random(seed)
     V = 40000
     links = random_links(rng, V, 120000, wmin=1, wmax=300, parallel=0.02)
@@ -177,6 +182,11 @@ def test_dstep_vs_frontier_gmem(gpu_ready, seed, monkeypatch):
         q = g.query(srcs, abi.SPF_F_NEXTHOPS, ignore=ign).run()
         assert q.kernel == "dstep"
         check_query(csr, q, srcs, True, ignore=ign, rows={0, 1, 2} if shift == "3" else {1})
+        # distances only: the push / atomicMin variant must give the same rows
+        qd = g.query(srcs, 0, ignore=ign).run()
+        assert qd.kernel == "dstep"
+        for i in range(len(srcs)):
+            assert (qd.dist(i) == q.dist(i)).all(), (shift, i)
         if shift == "9":
             monkeypatch.setenv("OPENR_SPF_DSTEP", "0")
             r = g.query(srcs, abi.SPF_F_NEXTHOPS, ignore=ign).run()
@@ -184,7 +194,20 @@ def test_dstep_vs_frontier_gmem(gpu_ready, seed, monkeypatch):
             assert r.kernel == "gmem"
             for i in range(len(srcs)):
                 assert (q.dist(i) == r.dist(i)).all()
-                assert (q.nexthops(i) == r.nexthops(i)).all()
+                if not (q.nexthops(i) == r.nexthops(i)).all():
+                    bad = np.flatnonzero((q.nexthops(i) != r.nexthops(i)).any(axis=1))
+                    ok_q = ok_r = True
+                    try:
+                        check_query(csr, q, srcs, True, ignore=ign, rows={i})
+                    except AssertionError:
+                        ok_q = False
+                    try:
+                        check_query(csr, r, srcs, True, ignore=ign, rows={i})
+                    except AssertionError:
+                        ok_r = False
+                    raise AssertionError(
+                        f"row {i}: {len(bad)} nodes differ (first {bad[:5]}); "
+                        f"dstep matches replay: {ok_q}, gmem matches replay: {ok_r}")
 
 
 @pytest.mark.parametrize("seed", [41, 42])
@@ -204,10 +227,9 @@ def test_msdstep_vs_dstep_and_replay(gpu_ready, seed, monkeypatch):
     g = abi.Graph(csr)
     drained = [int(v) for v in np.flatnonzero(ov)[:3]]
     srcs = [rng.randrange(V) for _ in range(150)] + drained + [5, 5, 77]
-    monkeypatch.setenv("OPENR_SPF_MSD", "0")
     ref = g.query(srcs, 0).run()
-    monkeypatch.delenv("OPENR_SPF_MSD")
     assert ref.kernel == "dstep"
+    monkeypatch.setenv("OPENR_SPF_MSD", "1")
     want = [ref.dist(i) for i in range(len(srcs))]
     for shift, cluster in (("0", "1"), ("4", "0"), (None, "1"), ("30", "1")):
         if shift is None:
@@ -238,7 +260,11 @@ def test_msdstep_wan_anchor(gpu_ready):
     g = abi.Graph(csr)
     srcs = np.arange(0, a["V"], 397, dtype=np.uint32)[:256]
     assert srcs[0] == 0
-    q = g.query(srcs, 0).run()
+    os.environ["OPENR_SPF_MSD"] = "1"
+    try:
+        q = g.query(srcs, 0).run()
+    finally:
+        del os.environ["OPENR_SPF_MSD"]
     assert q.kernel == "msdstep"
     d0 = q.dist(0)
     assert (d0 != UNREACH).all()

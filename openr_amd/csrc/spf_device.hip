@@ -628,16 +628,38 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
           }
           const uint32_t du = ld_coh(dist + u);
           const uint32_t beg = a.row[u], end = a.row[u + 1];
-          for (uint32_t e = beg + lg; e < end; e += G) {
-            if constexpr (IGN) {
-              if (nign && in_sorted(ignp, nign, a.link[e])) {
-                continue;
+          // kPushUnroll edges per lane per step: their (col, metric) loads,
+          // then their distance gathers, are independent and issued together
+          constexpr uint32_t kPushUnroll = 4;
+          for (uint32_t e0 = beg + lg; e0 < end; e0 += kPushUnroll * G) {
+            uint32_t v[kPushUnroll], c[kPushUnroll], dv[kPushUnroll];
+#pragma unroll
+            for (uint32_t j = 0; j < kPushUnroll; ++j) {
+              const uint32_t e = e0 + j * G;
+              bool ok = e < end;
+              if constexpr (IGN) {
+                ok = ok && !(nign && in_sorted(ignp, nign, a.link[e]));
+              }
+              v[j] = ok ? a.col[e] : kInf32;
+              c[j] = ok ? du + a.wout[e] : kInf32;
+              if constexpr (LBK) {
+                // bucket bytes only ever run ahead of (>=) a node's true
+                // bucket, so bkt[v] < bucket(c) proves dist[v] < c: no
+                // improvement, and no HBM read of dist[v]
+                if (v[j] != kInf32 && bkt[v[j]] < min(c[j] >> shift, 254u)) {
+                  v[j] = kInf32;
+                }
               }
             }
-            const uint32_t v = a.col[e];
-            const uint32_t c = du + a.wout[e];
-            if (c < dist[v] && atomicMin(&dist[v], c) > c) {
-              atomicOr(LBK ? &act[v >> 5] : &pend[v >> 5], 1u << (v & 31));
+#pragma unroll
+            for (uint32_t j = 0; j < kPushUnroll; ++j) {
+              dv[j] = v[j] != kInf32 ? dist[v[j]] : 0u;
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < kPushUnroll; ++j) {
+              if (v[j] != kInf32 && c[j] < dv[j] && atomicMin(&dist[v[j]], c[j]) > c[j]) {
+                atomicOr(LBK ? &act[v[j] >> 5] : &pend[v[j] >> 5], 1u << (v[j] & 31));
+              }
             }
           }
         }
@@ -2504,6 +2526,9 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       uint32_t shift = 0;
       while (shift < 20 && (double)(2u << shift) <= meanw / std::max(meandeg, 1.0)) {
         ++shift;
+      }
+      if (!want_nh) {
+        ++shift; // push-only runs: fewer, wider buckets measured faster
       }
       if (const char* env = getenv("OPENR_SPF_DSTEP_SHIFT")) {
         shift = (uint32_t)std::min(24, std::max(0, atoi(env)));

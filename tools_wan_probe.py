@@ -1,6 +1,7 @@
 """Probe: device time of the weighted distance plans on the 100k WAN
 (sampled sources), one line per env configuration.
-usage: tools_wan_probe.py N_SOURCES [ENV=VAL,ENV=VAL ...]"""
+usage: tools_wan_probe.py N_SOURCES [ENV=VAL,ENV=VAL ...]   (NH=1: with
+next-hop masks)"""
 import json
 import os
 import sys
@@ -18,10 +19,11 @@ g = abi.Graph(csr)
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 for cfg in sys.argv[2:] or ["-"]:
     env = dict(kv.split("=") for kv in cfg.split(",") if "=" in kv)
+    flags = abi.SPF_F_NEXTHOPS if env.pop("NH", "0") == "1" else 0
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     srcs = np.arange(0, V, max(1, V // n), dtype=np.uint32)[:n]
-    q = g.query(srcs, 0)
+    q = g.query(srcs, flags)
     q.run()
     q.run()
     ms = q.elapsed_ms()

@@ -61,6 +61,7 @@ def parse():
     p.add_argument("--cpu-sample", type=int, default=0, help="oracle sources (0 = auto ~15 s)")
     p.add_argument("--num-sws", type=int, default=10000)
     p.add_argument("--no-wan", action="store_true", help="skip the 100k WAN all-sources pass")
+    p.add_argument("--no-whatif", action="store_true", help="skip the 8,192 what-if SPF batch")
     p.add_argument("--wan-nodes", type=int, default=100000)
     p.add_argument("--wan-links", type=int, default=1000000)
     return p.parse_args()
@@ -138,16 +139,17 @@ def cpu_baseline(topo, sample):
     }
 
 
-def _rebuild_loop(M, topo, iters, timed):
+def _rebuild_loop(M, topo, iters, timed, fwd=(0, 0)):
     """DecisionBenchmark BM_DecisionFabric loop (DecisionBenchmark.cpp:
-    600-626): toggle an RSW's overload bit, rebuild the RouteDb of "2-0-0"."""
+    600-626): toggle an RSW's overload bit, rebuild the RouteDb of "2-0-0".
+    fwd = (PrefixForwardingType, PrefixForwardingAlgorithm) of every prefix."""
     areas = M.AreaLinkStates()
     ls = areas.add("0")
     dbs = topo.adj_dbs()
     for db in dbs:
         ls.updateAdjacencyDatabase(db)
     ps = M.PrefixState()
-    for pdb in topo.prefix_dbs():
+    for pdb in topo.prefix_dbs("0", fwd[0], fwd[1]):
         ps.updatePrefixDatabase(pdb)
     solver = M.SpfSolver("2-0-0", False, False)
     timed(solver, areas, ps)  # cold build (device graph for the engine)
@@ -196,6 +198,158 @@ def route_db_rebuild_ms(topo, device, iters=5):
     out["node"] = "2-0-0"
     out["what"] = "adj-db update (RSW overload toggle) + buildRouteDb, LFA off"
     return out
+
+
+def ksp2_route_db(topo, device, iters=2):
+    """BASELINE configs[3]: every fabric prefix SR_MPLS / KSP2_ED_ECMP, the
+    RouteDb of "2-0-0" after an RSW overload toggle.  Each build traces the
+    k=1 edge-disjoint paths to every destination on the host, runs one
+    ignore-list SPF per destination (the k=2 second pass, LinkState.cpp:
+    760-789) as ONE device batch, traces k=2 and builds the label stacks
+    (Decision.cpp:909-1066)."""
+    import openr_amd._openr_spf as E
+    from openr_amd import thrift as T
+
+    E.set_spf_device(device)
+
+    def timed(solver, areas, ps):
+        nu, nm, us = solver.buildRouteDbTimed("2-0-0", areas, ps)
+        return nu + nm, us
+
+    E.reset_counters()
+    out = _rebuild_loop(E, topo, iters, timed, (T.PrefixForwardingType.SR_MPLS,
+                                                T.PrefixForwardingAlgorithm.KSP2_ED_ECMP))
+    c = E.get_counters()
+    n = max(1, c.get("decision.route_build_runs", 1))
+    out["per_build"] = {
+        "spf_runs": round(c.get("decision.spf_runs", 0) / n, 1),
+        **{k.split(".", 1)[1]: round(c.get(k, 0) / n, 1)
+           for k in ("decision.route_prefetch_us", "decision.spf_batch_us", "decision.spf_device_us")},
+    }
+    out["what"] = ("adj-db update (RSW overload toggle) + buildRouteDb of 2-0-0, all prefixes "
+                   "SR_MPLS/KSP2_ED_ECMP (k=1 + k=2 paths to every node)")
+    return out
+
+
+def ksp2_cpu_sample(topo, sample=12):
+    """Reference-style CPU cost per destination of getKthPaths(k=1) +
+    (k=2) on the fabric (oracle restatement: k=2 runs an un-memoized runSpf
+    per destination, LinkState.cpp:776-777), timed on a sample of
+    destinations and extrapolated to all of them."""
+    from oracle import build as obuild
+
+    obuild.build()
+    from oracle import _oracle_ref as O
+
+    ls = O.LinkState("0")
+    for db in topo.adj_dbs():
+        ls.updateAdjacencyDatabase(db)
+    names = sorted(n for n in topo.names if n != "2-0-0")
+    dests = names[:: max(1, len(names) // sample)][:sample]
+    ls.getSpfResult("2-0-0", True)  # k=1 reads the memoized SPF of the source
+    t0 = time.perf_counter()
+    for d in dests:
+        ls.getKthPaths("2-0-0", d, 1)
+        ls.getKthPaths("2-0-0", d, 2)
+    per = (time.perf_counter() - t0) / len(dests)
+    return {"ms_per_destination": round(per * 1e3, 2),
+            "extrapolated_build_ms": round(per * 1e3 * len(names), 1),
+            "cores": 1, "kind": "port",
+            "sample": f"{len(dests)} destinations of 2-0-0, oracle/ref_decision.cpp getKthPaths k=1,2; "
+                      f"extrapolated x{len(names)} destinations"}
+
+
+def whatif_batch(world, rank, local, dist, steps=3):
+    """BASELINE configs[4]: 8,192 single-link-failure SPFs (runSpf with
+    linksToIgnore = {link}, LinkState.cpp:806-880) from one border node in
+    two areas: area A = the 10k fabric (from "2-0-0"), area B = the 10k-node
+    / 100k-link WAN (from "n0"), 4,096 sampled links each (seed 7), with ECMP
+    next-hop masks.  The 8,192 queries are split in contiguous blocks over
+    the ranks (strong scaling, no collective)."""
+    import numpy as np
+    import torch
+
+    from openr_amd import abi
+    from openr_amd import allsources as AS
+    from openr_amd import topologies as TP
+
+    fab = TP.fabric(10000)
+    wan = TP.wan(10000, 100000)
+    areas = []
+    rng = np.random.default_rng(7)
+    for topo, me in ((fab, "2-0-0"), (wan, "n0")):
+        csr = topo.csr()
+        r, _ = topo.rank()
+        src = int(r[topo.names.index(me)])
+        links = rng.choice(csr.num_links, 4096, replace=False).astype(np.uint32)
+        areas.append((csr, src, links))
+    allq = [(a, int(l)) for a, (_, _, links) in enumerate(areas) for l in links]
+    first, count = AS.shard(len(allq), world, rank)
+    mine = allq[first:first + count]
+    streams, graphs, queries = [], [], []
+    for a, (csr, src, _) in enumerate(areas):
+        ign = [[l] for (aa, l) in mine if aa == a]
+        if not ign:
+            continue
+        g = abi.Graph(csr, device=local)
+        st = torch.cuda.Stream(device=local)
+        g.set_stream(st.cuda_stream)
+        q = g.query(np.full(len(ign), src, dtype=np.uint32), abi.SPF_F_NEXTHOPS, ignore=ign)
+        graphs.append((a, g, ign))
+        streams.append(st)
+        queries.append(q)
+    for q in queries:  # warm-up
+        q.run(sync=False)
+    torch.cuda.synchronize(local)
+    times = []
+    for _ in range(steps):
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(local)
+        t0 = time.perf_counter()
+        for q in queries:
+            q.run(sync=False)  # the two areas overlap on their own streams
+        torch.cuda.synchronize(local)
+        times.append((time.perf_counter() - t0) * 1e3)
+    ms = sorted(times)[len(times) // 2]
+    dev_ms = max((q.elapsed_ms() for q in queries), default=0.0)
+    t = torch.tensor([ms, dev_ms], dtype=torch.float64, device=f"cuda:{local}")
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms, dev_ms = float(t[0]), float(t[1])
+    # parity spot check (rank 0): 2 queries per area against the literal
+    # DijkstraQ replay with the same ignored link
+    check = None
+    if rank == 0:
+        from oracle import spf_py
+
+        bad = 0
+        for (a, g, ign), q in zip(graphs, queries):
+            csr = areas[a][0]
+            for i in (0, len(ign) - 1):
+                s = areas[a][1]
+                ref = spf_py.run_spf(csr, s, True, frozenset(ign[i]))
+                d = q.dist(i)
+                got = q.nexthop_sets(i, s)
+                for v in range(csr.num_nodes):
+                    if v in ref:
+                        bad += int(d[v]) != ref[v][0] or (v != s and got[v] != ref[v][1])
+                    else:
+                        bad += d[v] != np.uint64(abi.SPF_UNREACHABLE)
+        check = "ok" if bad == 0 else f"{bad} mismatches"
+    kernels = sorted({q.kernel for q in queries})
+    for q in queries:
+        q.close()
+    for _, g, _ in graphs:
+        g.close()
+    return {
+        "config": "BASELINE configs[4]: 8,192 single-link-failure SPFs with ECMP next hops, "
+                  "area A = fabric (9,976 nodes) from 2-0-0, area B = WAN-10k from n0, 4,096 links each",
+        "queries": len(allq), "n_gpus": world, "scaling": "strong", "kernels": kernels,
+        "ms": round(ms, 3), "device_ms": round(dev_ms, 3),
+        "value": round(len(allq) / (ms / 1e3), 1), "unit": "SPF/s",
+        "parity_check": check,
+    }
 
 
 def route_db_rebuild_cpu(topo, iters=2):
@@ -464,7 +618,16 @@ def main():
             out["wan_all_sources"] = wan_all_sources(args, world, rank, local, dist)
         except Exception as e:  # reported, never silently replaced
             out["wan_all_sources"] = {"error": repr(e)}
+    if not args.no_whatif:
+        try:
+            out["whatif_batch"] = whatif_batch(world, rank, local, dist)
+        except Exception as e:
+            out["whatif_batch"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_route_db:
+        try:
+            out["ksp2_route_db"] = ksp2_route_db(topo, local)
+        except Exception as e:
+            out["ksp2_route_db"] = {"error": repr(e)}
         try:
             out["route_db_rebuild"] = route_db_rebuild_ms(topo, local)
         except Exception as e:  # reported, never silently replaced
@@ -475,6 +638,10 @@ def main():
             out["cpu_baseline"]["route_db_rebuild"] = route_db_rebuild_cpu(topo)
         except Exception as e:
             out["cpu_baseline"]["route_db_rebuild"] = {"error": repr(e)}
+        try:
+            out["cpu_baseline"]["ksp2"] = ksp2_cpu_sample(topo)
+        except Exception as e:
+            out["cpu_baseline"]["ksp2"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -74,6 +74,7 @@ def build_host(force=False):
                 "-shared",
                 "-fPIC",
                 "-fvisibility=hidden",
+                "-pthread",
                 f"-I{INC}",
                 f"-I{pybind11.get_include()}",
                 f"-I{sysconfig.get_paths()['include']}",

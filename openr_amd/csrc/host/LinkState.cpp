@@ -13,7 +13,10 @@
 #include <chrono>
 #include <map>
 #include <mutex>
+#include <shared_mutex>
 #include <stdexcept>
+
+#include "Parallel.h"
 
 #include "openr_spf.h"
 
@@ -318,6 +321,12 @@ struct LinkState::Engine {
   std::unordered_map<uint32_t, std::unique_ptr<SpfView>> prefetched[2];
   std::map<std::pair<uint32_t, uint32_t>, std::unique_ptr<SpfView>> kthPrefetch;
   std::unordered_map<std::string, std::unique_ptr<SpfView>> isolated;
+  // spfView may be called from the RouteDb worker threads of one build:
+  // memo hits take viewMu shared, fills (and kthPrefetch) exclusive; every
+  // device call of this graph is serialised by devMu (the C ABI is
+  // single-threaded per graph)
+  std::shared_mutex viewMu;
+  std::mutex devMu;
 
   ~Engine() {
     if (graph) {
@@ -611,6 +620,7 @@ LinkState::LinkState(LinkState&& o) noexcept
       spfResultsMetric_(std::move(o.spfResultsMetric_)),
       spfResultsHops_(std::move(o.spfResultsHops_)),
       kthPathResults_(std::move(o.kthPathResults_)),
+      kthMu_(std::move(o.kthMu_)),
       engine_(std::move(o.engine_)) {}
 
 size_t LinkState::LinkPtrHash::operator()(const std::shared_ptr<Link>& l) const {
@@ -977,6 +987,22 @@ float LinkState::lastDeviceMs() const {
 const SpfView& LinkState::spfView(const std::string& node, bool useLinkMetric) const {
   auto& eng = engine();
   auto idIt = eng.ids.find(node);
+  auto& memo = eng.memo[useLinkMetric ? 1 : 0];
+  {
+    std::shared_lock<std::shared_mutex> rd(eng.viewMu);
+    if (idIt == eng.ids.end()) {
+      auto it = eng.isolated.find(node);
+      if (it != eng.isolated.end()) {
+        return *it->second;
+      }
+    } else {
+      auto it = memo.find(idIt->second);
+      if (it != memo.end()) {
+        return *it->second;
+      }
+    }
+  }
+  std::unique_lock<std::shared_mutex> wr(eng.viewMu);
   if (idIt == eng.ids.end()) {
     // unknown source: the reference result holds only the source itself
     auto& slot = eng.isolated[node];
@@ -989,7 +1015,6 @@ const SpfView& LinkState::spfView(const std::string& node, bool useLinkMetric) c
     return *slot;
   }
   const uint32_t id = idIt->second;
-  auto& memo = eng.memo[useLinkMetric ? 1 : 0];
   auto it = memo.find(id);
   if (it != memo.end()) {
     return *it->second;
@@ -1002,6 +1027,7 @@ const SpfView& LinkState::spfView(const std::string& node, bool useLinkMetric) c
     pre.erase(pit);
   } else {
     const auto t0 = std::chrono::steady_clock::now();
+    std::lock_guard<std::mutex> dev(eng.devMu);
     auto batch = runBatch(eng, {id}, useLinkMetric, true, nullptr);
     view = std::move(batch.front());
     Counters::add(
@@ -1016,6 +1042,8 @@ const SpfView& LinkState::spfView(const std::string& node, bool useLinkMetric) c
 
 void LinkState::prefetchSpf(const std::vector<std::string>& nodes, bool useLinkMetric) const {
   auto& eng = engine();
+  std::unique_lock<std::shared_mutex> wr(eng.viewMu);
+  std::lock_guard<std::mutex> dev(eng.devMu);
   auto& memo = eng.memo[useLinkMetric ? 1 : 0];
   auto& pre = eng.prefetched[useLinkMetric ? 1 : 0];
   std::vector<uint32_t> todo;
@@ -1125,9 +1153,12 @@ std::vector<LinkState::Path> const& LinkState::getKthPaths(
     throw std::invalid_argument("getKthPaths: k must be >= 1");
   }
   KthKey key{src, dest, k};
-  auto found = kthPathResults_.find(key);
-  if (found != kthPathResults_.end()) {
-    return found->second;
+  {
+    std::shared_lock<std::shared_mutex> rd(*kthMu_);
+    auto found = kthPathResults_.find(key);
+    if (found != kthPathResults_.end()) {
+      return found->second;
+    }
   }
   LinkSet linksToIgnore;
   for (size_t i = 1; i < k; ++i) {
@@ -1147,9 +1178,6 @@ std::vector<LinkState::Path> const& LinkState::getKthPaths(
     auto sid = eng.ids.find(src);
     if (sid != eng.ids.end()) {
       auto did = eng.ids.find(dest);
-      auto pit = did == eng.ids.end()
-          ? eng.kthPrefetch.end()
-          : eng.kthPrefetch.find({sid->second, did->second});
       std::vector<uint32_t> ign;
       for (const auto& link : linksToIgnore) {
         auto li = eng.linkIndex.find(link.get());
@@ -1158,11 +1186,17 @@ std::vector<LinkState::Path> const& LinkState::getKthPaths(
         }
       }
       std::sort(ign.begin(), ign.end());
-      if (pit != eng.kthPrefetch.end() && pit->second->ignored == ign) {
-        second = std::move(pit->second);
-        eng.kthPrefetch.erase(pit);
-      } else {
+      if (did != eng.ids.end()) {
+        std::unique_lock<std::shared_mutex> wr(eng.viewMu);
+        auto pit = eng.kthPrefetch.find({sid->second, did->second});
+        if (pit != eng.kthPrefetch.end() && pit->second->ignored == ign) {
+          second = std::move(pit->second);
+          eng.kthPrefetch.erase(pit);
+        }
+      }
+      if (!second) {
         std::vector<std::vector<uint32_t>> lists{ign};
+        std::lock_guard<std::mutex> dev(eng.devMu);
         second = std::move(runBatch(eng, {sid->second}, true, false, &lists).front());
       }
       res = second.get();
@@ -1180,6 +1214,7 @@ std::vector<LinkState::Path> const& LinkState::getKthPaths(
       }
     }
   }
+  std::unique_lock<std::shared_mutex> wr(*kthMu_);
   return kthPathResults_.emplace(std::move(key), std::move(paths)).first->second;
 }
 
@@ -1190,21 +1225,34 @@ void LinkState::prefetchKthPaths(
   if (sid == eng.ids.end()) {
     return;
   }
-  std::vector<uint32_t> sources;
-  std::vector<uint32_t> dstIds;
-  std::vector<std::vector<uint32_t>> lists;
-  std::unordered_set<uint32_t> seen;
-  for (const auto& d : dests) {
-    auto did = eng.ids.find(d);
-    if (did == eng.ids.end() || !seen.insert(did->second).second) {
-      continue;
+  // destinations whose second pass is still to run
+  std::vector<std::pair<const std::string*, uint32_t>> todo;
+  {
+    std::shared_lock<std::shared_mutex> rk(*kthMu_);
+    std::shared_lock<std::shared_mutex> rv(eng.viewMu);
+    std::unordered_set<uint32_t> seen;
+    for (const auto& d : dests) {
+      auto did = eng.ids.find(d);
+      if (did == eng.ids.end() || !seen.insert(did->second).second) {
+        continue;
+      }
+      if (kthPathResults_.count(KthKey{src, d, 2}) ||
+          eng.kthPrefetch.count({sid->second, did->second})) {
+        continue;
+      }
+      todo.emplace_back(&d, did->second);
     }
-    if (kthPathResults_.count(KthKey{src, d, 2}) ||
-        eng.kthPrefetch.count({sid->second, did->second})) {
-      continue;
-    }
-    std::vector<uint32_t> ign;
-    for (const auto& path : getKthPaths(src, d, 1)) {
+  }
+  if (todo.empty()) {
+    return;
+  }
+  spfView(src, true); // every k = 1 trace reads the source's own SPF
+  // k = 1 paths of every destination (independent traces over the same
+  // row: host worker pool), then their links as the ignore lists
+  std::vector<std::vector<uint32_t>> ignAll(todo.size());
+  parallelFor(todo.size(), hostThreads(todo.size(), 32), [&](size_t i, unsigned) {
+    auto& ign = ignAll[i];
+    for (const auto& path : getKthPaths(src, *todo[i].first, 1)) {
       for (const auto& link : path) {
         auto li = eng.linkIndex.find(link.get());
         if (li != eng.linkIndex.end()) {
@@ -1212,19 +1260,29 @@ void LinkState::prefetchKthPaths(
         }
       }
     }
-    if (ign.empty()) {
-      continue;
-    }
     std::sort(ign.begin(), ign.end());
     ign.erase(std::unique(ign.begin(), ign.end()), ign.end());
+  });
+  std::vector<uint32_t> sources;
+  std::vector<uint32_t> dstIds;
+  std::vector<std::vector<uint32_t>> lists;
+  for (size_t i = 0; i < todo.size(); ++i) {
+    if (ignAll[i].empty()) {
+      continue;
+    }
     sources.push_back(sid->second);
-    dstIds.push_back(did->second);
-    lists.push_back(std::move(ign));
+    dstIds.push_back(todo[i].second);
+    lists.push_back(std::move(ignAll[i]));
   }
   if (sources.empty()) {
     return;
   }
-  auto views = runBatch(eng, sources, true, false, &lists);
+  std::vector<std::unique_ptr<SpfView>> views;
+  {
+    std::lock_guard<std::mutex> dev(eng.devMu);
+    views = runBatch(eng, sources, true, false, &lists);
+  }
+  std::unique_lock<std::shared_mutex> wr(eng.viewMu);
   for (size_t i = 0; i < views.size(); ++i) {
     eng.kthPrefetch[{sid->second, dstIds[i]}] = std::move(views[i]);
   }

@@ -23,6 +23,7 @@
 #include <limits>
 #include <memory>
 #include <optional>
+#include <shared_mutex>
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
@@ -326,6 +327,9 @@ class LinkState {
     size_t operator()(const KthKey& key) const;
   };
   mutable std::unordered_map<KthKey, std::vector<Path>, KthKeyHash> kthPathResults_;
+  // getKthPaths / spfView may be called from the worker threads of one
+  // RouteDb build (Parallel.h): memo hits share the lock, fills take it
+  mutable std::unique_ptr<std::shared_mutex> kthMu_ = std::make_unique<std::shared_mutex>();
   mutable std::unique_ptr<Engine> engine_;
 };
 

@@ -1,0 +1,76 @@
+// Parallel.h — the host worker pool of one RouteDb build.
+//
+// The reference builds a RouteDb on the Decision thread, one prefix at a
+// time (openr/decision/Decision.cpp:313-534).  Once the SPF rows a build
+// reads are resident (one device batch per area, SpfSolverImpl::prefetch),
+// the per-prefix / per-label / per-destination work only reads them, so it
+// is spread over host threads here.  Results are merged by the caller in a
+// fixed order; nothing observable depends on which thread ran which item.
+#pragma once
+
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
+#include <exception>
+#include <thread>
+#include <vector>
+
+namespace openr {
+
+// Worker threads for `n` independent items: OPENR_SPF_HOST_THREADS, else
+// min(hardware threads, 16); 1 (run inline) for small batches.
+inline unsigned hostThreads(size_t n, size_t minPerThread = 64) {
+  unsigned t = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (const char* env = std::getenv("OPENR_SPF_HOST_THREADS")) {
+    t = (unsigned)std::max(1, std::atoi(env));
+  }
+  const size_t cap = std::max<size_t>(1, n / std::max<size_t>(1, minPerThread));
+  return (unsigned)std::min<size_t>(t, cap);
+}
+
+// fn(item, worker) for item in [0, n), chunks handed out dynamically.  The
+// first exception (by worker index) is rethrown after every worker joined.
+template <class Fn>
+void parallelFor(size_t n, unsigned threads, Fn&& fn, size_t chunk = 16) {
+  if (threads <= 1 || n <= chunk) {
+    for (size_t i = 0; i < n; ++i) {
+      fn(i, 0u);
+    }
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::exception_ptr> errors(threads);
+  auto body = [&](unsigned w) {
+    try {
+      for (;;) {
+        const size_t b = next.fetch_add(chunk);
+        if (b >= n) {
+          break;
+        }
+        const size_t e = std::min(n, b + chunk);
+        for (size_t i = b; i < e; ++i) {
+          fn(i, w);
+        }
+      }
+    } catch (...) {
+      errors[w] = std::current_exception();
+      next.store(n); // stop handing out work
+    }
+  };
+  std::vector<std::thread> pool;
+  pool.reserve(threads - 1);
+  for (unsigned w = 1; w < threads; ++w) {
+    pool.emplace_back(body, w);
+  }
+  body(0);
+  for (auto& t : pool) {
+    t.join();
+  }
+  for (auto& e : errors) {
+    if (e) {
+      std::rethrow_exception(e);
+    }
+  }
+}
+
+} // namespace openr

@@ -16,6 +16,7 @@
 #include <string_view>
 #include <list>
 
+#include "Parallel.h"
 #include "Util.h"
 
 namespace openr {
@@ -390,6 +391,15 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
   DecisionRouteDb routeDb;
 
   // unicast routes: IP and IP->MPLS
+  struct PrefixWork {
+    const thrift::IpPrefix* prefix;
+    const thrift::PrefixEntries* entries;
+    bool srMpls;
+    bool hasBGP;
+    bool isV4;
+    thrift::PrefixForwardingAlgorithm algo;
+  };
+  std::vector<PrefixWork> work;
   for (const auto& [prefix, prefixEntries] : prefixState.prefixes()) {
     bool hasBGP = false, hasNonBGP = false, missingMv = false;
     for (const auto& [node, byArea] : prefixEntries) {
@@ -415,31 +425,90 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
     const auto algo = getPrefixForwardingAlgorithm(prefixEntries);
     const auto type = getPrefixForwardingType(prefixEntries);
     if (type == thrift::PrefixForwardingType::SR_MPLS) {
-      const auto nodes = getBestAnnouncingNodes(
-          myNodeName, prefix, prefixEntries, hasBGP, true, areaLinkStates);
-      if (!nodes.success || nodes.nodes.empty()) {
-        continue;
-      }
-      selectKsp2(
-          routeDb.unicastEntries, prefix, myNodeName, nodes, prefixEntries, hasBGP,
-          areaLinkStates, prefixState, algo);
+      work.push_back({&prefix, &prefixEntries, true, hasBGP, isV4Prefix, algo});
     } else if (algo == thrift::PrefixForwardingAlgorithm::SP_ECMP) {
       if (hasBGP) {
         selectEcmpBgp(
             routeDb.unicastEntries, myNodeName, prefix, prefixEntries, isV4Prefix,
             areaLinkStates, prefixState);
       } else {
-        selectEcmpOpenr(
-            routeDb.unicastEntries, myNodeName, prefix, prefixEntries, isV4Prefix,
-            areaLinkStates);
+        work.push_back({&prefix, &prefixEntries, false, hasBGP, isV4Prefix, algo});
       }
     } else {
       // KSP2 is not supported for plain IP routing
       Counters::add("decision.incompatible_forwarding_type", 1);
     }
   }
+  // Open/R ECMP and SR-MPLS KSP2 prefixes only read the prefetched SPF rows
+  // and the (thread-safe) path memo: one worker pool, per-worker route maps
+  // merged afterwards (prefixes are distinct keys)
+  const unsigned threads = hostThreads(work.size());
+  for (const auto& [area, ls] : areaLinkStates) {
+    myLinks(myNodeName, area, ls); // fill the per-build cache before the workers read it
+  }
+  std::vector<std::unordered_map<thrift::IpPrefix, RibUnicastEntry>> parts(threads);
+  parallelFor(work.size(), threads, [&](size_t i, unsigned w) {
+    const PrefixWork& x = work[i];
+    if (x.srMpls) {
+      const auto nodes = getBestAnnouncingNodes(
+          myNodeName, *x.prefix, *x.entries, x.hasBGP, true, areaLinkStates);
+      if (!nodes.success || nodes.nodes.empty()) {
+        return;
+      }
+      selectKsp2(
+          parts[w], *x.prefix, myNodeName, nodes, *x.entries, x.hasBGP, areaLinkStates,
+          prefixState, x.algo);
+    } else {
+      selectEcmpOpenr(parts[w], myNodeName, *x.prefix, *x.entries, x.isV4, areaLinkStates);
+    }
+  });
+  for (auto& part : parts) {
+    for (auto& kv : part) {
+      routeDb.unicastEntries.emplace(kv.first, std::move(kv.second));
+    }
+  }
 
-  // node-label MPLS routes: on a label collision the smaller node name wins
+  // node-label MPLS routes: on a label collision the smaller node name wins.
+  // Labels held by a single (other) node are expanded on the worker pool
+  // first; the sequential pass below applies the collision rule and uses
+  // those results, computing colliding labels in place as the reference does.
+  std::unordered_map<int32_t, uint32_t> labelUse;
+  for (const auto& [area, ls] : areaLinkStates) {
+    for (const auto& [_, adjDb] : ls.getAdjacencyDatabases()) {
+      if (adjDb.nodeLabel != 0 && isMplsLabelValid(adjDb.nodeLabel)) {
+        ++labelUse[adjDb.nodeLabel];
+      }
+    }
+  }
+  struct LabelJob {
+    const std::string* area;
+    const thrift::AdjacencyDatabase* db;
+  };
+  std::vector<LabelJob> labelJobs;
+  std::unordered_map<const thrift::AdjacencyDatabase*, size_t> labelJobOf;
+  for (const auto& [area, ls] : areaLinkStates) {
+    for (const auto& [_, adjDb] : ls.getAdjacencyDatabases()) {
+      if (adjDb.nodeLabel != 0 && isMplsLabelValid(adjDb.nodeLabel) &&
+          labelUse[adjDb.nodeLabel] == 1 && adjDb.thisNodeName != myNodeName) {
+        labelJobOf.emplace(&adjDb, labelJobs.size());
+        labelJobs.push_back({&area, &adjDb});
+      }
+    }
+  }
+  std::vector<std::optional<RibMplsEntry>> labelDone(labelJobs.size());
+  parallelFor(labelJobs.size(), hostThreads(labelJobs.size()), [&](size_t i, unsigned) {
+    const auto& db = *labelJobs[i].db;
+    const auto metricNhs =
+        getNextHopsWithMetric(myNodeName, {db.thisNodeName}, false, areaLinkStates);
+    if (metricNhs.second.empty()) {
+      return; // counted as no_route_to_label by the sequential pass
+    }
+    labelDone[i].emplace(
+        db.nodeLabel,
+        getNextHopsThrift(
+            myNodeName, {db.thisNodeName}, false, false, metricNhs.first, metricNhs.second,
+            db.nodeLabel, areaLinkStates, {*labelJobs[i].area}));
+  });
   std::unordered_map<int32_t, std::pair<std::string, RibMplsEntry>> labelToNode;
   for (const auto& [area, ls] : areaLinkStates) {
     for (const auto& [_, adjDb] : ls.getAdjacencyDatabases()) {
@@ -466,6 +535,18 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
         labelToNode.erase(topLabel);
         labelToNode.emplace(
             topLabel, std::make_pair(adjDb.thisNodeName, RibMplsEntry(topLabel, {nh})));
+        continue;
+      }
+      auto job = labelJobOf.find(&adjDb);
+      if (job != labelJobOf.end()) {
+        auto& done = labelDone[job->second];
+        if (!done) {
+          Counters::add("decision.no_route_to_label", 1);
+          continue;
+        }
+        labelToNode.erase(topLabel);
+        labelToNode.emplace(
+            topLabel, std::make_pair(adjDb.thisNodeName, std::move(*done)));
         continue;
       }
       const auto metricNhs =

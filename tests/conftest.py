@@ -16,6 +16,13 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def gpu_ready():
+    # PyTorch ships its own libamdhip64 (same SONAME as /opt/rocm's, which
+    # the engine links): initialise torch's HIP runtime first so the engine
+    # binds to the already-loaded one, as bench.py does.  Loaded the other
+    # way round, torch later reports "No HIP GPUs are available".
+    import torch
+
+    torch.cuda.init()
     from openr_amd import abi
 
     n = abi.device_count()

@@ -154,7 +154,7 @@ def _rebuild_loop(M, topo, iters, timed, fwd=(0, 0)):
     solver = M.SpfSolver("2-0-0", False, False)
     timed(solver, areas, ps)  # cold build (device graph for the engine)
     rsw = [i for i, n in enumerate(topo.names) if n.startswith("3-")]
-    tot, upd, bld = [], [], []
+    tot, upd, bld, rel = [], [], [], []
     routes = 0
     for it in range(iters):
         db = dbs[rsw[(it * 7919) % len(rsw)]]
@@ -163,14 +163,20 @@ def _rebuild_loop(M, topo, iters, timed, fwd=(0, 0)):
             t0 = time.perf_counter()
             ls.updateAdjacencyDatabase(db)
             t1 = time.perf_counter()
-            routes, us = timed(solver, areas, ps)
+            r = timed(solver, areas, ps)
+            routes, us = r[0], r[1]
             t2 = time.perf_counter()
             tot.append((t2 - t0) * 1e3)
             upd.append((t1 - t0) * 1e3)
             bld.append(us / 1e3)
+            if len(r) > 2:
+                rel.append(r[2] / 1e3)
     med = lambda x: round(sorted(x)[len(x) // 2], 3)  # noqa: E731
-    return {"ms_median": med(tot), "update_ms_median": med(upd),
-            "build_ms_median": med(bld), "routes": routes, "samples": len(tot)}
+    out = {"ms_median": med(tot), "update_ms_median": med(upd),
+           "build_ms_median": med(bld), "routes": routes, "samples": len(tot)}
+    if rel:
+        out["release_ms_median"] = med(rel)  # freeing the RouteDb (in ms_median)
+    return out
 
 
 def route_db_rebuild_ms(topo, device, iters=5):
@@ -182,8 +188,8 @@ def route_db_rebuild_ms(topo, device, iters=5):
     E.set_spf_device(device)
 
     def timed(solver, areas, ps):
-        nu, nm, us = solver.buildRouteDbTimed("2-0-0", areas, ps)
-        return nu + nm, us
+        nu, nm, us, free_us = solver.buildRouteDbTimed("2-0-0", areas, ps)
+        return nu + nm, us, free_us
 
     E.reset_counters()
     out = _rebuild_loop(E, topo, iters, timed)
@@ -213,8 +219,8 @@ def ksp2_route_db(topo, device, iters=2):
     E.set_spf_device(device)
 
     def timed(solver, areas, ps):
-        nu, nm, us = solver.buildRouteDbTimed("2-0-0", areas, ps)
-        return nu + nm, us
+        nu, nm, us, free_us = solver.buildRouteDbTimed("2-0-0", areas, ps)
+        return nu + nm, us, free_us
 
     E.reset_counters()
     out = _rebuild_loop(E, topo, iters, timed, (T.PrefixForwardingType.SR_MPLS,
@@ -360,7 +366,7 @@ def route_db_rebuild_cpu(topo, iters=2):
     from oracle import _oracle_ref as O
 
     def timed(solver, areas, ps):
-        nu, nm, us = solver.buildRouteDbTimed("2-0-0", areas, ps)
+        nu, nm, us = solver.buildRouteDbTimed("2-0-0", areas, ps)[:3]
         return nu + nm, us
 
     out = _rebuild_loop(O, topo, iters, timed)

@@ -164,6 +164,12 @@ int spf_query_fetch_rows(
     int dst_on_device);
 /* Elements between consecutive distance rows (>= V). */
 uint32_t spf_query_row_stride(const spf_query* q);
+/* Copy the next-hop masks of queries [first, first+count) to host memory in
+ * one transfer, back to back: query i occupies V * nh_words(i) words.  The
+ * bulk counterpart of spf_query_nexthops for batches whose every row the
+ * caller materialises (NodeSpfResult::nextHops, LinkState.h:203-257). */
+int spf_query_fetch_nexthops(
+    spf_query* q, uint32_t first, uint32_t count, uint64_t* dst);
 
 #ifdef __cplusplus
 }

@@ -52,6 +52,7 @@ EXPORTED_SYMBOLS = (
     "spf_query_device_rows",
     "spf_query_row_stride",
     "spf_query_fetch_rows",
+    "spf_query_fetch_nexthops",
 )
 
 
@@ -135,6 +136,7 @@ def load():
         "spf_query_order": (C.c_int, [vp, u32, pu32]),
         "spf_query_row_stride": (u32, [vp]),
         "spf_query_fetch_rows": (C.c_int, [vp, u32, u32, vp, C.c_size_t, C.c_int]),
+        "spf_query_fetch_nexthops": (C.c_int, [vp, u32, u32, pu64]),
         "spf_query_device_rows": (
             C.c_int,
             [vp, C.POINTER(vp), pu32, C.POINTER(vp), pu64],
@@ -397,6 +399,15 @@ class Query:
             load().spf_query_fetch_rows(self.h, first, count, dst_ptr, pitch, 1 if on_device else 0),
             "fetch_rows",
         )
+
+    def fetch_nexthops(self, first: int, count: int) -> np.ndarray:
+        """Masks of queries [first, first+count), back to back (V*W_i words
+        each), in one device-to-host transfer."""
+        n = sum(self.graph.V * self.nh_words(i) for i in range(first, first + count))
+        out = np.zeros(max(n, 1), dtype=np.uint64)
+        _check(load().spf_query_fetch_nexthops(self.h, first, count, _p(out, C.c_uint64)),
+               "fetch_nexthops")
+        return out[:n]
 
     def device_rows(self):
         dp = C.c_void_p()

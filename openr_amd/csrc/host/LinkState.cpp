@@ -502,21 +502,51 @@ std::vector<std::unique_ptr<SpfView>> runBatch(
   spf_query_elapsed_ms(q, &eng.lastMs);
   Counters::add("decision.spf_device_us", (int64_t)(eng.lastMs * 1000.0f));
   const uint32_t V = (uint32_t)eng.names.size();
-  out.reserve(sources.size());
-  for (uint32_t i = 0; i < sources.size(); ++i) {
+  const uint32_t nq = (uint32_t)sources.size();
+  out.resize(nq);
+  // 32-bit rows (every fast plan) and next-hop masks come back in one
+  // transfer each; the per-view expansion runs on the host worker pool
+  std::shared_ptr<std::vector<uint32_t>> rows32;
+  std::vector<uint64_t> masks;
+  std::vector<uint64_t> maskOff(nq + 1, 0);
+  std::vector<uint32_t> words(nq, 1);
+  if (!exact && nq > 1) {
+    rows32 = std::make_shared<std::vector<uint32_t>>((size_t)nq * V);
+    if ((s = spf_query_fetch_rows(q, 0, nq, rows32->data(), (size_t)V * 4, 0)) != SPF_OK) {
+      engineFailure("spf_query_fetch_rows", s);
+    }
+  }
+  if (wantNextHops) {
+    for (uint32_t i = 0; i < nq; ++i) {
+      words[i] = (uint32_t)spf_query_nh_words(q, i);
+      maskOff[i + 1] = maskOff[i] + (uint64_t)V * words[i];
+    }
+    if (nq > 1) {
+      masks.resize(maskOff[nq]);
+      if ((s = spf_query_fetch_nexthops(q, 0, nq, masks.data())) != SPF_OK) {
+        engineFailure("spf_query_fetch_nexthops", s);
+      }
+    }
+  }
+  auto fill = [&](size_t i, unsigned) {
     auto view = std::make_unique<SpfView>();
     view->src = sources[i];
     view->useLinkMetric = useLinkMetric;
     view->exact = exact;
-    view->dist.resize(V);
-    if ((s = spf_query_dist(q, i, view->dist.data())) != SPF_OK) {
-      engineFailure("spf_query_dist", s);
+    if (rows32) {
+      view->dist.share32(rows32, i * V, V);
+    } else if (int st = spf_query_dist(q, (uint32_t)i, view->dist.resize64(V)); st != SPF_OK) {
+      engineFailure("spf_query_dist", st);
     }
     if (wantNextHops) {
-      view->words = (uint32_t)spf_query_nh_words(q, i);
-      view->nh.resize((size_t)V * view->words);
-      if ((s = spf_query_nexthops(q, i, view->nh.data())) != SPF_OK) {
-        engineFailure("spf_query_nexthops", s);
+      view->words = words[i];
+      if (!masks.empty()) {
+        view->nh.assign(masks.begin() + maskOff[i], masks.begin() + maskOff[i + 1]);
+      } else {
+        view->nh.resize((size_t)V * view->words);
+        if (int st = spf_query_nexthops(q, (uint32_t)i, view->nh.data()); st != SPF_OK) {
+          engineFailure("spf_query_nexthops", st);
+        }
       }
       const int nn = spf_graph_num_nbrs(eng.graph, sources[i]);
       view->nbrs.resize(std::max(nn, 0));
@@ -526,15 +556,17 @@ std::vector<std::unique_ptr<SpfView>> runBatch(
     }
     if (exact) {
       view->order.resize(V);
-      if ((s = spf_query_order(q, i, view->order.data())) != SPF_OK) {
-        engineFailure("spf_query_order", s);
+      if (int st = spf_query_order(q, (uint32_t)i, view->order.data()); st != SPF_OK) {
+        engineFailure("spf_query_order", st);
       }
     }
     if (ignore) {
       view->ignored = (*ignore)[i];
     }
-    out.push_back(std::move(view));
-  }
+    out[i] = std::move(view);
+  };
+  // the single-row reads of the exact plan go through the ABI (one thread)
+  parallelFor(nq, exact ? 1u : hostThreads(nq, 32), fill, 8);
   return out;
 }
 
@@ -1119,7 +1151,8 @@ std::optional<LinkStateMetric> LinkState::getMetricFromAToB(
 LinkStateMetric LinkState::getMaxHopsToNode(const std::string& nodeName) const {
   const SpfView& view = spfView(nodeName, false);
   LinkStateMetric best = 0;
-  for (uint64_t d : view.dist) {
+  for (size_t v = 0; v < view.dist.size(); ++v) {
+    const uint64_t d = view.dist[v];
     if (d != SpfView::kUnreachable) {
       best = std::max(best, d);
     }

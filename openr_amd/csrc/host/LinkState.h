@@ -125,11 +125,46 @@ class Link {
 };
 
 // Flat single-source SPF result as produced by the device (one batch row).
+// Distances of one SPF row, by node id: either an owned uint64 row (exact
+// plan) or a window into a uint32 block shared by every row of one device
+// batch (fast plans: one transfer, no per-row copy; 0xFFFFFFFF = not reached).
+class DistRow {
+ public:
+  static constexpr uint64_t kUnreachable = ~0ull;
+  uint64_t operator[](size_t v) const {
+    if (d32_) {
+      const uint32_t x = d32_[v];
+      return x == 0xFFFFFFFFu ? kUnreachable : (uint64_t)x;
+    }
+    return d64_[v];
+  }
+  size_t size() const { return n_; }
+  uint64_t* resize64(size_t n) {
+    d64_.assign(n, kUnreachable);
+    block_.reset();
+    d32_ = nullptr;
+    n_ = n;
+    return d64_.data();
+  }
+  void share32(std::shared_ptr<const std::vector<uint32_t>> block, size_t offset, size_t n) {
+    d64_.clear();
+    d32_ = block->data() + offset;
+    block_ = std::move(block);
+    n_ = n;
+  }
+
+ private:
+  std::vector<uint64_t> d64_;
+  std::shared_ptr<const std::vector<uint32_t>> block_;
+  const uint32_t* d32_{nullptr};
+  size_t n_{0};
+};
+
 struct SpfView {
   uint32_t src{0};            // node id (name rank) of the source
   bool useLinkMetric{true};
   bool exact{false};          // settle order came from the exact kernel
-  std::vector<uint64_t> dist; // per node id; kUnreachable = not reached
+  DistRow dist;               // per node id; kUnreachable = not reached
   uint32_t words{1};          // words per next-hop mask
   std::vector<uint64_t> nh;   // [V * words]
   std::vector<uint32_t> nbrs; // mask bit -> node id

@@ -245,16 +245,23 @@ PYBIND11_MODULE(_openr_spf, m) {
       .def("buildRouteDbTimed",
            [](SpfSolver& s, const std::string& node, const AreaMapHolder& areas,
               const PrefixState& ps) {
-             // RouteDb build timed in C++ (no Python conversion of the routes)
+             // RouteDb build timed in C++ (no Python conversion of the
+             // routes); the release of the RouteDb (Decision drops the old
+             // one on every rebuild) is timed separately
              const auto t0 = std::chrono::steady_clock::now();
              auto db = s.buildRouteDb(node, areas.map, ps);
-             const double us = std::chrono::duration<double, std::micro>(
-                                   std::chrono::steady_clock::now() - t0)
-                                   .count();
-             if (!db) {
-               return py::make_tuple((long)-1, (long)-1, us);
+             const auto t1 = std::chrono::steady_clock::now();
+             const double us = std::chrono::duration<double, std::micro>(t1 - t0).count();
+             long nu = -1, nm = -1;
+             if (db) {
+               nu = (long)db->unicastEntries.size();
+               nm = (long)db->mplsEntries.size();
              }
-             return py::make_tuple((long)db->unicastEntries.size(), (long)db->mplsEntries.size(), us);
+             db.reset();
+             const double freeUs = std::chrono::duration<double, std::micro>(
+                                       std::chrono::steady_clock::now() - t1)
+                                       .count();
+             return py::make_tuple(nu, nm, us, freeUs);
            })
       .def("staticRoutesUpdated", &SpfSolver::staticRoutesUpdated)
       .def("pushRoutesDeltaUpdates",

@@ -3277,6 +3277,36 @@ int spf_query_fetch_rows(
   return SPF_OK;
 }
 
+int spf_query_fetch_nexthops(
+    spf_query* q, uint32_t first, uint32_t count, uint64_t* dst) {
+  if (!q || (count && !dst)) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  if (!(q->flags & SPF_F_NEXTHOPS) || !q->ran) {
+    return fail(SPF_E_INVALID, "no next hops for this query");
+  }
+  if ((uint64_t)first + count > q->nq) {
+    return fail(SPF_E_INVALID, "row range out of bounds");
+  }
+  if (count == 0 || q->g->V == 0) {
+    return SPF_OK;
+  }
+  const size_t V = q->g->V;
+  const uint64_t lo = q->nh_off[first];
+  const uint64_t hi = first + count < q->nq ? q->nh_off[first + count] : q->nh_total;
+  std::vector<uint64_t> tmp(hi - lo);
+  HIP_TRY(hipSetDevice(q->g->device));
+  HIP_TRY(hipStreamSynchronize(q->g->stream));
+  HIP_TRY(hipMemcpy(tmp.data(), q->d_nh + lo, (hi - lo) * 8, hipMemcpyDeviceToHost));
+  uint64_t out = 0;
+  for (uint32_t i = first; i < first + count; ++i) {
+    const size_t n = V * q->nh_w[i];
+    std::memcpy(dst + out, tmp.data() + (q->nh_off[i] - lo), n * 8);
+    out += n;
+  }
+  return SPF_OK;
+}
+
 uint32_t spf_query_row_stride(const spf_query* q) {
   if (!q) {
     return 0;

@@ -394,3 +394,25 @@ def test_gmem_bfs_plan_large(gpu_ready):
     q = g.query([0, 4321, 69999], abi.SPF_F_UNIT_METRIC).run()
     assert q.kernel == "bfs-gmem"
     check_query(csr, q, [0, 4321, 69999], False)
+
+
+def test_bulk_fetch_matches_row_reads(gpu_ready):
+    """spf_query_fetch_rows (host) / spf_query_fetch_nexthops return exactly
+    the per-row spf_query_dist / spf_query_nexthops contents, in order."""
+    rng = random.Random(12)
+    V = 300
+    csr = abi.Csr.from_links(V, random_links(rng, V, 900, parallel=0.05))
+    srcs = rng.sample(range(V), 40)
+    q = g_query = abi.Graph(csr).query(srcs, abi.SPF_F_NEXTHOPS).run()
+    rows = np.zeros((len(srcs), V), dtype=np.uint32)
+    q.fetch_rows(0, len(srcs), rows.ctypes.data, V * 4, on_device=False)
+    flat = q.fetch_nexthops(0, len(srcs))
+    off = 0
+    for i in range(len(srcs)):
+        d = q.dist(i)
+        assert (np.where(d == UNREACH, np.uint64(0xFFFFFFFF), d) == rows[i]).all()
+        m = q.nexthops(i).ravel()
+        assert (flat[off : off + m.size] == m).all()
+        off += m.size
+    assert off == flat.size
+    del g_query

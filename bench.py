@@ -107,6 +107,21 @@ def pmc_traffic(kernel_name):
     return None, None
 
 
+def pmc_traffic_largest(kernel_name):
+    """HBM bytes of the largest dispatch of `kernel_name` in the committed
+    PMC passes (the measured launch, not a warm-up batch)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        k = d.get("kernels", {}).get(kernel_name)
+        if k and "hbm_bytes_largest_launch" in k:
+            return int(k["hbm_bytes_largest_launch"]), os.path.relpath(f, ROOT)
+    return None, None
+
+
 def cpu_baseline(topo, sample):
     """The oracle's reference-style runSpf (DijkstraQ, string maps, reMake),
     single thread, on a bounded sample of the same all-sources workload."""
@@ -444,6 +459,7 @@ def wan_all_sources(args, world, rank, local, dist):
     per_sssp = 8 * E + 4 * (V + 1) + 4 * V
     kernel_s = spf_ms / 1e3
     achieved = sas.count * per_sssp / kernel_s / 1e9 if kernel_s else None
+    traffic, traffic_src = pmc_traffic_largest("spf_dstep_kernel")
     out = {
         "config": "BASELINE configs[2]: 100k-node / 1M-link WAN (SURVEY §8(d) row 3), all sources, "
                   "contiguous source blocks per GPU, RCCL all-gather of uint32 rows",
@@ -459,7 +475,12 @@ def wan_all_sources(args, world, rank, local, dist):
         "roofline": {"bound": "hbm", "kernel": "spf_dstep_kernel (push-only, LDS buckets)",
                      "algorithmic_bytes_per_sssp": per_sssp,
                      "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None},
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                     # PMC bytes of the one-GPU 100k-source launch, per SSSP (2*FETCH_SIZE +
+                     # WRITE_SIZE; the x2 is calibrated for streaming reads only — these are
+                     # 4-byte gathers and memory-side atomics)
+                     "traffic_per_sssp": (traffic // 100000) if traffic else None,
+                     "traffic_source": traffic_src},
         "parity_check": check,
         "generate_s": round(gen_s, 1),
     }

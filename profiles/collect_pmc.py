@@ -39,7 +39,8 @@ def _short(name):
     return n.split("<")[0].split("::")[-1]
 
 
-def per_kernel(d, counter):
+def per_dispatch(d, counter):
+    """{kernel: [value per dispatch, in dispatch order]} (kB)."""
     acc = defaultdict(lambda: defaultdict(float))
     for r in _rows(d):
         if r.get("Counter_Name") != counter:
@@ -47,19 +48,26 @@ def per_kernel(d, counter):
         k = _short(r.get("Kernel_Name", ""))
         disp = r.get("Dispatch_Id") or r.get("Correlation_Id") or str(len(acc[k]))
         acc[k][disp] += float(r.get("Counter_Value", 0) or 0)
-    return {k: sum(v.values()) / len(v) for k, v in acc.items() if v}
+    return {k: [v[x] for x in sorted(v, key=lambda x: int(x) if str(x).isdigit() else 0)]
+            for k, v in acc.items() if v}
 
 
 def main(fetch_dir, write_dir, out):
-    fetch = per_kernel(fetch_dir, "FETCH_SIZE")
-    write = per_kernel(write_dir, "WRITE_SIZE")
+    fetch = per_dispatch(fetch_dir, "FETCH_SIZE")
+    write = per_dispatch(write_dir, "WRITE_SIZE")
     kernels = {}
     for k in sorted(set(fetch) | set(write)):
-        f_kb = fetch.get(k)
-        w_kb = write.get(k)
+        f = fetch.get(k)
+        w = write.get(k)
+        f_kb = sum(f) / len(f) if f else None
+        w_kb = sum(w) / len(w) if w else None
         ent = {"FETCH_SIZE_kB": f_kb, "WRITE_SIZE_kB": w_kb}
         if f_kb is not None and w_kb is not None:
             ent["hbm_bytes_per_launch"] = int(round((2.0 * f_kb + w_kb) * 1024.0))
+            # the largest dispatch (kernels launched at several sizes, e.g.
+            # a warm-up batch before the measured one)
+            ent["hbm_bytes_largest_launch"] = int(round((2.0 * max(f) + max(w)) * 1024.0))
+            ent["dispatches"] = len(f)
         kernels[k] = ent
     json.dump(
         {

@@ -1,6 +1,8 @@
 #!/bin/bash
 # Round profile recipe (runs on the GPU box from the repo root):
-#   kernel trace + stats of the bench, then one PMC pass per counter group.
+#   kernel trace + stats of the bench (fabric all-sources step + the WAN
+#   all-sources pass), then one PMC pass per counter group (the MI355X guide:
+#   FETCH_SIZE and WRITE_SIZE cannot share a pass).
 # Usage: bash profiles/run_profiles.sh <round-tag>
 set -e
 R=$(pwd)
@@ -8,12 +10,13 @@ TAG=${1:-r01}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT/final
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $OUT/trace -o run --output-format csv -- \
-  python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-route-db > $OUT/trace_bench.json
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -T -d $OUT/pmc_fetch -o run --output-format csv -- \
-  python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-route-db > $OUT/pmc_fetch.json
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/pmc_write -o run --output-format csv -- \
-  python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-route-db > $OUT/pmc_write.json
+B="$R/bench.py --no-cpu-baseline --no-route-db --no-whatif"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -T -d $OUT/trace -o run --output-format csv -- \
+  python3 $B --steps 10 --warmup 3 > $OUT/trace_bench.json
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -T -d $OUT/pmc_fetch -o run --output-format csv -- \
+  python3 $B --steps 3 --warmup 1 > $OUT/pmc_fetch.json
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/pmc_write -o run --output-format csv -- \
+  python3 $B --steps 3 --warmup 1 > $OUT/pmc_write.json
 cd $R
 python3 profiles/collect_pmc.py $OUT/pmc_fetch $OUT/pmc_write $OUT/final/pmc_traffic.json
 cp $(find $OUT/trace -name "*kernel_stats.csv" | head -1) $OUT/final/kernel_stats.csv

@@ -1643,17 +1643,112 @@ __device__ __forceinline__ void nl_body(
   }
 }
 
+// One block sweeps chunks [c0, c1) of one source: the source's neighbour
+// list is staged once per mask word and reused by every chunk, so the
+// dependent staging loads (nbrs -> row_of / transit) are paid once per
+// block instead of once per 1024-node chunk, and a block keeps up to
+// kNlUnroll independent row loads in flight per thread per chunk.
+template <bool WIDE>
+__device__ __forceinline__ void nl_body_multi(
+    const NhLevelsArgs& a, uint32_t q, uint32_t s, uint32_t c0, uint32_t c1,
+    uint32_t* st_row, uint32_t* st_node) {
+  const uint32_t Wm = a.nh_w[q];
+  uint64_t* nhrow = a.nh_out + a.nh_off[q];
+  const uint32_t none = WIDE ? kInf32 : 255u;
+  const uint64_t step = WIDE ? (uint64_t)a.scale : 1ull;
+  const uint32_t beg = a.nbr_off[s], n = a.nbr_off[s + 1] - beg;
+  for (uint32_t w = 0; w < Wm; ++w) {
+    const uint32_t jlo = w * 64, cnt = min(64u, n - min(n, jlo)); // <= kNlStage
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < cnt; t += kNlThreads) {
+      const uint32_t f = a.nbrs[beg + jlo + t];
+      const uint32_t tf = (a.trbits[f >> 5] >> (f & 31)) & 1u;
+      st_row[t] = (uint32_t)a.row_of[f];
+      st_node[t] = f | (tf << 31);
+    }
+    __syncthreads();
+    for (uint32_t c = c0; c < c1; ++c) {
+      const uint32_t v0 = c * kNlChunk + threadIdx.x * kNlPer;
+      if (v0 >= a.V) {
+        break;
+      }
+      uint32_t ls[4];
+      nl_load<WIDE>(a, q, v0, ls);
+      bool live[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        live[i] = ls[i] != none && ls[i] != 0;
+      }
+      uint64_t acc[4] = {0, 0, 0, 0};
+      uint32_t t = 0;
+      for (; t + kNlUnroll <= cnt; t += kNlUnroll) {
+        uint32_t lf[kNlUnroll][4];
+#pragma unroll
+        for (uint32_t u = 0; u < kNlUnroll; ++u) {
+          nl_load<WIDE>(a, st_row[t + u], v0, lf[u]);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kNlUnroll; ++u) {
+          const uint32_t nd = st_node[t + u];
+          const uint32_t f = nd & 0x7FFFFFFFu;
+          const bool tf = nd >> 31;
+          const uint64_t bit = 1ull << (t + u);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (live[i] && lf[u][i] != none && (uint64_t)lf[u][i] + step == (uint64_t)ls[i] &&
+                (tf || v0 + i == f)) {
+              acc[i] |= bit;
+            }
+          }
+        }
+      }
+      for (; t < cnt; ++t) {
+        uint32_t lf[4];
+        nl_load<WIDE>(a, st_row[t], v0, lf);
+        const uint32_t nd = st_node[t];
+        const uint32_t f = nd & 0x7FFFFFFFu;
+        const bool tf = nd >> 31;
+        const uint64_t bit = 1ull << t;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (live[i] && lf[i] != none && (uint64_t)lf[i] + step == (uint64_t)ls[i] &&
+              (tf || v0 + i == f)) {
+            acc[i] |= bit;
+          }
+        }
+      }
+      if (Wm == 1 && v0 + 4 <= a.V) {
+        ulonglong2* o = reinterpret_cast<ulonglong2*>(nhrow + v0);
+        o[0] = make_ulonglong2(acc[0], acc[1]);
+        o[1] = make_ulonglong2(acc[2], acc[3]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (v0 + i < a.V) {
+            nhrow[(size_t)(v0 + i) * Wm + w] = acc[i];
+          }
+        }
+      }
+    }
+  }
+}
+
+// chunks of 1024 nodes swept by one block (all of them up to 16k nodes)
+constexpr uint32_t kNlChunksPerBlock = 16;
+
 __global__ __launch_bounds__(kNlThreads) void spf_nh_levels_kernel(NhLevelsArgs a) {
   __shared__ uint32_t st_row[kNlStage];
   __shared__ uint32_t st_node[kNlStage];
-  const uint32_t chunk = blockIdx.x / a.nq;
-  const uint32_t q = blockIdx.x - chunk * a.nq;
+  const uint32_t nchunks = (a.V + kNlChunk - 1) / kNlChunk;
+  const uint32_t cb = blockIdx.x / a.nq;
+  const uint32_t q = blockIdx.x - cb * a.nq;
   const uint32_t s = a.src[q];
-  const uint32_t v0 = chunk * kNlChunk + threadIdx.x * kNlPer;
+  const uint32_t c0 = cb * kNlChunksPerBlock;
+  const uint32_t c1 = min(nchunks, c0 + kNlChunksPerBlock);
   if (a.flags[0] != 0) {
-    nl_body<true>(a, q, s, v0, st_row, st_node);
+    nl_body_multi<true>(a, q, s, c0, c1, st_row, st_node);
   } else {
-    nl_body<false>(a, q, s, v0, st_row, st_node);
+    nl_body_multi<false>(a, q, s, c0, c1, st_row, st_node);
   }
 }
 
@@ -2941,7 +3036,9 @@ int launch_nh_levels(spf_query* q, bool unit) {
   a.Vp8 = q->Vp8;
   a.nq = q->nq;
   a.scale = unit ? 1u : g->uniform;
-  const uint64_t blocks = (uint64_t)((g->V + kNlChunk - 1) / kNlChunk) * q->nq;
+  const uint32_t nchunks = (g->V + kNlChunk - 1) / kNlChunk;
+  const uint64_t blocks =
+      (uint64_t)((nchunks + kNlChunksPerBlock - 1) / kNlChunksPerBlock) * q->nq;
   if (blocks > 0x7FFFFFFFull) {
     return fail(SPF_E_UNSUPPORTED, "batch too large for the next-hop pass");
   }

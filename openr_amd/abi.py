@@ -15,7 +15,8 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libopenr_spf.so")
+# OPENR_SPF_LIB: load another build of the engine (kernel tuning sweeps)
+LIB_PATH = os.environ.get("OPENR_SPF_LIB") or os.path.join(_HERE, "libopenr_spf.so")
 
 SPF_OK = 0
 SPF_UNREACHABLE = (1 << 64) - 1

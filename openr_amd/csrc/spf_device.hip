@@ -1531,7 +1531,10 @@ constexpr uint32_t kNlChunk = kNlThreads * kNlPer;
 // and the neighbour rows are loaded kNlUnroll at a time, so a block keeps
 // several independent row loads in flight instead of one dependent chain
 // (nbrs -> row_of -> trbits -> row) per neighbour.
-constexpr uint32_t kNlUnroll = 8;
+#ifndef OPENR_NL_UNROLL
+#define OPENR_NL_UNROLL 8
+#endif
+constexpr uint32_t kNlUnroll = OPENR_NL_UNROLL;
 constexpr uint32_t kNlStage = 1024; // neighbours staged per pass
 
 template <bool WIDE>
@@ -1733,8 +1736,12 @@ __device__ __forceinline__ void nl_body_multi(
   }
 }
 
-// chunks of 1024 nodes swept by one block (all of them up to 16k nodes)
-constexpr uint32_t kNlChunksPerBlock = 16;
+// chunks of 1024 nodes swept by one block (measured on the fabric: 2 ->
+// 0.676 ms, 4 -> 0.682, 16 = whole rows -> 0.710; kNlUnroll 4 / 16 slower)
+#ifndef OPENR_NL_CPB
+#define OPENR_NL_CPB 2
+#endif
+constexpr uint32_t kNlChunksPerBlock = OPENR_NL_CPB;
 
 __global__ __launch_bounds__(kNlThreads) void spf_nh_levels_kernel(NhLevelsArgs a) {
   __shared__ uint32_t st_row[kNlStage];

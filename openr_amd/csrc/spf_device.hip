@@ -41,6 +41,7 @@
 #include <functional>
 #include <queue>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "openr_spf.h"
@@ -197,6 +198,9 @@ struct SsspArgs {
   uint32_t nq;
   uint32_t G;       // lanes per node (power of two, <= 64)
   uint32_t ign_cap; // LDS words reserved for the ignore list
+  // what-if screen: queries whose rows were copied from the baseline run
+  // (skip[q] != 0) are not recomputed; nullptr = none
+  const uint32_t* skip;
 };
 
 // WMAX: max next-hop words (0 = distances only).  UNIT: every hop costs 1.
@@ -233,6 +237,9 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
   }
 
   for (uint32_t q = blockIdx.x; q < a.nq; q += gridDim.x) {
+    if (a.skip && a.skip[q]) {
+      continue; // uniform per block
+    }
     const uint32_t src = a.src[q];
     if constexpr (GMEM) {
       dist = a.dist_out + (size_t)q * a.Vp;
@@ -548,6 +555,9 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
   }
 
   for (uint32_t q = blockIdx.x; q < a.nq; q += gridDim.x) {
+    if (a.skip && a.skip[q]) {
+      continue; // uniform per block
+    }
     const uint32_t src = a.src[q];
     uint32_t* dist = a.dist_out + (size_t)q * a.Vp;
     uint32_t nign = 0;
@@ -1909,6 +1919,81 @@ __global__ __launch_bounds__(64) void spf_exact_kernel(ExactArgs a) {
   }
 }
 
+// ------------------------------------------------ what-if screen (config 5)
+//
+// Removing a link changes an SPF only if one of its half-edges u->v is a
+// USABLE TIGHT edge of the baseline run from the same source: u the source
+// or transit, d[u] + w(u->v) == d[v].  Distances and next-hop sets are
+// defined by those edges alone, so a query none of whose
+// ignored links is tight has exactly the baseline rows.  One block per
+// query checks its list against the baseline row and, if nothing is tight,
+// copies the baseline distance / next-hop rows and flags the query so the
+// SSSP kernel skips it.  Single-link failures off the source's shortest-path
+// DAG (most of them) then cost a row copy instead of an SSSP.
+struct WhatifArgs {
+  const uint32_t* col;
+  const uint32_t* rev;
+  const uint32_t* wout;
+  const uint32_t* trbits;
+  const uint32_t* link_half; // [2 * L] half-edges of each link (~0u = none)
+  const uint32_t* src;
+  const uint32_t* ign_off;
+  const uint32_t* ign;
+  const uint32_t* base_of;   // query -> baseline row
+  const uint32_t* base_dist; // [nb][Vp]
+  const uint64_t* base_nh;
+  const uint64_t* base_nh_off;
+  uint32_t* dist_out;
+  uint64_t* nh_out;
+  const uint64_t* nh_off;
+  const uint32_t* nh_w;
+  uint32_t* skip;
+  uint32_t V;
+  uint32_t Vp;
+  uint32_t L; // link ids >= L match no edge (ignored)
+  uint32_t want_nh;
+};
+
+__global__ __launch_bounds__(256) void spf_whatif_screen_kernel(WhatifArgs a) {
+  const uint32_t q = blockIdx.x;
+  const uint32_t s = a.src[q], b = a.base_of[q];
+  const uint32_t* bd = a.base_dist + (size_t)b * a.Vp;
+  const uint32_t lo = a.ign_off[q], n = a.ign_off[q + 1] - lo;
+  int tight = 0;
+  for (uint32_t i = threadIdx.x; i < 2 * n; i += blockDim.x) {
+    const uint32_t l = a.ign[lo + (i >> 1)];
+    const uint32_t e = l < a.L ? a.link_half[2 * (size_t)l + (i & 1)] : kInf32;
+    if (e == kInf32) {
+      continue;
+    }
+    const uint32_t u = a.col[a.rev[e]], v = a.col[e];
+    const uint32_t du = bd[u];
+    if (du == kInf32 || (u != s && !((a.trbits[u >> 5] >> (u & 31)) & 1u))) {
+      continue;
+    }
+    tight |= du + a.wout[e] == bd[v];
+  }
+  tight = __syncthreads_or(tight);
+  if (threadIdx.x == 0) {
+    a.skip[q] = tight ? 0u : 1u;
+  }
+  if (tight) {
+    return;
+  }
+  uint32_t* dst = a.dist_out + (size_t)q * a.Vp;
+  for (uint32_t v = threadIdx.x; v < a.V; v += blockDim.x) {
+    dst[v] = bd[v];
+  }
+  if (a.want_nh) {
+    const size_t n64 = (size_t)a.V * a.nh_w[q];
+    const uint64_t* from = a.base_nh + a.base_nh_off[b];
+    uint64_t* to = a.nh_out + a.nh_off[q];
+    for (size_t i = threadIdx.x; i < n64; i += blockDim.x) {
+      to[i] = from[i];
+    }
+  }
+}
+
 __global__ void fill_u32_kernel(uint32_t* p, size_t n, uint32_t v) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -1939,6 +2024,7 @@ struct spf_graph {
            *d_slot = nullptr, *d_tr = nullptr, *d_nbr_off = nullptr,
            *d_nbrs = nullptr, *d_nbr_w = nullptr;
   uint64_t* d_w64 = nullptr;
+  uint32_t* d_link_half = nullptr; // [2L] half-edges of each link (what-if screen)
 };
 
 // How a batch is computed.
@@ -1970,6 +2056,9 @@ struct spf_query {
   // per-workgroup pend / candidate / claimed / mask arrays
   uint32_t msd_nbatch = 0;
   uint32_t *d_perm = nullptr, *d_slab = nullptr, *d_msd = nullptr;
+  // what-if screen: baseline runs (one per distinct source, no ignore list)
+  spf_query* base = nullptr;
+  uint32_t *d_base_of = nullptr, *d_skip = nullptr;
   uint64_t* d_nh_off = nullptr;
   void* d_dist = nullptr;
   uint64_t* d_nh = nullptr;
@@ -2007,7 +2096,7 @@ void free_graph(spf_graph* g) {
        {(void*)g->d_row, (void*)g->d_col, (void*)g->d_wout, (void*)g->d_win,
         (void*)g->d_link, (void*)g->d_rev, (void*)g->d_slot, (void*)g->d_tr,
         (void*)g->d_w64, (void*)g->d_nbr_off, (void*)g->d_nbrs,
-        (void*)g->d_nbr_w}) {
+        (void*)g->d_nbr_w, (void*)g->d_link_half}) {
     if (p) {
       (void)hipFree(p);
     }
@@ -2028,10 +2117,14 @@ void free_query(spf_query* q) {
         (void*)q->d_nh_w, (void*)q->d_order, (void*)q->d_scratch,
         (void*)q->d_nh_off, q->d_dist, (void*)q->d_nh, (void*)q->d_row_of,
         (void*)q->d_lvl, (void*)q->d_flags, (void*)q->d_perm,
-        (void*)q->d_slab, (void*)q->d_msd}) {
+        (void*)q->d_slab, (void*)q->d_msd, (void*)q->d_base_of,
+        (void*)q->d_skip}) {
     if (p) {
       (void)hipFree(p);
     }
+  }
+  if (q->base) {
+    free_query(q->base);
   }
   if (q->ev0) {
     (void)hipEventDestroy(q->ev0);
@@ -2397,6 +2490,15 @@ int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
       (s = upload_weights(g))) {
     return bail(s);
   }
+  {
+    std::vector<uint32_t> half(2 * (size_t)g->L, kInf32);
+    for (uint32_t e = 0; e < E; ++e) {
+      half[2 * (size_t)g->link[e] + (e < g->rev[e] ? 0 : 1)] = e;
+    }
+    if ((s = dev_upload(&g->d_link_half, half.data(), half.size()))) {
+      return bail(s);
+    }
+  }
   *out = g;
   return SPF_OK;
 }
@@ -2745,6 +2847,37 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       return bail(fail(SPF_E_NOMEM, "exact-kernel scratch"));
     }
   }
+  // what-if screen (OPENR_SPF_WHATIF_SCREEN=0 disables): batches with
+  // ignore lists on the fast plans run one baseline SPF per distinct source
+  // first; queries whose ignored links are all off the baseline's shortest
+  // path DAG copy its rows instead of running
+  const char* scr = getenv("OPENR_SPF_WHATIF_SCREEN");
+  if (has_ign && !(scr && atoi(scr) == 0) &&
+      (q->dist == DistPlan::SsspLds || q->dist == DistPlan::SsspGmem ||
+       q->dist == DistPlan::Dstep)) {
+    std::vector<uint32_t> base_srcs, base_of(nq);
+    std::unordered_map<uint32_t, uint32_t> idx;
+    for (uint32_t i = 0; i < nq; ++i) {
+      auto it = idx.emplace(desc->sources[i], (uint32_t)base_srcs.size()).first;
+      if (it->second == base_srcs.size()) {
+        base_srcs.push_back(desc->sources[i]);
+      }
+      base_of[i] = it->second;
+    }
+    if (base_srcs.size() < nq) { // screening pays only if sources repeat
+      spf_query_desc bd{};
+      bd.num_queries = (uint32_t)base_srcs.size();
+      bd.sources = base_srcs.data();
+      bd.flags = desc->flags;
+      if ((s = spf_query_create(g, &bd, &q->base)) ||
+          (s = dev_upload(&q->d_base_of, base_of.data(), nq))) {
+        return bail(s);
+      }
+      if (hipMalloc((void**)&q->d_skip, (size_t)nq * 4) != hipSuccess) {
+        return bail(fail(SPF_E_NOMEM, "what-if screen flags"));
+      }
+    }
+  }
   if (hipEventCreate(&q->ev0) != hipSuccess ||
       hipEventCreate(&q->ev1) != hipSuccess ||
       hipEventCreate(&q->evm) != hipSuccess) {
@@ -2789,6 +2922,7 @@ int launch_sssp(spf_query* q) {
   a.nq = q->nq;
   a.G = g->G;
   a.ign_cap = q->ign_cap;
+  a.skip = q->d_skip;
   auto kern = spf_sssp_kernel<WMAX, UNIT, IGN, GMEM>;
   HIP_TRY(hipFuncSetAttribute(
       (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2844,6 +2978,7 @@ int launch_dstep_t(spf_query* q) {
   a.nq = q->nq;
   a.G = g->G;
   a.ign_cap = q->ign_cap;
+  a.skip = q->d_skip;
   // lanes per node: fewer than the median degree, so more nodes (and more
   // independent HBM gathers) are in flight per CU (4 with the PULL pass of
   // next-hop runs, 8 for the push-only distance runs: measured on the 100k
@@ -3097,8 +3232,53 @@ int mark_stage(spf_query* q) {
   return SPF_OK;
 }
 
+int run_plan(spf_query* q);
+
+int run_screen(spf_query* q) {
+  spf_query* b = q->base;
+  spf_graph* g = q->g;
+  int s = run_plan(b);
+  if (s != SPF_OK) {
+    return s;
+  }
+  WhatifArgs a;
+  a.col = g->d_col;
+  a.rev = g->d_rev;
+  a.wout = g->d_wout;
+  a.trbits = g->d_tr;
+  a.link_half = g->d_link_half;
+  a.src = q->d_src;
+  a.ign_off = q->d_ign_off;
+  a.ign = q->d_ign;
+  a.base_of = q->d_base_of;
+  a.base_dist = (const uint32_t*)b->d_dist;
+  a.base_nh = b->d_nh;
+  a.base_nh_off = b->d_nh_off;
+  a.dist_out = (uint32_t*)q->d_dist;
+  a.nh_out = q->d_nh;
+  a.nh_off = q->d_nh_off;
+  a.nh_w = q->d_nh_w;
+  a.skip = q->d_skip;
+  a.V = g->V;
+  a.Vp = q->Vp;
+  a.L = g->L;
+  a.want_nh = (q->flags & SPF_F_NEXTHOPS) ? 1u : 0u;
+  if (b->Vp != q->Vp) {
+    return fail(SPF_E_INVALID, "baseline row stride differs");
+  }
+  hipLaunchKernelGGL(spf_whatif_screen_kernel, dim3(q->nq), dim3(256), 0, g->stream, a);
+  HIP_TRY(hipGetLastError());
+  return SPF_OK;
+}
+
 int run_plan(spf_query* q) {
   const bool unit = q->flags & SPF_F_UNIT_METRIC;
+  if (q->base) {
+    const int s = run_screen(q);
+    if (s != SPF_OK) {
+      return s;
+    }
+  }
   switch (q->dist) {
   case DistPlan::Exact:
     return launch_exact(q);

@@ -416,3 +416,30 @@ def test_bulk_fetch_matches_row_reads(gpu_ready):
         off += m.size
     assert off == flat.size
     del g_query
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+def test_whatif_screen_matches_full_runs(gpu_ready, weighted, monkeypatch):
+    """Single-link-failure batches from repeated sources: queries whose
+    failed link is off the baseline shortest-path DAG copy the baseline rows
+    (the screen); the result must equal running every query in full, and the
+    replay on sampled queries, including drained nodes, parallel links and
+    link ids beyond the graph (they match nothing)."""
+    rng = random.Random(91 + weighted)
+    V = 2000
+    links = random_links(rng, V, 6000, wmin=1, wmax=30 if weighted else 1, parallel=0.03)
+    ov = np.zeros(V, dtype=np.uint8)
+    ov[rng.sample(range(V), 40)] = 1
+    csr = abi.Csr.from_links(V, links, overloaded=ov)
+    g = abi.Graph(csr)
+    srcs = [0] * 300 + [int(np.flatnonzero(ov)[0])] * 100 + [7] * 100
+    ign = [[rng.randrange(len(links))] for _ in srcs]
+    ign[5] = [len(links) + 3]  # no such link
+    ign[6] = []
+    q = g.query(srcs, abi.SPF_F_NEXTHOPS, ignore=ign).run()
+    monkeypatch.setenv("OPENR_SPF_WHATIF_SCREEN", "0")
+    r = g.query(srcs, abi.SPF_F_NEXTHOPS, ignore=ign).run()
+    for i in range(len(srcs)):
+        assert (q.dist(i) == r.dist(i)).all(), i
+        assert (q.nexthops(i) == r.nexthops(i)).all(), i
+    check_query(csr, q, srcs, True, ignore=ign, rows={0, 5, 6, 310, 499})

@@ -373,6 +373,48 @@ def whatif_batch(world, rank, local, dist, steps=3):
     }
 
 
+def grid_route_db(device, iters=20):
+    """BASELINE configs[0]: DecisionBenchmark's 10x10 grid (DecisionBenchmark.
+    cpp:360-431), buildRouteDb("1") with LFA on (the benchmark's Decision,
+    :75-83) after an overload toggle of a random node, engine and oracle
+    (reference data structures, 1 thread) side by side."""
+    import openr_amd._openr_spf as E
+    from oracle import build as obuild
+    from openr_amd import topologies as TP
+
+    obuild.build()
+    from oracle import _oracle_ref as O
+
+    E.set_spf_device(device)
+    topo = TP.grid(10)
+    out = {"config": "BASELINE configs[0]: 10x10 grid, buildRouteDb(\"1\"), SP_ECMP, LFA on"}
+    for tag, M in (("engine", E), ("cpu_oracle", O)):
+        areas = M.AreaLinkStates()
+        ls = areas.add("0")
+        dbs = topo.adj_dbs()
+        for db in dbs:
+            ls.updateAdjacencyDatabase(db)
+        ps = M.PrefixState()
+        for pdb in topo.prefix_dbs():
+            ps.updatePrefixDatabase(pdb)
+        solver = M.SpfSolver("1", False, True)
+        solver.buildRouteDbTimed("1", areas, ps)
+        times = []
+        routes = 0
+        for it in range(iters):
+            db = dbs[(it * 37 + 11) % len(dbs)]
+            for ov in (True, False):
+                db.isOverloaded = ov
+                t0 = time.perf_counter()
+                ls.updateAdjacencyDatabase(db)
+                r = solver.buildRouteDbTimed("1", areas, ps)
+                times.append((time.perf_counter() - t0) * 1e3)
+                routes = r[0] + r[1]
+        out[tag] = {"ms_median": round(sorted(times)[len(times) // 2], 3), "routes": routes,
+                    "samples": len(times)}
+    return out
+
+
 def route_db_rebuild_cpu(topo, iters=2):
     """The same loop on the oracle (reference data structures), 1 thread."""
     from oracle import build as obuild
@@ -651,6 +693,10 @@ def main():
         except Exception as e:
             out["whatif_batch"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_route_db:
+        try:
+            out["grid_route_db"] = grid_route_db(local)
+        except Exception as e:
+            out["grid_route_db"] = {"error": repr(e)}
         try:
             out["ksp2_route_db"] = ksp2_route_db(topo, local)
         except Exception as e:

@@ -1369,6 +1369,9 @@ __global__ __launch_bounds__(kNhThreads) void spf_nh_rows_kernel(NhRowsArgs a) {
 // as 32-bit rows plus an 8-bit level row that the next-hop pass streams
 // instead of the 32-bit distances.
 
+#ifndef OPENR_MS_UNROLL8
+#define OPENR_MS_UNROLL8 1
+#endif
 constexpr uint32_t kMsThreads = 1024;
 constexpr uint32_t kMsMaxK = 16; // nodes per thread -> V <= 16384
 
@@ -1463,6 +1466,14 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
           const uint32_t beg = a.row[v], end = a.row[v + 1];
           MT acc = 0;
           uint32_t e = beg;
+#if OPENR_MS_UNROLL8
+          for (; e + 8 <= end; e += 8) {
+            const uint4 c0 = {a.col[e], a.col[e + 1], a.col[e + 2], a.col[e + 3]};
+            const uint4 c1 = {a.col[e + 4], a.col[e + 5], a.col[e + 6], a.col[e + 7]};
+            acc |= cur[c0.x] | cur[c0.y] | cur[c0.z] | cur[c0.w] | cur[c1.x] | cur[c1.y] |
+                   cur[c1.z] | cur[c1.w];
+          }
+#endif
           for (; e + 4 <= end; e += 4) {
             const uint32_t u0 = a.col[e], u1 = a.col[e + 1], u2 = a.col[e + 2],
                            u3 = a.col[e + 3];

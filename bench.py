@@ -62,6 +62,7 @@ def parse():
     p.add_argument("--num-sws", type=int, default=10000)
     p.add_argument("--no-wan", action="store_true", help="skip the 100k WAN all-sources pass")
     p.add_argument("--no-whatif", action="store_true", help="skip the 8,192 what-if SPF batch")
+    p.add_argument("--no-repair", action="store_true", help="skip the WAN table-repair events")
     p.add_argument("--wan-nodes", type=int, default=100000)
     p.add_argument("--wan-links", type=int, default=1000000)
     return p.parse_args()
@@ -492,6 +493,7 @@ def wan_all_sources(args, world, rank, local, dist):
                "sample": f"{S} sources, scipy.sparse.csgraph.dijkstra (C binary-heap Dijkstra over the "
                          "same CSR), single thread; the reference's own runSpf needs ~587 s/SPF here "
                          "(SURVEY §6, reMake per strict improvement)"}
+    repair = None if args.no_repair else wan_table_repair(topo, csr, sas, world, rank, local, dist)
     sas.close()
     table_bytes = n * V * 4
     # algorithmic bytes per SSSP of the push-only delta-stepping plan: the
@@ -528,7 +530,101 @@ def wan_all_sources(args, world, rank, local, dist):
     }
     if cpu:
         out["cpu_baseline"] = cpu
+    if repair:
+        out["table_repair"] = repair
     return out
+
+
+def wan_table_repair(topo, csr, sas, world, rank, local, dist):
+    """SURVEY §8(f) row 2 on the WAN all-sources table: single churn events
+    (link down / up, metric up / down, node drain / undrain) applied with
+    ShardedAllSources.update() — edge diff, screen kernel, recompute of the
+    affected sources only, row scatter + exchange — instead of the
+    reference's drop-everything memo (LinkState.cpp:712-715) and a full
+    100k-source recompute.  Parity: the repaired table equals fresh engine
+    rows for sampled sources and scipy for one, on the final graph."""
+    import random
+
+    import numpy as np
+    import torch
+
+    from openr_amd import abi
+    from openr_amd import topologies as TP
+
+    rng = random.Random(2024)
+    links = list(topo.links)
+    ids, _ = topo.rank()
+    V = csr.num_nodes
+    ov = np.zeros(V, dtype=np.uint8)
+    events = []
+    gone = None
+    cur = csr
+    plan = ["link_down", "link_up", "metric_up", "metric_down", "drain", "undrain"]
+    drained = None
+    for kind in plan:
+        if kind == "link_down":
+            i = rng.randrange(len(links))
+            gone = (i, links.pop(i))
+        elif kind == "link_up":
+            links.insert(*gone)
+        elif kind in ("metric_up", "metric_down"):
+            i = rng.randrange(len(links))
+            a, b, wab, wba = links[i]
+            w = wab * 3 if kind == "metric_up" else max(1, wab // 3)
+            links[i] = (a, b, w, w)
+        elif kind == "drain":
+            drained = int(ids[rng.randrange(V)])
+            ov[drained] = 1
+        elif kind == "undrain":
+            ov[drained] = 0
+        if kind in ("link_down", "link_up"):
+            nxt = TP.Topology(topo.names, links, None).csr()
+            nxt.overloaded = ov.copy()
+        else:
+            nxt = abi.Csr(cur.num_nodes, cur.row_ptr, cur.col, cur.metric.copy(), cur.link_id,
+                          cur.rev, ov.copy(), cur.num_links)
+            if kind.startswith("metric"):
+                a, b, w, _ = links[i]
+                ra, rb = int(ids[a]), int(ids[b])
+                for (u, v) in ((ra, rb), (rb, ra)):
+                    lo, hi = int(cur.row_ptr[u]), int(cur.row_ptr[u + 1])
+                    e = lo + int(np.nonzero(cur.col[lo:hi] == v)[0][0])
+                    nxt.metric[e] = w
+        rep = sas.update(nxt)
+        t = torch.tensor([rep.wall_ms, rep.spf_ms, rep.screen_ms, rep.graph_ms, rep.exchange_ms],
+                         dtype=torch.float64, device=f"cuda:{local}")
+        if dist:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        events.append({"event": kind, "deltas": rep.deltas, "affected_sources": rep.affected_total,
+                       "ms": round(float(t[0]), 2), "spf_ms": round(float(t[1]), 2),
+                       "screen_ms": round(float(t[2]), 2), "graph_ms": round(float(t[3]), 2),
+                       "exchange_ms": round(float(t[4]), 2), "diff_ms": round(rep.diff_ms, 2),
+                       "graph_patched_in_place": rep.graph_patched})
+        cur = nxt
+    check = None
+    if rank == 0 and sas.gather or world == 1:
+        import scipy.sparse as sp
+        import scipy.sparse.csgraph as cg
+
+        probe = [0, V // 3, V - 1]
+        g = abi.Graph(cur, device=local)
+        q = g.query(np.asarray(probe, dtype=np.uint32), 0).run()
+        bad = 0
+        for k, i in enumerate(probe):
+            ref = q.dist(k)
+            ref = np.where(ref == np.uint64(abi.SPF_UNREACHABLE), np.uint64(0xFFFFFFFF), ref)
+            bad += int((sas.row(i).astype(np.uint64) != ref).sum())
+        q.close()
+        g.close()
+        A = sp.csr_matrix((cur.metric.astype(np.float64), cur.col, cur.row_ptr), shape=(V, V))
+        D = cg.dijkstra(A, indices=[probe[1]])[0]
+        ref = np.where(np.isfinite(D), D, 0xFFFFFFFF).astype(np.int64)
+        bad += int((sas.row(probe[1]).astype(np.int64) != ref).sum())
+        check = "ok" if bad == 0 else f"{bad} mismatches"
+    return {"what": "WAN all-sources uint32 table kept current under single churn events by "
+                    "ShardedAllSources.update (diff -> spf_table_screen_kernel -> SSSP of the affected "
+                    "sources -> spf_scatter_rows_kernel -> row exchange); compare the full pass 'ms'",
+            "events": events, "parity_check": check}
 
 
 def main():

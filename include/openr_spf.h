@@ -171,6 +171,56 @@ uint32_t spf_query_row_stride(const spf_query* q);
 int spf_query_fetch_nexthops(
     spf_query* q, uint32_t first, uint32_t count, uint64_t* dst);
 
+/* ---- incremental all-sources tables ----
+ * The reference drops every memoized SpfResult on any topology change
+ * (LinkState.cpp:510-511, 712-715, 728-729, driven by the LinkStateChange
+ * of updateAdjacencyDatabase :564-717) and recomputes each source on
+ * demand.  Here a resident table of distance rows is repaired instead: the
+ * change between two graphs over the same node ids is listed as directed
+ * edge deltas, a screen kernel finds the sources whose shortest-path DAG a
+ * delta can touch, and only those are recomputed and scattered back. */
+
+#define SPF_DELTA_REMOVED 1u /* usable before the change, not after */
+#define SPF_DELTA_ADDED 2u   /* usable after the change, not before */
+#define SPF_SCOPE_ALL 0u       /* the tail relaxes it for every source */
+#define SPF_SCOPE_TAIL_ONLY 1u /* only for source == tail (tail overloaded) */
+#define SPF_SCOPE_NOT_TAIL 2u  /* every source but the tail (transit flip) */
+
+typedef struct spf_edge_delta {
+  uint32_t tail, head; /* node ids shared by both graphs */
+  uint64_t metric;     /* metric in the graph where the edge is usable */
+  uint32_t kind;       /* SPF_DELTA_* */
+  uint32_t scope;      /* SPF_SCOPE_* */
+} spf_edge_delta;
+
+/* Host-only (no device): the directed edge deltas turning `before` into
+ * `after`, which must have the same num_nodes (ids = name ranks).  Per tail
+ * node: half-edges (head, metric) only in `before` are REMOVED, only in
+ * `after` ADDED (multiset difference, so parallel links count), and when the
+ * tail's overload bit flipped its unchanged half-edges are REMOVED / ADDED
+ * with SPF_SCOPE_NOT_TAIL (an overloaded node still expands as the source,
+ * LinkState.cpp:829-836).  Writes min(n, cap) deltas, *n_out = n. */
+int spf_graph_diff(
+    const spf_graph_desc* before, const spf_graph_desc* after,
+    spf_edge_delta* out, uint32_t cap, uint32_t* n_out);
+/* Screen the uint32 distance rows of `num_rows` sources against the deltas
+ * (kernel spf_table_screen_kernel on the graph stream): row i is affected
+ * iff some delta (u, v, w) in scope of sources[i] with d[u] reached has
+ * d[u] + w == d[v] (REMOVED: a tight edge of the DAG disappears) or
+ * d[u] + w <= d[v] (ADDED: a new tight or shorter edge).  Unaffected rows
+ * keep their distances and next-hop sets exactly (both are defined by the
+ * tight usable edges alone).  `rows` is device memory, `pitch` elements
+ * apart; `sources` and `affected` (one byte per row) are host memory. */
+int spf_table_screen(
+    spf_graph* g, const uint32_t* rows, size_t pitch, uint32_t num_rows,
+    const uint32_t* sources, const spf_edge_delta* deltas, uint32_t n_deltas,
+    uint8_t* affected);
+/* Copy distance row i of the query (uint32, as spf_query_fetch_rows) to
+ * row dst_rows[i] of the device table `table` (pitch bytes apart), for every
+ * query, in one kernel on the graph stream (asynchronous). */
+int spf_query_scatter_rows(
+    spf_query* q, const uint32_t* dst_rows, void* table, size_t pitch);
+
 #ifdef __cplusplus
 }
 #endif

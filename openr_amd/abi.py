@@ -54,6 +54,21 @@ EXPORTED_SYMBOLS = (
     "spf_query_row_stride",
     "spf_query_fetch_rows",
     "spf_query_fetch_nexthops",
+    "spf_graph_diff",
+    "spf_table_screen",
+    "spf_query_scatter_rows",
+)
+
+SPF_DELTA_REMOVED = 1
+SPF_DELTA_ADDED = 2
+SPF_SCOPE_ALL = 0
+SPF_SCOPE_TAIL_ONLY = 1
+SPF_SCOPE_NOT_TAIL = 2
+
+# numpy twin of spf_edge_delta (same layout: 24 bytes)
+EDGE_DELTA_DTYPE = np.dtype(
+    [("tail", np.uint32), ("head", np.uint32), ("metric", np.uint64),
+     ("kind", np.uint32), ("scope", np.uint32)]
 )
 
 
@@ -74,6 +89,32 @@ class _GraphDesc(C.Structure):
         ("num_links", C.c_uint32),
         ("device", C.c_int),
     ]
+
+
+def _graph_desc(csr: "Csr", device: int = 0):
+    """(spf_graph_desc, arrays it points into) for a Csr."""
+    keep = [
+        np.ascontiguousarray(csr.row_ptr, dtype=np.uint32),
+        np.ascontiguousarray(csr.col, dtype=np.uint32),
+        np.ascontiguousarray(csr.metric, dtype=np.uint64),
+        np.ascontiguousarray(csr.link_id, dtype=np.uint32),
+        np.ascontiguousarray(csr.rev, dtype=np.uint32),
+        np.ascontiguousarray(csr.overloaded, dtype=np.uint8),
+    ]
+    row, col, met, lid, rev, ov = keep
+    d = _GraphDesc(
+        csr.num_nodes,
+        len(col),
+        _p(row, C.c_uint32),
+        _p(col, C.c_uint32),
+        _p(met, C.c_uint64),
+        _p(lid, C.c_uint32),
+        _p(rev, C.c_uint32),
+        _p(ov, C.c_uint8),
+        csr.num_links,
+        device,
+    )
+    return d, keep
 
 
 class _QueryDesc(C.Structure):
@@ -142,6 +183,15 @@ def load():
             C.c_int,
             [vp, C.POINTER(vp), pu32, C.POINTER(vp), pu64],
         ),
+        "spf_graph_diff": (
+            C.c_int,
+            [C.POINTER(_GraphDesc), C.POINTER(_GraphDesc), vp, u32, pu32],
+        ),
+        "spf_table_screen": (
+            C.c_int,
+            [vp, vp, C.c_size_t, u32, pu32, vp, u32, C.POINTER(C.c_uint8)],
+        ),
+        "spf_query_scatter_rows": (C.c_int, [vp, pu32, vp, C.c_size_t]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -219,27 +269,7 @@ class Graph:
     def __init__(self, csr: Csr, device: int = 0):
         lib = load()
         self.csr = csr
-        self._keep = [
-            np.ascontiguousarray(csr.row_ptr, dtype=np.uint32),
-            np.ascontiguousarray(csr.col, dtype=np.uint32),
-            np.ascontiguousarray(csr.metric, dtype=np.uint64),
-            np.ascontiguousarray(csr.link_id, dtype=np.uint32),
-            np.ascontiguousarray(csr.rev, dtype=np.uint32),
-            np.ascontiguousarray(csr.overloaded, dtype=np.uint8),
-        ]
-        row, col, met, lid, rev, ov = self._keep
-        d = _GraphDesc(
-            csr.num_nodes,
-            len(col),
-            _p(row, C.c_uint32),
-            _p(col, C.c_uint32),
-            _p(met, C.c_uint64),
-            _p(lid, C.c_uint32),
-            _p(rev, C.c_uint32),
-            _p(ov, C.c_uint8),
-            csr.num_links,
-            device,
-        )
+        d, self._keep = _graph_desc(csr, device)
         h = C.c_void_p()
         _check(lib.spf_graph_create(C.byref(d), C.byref(h)), "spf_graph_create")
         self.h = h
@@ -273,11 +303,52 @@ class Graph:
         ov = np.ascontiguousarray(overloaded, dtype=np.uint8)
         _check(load().spf_graph_set_transit(self.h, _p(ov, C.c_uint8)), "transit")
 
+    def patch_metrics(self, edges, metrics):
+        """Metrics of existing half-edges, in place (spf_graph_patch_metrics)."""
+        e = np.ascontiguousarray(edges, dtype=np.uint32)
+        m = np.ascontiguousarray(metrics, dtype=np.uint64)
+        if len(e) != len(m):
+            raise ValueError("edges / metrics length mismatch")
+        _check(load().spf_graph_patch_metrics(self.h, len(e), _p(e, C.c_uint32), _p(m, C.c_uint64)),
+               "patch_metrics")
+
     def set_stream(self, stream_ptr: int | None):
         _check(load().spf_graph_set_stream(self.h, stream_ptr), "set_stream")
 
     def query(self, sources, flags=SPF_F_NEXTHOPS, ignore=None) -> "Query":
         return Query(self, sources, flags, ignore)
+
+    def table_screen(self, rows_ptr: int, pitch: int, sources, deltas) -> np.ndarray:
+        """uint8 [len(sources)]: 1 where the uint32 device row of sources[i]
+        (rows_ptr + i * pitch elements) can be changed by `deltas`."""
+        src = np.ascontiguousarray(sources, dtype=np.uint32)
+        dl = np.ascontiguousarray(deltas, dtype=EDGE_DELTA_DTYPE)
+        out = np.zeros(max(len(src), 1), dtype=np.uint8)
+        _check(
+            load().spf_table_screen(
+                self.h, rows_ptr, pitch, len(src), _p(src, C.c_uint32),
+                dl.ctypes.data if len(dl) else None, len(dl), _p(out, C.c_uint8),
+            ),
+            "table_screen",
+        )
+        return out[: len(src)]
+
+
+def graph_diff(before: "Csr", after: "Csr") -> np.ndarray:
+    """Directed edge deltas (EDGE_DELTA_DTYPE) turning `before` into `after`
+    (host only, spf_graph_diff)."""
+    lib = load()
+    da, ka = _graph_desc(before)
+    db, kb = _graph_desc(after)
+    n = C.c_uint32()
+    _check(lib.spf_graph_diff(C.byref(da), C.byref(db), None, 0, C.byref(n)), "graph_diff")
+    out = np.zeros(max(n.value, 1), dtype=EDGE_DELTA_DTYPE)
+    _check(
+        lib.spf_graph_diff(C.byref(da), C.byref(db), out.ctypes.data, n.value, C.byref(n)),
+        "graph_diff",
+    )
+    del ka, kb
+    return out[: n.value]
 
 
 class Query:
@@ -400,6 +471,13 @@ class Query:
             load().spf_query_fetch_rows(self.h, first, count, dst_ptr, pitch, 1 if on_device else 0),
             "fetch_rows",
         )
+
+    def scatter_rows(self, dst_rows, table_ptr: int, pitch: int):
+        """Row i of this query -> row dst_rows[i] of a device table (async
+        on the graph stream, spf_query_scatter_rows)."""
+        dr = np.ascontiguousarray(dst_rows, dtype=np.uint32)
+        _check(load().spf_query_scatter_rows(self.h, _p(dr, C.c_uint32), table_ptr, pitch),
+               "scatter_rows")
 
     def fetch_nexthops(self, first: int, count: int) -> np.ndarray:
         """Masks of queries [first, first+count), back to back (V*W_i words

@@ -100,6 +100,60 @@ def gather_rows(local, n: int, group=None, out=None):
     return out
 
 
+def exchange_rows(table, local_rows, n: int, group=None):
+    """Propagate repaired rows to every rank's copy of the gathered table.
+
+    `local_rows` (int64 [k], on the table's device) are rows of `table`
+    inside this rank's slot that were just rewritten; after the call every
+    rank's table holds them.  Ranks repair different numbers of rows, so the
+    counts are all-gathered first, each rank contributes a block padded to
+    the largest count (row index -1 = padding), and the received rows are
+    copied into place with index_copy_.  Traffic is proportional to the
+    repaired rows, not to the table.  Returns the number of rows received.
+    """
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world == 1:
+        return 0
+    dev = table.device
+    k = torch.tensor([int(local_rows.numel())], dtype=torch.int64, device=dev)
+    counts = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(counts, k, group=group)
+    m = int(counts.max().item())
+    if m == 0:
+        return 0
+    idx = torch.full((m,), -1, dtype=torch.int64, device=dev)
+    idx[: local_rows.numel()] = local_rows
+    rows = torch.zeros((m,) + tuple(table.shape[1:]), dtype=table.dtype, device=dev)
+    if local_rows.numel():
+        rows[: local_rows.numel()] = table.index_select(0, local_rows)
+    all_idx = torch.empty(world * m, dtype=torch.int64, device=dev)
+    all_rows = torch.empty((world * m,) + tuple(table.shape[1:]), dtype=table.dtype, device=dev)
+    dist.all_gather_into_tensor(all_idx, idx, group=group)
+    dist.all_gather_into_tensor(all_rows, rows, group=group)
+    keep = all_idx >= 0
+    table.index_copy_(0, all_idx[keep], all_rows[keep])
+    return int(keep.sum().item())
+
+
+@dataclass
+class RepairRun:
+    """One incremental table update on one rank (ShardedAllSources.update)."""
+
+    deltas: int = 0
+    affected: int = 0        # this rank's recomputed sources
+    affected_total: int = 0  # over all ranks
+    diff_ms: float = 0.0     # host edge diff (spf_graph_diff)
+    graph_ms: float = 0.0    # new device graph (host flatten + upload)
+    screen_ms: float = 0.0   # spf_table_screen (kernel + transfers)
+    spf_ms: float = 0.0      # device time of the affected sources' SSSPs
+    exchange_ms: float = 0.0 # repaired rows to the other ranks
+    wall_ms: float = 0.0     # barrier to barrier
+    graph_patched: bool = False  # device graph patched in place (same links)
+
+
 @dataclass
 class AllSourcesRun:
     """Timing of one sharded all-sources pass on one rank."""
@@ -150,6 +204,8 @@ class ShardedAllSources:
         self.kernel = self.query.kernel if self.query else ""
         rows = self.world * self.cap if gather else self.cap
         self.gather = gather
+        self.csr = csr
+        self.sources = src
         self.table = torch.full((rows, self.V), -1, dtype=torch.int32, device=f"cuda:{self.device}")
 
     def local_block(self):
@@ -161,6 +217,10 @@ class ShardedAllSources:
         import torch
         import torch.distributed as dist
 
+        if self.query is None and self.count:
+            mine = self.sources[self.first : self.first + self.count]
+            self.query = self.graph.query(mine, 0)
+            self.kernel = self.query.kernel
         out = AllSourcesRun(first=self.first, count=self.count, kernel=self.kernel)
         multi = self.world > 1
         if multi:
@@ -189,6 +249,105 @@ class ShardedAllSources:
         if self.query:
             out.spf_ms = self.query.elapsed_ms()
             out.fetch_ms = ev0.elapsed_time(ev1)
+        return out
+
+    def update(self, new_csr) -> RepairRun:
+        """Repair the table after a topology change instead of recomputing
+        every source (the reference clears its whole SPF
+        memo, LinkState.cpp:712-715).
+
+        `new_csr` must keep the node ids (same names, so the same ranks).
+        The change is listed as directed edge deltas (spf_graph_diff), the
+        screen kernel marks the sources of this rank whose shortest-path DAG
+        a delta can touch (spf_table_screen), only those are recomputed on
+        the new device graph and scattered into their rows, and the repaired
+        rows are exchanged between ranks (exchange_rows).  The result equals
+        a full recompute bit for bit (tests/test_allsources.py)."""
+        import numpy as np
+        import torch
+        import torch.distributed as dist
+
+        from openr_amd import abi
+
+        if new_csr.num_nodes != self.V:
+            raise ValueError("node set changed: node ids are not shared, rebuild the table")
+        out = RepairRun()
+        multi = self.world > 1
+        if multi:
+            dist.barrier(group=self.group)
+        torch.cuda.synchronize(self.device)
+        t0 = time.perf_counter()
+        deltas = abi.graph_diff(self.csr, new_csr)
+        t1 = time.perf_counter()
+        out.deltas = len(deltas)
+        # the full-batch query holds a result block the size of this rank's
+        # table slot: release it before the repair allocates
+        if self.query is not None:
+            self.query.close()
+            self.query = None
+        old = self.csr
+        same_links = (
+            len(old.col) == len(new_csr.col)
+            and np.array_equal(old.row_ptr, new_csr.row_ptr)
+            and np.array_equal(old.col, new_csr.col)
+            and np.array_equal(old.link_id, new_csr.link_id)
+            and np.array_equal(old.rev, new_csr.rev)
+        )
+        if same_links:
+            # metric / drain churn: patch the resident device graph in place
+            ch = np.nonzero(old.metric != new_csr.metric)[0]
+            if len(ch):
+                self.graph.patch_metrics(ch, new_csr.metric[ch])
+            if not np.array_equal(old.overloaded, new_csr.overloaded):
+                self.graph.set_transit(new_csr.overloaded)
+            self.graph.csr = new_csr
+            out.graph_patched = True
+        else:
+            graph = abi.Graph(new_csr, device=self.device)
+            graph.set_stream(self.stream.cuda_stream)
+            self.graph.close()
+            self.graph = graph
+        self.csr = new_csr
+        if self.graph.needs_exact:
+            raise abi.SpfError("all-sources tables need 32-bit sums (no metric 0 / 64-bit metrics)")
+        t2 = time.perf_counter()
+        block = self.local_block()
+        base = self.rank * self.cap if self.gather else 0
+        mine = self.sources[self.first : self.first + self.count]
+        hit = np.zeros(0, dtype=np.int64)
+        if self.count and len(deltas):
+            flags = self.graph.table_screen(block.data_ptr(), self.V, mine, deltas)
+            hit = np.nonzero(flags)[0]
+        t3 = time.perf_counter()
+        out.screen_ms = (t3 - t2) * 1e3
+        out.affected = len(hit)
+        if len(hit):
+            q = self.graph.query(mine[hit], 0)
+            try:
+                q.run(sync=False)
+                q.scatter_rows(hit.astype(np.uint32), block.data_ptr(), self.V * 4)
+                self.stream.synchronize()
+                out.spf_ms = q.elapsed_ms()
+            finally:
+                q.close()
+        t4 = time.perf_counter()
+        total = len(hit)
+        if self.gather and multi:
+            rows = torch.from_numpy(hit + base).to(block.device)
+            total = exchange_rows(self.table, rows, self.n, group=self.group) or 0
+            torch.cuda.synchronize(self.device)
+        elif multi:
+            t = torch.tensor([len(hit)], dtype=torch.int64, device=block.device)
+            dist.all_reduce(t, group=self.group)
+            total = int(t.item())
+        t5 = time.perf_counter()
+        if multi:
+            dist.barrier(group=self.group)
+        out.affected_total = total
+        out.diff_ms = (t1 - t0) * 1e3
+        out.graph_ms = (t2 - t1) * 1e3
+        out.exchange_ms = (t5 - t4) * 1e3
+        out.wall_ms = (time.perf_counter() - t0) * 1e3
         return out
 
     def row(self, i: int):

@@ -2005,6 +2005,78 @@ __global__ __launch_bounds__(256) void spf_whatif_screen_kernel(WhatifArgs a) {
   }
 }
 
+// Table repair screen (spf_table_screen): one lane per source row, every
+// lane walks the same delta list (wave-uniform loads of the delta arrays).
+// Reads two uint32 of the lane's row per in-scope delta and stops at the
+// first hit; the rows are untouched.
+struct ScreenArgs {
+  const uint32_t* rows;
+  size_t pitch;
+  const uint32_t* src;
+  const uint32_t* tail;
+  const uint32_t* head;
+  const uint64_t* metric;
+  const uint32_t* kind; // SPF_DELTA_* | scope << 4
+  uint32_t nrows;
+  uint32_t ndelta;
+  uint8_t* affected;
+};
+
+__global__ __launch_bounds__(256) void spf_table_screen_kernel(ScreenArgs a) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.nrows) {
+    return;
+  }
+  const uint32_t s = a.src[i];
+  const uint32_t* d = a.rows + (size_t)i * a.pitch;
+  uint8_t hit = 0;
+  for (uint32_t j = 0; j < a.ndelta && !hit; ++j) {
+    const uint32_t u = a.tail[j], k = a.kind[j];
+    const uint32_t scope = k >> 4;
+    if ((scope == SPF_SCOPE_TAIL_ONLY && s != u) ||
+        (scope == SPF_SCOPE_NOT_TAIL && s == u)) {
+      continue;
+    }
+    const uint32_t du = d[u];
+    if (du == kInf32) {
+      continue;
+    }
+    const uint64_t c = (uint64_t)du + a.metric[j];
+    const uint32_t dv = d[a.head[j]];
+    const uint64_t dv64 = dv == kInf32 ? ~0ull : (uint64_t)dv;
+    hit = (k & SPF_DELTA_REMOVED) ? (c == dv64) : (c <= dv64);
+  }
+  a.affected[i] = hit;
+}
+
+// Row scatter (spf_query_scatter_rows): workgroup (query, chunk) copies one
+// 16-byte-vectorised slice of query row q into table row dst[q].
+__global__ __launch_bounds__(256) void spf_scatter_rows_kernel(
+    const uint32_t* __restrict__ from, uint32_t from_pitch,
+    const uint32_t* __restrict__ dst_rows, char* __restrict__ table,
+    size_t pitch, uint32_t V) {
+  const uint32_t q = blockIdx.x;
+  const uint32_t* src = from + (size_t)q * from_pitch;
+  uint32_t* out = (uint32_t*)(table + (size_t)dst_rows[q] * pitch);
+  const uint32_t chunk = blockDim.x * 4 * 4; // 4 x uint4 per lane
+  const uint32_t lo = blockIdx.y * chunk;
+  const uint32_t hi = min(V, lo + chunk);
+  const bool vec = (reinterpret_cast<uintptr_t>(out) & 15) == 0 && (from_pitch & 3) == 0;
+  if (vec) {
+    const uint32_t n4 = (hi - lo) / 4;
+    for (uint32_t t = threadIdx.x; t < n4; t += blockDim.x) {
+      reinterpret_cast<uint4*>(out + lo)[t] = reinterpret_cast<const uint4*>(src + lo)[t];
+    }
+    for (uint32_t v = lo + n4 * 4 + threadIdx.x; v < hi; v += blockDim.x) {
+      out[v] = src[v];
+    }
+  } else {
+    for (uint32_t v = lo + threadIdx.x; v < hi; v += blockDim.x) {
+      out[v] = src[v];
+    }
+  }
+}
+
 __global__ void fill_u32_kernel(uint32_t* p, size_t n, uint32_t v) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -2070,6 +2142,8 @@ struct spf_query {
   // what-if screen: baseline runs (one per distinct source, no ignore list)
   spf_query* base = nullptr;
   uint32_t *d_base_of = nullptr, *d_skip = nullptr;
+  // spf_query_scatter_rows: destination row of every query
+  uint32_t* d_scatter = nullptr;
   uint64_t* d_nh_off = nullptr;
   void* d_dist = nullptr;
   uint64_t* d_nh = nullptr;
@@ -3607,6 +3681,197 @@ uint32_t spf_query_row_stride(const spf_query* q) {
     return 0;
   }
   return q->dist == DistPlan::Exact ? q->g->V : q->Vp;
+}
+
+} // extern "C"
+
+// ============================================ incremental all-sources tables
+
+extern "C" {
+
+int spf_graph_diff(
+    const spf_graph_desc* before, const spf_graph_desc* after,
+    spf_edge_delta* out, uint32_t cap, uint32_t* n_out) {
+  if (!before || !after || !n_out || (cap && !out)) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  if (before->num_nodes != after->num_nodes) {
+    return fail(SPF_E_INVALID, "graphs differ in node count (ids are not shared)");
+  }
+  const uint32_t V = before->num_nodes;
+  for (const spf_graph_desc* d : {before, after}) {
+    if (!d->row_ptr || (d->num_edges && (!d->col || !d->metric)) ||
+        (V && !d->node_overloaded) || d->row_ptr[V] != d->num_edges) {
+      return fail(SPF_E_INVALID, "malformed graph description");
+    }
+  }
+  uint64_t n = 0;
+  auto emit = [&](uint32_t u, uint32_t v, uint64_t w, uint32_t kind, uint32_t scope) {
+    if (n < cap) {
+      out[n] = spf_edge_delta{u, v, w, kind, scope};
+    }
+    ++n;
+  };
+  using HE = std::pair<uint32_t, uint64_t>; // (head, metric)
+  std::vector<HE> a, b;
+  for (uint32_t u = 0; u < V; ++u) {
+    const bool trA = !before->node_overloaded[u], trB = !after->node_overloaded[u];
+    const uint32_t ra = before->row_ptr[u], na = before->row_ptr[u + 1] - ra;
+    const uint32_t rb = after->row_ptr[u], nb = after->row_ptr[u + 1] - rb;
+    if (na == nb && std::equal(before->col + ra, before->col + ra + na, after->col + rb) &&
+        std::equal(before->metric + ra, before->metric + ra + na, after->metric + rb)) {
+      // the common case: this row is unchanged (only its transit bit may flip)
+      if (trA != trB) {
+        for (uint32_t k = 0; k < na; ++k) {
+          emit(u, before->col[ra + k], before->metric[ra + k],
+               trA ? SPF_DELTA_REMOVED : SPF_DELTA_ADDED, SPF_SCOPE_NOT_TAIL);
+        }
+      }
+      continue;
+    }
+    a.clear();
+    b.clear();
+    for (uint32_t e = before->row_ptr[u]; e < before->row_ptr[u + 1]; ++e) {
+      a.emplace_back(before->col[e], before->metric[e]);
+    }
+    for (uint32_t e = after->row_ptr[u]; e < after->row_ptr[u + 1]; ++e) {
+      b.emplace_back(after->col[e], after->metric[e]);
+    }
+    std::sort(a.begin(), a.end());
+    std::sort(b.begin(), b.end());
+    size_t i = 0, j = 0;
+    while (i < a.size() || j < b.size()) {
+      if (j == b.size() || (i < a.size() && a[i] < b[j])) {
+        emit(u, a[i].first, a[i].second, SPF_DELTA_REMOVED, trA ? SPF_SCOPE_ALL : SPF_SCOPE_TAIL_ONLY);
+        ++i;
+      } else if (i == a.size() || b[j] < a[i]) {
+        emit(u, b[j].first, b[j].second, SPF_DELTA_ADDED, trB ? SPF_SCOPE_ALL : SPF_SCOPE_TAIL_ONLY);
+        ++j;
+      } else {
+        if (trA && !trB) {
+          emit(u, a[i].first, a[i].second, SPF_DELTA_REMOVED, SPF_SCOPE_NOT_TAIL);
+        } else if (!trA && trB) {
+          emit(u, a[i].first, a[i].second, SPF_DELTA_ADDED, SPF_SCOPE_NOT_TAIL);
+        }
+        ++i;
+        ++j;
+      }
+    }
+  }
+  if (n > 0xFFFFFFFFull) {
+    return fail(SPF_E_UNSUPPORTED, "more than 2^32 deltas");
+  }
+  *n_out = (uint32_t)n;
+  return SPF_OK;
+}
+
+int spf_table_screen(
+    spf_graph* g, const uint32_t* rows, size_t pitch, uint32_t num_rows,
+    const uint32_t* sources, const spf_edge_delta* deltas, uint32_t n_deltas,
+    uint8_t* affected) {
+  if (!g || (num_rows && (!rows || !sources || !affected)) || (n_deltas && !deltas)) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  if (num_rows && pitch < g->V) {
+    return fail(SPF_E_INVALID, "row pitch < V");
+  }
+  for (uint32_t i = 0; i < num_rows; ++i) {
+    if (sources[i] >= g->V) {
+      return fail(SPF_E_INVALID, "source out of range");
+    }
+  }
+  for (uint32_t j = 0; j < n_deltas; ++j) {
+    if (deltas[j].tail >= g->V || deltas[j].head >= g->V ||
+        (deltas[j].kind != SPF_DELTA_REMOVED && deltas[j].kind != SPF_DELTA_ADDED) ||
+        deltas[j].scope > SPF_SCOPE_NOT_TAIL) {
+      return fail(SPF_E_INVALID, "bad delta " + std::to_string(j));
+    }
+  }
+  if (num_rows == 0) {
+    return SPF_OK;
+  }
+  if (n_deltas == 0) {
+    std::memset(affected, 0, num_rows);
+    return SPF_OK;
+  }
+  HIP_TRY(hipSetDevice(g->device));
+  // one device block: sources | tail | head | kind | metric (8-aligned) | flags
+  const size_t nd = n_deltas;
+  const size_t words = (size_t)num_rows + 3 * nd;
+  const size_t moff = (words * 4 + 7) & ~(size_t)7;
+  const size_t bytes = moff + nd * 8 + num_rows;
+  std::vector<char> h(bytes);
+  std::memcpy(h.data(), sources, (size_t)num_rows * 4);
+  uint32_t* ht = (uint32_t*)(h.data() + (size_t)num_rows * 4);
+  uint64_t* hm = (uint64_t*)(h.data() + moff);
+  for (size_t j = 0; j < nd; ++j) {
+    ht[j] = deltas[j].tail;
+    ht[nd + j] = deltas[j].head;
+    ht[2 * nd + j] = deltas[j].kind | (deltas[j].scope << 4);
+    hm[j] = deltas[j].metric;
+  }
+  char* d = nullptr;
+  HIP_TRY(hipMalloc((void**)&d, bytes));
+  int st = SPF_OK;
+  if (hipMemcpyAsync(d, h.data(), moff + nd * 8, hipMemcpyHostToDevice, g->stream) != hipSuccess) {
+    st = fail(SPF_E_DEVICE, "delta upload failed");
+  }
+  if (st == SPF_OK) {
+    ScreenArgs a;
+    a.rows = rows;
+    a.pitch = pitch;
+    a.src = (const uint32_t*)d;
+    a.tail = (const uint32_t*)(d + (size_t)num_rows * 4);
+    a.head = a.tail + nd;
+    a.kind = a.tail + 2 * nd;
+    a.metric = (const uint64_t*)(d + moff);
+    a.nrows = num_rows;
+    a.ndelta = n_deltas;
+    a.affected = (uint8_t*)(d + moff + nd * 8);
+    hipLaunchKernelGGL(spf_table_screen_kernel, dim3((num_rows + 255) / 256), dim3(256), 0,
+                       g->stream, a);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(affected, a.affected, num_rows, hipMemcpyDeviceToHost, g->stream) != hipSuccess ||
+        hipStreamSynchronize(g->stream) != hipSuccess) {
+      st = fail(SPF_E_DEVICE, "screen kernel failed");
+    }
+  }
+  (void)hipStreamSynchronize(g->stream);
+  (void)hipFree(d);
+  return st;
+}
+
+int spf_query_scatter_rows(
+    spf_query* q, const uint32_t* dst_rows, void* table, size_t pitch) {
+  if (!q || (q->nq && (!dst_rows || !table))) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  if (!q->ran) {
+    return fail(SPF_E_INVALID, "query has not run");
+  }
+  if (q->dist == DistPlan::Exact) {
+    return fail(SPF_E_UNSUPPORTED, "64-bit distance rows: use spf_query_dist");
+  }
+  const uint32_t V = q->g->V;
+  if (pitch < (size_t)V * 4) {
+    return fail(SPF_E_INVALID, "destination pitch < 4*V");
+  }
+  if (q->nq == 0 || V == 0) {
+    return SPF_OK;
+  }
+  HIP_TRY(hipSetDevice(q->g->device));
+  if (!q->d_scatter) {
+    HIP_TRY(hipMalloc((void**)&q->d_scatter, (size_t)q->nq * 4));
+  }
+  // the previous scatter of this query may still read d_scatter
+  HIP_TRY(hipStreamSynchronize(q->g->stream));
+  HIP_TRY(hipMemcpy(q->d_scatter, dst_rows, (size_t)q->nq * 4, hipMemcpyHostToDevice));
+  const uint32_t chunk = 256 * 16;
+  hipLaunchKernelGGL(spf_scatter_rows_kernel, dim3(q->nq, (V + chunk - 1) / chunk), dim3(256), 0,
+                     q->g->stream, (const uint32_t*)q->d_dist, q->Vp, q->d_scatter,
+                     (char*)table, pitch, V);
+  HIP_TRY(hipGetLastError());
+  return SPF_OK;
 }
 
 } // extern "C"

@@ -1,0 +1,279 @@
+"""Incremental all-sources tables.
+
+The reference drops its whole SPF memo on any topology change
+(openr/decision/LinkState.cpp:712-715, driven by updateAdjacencyDatabase
+:564-717).  The engine repairs a resident table instead: spf_graph_diff lists
+the change as directed edge deltas, spf_table_screen marks the sources whose
+shortest-path DAG a delta can touch, and only those are recomputed.
+
+CPU ("not gpu"):
+  * spf_graph_diff (host-only C) against a Python restatement;
+  * the screen RULE (restated in numpy below, test-only) is exact: on random
+    graphs and random churn (link down / up, metric up / down, node
+    overload / un-overload, several at once) every source it does NOT flag
+    has the same distances AND next-hop sets before and after, by the
+    literal DijkstraQ replay (oracle/spf_py.py);
+  * exchange_rows (repaired rows to the other ranks) over gloo, world 2 / 3.
+GPU: ShardedAllSources.update() (diff + screen kernel + partial recompute +
+scatter kernel) equals a full recompute bit for bit, on the frontier (LDS),
+delta-stepping (beyond LDS) and MS-BFS (uniform metric) plans.
+"""
+
+import os
+import random
+import socket
+
+import numpy as np
+import pytest
+
+from openr_amd import abi
+from openr_amd import allsources as AS
+
+INF = 0xFFFFFFFF
+
+
+def _random_links(V, L, rng, wmax=20):
+    links = [(rng.randrange(v), v, rng.randint(1, wmax), rng.randint(1, wmax)) for v in range(1, V)]
+    seen = {(min(u, v), max(u, v)) for (u, v, _, _) in links}
+    while len(links) < L:
+        u, v = rng.randrange(V), rng.randrange(V)
+        if u != v and (min(u, v), max(u, v)) not in seen:
+            seen.add((min(u, v), max(u, v)))
+            links.append((u, v, rng.randint(1, wmax), rng.randint(1, wmax)))
+    return links
+
+
+def _churn(V, links, ov, rng, kinds, wmax=20):
+    """One topology change: returns (links', ov')."""
+    links = list(links)
+    ov = np.array(ov, dtype=np.uint8)
+    for kind in kinds:
+        if kind == "down" and links:
+            links.pop(rng.randrange(len(links)))
+        elif kind == "up":
+            u, v = rng.randrange(V), rng.randrange(V)
+            if u != v:
+                links.append((u, v, rng.randint(1, wmax), rng.randint(1, wmax)))
+        elif kind in ("metric_up", "metric_down") and links:
+            i = rng.randrange(len(links))
+            u, v, a, b = links[i]
+            if kind == "metric_up":
+                a = a + rng.randint(1, wmax)
+            else:
+                a = max(1, a - rng.randint(1, wmax))
+            links[i] = (u, v, a, b)
+        elif kind == "drain":
+            ov[rng.randrange(V)] ^= 1
+    return links, ov
+
+
+def _diff_py(a, b):
+    """Python restatement of spf_graph_diff (include/openr_spf.h)."""
+    out = []
+    for u in range(a.num_nodes):
+        ea = sorted((int(a.col[e]), int(a.metric[e])) for e in range(a.row_ptr[u], a.row_ptr[u + 1]))
+        eb = sorted((int(b.col[e]), int(b.metric[e])) for e in range(b.row_ptr[u], b.row_ptr[u + 1]))
+        trA, trB = not a.overloaded[u], not b.overloaded[u]
+        ca = {}
+        for x in ea:
+            ca[x] = ca.get(x, 0) + 1
+        cb = {}
+        for x in eb:
+            cb[x] = cb.get(x, 0) + 1
+        for x in sorted(set(ca) | set(cb)):
+            na, nb = ca.get(x, 0), cb.get(x, 0)
+            common = min(na, nb)
+            out += [(u, x[0], x[1], abi.SPF_DELTA_REMOVED, 0 if trA else 1)] * (na - common)
+            out += [(u, x[0], x[1], abi.SPF_DELTA_ADDED, 0 if trB else 1)] * (nb - common)
+            if trA and not trB:
+                out += [(u, x[0], x[1], abi.SPF_DELTA_REMOVED, 2)] * common
+            elif trB and not trA:
+                out += [(u, x[0], x[1], abi.SPF_DELTA_ADDED, 2)] * common
+    return sorted(out)
+
+
+def _screen_np(D, sources, deltas):
+    """Test-only restatement of spf_table_screen_kernel's rule."""
+    out = np.zeros(len(sources), dtype=np.uint8)
+    for i, s in enumerate(sources):
+        for d in deltas:
+            u, v, w, kind, scope = int(d["tail"]), int(d["head"]), int(d["metric"]), int(d["kind"]), int(d["scope"])
+            if (scope == abi.SPF_SCOPE_TAIL_ONLY and s != u) or (scope == abi.SPF_SCOPE_NOT_TAIL and s == u):
+                continue
+            du = int(D[i][u])
+            if du == INF:
+                continue
+            dv = int(D[i][v])
+            dv = float("inf") if dv == INF else dv
+            if (kind == abi.SPF_DELTA_REMOVED and du + w == dv) or (kind == abi.SPF_DELTA_ADDED and du + w <= dv):
+                out[i] = 1
+                break
+    return out
+
+
+def _rows(csr, srcs):
+    from oracle import spf_py
+
+    D = np.full((len(srcs), csr.num_nodes), INF, dtype=np.uint64)
+    NH = []
+    for i, s in enumerate(srcs):
+        r = spf_py.run_spf(csr, int(s), True)
+        for v, (m, nh, _, _) in r.items():
+            D[i, v] = m
+        NH.append({v: nh for v, (m, nh, _, _) in r.items()})
+    return D, NH
+
+
+def test_graph_diff_matches_restatement():
+    rng = random.Random(3)
+    for trial in range(12):
+        V = rng.randint(2, 40)
+        links = _random_links(V, min(V * (V - 1) // 2, rng.randint(V - 1, 3 * V)), rng)
+        ov = np.array([rng.random() < 0.2 for _ in range(V)], dtype=np.uint8)
+        kinds = rng.choices(["down", "up", "metric_up", "metric_down", "drain"], k=rng.randint(0, 5))
+        links2, ov2 = _churn(V, links, ov, rng, kinds)
+        a = abi.Csr.from_links(V, links, ov)
+        b = abi.Csr.from_links(V, links2, ov2)
+        got = sorted(tuple(int(x) for x in d) for d in abi.graph_diff(a, b))
+        assert got == _diff_py(a, b), (trial, kinds)
+    # identical graphs: no deltas; different node counts: refused
+    assert len(abi.graph_diff(a, a)) == 0
+    with pytest.raises(abi.SpfError):
+        abi.graph_diff(a, abi.Csr.from_links(V + 1, links, np.append(ov, 0)))
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_screen_rule_is_exact(seed):
+    """Unflagged sources keep distances AND next-hop sets (replay oracle)."""
+    rng = random.Random(seed)
+    kept = total = 0
+    for trial in range(6):
+        V = 45
+        links = _random_links(V, 110, rng, wmax=6)  # small metrics: many ties
+        ov = np.array([rng.random() < 0.1 for _ in range(V)], dtype=np.uint8)
+        kinds = [rng.choice(["down", "up", "metric_up", "metric_down", "drain"])
+                 for _ in range(rng.choice([1, 1, 2, 4]))]
+        links2, ov2 = _churn(V, links, ov, rng, kinds, wmax=6)
+        a = abi.Csr.from_links(V, links, ov)
+        b = abi.Csr.from_links(V, links2, ov2)
+        srcs = list(range(V))
+        D0, NH0 = _rows(a, srcs)
+        D1, NH1 = _rows(b, srcs)
+        flags = _screen_np(D0, srcs, abi.graph_diff(a, b))
+        for i in range(V):
+            if not flags[i]:
+                assert (D0[i] == D1[i]).all(), (trial, kinds, i)
+                assert NH0[i] == NH1[i], (trial, kinds, i)
+                kept += 1
+            total += 1
+    assert kept > total // 10  # the screen does skip work
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _exchange_worker(rank, world, port, out_q):
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, V = 23, 17
+        cap = AS.shard_cap(n, world)
+        g = torch.Generator().manual_seed(5)
+        before = torch.randint(0, 1000, (world * cap, V), generator=g, dtype=torch.int32)
+        after = before.clone()
+        expect = before.clone()
+        # rank r rewrites r + 1 rows of its own slot (rank 0 also none-case below)
+        for r in range(world):
+            first, count = AS.shard(n, world, r)
+            k = min(count, r + 1)
+            rows = torch.arange(k, dtype=torch.int64) * 2 % max(count, 1) + r * cap
+            rows = torch.unique(rows)
+            new = torch.full((len(rows), V), 7000 + r, dtype=torch.int32)
+            expect[rows] = new
+            if r == rank:
+                after[rows] = new
+                mine = rows
+        got = AS.exchange_rows(after, mine, n)
+        ok = bool((after == expect).all())
+        # nothing repaired anywhere: no traffic, table unchanged
+        none = AS.exchange_rows(after, torch.zeros(0, dtype=torch.int64), n)
+        out_q.put((rank, ok and got > 0 and none == 0 and bool((after == expect).all())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_rows_gloo(world):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    res = dict(q.get(timeout=10) for _ in range(world))
+    assert all(res.values()), res
+
+
+def _full_table(csr, srcs):
+    import torch
+
+    g = abi.Graph(csr)
+    q = g.query(srcs, 0).run()
+    t = torch.full((len(srcs), csr.num_nodes), -1, dtype=torch.int32, device="cuda:0")
+    torch.cuda.synchronize()  # the fill runs on torch's stream, the copy on the graph's
+    q.fetch_rows(0, len(srcs), t.data_ptr(), csr.num_nodes * 4, on_device=True)
+    q.sync()
+    out = t.cpu().numpy().view(np.uint32).copy()
+    q.close()
+    g.close()
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize(
+    "V,L,wmax,nsrc,expect_kernel",
+    [(3000, 12000, 50, 3000, None), (40000, 160000, 1000, 400, "dstep"), (2500, 9000, 1, 2500, None)],
+)
+def test_repair_equals_full_recompute(gpu_ready, V, L, wmax, nsrc, expect_kernel):
+    import torch
+
+    rng = random.Random(V + L)
+    links = _random_links(V, L, rng, wmax=wmax)
+    ov = np.zeros(V, dtype=np.uint8)
+    csr = abi.Csr.from_links(V, links, ov)
+    srcs = np.asarray(sorted(rng.sample(range(V), nsrc)), dtype=np.uint32)
+    torch.cuda.set_device(0)
+    sas = AS.ShardedAllSources(csr, sources=srcs)
+    if expect_kernel:
+        assert sas.kernel == expect_kernel
+    sas.run()
+    plan = [["down"], ["up"], ["metric_up"], ["metric_down"], ["drain"], ["drain"],
+            ["down", "down", "up", "metric_down", "drain"], []]
+    affected = []
+    for kinds in plan:
+        links, ov = _churn(V, links, ov, rng, kinds, wmax=wmax)
+        csr = abi.Csr.from_links(V, links, ov)
+        rep = sas.update(csr)
+        affected.append(rep.affected)
+        got = sas.table.cpu().numpy().view(np.uint32)[: len(srcs)]
+        assert (got == _full_table(csr, srcs)).all(), kinds
+    assert affected[-1] == 0  # no change: nothing recomputed
+    assert min(affected[:-1]) < len(srcs)  # the screen skips sources
+    # a full run after repairs still works (the batch query is rebuilt)
+    sas.run()
+    assert (sas.table.cpu().numpy().view(np.uint32)[: len(srcs)] == _full_table(csr, srcs)).all()
+    sas.close()

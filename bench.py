@@ -599,7 +599,8 @@ def wan_table_repair(topo, csr, sas, world, rank, local, dist):
                        "ms": round(float(t[0]), 2), "spf_ms": round(float(t[1]), 2),
                        "screen_ms": round(float(t[2]), 2), "graph_ms": round(float(t[3]), 2),
                        "exchange_ms": round(float(t[4]), 2), "diff_ms": round(rep.diff_ms, 2),
-                       "graph_patched_in_place": rep.graph_patched})
+                       "graph_patched_in_place": rep.graph_patched,
+                       "rows": "repaired in place (spf_table_repair)" if rep.relaxed else "recomputed"})
         cur = nxt
     check = None
     if rank == 0 and sas.gather or world == 1:

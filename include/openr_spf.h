@@ -215,6 +215,22 @@ int spf_table_screen(
     spf_graph* g, const uint32_t* rows, size_t pitch, uint32_t num_rows,
     const uint32_t* sources, const spf_edge_delta* deltas, uint32_t n_deltas,
     uint8_t* affected);
+/* Repair rows in place instead of recomputing them: rows[row_idx[i]]
+ * (device table, pitch elements apart) hold source sources[i]'s distances
+ * on the graph before a change, `g` is the graph after it and `deltas` =
+ * spf_graph_diff(before, after).  Per row (spf_dstep_kernel, seeded mode):
+ * nodes whose every shortest path may have used a REMOVED edge are found
+ * (tight-edge closure from the removed tight edges) and those no longer
+ * supported by a surviving tight path are reset to unreached; every value is
+ * then an upper bound, and label-correcting delta-stepping from the reset
+ * boundary and the tails of the ADDED edges lowers the row to g's distances
+ * exactly, touching only the region that changed.  SPF_E_UNSUPPORTED when
+ * the bucket image does not fit LDS or g needs the exact kernel (then
+ * recompute the rows).  Synchronous. */
+int spf_table_repair(
+    spf_graph* g, uint32_t* rows, size_t pitch, uint32_t num_rows,
+    const uint32_t* sources, const uint32_t* row_idx,
+    const spf_edge_delta* deltas, uint32_t n_deltas);
 /* Copy distance row i of the query (uint32, as spf_query_fetch_rows) to
  * row dst_rows[i] of the device table `table` (pitch bytes apart), for every
  * query, in one kernel on the graph stream (asynchronous). */

@@ -19,6 +19,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("OPENR_SPF_LIB") or os.path.join(_HERE, "libopenr_spf.so")
 
 SPF_OK = 0
+SPF_E_UNSUPPORTED = -4
 SPF_UNREACHABLE = (1 << 64) - 1
 SPF_F_UNIT_METRIC = 0x1
 SPF_F_NEXTHOPS = 0x2
@@ -57,6 +58,7 @@ EXPORTED_SYMBOLS = (
     "spf_graph_diff",
     "spf_table_screen",
     "spf_query_scatter_rows",
+    "spf_table_repair",
 )
 
 SPF_DELTA_REMOVED = 1
@@ -192,6 +194,7 @@ def load():
             [vp, vp, C.c_size_t, u32, pu32, vp, u32, C.POINTER(C.c_uint8)],
         ),
         "spf_query_scatter_rows": (C.c_int, [vp, pu32, vp, C.c_size_t]),
+        "spf_table_repair": (C.c_int, [vp, vp, C.c_size_t, u32, pu32, pu32, vp, u32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -332,6 +335,21 @@ class Graph:
             "table_screen",
         )
         return out[: len(src)]
+
+    def table_repair(self, rows_ptr: int, pitch: int, sources, row_idx, deltas) -> bool:
+        """Repair device rows in place after `deltas` (spf_table_repair).
+        False when the engine cannot (SPF_E_UNSUPPORTED): recompute instead."""
+        src = np.ascontiguousarray(sources, dtype=np.uint32)
+        ri = np.ascontiguousarray(row_idx, dtype=np.uint32)
+        dl = np.ascontiguousarray(deltas, dtype=EDGE_DELTA_DTYPE)
+        if len(src) != len(ri):
+            raise ValueError("sources / row_idx length mismatch")
+        st = load().spf_table_repair(self.h, rows_ptr, pitch, len(src), _p(src, C.c_uint32),
+                                     _p(ri, C.c_uint32), dl.ctypes.data if len(dl) else None, len(dl))
+        if st == SPF_E_UNSUPPORTED:
+            return False
+        _check(st, "table_repair")
+        return True
 
 
 def graph_diff(before: "Csr", after: "Csr") -> np.ndarray:

@@ -24,6 +24,7 @@ producer on the GPU is the HIP engine (openr_amd.abi), never a CPU fallback.
 
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -152,6 +153,7 @@ class RepairRun:
     exchange_ms: float = 0.0 # repaired rows to the other ranks
     wall_ms: float = 0.0     # barrier to barrier
     graph_patched: bool = False  # device graph patched in place (same links)
+    relaxed: bool = False    # rows repaired in place (spf_table_repair), not recomputed
 
 
 @dataclass
@@ -321,7 +323,18 @@ class ShardedAllSources:
         t3 = time.perf_counter()
         out.screen_ms = (t3 - t2) * 1e3
         out.affected = len(hit)
-        if len(hit):
+        relaxed = False
+        if len(hit) and not os.environ.get("OPENR_SPF_REPAIR_RECOMPUTE"):
+            # repair the affected rows in place (reset what lost its support,
+            # relax from the boundary and the improved edges) instead of
+            # recomputing them from scratch
+            t = time.perf_counter()
+            relaxed = self.graph.table_repair(block.data_ptr(), self.V, mine[hit],
+                                              hit.astype(np.uint32), deltas)
+            if relaxed:
+                out.relaxed = True
+                out.spf_ms = (time.perf_counter() - t) * 1e3
+        if len(hit) and not relaxed:
             q = self.graph.query(mine[hit], 0)
             try:
                 q.run(sync=False)

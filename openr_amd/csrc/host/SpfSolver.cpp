@@ -57,6 +57,27 @@ thrift::RouteDatabase DecisionRouteDb::toThrift() const {
   return db;
 }
 
+void releaseRouteDb(DecisionRouteDb&& db) {
+  // The per-route payload (next-hop sets, prefix entries) is most of the
+  // memory and was allocated by the build's workers: free it on the same
+  // pool, bucket range by bucket range, then drop the emptied maps.
+  auto& u = db.unicastEntries;
+  const size_t nb = u.bucket_count();
+  parallelFor(nb, hostThreads(u.size(), 256), [&](size_t b, unsigned) {
+    for (auto it = u.begin(b); it != u.end(b); ++it) {
+      RibUnicastEntry dead(std::move(it->second));
+    }
+  }, 64);
+  auto& m = db.mplsEntries;
+  const size_t mb = m.bucket_count();
+  parallelFor(mb, hostThreads(m.size(), 256), [&](size_t b, unsigned) {
+    for (auto it = m.begin(b); it != m.end(b); ++it) {
+      RibMplsEntry dead(std::move(it->second));
+    }
+  }, 64);
+  DecisionRouteDb gone(std::move(db));
+}
+
 DecisionRouteUpdate getRouteDelta(const DecisionRouteDb& newDb, const DecisionRouteDb& oldDb) {
   DecisionRouteUpdate delta;
   for (const auto& [prefix, entry] : newDb.unicastEntries) {

@@ -84,6 +84,12 @@ struct DecisionRouteUpdate {
   std::vector<int32_t> mplsRoutesToDelete;
 };
 
+// Drop a RouteDb with its payload freed on the host worker pool: the
+// Decision thread replaces its RouteDb on every rebuild (Decision.cpp:
+// 1803-1804) and freeing ~10^5 next hops one by one costs more than the
+// build itself on the fabric.
+void releaseRouteDb(DecisionRouteDb&& db);
+
 // old vs new RouteDb -> delta (reference: Decision.cpp:47-85)
 DecisionRouteUpdate getRouteDelta(const DecisionRouteDb& newDb, const DecisionRouteDb& oldDb);
 

@@ -257,6 +257,9 @@ PYBIND11_MODULE(_openr_spf, m) {
                nu = (long)db->unicastEntries.size();
                nm = (long)db->mplsEntries.size();
              }
+             if (db) {
+               releaseRouteDb(std::move(*db));
+             }
              db.reset();
              const double freeUs = std::chrono::duration<double, std::micro>(
                                        std::chrono::steady_clock::now() - t1)

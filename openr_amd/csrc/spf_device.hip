@@ -443,6 +443,20 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
 struct DstepArgs {
   SsspArgs s;
   uint32_t shift; // bucket width 2^shift
+  // SEED (spf_table_repair): query q repairs table row row_idx[q] in place:
+  // nodes whose every shortest path used a removed edge are reset first,
+  // then relaxation runs from the seed nodes with the row's values
+  uint32_t* table = nullptr;
+  size_t pitch = 0;
+  const uint32_t* row_idx = nullptr;
+  const uint32_t* seed = nullptr; // tails of ADDED deltas
+  uint32_t nseed = 0;
+  const uint32_t* rm_tail = nullptr; // REMOVED deltas
+  const uint32_t* rm_head = nullptr;
+  const uint64_t* rm_w = nullptr;
+  const uint32_t* rm_scope = nullptr;
+  uint32_t nrem = 0;
+  uint32_t* gscratch2 = nullptr; // per-workgroup second node queue (V u32)
 };
 
 // Load that bypasses the (non-coherent) vector L1: values other lanes change
@@ -530,11 +544,154 @@ __device__ __forceinline__ uint32_t min_pending_bucket(
   return r;
 }
 
+__device__ __forceinline__ bool bit_test(const uint32_t* b, uint32_t v) {
+  return (b[v >> 5] >> (v & 31)) & 1u;
+}
+// set bit v; true if this call set it
+__device__ __forceinline__ bool bit_claim(uint32_t* b, uint32_t v) {
+  const uint32_t m = 1u << (v & 31);
+  return !(atomicOr(&b[v >> 5], m) & m);
+}
+
+// Repair prologue of the seeded delta-stepping run (spf_table_repair) for
+// one table row `dist` of source `src`, after edges were REMOVED (link down,
+// metric increase, node overload).  Exact rule (tests/test_table_repair.py):
+//  K  = heads of removed edges that were tight (d[u] + w == d[v], u in
+//       scope) and everything reachable from them over tight usable edges of
+//       the new graph — a superset of the nodes whose shortest paths can use
+//       a removed edge (every node outside K keeps a surviving tight path);
+//  ok = nodes of K reachable from outside K over tight usable edges of the
+//       new graph: their distance is still achieved, so it stays exact;
+//  K \ ok is reset to unreached, and every reached in-neighbour outside it
+//  becomes a seed of the relaxation that follows (added to `pend`).
+// `kb` / `ok` are zeroed LDS bitmaps (both zeroed again on exit), q1 / q2
+// per-workgroup node queues of V entries, ctl >= 2 LDS words.
+template <uint32_t BS>
+__device__ void repair_invalidate(
+    const DstepArgs& da, uint32_t src, uint32_t* dist, uint32_t* kb,
+    uint32_t* ok, uint32_t* pend, uint32_t* q1, uint32_t* q2, uint32_t* ctl) {
+  const SsspArgs& a = da.s;
+  const uint32_t tid = threadIdx.x, G = a.G;
+  const uint32_t lg = tid & (G - 1), grp = tid / G, ngrp = BS / G;
+  auto usable = [&](uint32_t u) {
+    return u == src || ((a.trbits[u >> 5] >> (u & 31)) & 1u);
+  };
+  if (tid == 0) {
+    ctl[0] = 0;
+    ctl[1] = 0;
+  }
+  __syncthreads();
+  // heads of removed tight edges
+  for (uint32_t j = tid; j < da.nrem; j += BS) {
+    const uint32_t u = da.rm_tail[j], sc = da.rm_scope[j];
+    if ((sc == SPF_SCOPE_TAIL_ONLY && src != u) || (sc == SPF_SCOPE_NOT_TAIL && src == u)) {
+      continue;
+    }
+    const uint32_t du = dist[u], v = da.rm_head[j], dv = dist[v];
+    if (du != kInf32 && dv != kInf32 && (uint64_t)du + da.rm_w[j] == dv && bit_claim(kb, v)) {
+      q1[atomicAdd(&ctl[0], 1u)] = v;
+    }
+  }
+  __syncthreads();
+  // K: closure over tight usable edges (q1 accumulates K in BFS order)
+  uint32_t lo = 0, hi = ctl[0];
+  __syncthreads();
+  while (lo < hi) {
+    for (uint32_t i = lo + grp; i < hi; i += ngrp) {
+      const uint32_t x = q1[i];
+      if (!usable(x)) {
+        continue;
+      }
+      const uint32_t dx = dist[x];
+      for (uint32_t e = a.row[x] + lg; e < a.row[x + 1]; e += G) {
+        const uint32_t z = a.col[e];
+        if (dx + a.wout[e] == dist[z] && bit_claim(kb, z)) {
+          q1[atomicAdd(&ctl[0], 1u)] = z;
+        }
+      }
+    }
+    __syncthreads();
+    lo = hi;
+    hi = ctl[0];
+    __syncthreads();
+  }
+  const uint32_t nk = hi;
+  // ok: K nodes with a tight usable in-edge from outside K ...
+  for (uint32_t i = grp; i < nk; i += ngrp) {
+    const uint32_t x = q1[i], dx = dist[x];
+    for (uint32_t e = a.row[x] + lg; e < a.row[x + 1]; e += G) {
+      const uint32_t y = a.col[e];
+      if (bit_test(kb, y) || !usable(y)) {
+        continue;
+      }
+      const uint32_t dy = dist[y];
+      if (dy != kInf32 && dy + a.win[e] == dx && bit_claim(ok, x)) {
+        q2[atomicAdd(&ctl[1], 1u)] = x;
+      }
+    }
+  }
+  __syncthreads();
+  // ... and everything of K they reach over tight usable edges
+  lo = 0;
+  hi = ctl[1];
+  __syncthreads();
+  while (lo < hi) {
+    for (uint32_t i = lo + grp; i < hi; i += ngrp) {
+      const uint32_t x = q2[i];
+      if (!usable(x)) {
+        continue;
+      }
+      const uint32_t dx = dist[x];
+      for (uint32_t e = a.row[x] + lg; e < a.row[x + 1]; e += G) {
+        const uint32_t z = a.col[e];
+        if (bit_test(kb, z) && dx + a.wout[e] == dist[z] && bit_claim(ok, z)) {
+          q2[atomicAdd(&ctl[1], 1u)] = z;
+        }
+      }
+    }
+    __syncthreads();
+    lo = hi;
+    hi = ctl[1];
+    __syncthreads();
+  }
+  // reset K \ ok; kb becomes "reset" (K \ ok) for the seed pass
+  for (uint32_t i = tid; i < nk; i += BS) {
+    const uint32_t x = q1[i];
+    if (bit_test(ok, x)) {
+      atomicAnd(&kb[x >> 5], ~(1u << (x & 31)));
+    } else {
+      dist[x] = kInf32;
+    }
+  }
+  __syncthreads();
+  // seeds: reached in-neighbours of reset nodes (the reset boundary)
+  for (uint32_t i = grp; i < nk; i += ngrp) {
+    const uint32_t x = q1[i];
+    if (!bit_test(kb, x)) {
+      continue;
+    }
+    for (uint32_t e = a.row[x] + lg; e < a.row[x + 1]; e += G) {
+      const uint32_t y = a.col[e];
+      if (!bit_test(kb, y) && dist[y] != kInf32) {
+        atomicOr(&pend[y >> 5], 1u << (y & 31));
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < nk; i += BS) {
+    const uint32_t x = q1[i];
+    kb[x >> 5] = 0;
+    ok[x >> 5] = 0;
+  }
+  __syncthreads();
+}
+
 // LBK: bucket bytes in LDS (V B: one workgroup per CU on the 100k WAN);
 // otherwise buckets are read from the distance row and the LDS image is the
 // two bitmaps only, so several workgroups (sources) share a CU.
-template <int WMAX, bool IGN, uint32_t BS, bool LBK>
+template <int WMAX, bool IGN, uint32_t BS, bool LBK, bool SEED = false>
 __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
+  static_assert(!SEED || (WMAX == 0 && !IGN && LBK), "seeded runs are distance-only");
   extern __shared__ __align__(16) uint32_t smem[];
   const SsspArgs& a = da.s;
   const uint32_t V = a.V, nbw = a.nbw, G = a.G, shift = da.shift;
@@ -552,14 +709,19 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
   for (uint32_t i = tid; i < nbw; i += BS) {
     act[i] = 0;
     pend[i] = 0;
+    if constexpr (SEED) {
+      reinterpret_cast<uint32_t*>(bkt + ((V + 15) & ~15u))[i] = 0;
+    }
   }
+  __syncthreads();
 
   for (uint32_t q = blockIdx.x; q < a.nq; q += gridDim.x) {
     if (a.skip && a.skip[q]) {
       continue; // uniform per block
     }
     const uint32_t src = a.src[q];
-    uint32_t* dist = a.dist_out + (size_t)q * a.Vp;
+    uint32_t* dist = SEED ? da.table + (size_t)da.row_idx[q] * da.pitch
+                          : a.dist_out + (size_t)q * a.Vp;
     uint32_t nign = 0;
     const uint32_t* ignp = ignl;
     if constexpr (IGN) {
@@ -579,26 +741,50 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
       Wm = a.nh_w[q];
       nhrow = a.nh_out + a.nh_off[q];
     }
-    for (uint32_t v = tid; v < V; v += BS) {
-      dist[v] = kInf32;
-      if constexpr (LBK) {
-        bkt[v] = 255;
+    if constexpr (SEED) {
+      if (da.nrem) {
+        // third bitmap after the bucket bytes (SEED launches reserve it)
+        uint32_t* okb = reinterpret_cast<uint32_t*>(bkt + ((V + 15) & ~15u));
+        repair_invalidate<BS>(da, src, dist, act, okb, pend, queue,
+                              da.gscratch2 + (size_t)blockIdx.x * V, ctl);
       }
-    }
-    if constexpr (WMAX > 0) {
-      for (uint32_t i = tid; i < V * Wm; i += BS) {
-        nhrow[i] = 0;
+      // every value is now an upper bound on the new distance (unchanged
+      // support, or reset): bucket bytes from the row, the seeds pending;
+      // relaxation only ever lowers it, to the new fixpoint
+      for (uint32_t v = tid; v < V; v += BS) {
+        const uint32_t dv = dist[v];
+        bkt[v] = dv == kInf32 ? 255 : (uint8_t)min(dv >> shift, 254u);
       }
-    }
-    __syncthreads();
-    if (tid == 0) {
-      dist[src] = 0;
-      if constexpr (LBK) {
-        bkt[src] = 0;
+      __syncthreads();
+      for (uint32_t i = tid; i < da.nseed; i += BS) {
+        const uint32_t u = da.seed[i];
+        if (dist[u] != kInf32) {
+          atomicOr(&pend[u >> 5], 1u << (u & 31));
+        }
       }
-      pend[src >> 5] |= 1u << (src & 31);
+      __syncthreads();
+    } else {
+      for (uint32_t v = tid; v < V; v += BS) {
+        dist[v] = kInf32;
+        if constexpr (LBK) {
+          bkt[v] = 255;
+        }
+      }
+      if constexpr (WMAX > 0) {
+        for (uint32_t i = tid; i < V * Wm; i += BS) {
+          nhrow[i] = 0;
+        }
+      }
+      __syncthreads();
+      if (tid == 0) {
+        dist[src] = 0;
+        if constexpr (LBK) {
+          bkt[src] = 0;
+        }
+        pend[src >> 5] |= 1u << (src & 31);
+      }
+      __syncthreads();
     }
-    __syncthreads();
     uint32_t cur = 0;
 
     for (;;) {
@@ -637,6 +823,9 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
             continue; // overloaded: recorded but never transited
           }
           const uint32_t du = ld_coh(dist + u);
+          if (SEED && du == kInf32) {
+            continue;
+          }
           const uint32_t beg = a.row[u], end = a.row[u + 1];
           // kPushUnroll edges per lane per step: their (col, metric) loads,
           // then their distance gathers, are independent and issued together
@@ -2383,6 +2572,29 @@ std::vector<uint32_t> msd_batches(
   return perm;
 }
 
+// delta-stepping bucket width 2^shift: ~ mean metric / mean degree
+// (delta-stepping's Delta = Theta(w/d)); push-only (distance) runs 4x wider,
+// measured fastest; OPENR_SPF_DSTEP_SHIFT overrides
+uint32_t dstep_bucket_shift(const spf_graph* g, bool want_nh) {
+  uint64_t wsum = 0;
+  for (uint32_t e = 0; e < g->E; ++e) {
+    wsum += std::min<uint64_t>(g->w64[e], 0xFFFFFFFFull);
+  }
+  const double meanw = g->E ? (double)wsum / g->E : 1.0;
+  const double meandeg = g->V ? (double)g->E / g->V : 1.0;
+  uint32_t shift = 0;
+  while (shift < 20 && (double)(2u << shift) <= meanw / std::max(meandeg, 1.0)) {
+    ++shift;
+  }
+  if (!want_nh) {
+    shift += 2;
+  }
+  if (const char* env = getenv("OPENR_SPF_DSTEP_SHIFT")) {
+    shift = (uint32_t)std::min(24, std::max(0, atoi(env)));
+  }
+  return shift;
+}
+
 // bucket width for spf_msdstep_kernel: the eccentricity of one source (host
 // Dijkstra) spread over ~200 of the 255 bucket bytes; at least the
 // delta-stepping Delta ~ mean metric / mean degree.
@@ -2813,23 +3025,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       q->lds_bytes = dstep_lds;
       // bucket width ~ mean metric / mean degree (delta-stepping's
       // Delta = Theta(w/d)), a power of two; OPENR_SPF_DSTEP_SHIFT overrides
-      uint64_t wsum = 0;
-      for (uint32_t e = 0; e < g->E; ++e) {
-        wsum += std::min<uint64_t>(g->w64[e], 0xFFFFFFFFull);
-      }
-      const double meanw = g->E ? (double)wsum / g->E : 1.0;
-      const double meandeg = V ? (double)g->E / V : 1.0;
-      uint32_t shift = 0;
-      while (shift < 20 && (double)(2u << shift) <= meanw / std::max(meandeg, 1.0)) {
-        ++shift;
-      }
-      if (!want_nh) {
-        shift += 2; // push-only runs: 4x wider buckets measured fastest
-      }
-      if (const char* env = getenv("OPENR_SPF_DSTEP_SHIFT")) {
-        shift = (uint32_t)std::min(24, std::max(0, atoi(env)));
-      }
-      q->dstep_shift = shift;
+      q->dstep_shift = dstep_bucket_shift(g, want_nh);
       const char* bs_env = getenv("OPENR_SPF_DSTEP_BS");
       q->dstep_bs = (bs_env && atoi(bs_env) == 512) ? 512 : 1024;
       // workgroups per CU: 2048 threads per CU, LDS permitting
@@ -3872,6 +4068,133 @@ int spf_query_scatter_rows(
                      (char*)table, pitch, V);
   HIP_TRY(hipGetLastError());
   return SPF_OK;
+}
+
+} // extern "C"
+
+extern "C" {
+
+int spf_table_repair(
+    spf_graph* g, uint32_t* rows, size_t pitch, uint32_t num_rows,
+    const uint32_t* sources, const uint32_t* row_idx,
+    const spf_edge_delta* deltas, uint32_t n_deltas) {
+  if (!g || (num_rows && (!rows || !sources || !row_idx)) || (n_deltas && !deltas)) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  if (num_rows && pitch < g->V) {
+    return fail(SPF_E_INVALID, "row pitch < V");
+  }
+  if (g->exact) {
+    return fail(SPF_E_UNSUPPORTED, "metric 0 / 64-bit sums: rows need the exact kernel");
+  }
+  for (uint32_t i = 0; i < num_rows; ++i) {
+    if (sources[i] >= g->V) {
+      return fail(SPF_E_INVALID, "source out of range");
+    }
+  }
+  std::vector<uint32_t> seeds, rt, rh, rs;
+  std::vector<uint64_t> rw;
+  for (uint32_t j = 0; j < n_deltas; ++j) {
+    const spf_edge_delta& d = deltas[j];
+    if (d.tail >= g->V || d.head >= g->V || d.scope > SPF_SCOPE_NOT_TAIL ||
+        (d.kind != SPF_DELTA_REMOVED && d.kind != SPF_DELTA_ADDED)) {
+      return fail(SPF_E_INVALID, "bad delta " + std::to_string(j));
+    }
+    if (d.kind == SPF_DELTA_ADDED) {
+      seeds.push_back(d.tail);
+    } else {
+      rt.push_back(d.tail);
+      rh.push_back(d.head);
+      rs.push_back(d.scope);
+      rw.push_back(d.metric);
+    }
+  }
+  std::sort(seeds.begin(), seeds.end());
+  seeds.erase(std::unique(seeds.begin(), seeds.end()), seeds.end());
+  const size_t bk = ((size_t)g->V + 15) & ~(size_t)15;
+  const size_t lds = (2 * (size_t)g->nbw + kCtlWords) * 4 + bk + (size_t)g->nbw * 4;
+  if (lds > kLdsLimit) {
+    return fail(SPF_E_UNSUPPORTED, "bucket image beyond LDS");
+  }
+  if (num_rows == 0 || n_deltas == 0 || g->V == 0) {
+    return SPF_OK;
+  }
+  HIP_TRY(hipSetDevice(g->device));
+  const uint32_t nrem = (uint32_t)rt.size(), nseed = (uint32_t)seeds.size();
+  const uint32_t grid = std::min<uint32_t>(num_rows, (uint32_t)g->num_cus);
+  // u32 block: sources | row_idx | seeds | rm_tail | rm_head | rm_scope, then
+  // the u64 removed metrics, then two V-entry queues per workgroup
+  const size_t n32 = (size_t)2 * num_rows + nseed + 3 * (size_t)nrem;
+  const size_t off64 = (n32 * 4 + 7) & ~(size_t)7;
+  const size_t meta = off64 + (size_t)nrem * 8;
+  const size_t offq = (meta + 255) & ~(size_t)255;
+  const size_t bytes = offq + (size_t)grid * g->V * 8;
+  std::vector<char> h(meta);
+  uint32_t* h32 = (uint32_t*)h.data();
+  std::memcpy(h32, sources, (size_t)num_rows * 4);
+  std::memcpy(h32 + num_rows, row_idx, (size_t)num_rows * 4);
+  size_t o = 2 * (size_t)num_rows;
+  for (auto* v : {&seeds, &rt, &rh, &rs}) {
+    if (!v->empty()) {
+      std::memcpy(h32 + o, v->data(), v->size() * 4);
+    }
+    o += v->size();
+  }
+  if (nrem) {
+    std::memcpy(h.data() + off64, rw.data(), (size_t)nrem * 8);
+  }
+  char* d = nullptr;
+  HIP_TRY(hipMalloc((void**)&d, bytes));
+  int st = SPF_OK;
+  if (hipMemcpyAsync(d, h.data(), meta, hipMemcpyHostToDevice, g->stream) != hipSuccess) {
+    st = fail(SPF_E_DEVICE, "delta upload failed");
+  }
+  if (st == SPF_OK) {
+    const uint32_t* d32 = (const uint32_t*)d;
+    DstepArgs da;
+    SsspArgs& a = da.s;
+    std::memset(&a, 0, sizeof(a));
+    a.row = g->d_row;
+    a.col = g->d_col;
+    a.wout = g->d_wout;
+    a.win = g->d_win;
+    a.link = g->d_link;
+    a.rev = g->d_rev;
+    a.slot = g->d_slot;
+    a.trbits = g->d_tr;
+    a.src = d32;
+    a.gscratch = (uint32_t*)(d + offq);
+    a.V = g->V;
+    a.Vp = (uint32_t)std::min<size_t>(pitch, 0xFFFFFFFFu);
+    a.nbw = g->nbw;
+    a.nq = num_rows;
+    a.G = 8;
+    da.shift = dstep_bucket_shift(g, false);
+    da.table = rows;
+    da.pitch = pitch;
+    da.row_idx = d32 + num_rows;
+    da.seed = d32 + 2 * (size_t)num_rows;
+    da.nseed = nseed;
+    da.rm_tail = da.seed + nseed;
+    da.rm_head = da.rm_tail + nrem;
+    da.rm_scope = da.rm_head + nrem;
+    da.rm_w = (const uint64_t*)(d + off64);
+    da.nrem = nrem;
+    da.gscratch2 = a.gscratch + (size_t)grid * g->V;
+    auto kern = spf_dstep_kernel<0, false, 1024, true, true>;
+    if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess) {
+      st = fail(SPF_E_DEVICE, "LDS attribute");
+    } else {
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), lds, g->stream, da);
+      if (hipGetLastError() != hipSuccess || hipStreamSynchronize(g->stream) != hipSuccess) {
+        st = fail(SPF_E_DEVICE, "repair kernel failed");
+      }
+    }
+  }
+  (void)hipStreamSynchronize(g->stream);
+  (void)hipFree(d);
+  return st;
 }
 
 } // extern "C"

@@ -14,9 +14,14 @@ CPU ("not gpu"):
     has the same distances AND next-hop sets before and after, by the
     literal DijkstraQ replay (oracle/spf_py.py);
   * exchange_rows (repaired rows to the other ranks) over gloo, world 2 / 3.
-GPU: ShardedAllSources.update() (diff + screen kernel + partial recompute +
-scatter kernel) equals a full recompute bit for bit, on the frontier (LDS),
-delta-stepping (beyond LDS) and MS-BFS (uniform metric) plans.
+  * the in-place repair RULE of spf_table_repair (reset the nodes that lost
+    every supporting tight path, relax from the reset boundary and the
+    improved edges; restated in Python below) gives the new distances of
+    every source exactly.
+GPU: ShardedAllSources.update() — diff + screen kernel + in-place repair
+kernel (or, forced, recompute of the affected sources + scatter kernel) —
+equals a full recompute bit for bit, on the frontier (LDS), delta-stepping
+(beyond LDS) and MS-BFS (uniform metric) plans.
 """
 
 import os
@@ -169,6 +174,100 @@ def test_screen_rule_is_exact(seed):
     assert kept > total // 10  # the screen does skip work
 
 
+def _repair_py(row, csr, src, deltas):
+    """Test-only restatement of spf_table_repair's rule for one row (the
+    seeded spf_dstep_kernel with its repair_invalidate prologue): returns
+    the repaired row (uint64, INF = unreached)."""
+    import heapq
+
+    d = [int(x) for x in row]
+    V = csr.num_nodes
+    rp, col, met, rev = csr.row_ptr, csr.col, csr.metric, csr.rev
+    ov = csr.overloaded
+
+    def usable(u):
+        return u == src or not ov[u]
+
+    K = set()
+    for x in deltas:
+        u, v, w, kind, sc = (int(x[k]) for k in ("tail", "head", "metric", "kind", "scope"))
+        if kind != abi.SPF_DELTA_REMOVED:
+            continue
+        if (sc == abi.SPF_SCOPE_TAIL_ONLY and src != u) or (sc == abi.SPF_SCOPE_NOT_TAIL and src == u):
+            continue
+        if d[u] != INF and d[v] != INF and d[u] + w == d[v]:
+            K.add(v)
+    stack = list(K)
+    while stack:
+        x = stack.pop()
+        if not usable(x):
+            continue
+        for e in range(rp[x], rp[x + 1]):
+            z = int(col[e])
+            if d[z] != INF and d[x] + int(met[e]) == d[z] and z not in K:
+                K.add(z)
+                stack.append(z)
+    ok = set()
+    for x in K:
+        for e in range(rp[x], rp[x + 1]):
+            y = int(col[e])
+            if y not in K and usable(y) and d[y] != INF and d[y] + int(met[rev[e]]) == d[x]:
+                ok.add(x)
+    stack = list(ok)
+    while stack:
+        x = stack.pop()
+        if not usable(x):
+            continue
+        for e in range(rp[x], rp[x + 1]):
+            z = int(col[e])
+            if z in K and z not in ok and d[x] + int(met[e]) == d[z]:
+                ok.add(z)
+                stack.append(z)
+    reset = K - ok
+    for x in reset:
+        d[x] = INF
+    seeds = {int(x["tail"]) for x in deltas if int(x["kind"]) == abi.SPF_DELTA_ADDED}
+    for x in reset:
+        for e in range(rp[x], rp[x + 1]):
+            y = int(col[e])
+            if y not in reset:
+                seeds.add(y)
+    pq = [(d[u], u) for u in seeds if d[u] != INF]
+    heapq.heapify(pq)
+    while pq:  # label-correcting relaxation from the seeds
+        du, u = heapq.heappop(pq)
+        if du != d[u] or not usable(u):
+            continue
+        for e in range(rp[u], rp[u + 1]):
+            v = int(col[e])
+            c = du + int(met[e])
+            if c < d[v]:
+                d[v] = c
+                heapq.heappush(pq, (c, v))
+    return d
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_repair_rule_is_exact(seed):
+    """The in-place repair rule reproduces the new distances exactly, for
+    every source, under every kind of churn (replay oracle)."""
+    rng = random.Random(seed)
+    for trial in range(10):
+        V = 40
+        links = _random_links(V, 90, rng, wmax=5)
+        ov = np.array([rng.random() < 0.1 for _ in range(V)], dtype=np.uint8)
+        kinds = [rng.choice(["down", "up", "metric_up", "metric_down", "drain"])
+                 for _ in range(rng.choice([1, 1, 2, 5]))]
+        links2, ov2 = _churn(V, links, ov, rng, kinds, wmax=5)
+        a = abi.Csr.from_links(V, links, ov)
+        b = abi.Csr.from_links(V, links2, ov2)
+        deltas = abi.graph_diff(a, b)
+        D0, _ = _rows(a, range(V))
+        D1, _ = _rows(b, range(V))
+        for s in range(V):
+            assert _repair_py(D0[s], b, s, deltas) == [int(x) for x in D1[s]], (trial, kinds, s)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -244,12 +343,16 @@ def _full_table(csr, srcs):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["repair", "recompute"])
 @pytest.mark.parametrize(
     "V,L,wmax,nsrc,expect_kernel",
     [(3000, 12000, 50, 3000, None), (40000, 160000, 1000, 400, "dstep"), (2500, 9000, 1, 2500, None)],
 )
-def test_repair_equals_full_recompute(gpu_ready, V, L, wmax, nsrc, expect_kernel):
+def test_repair_equals_full_recompute(gpu_ready, V, L, wmax, nsrc, expect_kernel, mode, monkeypatch):
     import torch
+
+    if mode == "recompute":
+        monkeypatch.setenv("OPENR_SPF_REPAIR_RECOMPUTE", "1")
 
     rng = random.Random(V + L)
     links = _random_links(V, L, rng, wmax=wmax)
@@ -263,16 +366,19 @@ def test_repair_equals_full_recompute(gpu_ready, V, L, wmax, nsrc, expect_kernel
     sas.run()
     plan = [["down"], ["up"], ["metric_up"], ["metric_down"], ["drain"], ["drain"],
             ["down", "down", "up", "metric_down", "drain"], []]
-    affected = []
+    affected, relaxed = [], []
     for kinds in plan:
         links, ov = _churn(V, links, ov, rng, kinds, wmax=wmax)
         csr = abi.Csr.from_links(V, links, ov)
         rep = sas.update(csr)
         affected.append(rep.affected)
+        relaxed.append(rep.relaxed)
         got = sas.table.cpu().numpy().view(np.uint32)[: len(srcs)]
         assert (got == _full_table(csr, srcs)).all(), kinds
     assert affected[-1] == 0  # no change: nothing recomputed
     assert min(affected[:-1]) < len(srcs)  # the screen skips sources
+    # rows repaired in place (spf_table_repair) unless recompute is forced
+    assert all(r == (mode == "repair") for r, n in zip(relaxed, affected) if n)
     # a full run after repairs still works (the batch query is rebuilt)
     sas.run()
     assert (sas.table.cpu().numpy().view(np.uint32)[: len(srcs)] == _full_table(csr, srcs)).all()

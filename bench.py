@@ -191,7 +191,8 @@ def _rebuild_loop(M, topo, iters, timed, fwd=(0, 0)):
     out = {"ms_median": med(tot), "update_ms_median": med(upd),
            "build_ms_median": med(bld), "routes": routes, "samples": len(tot)}
     if rel:
-        out["release_ms_median"] = med(rel)  # freeing the RouteDb (in ms_median)
+        # freeing the old RouteDb (releaseRouteDb, in ms_median)
+        out["release_ms_median"] = med(rel)
     return out
 
 

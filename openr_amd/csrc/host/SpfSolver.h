@@ -87,7 +87,7 @@ struct DecisionRouteUpdate {
 // Drop a RouteDb with its payload freed on the host worker pool: the
 // Decision thread replaces its RouteDb on every rebuild (Decision.cpp:
 // 1803-1804) and freeing ~10^5 next hops one by one costs more than the
-// build itself on the fabric.
+// build itself on the fabric (time exported as decision.route_release_us).
 void releaseRouteDb(DecisionRouteDb&& db);
 
 // old vs new RouteDb -> delta (reference: Decision.cpp:47-85)

@@ -223,6 +223,67 @@ def route_db_rebuild_ms(topo, device, iters=5):
     return out
 
 
+def all_nodes_route_table(topo, device, reps=3):
+    """the unicast RouteDb of EVERY fabric node at once
+    (AllNodesRouteTable: one all-sources SPF with next hops + the
+    spf_route_table_kernel over all 9,976 prefixes), against one
+    buildRouteDb per node on the host path.  Parity: three nodes' table rows
+    equal their buildRouteDb unicast entries."""
+    import numpy as np
+
+    import openr_amd._openr_spf as E
+
+    E.set_spf_device(device)
+    areas = E.AreaLinkStates()
+    ls = areas.add("0")
+    for db in topo.adj_dbs():
+        ls.updateAdjacencyDatabase(db)
+    ps = E.PrefixState()
+    for pdb in topo.prefix_dbs("0"):
+        ps.updatePrefixDatabase(pdb)
+    E.AllNodesRouteTable(areas, "0", ps, True)  # warm (kernels, allocations)
+    walls, spf, rt = [], [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        table = E.AllNodesRouteTable(areas, "0", ps, True)
+        walls.append((time.perf_counter() - t0) * 1e3)
+        spf.append(table.spf_ms)
+        rt.append(table.route_ms)
+    V, P = table.num_nodes, table.num_prefixes
+    routes = table.count_routes()
+    solver = E.SpfSolver("2-0-0", True, False)
+    names = sorted(topo.names)
+    bad = 0
+    for node in ("2-0-0", names[len(names) // 2], names[-1]):
+        if table.routes(node) != solver.buildRouteDb(node, areas, ps)["unicast"]:
+            bad += 1
+    n_mat, us_mat = table.routes_timed("2-0-0")
+    # algorithmic bytes of spf_route_table_kernel per launch: per (node,
+    # prefix) cell the metric + best words written, the link mask written
+    # (8 B x link words of the node), the announcer's distance read and its
+    # next-hop mask word(s) read (8 B x mask words of the node)
+    csr = topo.csr()
+    deg = np.diff(csr.row_ptr.astype(np.int64))
+    lw = (deg + 63) // 64
+    nbr = np.array([len(set(csr.col[csr.row_ptr[u]:csr.row_ptr[u + 1]].tolist())) for u in range(V)])
+    nw = np.maximum(1, (nbr + 63) // 64)
+    alg = int(P * (12 * V + 8 * int(lw.sum()) + 8 * int(nw.sum())))
+    med = lambda x: sorted(x)[len(x) // 2]  # noqa: E731
+    k_ms = med(rt)
+    return {
+        "what": "unicast RouteDb of every node of the fabric at once: AllNodesRouteTable = all-sources "
+                "SPF + next hops, then spf_route_table_kernel (selectEcmpOpenr per node x prefix)",
+        "nodes": V, "prefixes": P, "routes": int(routes),
+        "build_ms_median": round(med(walls), 2), "spf_ms_median": round(med(spf), 3),
+        "route_kernel_ms_median": round(k_ms, 3),
+        "route_kernel_roofline": {"bound": "hbm", "algorithmic_bytes": alg,
+                                  "achieved": round(alg / (k_ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                                  "unit": "GB/s", "frac": round(alg / (k_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
+        "materialise_one_node_ms": round(us_mat / 1e3, 3), "materialised_routes": n_mat,
+        "parity_check": "ok" if bad == 0 else f"{bad} nodes differ",
+    }
+
+
 def ksp2_route_db(topo, device, iters=2):
     """BASELINE configs[3]: every fabric prefix SR_MPLS / KSP2_ED_ECMP, the
     RouteDb of "2-0-0" after an RSW overload toggle.  Each build traces the
@@ -803,6 +864,10 @@ def main():
             out["route_db_rebuild"] = route_db_rebuild_ms(topo, local)
         except Exception as e:  # reported, never silently replaced
             out["route_db_rebuild"] = {"error": repr(e)}
+        try:
+            out["all_nodes_route_table"] = all_nodes_route_table(topo, local)
+        except Exception as e:
+            out["all_nodes_route_table"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(topo, args.cpu_sample)
         try:

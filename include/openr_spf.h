@@ -237,6 +237,36 @@ int spf_table_repair(
 int spf_query_scatter_rows(
     spf_query* q, const uint32_t* dst_rows, void* table, size_t pitch);
 
+/* ---- all-nodes unicast route tables ----
+ * The RouteDb of EVERY node of an area from one all-sources query, on the
+ * device: for query row i (node s) and prefix p, Open/R's ECMP selection
+ * (SpfSolverImpl::selectEcmpOpenr, Decision.cpp:668-712 with
+ * getBestAnnouncingNodes :544-630, maybeFilterDrainedNodes :651-666,
+ * getNextHopsWithMetric :1093-1179, getNextHopsThrift :1181-1271; one area,
+ * LFA off, not per destination — the reference runs it per node in
+ * buildRouteDb :291-542).  Output per (i, p): metric (UINT32_MAX = no route:
+ * s announces p or no announcer is reachable), best (the smallest reachable
+ * announcer: bestPrefixEntry's node) and a link mask over s's up links (bit
+ * j = the j-th half-edge of s's CSR row, i.e. linksFromNode order): the
+ * next hops of the route, each with metric `metric`. */
+typedef struct spf_route_table spf_route_table;
+/* `q` must be a metric query (no SPF_F_UNIT_METRIC) with SPF_F_NEXTHOPS and
+ * no ignore lists; prefix p is announced by announcers[ann_offsets[p] ..
+ * ann_offsets[p+1]) (node ids). */
+int spf_route_table_create(
+    spf_query* q, uint32_t num_prefixes, const uint32_t* ann_offsets,
+    const uint32_t* announcers, spf_route_table** out);
+int spf_route_table_destroy(spf_route_table* t);
+/* Enqueue spf_route_table_kernel after the query's last run (asynchronous,
+ * graph stream). */
+int spf_route_table_run(spf_route_table* t);
+int spf_route_table_elapsed_ms(spf_route_table* t, float* ms);
+/* Link-mask words per prefix of row i (ceil(up links of s / 64)). */
+int spf_route_table_link_words(const spf_route_table* t, uint32_t i);
+/* Row i to host: metric[P], best[P], links[P * link_words(i)]. */
+int spf_route_table_fetch(
+    spf_route_table* t, uint32_t i, uint32_t* metric, uint32_t* best, uint64_t* links);
+
 #ifdef __cplusplus
 }
 #endif

@@ -59,6 +59,12 @@ EXPORTED_SYMBOLS = (
     "spf_table_screen",
     "spf_query_scatter_rows",
     "spf_table_repair",
+    "spf_route_table_create",
+    "spf_route_table_destroy",
+    "spf_route_table_run",
+    "spf_route_table_elapsed_ms",
+    "spf_route_table_link_words",
+    "spf_route_table_fetch",
 )
 
 SPF_DELTA_REMOVED = 1

@@ -9,6 +9,7 @@
 // name ranks and whose rows list links in linksFromNode() iteration order.
 
 #include "LinkState.h"
+#include "Engine.h"
 
 #include <chrono>
 #include <map>
@@ -304,36 +305,7 @@ std::string Link::directionalToString(const std::string& fromNode) const {
 
 // ------------------------------------------------------------------ engine
 
-struct LinkState::Engine {
-  bool built{false};
-  std::vector<std::string> names; // id -> name, ascending
-  std::unordered_map<std::string, uint32_t> ids;
-  std::vector<uint32_t> row, col, linkId, rev;
-  std::vector<uint64_t> metric;
-  std::vector<uint8_t> overloaded;
-  std::vector<std::shared_ptr<Link>> links; // link id -> Link
-  std::unordered_map<const Link*, uint32_t> linkIndex;
-  std::vector<std::array<uint32_t, 2>> halves; // link id -> half-edge from first/second node
-  spf_graph* graph{nullptr};
-  bool exact{false};
-  float lastMs{0};
-  std::unordered_map<uint32_t, std::unique_ptr<SpfView>> memo[2];
-  std::unordered_map<uint32_t, std::unique_ptr<SpfView>> prefetched[2];
-  std::map<std::pair<uint32_t, uint32_t>, std::unique_ptr<SpfView>> kthPrefetch;
-  std::unordered_map<std::string, std::unique_ptr<SpfView>> isolated;
-  // spfView may be called from the RouteDb worker threads of one build:
-  // memo hits take viewMu shared, fills (and kthPrefetch) exclusive; every
-  // device call of this graph is serialised by devMu (the C ABI is
-  // single-threaded per graph)
-  std::shared_mutex viewMu;
-  std::mutex devMu;
-
-  ~Engine() {
-    if (graph) {
-      spf_graph_destroy(graph);
-    }
-  }
-};
+// struct LinkState::Engine: Engine.h (shared with RouteTable.cpp)
 
 namespace {
 

@@ -318,7 +318,8 @@ class LinkState {
   // release the device graph and every memoized result
   void invalidate() const;
 
-  struct Engine; // device graph + flat memo (LinkState.cpp)
+  struct Engine; // device graph + flat memo (Engine.h)
+  friend class AllNodesRouteTable; // reads the device graph (RouteTable.h)
 
  private:
   void clearMemo() const;

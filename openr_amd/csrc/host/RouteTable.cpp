@@ -1,0 +1,226 @@
+// RouteTable.cpp — AllNodesRouteTable (see RouteTable.h).
+
+#include "RouteTable.h"
+
+#include <algorithm>
+#include <stdexcept>
+
+#include "Engine.h"
+#include "Util.h"
+
+namespace openr {
+
+namespace {
+[[noreturn]] void tableFailure(const char* what, int status) {
+  throw std::runtime_error(
+      std::string("openr_spf: ") + what + ": " + spf_error_string(status) + " (" +
+      spf_last_error_detail() + ")");
+}
+} // namespace
+
+AllNodesRouteTable::AllNodesRouteTable(
+    const LinkState& ls, const PrefixState& ps, bool enableV4)
+    : area_(ls.getArea()), enableV4_(enableV4) {
+  LinkState::Engine& eng = ls.engine();
+  if (eng.exact) {
+    throw std::invalid_argument(
+        "AllNodesRouteTable: metric 0 / 64-bit sums need the exact kernel");
+  }
+  names_ = eng.names;
+  ids_ = eng.ids;
+  row_ = eng.row;
+  halfLink_.resize(eng.col.size());
+  for (size_t e = 0; e < eng.col.size(); ++e) {
+    halfLink_[e] = eng.links[eng.linkId[e]];
+  }
+  // eligible prefixes (Decision.cpp:313-412 restricted to selectEcmpOpenr)
+  std::vector<uint32_t> annOff{0}, ann;
+  for (const auto& [prefix, entries] : ps.prefixes()) {
+    bool otherArea = false, bgp = false;
+    for (const auto& [node, byArea] : entries) {
+      for (const auto& [area, entry] : byArea) {
+        otherArea |= area != area_;
+        bgp |= entry.type == thrift::PrefixType::BGP;
+      }
+    }
+    if (otherArea || bgp || entries.empty()) {
+      continue;
+    }
+    if (prefix.prefixAddress.addr.size() == 4 && !enableV4_) {
+      continue;
+    }
+    if (getPrefixForwardingType(entries) != thrift::PrefixForwardingType::IP ||
+        getPrefixForwardingAlgorithm(entries) != thrift::PrefixForwardingAlgorithm::SP_ECMP) {
+      continue;
+    }
+    std::vector<Announcer> as;
+    for (const auto& [node, byArea] : entries) {
+      auto it = ids_.find(node);
+      if (it == ids_.end()) {
+        continue; // not in the graph: never reachable
+      }
+      as.push_back(Announcer{it->second, byArea.at(area_)});
+    }
+    prefixes_.push_back(prefix);
+    announcers_.push_back(std::move(as));
+  }
+  // prefix order: by first announcer id, so neighbouring lanes of the
+  // kernel read neighbouring distance / next-hop mask words of a row
+  {
+    std::vector<uint32_t> order(prefixes_.size());
+    for (uint32_t i = 0; i < order.size(); ++i) {
+      order[i] = i;
+    }
+    auto key = [&](uint32_t i) {
+      return announcers_[i].empty() ? 0xFFFFFFFFu : announcers_[i][0].id;
+    };
+    std::stable_sort(order.begin(), order.end(),
+                     [&](uint32_t x, uint32_t y) { return key(x) < key(y); });
+    std::vector<thrift::IpPrefix> px;
+    std::vector<std::vector<Announcer>> ax;
+    px.reserve(order.size());
+    ax.reserve(order.size());
+    for (uint32_t i : order) {
+      px.push_back(std::move(prefixes_[i]));
+      ax.push_back(std::move(announcers_[i]));
+    }
+    prefixes_ = std::move(px);
+    announcers_ = std::move(ax);
+    for (const auto& as : announcers_) {
+      for (const auto& a : as) {
+        ann.push_back(a.id);
+      }
+      annOff.push_back((uint32_t)ann.size());
+    }
+  }
+  // own snapshot of the device graph: the table outlives LinkState changes
+  spf_graph_desc d{};
+  d.num_nodes = (uint32_t)eng.names.size();
+  d.num_edges = (uint32_t)eng.col.size();
+  d.row_ptr = eng.row.data();
+  d.col = eng.col.data();
+  d.metric = eng.metric.data();
+  d.link_id = eng.linkId.data();
+  d.rev = eng.rev.data();
+  d.node_overloaded = eng.overloaded.data();
+  d.num_links = (uint32_t)eng.links.size();
+  d.device = getSpfDevice();
+  if (int s = spf_graph_create(&d, &graph_); s != SPF_OK) {
+    tableFailure("spf_graph_create", s);
+  }
+  std::vector<uint32_t> src(d.num_nodes);
+  for (uint32_t i = 0; i < d.num_nodes; ++i) {
+    src[i] = i;
+  }
+  spf_query_desc qd{};
+  qd.num_queries = d.num_nodes;
+  qd.sources = src.data();
+  qd.flags = SPF_F_NEXTHOPS;
+  int s = SPF_OK;
+  if ((s = spf_query_create(graph_, &qd, &query_)) != SPF_OK) {
+    spf_graph_destroy(graph_);
+    tableFailure("spf_query_create", s);
+  }
+  auto cleanup = [&](const char* what, int st) {
+    spf_route_table_destroy(table_);
+    spf_query_destroy(query_);
+    spf_graph_destroy(graph_);
+    table_ = nullptr;
+    query_ = nullptr;
+    graph_ = nullptr;
+    tableFailure(what, st);
+  };
+  if ((s = spf_query_run(query_)) != SPF_OK) {
+    cleanup("spf_query_run", s);
+  }
+  if ((s = spf_route_table_create(
+           query_, (uint32_t)prefixes_.size(), annOff.data(), ann.empty() ? nullptr : ann.data(),
+           &table_)) != SPF_OK) {
+    cleanup("spf_route_table_create", s);
+  }
+  if ((s = spf_route_table_run(table_)) != SPF_OK) {
+    cleanup("spf_route_table_run", s);
+  }
+  if ((s = spf_query_elapsed_ms(query_, &spfMs_)) != SPF_OK ||
+      (s = spf_route_table_elapsed_ms(table_, &routeMs_)) != SPF_OK) {
+    cleanup("elapsed", s);
+  }
+  Counters::add("decision.route_table_builds", 1);
+}
+
+AllNodesRouteTable::~AllNodesRouteTable() {
+  spf_route_table_destroy(table_);
+  spf_query_destroy(query_);
+  spf_graph_destroy(graph_);
+}
+
+uint64_t AllNodesRouteTable::countRoutes() const {
+  uint64_t n = 0;
+  std::vector<uint32_t> metric(prefixes_.size()), best(prefixes_.size());
+  std::vector<uint64_t> links;
+  for (uint32_t i = 0; i < names_.size(); ++i) {
+    const int w = spf_route_table_link_words(table_, i);
+    links.resize(std::max<size_t>(1, prefixes_.size() * (size_t)std::max(w, 0)));
+    if (int s = spf_route_table_fetch(table_, i, metric.data(), best.data(), links.data());
+        s != SPF_OK) {
+      tableFailure("spf_route_table_fetch", s);
+    }
+    for (uint32_t m : metric) {
+      n += m != 0xFFFFFFFFu;
+    }
+  }
+  return n;
+}
+
+std::unordered_map<thrift::IpPrefix, RibUnicastEntry> AllNodesRouteTable::routes(
+    const std::string& node) const {
+  std::unordered_map<thrift::IpPrefix, RibUnicastEntry> out;
+  auto it = ids_.find(node);
+  if (it == ids_.end() || prefixes_.empty()) {
+    return out;
+  }
+  const uint32_t i = it->second;
+  const int w = spf_route_table_link_words(table_, i);
+  if (w < 0) {
+    tableFailure("spf_route_table_link_words", w);
+  }
+  const size_t P = prefixes_.size(), W = (size_t)w;
+  std::vector<uint32_t> metric(P), best(P);
+  std::vector<uint64_t> links(std::max<size_t>(1, P * W));
+  if (int s = spf_route_table_fetch(table_, i, metric.data(), best.data(), links.data());
+      s != SPF_OK) {
+    tableFailure("spf_route_table_fetch", s);
+  }
+  const uint32_t e0 = row_[i];
+  for (size_t p = 0; p < P; ++p) {
+    if (metric[p] == 0xFFFFFFFFu) {
+      continue;
+    }
+    const bool isV4 = prefixes_[p].prefixAddress.addr.size() == 4;
+    std::unordered_set<thrift::NextHopThrift> nhs;
+    for (size_t k = 0; k < W; ++k) {
+      uint64_t m = links[p * W + k];
+      while (m) {
+        const uint32_t j = (uint32_t)(k * 64 + __builtin_ctzll(m));
+        m &= m - 1;
+        const Link& l = *halfLink_[e0 + j];
+        nhs.insert(createNextHop(
+            isV4 ? l.getNhV4FromNode(node) : l.getNhV6FromNode(node), l.getIfaceFromNode(node),
+            (int32_t)metric[p], std::nullopt, false, l.getArea()));
+      }
+    }
+    const thrift::PrefixEntry* bestEntry = nullptr;
+    for (const auto& a : announcers_[p]) {
+      if (a.id == best[p]) {
+        bestEntry = &a.entry;
+      }
+    }
+    if (!bestEntry) {
+      throw std::logic_error("AllNodesRouteTable: best announcer not in the prefix");
+    }
+    out.emplace(prefixes_[p], RibUnicastEntry(prefixes_[p], std::move(nhs), *bestEntry, area_));
+  }
+  return out;
+}
+
+} // namespace openr

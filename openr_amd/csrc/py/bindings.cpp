@@ -11,6 +11,7 @@
 
 #include "../host/LinkState.h"
 #include "../host/PrefixState.h"
+#include "../host/RouteTable.h"
 #include "../host/SpfSolver.h"
 #include "../host/Util.h"
 #include "convert.h"
@@ -191,6 +192,35 @@ PYBIND11_MODULE(_openr_spf, m) {
              return out;
            })
       .def("__len__", [](const AreaMapHolder& am) { return am.map.size(); });
+
+  py::class_<AllNodesRouteTable>(m, "AllNodesRouteTable")
+      .def(py::init([](const AreaMapHolder& areas, const std::string& area, const PrefixState& ps,
+                       bool enableV4) {
+             return std::make_unique<AllNodesRouteTable>(areas.map.at(area), ps, enableV4);
+           }),
+           py::arg("areas"), py::arg("area"), py::arg("prefix_state"), py::arg("enable_v4") = true,
+           py::keep_alive<1, 2>())
+      .def_property_readonly("num_nodes", &AllNodesRouteTable::numNodes)
+      .def_property_readonly("num_prefixes", &AllNodesRouteTable::numPrefixes)
+      .def_property_readonly("spf_ms", &AllNodesRouteTable::spfMs)
+      .def_property_readonly("route_ms", &AllNodesRouteTable::routeMs)
+      .def("count_routes", &AllNodesRouteTable::countRoutes)
+      .def("routes", [](const AllNodesRouteTable& t, const std::string& node) {
+        DecisionRouteDb db;
+        db.unicastEntries = t.routes(node);
+        py::dict all = routeDbToPy(db);
+        py::object unicast = all["unicast"]; // owned before `all` goes away
+        return unicast;
+      })
+      .def("routes_timed", [](const AllNodesRouteTable& t, const std::string& node) {
+        // fetch + materialise the node's routes in C++, no Python conversion
+        const auto t0 = std::chrono::steady_clock::now();
+        auto r = t.routes(node);
+        const double us = std::chrono::duration<double, std::micro>(
+                              std::chrono::steady_clock::now() - t0)
+                              .count();
+        return py::make_tuple((long)r.size(), us);
+      });
 
   py::class_<PrefixState>(m, "PrefixState")
       .def(py::init<>())

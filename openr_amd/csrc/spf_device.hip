@@ -2266,6 +2266,169 @@ __global__ __launch_bounds__(256) void spf_scatter_rows_kernel(
   }
 }
 
+// All-nodes unicast route table (spf_route_table_run): for source row q
+// (node s) and prefix p, the reference's Open/R ECMP route selection
+// (SpfSolverImpl::selectEcmpOpenr, Decision.cpp:668-712, with
+// getBestAnnouncingNodes :544-630, maybeFilterDrainedNodes :651-666,
+// getNextHopsWithMetric :1093-1179 and getNextHopsThrift :1181-1271, one
+// area, LFA off, not per destination):
+//   no route if s announces p, or no announcer is reachable;
+//   best  = smallest reachable announcer (bestPrefixEntry's node);
+//   drop drained (overloaded) announcers unless all reachable ones are;
+//   min   = min d(s, a) over the rest; NH = OR of the next-hop masks of s at
+//           every announcer at distance min;
+//   links = up links l of s to a neighbour in NH whose metric(l) + min -
+//           d(s, nbr) == min, i.e. metric(l) == d(s, nbr) — bit j = the j-th
+//           half-edge of s's CSR row (linksFromNode order).
+// One workgroup per source row, one lane per prefix; the source's out-edges
+// (neighbour, metric, slot) are staged in LDS.
+constexpr uint32_t kRtStage = 1024;
+constexpr uint32_t kRtMaskWords = 4; // register fast path: sources with <= 256 neighbours
+struct RouteTableArgs {
+  const uint32_t* row;
+  const uint32_t* col;
+  const uint32_t* wout;
+  const uint32_t* slot;
+  const uint32_t* trbits;
+  const uint32_t* src;
+  const uint32_t* dist; // query rows, stride Vp
+  const uint64_t* nh;
+  const uint64_t* nh_off;
+  const uint32_t* nh_w;
+  const uint32_t* ann_off; // [P+1]
+  const uint32_t* ann;
+  const uint64_t* lk_off; // per query: first link-mask word
+  uint32_t* metric_out; // [nq][P]
+  uint32_t* best_out;   // [nq][P]
+  uint64_t* link_out;
+  uint32_t Vp, P, nq;
+};
+
+__global__ __launch_bounds__(256) void spf_route_table_kernel(RouteTableArgs a) {
+  __shared__ uint32_t st_nbr[kRtStage];
+  __shared__ uint32_t st_w[kRtStage];
+  __shared__ uint32_t st_slot[kRtStage];
+  for (uint32_t q = blockIdx.x; q < a.nq; q += gridDim.x) {
+    const uint32_t s = a.src[q];
+    const uint32_t* d = a.dist + (size_t)q * a.Vp;
+    const uint64_t* nhq = a.nh + a.nh_off[q];
+    const uint32_t W = a.nh_w[q];
+    const uint32_t e0 = a.row[s], deg = a.row[s + 1] - e0;
+    const uint32_t WL = (deg + 63) / 64;
+    uint64_t* lk = a.link_out + a.lk_off[q];
+    const bool staged = deg <= kRtStage;
+    __syncthreads();
+    if (staged) {
+      for (uint32_t j = threadIdx.x; j < deg; j += blockDim.x) {
+        const uint32_t nb = a.col[e0 + j];
+        // a link is a shortest-path link iff metric(l) == d(s, nbr): keep
+        // the slot only for those (others can never be selected)
+        st_nbr[j] = nb;
+        st_w[j] = a.wout[e0 + j];
+        st_slot[j] = a.wout[e0 + j] == d[nb] ? a.slot[e0 + j] : kInf32;
+      }
+    }
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < a.P; p += blockDim.x) {
+      const uint32_t lo = a.ann_off[p], hi = a.ann_off[p + 1];
+      bool self = false;
+      uint32_t best = kInf32, reach = 0, undrained = 0;
+      for (uint32_t i = lo; i < hi; ++i) {
+        const uint32_t x = a.ann[i];
+        self |= x == s;
+        if (d[x] == kInf32) {
+          continue;
+        }
+        best = min(best, x);
+        ++reach;
+        undrained += (a.trbits[x >> 5] >> (x & 31)) & 1u;
+      }
+      const size_t o = (size_t)q * a.P + p;
+      uint64_t* lkp = lk + (size_t)p * WL;
+      if (self || reach == 0) {
+        a.metric_out[o] = kInf32;
+        a.best_out[o] = kInf32;
+        for (uint32_t k = 0; k < WL; ++k) {
+          lkp[k] = 0;
+        }
+        continue;
+      }
+      const bool filt = undrained > 0;
+      uint32_t mn = kInf32;
+      for (uint32_t i = lo; i < hi; ++i) {
+        const uint32_t x = a.ann[i];
+        if (d[x] != kInf32 && (!filt || ((a.trbits[x >> 5] >> (x & 31)) & 1u))) {
+          mn = min(mn, d[x]);
+        }
+      }
+      a.metric_out[o] = mn;
+      a.best_out[o] = best;
+      if (staged && W <= kRtMaskWords) {
+        // OR of the next-hop masks of the min-cost announcers (registers),
+        // then slot -> link bits through the staged row (LDS broadcast)
+        uint64_t m[kRtMaskWords];
+#pragma unroll
+        for (uint32_t k = 0; k < kRtMaskWords; ++k) {
+          m[k] = 0;
+        }
+        for (uint32_t i = lo; i < hi; ++i) {
+          const uint32_t x = a.ann[i];
+          if (d[x] == mn && (!filt || ((a.trbits[x >> 5] >> (x & 31)) & 1u))) {
+            const uint64_t* mx = nhq + (size_t)x * W;
+#pragma unroll
+            for (uint32_t k = 0; k < kRtMaskWords; ++k) {
+              if (k < W) {
+                m[k] |= mx[k];
+              }
+            }
+          }
+        }
+        for (uint32_t k = 0; k < WL; ++k) {
+          uint64_t out = 0;
+          const uint32_t j1 = min(deg, 64 * k + 64);
+          for (uint32_t j = 64 * k; j < j1; ++j) {
+            const uint32_t sl = st_slot[j];
+            uint64_t w = 0;
+#pragma unroll
+            for (uint32_t kk = 0; kk < kRtMaskWords; ++kk) {
+              w = (sl >> 6) == kk ? m[kk] : w;
+            }
+            out |= (sl == kInf32 ? 0ull : (w >> (sl & 63)) & 1ull) << (j & 63);
+          }
+          lkp[k] = out;
+        }
+        continue;
+      }
+      // general path (high-degree source): word by word from HBM
+      for (uint32_t k = 0; k < WL; ++k) {
+        uint64_t out = 0;
+        const uint32_t j1 = min(deg, 64 * k + 64);
+        for (uint32_t j = 64 * k; j < j1; ++j) {
+          uint32_t sl;
+          if (staged) {
+            sl = st_slot[j];
+          } else {
+            const uint32_t nb = a.col[e0 + j];
+            sl = a.wout[e0 + j] == d[nb] ? a.slot[e0 + j] : kInf32;
+          }
+          if (sl == kInf32) {
+            continue;
+          }
+          uint64_t mm = 0;
+          for (uint32_t i = lo; i < hi && !mm; ++i) {
+            const uint32_t x = a.ann[i];
+            if (d[x] == mn && (!filt || ((a.trbits[x >> 5] >> (x & 31)) & 1u))) {
+              mm = (nhq[(size_t)x * W + (sl >> 6)] >> (sl & 63)) & 1ull;
+            }
+          }
+          out |= mm << (j & 63);
+        }
+        lkp[k] = out;
+      }
+    }
+  }
+}
+
 __global__ void fill_u32_kernel(uint32_t* p, size_t n, uint32_t v) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -4195,6 +4358,205 @@ int spf_table_repair(
   (void)hipStreamSynchronize(g->stream);
   (void)hipFree(d);
   return st;
+}
+
+} // extern "C"
+
+// ============================================ all-nodes unicast route table
+
+struct spf_route_table {
+  spf_query* q = nullptr;
+  uint32_t P = 0;
+  std::vector<uint64_t> lk_off; // [nq + 1]
+  uint32_t *d_ann_off = nullptr, *d_ann = nullptr, *d_metric = nullptr, *d_best = nullptr;
+  uint64_t *d_lk_off = nullptr, *d_links = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool ran = false;
+};
+
+namespace {
+void free_route_table(spf_route_table* t) {
+  if (!t) {
+    return;
+  }
+  (void)hipSetDevice(t->q->g->device);
+  for (void* p : {(void*)t->d_ann_off, (void*)t->d_ann, (void*)t->d_metric, (void*)t->d_best,
+                  (void*)t->d_lk_off, (void*)t->d_links}) {
+    if (p) {
+      (void)hipFree(p);
+    }
+  }
+  if (t->ev0) {
+    (void)hipEventDestroy(t->ev0);
+  }
+  if (t->ev1) {
+    (void)hipEventDestroy(t->ev1);
+  }
+  delete t;
+}
+} // namespace
+
+extern "C" {
+
+int spf_route_table_create(
+    spf_query* q, uint32_t num_prefixes, const uint32_t* ann_offsets,
+    const uint32_t* announcers, spf_route_table** out) {
+  if (!q || !out || (num_prefixes && !ann_offsets)) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  *out = nullptr;
+  if (!(q->flags & SPF_F_NEXTHOPS) || (q->flags & SPF_F_UNIT_METRIC) || q->has_ign) {
+    return fail(SPF_E_INVALID, "route tables need a metric query with next hops and no ignore lists");
+  }
+  if (q->dist == DistPlan::Exact) {
+    return fail(SPF_E_UNSUPPORTED, "64-bit distance rows");
+  }
+  const spf_graph* g = q->g;
+  if (ann_offsets && ann_offsets[0] != 0) {
+    return fail(SPF_E_INVALID, "ann_offsets[0] != 0");
+  }
+  const uint32_t na = num_prefixes ? ann_offsets[num_prefixes] : 0;
+  if (na && !announcers) {
+    return fail(SPF_E_INVALID, "null announcers");
+  }
+  for (uint32_t p = 0; p < num_prefixes; ++p) {
+    if (ann_offsets[p + 1] < ann_offsets[p]) {
+      return fail(SPF_E_INVALID, "ann_offsets not monotone");
+    }
+  }
+  for (uint32_t i = 0; i < na; ++i) {
+    if (announcers[i] >= g->V) {
+      return fail(SPF_E_INVALID, "announcer out of range");
+    }
+  }
+  std::vector<uint32_t> src(q->nq);
+  HIP_TRY(hipSetDevice(g->device));
+  HIP_TRY(hipMemcpy(src.data(), q->d_src, (size_t)q->nq * 4, hipMemcpyDeviceToHost));
+  auto* t = new spf_route_table();
+  t->q = q;
+  t->P = num_prefixes;
+  t->lk_off.assign(q->nq + 1, 0);
+  for (uint32_t i = 0; i < q->nq; ++i) {
+    const uint32_t deg = g->row[src[i] + 1] - g->row[src[i]];
+    t->lk_off[i + 1] = t->lk_off[i] + (uint64_t)num_prefixes * ((deg + 63) / 64);
+  }
+  auto bail = [&](int st) {
+    free_route_table(t);
+    return st;
+  };
+  const size_t cells = (size_t)q->nq * num_prefixes;
+  std::vector<uint32_t> off(ann_offsets, ann_offsets + num_prefixes + 1);
+  if (num_prefixes == 0) {
+    off.assign(1, 0);
+  }
+  int st = SPF_OK;
+  if ((st = dev_upload(&t->d_ann_off, off.data(), off.size())) ||
+      (na && (st = dev_upload(&t->d_ann, announcers, na))) ||
+      (st = dev_upload(&t->d_lk_off, t->lk_off.data(), t->lk_off.size()))) {
+    return bail(st);
+  }
+  if (cells) {
+    if (hipMalloc((void**)&t->d_metric, cells * 4) != hipSuccess ||
+        hipMalloc((void**)&t->d_best, cells * 4) != hipSuccess ||
+        (t->lk_off.back() &&
+         hipMalloc((void**)&t->d_links, t->lk_off.back() * 8) != hipSuccess)) {
+      return bail(fail(SPF_E_NOMEM, "route table allocation"));
+    }
+  }
+  if (hipEventCreate(&t->ev0) != hipSuccess || hipEventCreate(&t->ev1) != hipSuccess) {
+    return bail(fail(SPF_E_DEVICE, "hipEventCreate"));
+  }
+  *out = t;
+  return SPF_OK;
+}
+
+int spf_route_table_destroy(spf_route_table* t) {
+  free_route_table(t);
+  return SPF_OK;
+}
+
+int spf_route_table_run(spf_route_table* t) {
+  if (!t) {
+    return fail(SPF_E_INVALID, "null table");
+  }
+  spf_query* q = t->q;
+  if (!q->ran) {
+    return fail(SPF_E_INVALID, "the query has not run");
+  }
+  spf_graph* g = q->g;
+  HIP_TRY(hipSetDevice(g->device));
+  HIP_TRY(hipEventRecord(t->ev0, g->stream));
+  if (q->nq && t->P) {
+    RouteTableArgs a;
+    a.row = g->d_row;
+    a.col = g->d_col;
+    a.wout = g->d_wout;
+    a.slot = g->d_slot;
+    a.trbits = g->d_tr;
+    a.src = q->d_src;
+    a.dist = (const uint32_t*)q->d_dist;
+    a.nh = q->d_nh;
+    a.nh_off = q->d_nh_off;
+    a.nh_w = q->d_nh_w;
+    a.ann_off = t->d_ann_off;
+    a.ann = t->d_ann;
+    a.lk_off = t->d_lk_off;
+    a.metric_out = t->d_metric;
+    a.best_out = t->d_best;
+    a.link_out = t->d_links;
+    a.Vp = q->Vp;
+    a.P = t->P;
+    a.nq = q->nq;
+    const uint32_t grid = std::min<uint32_t>(q->nq, (uint32_t)g->num_cus * 8);
+    hipLaunchKernelGGL(spf_route_table_kernel, dim3(grid), dim3(256), 0, g->stream, a);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipEventRecord(t->ev1, g->stream));
+  t->ran = true;
+  return SPF_OK;
+}
+
+int spf_route_table_elapsed_ms(spf_route_table* t, float* ms) {
+  if (!t || !ms || !t->ran) {
+    return fail(SPF_E_INVALID, "no run to time");
+  }
+  HIP_TRY(hipEventSynchronize(t->ev1));
+  HIP_TRY(hipEventElapsedTime(ms, t->ev0, t->ev1));
+  return SPF_OK;
+}
+
+int spf_route_table_link_words(const spf_route_table* t, uint32_t i) {
+  if (!t || i >= t->q->nq) {
+    return fail(SPF_E_INVALID, "row out of range");
+  }
+  return t->P ? (int)((t->lk_off[i + 1] - t->lk_off[i]) / t->P) : 0;
+}
+
+int spf_route_table_fetch(
+    spf_route_table* t, uint32_t i, uint32_t* metric, uint32_t* best, uint64_t* links) {
+  if (!t || i >= t->q->nq || (t->P && (!metric || !best))) {
+    return fail(SPF_E_INVALID, "bad argument");
+  }
+  if (!t->ran) {
+    return fail(SPF_E_INVALID, "table has not run");
+  }
+  if (t->P == 0) {
+    return SPF_OK;
+  }
+  spf_graph* g = t->q->g;
+  HIP_TRY(hipSetDevice(g->device));
+  HIP_TRY(hipStreamSynchronize(g->stream));
+  const size_t o = (size_t)i * t->P;
+  HIP_TRY(hipMemcpy(metric, t->d_metric + o, (size_t)t->P * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(best, t->d_best + o, (size_t)t->P * 4, hipMemcpyDeviceToHost));
+  const uint64_t nw = t->lk_off[i + 1] - t->lk_off[i];
+  if (nw) {
+    if (!links) {
+      return fail(SPF_E_INVALID, "null links");
+    }
+    HIP_TRY(hipMemcpy(links, t->d_links + t->lk_off[i], nw * 8, hipMemcpyDeviceToHost));
+  }
+  return SPF_OK;
 }
 
 } // extern "C"

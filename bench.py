@@ -223,6 +223,11 @@ def route_db_rebuild_ms(topo, device, iters=5):
     return out
 
 
+def _unicast_delta(new, old):
+    """getRouteDelta (Decision.cpp:47-85) over unicast route dicts."""
+    return {k: v for k, v in new.items() if old.get(k) != v}, sorted(k for k in old if k not in new)
+
+
 def all_nodes_route_table(topo, device, reps=3):
     """the unicast RouteDb of EVERY fabric node at once
     (AllNodesRouteTable: one all-sources SPF with next hops + the
@@ -258,6 +263,21 @@ def all_nodes_route_table(topo, device, reps=3):
         if table.routes(node) != solver.buildRouteDb(node, areas, ps)["unicast"]:
             bad += 1
     n_mat, us_mat = table.routes_timed("2-0-0")
+    # network-wide route delta of one RSW drain (DecisionBenchmark's churn):
+    # rebuild the table on the drained topology, diff it on the device
+    rsw = next(i for i, n in enumerate(topo.names) if n.startswith("3-"))
+    dbs = topo.adj_dbs()
+    dbs[rsw].isOverloaded = True
+    ls.updateAdjacencyDatabase(dbs[rsw])
+    t0 = time.perf_counter()
+    drained = E.AllNodesRouteTable(areas, "0", ps, True)
+    t1 = time.perf_counter()
+    changed = drained.diff(table)
+    t2 = time.perf_counter()
+    changed = np.asarray(changed, dtype=np.int64)
+    upd, dele = drained.delta("2-0-0")
+    delta_ok = (upd, sorted(dele)) == _unicast_delta(solver.buildRouteDb("2-0-0", areas, ps)["unicast"],
+                                                     table.routes("2-0-0"))
     # algorithmic bytes of spf_route_table_kernel per launch: per (node,
     # prefix) cell the metric + best words written, the link mask written
     # (8 B x link words of the node), the announcer's distance read and its
@@ -281,6 +301,13 @@ def all_nodes_route_table(topo, device, reps=3):
                                   "unit": "GB/s", "frac": round(alg / (k_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
         "materialise_one_node_ms": round(us_mat / 1e3, 3), "materialised_routes": n_mat,
         "parity_check": "ok" if bad == 0 else f"{bad} nodes differ",
+        "drain_delta": {
+            "what": f"RSW {topo.names[rsw]} drained: table rebuilt + spf_route_table_diff_kernel = "
+                    "getRouteDelta of every node at once",
+            "table_rebuild_ms": round((t1 - t0) * 1e3, 2), "diff_ms": round((t2 - t1) * 1e3, 3),
+            "changed_routes": int(changed.sum()), "nodes_with_changes": int((changed > 0).sum()),
+            "parity_check": "ok" if delta_ok else "2-0-0 delta differs from getRouteDelta",
+        },
     }
 
 

@@ -267,6 +267,17 @@ int spf_route_table_link_words(const spf_route_table* t, uint32_t i);
 int spf_route_table_fetch(
     spf_route_table* t, uint32_t i, uint32_t* metric, uint32_t* best, uint64_t* links);
 
+/* Network-wide route delta: compare two tables built
+ * over graphs with the same CSR layout (e.g. before and after an overload or
+ * metric change) and the same prefixes; cell (i, p) changed iff its metric,
+ * best announcer or link mask differs — getRouteDelta's (Decision.cpp:47-85)
+ * unicast updates and deletes for every node at once.  changed[i] = changed
+ * prefixes of row i (host [num rows]); the per-row bitmap is kept in `newer`
+ * (spf_route_table_changed).  SPF_E_UNSUPPORTED if the layouts differ. */
+int spf_route_table_diff(spf_route_table* older, spf_route_table* newer, uint32_t* changed);
+/* Changed-prefix bitmap of row i from the last diff: bits[ceil(P/64)]. */
+int spf_route_table_changed(spf_route_table* t, uint32_t i, uint64_t* bits);
+
 #ifdef __cplusplus
 }
 #endif

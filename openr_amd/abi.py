@@ -65,6 +65,8 @@ EXPORTED_SYMBOLS = (
     "spf_route_table_elapsed_ms",
     "spf_route_table_link_words",
     "spf_route_table_fetch",
+    "spf_route_table_diff",
+    "spf_route_table_changed",
 )
 
 SPF_DELTA_REMOVED = 1

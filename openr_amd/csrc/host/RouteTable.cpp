@@ -172,6 +172,52 @@ uint64_t AllNodesRouteTable::countRoutes() const {
   return n;
 }
 
+AllNodesRouteTable::Row AllNodesRouteTable::fetchRow(uint32_t i) const {
+  Row r;
+  const int w = spf_route_table_link_words(table_, i);
+  if (w < 0) {
+    tableFailure("spf_route_table_link_words", w);
+  }
+  const size_t P = prefixes_.size();
+  r.W = (size_t)w;
+  r.metric.resize(P);
+  r.best.resize(P);
+  r.links.resize(std::max<size_t>(1, P * r.W));
+  if (int s = spf_route_table_fetch(table_, i, r.metric.data(), r.best.data(), r.links.data());
+      s != SPF_OK) {
+    tableFailure("spf_route_table_fetch", s);
+  }
+  return r;
+}
+
+RibUnicastEntry AllNodesRouteTable::materialise(
+    const std::string& node, uint32_t i, const Row& r, size_t p) const {
+  const bool isV4 = prefixes_[p].prefixAddress.addr.size() == 4;
+  const uint32_t e0 = row_[i];
+  std::unordered_set<thrift::NextHopThrift> nhs;
+  for (size_t k = 0; k < r.W; ++k) {
+    uint64_t m = r.links[p * r.W + k];
+    while (m) {
+      const uint32_t j = (uint32_t)(k * 64 + __builtin_ctzll(m));
+      m &= m - 1;
+      const Link& l = *halfLink_[e0 + j];
+      nhs.insert(createNextHop(
+          isV4 ? l.getNhV4FromNode(node) : l.getNhV6FromNode(node), l.getIfaceFromNode(node),
+          (int32_t)r.metric[p], std::nullopt, false, l.getArea()));
+    }
+  }
+  const thrift::PrefixEntry* bestEntry = nullptr;
+  for (const auto& a : announcers_[p]) {
+    if (a.id == r.best[p]) {
+      bestEntry = &a.entry;
+    }
+  }
+  if (!bestEntry) {
+    throw std::logic_error("AllNodesRouteTable: best announcer not in the prefix");
+  }
+  return RibUnicastEntry(prefixes_[p], std::move(nhs), *bestEntry, area_);
+}
+
 std::unordered_map<thrift::IpPrefix, RibUnicastEntry> AllNodesRouteTable::routes(
     const std::string& node) const {
   std::unordered_map<thrift::IpPrefix, RibUnicastEntry> out;
@@ -179,48 +225,65 @@ std::unordered_map<thrift::IpPrefix, RibUnicastEntry> AllNodesRouteTable::routes
   if (it == ids_.end() || prefixes_.empty()) {
     return out;
   }
-  const uint32_t i = it->second;
-  const int w = spf_route_table_link_words(table_, i);
-  if (w < 0) {
-    tableFailure("spf_route_table_link_words", w);
-  }
-  const size_t P = prefixes_.size(), W = (size_t)w;
-  std::vector<uint32_t> metric(P), best(P);
-  std::vector<uint64_t> links(std::max<size_t>(1, P * W));
-  if (int s = spf_route_table_fetch(table_, i, metric.data(), best.data(), links.data());
-      s != SPF_OK) {
-    tableFailure("spf_route_table_fetch", s);
-  }
-  const uint32_t e0 = row_[i];
-  for (size_t p = 0; p < P; ++p) {
-    if (metric[p] == 0xFFFFFFFFu) {
-      continue;
+  const Row r = fetchRow(it->second);
+  for (size_t p = 0; p < prefixes_.size(); ++p) {
+    if (r.metric[p] != 0xFFFFFFFFu) {
+      out.emplace(prefixes_[p], materialise(node, it->second, r, p));
     }
-    const bool isV4 = prefixes_[p].prefixAddress.addr.size() == 4;
-    std::unordered_set<thrift::NextHopThrift> nhs;
-    for (size_t k = 0; k < W; ++k) {
-      uint64_t m = links[p * W + k];
-      while (m) {
-        const uint32_t j = (uint32_t)(k * 64 + __builtin_ctzll(m));
-        m &= m - 1;
-        const Link& l = *halfLink_[e0 + j];
-        nhs.insert(createNextHop(
-            isV4 ? l.getNhV4FromNode(node) : l.getNhV6FromNode(node), l.getIfaceFromNode(node),
-            (int32_t)metric[p], std::nullopt, false, l.getArea()));
-      }
-    }
-    const thrift::PrefixEntry* bestEntry = nullptr;
-    for (const auto& a : announcers_[p]) {
-      if (a.id == best[p]) {
-        bestEntry = &a.entry;
-      }
-    }
-    if (!bestEntry) {
-      throw std::logic_error("AllNodesRouteTable: best announcer not in the prefix");
-    }
-    out.emplace(prefixes_[p], RibUnicastEntry(prefixes_[p], std::move(nhs), *bestEntry, area_));
   }
   return out;
 }
 
+std::vector<uint32_t> AllNodesRouteTable::diff(const AllNodesRouteTable& older) {
+  if (older.names_ != names_ || older.prefixes_ != prefixes_ || older.row_ != row_) {
+    throw std::invalid_argument("AllNodesRouteTable::diff: different nodes, prefixes or links");
+  }
+  std::vector<uint32_t> changed(names_.size());
+  if (int s = spf_route_table_diff(older.table_, table_, changed.data()); s != SPF_OK) {
+    if (s == SPF_E_UNSUPPORTED) {
+      throw std::invalid_argument(std::string("AllNodesRouteTable::diff: ") +
+                                  spf_last_error_detail());
+    }
+    tableFailure("spf_route_table_diff", s);
+  }
+  diffed_ = true;
+  return changed;
+}
+
+DecisionRouteUpdate AllNodesRouteTable::delta(const std::string& node) const {
+  DecisionRouteUpdate u;
+  auto it = ids_.find(node);
+  if (!diffed_) {
+    throw std::logic_error("AllNodesRouteTable::delta: no diff has run");
+  }
+  if (it == ids_.end() || prefixes_.empty()) {
+    return u;
+  }
+  const size_t P = prefixes_.size();
+  std::vector<uint64_t> bits((P + 63) / 64);
+  if (int s = spf_route_table_changed(table_, it->second, bits.data()); s != SPF_OK) {
+    tableFailure("spf_route_table_changed", s);
+  }
+  bool any = false;
+  for (uint64_t b : bits) {
+    any |= b != 0;
+  }
+  if (!any) {
+    return u;
+  }
+  const Row r = fetchRow(it->second);
+  for (size_t k = 0; k < bits.size(); ++k) {
+    uint64_t m = bits[k];
+    while (m) {
+      const size_t p = k * 64 + __builtin_ctzll(m);
+      m &= m - 1;
+      if (r.metric[p] == 0xFFFFFFFFu) {
+        u.unicastRoutesToDelete.push_back(prefixes_[p]);
+      } else {
+        u.unicastRoutesToUpdate.push_back(materialise(node, it->second, r, p));
+      }
+    }
+  }
+  return u;
+}
 } // namespace openr

@@ -51,7 +51,26 @@ class AllNodesRouteTable {
   // The unicast routes of `node` (empty if the node is not in the area).
   std::unordered_map<thrift::IpPrefix, RibUnicastEntry> routes(const std::string& node) const;
 
+  // Network-wide route delta against an older table over the same graph
+  // layout and prefixes (spf_route_table_diff): per node (id order, see
+  // nodeName) the number of prefixes whose route changed.  Throws
+  // std::invalid_argument when the layouts differ.
+  std::vector<uint32_t> diff(const AllNodesRouteTable& older);
+  // The unicast part of getRouteDelta(routes(node), older.routes(node))
+  // (Decision.cpp:47-85) from the last diff: changed routes materialised,
+  // vanished ones deleted.
+  DecisionRouteUpdate delta(const std::string& node) const;
+  const std::string& nodeName(uint32_t id) const { return names_.at(id); }
+
  private:
+  struct Row {
+    std::vector<uint32_t> metric, best;
+    std::vector<uint64_t> links;
+    size_t W = 0;
+  };
+  Row fetchRow(uint32_t i) const;
+  RibUnicastEntry materialise(const std::string& node, uint32_t i, const Row& r, size_t p) const;
+
   struct Announcer {
     uint32_t id;
     thrift::PrefixEntry entry;
@@ -68,6 +87,7 @@ class AllNodesRouteTable {
   spf_query* query_{nullptr};
   spf_route_table* table_{nullptr};
   float spfMs_{0}, routeMs_{0};
+  bool diffed_{false};
 };
 
 } // namespace openr

@@ -212,6 +212,23 @@ PYBIND11_MODULE(_openr_spf, m) {
         py::object unicast = all["unicast"]; // owned before `all` goes away
         return unicast;
       })
+      .def("diff", &AllNodesRouteTable::diff, py::arg("older"))
+      .def("node_name", &AllNodesRouteTable::nodeName)
+      .def("delta", [](const AllNodesRouteTable& t, const std::string& node) {
+        // (updated unicast routes as routes() renders them, deleted prefixes)
+        const DecisionRouteUpdate u = t.delta(node);
+        DecisionRouteDb db;
+        for (const auto& e : u.unicastRoutesToUpdate) {
+          db.unicastEntries.emplace(e.prefix, e);
+        }
+        py::dict all = routeDbToPy(db);
+        py::object upd = all["unicast"];
+        py::list del;
+        for (const auto& p : u.unicastRoutesToDelete) {
+          del.append(prefixKey(p));
+        }
+        return py::make_tuple(upd, del);
+      })
       .def("routes_timed", [](const AllNodesRouteTable& t, const std::string& node) {
         // fetch + materialise the node's routes in C++, no Python conversion
         const auto t0 = std::chrono::steady_clock::now();

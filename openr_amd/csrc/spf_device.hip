@@ -2429,6 +2429,46 @@ __global__ __launch_bounds__(256) void spf_route_table_kernel(RouteTableArgs a) 
   }
 }
 
+// Route-table diff (spf_route_table_diff): cell (q, p) changed iff its
+// metric, best announcer or link mask differs between the two tables — the
+// route-selection part of RibUnicastEntry equality, so the changed cells are
+// getRouteDelta's (Decision.cpp:47-85) unicast updates + deletes for every
+// node at once.  One wave per 64 prefixes of a row: the ballot of changed
+// lanes is the row's bitmap word; popcounts add up per row.
+__global__ __launch_bounds__(256) void spf_route_table_diff_kernel(
+    const uint32_t* __restrict__ ma, const uint32_t* __restrict__ ba,
+    const uint64_t* __restrict__ la, const uint32_t* __restrict__ mb,
+    const uint32_t* __restrict__ bb, const uint64_t* __restrict__ lb,
+    const uint64_t* __restrict__ lk_off, uint32_t P, uint32_t nq, uint32_t pw,
+    uint64_t* __restrict__ bits, uint32_t* __restrict__ count) {
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  for (uint32_t q = blockIdx.x; q < nq; q += gridDim.x) {
+    const uint32_t WL = P ? (uint32_t)((lk_off[q + 1] - lk_off[q]) / P) : 0;
+    const uint64_t* la_q = la + lk_off[q];
+    const uint64_t* lb_q = lb + lk_off[q];
+    uint32_t n = 0;
+    for (uint32_t w = wv; w < pw; w += blockDim.x / 64) {
+      const uint32_t p = w * 64 + lane;
+      bool ch = false;
+      if (p < P) {
+        const size_t o = (size_t)q * P + p;
+        ch = ma[o] != mb[o] || ba[o] != bb[o];
+        for (uint32_t k = 0; k < WL && !ch; ++k) {
+          ch = la_q[(size_t)p * WL + k] != lb_q[(size_t)p * WL + k];
+        }
+      }
+      const uint64_t word = __ballot(ch);
+      if (lane == 0) {
+        bits[(size_t)q * pw + w] = word;
+        n += __popcll(word);
+      }
+    }
+    if (lane == 0 && n) {
+      atomicAdd(&count[q], n);
+    }
+  }
+}
+
 __global__ void fill_u32_kernel(uint32_t* p, size_t n, uint32_t v) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -4372,6 +4412,9 @@ struct spf_route_table {
   uint64_t *d_lk_off = nullptr, *d_links = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool ran = false;
+  // spf_route_table_diff against an older table: changed-cell bitmap
+  uint64_t* d_diff = nullptr;
+  uint32_t* d_count = nullptr;
 };
 
 namespace {
@@ -4381,7 +4424,7 @@ void free_route_table(spf_route_table* t) {
   }
   (void)hipSetDevice(t->q->g->device);
   for (void* p : {(void*)t->d_ann_off, (void*)t->d_ann, (void*)t->d_metric, (void*)t->d_best,
-                  (void*)t->d_lk_off, (void*)t->d_links}) {
+                  (void*)t->d_lk_off, (void*)t->d_links, (void*)t->d_diff, (void*)t->d_count}) {
     if (p) {
       (void)hipFree(p);
     }
@@ -4556,6 +4599,69 @@ int spf_route_table_fetch(
     }
     HIP_TRY(hipMemcpy(links, t->d_links + t->lk_off[i], nw * 8, hipMemcpyDeviceToHost));
   }
+  return SPF_OK;
+}
+
+} // extern "C"
+
+extern "C" {
+
+int spf_route_table_diff(spf_route_table* older, spf_route_table* newer, uint32_t* changed) {
+  if (!older || !newer || (newer->q->nq && !changed)) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  if (!older->ran || !newer->ran) {
+    return fail(SPF_E_INVALID, "both tables must have run");
+  }
+  const spf_graph* ga = older->q->g;
+  const spf_graph* gb = newer->q->g;
+  if (ga->device != gb->device || older->q->nq != newer->q->nq || older->P != newer->P ||
+      older->lk_off != newer->lk_off || ga->row != gb->row || ga->col != gb->col) {
+    return fail(SPF_E_UNSUPPORTED,
+                "tables differ in rows, prefixes or link layout (rematerialise instead)");
+  }
+  const uint32_t nq = newer->q->nq, P = newer->P, pw = (P + 63) / 64;
+  if (nq == 0) {
+    return SPF_OK;
+  }
+  HIP_TRY(hipSetDevice(gb->device));
+  if (!newer->d_count) {
+    HIP_TRY(hipMalloc((void**)&newer->d_count, (size_t)nq * 4));
+    if (pw) {
+      HIP_TRY(hipMalloc((void**)&newer->d_diff, (size_t)nq * pw * 8));
+    }
+  }
+  // the older table's rows are read on the newer table's stream
+  HIP_TRY(hipStreamSynchronize(ga->stream));
+  HIP_TRY(hipMemsetAsync(newer->d_count, 0, (size_t)nq * 4, gb->stream));
+  if (P) {
+    const uint32_t grid = std::min<uint32_t>(nq, (uint32_t)gb->num_cus * 8);
+    hipLaunchKernelGGL(spf_route_table_diff_kernel, dim3(grid), dim3(256), 0, gb->stream,
+                       older->d_metric, older->d_best, older->d_links, newer->d_metric,
+                       newer->d_best, newer->d_links, newer->d_lk_off, P, nq, pw,
+                       newer->d_diff, newer->d_count);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipMemcpyAsync(changed, newer->d_count, (size_t)nq * 4, hipMemcpyDeviceToHost,
+                         gb->stream));
+  HIP_TRY(hipStreamSynchronize(gb->stream));
+  return SPF_OK;
+}
+
+int spf_route_table_changed(spf_route_table* t, uint32_t i, uint64_t* bits) {
+  if (!t || i >= t->q->nq || !bits) {
+    return fail(SPF_E_INVALID, "bad argument");
+  }
+  if (!t->d_count) {
+    return fail(SPF_E_INVALID, "no diff has run on this table");
+  }
+  const uint32_t pw = (t->P + 63) / 64;
+  if (!pw) {
+    return SPF_OK;
+  }
+  HIP_TRY(hipSetDevice(t->q->g->device));
+  HIP_TRY(hipStreamSynchronize(t->q->g->stream));
+  HIP_TRY(hipMemcpy(bits, t->d_diff + (size_t)i * pw, (size_t)pw * 8, hipMemcpyDeviceToHost));
   return SPF_OK;
 }
 

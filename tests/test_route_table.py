@@ -71,3 +71,48 @@ def test_route_table_fabric(E):
     for node in sorted(topo.names)[:: max(1, topo.num_nodes // 25)] + ["2-0-0"]:
         db = solver.buildRouteDb(node, areas, ps)
         assert table.routes(node) == db["unicast"], node
+
+
+def _delta_py(new, old):
+    """getRouteDelta (Decision.cpp:47-85) over unicast dicts: updates = new
+    or changed entries, deletes = prefixes only in old."""
+    upd = {k: v for k, v in new.items() if old.get(k) != v}
+    dele = sorted(k for k in old if k not in new)
+    return upd, dele
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_route_table_diff_equals_route_delta(E, seed):
+    """Overload / metric churn (same links): the device diff + delta of every
+    node equal getRouteDelta of that node's buildRouteDb before and after."""
+    import random
+
+    names, adj_dbs, prefix_dbs = RZ.random_network(
+        900 + seed, n_nodes=40, n_links=90, overload_prob=0.1, link_overload_prob=0.0
+    )
+    areas, ps = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    solver = E.SpfSolver(names[0], True, False)
+    before = {n: solver.buildRouteDb(n, areas, ps) for n in names}
+    t0 = E.AllNodesRouteTable(areas, "0", ps, True)
+    rng = random.Random(seed)
+    for db in rng.sample(adj_dbs["0"], 3):  # drain toggles and metric changes
+        db.isOverloaded = not db.isOverloaded
+        if db.adjacencies:
+            db.adjacencies[0].metric += rng.randint(1, 9)
+    # the same load order: same links, same linksFromNode order (CSR layout)
+    areas, ps = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    t1 = E.AllNodesRouteTable(areas, "0", ps, True)
+    changed = t1.diff(t0)
+    total = 0
+    for i, c in enumerate(changed):
+        node = t1.node_name(i)
+        upd, dele = t1.delta(node)
+        assert len(upd) + len(dele) == c, node
+        # device delta == delta of the table rows == getRouteDelta of the host RouteDbs
+        assert (upd, sorted(dele)) == _delta_py(t1.routes(node), t0.routes(node)), node
+        after = solver.buildRouteDb(node, areas, ps)
+        b = _ecmp_only(before[node]["unicast"]) if before.get(node) else {}
+        a = _ecmp_only(after["unicast"]) if after else {}
+        assert (upd, sorted(dele)) == _delta_py(a, b), node
+        total += c
+    assert total > 0

@@ -290,6 +290,7 @@ def all_nodes_route_table(topo, device, reps=3):
     alg = int(P * (12 * V + 8 * int(lw.sum()) + 8 * int(nw.sum())))
     med = lambda x: sorted(x)[len(x) // 2]  # noqa: E731
     k_ms = med(rt)
+    rt_traffic, rt_src = pmc_traffic_largest("spf_route_table_kernel")
     return {
         "what": "unicast RouteDb of every node of the fabric at once: AllNodesRouteTable = all-sources "
                 "SPF + next hops, then spf_route_table_kernel (selectEcmpOpenr per node x prefix)",
@@ -298,7 +299,8 @@ def all_nodes_route_table(topo, device, reps=3):
         "route_kernel_ms_median": round(k_ms, 3),
         "route_kernel_roofline": {"bound": "hbm", "algorithmic_bytes": alg,
                                   "achieved": round(alg / (k_ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBS,
-                                  "unit": "GB/s", "frac": round(alg / (k_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
+                                  "unit": "GB/s", "frac": round(alg / (k_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                  "traffic": rt_traffic, "traffic_source": rt_src},
         "materialise_one_node_ms": round(us_mat / 1e3, 3), "materialised_routes": n_mat,
         "parity_check": "ok" if bad == 0 else f"{bad} nodes differ",
         "drain_delta": {

@@ -261,10 +261,12 @@ class ShardedAllSources:
         `new_csr` must keep the node ids (same names, so the same ranks).
         The change is listed as directed edge deltas (spf_graph_diff), the
         screen kernel marks the sources of this rank whose shortest-path DAG
-        a delta can touch (spf_table_screen), only those are recomputed on
-        the new device graph and scattered into their rows, and the repaired
-        rows are exchanged between ranks (exchange_rows).  The result equals
-        a full recompute bit for bit (tests/test_allsources.py)."""
+        a delta can touch (spf_table_screen), only those rows are repaired in
+        place on the new device graph (spf_table_repair; or recomputed and
+        scattered when the repair image does not fit LDS, or with
+        OPENR_SPF_REPAIR_RECOMPUTE=1), and the repaired rows are exchanged
+        between ranks (exchange_rows).  The result equals a full recompute
+        bit for bit (tests/test_table_repair.py)."""
         import numpy as np
         import torch
         import torch.distributed as dist

@@ -337,7 +337,8 @@ def ksp2_route_db(topo, device, iters=2):
     out["per_build"] = {
         "spf_runs": round(c.get("decision.spf_runs", 0) / n, 1),
         **{k.split(".", 1)[1]: round(c.get(k, 0) / n, 1)
-           for k in ("decision.route_prefetch_us", "decision.spf_batch_us", "decision.spf_device_us")},
+           for k in ("decision.route_prefetch_us", "decision.spf_batch_us", "decision.spf_device_us",
+                     "decision.route_prefix_pool_us", "decision.route_merge_us")},
     }
     out["what"] = ("adj-db update (RSW overload toggle) + buildRouteDb of 2-0-0, all prefixes "
                    "SR_MPLS/KSP2_ED_ECMP (k=1 + k=2 paths to every node)")

@@ -30,6 +30,11 @@ struct LinkState::Engine {
   std::unordered_map<const Link*, uint32_t> linkIndex;
   std::vector<std::array<uint32_t, 2>> halves; // link id -> half-edge from first/second node
   spf_graph* graph{nullptr};
+  // host block the 32-bit rows of a batch land in (runBatch): reused while no
+  // view of an earlier batch holds it, so big batches (the KSP2 second
+  // passes: 9,975 x 9,976 rows on the fabric) skip the zero fill and the
+  // page faults of a fresh 400 MB allocation
+  std::shared_ptr<std::vector<uint32_t>> rowBlock;
   bool exact{false};
   float lastMs{0};
   std::unordered_map<uint32_t, std::unique_ptr<SpfView>> memo[2];

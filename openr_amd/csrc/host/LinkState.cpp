@@ -483,7 +483,15 @@ std::vector<std::unique_ptr<SpfView>> runBatch(
   std::vector<uint64_t> maskOff(nq + 1, 0);
   std::vector<uint32_t> words(nq, 1);
   if (!exact && nq > 1) {
-    rows32 = std::make_shared<std::vector<uint32_t>>((size_t)nq * V);
+    const size_t need = (size_t)nq * V;
+    if (eng.rowBlock && eng.rowBlock.use_count() == 1 && eng.rowBlock->size() >= need) {
+      rows32 = eng.rowBlock; // no live view reads it: overwrite in place
+    } else {
+      rows32 = std::make_shared<std::vector<uint32_t>>(need);
+      if (!eng.rowBlock || eng.rowBlock.use_count() > 1 || eng.rowBlock->size() < need) {
+        eng.rowBlock = rows32;
+      }
+    }
     if ((s = spf_query_fetch_rows(q, 0, nq, rows32->data(), (size_t)V * 4, 0)) != SPF_OK) {
       engineFailure("spf_query_fetch_rows", s);
     }
@@ -1132,23 +1140,72 @@ LinkStateMetric LinkState::getMaxHopsToNode(const std::string& nodeName) const {
   return best;
 }
 
+// The reference's greedy edge-disjoint DFS (traceOnePath, LinkState.cpp:
+// 398-419), with two memos that keep its result and order exactly:
+//  * preds: pathLinksOf(v) depends on the SPF result and v only, so it is
+//    computed once per node per getKthPaths call instead of on every visit;
+//  * dead: a node whose search failed has had every predecessor link
+//    inserted into linksToIgnore (the loop only stops early on success, and
+//    links are never removed), so any later search from it fails with no
+//    side effect — return at once.  This turns the final, exhaustive search
+//    of every call from O(visits x degree) into O(DAG).
+// The reference's visited LinkSet (shared by the successive traces of one
+// getKthPaths call, LinkState.cpp:776-786) is a link-id stamp array here:
+// same membership, no hashing or allocation per link.
+struct LinkState::TraceMemo {
+  std::vector<uint32_t> stamp;   // == epoch: preds[v] valid
+  std::vector<uint32_t> visited; // == epoch: link id taken by some trace
+  std::vector<uint8_t> dead;
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> preds;
+  uint32_t epoch = 0;
+  void reset(uint32_t V, uint32_t L) {
+    if (stamp.size() != V || visited.size() != L) {
+      stamp.assign(V, 0);
+      visited.assign(L, 0);
+      preds.assign(V, {});
+      epoch = 0;
+    }
+    dead.assign(V, 0);
+    if (++epoch == 0) {
+      std::fill(stamp.begin(), stamp.end(), 0);
+      std::fill(visited.begin(), visited.end(), 0);
+      epoch = 1;
+    }
+  }
+  bool take(uint32_t lid) {
+    if (visited[lid] == epoch) {
+      return false;
+    }
+    visited[lid] = epoch;
+    return true;
+  }
+};
+
 std::optional<LinkState::Path> LinkState::traceOnePath(
-    uint32_t src, uint32_t dest, const SpfView& result, LinkSet& linksToIgnore) const {
+    uint32_t src, uint32_t dest, const SpfView& result, TraceMemo& memo) const {
   if (src == dest) {
     return Path{};
   }
+  if (memo.dead[dest]) {
+    return std::nullopt;
+  }
   const auto& eng = *engine_;
-  std::vector<std::pair<uint32_t, uint32_t>> preds;
-  pathLinksOf(eng, result, dest, preds);
-  for (const auto& [eu, u] : preds) {
-    const auto& link = eng.links[eng.linkId[eu]];
-    if (linksToIgnore.insert(link).second) {
-      if (auto path = traceOnePath(src, u, result, linksToIgnore)) {
-        path->push_back(link);
+  auto& preds = memo.preds[dest];
+  if (memo.stamp[dest] != memo.epoch) {
+    pathLinksOf(eng, result, dest, preds);
+    memo.stamp[dest] = memo.epoch;
+  }
+  for (size_t i = 0; i < preds.size(); ++i) {
+    const auto [eu, u] = preds[i];
+    const uint32_t lid = eng.linkId[eu];
+    if (memo.take(lid)) {
+      if (auto path = traceOnePath(src, u, result, memo)) {
+        path->push_back(eng.links[lid]);
         return path;
       }
     }
   }
+  memo.dead[dest] = 1;
   return std::nullopt;
 }
 
@@ -1165,32 +1222,34 @@ std::vector<LinkState::Path> const& LinkState::getKthPaths(
       return found->second;
     }
   }
-  LinkSet linksToIgnore;
+  // linksToIgnore of the reference (LinkState.cpp:766-775), as the sorted
+  // ids of the links on the paths of ranks < k (every path link is an up
+  // link of the device graph)
+  auto& eng = engine();
+  std::vector<uint32_t> ign;
+  bool anyLink = false;
   for (size_t i = 1; i < k; ++i) {
     for (const auto& path : getKthPaths(src, dest, i)) {
       for (const auto& link : path) {
-        linksToIgnore.insert(link);
-      }
-    }
-  }
-  std::vector<Path> paths;
-  auto& eng = engine();
-  const SpfView* res = nullptr;
-  std::unique_ptr<SpfView> second;
-  if (linksToIgnore.empty()) {
-    res = &spfView(src, true);
-  } else {
-    auto sid = eng.ids.find(src);
-    if (sid != eng.ids.end()) {
-      auto did = eng.ids.find(dest);
-      std::vector<uint32_t> ign;
-      for (const auto& link : linksToIgnore) {
+        anyLink = true;
         auto li = eng.linkIndex.find(link.get());
         if (li != eng.linkIndex.end()) {
           ign.push_back(li->second);
         }
       }
-      std::sort(ign.begin(), ign.end());
+    }
+  }
+  std::sort(ign.begin(), ign.end());
+  ign.erase(std::unique(ign.begin(), ign.end()), ign.end());
+  std::vector<Path> paths;
+  const SpfView* res = nullptr;
+  std::unique_ptr<SpfView> second;
+  if (!anyLink) {
+    res = &spfView(src, true);
+  } else {
+    auto sid = eng.ids.find(src);
+    if (sid != eng.ids.end()) {
+      auto did = eng.ids.find(dest);
       if (did != eng.ids.end()) {
         std::unique_lock<std::shared_mutex> wr(eng.viewMu);
         auto pit = eng.kthPrefetch.find({sid->second, did->second});
@@ -1211,11 +1270,12 @@ std::vector<LinkState::Path> const& LinkState::getKthPaths(
   if (res && res->src != ~0u) {
     auto did = eng.ids.find(dest);
     if (did != eng.ids.end() && res->reached(did->second)) {
-      LinkSet visited;
-      auto path = traceOnePath(res->src, did->second, *res, visited);
+      thread_local TraceMemo memo;
+      memo.reset((uint32_t)eng.names.size(), (uint32_t)eng.links.size());
+      auto path = traceOnePath(res->src, did->second, *res, memo);
       while (path && !path->empty()) {
         paths.push_back(std::move(*path));
-        path = traceOnePath(res->src, did->second, *res, visited);
+        path = traceOnePath(res->src, did->second, *res, memo);
       }
     }
   }

@@ -327,8 +327,9 @@ class LinkState {
       const std::vector<std::string>& transitNodes,
       const std::vector<std::pair<std::shared_ptr<Link>, std::string>>& metricPatches) const;
   Engine& engine() const;
+  struct TraceMemo; // per getKthPaths call (LinkState.cpp)
   std::optional<Path> traceOnePath(
-      uint32_t src, uint32_t dest, const SpfView& result, LinkSet& linksToIgnore) const;
+      uint32_t src, uint32_t dest, const SpfView& result, TraceMemo& memo) const;
   void addLink(std::shared_ptr<Link> link);
   void removeLink(std::shared_ptr<Link> link);
   void removeNode(const std::string& nodeName);

@@ -476,6 +476,7 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
     myLinks(myNodeName, area, ls); // fill the per-build cache before the workers read it
   }
   std::vector<std::unordered_map<thrift::IpPrefix, RibUnicastEntry>> parts(threads);
+  const auto tpar = std::chrono::steady_clock::now();
   parallelFor(work.size(), threads, [&](size_t i, unsigned w) {
     const PrefixWork& x = work[i];
     if (x.srMpls) {
@@ -491,11 +492,18 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
       selectEcmpOpenr(parts[w], myNodeName, *x.prefix, *x.entries, x.isV4, areaLinkStates);
     }
   });
+  const auto tmerge = std::chrono::steady_clock::now();
   for (auto& part : parts) {
     for (auto& kv : part) {
       routeDb.unicastEntries.emplace(kv.first, std::move(kv.second));
     }
   }
+  Counters::add("decision.route_prefix_pool_us",
+                std::chrono::duration_cast<std::chrono::microseconds>(tmerge - tpar).count());
+  Counters::add("decision.route_merge_us",
+                std::chrono::duration_cast<std::chrono::microseconds>(
+                    std::chrono::steady_clock::now() - tmerge)
+                    .count());
 
   // node-label MPLS routes: on a label collision the smaller node name wins.
   // Labels held by a single (other) node are expanded on the worker pool

@@ -196,6 +196,56 @@ def _rebuild_loop(M, topo, iters, timed, fwd=(0, 0)):
     return out
 
 
+def publication_ingest(topo, reps=3):
+    """SURVEY §8(f) row 4, the step before the path: Decision::
+    processPublication (Decision.cpp:1631-1763) of the whole fabric LSDB —
+    one publication holding every "adj:<node>" and "prefix:<node>" key as a
+    CompactProtocol blob — decoded and applied to LinkState / PrefixState by
+    PublicationIngest (host C++).  Then one churn publication (an RSW's
+    adjacency database with its overload bit set).  The CPU line is the
+    oracle's reference-style updateAdjacencyDatabase over already-decoded
+    objects (no deserialisation), single thread."""
+    import openr_amd._openr_spf as E
+    from oracle import build as obuild
+
+    dbs = topo.adj_dbs()
+    pdbs = topo.prefix_dbs("0")
+    kv = {f"adj:{d.thisNodeName}": E.compact_encode_adj_db(d) for d in dbs}
+    kv.update({f"prefix:{p.thisNodeName}": E.compact_encode_prefix_db(p) for p in pdbs})
+    nbytes = sum(len(v) for v in kv.values())
+    full, churn = [], []
+    rsw = next(d for d in dbs if d.thisNodeName.startswith("3-"))
+    for _ in range(reps):
+        areas, ps = E.AreaLinkStates(), E.PrefixState()
+        ing = E.PublicationIngest("2-0-0")
+        _, us = ing.processPublicationTimed(areas, ps, "0", kv)
+        full.append(us / 1e3)
+        ing.resetPending()
+        rsw.isOverloaded = True
+        _, us = ing.processPublicationTimed(areas, ps, "0", {f"adj:{rsw.thisNodeName}": E.compact_encode_adj_db(rsw)})
+        rsw.isOverloaded = False
+        churn.append(us / 1e3)
+        links = areas["0"].numLinks()
+    obuild.build()
+    from oracle import _oracle_ref as O
+
+    ols = O.LinkState("0")
+    t0 = time.perf_counter()
+    for d in dbs:
+        ols.updateAdjacencyDatabase(d)
+    oracle_ms = (time.perf_counter() - t0) * 1e3
+    med = lambda x: round(sorted(x)[len(x) // 2], 2)  # noqa: E731
+    return {
+        "what": "processPublication of the full fabric LSDB (9,976 adj + 9,976 prefix keys, CompactProtocol) "
+                "then one RSW overload churn publication",
+        "keys": len(kv), "bytes": nbytes, "links": links,
+        "full_ms_median": med(full), "churn_ms_median": med(churn),
+        "cpu_oracle_adj_only_ms": round(oracle_ms, 1),
+        "cpu_oracle_note": "oracle/ref_decision.cpp updateAdjacencyDatabase of the same adjacency "
+                           "databases as objects (no decode, no prefixes), 1 thread",
+    }
+
+
 def route_db_rebuild_ms(topo, device, iters=5):
     """Full RouteDb rebuild of the benchmark node "2-0-0" after an RSW
     overload toggle: LinkState update + SPF on the engine (LFA off, as the
@@ -898,6 +948,10 @@ def main():
             out["all_nodes_route_table"] = all_nodes_route_table(topo, local)
         except Exception as e:
             out["all_nodes_route_table"] = {"error": repr(e)}
+        try:
+            out["publication_ingest"] = publication_ingest(topo)
+        except Exception as e:
+            out["publication_ingest"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(topo, args.cpu_sample)
         try:

@@ -857,11 +857,21 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
     thrift::AdjacencyDatabase const& newDb,
     LinkStateMetric holdUpTtl,
     LinkStateMetric holdDownTtl) {
-  LinkStateChange change;
-  const std::string& nodeName = newDb.thisNodeName;
+  return updateAdjacencyDatabase(thrift::AdjacencyDatabase(newDb), holdUpTtl, holdDownTtl);
+}
 
-  thrift::AdjacencyDatabase priorDb(std::move(adjacencyDatabases_[nodeName]));
-  adjacencyDatabases_[nodeName] = newDb;
+LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
+    thrift::AdjacencyDatabase&& db,
+    LinkStateMetric holdUpTtl,
+    LinkStateMetric holdDownTtl) {
+  LinkStateChange change;
+  // the database moves into adjacencyDatabases_ (a decoded publication is
+  // not copied a second time); newDb refers to the stored one
+  auto slot = adjacencyDatabases_.try_emplace(db.thisNodeName).first;
+  const std::string& nodeName = slot->first;
+  thrift::AdjacencyDatabase priorDb(std::move(slot->second));
+  slot->second = std::move(db);
+  const thrift::AdjacencyDatabase& newDb = slot->second;
 
   // both sides sorted by Link::operator< so one merge pass finds the diff
   const auto oldLinks = orderedLinksFromNode(nodeName);

@@ -270,6 +270,10 @@ class LinkState {
       thrift::AdjacencyDatabase const& adjacencyDb,
       LinkStateMetric holdUpTtl = 0,
       LinkStateMetric holdDownTtl = 0);
+  LinkStateChange updateAdjacencyDatabase(
+      thrift::AdjacencyDatabase&& adjacencyDb,
+      LinkStateMetric holdUpTtl = 0,
+      LinkStateMetric holdDownTtl = 0);
   LinkStateChange deleteAdjacencyDatabase(const std::string& nodeName);
 
   std::optional<LinkStateMetric> getMetricFromAToB(

@@ -11,6 +11,7 @@
 
 #include "../host/LinkState.h"
 #include "../host/PrefixState.h"
+#include "../host/Publication.h"
 #include "../host/RouteTable.h"
 #include "../host/SpfSolver.h"
 #include "../host/Util.h"
@@ -61,6 +62,75 @@ struct AreaMapHolder {
   AreaMapHolder() = default;
   AreaMapHolder(const AreaMapHolder&) = delete;
 };
+
+py::object pyAddr(py::module_& T, const thrift::BinaryAddress& a) {
+  return T.attr("BinaryAddress")(py::bytes(a.addr), a.ifName ? py::object(py::str(*a.ifName)) : py::none());
+}
+
+py::object pyAdjDb(const thrift::AdjacencyDatabase& db) {
+  py::module_ T = py::module_::import("openr_amd.thrift");
+  py::list adjs;
+  for (const auto& a : db.adjacencies) {
+    adjs.append(T.attr("Adjacency")(a.otherNodeName, a.ifName, pyAddr(T, a.nextHopV6),
+                                    pyAddr(T, a.nextHopV4), a.metric, a.adjLabel, a.isOverloaded,
+                                    a.rtt, a.timestamp, a.weight, a.otherIfName));
+  }
+  return T.attr("AdjacencyDatabase")(db.thisNodeName, db.isOverloaded, adjs, db.nodeLabel, db.area);
+}
+
+py::object pyPrefixDb(const thrift::PrefixDatabase& db) {
+  py::module_ T = py::module_::import("openr_amd.thrift");
+  py::list entries;
+  for (const auto& e : db.prefixEntries) {
+    py::object mv = py::none();
+    if (e.mv) {
+      py::list ms;
+      for (const auto& me : e.mv->metrics) {
+        ms.append(T.attr("MetricEntity")(me.type, me.priority, (int)me.op, me.isBestPathTieBreaker,
+                                         py::cast(me.metric)));
+      }
+      mv = T.attr("MetricVector")(e.mv->version, ms);
+    }
+    entries.append(T.attr("PrefixEntry")(
+        T.attr("IpPrefix")(pyAddr(T, e.prefix.prefixAddress), e.prefix.prefixLength), (int)e.type,
+        e.data ? py::object(py::bytes(*e.data)) : py::none(), (int)e.forwardingType,
+        (int)e.forwardingAlgorithm, e.ephemeral ? py::object(py::bool_(*e.ephemeral)) : py::none(), mv,
+        e.minNexthop ? py::object(py::int_(*e.minNexthop)) : py::none(),
+        e.prependLabel ? py::object(py::int_(*e.prependLabel)) : py::none()));
+  }
+  return T.attr("PrefixDatabase")(db.thisNodeName, entries, db.deletePrefix, db.area);
+}
+
+thrift::Publication toPublication(const std::string& area, py::dict keyVals, py::list expired) {
+  thrift::Publication pub;
+  pub.area = area;
+  for (auto kv : keyVals) {
+    thrift::Value v;
+    if (!kv.second.is_none()) {
+      v.value = kv.second.cast<std::string>();
+    } else {
+      v.ttlVersion = 1;
+    }
+    pub.keyVals.emplace(kv.first.cast<std::string>(), std::move(v));
+  }
+  for (auto k : expired) {
+    pub.expiredKeys.push_back(k.cast<std::string>());
+  }
+  return pub;
+}
+
+py::dict pendingToPy(const PendingUpdates& p) {
+  py::dict d;
+  py::set prefixes;
+  for (const auto& x : p.updatedPrefixes) {
+    prefixes.add(prefixKey(x));
+  }
+  d["needsFullRebuild"] = p.needsFullRebuild;
+  d["updatedPrefixes"] = prefixes;
+  d["count"] = p.count;
+  d["needsRouteUpdate"] = p.needsRouteUpdate();
+  return d;
+}
 
 } // namespace
 
@@ -238,6 +308,77 @@ PYBIND11_MODULE(_openr_spf, m) {
                               .count();
         return py::make_tuple((long)r.size(), us);
       });
+
+  // CompactProtocol blobs and Decision::processPublication
+  m.def("compact_encode_adj_db", [](py::handle db) { return py::bytes(compact::encode(toAdjDb(db))); });
+  m.def(
+      "compact_encode_prefix_db",
+      [](py::handle db, py::object areaStacks) {
+        if (areaStacks.is_none()) {
+          return py::bytes(compact::encode(toPrefixDb(db)));
+        }
+        auto st = areaStacks.cast<std::vector<std::vector<std::string>>>();
+        return py::bytes(compact::encode(toPrefixDb(db), &st));
+      },
+      py::arg("db"), py::arg("area_stacks") = py::none());
+  m.def("compact_decode_adj_db", [](py::bytes b) {
+    try {
+      return pyAdjDb(compact::decodeAdjacencyDatabase(std::string(b)));
+    } catch (const compact::DecodeError& e) {
+      throw py::value_error(e.what());
+    }
+  });
+  m.def("compact_decode_prefix_db", [](py::bytes b) {
+    try {
+      auto w = compact::decodePrefixDatabase(std::string(b));
+      return py::make_tuple(pyPrefixDb(w.db), py::cast(w.areaStacks),
+                            w.perPrefixKey ? py::object(py::bool_(*w.perPrefixKey)) : py::none());
+    } catch (const compact::DecodeError& e) {
+      throw py::value_error(e.what());
+    }
+  });
+  m.def("parse_prefix_key", [](const std::string& key) -> py::object {
+    auto k = parsePrefixKey(key);
+    if (!k) {
+      return py::none();
+    }
+    return py::make_tuple(k->node, k->area, prefixKey(k->prefix));
+  });
+  m.def("get_node_name_from_key", &getNodeNameFromKey);
+
+  py::class_<PublicationIngest>(m, "PublicationIngest")
+      .def(py::init<std::string, bool>(), py::arg("my_node_name"), py::arg("enable_ordered_fib") = false)
+      .def(
+          "processPublication",
+          [](PublicationIngest& d, AreaMapHolder& areas, PrefixState& ps, const std::string& area,
+             py::dict keyVals, py::list expiredKeys) {
+            const auto pub = toPublication(area, keyVals, expiredKeys);
+            try {
+              return pendingToPy(d.processPublication(pub, areas.map, ps));
+            } catch (const CheckFailure& e) {
+              throw std::runtime_error(e.what());
+            }
+          },
+          py::arg("areas"), py::arg("prefix_state"), py::arg("area"), py::arg("key_vals"),
+          py::arg("expired_keys") = py::list())
+      .def(
+          "processPublicationTimed",
+          [](PublicationIngest& d, AreaMapHolder& areas, PrefixState& ps, const std::string& area,
+             py::dict keyVals, py::list expiredKeys) {
+            // (count, microseconds of processPublication alone: decode + LinkState /
+            // PrefixState updates, the publication already in C++ form)
+            const auto pub = toPublication(area, keyVals, expiredKeys);
+            const auto t0 = std::chrono::steady_clock::now();
+            const auto& p = d.processPublication(pub, areas.map, ps);
+            const double us = std::chrono::duration<double, std::micro>(
+                                  std::chrono::steady_clock::now() - t0)
+                                  .count();
+            return py::make_tuple(p.count, us);
+          },
+          py::arg("areas"), py::arg("prefix_state"), py::arg("area"), py::arg("key_vals"),
+          py::arg("expired_keys") = py::list())
+      .def("pending", [](PublicationIngest& d) { return pendingToPy(d.pending()); })
+      .def("resetPending", [](PublicationIngest& d) { d.pending().reset(); });
 
   py::class_<PrefixState>(m, "PrefixState")
       .def(py::init<>())

@@ -286,3 +286,61 @@ def test_route_db_after_byte_ingest_gpu(gpu_ready, seed):
                     for kind in a}
             pytest.fail(f"{node}: differing keys {diff}; first: "
                         f"{[(a[k].get(x), b[k].get(x)) for k, v in diff.items() for x in v[:1]]}")
+
+
+@pytest.mark.gpu
+def test_ordered_fib_holds_after_byte_ingest_gpu(gpu_ready):
+    """enable_ordered_fib_programming: processPublication derives holdUp /
+    holdDown TTLs from hop counts of the current LinkState (Decision.cpp:
+    1670-1680).  The oracle gets the same TTLs from its own hop queries; the
+    hold state and every RouteDb must match while the holds drain."""
+    import openr_amd._openr_spf as E
+    from oracle import build as obuild
+
+    obuild.build()
+    from oracle import _oracle_ref as O
+
+    names, adj_dbs, prefix_dbs = RZ.random_network(977, n_nodes=24, n_links=50, parallel_prob=0.0)
+    me = names[0]
+    ba, bp = E.AreaLinkStates(), E.PrefixState()
+    ing = E.PublicationIngest(me, True)
+    rng = random.Random(3)
+    order = list(adj_dbs["0"])
+    rng.shuffle(order)
+    oa = O.AreaLinkStates()
+    ols = oa.add("0")
+    for db in order:
+        up = down = 0
+        h = ols.getHopsFromAToB(me, db.thisNodeName)
+        if h is not None:
+            up = h
+            down = ols.getMaxHopsToNode(db.thisNodeName) - h
+        ols.updateAdjacencyDatabase(db, up, down)
+        ing.processPublication(ba, bp, "0", {f"adj:{db.thisNodeName}": E.compact_encode_adj_db(db)})
+    op = O.PrefixState()
+    for p in prefix_dbs:
+        op.updatePrefixDatabase(p)
+        ing.processPublication(ba, bp, p.area, {f"prefix:{p.thisNodeName}": E.compact_encode_prefix_db(p)})
+    # churn: raise one link's metric on both ends -> holds
+    def ttls(db):
+        h = ols.getHopsFromAToB(me, db.thisNodeName)
+        return (h, ols.getMaxHopsToNode(db.thisNodeName) - h) if h is not None else (0, 0)
+
+    # a reachable node whose hold-down TTL is positive: a metric increase
+    # ("bringing down") is then held for that many decrements
+    victim = next(db for db in order if db.adjacencies and ttls(db)[1] > 0)
+    victim.adjacencies[0].metric += 7
+    up, down = ttls(victim)
+    ols.updateAdjacencyDatabase(victim, up, down)
+    assert ols.hasHolds()
+    ing.processPublication(ba, bp, "0", {f"adj:{victim.thisNodeName}": E.compact_encode_adj_db(victim)})
+    es = E.SpfSolver(me, True, False)
+    os_ = O.SpfSolver(me, True, False)
+    for _ in range(8):
+        assert ba["0"].hasHolds() == ols.hasHolds()
+        for node in names[:6]:
+            assert es.buildRouteDb(node, ba, bp) == os_.buildRouteDb(node, oa, op), node
+        if not ols.hasHolds():
+            break
+        ba["0"].decrementHolds()
+        ols.decrementHolds()

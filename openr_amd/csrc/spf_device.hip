@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -45,12 +46,15 @@
 #include <vector>
 
 #include "openr_spf.h"
+#include "host/Parallel.h"
 
 namespace {
 
 constexpr uint32_t kBlock = 512;           // threads per workgroup (8 waves)
 constexpr uint32_t kWaves = kBlock / 64;
 constexpr uint32_t kInf32 = 0xFFFFFFFFu;
+// nodes per host-pool work item of the graph preparation loops
+constexpr uint32_t kHostBlock = 2048;
 constexpr uint32_t kCtlWords = 32;         // qlen + scan scratch (<= 16 waves + 1)
 constexpr size_t kLdsLimit = 160 * 1024;   // gfx950 LDS per CU
 constexpr uint32_t kIgnLdsMax = 2048;      // ignore-list entries staged in LDS
@@ -2625,14 +2629,32 @@ void free_query(spf_query* q) {
 // fast-path weights, exactness, uniformity and per-neighbour cheapest metric
 int upload_weights(spf_graph* g) {
   const uint32_t E = g->E, V = g->V;
+  const unsigned nth = openr::hostThreads(E, 1u << 16);
+  const uint32_t nblk = (V + kHostBlock - 1) / kHostBlock;
+  auto blocks = [&](auto&& fn) {
+    openr::parallelFor(nblk, nth, [&](size_t b, unsigned w) {
+      const uint32_t u1 = std::min<uint32_t>(V, (uint32_t)(b + 1) * kHostBlock);
+      for (uint32_t u = (uint32_t)b * kHostBlock; u < u1; ++u) {
+        fn(u, w);
+      }
+    }, 1);
+  };
+  std::vector<uint64_t> wmax(nth, 0);
+  std::vector<uint8_t> wexact(nth, 0);
+  blocks([&](uint32_t u, unsigned w) {
+    for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
+      const uint64_t m = g->w64[e];
+      if (m == 0 || m > 0x7FFFFFFFull) {
+        wexact[w] = 1;
+      }
+      wmax[w] = std::max(wmax[w], m);
+    }
+  });
   uint64_t maxw = 0;
   bool exact = false;
-  for (uint32_t e = 0; e < E; ++e) {
-    const uint64_t m = g->w64[e];
-    if (m == 0 || m > 0x7FFFFFFFull) {
-      exact = true;
-    }
-    maxw = std::max(maxw, m);
+  for (unsigned w = 0; w < nth; ++w) {
+    maxw = std::max(maxw, wmax[w]);
+    exact = exact || wexact[w];
   }
   if (!exact && V > 1 && maxw > 0 &&
       (unsigned __int128)maxw * (V - 1) >= 0xFFFFFFFFull) {
@@ -2649,20 +2671,20 @@ int upload_weights(spf_graph* g) {
     g->uniform = same ? (uint32_t)c : 0;
   }
   std::vector<uint32_t> wout(E), win(E);
-  for (uint32_t e = 0; e < E; ++e) {
-    wout[e] = (uint32_t)std::min<uint64_t>(g->w64[e], 0xFFFFFFFFull);
-  }
-  for (uint32_t e = 0; e < E; ++e) {
-    win[e] = wout[g->rev[e]];
-  }
+  blocks([&](uint32_t u, unsigned) {
+    for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
+      wout[e] = (uint32_t)std::min<uint64_t>(g->w64[e], 0xFFFFFFFFull);
+    }
+  });
   // cheapest usable link to each distinct neighbour (parallel links)
   g->nbr_w.assign(g->nbrs.size(), 0xFFFFFFFFu);
-  for (uint32_t u = 0; u < V; ++u) {
+  blocks([&](uint32_t u, unsigned) {
     for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
+      win[e] = (uint32_t)std::min<uint64_t>(g->w64[g->rev[e]], 0xFFFFFFFFull);
       uint32_t& w = g->nbr_w[g->nbr_off[u] + g->slot[e]];
       w = std::min(w, wout[e]);
     }
-  }
+  });
   if (E) {
     if (!g->d_wout) {
       HIP_TRY(hipMalloc((void**)&g->d_wout, E * 4));
@@ -2891,15 +2913,30 @@ int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
       return fail(SPF_E_INVALID, "row_ptr not monotone");
     }
   }
-  for (uint32_t u = 0; u < V; ++u) {
-    for (uint32_t e = desc->row_ptr[u]; e < desc->row_ptr[u + 1]; ++e) {
-      const uint32_t v = desc->col[e], r = desc->rev[e];
-      if (v >= V || v == u || r >= E || desc->rev[r] != e ||
-          desc->col[r] != u || desc->link_id[e] >= desc->num_links ||
-          desc->link_id[r] != desc->link_id[e]) {
-        return fail(SPF_E_INVALID, "inconsistent half-edge at " +
-                                       std::to_string(e));
+  {
+    // half-edge consistency, node blocks on the host pool; the lowest bad
+    // edge is reported (same message as a sequential scan)
+    std::atomic<uint32_t> bad{kInf32};
+    const uint32_t nblk = (V + kHostBlock - 1) / kHostBlock;
+    openr::parallelFor(nblk, openr::hostThreads(E, 1u << 16), [&](size_t b, unsigned) {
+      const uint32_t u1 = std::min<uint32_t>(V, (uint32_t)(b + 1) * kHostBlock);
+      for (uint32_t u = (uint32_t)b * kHostBlock; u < u1; ++u) {
+        for (uint32_t e = desc->row_ptr[u]; e < desc->row_ptr[u + 1]; ++e) {
+          const uint32_t v = desc->col[e], r = desc->rev[e];
+          if (v >= V || v == u || r >= E || desc->rev[r] != e ||
+              desc->col[r] != u || desc->link_id[e] >= desc->num_links ||
+              desc->link_id[r] != desc->link_id[e]) {
+            uint32_t cur = bad.load();
+            while (e < cur && !bad.compare_exchange_weak(cur, e)) {
+            }
+            return;
+          }
+        }
       }
+    }, 1);
+    if (bad.load() != kInf32) {
+      return fail(SPF_E_INVALID, "inconsistent half-edge at " +
+                                     std::to_string(bad.load()));
     }
   }
   const int ndev = spf_device_count();
@@ -2928,20 +2965,38 @@ int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
     }
   }
   // distinct neighbours per node (ascending id = name order) and edge slots
+  // (sorted unique neighbours of u staged in scratch[row[u] ..], counted,
+  // then packed; node blocks on the host pool)
   g->nbr_off.assign(V + 1, 0);
   g->slot.assign(E, 0);
-  std::vector<uint32_t> tmp;
-  for (uint32_t u = 0; u < V; ++u) {
-    tmp.assign(g->col.begin() + g->row[u], g->col.begin() + g->row[u + 1]);
-    std::sort(tmp.begin(), tmp.end());
-    tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
-    g->nbr_off[u + 1] = g->nbr_off[u] + (uint32_t)tmp.size();
-    g->nbrs.insert(g->nbrs.end(), tmp.begin(), tmp.end());
-    for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
-      g->slot[e] = (uint32_t)(std::lower_bound(tmp.begin(), tmp.end(),
-                                               g->col[e]) -
-                              tmp.begin());
+  {
+    std::vector<uint32_t> scratch(g->col);
+    const uint32_t nblk = (V + kHostBlock - 1) / kHostBlock;
+    const unsigned nth = openr::hostThreads(E, 1u << 16);
+    openr::parallelFor(nblk, nth, [&](size_t b, unsigned) {
+      const uint32_t u1 = std::min<uint32_t>(V, (uint32_t)(b + 1) * kHostBlock);
+      for (uint32_t u = (uint32_t)b * kHostBlock; u < u1; ++u) {
+        uint32_t* lo = scratch.data() + g->row[u];
+        uint32_t* hi = scratch.data() + g->row[u + 1];
+        std::sort(lo, hi);
+        hi = std::unique(lo, hi);
+        g->nbr_off[u + 1] = (uint32_t)(hi - lo);
+        for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
+          g->slot[e] = (uint32_t)(std::lower_bound(lo, hi, g->col[e]) - lo);
+        }
+      }
+    }, 1);
+    for (uint32_t u = 0; u < V; ++u) {
+      g->nbr_off[u + 1] += g->nbr_off[u];
     }
+    g->nbrs.resize(g->nbr_off[V]);
+    openr::parallelFor(nblk, nth, [&](size_t b, unsigned) {
+      const uint32_t u1 = std::min<uint32_t>(V, (uint32_t)(b + 1) * kHostBlock);
+      for (uint32_t u = (uint32_t)b * kHostBlock; u < u1; ++u) {
+        std::copy_n(scratch.data() + g->row[u], g->nbr_off[u + 1] - g->nbr_off[u],
+                    g->nbrs.data() + g->nbr_off[u]);
+      }
+    }, 1);
   }
   // lanes per node: the median degree, rounded to a power of two in [4, 64]
   {

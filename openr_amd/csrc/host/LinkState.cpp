@@ -633,6 +633,7 @@ LinkState::LinkState(LinkState&& o) noexcept
       spfResultsHops_(std::move(o.spfResultsHops_)),
       kthPathResults_(std::move(o.kthPathResults_)),
       kthMu_(std::move(o.kthMu_)),
+      kthFill_(std::move(o.kthFill_)),
       engine_(std::move(o.engine_)) {}
 
 size_t LinkState::LinkPtrHash::operator()(const std::shared_ptr<Link>& l) const {
@@ -708,22 +709,31 @@ void LinkState::patchMemo(
   eng.kthPrefetch.clear();
   eng.isolated.clear();
   const auto t0 = std::chrono::steady_clock::now();
-  if (transit) {
-    const int s = spf_graph_set_transit(eng.graph, eng.overloaded.data());
-    if (s != SPF_OK) {
-      engineFailure("spf_graph_set_transit", s);
+  // The host mirrors (eng.overloaded, eng.metric) were / are updated before
+  // the device upload: if an upload fails, drop the whole engine so the next
+  // access rebuilds the device graph from linkMap_ instead of comparing
+  // against mirrors that no longer describe the device state.
+  try {
+    if (transit) {
+      const int s = spf_graph_set_transit(eng.graph, eng.overloaded.data());
+      if (s != SPF_OK) {
+        engineFailure("spf_graph_set_transit", s);
+      }
     }
-  }
-  if (!edges.empty()) {
-    for (size_t i = 0; i < edges.size(); ++i) {
-      eng.metric[edges[i]] = metrics[i];
+    if (!edges.empty()) {
+      for (size_t i = 0; i < edges.size(); ++i) {
+        eng.metric[edges[i]] = metrics[i];
+      }
+      const int s = spf_graph_patch_metrics(
+          eng.graph, (uint32_t)edges.size(), edges.data(), metrics.data());
+      if (s != SPF_OK) {
+        engineFailure("spf_graph_patch_metrics", s);
+      }
+      eng.exact = spf_graph_needs_exact(eng.graph) != 0;
     }
-    const int s = spf_graph_patch_metrics(
-        eng.graph, (uint32_t)edges.size(), edges.data(), metrics.data());
-    if (s != SPF_OK) {
-      engineFailure("spf_graph_patch_metrics", s);
-    }
-    eng.exact = spf_graph_needs_exact(eng.graph) != 0;
+  } catch (...) {
+    clearMemo();
+    throw;
   }
   Counters::add("decision.graph_patches", 1);
   Counters::add(
@@ -737,14 +747,14 @@ void LinkState::addLink(std::shared_ptr<Link> link) {
   if (!linkMap_[link->firstNodeName()].insert(link).second ||
       !linkMap_[link->secondNodeName()].insert(link).second ||
       !allLinks_.insert(link).second) {
-    throw std::logic_error("addLink: duplicate link " + link->toString());
+    throw CheckFailure("addLink: duplicate link " + link->toString());
   }
 }
 
 void LinkState::removeLink(std::shared_ptr<Link> link) {
   if (!linkMap_.at(link->firstNodeName()).erase(link) ||
       !linkMap_.at(link->secondNodeName()).erase(link) || !allLinks_.erase(link)) {
-    throw std::logic_error("removeLink: missing link " + link->toString());
+    throw CheckFailure("removeLink: missing link " + link->toString());
   }
 }
 
@@ -756,7 +766,7 @@ void LinkState::removeNode(const std::string& nodeName) {
   for (const auto& link : it->second) {
     if (!linkMap_.at(link->getOtherNodeName(nodeName)).erase(link) ||
         !allLinks_.erase(link)) {
-      throw std::logic_error("removeNode: inconsistent link set");
+      throw CheckFailure("removeNode: inconsistent link set");
     }
   }
   linkMap_.erase(it);
@@ -1225,12 +1235,21 @@ std::vector<LinkState::Path> const& LinkState::getKthPaths(
     throw std::invalid_argument("getKthPaths: k must be >= 1");
   }
   KthKey key{src, dest, k};
-  {
+  auto lookup = [&]() -> const std::vector<Path>* {
     std::shared_lock<std::shared_mutex> rd(*kthMu_);
     auto found = kthPathResults_.find(key);
-    if (found != kthPathResults_.end()) {
-      return found->second;
-    }
+    return found == kthPathResults_.end() ? nullptr : &found->second;
+  };
+  if (auto hit = lookup()) {
+    return *hit;
+  }
+  // once-only fill: concurrent callers of the same key wait for the first
+  std::mutex& fillMu = k == 1 ? kthFill_->k1[KthKeyHash{}(key) % KthFillLocks::kStripes]
+      : k == 2 ? kthFill_->k2[KthKeyHash{}(key) % KthFillLocks::kStripes]
+               : kthFill_->kN;
+  std::lock_guard<std::mutex> fill(fillMu);
+  if (auto hit = lookup()) {
+    return *hit;
   }
   // linksToIgnore of the reference (LinkState.cpp:766-775), as the sorted
   // ids of the links on the paths of ranks < k (every path link is an up

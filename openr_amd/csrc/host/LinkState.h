@@ -23,6 +23,7 @@
 #include <limits>
 #include <memory>
 #include <optional>
+#include <mutex>
 #include <shared_mutex>
 #include <string>
 #include <unordered_map>
@@ -371,6 +372,15 @@ class LinkState {
   // getKthPaths / spfView may be called from the worker threads of one
   // RouteDb build (Parallel.h): memo hits share the lock, fills take it
   mutable std::unique_ptr<std::shared_mutex> kthMu_ = std::make_unique<std::shared_mutex>();
+  // once-only fills of kthPathResults_ (the reference memo runs each
+  // (src, dst, k) once, and decision.spf_runs counts it once): a fill holds
+  // the stripe of its key; stripes are per k (k = 1, 2; one lock for k >= 3)
+  // and a k-fill only ever takes stripes of smaller k, so there is no cycle
+  struct KthFillLocks {
+    static constexpr size_t kStripes = 64;
+    std::mutex k1[kStripes], k2[kStripes], kN;
+  };
+  mutable std::unique_ptr<KthFillLocks> kthFill_ = std::make_unique<KthFillLocks>();
   mutable std::unique_ptr<Engine> engine_;
 };
 

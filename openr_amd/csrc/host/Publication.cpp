@@ -823,48 +823,58 @@ const PendingUpdates& PublicationIngest::processPublication(
     if (!val.value) {
       continue; // TTL refresh
     }
-    try {
-      if (key.compare(0, kAdj.size(), kAdj) == 0) {
-        auto db = compact::decodeAdjacencyDatabase(*val.value);
-        db.area = area;
-        if (nodeName != db.thisNodeName) {
-          throw CheckFailure("CHECK_EQ(nodeName, adjacencyDb.thisNodeName) failed: " +
-                                 nodeName + " vs " + db.thisNodeName);
-        }
-        LinkStateMetric holdUp = 0, holdDown = 0;
-        if (enableOrderedFib_) {
-          if (auto h = als.getHopsFromAToB(myNodeName_, db.thisNodeName)) {
-            holdUp = *h;
-            holdDown = als.getMaxHopsToNode(db.thisNodeName) - holdUp;
-          }
-        }
-        Counters::add("decision.adj_db_update", 1);
-        const std::string node = db.thisNodeName;
-        applyLs(node, als.updateAdjacencyDatabase(std::move(db), holdUp, holdDown));
+    // Only deserialisation failures are per-key errors (the reference logs
+    // them and moves on, Decision.cpp:1718-1721).  Everything after a
+    // successful decode -- CHECK failures, engine / device errors, bad_alloc --
+    // propagates: the reference aborts on those (Decision.cpp:1392-1404) and a
+    // half-applied update must never be counted as a decode error.
+    if (key.compare(0, kAdj.size(), kAdj) == 0) {
+      thrift::AdjacencyDatabase db;
+      try {
+        db = compact::decodeAdjacencyDatabase(*val.value);
+      } catch (const compact::DecodeError&) {
+        Counters::add("decision.publication_decode_errors", 1);
         continue;
       }
-      if (key.compare(0, kPrefix.size(), kPrefix) == 0) {
-        auto wire = compact::decodePrefixDatabase(*val.value);
-        if (nodeName != wire.db.thisNodeName) {
-          throw CheckFailure("CHECK_EQ(nodeName, prefixDb.thisNodeName) failed: " +
-                                 nodeName + " vs " + wire.db.thisNodeName);
-        }
-        auto nodeDb = updateNodePrefixDatabase(key, wire, areaLinkStates);
-        if (!nodeDb) {
-          continue;
-        }
-        nodeDb->area = area;
-        Counters::add("decision.prefix_db_update", 1);
-        applyPs(prefixState.updatePrefixDatabase(*nodeDb));
-        continue;
+      db.area = area;
+      if (nodeName != db.thisNodeName) {
+        throw CheckFailure("CHECK_EQ(nodeName, adjacencyDb.thisNodeName) failed: " +
+                               nodeName + " vs " + db.thisNodeName);
       }
-      // fibtime: keys only feed Decision's fib-time estimate (not this path)
-    } catch (const CheckFailure&) {
-      throw;
-    } catch (const std::exception&) {
-      // the reference logs and moves on to the next key (Decision.cpp:1718-1721)
-      Counters::add("decision.publication_decode_errors", 1);
+      LinkStateMetric holdUp = 0, holdDown = 0;
+      if (enableOrderedFib_) {
+        if (auto h = als.getHopsFromAToB(myNodeName_, db.thisNodeName)) {
+          holdUp = *h;
+          holdDown = als.getMaxHopsToNode(db.thisNodeName) - holdUp;
+        }
+      }
+      Counters::add("decision.adj_db_update", 1);
+      const std::string node = db.thisNodeName;
+      applyLs(node, als.updateAdjacencyDatabase(std::move(db), holdUp, holdDown));
+      continue;
     }
+    if (key.compare(0, kPrefix.size(), kPrefix) == 0) {
+      compact::PrefixDbWire wire;
+      try {
+        wire = compact::decodePrefixDatabase(*val.value);
+      } catch (const compact::DecodeError&) {
+        Counters::add("decision.publication_decode_errors", 1);
+        continue;
+      }
+      if (nodeName != wire.db.thisNodeName) {
+        throw CheckFailure("CHECK_EQ(nodeName, prefixDb.thisNodeName) failed: " +
+                               nodeName + " vs " + wire.db.thisNodeName);
+      }
+      auto nodeDb = updateNodePrefixDatabase(key, wire, areaLinkStates);
+      if (!nodeDb) {
+        continue;
+      }
+      nodeDb->area = area;
+      Counters::add("decision.prefix_db_update", 1);
+      applyPs(prefixState.updatePrefixDatabase(*nodeDb));
+      continue;
+    }
+    // fibtime: keys only feed Decision's fib-time estimate (not this path)
   }
   for (const auto& key : pub.expiredKeys) {
     const std::string nodeName = getNodeNameFromKey(key);

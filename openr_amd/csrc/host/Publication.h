@@ -74,12 +74,6 @@ std::string encode(
 
 } // namespace compact
 
-// A reference CHECK on the path failed (fatal there; thrown here and never
-// swallowed by processPublication's per-key error handling).
-struct CheckFailure : std::logic_error {
-  using std::logic_error::logic_error;
-};
-
 // Decision's pending-update state (Decision.h:105-160).
 struct PendingUpdates {
   bool needsFullRebuild{false};

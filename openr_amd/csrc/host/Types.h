@@ -18,6 +18,7 @@
 #include <map>
 #include <optional>
 #include <set>
+#include <stdexcept>
 #include <string>
 #include <tuple>
 #include <unordered_map>
@@ -25,6 +26,14 @@
 #include <vector>
 
 namespace openr {
+
+// A reference CHECK on the path failed (glog CHECK aborts the daemon there,
+// e.g. LinkState.cpp:423-433; thrown here and never swallowed as a
+// per-key or per-prefix error).
+struct CheckFailure : std::logic_error {
+  using std::logic_error::logic_error;
+};
+
 namespace thrift {
 
 enum class PrefixType : int32_t {

@@ -149,8 +149,29 @@ PYBIND11_MODULE(_openr_spf, m) {
   });
   m.def("reset_counters", &Counters::reset);
 
+  // HoldableValue<bool> / HoldableValue<LinkStateMetric> (LinkState.h:36-58)
+  py::class_<HoldableValue<bool>>(m, "HoldableValueBool")
+      .def(py::init<bool>())
+      .def("value", [](const HoldableValue<bool>& h) { return h.value(); })
+      .def("hasHold", &HoldableValue<bool>::hasHold)
+      .def("decrementTtl", &HoldableValue<bool>::decrementTtl)
+      .def("updateValue", &HoldableValue<bool>::updateValue);
+  py::class_<HoldableValue<LinkStateMetric>>(m, "HoldableValueMetric")
+      .def(py::init<LinkStateMetric>())
+      .def("value", [](const HoldableValue<LinkStateMetric>& h) { return h.value(); })
+      .def("hasHold", &HoldableValue<LinkStateMetric>::hasHold)
+      .def("decrementTtl", &HoldableValue<LinkStateMetric>::decrementTtl)
+      .def("updateValue", &HoldableValue<LinkStateMetric>::updateValue);
+
   py::class_<Link, std::shared_ptr<Link>>(m, "Link")
       .def(py::init<std::string, std::string, std::string, std::string, std::string>())
+      .def_static("fromAdjacencies",
+                  [](const std::string& area, const std::string& n1, py::handle a1,
+                     const std::string& n2, py::handle a2) {
+                    return std::make_shared<Link>(area, n1, toAdjacency(a1), n2, toAdjacency(a2));
+                  })
+      .def("setMetricFromNode", &Link::setMetricFromNode)
+      .def("setOverloadFromNode", &Link::setOverloadFromNode)
       .def("key", [](const Link& l) { return linkKey(l); })
       .def("getArea", &Link::getArea)
       .def("getOtherNodeName", &Link::getOtherNodeName)
@@ -417,6 +438,35 @@ PYBIND11_MODULE(_openr_spf, m) {
              return out;
            });
 
+  py::class_<DecisionRouteDb>(m, "DecisionRouteDb")
+      .def(py::init<>())
+      .def("to_dict", [](const DecisionRouteDb& db) { return routeDbToPy(db); });
+  // getRouteDelta (Decision.cpp:47-85) on the host RouteDbs
+  m.def("getRouteDelta", [](const DecisionRouteDb& newDb, const DecisionRouteDb& oldDb) {
+    const DecisionRouteUpdate u = getRouteDelta(newDb, oldDb);
+    DecisionRouteDb upd;
+    for (const auto& e : u.unicastRoutesToUpdate) {
+      upd.unicastEntries.emplace(e.prefix, e);
+    }
+    for (const auto& e : u.mplsRoutesToUpdate) {
+      upd.mplsEntries.emplace(e.label, e);
+    }
+    py::dict all = routeDbToPy(upd);
+    py::list udel, mdel;
+    for (const auto& p : u.unicastRoutesToDelete) {
+      udel.append(prefixKey(p));
+    }
+    for (const auto l : u.mplsRoutesToDelete) {
+      mdel.append(py::int_(l));
+    }
+    py::dict out;
+    out["unicastRoutesToUpdate"] = all["unicast"];
+    out["unicastRoutesToDelete"] = udel;
+    out["mplsRoutesToUpdate"] = all["mpls"];
+    out["mplsRoutesToDelete"] = mdel;
+    return out;
+  });
+
   py::class_<SpfSolver>(m, "SpfSolver")
       .def(py::init<std::string, bool, bool, bool, bool, bool>(), py::arg("myNodeName"),
            py::arg("enableV4"), py::arg("computeLfaPaths"), py::arg("enableOrderedFib") = false,
@@ -453,6 +503,15 @@ PYBIND11_MODULE(_openr_spf, m) {
                                        std::chrono::steady_clock::now() - t1)
                                        .count();
              return py::make_tuple(nu, nm, us, freeUs);
+           })
+      .def("buildRouteDbObject",
+           [](SpfSolver& s, const std::string& node, const AreaMapHolder& areas,
+              const PrefixState& ps) -> py::object {
+             auto db = s.buildRouteDb(node, areas.map, ps);
+             if (!db) {
+               return py::none();
+             }
+             return py::cast(std::move(*db));
            })
       .def("staticRoutesUpdated", &SpfSolver::staticRoutesUpdated)
       .def("pushRoutesDeltaUpdates",

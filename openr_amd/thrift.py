@@ -179,9 +179,10 @@ def toBinaryAddress(addr: str) -> BinaryAddress:
 
 
 def toIpPrefix(prefix: str) -> IpPrefix:
+    # NetworkUtil.h:120-123: folly::IPAddress::createNetwork(prefix), whose
+    # applyMask defaults to true ("2401:1::10.1.1.1/32" -> 2401:1::/32)
     net = ipaddress.ip_network(prefix, strict=False)
-    addr = ipaddress.ip_address(prefix.split("/")[0])
-    return IpPrefix(BinaryAddress(addr.packed), net.prefixlen)
+    return IpPrefix(BinaryAddress(net.network_address.packed), net.prefixlen)
 
 
 def prefixToString(key) -> str:

@@ -648,6 +648,37 @@ struct RouteDb {
   std::unordered_map<int32_t, std::unordered_set<NextHopThrift>> mpls;
 };
 using Areas = std::unordered_map<std::string, Graph>;
+
+// RibUnicastEntry::operator== (RibEntry.h:31-34, 60-66): prefix, best entry,
+// best next hop, doNotInstall and the next-hop SET
+inline bool sameEntry(const UEntry& a, const UEntry& b) {
+  return a.nhs == b.nhs && a.best == b.best && a.bestNh == b.bestNh && a.dni == b.dni;
+}
+struct RouteDelta {
+  std::vector<std::pair<IpPrefix, UEntry>> uniUpdate;
+  std::vector<IpPrefix> uniDelete;
+  std::vector<std::pair<int32_t, std::unordered_set<NextHopThrift>>> mplsUpdate;
+  std::vector<int32_t> mplsDelete;
+};
+// Decision.cpp:47-85 getRouteDelta(newDb, oldDb)
+inline RouteDelta routeDelta(const RouteDb& nw, const RouteDb& old) {
+  RouteDelta d;
+  for (const auto& [p, e] : nw.unicast) {
+    auto it = old.unicast.find(p);
+    if (it != old.unicast.end() && sameEntry(it->second, e)) continue;
+    d.uniUpdate.emplace_back(p, e);
+  }
+  for (const auto& [p, _] : old.unicast)
+    if (!nw.unicast.count(p)) d.uniDelete.push_back(p);
+  for (const auto& [l, e] : nw.mpls) {
+    auto it = old.mpls.find(l);
+    if (it != old.mpls.end() && it->second == e) continue;
+    d.mplsUpdate.emplace_back(l, e);
+  }
+  for (const auto& [l, _] : old.mpls)
+    if (!nw.mpls.count(l)) d.mplsDelete.push_back(l);
+  return d;
+}
 struct SPH {
   size_t operator()(const std::pair<std::string, std::string>& p) const {
     return h128(std::hash<std::string>()(p.first), std::hash<std::string>()(p.second));
@@ -660,6 +691,25 @@ class Solver {
   Solver(bool v4, bool lfa, bool dryRun, bool useIgp)
       : v4_(v4), lfa_(lfa), dryRun_(dryRun), useIgp_(useIgp) {}
   std::unordered_map<int32_t, std::vector<NextHopThrift>> staticMpls;
+  // Decision.cpp:281-285 / 868-907: queued RouteDatabaseDeltas of static
+  // MPLS routes, squashed in order (a later update / delete of a label wins)
+  std::vector<std::pair<std::vector<std::pair<int32_t, std::vector<NextHopThrift>>>,
+                        std::vector<int32_t>>> staticQueue;
+  // (labels updated -> next hops, labels deleted), or nullopt when nothing queued
+  std::optional<std::pair<std::unordered_map<int32_t, std::vector<NextHopThrift>>,
+                          std::vector<int32_t>>> processStatic() {
+    std::unordered_map<int32_t, std::vector<NextHopThrift>> upd;
+    std::unordered_set<int32_t> del;
+    for (const auto& [u, d] : staticQueue) {
+      for (const auto& [lab, nhs] : u) { upd[lab] = nhs; del.erase(lab); }
+      for (int32_t lab : d) { del.insert(lab); upd.erase(lab); }
+    }
+    staticQueue.clear();
+    if (upd.empty() && del.empty()) return std::nullopt;
+    for (const auto& [lab, nhs] : upd) staticMpls[lab] = nhs;
+    for (int32_t lab : del) staticMpls.erase(lab);
+    return std::make_pair(upd, std::vector<int32_t>(del.begin(), del.end()));
+  }
 
   // Decision.cpp:544-630
   Best announcers(const std::string& me, const PrefixEntries& es, bool bgp, bool ksp2,
@@ -974,7 +1024,10 @@ class Solver {
         const int32_t top = adb.nodeLabel;
         if (top == 0 || !labelOk(top)) continue;
         auto it = l2n.find(top);
-        if (it != l2n.end() && it->second.first < adb.thisNodeName) continue;
+        if (it != l2n.end()) {
+          ++g_counters["decision.duplicate_node_label"];
+          if (it->second.first < adb.thisNodeName) continue;
+        }
         if (adb.thisNodeName == me) {
           NextHopThrift nh;
           nh.address.addr = std::string(16, '\0');
@@ -1058,6 +1111,23 @@ py::tuple linkKey(const OLink& l) {
 py::tuple chg(const std::tuple<bool, bool, bool>& t) {
   return py::make_tuple(std::get<0>(t), std::get<1>(t), std::get<2>(t));
 }
+py::dict routeDbDict(const RouteDb& db) {
+  py::dict uni, mpls;
+  for (const auto& [p, e] : db.unicast) {
+    py::dict d;
+    d["nexthops"] = nextHopSet(e.nhs);
+    d["bestArea"] = e.bestArea;
+    d["doNotInstall"] = e.dni;
+    d["bestNexthop"] = e.bestNh ? py::object(nextHopKey(*e.bestNh)) : py::none();
+    d["bestPrefixEntry"] = prefixEntryKey(e.best);
+    uni[prefixKey(p)] = d;
+  }
+  for (const auto& [l, s2] : db.mpls) mpls[py::int_(l)] = nextHopSet(s2);
+  py::dict out;
+  out["unicast"] = uni;
+  out["mpls"] = mpls;
+  return out;
+}
 struct AreaHolder {
   Areas map;
   AreaHolder() = default;
@@ -1085,14 +1155,56 @@ PYBIND11_MODULE(_oracle_ref, m) {
     return out;
   });
 
+  // HoldableValue<bool> / HoldableValue<LinkStateMetric> (LinkState.cpp:54-125)
+  py::class_<Held<bool>>(m, "HoldableValueBool")
+      .def(py::init<bool>())
+      .def("value", [](const Held<bool>& h) { return h.value(); })
+      .def("hasHold", &Held<bool>::hasHold)
+      .def("decrementTtl", &Held<bool>::decrementTtl)
+      .def("updateValue", &Held<bool>::update);
+  py::class_<Held<Metric>>(m, "HoldableValueMetric")
+      .def(py::init<Metric>())
+      .def("value", [](const Held<Metric>& h) { return h.value(); })
+      .def("hasHold", &Held<Metric>::hasHold)
+      .def("decrementTtl", &Held<Metric>::decrementTtl)
+      .def("updateValue", &Held<Metric>::update);
+
   py::class_<OLink, std::shared_ptr<OLink>>(m, "Link")
       .def(py::init<std::string, std::string, std::string, std::string, std::string>())
+      // Link(area, n1, adj1, n2, adj2) (LinkState.cpp:144-160)
+      .def_static("fromAdjacencies",
+                  [](const std::string& area, const std::string& n1, py::handle a1,
+                     const std::string& n2, py::handle a2) {
+                    const Adjacency x = toAdjacency(a1), y = toAdjacency(a2);
+                    auto l = std::make_shared<OLink>(area, n1, x.ifName, n2, y.ifName);
+                    l->m1.set((Metric)(int64_t)x.metric);
+                    l->m2.set((Metric)(int64_t)y.metric);
+                    l->o1.set(x.isOverloaded);
+                    l->o2.set(y.isOverloaded);
+                    l->lab1 = x.adjLabel;
+                    l->lab2 = y.adjLabel;
+                    l->v41 = x.nextHopV4;
+                    l->v42 = y.nextHopV4;
+                    l->v61 = x.nextHopV6;
+                    l->v62 = y.nextHopV6;
+                    return l;
+                  })
       .def("key", [](const OLink& l) { return linkKey(l); })
+      .def("getArea", [](const OLink& l) { return l.area; })
       .def("getMetricFromNode", &OLink::metric)
       .def("getOtherNodeName", &OLink::other)
       .def("getIfaceFromNode", &OLink::iface)
+      .def("getAdjLabelFromNode", &OLink::adjLabel)
+      .def("getOverloadFromNode", &OLink::overload)
+      // LinkState.cpp:303-315 / 328-345
+      .def("setMetricFromNode",
+           [](OLink& l, const std::string& n, Metric d, Metric up, Metric down) {
+             return (l.side1(n) ? l.m1 : l.m2).update(d, up, down);
+           })
+      .def("setOverloadFromNode", &OLink::setOverload)
       .def("isUp", &OLink::isUp)
       .def("__eq__", [](const OLink& a, const OLink& b) { return a == b; })
+      .def("__lt__", [](const OLink& a, const OLink& b) { return a < b; })
       .def("__hash__", [](const OLink& l) { return l.hash; });
 
   py::class_<Graph>(m, "LinkState")
@@ -1178,6 +1290,27 @@ PYBIND11_MODULE(_oracle_ref, m) {
         return out;
       });
 
+  py::class_<RouteDb>(m, "DecisionRouteDb")
+      .def(py::init<>())
+      .def("to_dict", [](const RouteDb& db) { return routeDbDict(db); });
+  // Decision.cpp:47-85
+  m.def("getRouteDelta", [](const RouteDb& nw, const RouteDb& old) {
+    const RouteDelta d = routeDelta(nw, old);
+    RouteDb upd;
+    for (const auto& [p, e] : d.uniUpdate) upd.unicast.emplace(p, e);
+    for (const auto& [l, e] : d.mplsUpdate) upd.mpls.emplace(l, e);
+    py::dict u = routeDbDict(upd);
+    py::list udel, mdel;
+    for (const auto& p : d.uniDelete) udel.append(prefixKey(p));
+    for (int32_t l : d.mplsDelete) mdel.append(py::int_(l));
+    py::dict out;
+    out["unicastRoutesToUpdate"] = u["unicast"];
+    out["unicastRoutesToDelete"] = udel;
+    out["mplsRoutesToUpdate"] = u["mpls"];
+    out["mplsRoutesToDelete"] = mdel;
+    return out;
+  });
+
   py::class_<Solver>(m, "SpfSolver")
       .def(py::init([](std::string /*me*/, bool v4, bool lfa, bool /*ofib*/, bool dry, bool igp) {
              return std::make_unique<Solver>(v4, lfa, dry, igp);
@@ -1185,6 +1318,32 @@ PYBIND11_MODULE(_oracle_ref, m) {
            py::arg("myNodeName"), py::arg("enableV4"), py::arg("computeLfaPaths"),
            py::arg("enableOrderedFib") = false, py::arg("bgpDryRun") = false,
            py::arg("bgpUseIgpMetric") = false)
+      .def("pushRoutesDeltaUpdates",
+           [](Solver& s, py::list toUpdate, std::vector<int32_t> toDelete) {
+             std::vector<std::pair<int32_t, std::vector<NextHopThrift>>> u;
+             for (auto r : toUpdate) {
+               std::vector<NextHopThrift> v;
+               for (auto nh : r.attr("nextHops")) v.push_back(toNextHop(nh));
+               u.emplace_back(r.attr("topLabel").cast<int32_t>(), std::move(v));
+             }
+             s.staticQueue.emplace_back(std::move(u), std::move(toDelete));
+           })
+      .def("staticRoutesUpdated", [](const Solver& s) { return !s.staticQueue.empty(); })
+      .def("processStaticRouteUpdates", [](Solver& s) -> py::object {
+        auto r = s.processStatic();
+        if (!r) return py::none();
+        py::dict upd;
+        for (const auto& [lab, nhs] : r->first)
+          upd[py::int_(lab)] = nextHopSet(std::unordered_set<NextHopThrift>(nhs.begin(), nhs.end()));
+        return py::make_tuple(upd, py::cast(r->second));
+      })
+      .def("buildRouteDbObject",
+           [](Solver& s, const std::string& me, const AreaHolder& areas,
+              const Prefixes& ps) -> py::object {
+             auto db = s.build(me, areas.map, ps);
+             if (!db) return py::none();
+             return py::cast(std::move(*db));
+           })
       .def("setStaticMplsRoute",
            [](Solver& s, int32_t label, py::list nhs) {
              std::vector<NextHopThrift> v;
@@ -1206,20 +1365,6 @@ PYBIND11_MODULE(_oracle_ref, m) {
               const Prefixes& ps) -> py::object {
              auto db = s.build(me, areas.map, ps);
              if (!db) return py::none();
-             py::dict uni, mpls;
-             for (const auto& [p, e] : db->unicast) {
-               py::dict d;
-               d["nexthops"] = nextHopSet(e.nhs);
-               d["bestArea"] = e.bestArea;
-               d["doNotInstall"] = e.dni;
-               d["bestNexthop"] = e.bestNh ? py::object(nextHopKey(*e.bestNh)) : py::none();
-               d["bestPrefixEntry"] = prefixEntryKey(e.best);
-               uni[prefixKey(p)] = d;
-             }
-             for (const auto& [l, s2] : db->mpls) mpls[py::int_(l)] = nextHopSet(s2);
-             py::dict out;
-             out["unicast"] = uni;
-             out["mpls"] = mpls;
-             return out;
+             return py::object(routeDbDict(*db));
            });
 }

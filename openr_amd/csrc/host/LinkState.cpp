@@ -9,6 +9,7 @@
 // name ranks and whose rows list links in linksFromNode() iteration order.
 
 #include "LinkState.h"
+#include "FollyHash.h"
 #include "Engine.h"
 
 #include <chrono>
@@ -64,22 +65,13 @@ int getSpfDevice() { return spfDevice(); }
 // --------------------------------------------------------------- hashing
 
 namespace {
-// folly::hash::hash_128_to_64 — folly's std::hash<std::pair> combines the two
-// member hashes with it (folly/hash/Hash.h @ ab8339ea).  Link::hash feeds
-// Link::operator< and the bucket order of every LinkSet, and that order picks
-// the parallel link a KSP2 trace takes (DecisionTest.cpp:3276-3279).
-inline uint64_t hash128to64(uint64_t upper, uint64_t lower) {
-  const uint64_t kMul = 0x9ddfea08eb382d69ULL;
-  uint64_t a = (lower ^ upper) * kMul;
-  a ^= (a >> 47);
-  uint64_t b = (upper ^ a) * kMul;
-  b ^= (b >> 47);
-  b *= kMul;
-  return b;
-}
+// Link::hash = folly's std::hash<pair<pair<string,string>, pair<string,string>>>
+// (FollyHash.h): it feeds Link::operator< and the bucket order of every
+// LinkSet, and that order picks the parallel link a KSP2 trace takes
+// (DecisionTest.cpp:3276-3279, 3694-3696, 3726-3727).
+using follyhash::hash128to64;
 inline size_t hashStrPair(const std::pair<std::string, std::string>& p) {
-  return hash128to64(
-      std::hash<std::string>()(p.first), std::hash<std::string>()(p.second));
+  return follyhash::hashStringPair(p);
 }
 } // namespace
 

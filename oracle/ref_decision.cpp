@@ -66,6 +66,107 @@ static uint64_t h128(uint64_t upper, uint64_t lower) {
   return b;
 }
 
+// ------------------------------------------------- folly hasher<std::string>
+// folly::hasher<std::string> = SpookyHashV2::Hash64(data, len, 0) (Bob
+// Jenkins' SpookyHash V2, public domain); folly's std::hash<std::pair>
+// combines member hashes with hash_128_to_64 (h128 above).  Restated from the
+// published algorithm; pinned by the reference's hash-dependent parallel-link
+// goldens (DecisionTest.cpp:3276-3279, 3694-3696, 3726-3727), which libstdc++'s
+// std::hash<std::string> in its place does not reproduce.
+static inline uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+static uint64_t ld(const unsigned char* p, int n) {  // little-endian n-byte load
+  uint64_t v = 0;
+  for (int i = n - 1; i >= 0; --i) v = (v << 8) | p[i];
+  return v;
+}
+static uint64_t spooky64(const std::string& str) {
+  const unsigned char* p = reinterpret_cast<const unsigned char*>(str.data());
+  const size_t len = str.size();
+  const uint64_t K = 0xdeadbeefdeadbeefULL;
+  if (len >= 192) {  // SpookyHash::Hash128 long path
+    uint64_t h[12];
+    for (int i = 0; i < 12; ++i) h[i] = (i % 3 == 2) ? K : 0;
+    static const int mr[12] = {11, 32, 43, 31, 17, 28, 39, 57, 55, 54, 22, 46};
+    static const int er[12] = {44, 15, 34, 21, 38, 33, 10, 13, 38, 53, 42, 54};
+    auto mixBlock = [&](const uint64_t* d) {
+      for (int i = 0; i < 12; ++i) {
+        h[i] += d[i];
+        h[(i + 2) % 12] ^= h[(i + 10) % 12];
+        h[(i + 11) % 12] ^= h[i];
+        h[i] = rotl(h[i], mr[i]);
+        h[(i + 11) % 12] += h[(i + 1) % 12];
+      }
+    };
+    size_t off = 0;
+    uint64_t d[12];
+    for (; off + 96 <= len; off += 96) {
+      for (int i = 0; i < 12; ++i) d[i] = ld(p + off + 8 * i, 8);
+      mixBlock(d);
+    }
+    unsigned char last[96] = {0};
+    std::copy(p + off, p + len, last);
+    last[95] = (unsigned char)(len - off);
+    for (int i = 0; i < 12; ++i) h[i] += ld(last + 8 * i, 8);
+    for (int rep = 0; rep < 3; ++rep)
+      for (int i = 0; i < 12; ++i) {
+        h[(i + 11) % 12] += h[(i + 1) % 12];
+        h[(i + 2) % 12] ^= h[(i + 11) % 12];
+        h[(i + 1) % 12] = rotl(h[(i + 1) % 12], er[i]);
+      }
+    return h[0];
+  }
+  // SpookyHash::Short
+  uint64_t v[4] = {0, 0, K, K};  // a, b, c, d
+  auto smix = [&]() {
+    static const int r[12] = {50, 52, 30, 41, 54, 48, 38, 37, 62, 34, 5, 36};
+    for (int i = 0; i < 12; ++i) {
+      const int x = (i + 2) % 4, y = (i + 3) % 4, z = i % 4;
+      v[x] = rotl(v[x], r[i]);
+      v[x] += v[y];
+      v[z] ^= v[x];
+    }
+  };
+  size_t rem = len % 32, off = 0;
+  if (len > 15) {
+    for (; off + 32 <= len; off += 32) {
+      v[2] += ld(p + off, 8);
+      v[3] += ld(p + off + 8, 8);
+      smix();
+      v[0] += ld(p + off + 16, 8);
+      v[1] += ld(p + off + 24, 8);
+    }
+    if (rem >= 16) {
+      v[2] += ld(p + off, 8);
+      v[3] += ld(p + off + 8, 8);
+      smix();
+      off += 16;
+      rem -= 16;
+    }
+  }
+  v[3] += (uint64_t)len << 56;
+  if (rem == 0) {
+    v[2] += K;
+    v[3] += K;
+  } else if (rem >= 12) {
+    v[2] += ld(p + off, 8);
+    v[3] += ld(p + off + 8, rem - 8);
+  } else if (rem >= 8) {
+    v[2] += ld(p + off, 8);
+    v[3] += ld(p + off + 8, rem - 8);
+  } else {
+    v[2] += ld(p + off, rem);
+  }
+  // ShortEnd
+  static const int er[11] = {15, 52, 26, 51, 28, 9, 47, 54, 32, 25, 63};
+  for (int i = 0; i < 11; ++i) {
+    const int x = (i + 3) % 4, y = (i + 2) % 4;
+    v[x] ^= v[y];
+    v[y] = rotl(v[y], er[i]);
+    v[x] += v[y];
+  }
+  return v[0];
+}
+
 // ------------------------------------- HoldableValue (LinkState.cpp:54-125)
 template <class T>
 struct Held {
@@ -108,7 +209,7 @@ struct OLink {
       : area(a), n1(x), n2(y), if1(ix), if2(iy) {
     names = std::minmax(std::make_pair(n1, if1), std::make_pair(n2, if2));
     auto ph = [](const std::pair<std::string, std::string>& p) {
-      return h128(std::hash<std::string>()(p.first), std::hash<std::string>()(p.second));
+      return h128(spooky64(p.first), spooky64(p.second));
     };
     hash = h128(ph(names.first), ph(names.second));
   }

@@ -8,11 +8,14 @@ import pytest
 
 from openr_amd import thrift as T
 from tests import known_answers as KA
+from tests import known_answers_more as KB
 from tests import randomized as RZ
 
 pytestmark = pytest.mark.gpu
 
-SCENARIOS = [getattr(KA, n) for n in dir(KA) if n.startswith("sc_")]
+SCENARIOS = [getattr(M, n) for M in (KA, KB) for n in dir(M) if n.startswith("sc_")]
+# DecisionTestFixture cases, replayed through PublicationIngest (CompactProtocol)
+WIRE_SCENARIOS = [getattr(KB, n) for n in dir(KB) if n.startswith("sc_decision_")]
 
 
 @pytest.fixture(scope="module")
@@ -28,6 +31,12 @@ def test_engine_known_answer(mods, scenario):
     E, _ = mods
     E.reset_counters()
     scenario(E)
+
+
+@pytest.mark.parametrize("scenario", WIRE_SCENARIOS, ids=lambda f: f.__name__)
+def test_engine_known_answer_via_publication_ingest(mods, scenario):
+    E, _ = mods
+    scenario(E, wire=True)
 
 
 def _spf_equal(e_ls, o_ls, node, use_metric=True):

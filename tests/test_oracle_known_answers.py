@@ -5,8 +5,9 @@ This pins the oracle before it is used to check the MI355X engine."""
 import pytest
 
 from tests import known_answers as KA
+from tests import known_answers_more as KB
 
-SCENARIOS = [getattr(KA, n) for n in dir(KA) if n.startswith("sc_")]
+SCENARIOS = [getattr(M, n) for M in (KA, KB) for n in dir(M) if n.startswith("sc_")]
 
 
 @pytest.fixture(scope="module")

@@ -626,7 +626,8 @@ LinkState::LinkState(LinkState&& o) noexcept
       kthPathResults_(std::move(o.kthPathResults_)),
       kthMu_(std::move(o.kthMu_)),
       kthFill_(std::move(o.kthFill_)),
-      engine_(std::move(o.engine_)) {}
+      engine_(std::move(o.engine_)),
+      topoGen_(o.topoGen_) {}
 
 size_t LinkState::LinkPtrHash::operator()(const std::shared_ptr<Link>& l) const {
   return l->hash;
@@ -641,6 +642,7 @@ bool LinkState::LinkPtrEqual::operator()(
 }
 
 void LinkState::clearMemo() const {
+  ++topoGen_;
   spfResultsMetric_.clear();
   spfResultsHops_.clear();
   kthPathResults_.clear();
@@ -662,6 +664,7 @@ void LinkState::patchMemo(
     return;
   }
   auto& eng = *engine_;
+  ++topoGen_;
   std::vector<uint32_t> edges;
   std::vector<uint64_t> metrics;
   for (const auto& [link, from] : metricPatches) {
@@ -1100,28 +1103,87 @@ LinkState::SpfResult const& LinkState::getSpfResult(
     return it->second;
   }
   const SpfView& view = spfView(nodeName, useLinkMetric);
+  return cache.emplace(nodeName, materialize(view, nodeName)).first->second;
+}
+
+LinkState::SpfResult LinkState::materialize(const SpfView& view, const std::string& srcName) const {
   const auto& eng = *engine_;
   SpfResult res;
   if (view.src == ~0u) {
-    res.emplace(nodeName, NodeSpfResult(0));
-  } else {
-    std::vector<std::pair<uint32_t, uint32_t>> preds;
-    const uint32_t V = (uint32_t)eng.names.size();
-    res.reserve(V);
-    for (uint32_t v = 0; v < V; ++v) {
-      if (!view.reached(v)) {
-        continue;
-      }
-      NodeSpfResult r(view.dist[v]);
-      pathLinksOf(eng, view, v, preds);
-      for (const auto& [eu, u] : preds) {
-        r.addPath(eng.links[eng.linkId[eu]], eng.names[u]);
-      }
-      view.forEachNextHop(v, [&](uint32_t h) { r.addNextHop(eng.names[h]); });
-      res.emplace(eng.names[v], std::move(r));
-    }
+    res.emplace(srcName, NodeSpfResult(0));
+    return res;
   }
-  return cache.emplace(nodeName, std::move(res)).first->second;
+  std::vector<std::pair<uint32_t, uint32_t>> preds;
+  const uint32_t V = (uint32_t)eng.names.size();
+  res.reserve(V);
+  for (uint32_t v = 0; v < V; ++v) {
+    if (!view.reached(v)) {
+      continue;
+    }
+    NodeSpfResult r(view.dist[v]);
+    pathLinksOf(eng, view, v, preds);
+    for (const auto& [eu, u] : preds) {
+      r.addPath(eng.links[eng.linkId[eu]], eng.names[u]);
+    }
+    view.forEachNextHop(v, [&](uint32_t h) { r.addNextHop(eng.names[h]); });
+    res.emplace(eng.names[v], std::move(r));
+  }
+  return res;
+}
+
+std::unique_ptr<LinkState::SpfBatch> LinkState::runSpfBatch(
+    const std::string& src, const std::vector<LinkSet>& linksToIgnore, bool useLinkMetric) const {
+  auto& eng = engine();
+  auto batch = std::make_unique<SpfBatch>();
+  batch->ls_ = this;
+  batch->gen_ = topoGen_;
+  batch->src_ = src;
+  const size_t nq = linksToIgnore.size();
+  Counters::add("decision.spf_runs", (int64_t)nq);
+  auto sid = eng.ids.find(src);
+  if (sid == eng.ids.end()) {
+    // unknown source: every result holds only the source itself
+    for (size_t i = 0; i < nq; ++i) {
+      auto v = std::make_unique<SpfView>();
+      v->src = ~0u;
+      v->useLinkMetric = useLinkMetric;
+      batch->views_.push_back(std::move(v));
+    }
+    return batch;
+  }
+  // ignore lists as sorted device link ids (links that are not up links of
+  // this area cannot be relaxed anyway)
+  std::vector<std::vector<uint32_t>> lists(nq);
+  for (size_t i = 0; i < nq; ++i) {
+    for (const auto& link : linksToIgnore[i]) {
+      auto li = eng.linkIndex.find(link.get());
+      if (li == eng.linkIndex.end()) {
+        // an equal Link object of this LinkState (the caller may hold a copy)
+        auto own = allLinks_.find(link);
+        if (own != allLinks_.end()) {
+          li = eng.linkIndex.find(own->get());
+        }
+      }
+      if (li != eng.linkIndex.end()) {
+        lists[i].push_back(li->second);
+      }
+    }
+    std::sort(lists[i].begin(), lists[i].end());
+    lists[i].erase(std::unique(lists[i].begin(), lists[i].end()), lists[i].end());
+  }
+  std::vector<uint32_t> sources(nq, sid->second);
+  {
+    std::lock_guard<std::mutex> dev(eng.devMu);
+    batch->views_ = runBatch(eng, sources, useLinkMetric, true, &lists);
+  }
+  return batch;
+}
+
+LinkState::SpfResult LinkState::SpfBatch::result(size_t i) const {
+  if (!ls_ || ls_->topoGen_ != gen_ || !ls_->engine_) {
+    throw std::logic_error("SpfBatch::result: the topology changed since the batch ran");
+  }
+  return ls_->materialize(*views_.at(i), src_);
 }
 
 std::optional<LinkStateMetric> LinkState::getMetricFromAToB(

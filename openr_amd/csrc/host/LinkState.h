@@ -318,6 +318,32 @@ class LinkState {
   // id -> name of the device graph (valid until the next topology change)
   const std::vector<std::string>& nodeNames() const;
   uint32_t numGraphNodes() const;
+  // What-if link-failure SPFs (BASELINE config 5, LFA / failure
+  // precomputation): runSpf(src, useLinkMetric, linksToIgnore[i])
+  // (LinkState.cpp:806-880 -- the reference's own ignore-set semantics, which
+  // it reaches only through getKthPaths, :776-777) for every i, as ONE device
+  // batch.  Each query counts one decision.spf_runs, as each runSpf does.
+  // Results stay flat; result(i) materialises the reference's SpfResult
+  // (pathLinks in reference order) and, like getSpfResult's reference, is
+  // valid only until the next topology change of this LinkState
+  // (std::logic_error afterwards).
+  class SpfBatch {
+   public:
+    size_t size() const { return views_.size(); }
+    const SpfView& view(size_t i) const { return *views_.at(i); }
+    SpfResult result(size_t i) const;
+
+   private:
+    friend class LinkState;
+    const LinkState* ls_{nullptr};
+    uint64_t gen_{0};
+    std::string src_;
+    std::vector<std::unique_ptr<SpfView>> views_;
+  };
+  std::unique_ptr<SpfBatch> runSpfBatch(
+      const std::string& src,
+      const std::vector<LinkSet>& linksToIgnore,
+      bool useLinkMetric = true) const;
   // device time of the last batch, ms (HIP events)
   float lastDeviceMs() const;
   // release the device graph and every memoized result
@@ -328,6 +354,11 @@ class LinkState {
 
  private:
   void clearMemo() const;
+  // reference-form SpfResult of one flat view of the current device graph
+  SpfResult materialize(const SpfView& view, const std::string& srcName) const;
+  // bumped on every topology change (clearMemo / patchMemo): flat views of an
+  // older generation are stale
+  mutable uint64_t topoGen_{0};
   void patchMemo(
       const std::vector<std::string>& transitNodes,
       const std::vector<std::pair<std::shared_ptr<Link>, std::string>>& metricPatches) const;

@@ -52,6 +52,22 @@ py::tuple linkKey(const Link& l) {
       py::make_tuple(n.second.first, n.second.second));
 }
 
+py::dict spfResultToPy(const LinkState::SpfResult& res) {
+  py::dict out;
+  for (const auto& [name, r] : res) {
+    py::list paths;
+    for (const auto& pl : r.pathLinks()) {
+      paths.append(py::make_tuple(linkKey(*pl.link), pl.prevNode));
+    }
+    py::set nhs;
+    for (const auto& h : r.nextHops()) {
+      nhs.add(py::str(h));
+    }
+    out[py::str(name)] = py::make_tuple(r.metric(), py::frozenset(nhs), paths);
+  }
+  return out;
+}
+
 py::tuple changeToPy(const LinkState::LinkStateChange& c) {
   return py::make_tuple(c.topologyChanged, c.linkAttributesChanged, c.nodeLabelChanged);
 }
@@ -219,21 +235,29 @@ PYBIND11_MODULE(_openr_spf, m) {
       .def(
           "getSpfResult",
           [](const LinkState& ls, const std::string& node, bool useLinkMetric) {
-            py::dict out;
-            for (const auto& [name, r] : ls.getSpfResult(node, useLinkMetric)) {
-              py::list paths;
-              for (const auto& pl : r.pathLinks()) {
-                paths.append(py::make_tuple(linkKey(*pl.link), pl.prevNode));
-              }
-              py::set nhs;
-              for (const auto& h : r.nextHops()) {
-                nhs.add(py::str(h));
-              }
-              out[py::str(name)] = py::make_tuple(r.metric(), py::frozenset(nhs), paths);
-            }
-            return out;
+            return spfResultToPy(ls.getSpfResult(node, useLinkMetric));
           },
           py::arg("node"), py::arg("useLinkMetric") = true)
+      .def(
+          "runSpfBatch",
+          [](const LinkState& ls, const std::string& src, py::list ignoreSets, bool useLinkMetric) {
+            std::vector<LinkState::LinkSet> sets;
+            for (auto lst : ignoreSets) {
+              LinkState::LinkSet set;
+              for (auto l : lst) {
+                set.insert(l.cast<std::shared_ptr<Link>>());
+              }
+              sets.push_back(std::move(set));
+            }
+            std::unique_ptr<LinkState::SpfBatch> b;
+            {
+              py::gil_scoped_release rel;
+              b = ls.runSpfBatch(src, sets, useLinkMetric);
+            }
+            return b;
+          },
+          py::arg("src"), py::arg("linksToIgnore"), py::arg("useLinkMetric") = true,
+          py::keep_alive<0, 1>())
       .def(
           "getKthPaths",
           [](const LinkState& ls, const std::string& s, const std::string& d, size_t k) {
@@ -261,6 +285,18 @@ PYBIND11_MODULE(_openr_spf, m) {
         for (auto x : a) pa.push_back(x.cast<std::shared_ptr<Link>>());
         for (auto x : b) pb.push_back(x.cast<std::shared_ptr<Link>>());
         return LinkState::pathAInPathB(pa, pb);
+      });
+
+  py::class_<LinkState::SpfBatch>(m, "SpfBatch")
+      .def("size", &LinkState::SpfBatch::size)
+      .def("__len__", &LinkState::SpfBatch::size)
+      .def("result", [](const LinkState::SpfBatch& b, size_t i) { return spfResultToPy(b.result(i)); })
+      .def("metric", [](const LinkState::SpfBatch& b, size_t i, uint32_t nodeId) -> py::object {
+        const auto& v = b.view(i);
+        if (!v.reached(nodeId)) {
+          return py::none();
+        }
+        return py::int_(v.dist[nodeId]);
       });
 
   // std::unordered_map<std::string, LinkState> as the reference tests build it

@@ -258,3 +258,30 @@ def wan(V=100000, L=1000000, seed=12345, wmax=1000):
     names = [f"n{i}" for i in range(V)]
     ifn = [(f"if_{a}_{b}", f"if_{b}_{a}") for (a, b, _, _) in links]
     return Topology(names, links, ifn, None, None)
+
+
+# ------------------------------------------------- config 5 (what-if, 2 areas)
+
+WHATIF_BORDER = "2-0-0"
+
+
+def wan_border(V=10000, L=100000, border=WHATIF_BORDER):
+    """The WAN of wan(V, L) with node n0 renamed to the border node, so that
+    one node is present in both what-if areas (BASELINE configs[4]: "multi-area
+    LinkState", the border-node setup of DecisionTest.cpp:4503-4545)."""
+    t = wan(V, L)
+    t.names[0] = border
+    return t
+
+
+def whatif_two_area(per_area=4096, seed=7):
+    """BASELINE configs[4]: area "A" = fabric(10000), area "B" = WAN-10k (100k
+    links) sharing the border node "2-0-0"; `per_area` links of each area
+    sampled without replacement (numpy default_rng(seed), area A first).
+    Returns [(area, topology, link creation ids)]."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for area, topo in (("A", fabric(10000)), ("B", wan_border(10000, 100000))):
+        links = rng.choice(len(topo.links), per_area, replace=False).astype(np.int64)
+        out.append((area, topo, links))
+    return out

@@ -17,6 +17,7 @@ ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "ref_decision.cpp")
 DEPS = [
     SRC,
+    os.path.join(HERE, "csr_spf.h"),
     os.path.join(ROOT, "openr_amd", "csrc", "host", "Types.h"),
     os.path.join(ROOT, "openr_amd", "csrc", "py", "convert.h"),
 ]
@@ -36,6 +37,7 @@ def build(force=False):
         "-std=c++17",
         "-shared",
         "-fPIC",
+        "-pthread",
         "-fvisibility=hidden",
         f"-I{pybind11.get_include()}",
         f"-I{sysconfig.get_paths()['include']}",

@@ -34,6 +34,9 @@
 
 #include "../openr_amd/csrc/host/Types.h"
 #include "../openr_amd/csrc/py/convert.h"
+#include "csr_spf.h"
+
+#include <pybind11/numpy.h>
 
 namespace oracle {
 
@@ -1245,6 +1248,99 @@ PYBIND11_MODULE(_oracle_ref, m) {
   });
   m.def("reset_counters", [] { g_counters.clear(); });
 
+  // csr_spf.h: the fast flat restatement (goldens, all-cores CPU baseline).
+  // Returns uint64 [Q, 4] = (reached, sum of distances, (node, next hop)
+  // pairs, mix) per query; ignore = (offsets u32[Q+1], sorted link ids).
+  m.def(
+      "csr_spf_summary",
+      [](py::array_t<uint32_t, py::array::c_style> row, py::array_t<uint32_t, py::array::c_style> col,
+         py::array_t<uint64_t, py::array::c_style> w, py::array_t<uint32_t, py::array::c_style> link,
+         py::array_t<uint8_t, py::array::c_style> ov, py::array_t<uint32_t, py::array::c_style> sources,
+         py::object ignOff, py::object ign, bool useMetric, bool wantNh, unsigned threads) {
+        csr::Graph g;
+        g.V = (uint32_t)ov.size();
+        if (row.size() != (ssize_t)g.V + 1 || col.size() != w.size() || col.size() != link.size())
+          throw std::invalid_argument("csr_spf_summary: inconsistent CSR");
+        g.row = row.data();
+        g.col = col.data();
+        g.w = w.data();
+        g.link = link.data();
+        g.overloaded = ov.data();
+        std::vector<csr::Query> qs(sources.size());
+        py::array_t<uint32_t, py::array::c_style> io, il;
+        if (!ignOff.is_none()) {
+          io = ignOff.cast<py::array_t<uint32_t, py::array::c_style>>();
+          il = ign.cast<py::array_t<uint32_t, py::array::c_style>>();
+          if (io.size() != sources.size() + 1) throw std::invalid_argument("ignore offsets");
+        }
+        for (ssize_t i = 0; i < sources.size(); ++i) {
+          qs[i].src = sources.data()[i];
+          if (qs[i].src >= g.V) throw std::invalid_argument("source out of range");
+          if (io.size()) {
+            qs[i].ign = il.data() + io.data()[i];
+            qs[i].nign = io.data()[i + 1] - io.data()[i];
+          }
+        }
+        std::vector<csr::Summary> out;
+        {
+          py::gil_scoped_release rel;
+          out = csr::summaries(g, qs, useMetric, wantNh, threads);
+        }
+        py::array_t<uint64_t> res({(ssize_t)out.size(), (ssize_t)4});
+        auto r = res.mutable_unchecked<2>();
+        for (size_t i = 0; i < out.size(); ++i) {
+          r(i, 0) = out[i].reached;
+          r(i, 1) = out[i].sumDist;
+          r(i, 2) = out[i].sumNh;
+          r(i, 3) = out[i].mix;
+        }
+        return res;
+      },
+      py::arg("row"), py::arg("col"), py::arg("w"), py::arg("link"), py::arg("overloaded"),
+      py::arg("sources"), py::arg("ign_off") = py::none(), py::arg("ign") = py::none(),
+      py::arg("use_metric") = true, py::arg("want_nh") = true, py::arg("threads") = 1);
+  // distance rows (uint64 [Q, V], ~0 = unreached) of a few sources
+  m.def(
+      "csr_spf_rows",
+      [](py::array_t<uint32_t, py::array::c_style> row, py::array_t<uint32_t, py::array::c_style> col,
+         py::array_t<uint64_t, py::array::c_style> w, py::array_t<uint32_t, py::array::c_style> link,
+         py::array_t<uint8_t, py::array::c_style> ov, py::array_t<uint32_t, py::array::c_style> sources,
+         bool useMetric, unsigned threads) {
+        csr::Graph g;
+        g.V = (uint32_t)ov.size();
+        g.row = row.data();
+        g.col = col.data();
+        g.w = w.data();
+        g.link = link.data();
+        g.overloaded = ov.data();
+        const ssize_t nq = sources.size();
+        for (ssize_t i = 0; i < nq; ++i)
+          if (sources.data()[i] >= g.V) throw std::invalid_argument("source out of range");
+        py::array_t<uint64_t> res({(ssize_t)nq, (ssize_t)g.V});
+        uint64_t* out = res.mutable_data();
+        const uint32_t* src = sources.data();
+        {
+          py::gil_scoped_release rel;
+          std::atomic<ssize_t> next{0};
+          auto worker = [&]() {
+            csr::Work wk;
+            for (ssize_t i; (i = next.fetch_add(1)) < nq;) {
+              csr::Query q;
+              q.src = src[i];
+              csr::run(g, q, useMetric, false, wk);
+              std::copy(wk.dist.begin(), wk.dist.end(), out + (size_t)i * g.V);
+            }
+          };
+          std::vector<std::thread> pool;
+          for (unsigned t = 1; t < std::max(1u, threads); ++t) pool.emplace_back(worker);
+          worker();
+          for (auto& t : pool) t.join();
+        }
+        return res;
+      },
+      py::arg("row"), py::arg("col"), py::arg("w"), py::arg("link"), py::arg("overloaded"),
+      py::arg("sources"), py::arg("use_metric") = true, py::arg("threads") = 1);
+
   // iteration order of a libstdc++ std::unordered_map<int, ...> built from an
   // initializer list in `keys` order (DecisionTestUtils.cpp:16-43 iterates one)
   m.def("cxx_unordered_int_order", [](std::vector<int> keys) {
@@ -1341,6 +1437,23 @@ PYBIND11_MODULE(_oracle_ref, m) {
              return out;
            },
            py::arg("node"), py::arg("useLinkMetric") = true)
+      // runSpf(src, useLinkMetric, linksToIgnore) (LinkState.cpp:806-880) for
+      // a what-if link failure: un-memoized, counts one spf_runs
+      .def("runSpfIgnoring",
+           [](const Graph& g, const std::string& n, py::list links, bool useMetric) {
+             LinkSet ign;
+             for (auto l : links) ign.insert(l.cast<LinkP>());
+             py::dict out;
+             for (const auto& [name, r] : g.runSpf(n, useMetric, ign)) {
+               py::list paths;
+               for (const auto& [l, prev] : r.paths) paths.append(py::make_tuple(linkKey(*l), prev));
+               py::set nhs;
+               for (const auto& h : r.nhs) nhs.add(py::str(h));
+               out[py::str(name)] = py::make_tuple(r.metric, py::frozenset(nhs), paths);
+             }
+             return out;
+           },
+           py::arg("src"), py::arg("linksToIgnore"), py::arg("useLinkMetric") = true)
       .def("runSpfTimed",
            [](const Graph& g, std::vector<std::string> srcs, bool useMetric) {
              // the cpu_baseline leg: uncached runSpf per source

@@ -150,7 +150,100 @@ def main():
             })
     json.dump({"topology": "fabric_full(10000)", "queries": wi},
               open(os.path.join(HERE, "whatif_fabric.json"), "w"), indent=0, sort_keys=True)
+    config_sized(O, f)
     print("goldens written")
+
+
+def csr_summary(O, csr, sources, ignore=None, want_nh=True, threads=None):
+    """oracle/csr_spf.h per-query (reached, sum of distances, (node, next hop)
+    pairs, mix) -- see tests/golden/summary.py for the same numbers computed
+    from the engine's rows."""
+    import numpy as np
+
+    ioff = ign = None
+    if ignore is not None:
+        ioff = np.zeros(len(ignore) + 1, dtype=np.uint32)
+        ioff[1:] = np.cumsum([len(x) for x in ignore])
+        ign = np.asarray([int(v) for x in ignore for v in sorted(x)] or [0], dtype=np.uint32)
+    return O.csr_spf_summary(csr.row_ptr, csr.col, csr.metric.astype(np.uint64), csr.link_id,
+                             csr.overloaded, np.asarray(sources, dtype=np.uint32), ioff, ign,
+                             True, want_nh, threads or os.cpu_count())
+
+
+def config_sized(O, fab):
+    """Round-2 goldens for the configs at their real plans:
+      fabric_allsources.npz  every one of the 9,976 fabric sources (config 2)
+      whatif_two_area.npz    the 8,192 two-area what-if queries (config 5)
+      whatif_two_area.json   reference-form digests of sampled what-if queries
+                             through the oracle's multi-area LinkState
+      wan100k_rows.json      sampled rows of the 100k WAN (config 3)
+    The flat summaries come from oracle/csr_spf.h, cross-checked here against
+    the reference-style oracle on sampled sources."""
+    import numpy as np
+
+    from oracle import spf_py
+    from openr_amd import topologies as TP
+    from tests.golden.summary import summary_from_spf_result
+
+    # ---- config 2: all fabric sources
+    csr = fab.csr()
+    V = csr.num_nodes
+    S = csr_summary(O, csr, np.arange(V))
+    r, names_by_rank = fab.rank()
+    areas, ls, _ = load(O, fab)
+    for src in FABRIC_SOURCES[:3]:
+        sid = names_by_rank.index(src)
+        assert tuple(int(x) for x in S[sid]) == summary_from_spf_result(ls.getSpfResult(src, True),
+                                                                        names_by_rank), src
+    np.savez_compressed(os.path.join(HERE, "fabric_allsources.npz"), summary=S)
+
+    # ---- config 5: two areas, border node 2-0-0, 4,096 link failures each
+    meta = {"border": TP.WHATIF_BORDER, "areas": []}
+    summ = []
+    for area, topo, links in TP.whatif_two_area():
+        c = topo.csr()
+        rr, nbr = topo.rank()
+        sid = int(rr[topo.names.index(TP.WHATIF_BORDER)])
+        Sa = csr_summary(O, c, np.full(len(links), sid), [[int(l)] for l in links])
+        summ.append(Sa)
+        # reference-form digests of sampled queries through the oracle's
+        # multi-area LinkState (runSpf with linksToIgnore = {link})
+        oareas = O.AreaLinkStates()
+        ols = oareas.add(area)
+        for db in topo.adj_dbs(area):
+            ols.updateAdjacencyDatabase(db)
+        sampled = []
+        for qi in list(range(0, len(links), len(links) // 12))[:12]:
+            a, b = topo.links[int(links[qi])][:2]
+            na, nb = topo.names[a], topo.names[b]
+            lk = [l for l in ols.linksFromNode(na) if l.getOtherNodeName(na) == nb]
+            res = ols.runSpfIgnoring(TP.WHATIF_BORDER, lk, True)
+            assert summary_from_spf_result(res, nbr) == tuple(int(x) for x in Sa[qi]), (area, qi)
+            sampled.append({"query": qi, "link": [na, nb], "reached": len(res),
+                            "digest": digest(spf_canon(res))})
+        # one literal DijkstraQ replay per area pins csr_spf on the ignore path
+        q0 = sampled[0]["query"]
+        rep = spf_py.run_spf(c, sid, True, frozenset([int(links[q0])]))
+        assert len(rep) == sampled[0]["reached"]
+        meta["areas"].append({"area": area, "links": [int(x) for x in links], "sampled": sampled})
+    np.savez_compressed(os.path.join(HERE, "whatif_two_area.npz"), summary=np.concatenate(summ))
+    json.dump(meta, open(os.path.join(HERE, "whatif_two_area.json"), "w"), sort_keys=True)
+
+    # ---- config 3: sampled rows of the 100k WAN
+    import hashlib
+
+    w = TP.wan(100000, 1000000)
+    c = w.csr()
+    srcs = [0, 1, 99999] + [int(x) for x in np.random.default_rng(3).choice(100000, 29, replace=False)]
+    rows = O.csr_spf_rows(c.row_ptr, c.col, c.metric.astype(np.uint64), c.link_id, c.overloaded,
+                          np.asarray(srcs, dtype=np.uint32), True)
+    out = []
+    for s, row in zip(srcs, rows):
+        r32 = np.where(row == np.uint64(2**64 - 1), np.uint64(0xFFFFFFFF), row).astype(np.uint32)
+        out.append({"src": s, "sum": int(row[row != np.uint64(2**64 - 1)].sum()),
+                    "sha256": hashlib.sha256(r32.tobytes()).hexdigest()})
+    json.dump({"topology": "wan(100000, 1000000)", "rows": out},
+              open(os.path.join(HERE, "wan100k_rows.json"), "w"), indent=0, sort_keys=True)
 
 
 if __name__ == "__main__":

@@ -22,6 +22,7 @@ def random_network(
     link_overload_prob=0.03,
     node_labels=True,
     areas=("0",),
+    bgp=False,
 ):
     """Returns (adj_dbs per area, prefix_dbs).  Node names are random-ish
     strings so that name order differs from creation order."""
@@ -78,9 +79,41 @@ def random_network(
             entries.append(e)
         if rng.random() < 0.1:  # anycast prefix shared by a few nodes
             entries.append(T.createPrefixEntry(T.toIpPrefix("fc99::1/128")))
+        if bgp:
+            entries += _bgp_entries(rng, idx)
         for area in areas:
             prefix_dbs.append(T.createPrefixDb(n, entries, area))
     return names, adj_dbs, prefix_dbs
+
+
+# BGP prefixes shared by random announcers, each with a random MetricVector
+# (Lsdb.thrift:183-213): few metric types, small values and random ops so that
+# best-path selection (Decision.cpp:715-800, MetricVectorUtils Util.cpp:
+# 1051-1228) hits wins, losses, ties, tie-breakers and absent entries
+_BGP_PREFIXES = [f"2001:db8:{k:x}::/48" for k in range(6)]
+
+
+def _bgp_entries(rng, idx):
+    out = []
+    for k, pfx in enumerate(_BGP_PREFIXES):
+        if rng.random() >= 0.25:
+            continue
+        metrics = []
+        for t in rng.sample(range(4), rng.randint(1, 3)):
+            metrics.append(T.createMetricEntity(
+                t, 10 - t,  # priority fixed per type
+                rng.choice([T.CompareType.WIN_IF_PRESENT, T.CompareType.WIN_IF_NOT_PRESENT,
+                            T.CompareType.IGNORE_IF_NOT_PRESENT]),
+                rng.random() < 0.3,
+                [rng.randint(0, 2) for _ in range(rng.randint(1, 2))]))
+        e = T.createPrefixEntry(T.toIpPrefix(pfx), T.PrefixType.BGP, f"d{idx}",
+                                mv=T.MetricVector(0, metrics))
+        if k >= 4:  # SR-MPLS BGP prefixes (selectKsp2 with metric-vector best path)
+            e.forwardingType = T.PrefixForwardingType.SR_MPLS
+            e.forwardingAlgorithm = rng.choice([T.PrefixForwardingAlgorithm.SP_ECMP,
+                                                T.PrefixForwardingAlgorithm.KSP2_ED_ECMP])
+        out.append(e)
+    return out
 
 
 def load(M, adj_dbs, prefix_dbs, order_seed=0):

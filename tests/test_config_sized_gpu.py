@@ -1,0 +1,203 @@
+"""BASELINE configs 2, 3 and 5 at their real sizes and production plans,
+against goldens made on the CPU (tests/golden/make_golden.py: oracle/csr_spf.h,
+itself cross-checked there against the reference-style oracle and the literal
+DijkstraQ replay) and against size-independent properties.
+
+  config 2  all 9,976 fabric sources in ONE batch (the msbfs+levels plan):
+            per-source (reached, sum of distances, next-hop pairs) for every
+            source, the order-free mix of every (node, distance) and (node,
+            next hop) pair for 512 sampled sources, the reference-form digest
+            of the 8 fabric_sampled.json sources.
+  config 3  the 100k-node / 1M-link WAN, all 100,000 sources through
+            ShardedAllSources (world 1, push-only delta-stepping): the
+            reference's own checksum of row n0, 32 sampled rows by sha256, and
+            for those rows the Bellman conditions (no edge relaxes, every
+            reached node has a tight in-edge) plus D[s][t] == D[t][s].
+  config 5  8,192 single-link-failure SPFs from the border node 2-0-0 over two
+            areas (fabric + WAN-10k): every query's summary through the C ABI,
+            and sampled queries' reference-form SpfResults through the
+            multi-area LinkState (LinkState::runSpfBatch).
+"""
+
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from tests.golden.make_golden import FABRIC_SOURCES, digest, spf_canon
+from tests.golden.summary import summaries_from_rows
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _batch_summaries(q, g, sources, mix_rows):
+    n = len(sources)
+    V = g.V
+    rows = np.empty((n, V), dtype=np.uint32)
+    q.fetch_rows(0, n, rows.ctypes.data, V * 4, on_device=False)
+    words = [q.nh_words(i) for i in range(n)]
+    masks = q.fetch_nexthops(0, n)
+    nbr_cache = {}
+    nbrs = []
+    for s in sources:
+        s = int(s)
+        if s not in nbr_cache:
+            nbr_cache[s] = g.nbrs(s)
+        nbrs.append(nbr_cache[s])
+    return summaries_from_rows(rows, masks, words, nbrs, mix_rows)
+
+
+def _check_summary(got, want, mix_rows, what):
+    bad = np.nonzero((got[:, :3] != want[:, :3]).any(axis=1))[0]
+    assert len(bad) == 0, f"{what}: {len(bad)} queries differ, first {bad[:5].tolist()}"
+    mr = np.asarray(sorted(mix_rows), dtype=np.int64)
+    bad = mr[got[mr, 3] != want[mr, 3]]
+    assert len(bad) == 0, f"{what}: mix differs for queries {bad[:5].tolist()}"
+
+
+def test_config2_fabric_all_sources_msbfs(gpu_ready):
+    from openr_amd import abi
+    from openr_amd import topologies as TP
+
+    want = np.load(os.path.join(GOLD, "fabric_allsources.npz"))["summary"]
+    topo = TP.fabric(10000)
+    csr = topo.csr()
+    V = csr.num_nodes
+    g = abi.Graph(csr)
+    sources = np.arange(V, dtype=np.uint32)
+    q = g.query(sources, abi.SPF_F_NEXTHOPS)
+    assert q.kernel == "msbfs+levels"  # the production plan of config 2
+    q.run()
+    _, names_by_rank = topo.rank()
+    sampled_ids = [names_by_rank.index(s) for s in FABRIC_SOURCES]
+    mix_rows = sorted(set(range(0, V, V // 512)) | set(sampled_ids))
+    got = _batch_summaries(q, g, sources, mix_rows)
+    _check_summary(got, want, mix_rows, "fabric all-sources")
+    gold = json.load(open(os.path.join(GOLD, "fabric_sampled.json")))
+    for src, sid in zip(FABRIC_SOURCES, sampled_ids):
+        d = q.dist(sid)
+        nh = q.nexthop_sets(sid, sid)
+        c = {names_by_rank[v]: (int(d[v]), sorted(names_by_rank[h] for h in nh[v])) for v in nh}
+        assert digest(c) == gold["spf"][src]["digest"], src
+    q.close()
+    g.close()
+
+
+def test_config3_wan100k_all_sources_sharded(gpu_ready):
+    import torch
+
+    from openr_amd import allsources as AS
+    from openr_amd import topologies as TP
+
+    torch.cuda.set_device(0)
+    gold = json.load(open(os.path.join(GOLD, "wan100k_rows.json")))["rows"]
+    anchor = [a for a in json.load(open(os.path.join(GOLD, "wan_anchors.json")))["anchors"]
+              if a["V"] == 100000 and a["S"] == 1][0]
+    topo = TP.wan(100000, 1000000)
+    csr = topo.csr()
+    V = csr.num_nodes
+    sas = AS.ShardedAllSources(csr, device=0, gather=False)
+    assert sas.kernel == "dstep"  # push-only delta-stepping, the config-3 plan
+    sas.run()
+    # the reference's runSpf checksum of source n0
+    assert int(sas.row(0).astype(np.int64).sum()) == anchor["sum_dist"]
+    row = csr.row_ptr.astype(np.int64)
+    src_of_edge = np.repeat(np.arange(V, dtype=np.int64), np.diff(row))
+    col = csr.col.astype(np.int64)
+    w = csr.metric.astype(np.int64)
+    rows = {}
+    for r in gold:
+        d = sas.row(r["src"])
+        assert hashlib.sha256(d.tobytes()).hexdigest() == r["sha256"], r["src"]
+        rows[r["src"]] = d
+        dd = d.astype(np.int64)
+        reach = d != np.uint32(0xFFFFFFFF)
+        assert reach.all()  # the WAN is connected
+        # Bellman: no edge relaxes, and every non-source node has a tight in-edge
+        cand = dd[src_of_edge] + w
+        assert (cand >= dd[col]).all(), r["src"]
+        tight = np.zeros(V, dtype=bool)
+        tight[col[cand == dd[col]]] = True
+        tight[r["src"]] = True
+        assert tight.all() and dd[r["src"]] == 0, r["src"]
+    srcs = list(rows)
+    for a in srcs:  # symmetric metrics: D[a][b] == D[b][a]
+        for b in srcs:
+            assert rows[a][b] == rows[b][a], (a, b)
+    sas.close()
+
+
+def _two_area():
+    from openr_amd import topologies as TP
+
+    meta = json.load(open(os.path.join(GOLD, "whatif_two_area.json")))
+    want = np.load(os.path.join(GOLD, "whatif_two_area.npz"))["summary"]
+    areas = TP.whatif_two_area()
+    for (area, _, links), m in zip(areas, meta["areas"]):
+        assert m["area"] == area and m["links"] == [int(x) for x in links]
+    return meta, want, areas
+
+
+def test_config5_whatif_batch_c_abi(gpu_ready):
+    from openr_amd import abi
+    from openr_amd import topologies as TP
+
+    meta, want, areas = _two_area()
+    off = 0
+    for area, topo, links in areas:
+        csr = topo.csr()
+        r, _ = topo.rank()
+        sid = int(r[topo.names.index(TP.WHATIF_BORDER)])
+        n = len(links)
+        g = abi.Graph(csr)
+        srcs = np.full(n, sid, dtype=np.uint32)
+        q = g.query(srcs, abi.SPF_F_NEXTHOPS, ignore=[[int(l)] for l in links]).run()
+        mix_rows = sorted(set(range(0, n, 16)) | {s["query"] for m in meta["areas"] if m["area"] == area
+                                                  for s in m["sampled"]})
+        got = _batch_summaries(q, g, srcs, mix_rows)
+        _check_summary(got, want[off:off + n], mix_rows, f"what-if area {area}")
+        off += n
+        q.close()
+        g.close()
+    assert off == len(want) == 8192
+
+
+def test_config5_whatif_multi_area_linkstate(gpu_ready):
+    """The same failures through the drop-in: one AreaLinkStates holding both
+    areas, LinkState::runSpfBatch(border, {link}) per area, sampled results
+    materialised in the reference's SpfResult form."""
+    import openr_amd._openr_spf as E
+    from openr_amd import topologies as TP
+
+    meta, want, areas = _two_area()
+    la = E.AreaLinkStates()
+    for area, topo, _ in areas:
+        ls = la.add(area)
+        for db in topo.adj_dbs(area):
+            ls.updateAdjacencyDatabase(db)
+    off = 0
+    for (area, topo, links), m in zip(areas, meta["areas"]):
+        ls = la[area]
+        ign = []
+        for l in links:
+            a, b = topo.links[int(l)][:2]
+            na, nb = topo.names[a], topo.names[b]
+            ign.append([x for x in ls.linksFromNode(na) if x.getOtherNodeName(na) == nb])
+        E.reset_counters()
+        batch = ls.runSpfBatch(TP.WHATIF_BORDER, ign, True)
+        assert len(batch) == len(links)
+        assert E.get_counters()["decision.spf_runs"] == len(links)
+        _, names_by_rank = topo.rank()
+        for s in m["sampled"]:
+            res = batch.result(s["query"])
+            assert len(res) == s["reached"]
+            assert digest(spf_canon(res)) == s["digest"], (area, s["query"])
+        # every query's distance checksum from the flat batch (node ids = ranks)
+        for qi in range(0, len(links), 97):
+            tot = sum(batch.metric(qi, v) or 0 for v in range(topo.num_nodes))
+            assert tot == int(want[off + qi, 1]), (area, qi)
+        off += len(links)

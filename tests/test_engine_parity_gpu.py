@@ -103,6 +103,24 @@ def test_random_route_db(mods, seed, lfa):
         assert a == b, node
 
 
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("igp", [False, True])
+def test_random_route_db_bgp(mods, seed, igp):
+    """BGP prefixes with random metric vectors (runBestPathSelectionBgp /
+    selectEcmpBgp, Decision.cpp:715-866; SR-MPLS BGP through selectKsp2):
+    every node's RouteDb equals the oracle's (whose BGP rules are pinned by
+    the BGPRedistribution / Ksp2EdEcmpForBGP known answers)."""
+    E, O = mods
+    names, adj_dbs, prefix_dbs = RZ.random_network(600 + seed, n_nodes=24, n_links=50, bgp=True)
+    ea, ep = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    oa, op = RZ.load(O, adj_dbs, prefix_dbs, seed)
+    for lfa in (False, True):
+        es = E.SpfSolver(names[0], True, lfa, False, seed % 2 == 1, igp)
+        os_ = O.SpfSolver(names[0], True, lfa, False, seed % 2 == 1, igp)
+        for node in names:
+            assert es.buildRouteDb(node, ea, ep) == os_.buildRouteDb(node, oa, op), (node, lfa)
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_random_route_db_multi_area(mods, seed):
     E, O = mods

@@ -6,8 +6,9 @@ SP_ECMP prefix: the restatement of SpfSolverImpl::selectEcmpOpenr
 (openr/decision/Decision.cpp:668-712 with getBestAnnouncingNodes :544-630,
 maybeFilterDrainedNodes :651-666, getNextHopsWithMetric :1093-1179,
 getNextHopsThrift :1181-1271).  Parity: for EVERY node, the table's routes
-equal the unicast entries of SpfSolver::buildRouteDb(node) (itself checked
-against the CPU oracle in test_engine_parity_gpu.py) for those prefixes —
+equal the unicast entries of the CPU oracle's buildRouteDb(node) (the
+reference-style restatement, pinned by the reference's known answers) for
+those prefixes —
 seeded random networks with anycast prefixes, drained nodes, overloaded
 links, parallel links and v4 / v6 prefixes, and the benchmark fabric.
 """
@@ -26,6 +27,16 @@ def E(gpu_ready):
     return E
 
 
+@pytest.fixture(scope="module")
+def O():
+    from oracle import build
+
+    build.build()
+    from oracle import _oracle_ref
+
+    return _oracle_ref
+
+
 def _ecmp_only(unicast):
     # SR_MPLS prefixes (fd00::/64 in the generator) are not in the table
     return {k: v for k, v in unicast.items() if not bytes(k[0][0] if isinstance(k[0], tuple) else k[0]).startswith(b"\xfd\x00")}
@@ -33,17 +44,20 @@ def _ecmp_only(unicast):
 
 @pytest.mark.parametrize("seed", range(6))
 @pytest.mark.parametrize("v4", [True, False])
-def test_route_table_matches_build_route_db(E, seed, v4):
+def test_route_table_matches_build_route_db(E, O, seed, v4):
+    """Every node's table routes == the CPU oracle's buildRouteDb (the
+    reference-style restatement, pinned by the reference known answers)."""
     names, adj_dbs, prefix_dbs = RZ.random_network(
         700 + seed, n_nodes=40, n_links=90, overload_prob=0.15, link_overload_prob=0.05
     )
     areas, ps = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    oareas, ops = RZ.load(O, adj_dbs, prefix_dbs, seed)
     table = E.AllNodesRouteTable(areas, "0", ps, v4)
     assert table.spf_ms > 0 and table.route_ms > 0
-    solver = E.SpfSolver(names[0], v4, False)
+    solver = O.SpfSolver(names[0], v4, False)
     checked = 0
     for node in names:
-        db = solver.buildRouteDb(node, areas, ps)
+        db = solver.buildRouteDb(node, oareas, ops)
         got = table.routes(node)
         if db is None:
             assert got == {}, node
@@ -53,23 +67,26 @@ def test_route_table_matches_build_route_db(E, seed, v4):
     assert checked > 0
 
 
-def test_route_table_fabric(E):
+def test_route_table_fabric(E, O):
     from openr_amd import topologies as TP
 
     topo = TP.fabric(600)
-    areas = E.AreaLinkStates()
-    ls = areas.add("0")
     dbs = topo.adj_dbs(overloaded=[5, 77])
-    for db in dbs:
-        ls.updateAdjacencyDatabase(db)
-    ps = E.PrefixState()
-    for pdb in topo.prefix_dbs("0"):
-        ps.updatePrefixDatabase(pdb)
-    table = E.AllNodesRouteTable(areas, "0", ps, True)
+    built = {}
+    for M in (E, O):
+        areas = M.AreaLinkStates()
+        ls = areas.add("0")
+        for db in dbs:
+            ls.updateAdjacencyDatabase(db)
+        ps = M.PrefixState()
+        for pdb in topo.prefix_dbs("0"):
+            ps.updatePrefixDatabase(pdb)
+        built[M] = (areas, ps)
+    table = E.AllNodesRouteTable(built[E][0], "0", built[E][1], True)
     assert table.num_nodes == topo.num_nodes and table.num_prefixes == topo.num_nodes
-    solver = E.SpfSolver("2-0-0", False, False)
+    solver = O.SpfSolver("2-0-0", False, False)
     for node in sorted(topo.names)[:: max(1, topo.num_nodes // 25)] + ["2-0-0"]:
-        db = solver.buildRouteDb(node, areas, ps)
+        db = solver.buildRouteDb(node, *built[O])
         assert table.routes(node) == db["unicast"], node
 
 
@@ -82,7 +99,7 @@ def _delta_py(new, old):
 
 
 @pytest.mark.parametrize("seed", range(4))
-def test_route_table_diff_equals_route_delta(E, seed):
+def test_route_table_diff_equals_route_delta(E, O, seed):
     """Overload / metric churn (same links): the device diff + delta of every
     node equal getRouteDelta of that node's buildRouteDb before and after."""
     import random
@@ -91,8 +108,9 @@ def test_route_table_diff_equals_route_delta(E, seed):
         900 + seed, n_nodes=40, n_links=90, overload_prob=0.1, link_overload_prob=0.0
     )
     areas, ps = RZ.load(E, adj_dbs, prefix_dbs, seed)
-    solver = E.SpfSolver(names[0], True, False)
-    before = {n: solver.buildRouteDb(n, areas, ps) for n in names}
+    oareas, ops = RZ.load(O, adj_dbs, prefix_dbs, seed)
+    osolver = O.SpfSolver(names[0], True, False)
+    before = {n: osolver.buildRouteDb(n, oareas, ops) for n in names}
     t0 = E.AllNodesRouteTable(areas, "0", ps, True)
     rng = random.Random(seed)
     for db in rng.sample(adj_dbs["0"], 3):  # drain toggles and metric changes
@@ -101,6 +119,7 @@ def test_route_table_diff_equals_route_delta(E, seed):
             db.adjacencies[0].metric += rng.randint(1, 9)
     # the same load order: same links, same linksFromNode order (CSR layout)
     areas, ps = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    oareas, ops = RZ.load(O, adj_dbs, prefix_dbs, seed)
     t1 = E.AllNodesRouteTable(areas, "0", ps, True)
     changed = t1.diff(t0)
     total = 0
@@ -110,7 +129,7 @@ def test_route_table_diff_equals_route_delta(E, seed):
         assert len(upd) + len(dele) == c, node
         # device delta == delta of the table rows == getRouteDelta of the host RouteDbs
         assert (upd, sorted(dele)) == _delta_py(t1.routes(node), t0.routes(node)), node
-        after = solver.buildRouteDb(node, areas, ps)
+        after = osolver.buildRouteDb(node, oareas, ops)
         b = _ecmp_only(before[node]["unicast"]) if before.get(node) else {}
         a = _ecmp_only(after["unicast"]) if after else {}
         assert (upd, sorted(dele)) == _delta_py(a, b), node

@@ -327,6 +327,19 @@ def test_exchange_rows_gloo(world):
     assert all(res.values()), res
 
 
+def _oracle_rows(csr, srcs):
+    """uint32 distance rows of the CPU oracle's flat restatement
+    (oracle/csr_spf.h; 0xFFFFFFFF = unreached, like the device table)."""
+    from oracle import build
+
+    build.build()
+    from oracle import _oracle_ref as O
+
+    rows = O.csr_spf_rows(csr.row_ptr, csr.col, csr.metric.astype(np.uint64), csr.link_id,
+                          csr.overloaded, np.asarray(srcs, dtype=np.uint32), True, 8)
+    return np.where(rows == np.uint64(2**64 - 1), np.uint64(0xFFFFFFFF), rows).astype(np.uint32)
+
+
 def _full_table(csr, srcs):
     import torch
 
@@ -375,6 +388,10 @@ def test_repair_equals_full_recompute(gpu_ready, V, L, wmax, nsrc, expect_kernel
         relaxed.append(rep.relaxed)
         got = sas.table.cpu().numpy().view(np.uint32)[: len(srcs)]
         assert (got == _full_table(csr, srcs)).all(), kinds
+        # and against the CPU oracle (oracle/csr_spf.h) on sampled rows
+        pick = np.asarray(sorted(rng.sample(range(len(srcs)), min(48, len(srcs)))))
+        ref = _oracle_rows(csr, srcs[pick])
+        assert (got[pick] == ref).all(), kinds
     assert affected[-1] == 0  # no change: nothing recomputed
     assert min(affected[:-1]) < len(srcs)  # the screen skips sources
     # rows repaired in place (spf_table_repair) unless recompute is forced

@@ -54,6 +54,9 @@ def build_device(force=False):
                 "-o",
                 LIB,
                 srcs[0],
+                "-L/opt/rocm/lib",
+                "-lrocprofiler-sdk-roctx",
+                "-Wl,-rpath,/opt/rocm/lib",
             ]
         )
     return LIB

@@ -35,6 +35,32 @@ std::unordered_map<std::string, int64_t>& counterMap() {
   static std::unordered_map<std::string, int64_t> m;
   return m;
 }
+std::unordered_map<std::string, int64_t>& sampleMap() {
+  static std::unordered_map<std::string, int64_t> m;
+  return m;
+}
+enum class ExportType { COUNT, SUM, AVG };
+// the export types the reference registers (Decision.cpp:105-127)
+const std::unordered_map<std::string, ExportType>& exportTypes() {
+  static const std::unordered_map<std::string, ExportType> m = {
+      {"decision.adj_db_update", ExportType::COUNT},
+      {"decision.incompatible_forwarding_type", ExportType::COUNT},
+      {"decision.missing_loopback_addr", ExportType::SUM},
+      {"decision.no_route_to_label", ExportType::COUNT},
+      {"decision.no_route_to_prefix", ExportType::COUNT},
+      {"decision.path_build_ms", ExportType::AVG},
+      {"decision.prefix_db_update", ExportType::COUNT},
+      {"decision.route_build_ms", ExportType::AVG},
+      {"decision.route_build_runs", ExportType::COUNT},
+      {"decision.skipped_mpls_route", ExportType::COUNT},
+      {"decision.duplicate_node_label", ExportType::COUNT},
+      {"decision.skipped_unicast_route", ExportType::COUNT},
+      {"decision.spf_ms", ExportType::AVG},
+      {"decision.spf_runs", ExportType::COUNT},
+      {"decision.errors", ExportType::COUNT},
+  };
+  return m;
+}
 int& spfDevice() {
   static int d = 0;
   return d;
@@ -44,6 +70,28 @@ int& spfDevice() {
 void Counters::add(const std::string& key, int64_t v) {
   std::lock_guard<std::mutex> g(counterMutex());
   counterMap()[key] += v;
+  ++sampleMap()[key];
+}
+std::unordered_map<std::string, int64_t> Counters::fb303Snapshot() {
+  std::lock_guard<std::mutex> g(counterMutex());
+  std::unordered_map<std::string, int64_t> out;
+  for (const auto& [key, sum] : counterMap()) {
+    auto t = exportTypes().find(key);
+    if (t == exportTypes().end()) {
+      continue; // engine-internal timing keys are not fb303 stats
+    }
+    const int64_t n = sampleMap()[key];
+    const char* suffix = t->second == ExportType::COUNT ? ".count"
+        : t->second == ExportType::SUM                  ? ".sum"
+                                                         : ".avg";
+    const int64_t value = t->second == ExportType::COUNT ? n
+        : t->second == ExportType::SUM                   ? sum
+                                                         : (n ? sum / n : 0);
+    for (const char* window : {"", ".60", ".600", ".3600"}) {
+      out[key + suffix + window] = value;
+    }
+  }
+  return out;
 }
 int64_t Counters::get(const std::string& key) {
   std::lock_guard<std::mutex> g(counterMutex());
@@ -57,6 +105,7 @@ std::unordered_map<std::string, int64_t> Counters::snapshot() {
 void Counters::reset() {
   std::lock_guard<std::mutex> g(counterMutex());
   counterMap().clear();
+  sampleMap().clear();
 }
 
 void setSpfDevice(int device) { spfDevice() = device; }
@@ -465,6 +514,17 @@ std::vector<std::unique_ptr<SpfView>> runBatch(
   }
   spf_query_elapsed_ms(q, &eng.lastMs);
   Counters::add("decision.spf_device_us", (int64_t)(eng.lastMs * 1000.0f));
+  {
+    // decision.spf_ms (LinkState.cpp:875-878): one AVG sample of whole
+    // milliseconds per SPF; a batch's SPFs share its wall time
+    const double batchMs = std::chrono::duration<double, std::milli>(
+                               std::chrono::steady_clock::now() - tBatch)
+                               .count();
+    const int64_t perSpf = (int64_t)(batchMs / (double)sources.size());
+    for (size_t i = 0; i < sources.size(); ++i) {
+      Counters::add("decision.spf_ms", perSpf);
+    }
+  }
   const uint32_t V = (uint32_t)eng.names.size();
   const uint32_t nq = (uint32_t)sources.size();
   out.resize(nq);

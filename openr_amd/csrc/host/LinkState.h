@@ -417,10 +417,17 @@ class LinkState {
 
 // Process-wide counters mirroring the fb303 keys the reference bumps
 // (decision.spf_runs, decision.spf_ms, ...).  Tests assert exact spf_runs.
+// add() is fb303::fbData->addStatValue(key, v, <export type>): the sum and
+// the number of samples are kept; fb303Snapshot() renders them under the
+// names fb303 exports for the key's type (Decision.cpp:105-127,
+// LinkState.cpp:813/878): COUNT -> "<key>.count[.60|.600|.3600]", SUM ->
+// "<key>.sum[...]", AVG -> "<key>.avg[...]".  There are no time windows here:
+// the windowed names carry the all-time value.
 struct Counters {
   static void add(const std::string& key, int64_t v);
   static int64_t get(const std::string& key);
   static std::unordered_map<std::string, int64_t> snapshot();
+  static std::unordered_map<std::string, int64_t> fb303Snapshot();
   static void reset();
 };
 

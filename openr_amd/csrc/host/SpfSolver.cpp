@@ -630,11 +630,14 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
     }
   }
 
+  const auto elapsed = std::chrono::steady_clock::now() - t0;
   Counters::add(
       "decision.route_build_us",
-      std::chrono::duration_cast<std::chrono::microseconds>(
-          std::chrono::steady_clock::now() - t0)
-          .count());
+      std::chrono::duration_cast<std::chrono::microseconds>(elapsed).count());
+  // Decision.cpp:536-540 (AVG of whole milliseconds)
+  Counters::add(
+      "decision.route_build_ms",
+      std::chrono::duration_cast<std::chrono::milliseconds>(elapsed).count());
   return routeDb;
 }
 

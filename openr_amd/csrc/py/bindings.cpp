@@ -164,6 +164,14 @@ PYBIND11_MODULE(_openr_spf, m) {
     return d;
   });
   m.def("reset_counters", &Counters::reset);
+  // fb303-exported names (decision.spf_runs.count, decision.spf_ms.avg, ...)
+  m.def("get_fb303_counters", [] {
+    py::dict d;
+    for (const auto& [k, v] : Counters::fb303Snapshot()) {
+      d[py::str(k)] = v;
+    }
+    return d;
+  });
 
   // HoldableValue<bool> / HoldableValue<LinkStateMetric> (LinkState.h:36-58)
   py::class_<HoldableValue<bool>>(m, "HoldableValueBool")

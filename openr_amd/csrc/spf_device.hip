@@ -48,6 +48,20 @@
 #include "openr_spf.h"
 #include "host/Parallel.h"
 
+// roctx ranges around every C-ABI entry point (SURVEY.md §5 tracing): a
+// rocprofv3 --marker-trace / --kernel-trace run shows which Decision call
+// (graph build, query run, table repair, ...) each kernel belongs to.
+#include <rocprofiler-sdk-roctx/roctx.h>
+namespace {
+struct AbiRange {
+  explicit AbiRange(const char* name) { roctxRangePushA(name); }
+  ~AbiRange() { roctxRangePop(); }
+  AbiRange(const AbiRange&) = delete;
+  AbiRange& operator=(const AbiRange&) = delete;
+};
+} // namespace
+#define SPF_ABI_RANGE(name) AbiRange spf_abi_range_(name)
+
 namespace {
 
 constexpr uint32_t kBlock = 512;           // threads per workgroup (8 waves)
@@ -1950,6 +1964,13 @@ __device__ __forceinline__ void nl_body_multi(
   }
 }
 
+// Write traffic: sources with Wm > 1 mask words store word w of 4 nodes per
+// thread in pass w, i.e. 8-byte pieces at a stride of 8*Wm bytes, so their
+// cache lines are written Wm times, partially (PMC: 1.31 GB written for
+// 0.95 GB of masks on the fabric).  Keeping all words of a node in registers
+// and writing each row once (r02 experiment) removed the excess writes but
+// cost occupancy (91 VGPRs) and time: 0.70 -> 0.82 ms in one launch, 0.92 ms
+// as two launches split by word count.  The per-word pass stays.
 // chunks of 1024 nodes swept by one block (measured on the fabric: 2 ->
 // 0.676 ms, 4 -> 0.682, 16 = whole rows -> 0.710; kNlUnroll 4 / 16 slower)
 #ifndef OPENR_NL_CPB
@@ -2895,6 +2916,7 @@ const char* spf_last_error_detail(void) {
 }
 
 int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
+  SPF_ABI_RANGE("spf_graph_create");
   if (!desc || !out) {
     return fail(SPF_E_INVALID, "null argument");
   }
@@ -3059,11 +3081,13 @@ int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
 }
 
 int spf_graph_destroy(spf_graph* g) {
+  SPF_ABI_RANGE("spf_graph_destroy");
   free_graph(g);
   return SPF_OK;
 }
 
 int spf_graph_set_transit(spf_graph* g, const uint8_t* node_overloaded) {
+  SPF_ABI_RANGE("spf_graph_set_transit");
   if (!g || (g->V && !node_overloaded)) {
     return fail(SPF_E_INVALID, "null argument");
   }
@@ -3082,6 +3106,7 @@ int spf_graph_set_transit(spf_graph* g, const uint8_t* node_overloaded) {
 
 int spf_graph_patch_metrics(
     spf_graph* g, uint32_t n, const uint32_t* edge_idx, const uint64_t* m) {
+  SPF_ABI_RANGE("spf_graph_patch_metrics");
   if (!g || (n && (!edge_idx || !m))) {
     return fail(SPF_E_INVALID, "null argument");
   }
@@ -3131,6 +3156,7 @@ int spf_graph_nbrs(const spf_graph* g, uint32_t node, uint32_t* out) {
 }
 
 int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) {
+  SPF_ABI_RANGE("spf_query_create");
   if (!g || !desc || !out) {
     return fail(SPF_E_INVALID, "null argument");
   }
@@ -3427,6 +3453,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
 }
 
 int spf_query_destroy(spf_query* q) {
+  SPF_ABI_RANGE("spf_query_destroy");
   free_query(q);
   return SPF_OK;
 }
@@ -3879,6 +3906,7 @@ int run_plan(spf_query* q) {
 extern "C" {
 
 int spf_query_run(spf_query* q) {
+  SPF_ABI_RANGE("spf_query_run");
   if (!q) {
     return fail(SPF_E_INVALID, "null query");
   }
@@ -3906,6 +3934,7 @@ int spf_query_run(spf_query* q) {
 }
 
 int spf_query_sync(spf_query* q) {
+  SPF_ABI_RANGE("spf_query_sync");
   if (!q) {
     return fail(SPF_E_INVALID, "null query");
   }
@@ -3986,6 +4015,7 @@ const char* spf_query_kernel_name(const spf_query* q) {
 }
 
 int spf_query_dist(spf_query* q, uint32_t i, uint64_t* out) {
+  SPF_ABI_RANGE("spf_query_dist");
   if (!q || !out || i >= q->nq) {
     return fail(SPF_E_INVALID, "bad query row");
   }
@@ -4022,6 +4052,7 @@ int spf_query_nh_words(const spf_query* q, uint32_t i) {
 }
 
 int spf_query_nexthops(spf_query* q, uint32_t i, uint64_t* out) {
+  SPF_ABI_RANGE("spf_query_nexthops");
   if (!q || !out || i >= q->nq || !(q->flags & SPF_F_NEXTHOPS)) {
     return fail(SPF_E_INVALID, "no next hops for this row");
   }
@@ -4070,6 +4101,7 @@ int spf_query_device_rows(
 int spf_query_fetch_rows(
     spf_query* q, uint32_t first, uint32_t count, void* dst, size_t dst_pitch,
     int dst_on_device) {
+  SPF_ABI_RANGE("spf_query_fetch_rows");
   if (!q || (count && !dst)) {
     return fail(SPF_E_INVALID, "null argument");
   }
@@ -4102,6 +4134,7 @@ int spf_query_fetch_rows(
 
 int spf_query_fetch_nexthops(
     spf_query* q, uint32_t first, uint32_t count, uint64_t* dst) {
+  SPF_ABI_RANGE("spf_query_fetch_nexthops");
   if (!q || (count && !dst)) {
     return fail(SPF_E_INVALID, "null argument");
   }
@@ -4146,6 +4179,7 @@ extern "C" {
 int spf_graph_diff(
     const spf_graph_desc* before, const spf_graph_desc* after,
     spf_edge_delta* out, uint32_t cap, uint32_t* n_out) {
+  SPF_ABI_RANGE("spf_graph_diff");
   if (!before || !after || !n_out || (cap && !out)) {
     return fail(SPF_E_INVALID, "null argument");
   }
@@ -4223,6 +4257,7 @@ int spf_table_screen(
     spf_graph* g, const uint32_t* rows, size_t pitch, uint32_t num_rows,
     const uint32_t* sources, const spf_edge_delta* deltas, uint32_t n_deltas,
     uint8_t* affected) {
+  SPF_ABI_RANGE("spf_table_screen");
   if (!g || (num_rows && (!rows || !sources || !affected)) || (n_deltas && !deltas)) {
     return fail(SPF_E_INVALID, "null argument");
   }
@@ -4297,6 +4332,7 @@ int spf_table_screen(
 
 int spf_query_scatter_rows(
     spf_query* q, const uint32_t* dst_rows, void* table, size_t pitch) {
+  SPF_ABI_RANGE("spf_query_scatter_rows");
   if (!q || (q->nq && (!dst_rows || !table))) {
     return fail(SPF_E_INVALID, "null argument");
   }
@@ -4336,6 +4372,7 @@ int spf_table_repair(
     spf_graph* g, uint32_t* rows, size_t pitch, uint32_t num_rows,
     const uint32_t* sources, const uint32_t* row_idx,
     const spf_edge_delta* deltas, uint32_t n_deltas) {
+  SPF_ABI_RANGE("spf_table_repair");
   if (!g || (num_rows && (!rows || !sources || !row_idx)) || (n_deltas && !deltas)) {
     return fail(SPF_E_INVALID, "null argument");
   }
@@ -4499,6 +4536,7 @@ extern "C" {
 int spf_route_table_create(
     spf_query* q, uint32_t num_prefixes, const uint32_t* ann_offsets,
     const uint32_t* announcers, spf_route_table** out) {
+  SPF_ABI_RANGE("spf_route_table_create");
   if (!q || !out || (num_prefixes && !ann_offsets)) {
     return fail(SPF_E_INVALID, "null argument");
   }
@@ -4574,6 +4612,7 @@ int spf_route_table_destroy(spf_route_table* t) {
 }
 
 int spf_route_table_run(spf_route_table* t) {
+  SPF_ABI_RANGE("spf_route_table_run");
   if (!t) {
     return fail(SPF_E_INVALID, "null table");
   }
@@ -4632,6 +4671,7 @@ int spf_route_table_link_words(const spf_route_table* t, uint32_t i) {
 
 int spf_route_table_fetch(
     spf_route_table* t, uint32_t i, uint32_t* metric, uint32_t* best, uint64_t* links) {
+  SPF_ABI_RANGE("spf_route_table_fetch");
   if (!t || i >= t->q->nq || (t->P && (!metric || !best))) {
     return fail(SPF_E_INVALID, "bad argument");
   }
@@ -4662,6 +4702,7 @@ int spf_route_table_fetch(
 extern "C" {
 
 int spf_route_table_diff(spf_route_table* older, spf_route_table* newer, uint32_t* changed) {
+  SPF_ABI_RANGE("spf_route_table_diff");
   if (!older || !newer || (newer->q->nq && !changed)) {
     return fail(SPF_E_INVALID, "null argument");
   }

@@ -89,6 +89,7 @@ def summaries_from_rows(rows32, masks, words, nbrs, mix_rows=()):
         if len(vv):
             nb = np.asarray(nbrs[q], dtype=np.uint64)[bb]
             key = ((vv.astype(np.uint64) + np.uint64(1)) << np.uint64(32)) | nb
-            mix = mix + splitmix64_np(key).sum(dtype=np.uint64)
+            with np.errstate(over="ignore"):
+                mix = mix + splitmix64_np(key).sum(dtype=np.uint64)
         out[q, 3] = mix
     return out

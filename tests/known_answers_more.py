@@ -974,3 +974,24 @@ def sc_decision_duplicate_prefixes(M, wire=False):
     u1 = d.unicast("1")
     assert u1[addr2.key()]["nexthops"] == NH(nh(adj13, False, 10))
     assert u1[addr4.key()]["nexthops"] == NH(nh(a14, False, 5))
+
+
+def sc_fb303_counter_names(M):
+    """The fb303-exported names the reference tests read: DecisionTest.cpp:
+    1970 (decision.spf_runs.count == 16 on the KSP2 ring) and :1794
+    (decision.duplicate_node_label.count.60).  Engine only (the oracle keeps
+    raw keys)."""
+    if not hasattr(M, "get_fb303_counters"):
+        return
+    M.reset_counters()
+    s, areas, ls, ps, dbs = KA.ring_setup(M, False, True, True)
+    get_route_map(s, ["1", "2", "3", "4"], areas, ps)
+    c = M.get_fb303_counters()
+    assert c["decision.spf_runs.count"] == 16
+    assert c["decision.route_build_runs.count"] == 4
+    assert "decision.spf_ms.avg" in c and "decision.route_build_ms.avg.60" in c
+    dbs["1"].nodeLabel = 2
+    ls.updateAdjacencyDatabase(dbs["1"])
+    M.reset_counters()
+    s.buildRouteDb("1", areas, ps)
+    assert M.get_fb303_counters()["decision.duplicate_node_label.count.60"] == 1

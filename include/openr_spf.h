@@ -278,6 +278,70 @@ int spf_route_table_diff(spf_route_table* older, spf_route_table* newer, uint32_
 /* Changed-prefix bitmap of row i from the last diff: bits[ceil(P/64)]. */
 int spf_route_table_changed(spf_route_table* t, uint32_t i, uint64_t* bits);
 
+/* ---- multi-GPU all-sources tables ----
+ * The reference computes every SpfResult on the one Decision thread
+ * (getSpfResult, LinkState.cpp:791-801; all sources = Decision::
+ * getDecisionRouteDb per node, Decision.cpp:1437-1462).  Here one call fans
+ * an all-sources batch out over devices: sources are split in contiguous
+ * blocks (rank r of `world`: n / world sources, the first n % world ranks one
+ * more), each block runs as one spf_query on its device, and the rows are
+ * exchanged with an in-place RCCL all-gather over xGMI into equal-sized rank
+ * slots.  A cluster is either every device of this process
+ * (spf_cluster_create_local: ncclCommInitAll) or one rank of a
+ * one-process-per-GPU job (spf_cluster_create_rank: ncclCommInitRank over an
+ * id from spf_cluster_unique_id that the caller hands to every rank). */
+typedef struct spf_cluster spf_cluster;
+typedef struct spf_table spf_table;
+
+#define SPF_CLUSTER_ID_BYTES 128
+#define SPF_T_GATHER_ROWS 0x100u     /* all-gather the uint32 distance rows */
+#define SPF_T_GATHER_NEXTHOPS 0x200u /* all-gather the packed next-hop masks */
+
+int spf_cluster_unique_id(uint8_t* id /*[SPF_CLUSTER_ID_BYTES]*/);
+int spf_cluster_create_local(uint32_t num_devices, const int* devices, spf_cluster** out);
+int spf_cluster_create_rank(
+    uint32_t world, uint32_t rank, const uint8_t* id, int device, spf_cluster** out);
+int spf_cluster_destroy(spf_cluster* c);
+int spf_cluster_info(
+    const spf_cluster* c, uint32_t* world, uint32_t* first_rank, uint32_t* local_devices);
+const char* spf_cluster_last_error(void);
+
+/* Host only: the block boundaries (block_first[world + 1]) and, when
+ * mask_off is non-NULL, the word offset of every source's next-hop masks in
+ * the gathered mask buffer (rank slots of *mask_cap words; within a slot the
+ * block's sources back to back, V * nh_words[i] words each rounded up to 4).
+ * nh_words may be NULL (one word each). */
+int spf_table_layout(
+    uint32_t num_sources, uint32_t world, uint32_t num_nodes, const uint32_t* nh_words,
+    uint64_t* block_first, uint64_t* mask_off, uint64_t* mask_cap);
+/* One graph per local device from `desc` (desc->device ignored), the local
+ * ranks' source blocks as queries.  flags: SPF_F_UNIT_METRIC,
+ * SPF_F_NEXTHOPS, SPF_T_GATHER_ROWS, SPF_T_GATHER_NEXTHOPS. */
+int spf_table_create(
+    spf_cluster* c, const spf_graph_desc* desc, uint32_t num_sources, const uint32_t* sources,
+    uint32_t flags, spf_table** out);
+int spf_table_destroy(spf_table* t);
+/* Enqueue every local block and the all-gathers (asynchronous). */
+int spf_table_run(spf_table* t);
+int spf_table_sync(spf_table* t);
+/* Device time of the last run, max over local devices: the SPF batch (plus
+ * the copy into the own slot) and the RCCL exchange. */
+int spf_table_elapsed_ms(spf_table* t, float* compute_ms, float* gather_ms);
+int spf_table_block(const spf_table* t, uint32_t rank, uint32_t* first, uint32_t* count);
+int spf_table_nh_words(const spf_table* t, uint32_t i);
+/* Rows / masks of sources [first, first+count) to host memory (from the
+ * local owner, or from the gathered copy; SPF_E_UNSUPPORTED for another
+ * rank's rows without the gather flag).  Masks back to back, V * nh_words(i)
+ * words each. */
+int spf_table_fetch_rows(spf_table* t, uint32_t first, uint32_t count, uint32_t* dst);
+int spf_table_fetch_nexthops(spf_table* t, uint32_t first, uint32_t count, uint64_t* dst);
+/* Gathered buffers on local device `local`: rows [world * cap][V] uint32
+ * (cap = ceil(n / world)), masks [world * mask_cap] uint64; NULL when that
+ * gather is off. */
+int spf_table_device_buffers(
+    spf_table* t, uint32_t local, void** rows, void** masks, uint64_t* mask_cap_words);
+int spf_table_kernel_name(spf_table* t, uint32_t local, const char** name);
+
 #ifdef __cplusplus
 }
 #endif

@@ -67,7 +67,29 @@ EXPORTED_SYMBOLS = (
     "spf_route_table_fetch",
     "spf_route_table_diff",
     "spf_route_table_changed",
+    "spf_cluster_unique_id",
+    "spf_cluster_create_local",
+    "spf_cluster_create_rank",
+    "spf_cluster_destroy",
+    "spf_cluster_info",
+    "spf_cluster_last_error",
+    "spf_table_layout",
+    "spf_table_create",
+    "spf_table_destroy",
+    "spf_table_run",
+    "spf_table_sync",
+    "spf_table_elapsed_ms",
+    "spf_table_block",
+    "spf_table_nh_words",
+    "spf_table_fetch_rows",
+    "spf_table_fetch_nexthops",
+    "spf_table_device_buffers",
+    "spf_table_kernel_name",
 )
+
+SPF_CLUSTER_ID_BYTES = 128
+SPF_T_GATHER_ROWS = 0x100
+SPF_T_GATHER_NEXTHOPS = 0x200
 
 SPF_DELTA_REMOVED = 1
 SPF_DELTA_ADDED = 2
@@ -203,6 +225,24 @@ def load():
         ),
         "spf_query_scatter_rows": (C.c_int, [vp, pu32, vp, C.c_size_t]),
         "spf_table_repair": (C.c_int, [vp, vp, C.c_size_t, u32, pu32, pu32, vp, u32]),
+        "spf_cluster_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
+        "spf_cluster_create_local": (C.c_int, [u32, C.POINTER(C.c_int), C.POINTER(vp)]),
+        "spf_cluster_create_rank": (C.c_int, [u32, u32, C.POINTER(C.c_uint8), C.c_int, C.POINTER(vp)]),
+        "spf_cluster_destroy": (C.c_int, [vp]),
+        "spf_cluster_info": (C.c_int, [vp, pu32, pu32, pu32]),
+        "spf_cluster_last_error": (C.c_char_p, []),
+        "spf_table_layout": (C.c_int, [u32, u32, u32, pu32, pu64, pu64, pu64]),
+        "spf_table_create": (C.c_int, [vp, C.POINTER(_GraphDesc), u32, pu32, u32, C.POINTER(vp)]),
+        "spf_table_destroy": (C.c_int, [vp]),
+        "spf_table_run": (C.c_int, [vp]),
+        "spf_table_sync": (C.c_int, [vp]),
+        "spf_table_elapsed_ms": (C.c_int, [vp, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+        "spf_table_block": (C.c_int, [vp, u32, pu32, pu32]),
+        "spf_table_nh_words": (C.c_int, [vp, u32]),
+        "spf_table_fetch_rows": (C.c_int, [vp, u32, u32, pu32]),
+        "spf_table_fetch_nexthops": (C.c_int, [vp, u32, u32, pu64]),
+        "spf_table_device_buffers": (C.c_int, [vp, u32, C.POINTER(vp), C.POINTER(vp), pu64]),
+        "spf_table_kernel_name": (C.c_int, [vp, u32, C.POINTER(C.c_char_p)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -526,3 +566,143 @@ class Query:
             "device_rows",
         )
         return dp.value, eb.value, np_.value, nt.value
+
+
+# ------------------------------------------------- multi-GPU tables (RCCL)
+
+
+def _check_cl(status: int, what: str):
+    if status != SPF_OK:
+        lib = load()
+        raise SpfError(
+            f"{what}: {lib.spf_error_string(status).decode()} "
+            f"({lib.spf_cluster_last_error().decode()} / {lib.spf_last_error_detail().decode()})"
+        )
+
+
+def table_layout(n: int, world: int, V: int, nh_words=None):
+    """spf_table_layout (host only): (block_first uint64[world+1],
+    mask_off uint64[n], mask_cap words per rank slot)."""
+    bf = np.zeros(world + 1, dtype=np.uint64)
+    mo = np.zeros(max(n, 1), dtype=np.uint64)
+    cap = C.c_uint64()
+    w = None if nh_words is None else np.ascontiguousarray(nh_words, dtype=np.uint32)
+    _check_cl(load().spf_table_layout(n, world, V, _p(w, C.c_uint32) if w is not None else None,
+                                      _p(bf, C.c_uint64), _p(mo, C.c_uint64), C.byref(cap)),
+              "spf_table_layout")
+    return bf, mo[:n], int(cap.value)
+
+
+def cluster_unique_id() -> bytes:
+    buf = (C.c_uint8 * SPF_CLUSTER_ID_BYTES)()
+    _check_cl(load().spf_cluster_unique_id(buf), "spf_cluster_unique_id")
+    return bytes(buf)
+
+
+class Cluster:
+    """RCCL communicator(s) of an all-sources fan-out: every listed local
+    device (spf_cluster_create_local) or one rank of a one-process-per-GPU
+    job (spf_cluster_create_rank, `uid` from cluster_unique_id on one rank)."""
+
+    def __init__(self, devices=None, *, world=None, rank=None, uid=None, device=0):
+        lib = load()
+        h = C.c_void_p()
+        if world is None:
+            devs = (C.c_int * len(devices))(*devices)
+            _check_cl(lib.spf_cluster_create_local(len(devices), devs, C.byref(h)),
+                      "spf_cluster_create_local")
+        else:
+            idb = (C.c_uint8 * SPF_CLUSTER_ID_BYTES)(*uid)
+            _check_cl(lib.spf_cluster_create_rank(world, rank, idb, device, C.byref(h)),
+                      "spf_cluster_create_rank")
+        self.h = h
+        w, f, n = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        _check_cl(lib.spf_cluster_info(h, C.byref(w), C.byref(f), C.byref(n)), "spf_cluster_info")
+        self.world, self.first_rank, self.local_devices = w.value, f.value, n.value
+
+    def close(self):
+        if self.h:
+            load().spf_cluster_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Table:
+    """All-sources table sharded over a Cluster (spf_table_*)."""
+
+    def __init__(self, cluster: Cluster, csr: "Csr", sources, flags):
+        lib = load()
+        self.cluster = cluster
+        self.V = csr.num_nodes
+        src = np.ascontiguousarray(sources, dtype=np.uint32)
+        d, keep = _graph_desc(csr, 0)
+        h = C.c_void_p()
+        _check_cl(lib.spf_table_create(cluster.h, C.byref(d), len(src), _p(src, C.c_uint32), flags,
+                                       C.byref(h)), "spf_table_create")
+        self.h = h
+        self.n = len(src)
+        self.flags = flags
+        self._keep = (keep, src)
+
+    def close(self):
+        if self.h:
+            load().spf_table_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def run(self, sync=True):
+        _check_cl(load().spf_table_run(self.h), "spf_table_run")
+        if sync:
+            self.sync()
+        return self
+
+    def sync(self):
+        _check_cl(load().spf_table_sync(self.h), "spf_table_sync")
+
+    def elapsed_ms(self):
+        a, b = C.c_float(), C.c_float()
+        _check_cl(load().spf_table_elapsed_ms(self.h, C.byref(a), C.byref(b)), "spf_table_elapsed_ms")
+        return float(a.value), float(b.value)
+
+    def block(self, rank: int):
+        f, c = C.c_uint32(), C.c_uint32()
+        _check_cl(load().spf_table_block(self.h, rank, C.byref(f), C.byref(c)), "spf_table_block")
+        return f.value, c.value
+
+    def nh_words(self, i: int) -> int:
+        return load().spf_table_nh_words(self.h, i)
+
+    def kernel(self, local: int = 0) -> str:
+        n = C.c_char_p()
+        _check_cl(load().spf_table_kernel_name(self.h, local, C.byref(n)), "spf_table_kernel_name")
+        return n.value.decode()
+
+    def fetch_rows(self, first: int, count: int) -> np.ndarray:
+        out = np.empty((count, self.V), dtype=np.uint32)
+        _check_cl(load().spf_table_fetch_rows(self.h, first, count, _p(out, C.c_uint32)),
+                  "spf_table_fetch_rows")
+        return out
+
+    def fetch_nexthops(self, first: int, count: int) -> np.ndarray:
+        n = sum(self.V * self.nh_words(i) for i in range(first, first + count))
+        out = np.zeros(max(n, 1), dtype=np.uint64)
+        _check_cl(load().spf_table_fetch_nexthops(self.h, first, count, _p(out, C.c_uint64)),
+                  "spf_table_fetch_nexthops")
+        return out[:n]
+
+    def device_buffers(self, local: int = 0):
+        r, m = C.c_void_p(), C.c_void_p()
+        cap = C.c_uint64()
+        _check_cl(load().spf_table_device_buffers(self.h, local, C.byref(r), C.byref(m), C.byref(cap)),
+                  "spf_table_device_buffers")
+        return r.value, m.value, int(cap.value)

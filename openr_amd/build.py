@@ -40,7 +40,8 @@ def _run(cmd):
 
 
 def build_device(force=False):
-    srcs = [os.path.join(CSRC, "spf_device.hip"), os.path.join(INC, "openr_spf.h")]
+    srcs = [os.path.join(CSRC, "spf_device.hip"), os.path.join(CSRC, "spf_cluster.hip"),
+            os.path.join(INC, "openr_spf.h")]
     if force or _newer(LIB, srcs):
         _run(
             [
@@ -54,7 +55,9 @@ def build_device(force=False):
                 "-o",
                 LIB,
                 srcs[0],
+                srcs[1],
                 "-L/opt/rocm/lib",
+                "-lrccl",
                 "-lrocprofiler-sdk-roctx",
                 "-Wl,-rpath,/opt/rocm/lib",
             ]

@@ -111,6 +111,39 @@ void Counters::reset() {
 void setSpfDevice(int device) { spfDevice() = device; }
 int getSpfDevice() { return spfDevice(); }
 
+namespace {
+struct ClusterState {
+  std::mutex mu;
+  std::vector<int> devices;
+  // not destroyed at process exit: RCCL / HIP teardown from a static
+  // destructor can run after the runtime's own exit handlers
+  spf_cluster* cluster{nullptr};
+};
+ClusterState& clusterState() {
+  static ClusterState s;
+  return s;
+}
+} // namespace
+
+void setSpfDevices(const std::vector<int>& devices) {
+  auto& cs = clusterState();
+  std::lock_guard<std::mutex> g(cs.mu);
+  if (cs.devices == devices) {
+    return;
+  }
+  if (cs.cluster) {
+    spf_cluster_destroy(cs.cluster);
+    cs.cluster = nullptr;
+  }
+  cs.devices = devices;
+}
+
+std::vector<int> getSpfDevices() {
+  auto& cs = clusterState();
+  std::lock_guard<std::mutex> g(cs.mu);
+  return cs.devices;
+}
+
 // --------------------------------------------------------------- hashing
 
 namespace {
@@ -599,6 +632,94 @@ std::vector<std::unique_ptr<SpfView>> runBatch(
   };
   // the single-row reads of the exact plan go through the ABI (one thread)
   parallelFor(nq, exact ? 1u : hostThreads(nq, 32), fill, 8);
+  return out;
+}
+
+// The multi-GPU fan-out of one all-sources batch (setSpfDevices): the
+// sources are split over the cluster's devices in one spf_table run and every
+// block comes back to the host from the device that computed it.  Same
+// views as runBatch (32-bit rows shared from one block, next-hop masks).
+std::vector<std::unique_ptr<SpfView>> runBatchCluster(
+    LinkState::Engine& eng, const std::vector<uint32_t>& sources, bool useLinkMetric) {
+  const auto tBatch = std::chrono::steady_clock::now();
+  auto& cs = clusterState();
+  std::lock_guard<std::mutex> g(cs.mu);
+  if (!cs.cluster) {
+    const int s = spf_cluster_create_local(
+        (uint32_t)cs.devices.size(), cs.devices.data(), &cs.cluster);
+    if (s != SPF_OK) {
+      throw std::runtime_error(
+          std::string("MI355X SPF engine failure in spf_cluster_create_local: ") +
+          spf_error_string(s) + " (" + spf_cluster_last_error() + ")");
+    }
+  }
+  const uint32_t V = (uint32_t)eng.names.size();
+  const uint32_t nq = (uint32_t)sources.size();
+  spf_graph_desc d{};
+  d.num_nodes = V;
+  d.num_edges = (uint32_t)eng.col.size();
+  d.row_ptr = eng.row.data();
+  d.col = eng.col.data();
+  d.metric = eng.metric.data();
+  d.link_id = eng.linkId.data();
+  d.rev = eng.rev.data();
+  d.node_overloaded = eng.overloaded.data();
+  d.num_links = (uint32_t)eng.links.size();
+  spf_table* t = nullptr;
+  auto check = [&](int s, const char* what) {
+    if (s != SPF_OK) {
+      if (t) {
+        spf_table_destroy(t);
+      }
+      throw std::runtime_error(
+          std::string("MI355X SPF engine failure in ") + what + ": " + spf_error_string(s) +
+          " (" + spf_cluster_last_error() + " / " + spf_last_error_detail() + ")");
+    }
+  };
+  check(spf_table_create(cs.cluster, &d, nq, sources.data(),
+                         SPF_F_NEXTHOPS | (useLinkMetric ? 0u : SPF_F_UNIT_METRIC), &t),
+        "spf_table_create");
+  check(spf_table_run(t), "spf_table_run");
+  check(spf_table_sync(t), "spf_table_sync");
+  float cm = 0, gm = 0;
+  check(spf_table_elapsed_ms(t, &cm, &gm), "spf_table_elapsed_ms");
+  eng.lastMs = cm + gm;
+  Counters::add("decision.spf_device_us", (int64_t)(eng.lastMs * 1000.0f));
+  Counters::add("decision.spf_cluster_batches", 1);
+  auto rows32 = std::make_shared<std::vector<uint32_t>>((size_t)nq * V);
+  check(spf_table_fetch_rows(t, 0, nq, rows32->data()), "spf_table_fetch_rows");
+  std::vector<uint32_t> words(nq);
+  std::vector<uint64_t> maskOff(nq + 1, 0);
+  for (uint32_t i = 0; i < nq; ++i) {
+    words[i] = (uint32_t)spf_table_nh_words(t, i);
+    maskOff[i + 1] = maskOff[i] + (uint64_t)V * words[i];
+  }
+  std::vector<uint64_t> masks(maskOff[nq]);
+  check(spf_table_fetch_nexthops(t, 0, nq, masks.data()), "spf_table_fetch_nexthops");
+  spf_table_destroy(t);
+  t = nullptr;
+  std::vector<std::unique_ptr<SpfView>> out(nq);
+  parallelFor(nq, hostThreads(nq, 32), [&](size_t i, unsigned) {
+    auto view = std::make_unique<SpfView>();
+    view->src = sources[i];
+    view->useLinkMetric = useLinkMetric;
+    view->dist.share32(rows32, i * V, V);
+    view->words = words[i];
+    view->nh.assign(masks.begin() + maskOff[i], masks.begin() + maskOff[i + 1]);
+    const int nn = spf_graph_num_nbrs(eng.graph, sources[i]);
+    view->nbrs.resize(std::max(nn, 0));
+    if (nn > 0) {
+      spf_graph_nbrs(eng.graph, sources[i], view->nbrs.data());
+    }
+    out[i] = std::move(view);
+  }, 8);
+  const double batchMs = std::chrono::duration<double, std::milli>(
+                             std::chrono::steady_clock::now() - tBatch)
+                             .count();
+  Counters::add("decision.spf_batch_us", (int64_t)(batchMs * 1000.0));
+  for (uint32_t i = 0; i < nq; ++i) {
+    Counters::add("decision.spf_ms", (int64_t)(batchMs / (double)nq));
+  }
   return out;
 }
 
@@ -1149,7 +1270,11 @@ void LinkState::prefetchSpf(const std::vector<std::string>& nodes, bool useLinkM
   if (todo.empty()) {
     return;
   }
-  auto views = runBatch(eng, todo, useLinkMetric, true, nullptr);
+  // the multi-GPU fan-out for big batches on the fast (32-bit) plans
+  const bool fanOut = !getSpfDevices().empty() && todo.size() >= kClusterMinSources &&
+      !(eng.exact && useLinkMetric);
+  auto views = fanOut ? runBatchCluster(eng, todo, useLinkMetric)
+                      : runBatch(eng, todo, useLinkMetric, true, nullptr);
   for (size_t i = 0; i < todo.size(); ++i) {
     pre.emplace(todo[i], std::move(views[i]));
   }

@@ -434,6 +434,15 @@ struct Counters {
 // Which HIP device new LinkStates bind to (one process per GPU).
 void setSpfDevice(int device);
 int getSpfDevice();
+// Devices of the multi-GPU fan-out: when non-empty,
+// LinkState::prefetchSpf batches of at least kClusterMinSources sources
+// (all-sources views, every node's RouteDb) are split over these devices in
+// one call (spf_cluster_create_local + spf_table_*, one RCCL communicator per
+// device) and every block's rows come back to the host from its own device.
+// Empty (the default) = everything on getSpfDevice().
+void setSpfDevices(const std::vector<int>& devices);
+std::vector<int> getSpfDevices();
+constexpr size_t kClusterMinSources = 64;
 
 } // namespace openr
 

@@ -156,6 +156,8 @@ PYBIND11_MODULE(_openr_spf, m) {
   m.def("device_count", &spf_device_count);
   m.def("set_spf_device", &setSpfDevice);
   m.def("get_spf_device", &getSpfDevice);
+  m.def("set_spf_devices", &setSpfDevices);
+  m.def("get_spf_devices", &getSpfDevices);
   m.def("get_counters", [] {
     py::dict d;
     for (const auto& [k, v] : Counters::snapshot()) {

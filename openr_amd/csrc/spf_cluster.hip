@@ -1,0 +1,552 @@
+// spf_cluster.hip — multi-GPU all-sources tables inside the C ABI
+// (SURVEY.md §8(b) "the multi-GPU fan-out happens inside the call", §8(e)).
+//
+// Open/R's Decision is one thread in one process (Decision.cpp:1771-1814), so
+// the fan-out is first a single-process one: spf_cluster_create_local builds
+// one RCCL communicator per local device (ncclCommInitAll) and a table keeps
+// one spf_graph + one spf_query per device.  A job launched one process per
+// GPU (the benchmark's torchrun mode) joins the same machinery with
+// spf_cluster_create_rank (ncclCommInitRank over an id the caller
+// distributes).  Sources are sharded in contiguous blocks (block r of n
+// sources over `world` ranks: base = n / world, the first n % world ranks one
+// more), every block runs as one batch on its device, and the one exchange
+// step is an in-place ncclAllGather over xGMI of the uint32 distance rows
+// (SPF_T_GATHER_ROWS) and of the packed next-hop masks (SPF_T_GATHER_NEXTHOPS)
+// into equal-sized rank slots.  Without the gather flags the rows stay on
+// their owner device (a RouteDb needs only its own row; the host fetches
+// blocks directly).
+//
+// This layer composes the single-device ABI (spf_graph_* / spf_query_*) with
+// RCCL; it launches no kernels of its own.
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "openr_spf.h"
+
+#include <rocprofiler-sdk-roctx/roctx.h>
+
+namespace {
+
+struct ClusterRange {
+  explicit ClusterRange(const char* name) { roctxRangePushA(name); }
+  ~ClusterRange() { roctxRangePop(); }
+  ClusterRange(const ClusterRange&) = delete;
+  ClusterRange& operator=(const ClusterRange&) = delete;
+};
+#define SPF_ABI_RANGE_CLUSTER(name) ClusterRange spf_cluster_range_(name)
+
+thread_local std::string g_cluster_err;
+
+int cfail(int status, const std::string& what) {
+  g_cluster_err = what;
+  return status;
+}
+
+#define CL_HIP(expr)                                                        \
+  do {                                                                      \
+    hipError_t e_ = (expr);                                                 \
+    if (e_ != hipSuccess) {                                                 \
+      return cfail(SPF_E_DEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    }                                                                       \
+  } while (0)
+
+#define CL_NCCL(expr)                                                        \
+  do {                                                                       \
+    ncclResult_t r_ = (expr);                                                \
+    if (r_ != ncclSuccess) {                                                 \
+      return cfail(SPF_E_DEVICE, std::string(#expr ": ") + ncclGetErrorString(r_)); \
+    }                                                                        \
+  } while (0)
+
+#define CL_TRY(expr)        \
+  do {                      \
+    int s_ = (expr);        \
+    if (s_ != SPF_OK) {     \
+      return s_;            \
+    }                       \
+  } while (0)
+
+uint64_t roundup4(uint64_t x) { return (x + 3) & ~3ull; }
+
+} // namespace
+
+struct spf_cluster {
+  uint32_t world = 1;
+  uint32_t first_rank = 0; // global rank of local device 0
+  std::vector<int> devices;
+  std::vector<ncclComm_t> comms;
+};
+
+struct spf_table {
+  spf_cluster* c = nullptr;
+  uint32_t V = 0, n = 0, flags = 0, cap = 0;
+  std::vector<uint32_t> sources;
+  std::vector<uint32_t> words;       // next-hop words per source
+  std::vector<uint64_t> block_first; // [world + 1] source index boundaries
+  std::vector<uint64_t> mask_off;    // word offset of each source in the gathered masks
+  uint64_t mask_cap = 0;             // words per rank slot of the gathered masks
+  struct Local {
+    int device = 0;
+    uint32_t rank = 0;
+    spf_graph* g = nullptr;
+    spf_query* q = nullptr;
+    uint32_t* rows = nullptr;  // gathered rows [world * cap][V] (GATHER_ROWS)
+    uint64_t* masks = nullptr; // gathered masks [world * mask_cap] (GATHER_NEXTHOPS)
+    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+  };
+  std::vector<Local> local;
+  bool ran = false;
+};
+
+extern "C" {
+
+const char* spf_cluster_last_error(void) { return g_cluster_err.c_str(); }
+
+int spf_table_layout(
+    uint32_t num_sources, uint32_t world, uint32_t num_nodes, const uint32_t* nh_words,
+    uint64_t* block_first, uint64_t* mask_off, uint64_t* mask_cap) {
+  if (world == 0 || !block_first) {
+    return cfail(SPF_E_INVALID, "spf_table_layout: world == 0 or no block_first");
+  }
+  const uint32_t base = num_sources / world, extra = num_sources % world;
+  for (uint32_t r = 0; r <= world; ++r) {
+    block_first[r] = (uint64_t)r * base + std::min(r, extra);
+  }
+  uint64_t cap = 0;
+  for (uint32_t r = 0; r < world; ++r) {
+    uint64_t words = 0;
+    for (uint64_t i = block_first[r]; i < block_first[r + 1]; ++i) {
+      if (mask_off) {
+        mask_off[i] = words; // within the slot; the slot base is added below
+      }
+      words += roundup4((uint64_t)num_nodes * (nh_words ? nh_words[i] : 1));
+    }
+    cap = std::max(cap, words);
+  }
+  if (mask_off) {
+    for (uint32_t r = 0; r < world; ++r) {
+      for (uint64_t i = block_first[r]; i < block_first[r + 1]; ++i) {
+        mask_off[i] += (uint64_t)r * cap;
+      }
+    }
+  }
+  if (mask_cap) {
+    *mask_cap = cap;
+  }
+  return SPF_OK;
+}
+
+int spf_cluster_unique_id(uint8_t* id) {
+  if (!id) {
+    return cfail(SPF_E_INVALID, "spf_cluster_unique_id: null id");
+  }
+  ncclUniqueId u;
+  CL_NCCL(ncclGetUniqueId(&u));
+  std::memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+  return SPF_OK;
+}
+
+int spf_cluster_create_local(uint32_t num_devices, const int* devices, spf_cluster** out) {
+  SPF_ABI_RANGE_CLUSTER("spf_cluster_create_local");
+  if (!out || num_devices == 0 || !devices) {
+    return cfail(SPF_E_INVALID, "spf_cluster_create_local: no devices");
+  }
+  int have = 0;
+  if (hipGetDeviceCount(&have) != hipSuccess || have <= 0) {
+    return cfail(SPF_E_DEVICE, "spf_cluster_create_local: no HIP device");
+  }
+  for (uint32_t i = 0; i < num_devices; ++i) {
+    if (devices[i] < 0 || devices[i] >= have) {
+      return cfail(SPF_E_INVALID, "spf_cluster_create_local: device out of range");
+    }
+  }
+  auto c = std::make_unique<spf_cluster>();
+  c->world = num_devices;
+  c->devices.assign(devices, devices + num_devices);
+  c->comms.resize(num_devices);
+  CL_NCCL(ncclCommInitAll(c->comms.data(), (int)num_devices, devices));
+  *out = c.release();
+  return SPF_OK;
+}
+
+int spf_cluster_create_rank(
+    uint32_t world, uint32_t rank, const uint8_t* id, int device, spf_cluster** out) {
+  SPF_ABI_RANGE_CLUSTER("spf_cluster_create_rank");
+  if (!out || !id || world == 0 || rank >= world) {
+    return cfail(SPF_E_INVALID, "spf_cluster_create_rank: bad rank / world / id");
+  }
+  CL_HIP(hipSetDevice(device));
+  auto c = std::make_unique<spf_cluster>();
+  c->world = world;
+  c->first_rank = rank;
+  c->devices = {device};
+  c->comms.resize(1);
+  ncclUniqueId u;
+  std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+  CL_NCCL(ncclCommInitRank(&c->comms[0], (int)world, u, (int)rank));
+  *out = c.release();
+  return SPF_OK;
+}
+
+int spf_cluster_destroy(spf_cluster* c) {
+  if (!c) {
+    return SPF_OK;
+  }
+  for (auto comm : c->comms) {
+    if (comm) {
+      (void)ncclCommDestroy(comm);
+    }
+  }
+  delete c;
+  return SPF_OK;
+}
+
+int spf_cluster_info(
+    const spf_cluster* c, uint32_t* world, uint32_t* first_rank, uint32_t* local_devices) {
+  if (!c) {
+    return cfail(SPF_E_INVALID, "spf_cluster_info: null cluster");
+  }
+  if (world) {
+    *world = c->world;
+  }
+  if (first_rank) {
+    *first_rank = c->first_rank;
+  }
+  if (local_devices) {
+    *local_devices = (uint32_t)c->devices.size();
+  }
+  return SPF_OK;
+}
+
+static void free_table(spf_table* t) {
+  for (auto& L : t->local) {
+    (void)hipSetDevice(L.device);
+    if (L.q) {
+      spf_query_destroy(L.q);
+    }
+    if (L.g) {
+      spf_graph_destroy(L.g);
+    }
+    if (L.rows) {
+      (void)hipFree(L.rows);
+    }
+    if (L.masks) {
+      (void)hipFree(L.masks);
+    }
+    for (hipEvent_t e : {L.e0, L.e1, L.e2}) {
+      if (e) {
+        (void)hipEventDestroy(e);
+      }
+    }
+  }
+  delete t;
+}
+
+int spf_table_destroy(spf_table* t) {
+  if (t) {
+    free_table(t);
+  }
+  return SPF_OK;
+}
+
+int spf_table_create(
+    spf_cluster* c, const spf_graph_desc* desc, uint32_t num_sources, const uint32_t* sources,
+    uint32_t flags, spf_table** out) {
+  SPF_ABI_RANGE_CLUSTER("spf_table_create");
+  if (!c || !desc || !out || (num_sources && !sources)) {
+    return cfail(SPF_E_INVALID, "spf_table_create: null argument");
+  }
+  const uint32_t qflags = flags & (SPF_F_UNIT_METRIC | SPF_F_NEXTHOPS);
+  if ((flags & SPF_T_GATHER_NEXTHOPS) && !(flags & SPF_F_NEXTHOPS)) {
+    return cfail(SPF_E_INVALID, "spf_table_create: GATHER_NEXTHOPS needs SPF_F_NEXTHOPS");
+  }
+  for (uint32_t i = 0; i < num_sources; ++i) {
+    if (sources[i] >= desc->num_nodes) {
+      return cfail(SPF_E_INVALID, "spf_table_create: source out of range");
+    }
+  }
+  std::unique_ptr<spf_table, void (*)(spf_table*)> t(new spf_table, free_table);
+  t->c = c;
+  t->V = desc->num_nodes;
+  t->n = num_sources;
+  t->flags = flags;
+  t->sources.assign(sources, sources + num_sources);
+  t->cap = (num_sources + c->world - 1) / c->world;
+  t->block_first.resize(c->world + 1);
+  t->local.resize(c->devices.size());
+  for (size_t d = 0; d < c->devices.size(); ++d) {
+    auto& L = t->local[d];
+    L.device = c->devices[d];
+    L.rank = c->first_rank + (uint32_t)d;
+    spf_graph_desc gd = *desc;
+    gd.device = L.device;
+    CL_TRY(spf_graph_create(&gd, &L.g));
+  }
+  // next-hop words of every source (the gathered mask layout needs all of
+  // them; distinct neighbour counts come from the graph, any device)
+  t->words.assign(num_sources, 1);
+  if (qflags & SPF_F_NEXTHOPS) {
+    for (uint32_t i = 0; i < num_sources; ++i) {
+      const int nb = spf_graph_num_nbrs(t->local[0].g, sources[i]);
+      if (nb < 0) {
+        return nb;
+      }
+      t->words[i] = std::max<uint32_t>(1, ((uint32_t)nb + 63) / 64);
+    }
+  }
+  t->mask_off.resize(num_sources);
+  CL_TRY(spf_table_layout(num_sources, c->world, t->V, t->words.data(), t->block_first.data(),
+                          t->mask_off.data(), &t->mask_cap));
+  for (auto& L : t->local) {
+    CL_HIP(hipSetDevice(L.device));
+    const uint64_t first = t->block_first[L.rank], count = t->block_first[L.rank + 1] - first;
+    if (count) {
+      spf_query_desc qd{};
+      qd.num_queries = (uint32_t)count;
+      qd.sources = t->sources.data() + first;
+      qd.flags = qflags;
+      CL_TRY(spf_query_create(L.g, &qd, &L.q));
+    }
+    if (flags & SPF_T_GATHER_ROWS) {
+      CL_HIP(hipMalloc((void**)&L.rows, (size_t)c->world * t->cap * t->V * sizeof(uint32_t)));
+    }
+    if (flags & SPF_T_GATHER_NEXTHOPS) {
+      CL_HIP(hipMalloc((void**)&L.masks, (size_t)c->world * t->mask_cap * sizeof(uint64_t)));
+    }
+    CL_HIP(hipEventCreate(&L.e0));
+    CL_HIP(hipEventCreate(&L.e1));
+    CL_HIP(hipEventCreate(&L.e2));
+  }
+  *out = t.release();
+  return SPF_OK;
+}
+
+int spf_table_run(spf_table* t) {
+  SPF_ABI_RANGE_CLUSTER("spf_table_run");
+  if (!t) {
+    return cfail(SPF_E_INVALID, "spf_table_run: null table");
+  }
+  spf_cluster* c = t->c;
+  // 1. every local block: one batch on its device, then its rows / masks
+  //    into its own slot of the gathered buffers (device to device)
+  for (auto& L : t->local) {
+    CL_HIP(hipSetDevice(L.device));
+    hipStream_t st = (hipStream_t)spf_graph_get_stream(L.g);
+    CL_HIP(hipEventRecord(L.e0, st));
+    const uint64_t first = t->block_first[L.rank], count = t->block_first[L.rank + 1] - first;
+    if (L.q) {
+      CL_TRY(spf_query_run(L.q));
+      if (L.rows) {
+        CL_TRY(spf_query_fetch_rows(L.q, 0, (uint32_t)count,
+                                    L.rows + (size_t)L.rank * t->cap * t->V,
+                                    (size_t)t->V * sizeof(uint32_t), 1));
+      }
+      if (L.masks) {
+        void* dr = nullptr;
+        uint32_t eb = 0;
+        void* nh = nullptr;
+        uint64_t total = 0;
+        CL_TRY(spf_query_device_rows(L.q, &dr, &eb, &nh, &total));
+        CL_HIP(hipMemcpyAsync(L.masks + (size_t)L.rank * t->mask_cap, nh,
+                              total * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+      }
+    }
+    CL_HIP(hipEventRecord(L.e1, st));
+  }
+  // 2. the exchange: in-place all-gathers into equal-sized rank slots
+  if (t->flags & (SPF_T_GATHER_ROWS | SPF_T_GATHER_NEXTHOPS)) {
+    CL_NCCL(ncclGroupStart());
+    for (size_t d = 0; d < t->local.size(); ++d) {
+      auto& L = t->local[d];
+      CL_HIP(hipSetDevice(L.device));
+      hipStream_t st = (hipStream_t)spf_graph_get_stream(L.g);
+      if (L.rows) {
+        const size_t cnt = (size_t)t->cap * t->V;
+        CL_NCCL(ncclAllGather(L.rows + (size_t)L.rank * cnt, L.rows, cnt, ncclUint32,
+                              c->comms[d], st));
+      }
+      if (L.masks) {
+        CL_NCCL(ncclAllGather(L.masks + (size_t)L.rank * t->mask_cap, L.masks, t->mask_cap,
+                              ncclUint64, c->comms[d], st));
+      }
+    }
+    CL_NCCL(ncclGroupEnd());
+  }
+  for (auto& L : t->local) {
+    CL_HIP(hipSetDevice(L.device));
+    CL_HIP(hipEventRecord(L.e2, (hipStream_t)spf_graph_get_stream(L.g)));
+  }
+  t->ran = true;
+  return SPF_OK;
+}
+
+int spf_table_sync(spf_table* t) {
+  if (!t) {
+    return cfail(SPF_E_INVALID, "spf_table_sync: null table");
+  }
+  for (auto& L : t->local) {
+    CL_HIP(hipSetDevice(L.device));
+    CL_HIP(hipEventSynchronize(L.e2));
+  }
+  return SPF_OK;
+}
+
+int spf_table_elapsed_ms(spf_table* t, float* compute_ms, float* gather_ms) {
+  if (!t || !t->ran) {
+    return cfail(SPF_E_INVALID, "spf_table_elapsed_ms: table has not run");
+  }
+  float cm = 0, gm = 0;
+  for (auto& L : t->local) {
+    CL_HIP(hipSetDevice(L.device));
+    float a = 0, b = 0;
+    CL_HIP(hipEventElapsedTime(&a, L.e0, L.e1));
+    CL_HIP(hipEventElapsedTime(&b, L.e1, L.e2));
+    cm = std::max(cm, a);
+    gm = std::max(gm, b);
+  }
+  if (compute_ms) {
+    *compute_ms = cm;
+  }
+  if (gather_ms) {
+    *gather_ms = gm;
+  }
+  return SPF_OK;
+}
+
+int spf_table_block(const spf_table* t, uint32_t rank, uint32_t* first, uint32_t* count) {
+  if (!t || rank >= t->c->world) {
+    return cfail(SPF_E_INVALID, "spf_table_block: bad rank");
+  }
+  if (first) {
+    *first = (uint32_t)t->block_first[rank];
+  }
+  if (count) {
+    *count = (uint32_t)(t->block_first[rank + 1] - t->block_first[rank]);
+  }
+  return SPF_OK;
+}
+
+int spf_table_nh_words(const spf_table* t, uint32_t i) {
+  if (!t || i >= t->n) {
+    return cfail(SPF_E_INVALID, "spf_table_nh_words: bad index");
+  }
+  return (int)t->words[i];
+}
+
+// rank owning source index i
+static uint32_t owner_of(const spf_table* t, uint32_t i) {
+  const auto it = std::upper_bound(t->block_first.begin(), t->block_first.end(), (uint64_t)i);
+  return (uint32_t)(it - t->block_first.begin()) - 1;
+}
+
+int spf_table_fetch_rows(spf_table* t, uint32_t first, uint32_t count, uint32_t* dst) {
+  SPF_ABI_RANGE_CLUSTER("spf_table_fetch_rows");
+  if (!t || !dst || first + (uint64_t)count > t->n) {
+    return cfail(SPF_E_INVALID, "spf_table_fetch_rows: bad range");
+  }
+  uint32_t i = first;
+  while (i < first + count) {
+    const uint32_t r = owner_of(t, i);
+    const uint32_t bend = (uint32_t)std::min<uint64_t>(t->block_first[r + 1], first + count);
+    // the owner's device, or any local device holding the gathered rows
+    const spf_table::Local* src = nullptr;
+    for (const auto& L : t->local) {
+      if (L.rank == r) {
+        src = &L;
+      }
+    }
+    if (!src || !src->q) {
+      if (!(t->flags & SPF_T_GATHER_ROWS)) {
+        return cfail(SPF_E_UNSUPPORTED, "spf_table_fetch_rows: rows of another rank (no gather)");
+      }
+      const auto& L = t->local[0];
+      CL_HIP(hipSetDevice(L.device));
+      CL_HIP(hipMemcpy(dst + (size_t)(i - first) * t->V,
+                       L.rows + ((size_t)r * t->cap + (i - t->block_first[r])) * t->V,
+                       (size_t)(bend - i) * t->V * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    } else {
+      CL_TRY(spf_query_fetch_rows(src->q, (uint32_t)(i - t->block_first[r]), bend - i,
+                                  dst + (size_t)(i - first) * t->V,
+                                  (size_t)t->V * sizeof(uint32_t), 0));
+    }
+    i = bend;
+  }
+  return SPF_OK;
+}
+
+int spf_table_fetch_nexthops(spf_table* t, uint32_t first, uint32_t count, uint64_t* dst) {
+  SPF_ABI_RANGE_CLUSTER("spf_table_fetch_nexthops");
+  if (!t || !dst || first + (uint64_t)count > t->n || !(t->flags & SPF_F_NEXTHOPS)) {
+    return cfail(SPF_E_INVALID, "spf_table_fetch_nexthops: bad range or no next hops");
+  }
+  uint32_t i = first;
+  uint64_t out = 0;
+  while (i < first + count) {
+    const uint32_t r = owner_of(t, i);
+    const uint32_t bend = (uint32_t)std::min<uint64_t>(t->block_first[r + 1], first + count);
+    const spf_table::Local* src = nullptr;
+    for (const auto& L : t->local) {
+      if (L.rank == r) {
+        src = &L;
+      }
+    }
+    uint64_t words = 0;
+    for (uint32_t k = i; k < bend; ++k) {
+      words += (uint64_t)t->V * t->words[k];
+    }
+    if (src && src->q) {
+      CL_TRY(spf_query_fetch_nexthops(src->q, (uint32_t)(i - t->block_first[r]), bend - i, dst + out));
+    } else {
+      if (!(t->flags & SPF_T_GATHER_NEXTHOPS)) {
+        return cfail(SPF_E_UNSUPPORTED, "spf_table_fetch_nexthops: masks of another rank (no gather)");
+      }
+      const auto& L = t->local[0];
+      CL_HIP(hipSetDevice(L.device));
+      uint64_t o = out;
+      for (uint32_t k = i; k < bend; ++k) {
+        const size_t w = (size_t)t->V * t->words[k];
+        CL_HIP(hipMemcpy(dst + o, L.masks + t->mask_off[k], w * sizeof(uint64_t),
+                         hipMemcpyDeviceToHost));
+        o += w;
+      }
+    }
+    out += words;
+    i = bend;
+  }
+  return SPF_OK;
+}
+
+int spf_table_device_buffers(
+    spf_table* t, uint32_t local, void** rows, void** masks, uint64_t* mask_cap_words) {
+  if (!t || local >= t->local.size()) {
+    return cfail(SPF_E_INVALID, "spf_table_device_buffers: bad local index");
+  }
+  if (rows) {
+    *rows = t->local[local].rows;
+  }
+  if (masks) {
+    *masks = t->local[local].masks;
+  }
+  if (mask_cap_words) {
+    *mask_cap_words = t->mask_cap;
+  }
+  return SPF_OK;
+}
+
+int spf_table_kernel_name(spf_table* t, uint32_t local, const char** name) {
+  if (!t || local >= t->local.size() || !name) {
+    return cfail(SPF_E_INVALID, "spf_table_kernel_name: bad local index");
+  }
+  *name = t->local[local].q ? spf_query_kernel_name(t->local[local].q) : "";
+  return SPF_OK;
+}
+
+} // extern "C"

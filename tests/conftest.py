@@ -3,6 +3,12 @@ import sys
 
 import pytest
 
+# PyTorch ships its own libamdhip64 under the SONAME /opt/rocm's has: import
+# it before anything loads the engine library (tests that only touch the
+# host-side ABI, e.g. spf_table_layout, load it too), so the engine binds to
+# torch's already-loaded HIP runtime (see gpu_ready).
+import torch  # noqa: F401,E402
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

@@ -65,6 +65,8 @@ def parse():
     p.add_argument("--no-repair", action="store_true", help="skip the WAN table-repair events")
     p.add_argument("--wan-nodes", type=int, default=100000)
     p.add_argument("--wan-links", type=int, default=1000000)
+    p.add_argument("--sharded", action="store_true",
+                   help="use the multi-GPU spf_table path even at N = 1 (tests it on one GPU)")
     return p.parse_args()
 
 
@@ -522,10 +524,10 @@ def ksp2_cpu_sample(topo, sample=12):
 
 def whatif_batch(world, rank, local, dist, steps=3):
     """BASELINE configs[4]: 8,192 single-link-failure SPFs (runSpf with
-    linksToIgnore = {link}, LinkState.cpp:806-880) from one border node in
-    two areas: area A = the 10k fabric (from "2-0-0"), area B = the 10k-node
-    / 100k-link WAN (from "n0"), 4,096 sampled links each (seed 7), with ECMP
-    next-hop masks.  The 8,192 queries are split in contiguous blocks over
+    linksToIgnore = {link}, LinkState.cpp:806-880) from the border node
+    "2-0-0" of two areas: area A = the 10k fabric, area B = the 10k-node /
+    100k-link WAN, 4,096 sampled links each (seed 7), with ECMP next-hop
+    masks.  The 8,192 queries are split in contiguous blocks over
     the ranks (strong scaling, no collective)."""
     import numpy as np
     import torch
@@ -534,16 +536,14 @@ def whatif_batch(world, rank, local, dist, steps=3):
     from openr_amd import allsources as AS
     from openr_amd import topologies as TP
 
-    fab = TP.fabric(10000)
-    wan = TP.wan(10000, 100000)
+    # the two areas share the border node 2-0-0 (TP.whatif_two_area, the
+    # setup of tests/golden/whatif_two_area.*)
     areas = []
-    rng = np.random.default_rng(7)
-    for topo, me in ((fab, "2-0-0"), (wan, "n0")):
+    for _, topo, links in TP.whatif_two_area():
         csr = topo.csr()
         r, _ = topo.rank()
-        src = int(r[topo.names.index(me)])
-        links = rng.choice(csr.num_links, 4096, replace=False).astype(np.uint32)
-        areas.append((csr, src, links))
+        src = int(r[topo.names.index(TP.WHATIF_BORDER)])
+        areas.append((csr, src, links.astype(np.uint32)))
     allq = [(a, int(l)) for a, (_, _, links) in enumerate(areas) for l in links]
     first, count = AS.shard(len(allq), world, rank)
     mine = allq[first:first + count]
@@ -604,8 +604,8 @@ def whatif_batch(world, rank, local, dist, steps=3):
     for _, g, _ in graphs:
         g.close()
     return {
-        "config": "BASELINE configs[4]: 8,192 single-link-failure SPFs with ECMP next hops, "
-                  "area A = fabric (9,976 nodes) from 2-0-0, area B = WAN-10k from n0, 4,096 links each",
+        "config": "BASELINE configs[4]: 8,192 single-link-failure SPFs with ECMP next hops from the "
+                  "border node 2-0-0 of two areas: A = fabric (9,976 nodes), B = WAN-10k, 4,096 links each",
         "queries": len(allq), "n_gpus": world, "scaling": "strong", "kernels": kernels,
         "ms": round(ms, 3), "device_ms": round(dev_ms, 3),
         "value": round(len(allq) / (ms / 1e3), 1), "unit": "SPF/s",
@@ -669,6 +669,96 @@ def route_db_rebuild_cpu(topo, iters=2):
     out = _rebuild_loop(O, topo, iters, timed)
     out["cores"] = 1
     out["kind"] = "port"
+    return out
+
+
+def wan_all_sources_table(args, world, rank, local, dist, cluster):
+    """BASELINE configs[2] at N > 1 (or --sharded): the 100k-source WAN table
+    as ONE engine call -- spf_table over the RCCL cluster: contiguous source
+    blocks per GPU (push-only delta-stepping), then the uint32 rows
+    all-gathered in place over xGMI inside spf_table_run, so every GPU holds
+    the whole 40 GB table.  `ms` = the slowest rank's wall time of the call
+    (compute + exchange); parity: the reference's checksum of row n0 and two
+    rows (the last one from the last rank's block, read from the gathered
+    copy) against scipy."""
+    import numpy as np
+    import torch
+
+    from openr_amd import abi
+    from openr_amd import topologies as TP
+
+    t0 = time.perf_counter()
+    topo = TP.wan(args.wan_nodes, args.wan_links)
+    csr = topo.csr()
+    gen_s = time.perf_counter() - t0
+    V, E = csr.num_nodes, len(csr.col)
+    g = abi.Graph(csr, device=local)
+    g.query(np.arange(min(256, V), dtype=np.uint32), 0).run().close()
+    g.close()
+    flags = abi.SPF_T_GATHER_ROWS if world > 1 else 0
+    tab = abi.Table(cluster, csr, np.arange(V, dtype=np.uint32), flags)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    tab.run()
+    if dist:
+        dist.barrier()
+    wall_ms = (time.perf_counter() - t1) * 1e3
+    comp_ms, gather_ms = tab.elapsed_ms()
+    red = torch.tensor([wall_ms, comp_ms, gather_ms], dtype=torch.float64, device=f"cuda:{local}")
+    if dist:
+        dist.all_reduce(red, op=dist.ReduceOp.MAX)
+    wall_ms, comp_ms, gather_ms = (float(x) for x in red)
+    check = None
+    if rank == 0:
+        import scipy.sparse as sp
+        import scipy.sparse.csgraph as cg
+
+        anchors = json.load(open(os.path.join(ROOT, "tests", "golden", "wan_anchors.json")))["anchors"]
+        want = [a["sum_dist"] for a in anchors if a["V"] == V and a["L"] == args.wan_links and a["S"] == 1]
+        bad = 0
+        row0 = tab.fetch_rows(0, 1)[0]
+        if want and int(row0.astype(np.int64).sum()) != want[0]:
+            bad += 1
+        A = sp.csr_matrix((csr.metric.astype(np.float64), csr.col, csr.row_ptr), shape=(V, V))
+        probe = [0, V - 1]
+        D = cg.dijkstra(A, indices=probe)
+        for k, i in enumerate(probe):
+            ref = np.where(np.isfinite(D[k]), D[k], 0xFFFFFFFF).astype(np.int64)
+            bad += int((tab.fetch_rows(i, 1)[0].astype(np.int64) != ref).sum())
+        check = "ok" if bad == 0 else f"{bad} mismatches"
+    kernel = tab.kernel(0)
+    tab.close()
+    per_sssp = 8 * E + 4 * (V + 1) + 4 * V
+    out = {
+        "config": "BASELINE configs[2]: 100k-node / 1M-link WAN (SURVEY §8(d) row 3), all sources, "
+                  f"one engine call over {world} GPU(s): contiguous source blocks + in-engine RCCL "
+                  "all-gather of the uint32 rows",
+        "nodes": V, "links": int(csr.num_links), "directed_edges": E, "sources": V,
+        "n_gpus": world, "kernel": kernel, "scaling": "strong",
+        "ms": round(wall_ms, 2), "device_compute_ms": round(comp_ms, 2),
+        "gather_ms": round(gather_ms, 2),
+        "value": round(V / (wall_ms / 1e3), 1), "unit": "SPF/s",
+        "value_no_gather": round(V / ((wall_ms - gather_ms) / 1e3), 1),
+        "gteps": round(V * E / (wall_ms / 1e3) / 1e9, 2),
+        "table_bytes": V * V * 4,
+        "gather_algbw_gbs": round(V * V * 4 / (gather_ms / 1e3) / 1e9, 1) if world > 1 and gather_ms else None,
+        "roofline": {"bound": "hbm", "kernel": "spf_dstep_kernel (push-only, LDS buckets)",
+                     "algorithmic_bytes_per_sssp": per_sssp,
+                     "algorithmic_achieved": round(V * per_sssp / (comp_ms / 1e3) / 1e9 / world, 1),
+                     "algorithmic_frac": round(V * per_sssp / (comp_ms / 1e3) / 1e9 / world / HBM_PEAK_GBS, 4),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "note": "per GPU"},
+        "parity_check": check,
+        "generate_s": round(gen_s, 1),
+    }
+    if not args.no_repair:
+        from openr_amd import allsources as AS
+
+        sas = AS.ShardedAllSources(csr, device=local, gather=world > 1)
+        sas.run()
+        out["table_repair"] = wan_table_repair(topo, csr, sas, world, rank, local, dist)
+        sas.close()
     return out
 
 
@@ -873,26 +963,142 @@ def wan_table_repair(topo, csr, sas, world, rank, local, dist):
             "events": events, "parity_check": check}
 
 
-def main():
-    args = parse()
+def cluster_for(world, rank, local, dist):
+    """The engine's RCCL communicator for this rank (include/openr_spf.h
+    spf_cluster_create_rank): rank 0 makes the id, torch.distributed hands
+    it to the other ranks (plumbing only; the exchange itself runs inside
+    the engine's spf_table_run)."""
+    import torch
+
+    from openr_amd import abi
+
+    if world == 1:
+        return abi.Cluster(world=1, rank=0, uid=abi.cluster_unique_id(), device=local)
+    t = torch.zeros(abi.SPF_CLUSTER_ID_BYTES, dtype=torch.uint8, device=f"cuda:{local}")
+    if rank == 0:
+        t.copy_(torch.frombuffer(bytearray(abi.cluster_unique_id()), dtype=torch.uint8))
+    dist.broadcast(t, 0)
+    uid = bytes(t.cpu().numpy().tobytes())
+    return abi.Cluster(world=world, rank=rank, uid=uid, device=local)
+
+
+def _timed_table(t, steps, warmup, dist):
+    import torch
+
+    for _ in range(warmup):
+        t.run()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        t.run(sync=False)
+    t.sync()
+    if dist:
+        dist.barrier()
+    return (time.perf_counter() - t0) * 1000.0 / steps, t.elapsed_ms()
+
+
+def fabric_sharded(args, topo, world, rank, local, dist, cluster):
+    """N > 1 headline: STRONG scaling of the one 9,976-source fabric table.
+    The engine splits the sources into contiguous blocks, one per GPU
+    (spf_table over a one-process-per-GPU RCCL cluster); each block's rows and
+    next-hop masks stay resident on the GPU that computed them (a RouteDb
+    reads only its own row).  `value` = 9,976 SPFs / the slowest rank's step.
+    The same table with the distance rows all-gathered over xGMI inside the
+    engine (ncclAllGather in spf_table_run) is timed beside it."""
     import numpy as np
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    else:
-        torch.cuda.set_device(0)
     from openr_amd import abi
-    from openr_amd import topologies as TP
 
-    topo = TP.fabric(args.num_sws)
+    csr = topo.csr()
+    V, E = csr.num_nodes, len(csr.col)
+    sources = np.arange(V, dtype=np.uint32)
+    t = abi.Table(cluster, csr, sources, abi.SPF_F_NEXTHOPS)
+    step_ms, (comp_ms, _) = _timed_table(t, args.steps, args.warmup, dist)
+    tg = abi.Table(cluster, csr, sources, abi.SPF_F_NEXTHOPS | abi.SPF_T_GATHER_ROWS)
+    gstep_ms, (gcomp_ms, gather_ms) = _timed_table(tg, max(3, args.steps // 2), 1, dist)
+    red = torch.tensor([step_ms, comp_ms, gstep_ms, gather_ms], dtype=torch.float64,
+                       device=f"cuda:{local}")
+    if dist:
+        dist.all_reduce(red, op=dist.ReduceOp.MAX)
+    step_ms, comp_ms, gstep_ms, gather_ms = (float(x) for x in red)
+    first, count = t.block(cluster.first_rank)
+    # parity (rank 0): rows + next hops of its own block, and rows of the LAST
+    # rank's block read from the gathered copy, against the DijkstraQ replay
+    check = None
+    if rank == 0:
+        from oracle import spf_py
+
+        bad = 0
+        picks = [first, first + count // 2, first + count - 1]
+        rows = {i: t.fetch_rows(i, 1)[0] for i in picks}
+        lf, lc = tg.block(world - 1)
+        for i in (lf, lf + lc - 1):
+            rows[i] = tg.fetch_rows(i, 1)[0]
+        g = abi.Graph(csr, device=local)
+        for i, d in rows.items():
+            ref = spf_py.run_spf(csr, int(sources[i]), True)
+            for v in range(V):
+                want = ref[v][0] if v in ref else 0xFFFFFFFF
+                bad += int(d[v]) != want
+            if first <= i < first + count:
+                m = t.fetch_nexthops(i, 1).reshape(V, t.nh_words(i))
+                nb = g.nbrs(int(sources[i]))
+                for v in ref:
+                    if v == sources[i]:
+                        continue
+                    got = {int(nb[w * 64 + b]) for w in range(m.shape[1]) for b in range(64)
+                           if (int(m[v, w]) >> b) & 1}
+                    bad += got != set(ref[v][1])
+        g.close()
+        check = "ok" if bad == 0 else f"{bad} mismatches"
+    kernel = t.kernel(0)
+    t.close()
+    tg.close()
+    return {
+        "metric": "all-sources SPF/sec + GTEPS on 10k-node fabric; full RouteDb rebuild ms",
+        "value": round(V / (step_ms / 1000.0), 1),
+        "unit": "SPF/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(step_ms, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic fabric (DecisionBenchmark createFabric, SSW bug fixed), metric 1",
+        "config": {
+            "workload": "fabric_full all-sources SPF + ECMP next-hop sets (BASELINE configs[1]), "
+                        "one table sharded over the GPUs",
+            "nodes": V, "links": int(csr.num_links), "directed_edges": E,
+            "sources_total": V, "kernel": kernel,
+            "parallelism": f"contiguous source blocks over {world} GPUs inside the engine "
+                           "(spf_table, RCCL cluster); rows stay on their owner GPU",
+        },
+        "gteps": round(V * E / (step_ms / 1000.0) / 1e9, 2),
+        "device_compute_ms": round(comp_ms, 4),
+        "with_row_gather": {
+            "what": "the same table with every GPU's uint32 distance rows all-gathered over xGMI "
+                    "(in-place ncclAllGather inside spf_table_run)",
+            "ms_per_step": round(gstep_ms, 4), "gather_ms": round(gather_ms, 4),
+            "value": round(V / (gstep_ms / 1000.0), 1),
+            "gathered_bytes": int(V * V * 4),
+        },
+        "parity_spot_check": check,
+    }
+
+
+def fabric_single(args, topo, world, rank, local, dist):
+    """N = 1 headline: the fabric all-sources step as one query on one GPU,
+    with the per-kernel split and roofline."""
+    import numpy as np
+    import torch
+
+    from openr_amd import abi
+
     # drain scenario of this rank (weak scaling: one all-sources table each)
     rsw = [i for i, n in enumerate(topo.names) if n.startswith("3-")]
     drained = [] if rank == 0 else [rsw[(rank * 1009) % len(rsw)]]
@@ -1025,9 +1231,41 @@ def main():
     }
     q.close()
     g.close()
+    return out
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    from openr_amd import abi
+    from openr_amd import topologies as TP
+
+    topo = TP.fabric(args.num_sws)
+    if world > 1 or args.sharded:
+        cluster = cluster_for(world, rank, local, dist)
+        out = fabric_sharded(args, topo, world, rank, local, dist, cluster)
+    else:
+        cluster = None
+        out = fabric_single(args, topo, world, rank, local, dist)
     if not args.no_wan:
         try:
-            out["wan_all_sources"] = wan_all_sources(args, world, rank, local, dist)
+            if cluster is not None:
+                out["wan_all_sources"] = wan_all_sources_table(args, world, rank, local, dist, cluster)
+            else:
+                out["wan_all_sources"] = wan_all_sources(args, world, rank, local, dist)
         except Exception as e:  # reported, never silently replaced
             out["wan_all_sources"] = {"error": repr(e)}
     if not args.no_whatif:

@@ -460,7 +460,13 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
 // the result is the order-free restatement of runSpf.
 struct DstepArgs {
   SsspArgs s;
-  uint32_t shift; // bucket width 2^shift
+  uint32_t shift = 5; // processing bucket width 2^shift
+  uint32_t fshift = 0; // LDS bucket bytes quantise d >> fshift (fshift <= shift)
+  uint32_t noret = 0;  // bit 0: atomicMin without return, bit 1: coherent gathers
+  // OPENR_SPF_DSTEP_STATS: per-launch event counts of the push-only pass
+  // (expansions, edges, bucket-filtered, gathers, atomics, improvements,
+  // relax rounds, refreshed nodes)
+  unsigned long long* stats = nullptr;
   // SEED (spf_table_repair): query q repairs table row row_idx[q] in place:
   // nodes whose every shortest path used a removed edge are reset first,
   // then relaxation runs from the seed nodes with the row's values
@@ -475,7 +481,12 @@ struct DstepArgs {
   const uint32_t* rm_scope = nullptr;
   uint32_t nrem = 0;
   uint32_t* gscratch2 = nullptr; // per-workgroup second node queue (V u32)
+  // packed out-edges (head | metric << cwbits), 0 bits = unpacked
+  const uint32_t* cw = nullptr;
+  uint32_t cwbits = 0;
+  uint32_t cwvec = 0; // read cw as 16-byte chunks (padded to 4 edges)
 };
+
 
 // Load that bypasses the (non-coherent) vector L1: values other lanes change
 // with atomics in L2 during the same phase.
@@ -707,15 +718,24 @@ __device__ void repair_invalidate(
 // LBK: bucket bytes in LDS (V B: one workgroup per CU on the 100k WAN);
 // otherwise buckets are read from the distance row and the LDS image is the
 // two bitmaps only, so several workgroups (sources) share a CU.
-template <int WMAX, bool IGN, uint32_t BS, bool LBK, bool SEED = false>
+// PK: the tuned push-only pass compiled in (packed 16-byte edge chunks,
+// coherent gathers, non-returning atomics; dstep_tune), else runtime modes.
+template <int WMAX, bool IGN, uint32_t BS, bool LBK, bool SEED = false, bool PK = false>
 __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
   static_assert(!SEED || (WMAX == 0 && !IGN && LBK), "seeded runs are distance-only");
+  static_assert(!PK || (WMAX == 0 && LBK), "the packed pass is push-only with LDS buckets");
   extern __shared__ __align__(16) uint32_t smem[];
   const SsspArgs& a = da.s;
-  const uint32_t V = a.V, nbw = a.nbw, G = a.G, shift = da.shift;
+  const uint32_t V = a.V, nbw = a.nbw, G = a.G;
+  // LBK: bytes are d >> fshift and a phase takes 2^kg byte values at once;
+  // buckets derived from the row use d >> shift directly
+  const uint32_t shift = LBK ? da.fshift : da.shift;
+  const uint32_t kg = LBK ? da.shift - da.fshift : 0;
   const uint32_t tid = threadIdx.x;
   const uint32_t lg = tid & (G - 1);
   const uint32_t grp = tid / G, ngrp = BS / G;
+  uint32_t st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bool stats = da.stats != nullptr;
 
   uint32_t* act = smem;        // marked heads (PULL)
   uint32_t* pend = act + nbw;  // improved, not yet pushed
@@ -823,7 +843,7 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
         if (m >= 255) {
           break;
         }
-        cur = m;
+        cur = min(((m >> kg) << kg) + (1u << kg) - 1u, 254u);
         continue;
       }
       if constexpr (WMAX == 0) {
@@ -834,61 +854,166 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
         // coherent read of its final distance after the phase; otherwise
         // its pending bit is set and the bucket is derived from the row).
         // du is re-read coherently: a drop of dist[u] that landed before u
-        // was claimed has already cleared its pending bit.
+        // was claimed has already cleared its pending bit.  The header of a
+        // group's next node (row range, du) and the id of the one after are
+        // loaded while the current node's edges are in flight; a du read
+        // early can only miss drops that mark u again (every improvement
+        // marks its node), so it stays exact.
+        uint32_t nu = grp < qlen ? queue[grp] : kInf32;
+        uint32_t nbeg = 0, nend = 0, ndu = kInf32;
+        if (nu != kInf32) {
+          nbeg = a.row[nu];
+          nend = a.row[nu + 1];
+          ndu = ld_coh(dist + nu);
+        }
+        uint32_t nnu = grp + ngrp < qlen ? queue[grp + ngrp] : kInf32;
         for (uint32_t i = grp; i < qlen; i += ngrp) {
-          const uint32_t u = queue[i];
+          const uint32_t u = nu, du = ndu, beg = nbeg, end = nend;
+          nu = nnu;
+          if (nu != kInf32) {
+            nbeg = a.row[nu];
+            nend = a.row[nu + 1];
+            ndu = ld_coh(dist + nu);
+          }
+          nnu = i + 2 * ngrp < qlen ? queue[i + 2 * ngrp] : kInf32;
           if (u != src && !((a.trbits[u >> 5] >> (u & 31)) & 1u)) {
             continue; // overloaded: recorded but never transited
           }
-          const uint32_t du = ld_coh(dist + u);
           if (SEED && du == kInf32) {
             continue;
           }
-          const uint32_t beg = a.row[u], end = a.row[u + 1];
-          // kPushUnroll edges per lane per step: their (col, metric) loads,
+          if (stats && lg == 0) {
+            st[0] += 1;
+            st[1] += end - beg;
+          }
+          // kPushUnroll edges per lane per step: their (head, metric) loads,
           // then their distance gathers, are independent and issued together
           constexpr uint32_t kPushUnroll = 4;
-          for (uint32_t e0 = beg + lg; e0 < end; e0 += kPushUnroll * G) {
-            uint32_t v[kPushUnroll], c[kPushUnroll], dv[kPushUnroll];
+          auto relax = [&](auto& v, const auto& c) {
+            constexpr uint32_t N = sizeof(v) / sizeof(v[0]);
+            uint32_t dv[N];
 #pragma unroll
-            for (uint32_t j = 0; j < kPushUnroll; ++j) {
-              const uint32_t e = e0 + j * G;
-              bool ok = e < end;
-              if constexpr (IGN) {
-                ok = ok && !(nign && in_sorted(ignp, nign, a.link[e]));
-              }
-              v[j] = ok ? a.col[e] : kInf32;
-              c[j] = ok ? du + a.wout[e] : kInf32;
+            for (uint32_t j = 0; j < N; ++j) {
               if constexpr (LBK) {
                 // bucket bytes only ever run ahead of (>=) a node's true
                 // bucket, so bkt[v] < bucket(c) proves dist[v] < c: no
                 // improvement, and no HBM read of dist[v]
                 if (v[j] != kInf32 && bkt[v[j]] < min(c[j] >> shift, 254u)) {
                   v[j] = kInf32;
+                  st[2] += stats;
                 }
               }
             }
 #pragma unroll
-            for (uint32_t j = 0; j < kPushUnroll; ++j) {
-              dv[j] = v[j] != kInf32 ? dist[v[j]] : 0u;
+            for (uint32_t j = 0; j < N; ++j) {
+              dv[j] = v[j] == kInf32 ? 0u
+                      : ((PK || (LBK && (da.noret & 2u))) ? ld_coh(dist + v[j]) : dist[v[j]]);
             }
 #pragma unroll
-            for (uint32_t j = 0; j < kPushUnroll; ++j) {
-              if (v[j] != kInf32 && c[j] < dv[j] && atomicMin(&dist[v[j]], c[j]) > c[j]) {
+            for (uint32_t j = 0; j < N; ++j) {
+              st[3] += stats && v[j] != kInf32;
+              if (v[j] == kInf32 || c[j] >= dv[j]) {
+                continue;
+              }
+              st[4] += stats;
+              if (PK || (LBK && (da.noret & 1u))) {
+                // fire-and-forget: the wave does not wait for the old value;
+                // a mark lost to a racing lower write only re-expands v once
+                // with its current distance (the refresh below reads it)
+                atomicMin(&dist[v[j]], c[j]);
+                atomicOr(&act[v[j] >> 5], 1u << (v[j] & 31));
+              } else if (atomicMin(&dist[v[j]], c[j]) > c[j]) {
+                st[5] += stats;
                 atomicOr(LBK ? &act[v[j] >> 5] : &pend[v[j] >> 5], 1u << (v[j] & 31));
               }
+            }
+          };
+          if (PK || da.cwvec) {
+            // packed edges four at a time: lane lg takes the aligned 16-byte
+            // chunks lg, lg + G, ... of [beg, end) (one load per 4 edges)
+            // (PK: two chunks per lane per step, 8 edges in flight)
+            const uint32_t mask = (1u << da.cwbits) - 1u;
+            constexpr uint32_t kCh = PK ? 2 : 1;
+            for (uint32_t k = (beg >> 2) + lg; 4 * k < end; k += kCh * G) {
+              uint32_t v[4 * kCh], c[4 * kCh];
+#pragma unroll
+              for (uint32_t h = 0; h < kCh; ++h) {
+                const uint32_t kk = k + h * G;
+                const uint4 x = 4 * kk < end ? reinterpret_cast<const uint4*>(da.cw)[kk]
+                                             : make_uint4(0, 0, 0, 0);
+                const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                  const uint32_t e = 4 * kk + j;
+                  bool ok = e >= beg && e < end;
+                  if constexpr (IGN) {
+                    ok = ok && !(nign && in_sorted(ignp, nign, a.link[e]));
+                  }
+                  v[4 * h + j] = ok ? (xs[j] & mask) : kInf32;
+                  c[4 * h + j] = ok ? du + (xs[j] >> da.cwbits) : kInf32;
+                }
+              }
+              relax(v, c);
+            }
+          } else {
+            for (uint32_t e0 = beg + lg; e0 < end; e0 += kPushUnroll * G) {
+              uint32_t v[kPushUnroll], c[kPushUnroll];
+#pragma unroll
+              for (uint32_t j = 0; j < kPushUnroll; ++j) {
+                const uint32_t e = e0 + j * G;
+                bool ok = e < end;
+                if constexpr (IGN) {
+                  ok = ok && !(nign && in_sorted(ignp, nign, a.link[e]));
+                }
+                if (da.cwbits) {
+                  const uint32_t x = ok ? da.cw[e] : 0u;
+                  v[j] = ok ? (x & ((1u << da.cwbits) - 1u)) : kInf32;
+                  c[j] = ok ? du + (x >> da.cwbits) : kInf32;
+                } else {
+                  v[j] = ok ? a.col[e] : kInf32;
+                  c[j] = ok ? du + a.wout[e] : kInf32;
+                }
+              }
+              relax(v, c);
             }
           }
         }
         __syncthreads();
         if constexpr (LBK) {
-          const uint32_t nimp = compact_bits<uint32_t, BS>(act, nbw, queue, ctl + 1);
-          __syncthreads(); // queue entries come from every wave
-          for (uint32_t i = tid; i < nimp; i += BS) {
-            const uint32_t v = queue[i];
-            bkt[v] = (uint8_t)min(ld_coh(dist + v) >> shift, 254u);
-            atomicOr(&pend[v >> 5], 1u << (v & 31));
+          // refresh straight from the marked words: each thread owns words
+          // tid, tid + BS, ... (sole writer of those pend words in this
+          // phase); four coherent distance reads in flight per step
+          for (uint32_t w = tid; w < nbw; w += BS) {
+            uint32_t b = act[w];
+            if (!b) {
+              continue;
+            }
+            act[w] = 0;
+            pend[w] |= b;
+            st[7] += stats ? __popc(b) : 0u;
+            while (b) {
+              uint32_t vs[4], dd[4];
+#pragma unroll
+              for (uint32_t j = 0; j < 4; ++j) {
+                vs[j] = kInf32;
+                if (b) {
+                  vs[j] = w * 32 + (__ffs(b) - 1);
+                  b &= b - 1;
+                }
+              }
+#pragma unroll
+              for (uint32_t j = 0; j < 4; ++j) {
+                dd[j] = vs[j] != kInf32 ? ld_coh(dist + vs[j]) : 0u;
+              }
+#pragma unroll
+              for (uint32_t j = 0; j < 4; ++j) {
+                if (vs[j] != kInf32) {
+                  bkt[vs[j]] = (uint8_t)min(dd[j] >> shift, 254u);
+                }
+              }
+            }
           }
+          st[6] += stats && tid == 0;
           __syncthreads();
         }
         continue;
@@ -1025,6 +1150,14 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
       __syncthreads();
     }
     __syncthreads();
+  }
+  if (stats) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (st[k]) {
+        atomicAdd(&da.stats[k], (unsigned long long)st[k]);
+      }
+    }
   }
 }
 
@@ -2525,6 +2658,11 @@ struct spf_graph {
            *d_nbrs = nullptr, *d_nbr_w = nullptr;
   uint64_t* d_w64 = nullptr;
   uint32_t* d_link_half = nullptr; // [2L] half-edges of each link (what-if screen)
+  // out-edges packed as head | metric << cw_bits (one u32 per edge) when
+  // both fit; cw_bits = 0: not packed
+  uint32_t* d_cw = nullptr;
+  uint32_t cw_bits = 0;
+  uint64_t ecc_est = 0; // graph_ecc cache (0 = not computed)
 };
 
 // How a batch is computed.
@@ -2541,6 +2679,9 @@ struct spf_query {
   uint32_t dstep_shift = 5; // delta-stepping bucket width 2^shift
   bool dstep_lbk = false;    // bucket bytes in LDS (else from the dist row)
   uint32_t dstep_bs = 1024;  // delta-stepping workgroup size
+  uint32_t dstep_fshift = 5; // bucket-byte resolution (dstep_tune)
+  uint32_t dstep_noret = 0;  // relaxation mode bits (dstep_tune)
+  uint32_t dstep_pack = 0;   // packed out-edges: 0 off, 1 scalar, 2 vector
   uint32_t ign_cap = 0, grid = 0, Vp = 0, Vp8 = 0;
   uint8_t* d_lvl = nullptr;
   uint32_t* d_flags = nullptr;
@@ -2598,7 +2739,7 @@ void free_graph(spf_graph* g) {
        {(void*)g->d_row, (void*)g->d_col, (void*)g->d_wout, (void*)g->d_win,
         (void*)g->d_link, (void*)g->d_rev, (void*)g->d_slot, (void*)g->d_tr,
         (void*)g->d_w64, (void*)g->d_nbr_off, (void*)g->d_nbrs,
-        (void*)g->d_nbr_w, (void*)g->d_link_half}) {
+        (void*)g->d_nbr_w, (void*)g->d_link_half, (void*)g->d_cw}) {
     if (p) {
       (void)hipFree(p);
     }
@@ -2718,6 +2859,33 @@ int upload_weights(spf_graph* g) {
     HIP_TRY(hipMemcpy(g->d_w64, g->w64.data(), E * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(g->d_nbr_w, g->nbr_w.data(), g->nbr_w.size() * 4,
                       hipMemcpyHostToDevice));
+  }
+  g->ecc_est = 0;
+  // packed out-edges for the push-only delta-stepping pass
+  uint32_t bits = 1;
+  while (bits < 32 && (1ull << bits) < V) {
+    ++bits;
+  }
+  const bool pack = E && bits < 32 && maxw < (1ull << (32 - bits));
+  if (g->d_cw && !pack) {
+    (void)hipFree(g->d_cw);
+    g->d_cw = nullptr;
+  }
+  g->cw_bits = 0;
+  if (pack) {
+    std::vector<uint32_t> cw(E);
+    blocks([&](uint32_t u, unsigned) {
+      for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
+        cw[e] = g->col[e] | (wout[e] << bits);
+      }
+    });
+    // padded to whole 16-byte chunks (the vector reads of the last one)
+    cw.resize(((size_t)E + 3) & ~(size_t)3, 0u);
+    if (!g->d_cw) {
+      HIP_TRY(hipMalloc((void**)&g->d_cw, cw.size() * 4));
+    }
+    HIP_TRY(hipMemcpy(g->d_cw, cw.data(), cw.size() * 4, hipMemcpyHostToDevice));
+    g->cw_bits = bits;
   }
   return SPF_OK;
 }
@@ -2839,6 +3007,80 @@ uint32_t dstep_bucket_shift(const spf_graph* g, bool want_nh) {
     shift = (uint32_t)std::min(24, std::max(0, atoi(env)));
   }
   return shift;
+}
+
+// Largest distance from one node (host Dijkstra over the 64-bit metrics),
+// cached per graph: sizes the bucket-byte resolution of the push-only
+// delta-stepping pass (upload_weights resets it).
+uint64_t graph_ecc(spf_graph* g) {
+  if (g->ecc_est || !g->V) {
+    return g->ecc_est;
+  }
+  std::vector<uint64_t> dist(g->V, UINT64_MAX);
+  using HE = std::pair<uint64_t, uint32_t>;
+  std::priority_queue<HE, std::vector<HE>, std::greater<HE>> pq;
+  dist[0] = 0;
+  pq.push({0, 0});
+  uint64_t ecc = 1;
+  while (!pq.empty()) {
+    const HE t = pq.top();
+    pq.pop();
+    if (t.first != dist[t.second]) {
+      continue;
+    }
+    ecc = std::max(ecc, t.first);
+    const uint32_t u = t.second;
+    for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
+      const uint64_t c = t.first + g->w64[e];
+      if (c < dist[g->col[e]]) {
+        dist[g->col[e]] = c;
+        pq.push({c, g->col[e]});
+      }
+    }
+  }
+  g->ecc_est = ecc;
+  return ecc;
+}
+
+// Push-only delta-stepping (distance rows, LDS bucket bytes), measured on the
+// 100k / 1M WAN (profiles/quick_wan.py; 8,361 sources, 24.0 -> 15.7 us/SPF):
+// the bucket bytes quantise d at 1/16 of the processing bucket width (a
+// sharper settled filter; twice as wide processing buckets, so fewer rounds),
+// down to the resolution that still spreads 1.25x one node's eccentricity
+// over the 254 byte values (saturation is exact, only slower); relaxations gather d[v] coherently and issue
+// non-returning atomicMin; out-edges are read as packed 16-byte chunks.
+// OPENR_SPF_DSTEP_FINE (byte bits below the bucket width), _NORET (bit 0
+// non-returning atomics, bit 1 coherent gathers) and _PACK (0 off, 1 scalar,
+// 2 vector) override.
+void dstep_tune(spf_graph* g, spf_query* q, bool push_only) {
+  q->dstep_fshift = q->dstep_shift;
+  q->dstep_noret = 0;
+  q->dstep_pack = 0;
+  if (!push_only || !q->dstep_lbk) {
+    return;
+  }
+  uint32_t fine = 4;
+  if (getenv("OPENR_SPF_DSTEP_SHIFT") == nullptr) {
+    q->dstep_shift += 1;
+  }
+  const uint64_t span = graph_ecc(g) + graph_ecc(g) / 4;
+  uint32_t fs = q->dstep_shift - std::min(fine, q->dstep_shift);
+  while (fs < q->dstep_shift && (span >> fs) > 250) {
+    ++fs;
+  }
+  if (const char* env = getenv("OPENR_SPF_DSTEP_FINE")) {
+    fine = (uint32_t)std::max(0, atoi(env));
+    fs = q->dstep_shift - std::min(fine, q->dstep_shift);
+  }
+  q->dstep_fshift = fs;
+  q->dstep_noret = 3;
+  if (const char* env = getenv("OPENR_SPF_DSTEP_NORET")) {
+    q->dstep_noret = (uint32_t)std::max(0, std::min(3, atoi(env)));
+  }
+  q->dstep_pack = g->cw_bits ? 2 : 0;
+  if (const char* env = getenv("OPENR_SPF_DSTEP_PACK")) {
+    q->dstep_pack = g->cw_bits ? (uint32_t)std::max(0, std::min(2, atoi(env))) : 0;
+  }
 }
 
 // bucket width for spf_msdstep_kernel: the eccentricity of one source (host
@@ -3310,6 +3552,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       // bucket width ~ mean metric / mean degree (delta-stepping's
       // Delta = Theta(w/d)), a power of two; OPENR_SPF_DSTEP_SHIFT overrides
       q->dstep_shift = dstep_bucket_shift(g, want_nh);
+      dstep_tune(g, q, !want_nh);
       const char* bs_env = getenv("OPENR_SPF_DSTEP_BS");
       q->dstep_bs = (bs_env && atoi(bs_env) == 512) ? 512 : 1024;
       // workgroups per CU: 2048 threads per CU, LDS permitting
@@ -3546,10 +3789,10 @@ int launch_dstep_t(spf_query* q) {
   a.ign_cap = q->ign_cap;
   a.skip = q->d_skip;
   // lanes per node: fewer than the median degree, so more nodes (and more
-  // independent HBM gathers) are in flight per CU (4 with the PULL pass of
-  // next-hop runs, 8 for the push-only distance runs: measured on the 100k
-  // WAN); OPENR_SPF_DSTEP_G overrides
-  uint32_t G = WMAX == 0 ? 8 : 4;
+  // independent HBM gathers) are in flight per CU (4: measured on the 100k
+  // WAN for the PULL pass of next-hop runs and for the push-only runs with
+  // 16-byte edge chunks); OPENR_SPF_DSTEP_G overrides
+  uint32_t G = 4;
   if (const char* env = getenv("OPENR_SPF_DSTEP_G")) {
     const int x = atoi(env);
     if (x == 1 || x == 2 || x == 4 || x == 8 || x == 16 || x == 32 || x == 64) {
@@ -3558,13 +3801,41 @@ int launch_dstep_t(spf_query* q) {
   }
   a.G = G;
   d.shift = q->dstep_shift;
+  d.fshift = q->dstep_fshift;
+  d.noret = q->dstep_noret;
+  if (WMAX == 0 && q->dstep_pack && g->cw_bits) {
+    d.cw = g->d_cw;
+    d.cwbits = g->cw_bits;
+    d.cwvec = q->dstep_pack == 2;
+  }
   auto kern = q->dstep_lbk ? spf_dstep_kernel<WMAX, IGN, BS, true>
                            : spf_dstep_kernel<WMAX, IGN, BS, false>;
+  if constexpr (WMAX == 0) {
+    if (q->dstep_lbk && d.cwvec && d.noret == 3) {
+      kern = spf_dstep_kernel<WMAX, IGN, BS, true, false, true>;
+    }
+  }
+  const size_t lds = q->lds_bytes;
   HIP_TRY(hipFuncSetAttribute(
       (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-      (int)q->lds_bytes));
-  hipLaunchKernelGGL(kern, dim3(q->grid), dim3(BS), q->lds_bytes, g->stream, d);
+      (int)lds));
+  const char* st_env = getenv("OPENR_SPF_DSTEP_STATS");
+  if (st_env && atoi(st_env) == 1) {
+    HIP_TRY(hipMalloc((void**)&d.stats, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemsetAsync(d.stats, 0, 8 * sizeof(unsigned long long), g->stream));
+  }
+  hipLaunchKernelGGL(kern, dim3(q->grid), dim3(BS), lds, g->stream, d);
   HIP_TRY(hipGetLastError());
+  if (d.stats) {
+    unsigned long long h[8];
+    HIP_TRY(hipStreamSynchronize(g->stream));
+    HIP_TRY(hipMemcpy(h, d.stats, sizeof(h), hipMemcpyDeviceToHost));
+    HIP_TRY(hipFree(d.stats));
+    fprintf(stderr,
+            "[dstep stats] nq=%u expand=%llu edges=%llu filtered=%llu gathers=%llu "
+            "atomics=%llu improved=%llu rounds=%llu refreshed=%llu\n",
+            q->nq, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
+  }
   return SPF_OK;
 }
 
@@ -4465,6 +4736,15 @@ int spf_table_repair(
     a.nq = num_rows;
     a.G = 8;
     da.shift = dstep_bucket_shift(g, false);
+    da.fshift = da.shift;
+    // coherent gathers + non-returning atomics and 16-byte packed edges, as
+    // the full pass (dstep_tune); bucket bytes at the bucket width
+    da.noret = 3;
+    if (g->cw_bits) {
+      da.cw = g->d_cw;
+      da.cwbits = g->cw_bits;
+      da.cwvec = 1;
+    }
     da.table = rows;
     da.pitch = pitch;
     da.row_idx = d32 + num_rows;
@@ -4476,7 +4756,8 @@ int spf_table_repair(
     da.rm_w = (const uint64_t*)(d + off64);
     da.nrem = nrem;
     da.gscratch2 = a.gscratch + (size_t)grid * g->V;
-    auto kern = spf_dstep_kernel<0, false, 1024, true, true>;
+    auto kern = g->cw_bits ? spf_dstep_kernel<0, false, 1024, true, true, true>
+                           : spf_dstep_kernel<0, false, 1024, true, true, false>;
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds) != hipSuccess) {
       st = fail(SPF_E_DEVICE, "LDS attribute");

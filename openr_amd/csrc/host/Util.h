@@ -81,6 +81,61 @@ inline thrift::NextHopThrift createNextHop(
   return nh;
 }
 
+// Fib's programmed subset of a unicast route's next hops (Util.cpp:473-495):
+// those at the minimum metric, plus any marked useNonShortestRoute; input
+// order kept.
+inline std::vector<thrift::NextHopThrift> getBestNextHopsUnicast(
+    const std::vector<thrift::NextHopThrift>& allNextHops) {
+  if (allNextHops.size() <= 1) {
+    return allNextHops;
+  }
+  int32_t minCost = std::numeric_limits<int32_t>::max();
+  for (const auto& nh : allNextHops) {
+    minCost = std::min(minCost, nh.metric);
+  }
+  std::vector<thrift::NextHopThrift> best;
+  for (const auto& nh : allNextHops) {
+    if (nh.metric == minCost || nh.useNonShortestRoute) {
+      best.push_back(nh);
+    }
+  }
+  return best;
+}
+
+// The MPLS counterpart (Util.cpp:497-531): minimum metric, and among the
+// next hops reaching it PHP is preferred over SWAP; PUSH and POP_AND_LOOKUP
+// are invalid in a multi-next-hop label route (the reference CHECKs).
+inline std::vector<thrift::NextHopThrift> getBestNextHopsMpls(
+    const std::vector<thrift::NextHopThrift>& allNextHops) {
+  if (allNextHops.size() <= 1) {
+    return allNextHops;
+  }
+  int32_t minCost = std::numeric_limits<int32_t>::max();
+  thrift::MplsActionCode code = thrift::MplsActionCode::SWAP;
+  for (const auto& nh : allNextHops) {
+    if (!nh.mplsAction) {
+      throw CheckFailure("getBestNextHopsMpls: next hop without an MPLS action");
+    }
+    if (nh.mplsAction->action == thrift::MplsActionCode::PUSH ||
+        nh.mplsAction->action == thrift::MplsActionCode::POP_AND_LOOKUP) {
+      throw CheckFailure("getBestNextHopsMpls: PUSH / POP_AND_LOOKUP in a label route");
+    }
+    if (nh.metric <= minCost) {
+      minCost = nh.metric;
+      if (nh.mplsAction->action == thrift::MplsActionCode::PHP) {
+        code = thrift::MplsActionCode::PHP;
+      }
+    }
+  }
+  std::vector<thrift::NextHopThrift> best;
+  for (const auto& nh : allNextHops) {
+    if (nh.metric == minCost && nh.mplsAction->action == code) {
+      best.push_back(nh);
+    }
+  }
+  return best;
+}
+
 // IP wins over SR_MPLS when advertisers disagree (Util.cpp:635-652)
 inline thrift::PrefixForwardingType getPrefixForwardingType(
     const thrift::PrefixEntries& entries) {

@@ -488,6 +488,30 @@ PYBIND11_MODULE(_openr_spf, m) {
       .def(py::init<>())
       .def("to_dict", [](const DecisionRouteDb& db) { return routeDbToPy(db); });
   // getRouteDelta (Decision.cpp:47-85) on the host RouteDbs
+  // Fib's best-next-hop filters (Util.cpp:473-531): NextHopThrift objects in,
+  // canonical next-hop tuples out, input order kept
+  m.def("getBestNextHopsUnicast", [](py::iterable nhs) {
+    std::vector<openr::thrift::NextHopThrift> v;
+    for (auto nh : nhs) {
+      v.push_back(toNextHop(nh));
+    }
+    py::list out;
+    for (const auto& nh : openr::getBestNextHopsUnicast(v)) {
+      out.append(nextHopKey(nh));
+    }
+    return out;
+  });
+  m.def("getBestNextHopsMpls", [](py::iterable nhs) {
+    std::vector<openr::thrift::NextHopThrift> v;
+    for (auto nh : nhs) {
+      v.push_back(toNextHop(nh));
+    }
+    py::list out;
+    for (const auto& nh : openr::getBestNextHopsMpls(v)) {
+      out.append(nextHopKey(nh));
+    }
+    return out;
+  });
   m.def("getRouteDelta", [](const DecisionRouteDb& newDb, const DecisionRouteDb& oldDb) {
     const DecisionRouteUpdate u = getRouteDelta(newDb, oldDb);
     DecisionRouteDb upd;

@@ -1248,6 +1248,45 @@ PYBIND11_MODULE(_oracle_ref, m) {
   });
   m.def("reset_counters", [] { g_counters.clear(); });
 
+  // Util.cpp:473-495 getBestNextHopsUnicast / :497-531 getBestNextHopsMpls
+  m.def("getBestNextHopsUnicast", [](py::iterable in) {
+    std::vector<NextHopThrift> all;
+    for (auto o : in) all.push_back(toNextHop(o));
+    py::list out;
+    if (all.size() <= 1) {
+      for (const auto& nh : all) out.append(nextHopKey(nh));
+      return out;
+    }
+    int32_t lo = INT32_MAX;
+    for (const auto& nh : all) lo = std::min(lo, nh.metric);
+    for (const auto& nh : all)
+      if (nh.metric == lo || nh.useNonShortestRoute) out.append(nextHopKey(nh));
+    return out;
+  });
+  m.def("getBestNextHopsMpls", [](py::iterable in) {
+    std::vector<NextHopThrift> all;
+    for (auto o : in) all.push_back(toNextHop(o));
+    py::list out;
+    if (all.size() <= 1) {
+      for (const auto& nh : all) out.append(nextHopKey(nh));
+      return out;
+    }
+    int32_t lo = INT32_MAX;
+    MplsActionCode want = MplsActionCode::SWAP;
+    for (const auto& nh : all) {
+      if (!nh.mplsAction || nh.mplsAction->action == MplsActionCode::PUSH ||
+          nh.mplsAction->action == MplsActionCode::POP_AND_LOOKUP)
+        throw std::logic_error("getBestNextHopsMpls: CHECK failed");
+      if (nh.metric <= lo) {
+        lo = nh.metric;
+        if (nh.mplsAction->action == MplsActionCode::PHP) want = MplsActionCode::PHP;
+      }
+    }
+    for (const auto& nh : all)
+      if (nh.metric == lo && nh.mplsAction->action == want) out.append(nextHopKey(nh));
+    return out;
+  });
+
   // csr_spf.h: the fast flat restatement (goldens, all-cores CPU baseline).
   // Returns uint64 [Q, 4] = (reached, sum of distances, (node, next hop)
   // pairs, mix) per query; ignore = (offsets u32[Q+1], sorted link ids).

@@ -109,7 +109,9 @@ int spf_graph_patch_metrics(
  * graph's own stream). */
 int spf_graph_set_stream(spf_graph* g, void* stream);
 void* spf_graph_get_stream(spf_graph* g);
-/* 1 if metric runs on this graph need the exact (metric-0 / 64-bit) kernel. */
+/* 1 if metric runs on this graph need 64-bit rows and a settle order: metric
+ * 0 or sums that may pass 32 bits (the wide plan), or metrics that wrap
+ * (negative i32, the literal DijkstraQ replay). */
 int spf_graph_needs_exact(const spf_graph* g);
 /* Number of distinct neighbours of `node` = bits in its next-hop masks. */
 int spf_graph_num_nbrs(const spf_graph* g, uint32_t node);
@@ -134,7 +136,8 @@ int spf_query_stage_ms(spf_query* q, float* dist_ms, float* nh_ms);
  * (lets a caller time a loop of asynchronous runs per kernel). */
 int spf_query_stage_history(
     spf_query* q, uint32_t n, float* dist_ms, float* nh_ms, uint32_t* got);
-/* Name of the kernel the last run used ("lds", "gmem", "exact"). */
+/* Name of the plan the last run used ("lds", "dstep", "msbfs+levels", "wide",
+ * "exact", ...). */
 const char* spf_query_kernel_name(const spf_query* q);
 
 /* Distances of query i, one per node; SPF_UNREACHABLE = not reached. */
@@ -146,6 +149,12 @@ int spf_query_nexthops(spf_query* q, uint32_t i, uint64_t* out /*[V*W]*/);
 /* Settle rank of every node for query i (SPF_F_ORDER): the order in which the
  * reference's DijkstraQ extracts nodes; UINT32_MAX = not reached. */
 int spf_query_order(spf_query* q, uint32_t i, uint32_t* out /*[V]*/);
+/* Settle keys of query i (SPF_F_ORDER on a graph that needs 64-bit rows and
+ * whose metrics do not wrap, i.e. the wide plan): node u settles before node v
+ * iff (dist[u], key[u]) < (dist[v], key[v]) lexicographically, so a caller
+ * compares instead of sorting; SPF_UNREACHABLE = not reached.
+ * SPF_E_UNSUPPORTED for the literal-replay plan (use spf_query_order). */
+int spf_query_order_keys(spf_query* q, uint32_t i, uint64_t* out /*[V]*/);
 /* Device pointers of the result rows (for RCCL gathers): dist rows are
  * uint32 (fast kernels) or uint64 (exact kernel), spf_query_row_stride
  * elements apart (V entries used per row).  Next-hop rows are packed:

@@ -51,6 +51,7 @@ EXPORTED_SYMBOLS = (
     "spf_query_nh_words",
     "spf_query_nexthops",
     "spf_query_order",
+    "spf_query_order_keys",
     "spf_query_device_rows",
     "spf_query_row_stride",
     "spf_query_fetch_rows",
@@ -208,6 +209,7 @@ def load():
         "spf_query_nh_words": (C.c_int, [vp, u32]),
         "spf_query_nexthops": (C.c_int, [vp, u32, pu64]),
         "spf_query_order": (C.c_int, [vp, u32, pu32]),
+        "spf_query_order_keys": (C.c_int, [vp, u32, pu64]),
         "spf_query_row_stride": (u32, [vp]),
         "spf_query_fetch_rows": (C.c_int, [vp, u32, u32, vp, C.c_size_t, C.c_int]),
         "spf_query_fetch_nexthops": (C.c_int, [vp, u32, u32, pu64]),
@@ -528,6 +530,12 @@ class Query:
     def order(self, i: int) -> np.ndarray:
         out = np.zeros(self.graph.V, dtype=np.uint32)
         _check(load().spf_query_order(self.h, i, _p(out, C.c_uint32)), "order")
+        return out
+
+    def order_keys(self, i: int) -> np.ndarray:
+        """Wide plan: settle order = lexicographic (dist, key)."""
+        out = np.zeros(self.graph.V, dtype=np.uint64)
+        _check(load().spf_query_order_keys(self.h, i, _p(out, C.c_uint64)), "order_keys")
         return out
 
     def fetch_rows(self, first: int, count: int, dst_ptr: int, pitch: int, on_device=True):

@@ -620,8 +620,15 @@ std::vector<std::unique_ptr<SpfView>> runBatch(
       }
     }
     if (exact) {
-      view->order.resize(V);
-      if (int st = spf_query_order(q, (uint32_t)i, view->order.data()); st != SPF_OK) {
+      // wide plan: compare (dist, key); literal replay: settle ranks
+      view->okey.resize(V);
+      int st = spf_query_order_keys(q, (uint32_t)i, view->okey.data());
+      if (st == SPF_E_UNSUPPORTED) {
+        view->okey.clear();
+        view->order.resize(V);
+        st = spf_query_order(q, (uint32_t)i, view->order.data());
+      }
+      if (st != SPF_OK) {
         engineFailure("spf_query_order", st);
       }
     }
@@ -753,8 +760,7 @@ void pathLinksOf(
     if (view.dist[u] + w != dv) {
       continue;
     }
-    if (view.exact ? !(view.order[u] < view.order[v])
-                   : !(view.dist[u] < dv)) {
+    if (!view.settlesBefore(u, v)) {
       continue;
     }
     out.emplace_back(eu, u);
@@ -762,13 +768,7 @@ void pathLinksOf(
   std::sort(out.begin(), out.end(), [&](const auto& a, const auto& b) {
     const uint32_t ua = a.second, ub = b.second;
     if (ua != ub) {
-      if (view.exact) {
-        return view.order[ua] < view.order[ub];
-      }
-      if (view.dist[ua] != view.dist[ub]) {
-        return view.dist[ua] < view.dist[ub];
-      }
-      return ua < ub;
+      return view.settlesBefore(ua, ub);
     }
     return a.first < b.first; // row-u position = linksFromNode(u) order
   });

@@ -169,11 +169,23 @@ struct SpfView {
   uint32_t words{1};          // words per next-hop mask
   std::vector<uint64_t> nh;   // [V * words]
   std::vector<uint32_t> nbrs; // mask bit -> node id
-  std::vector<uint32_t> order; // exact kernel: settle rank per node id
+  std::vector<uint32_t> order; // literal replay: settle rank per node id
+  std::vector<uint64_t> okey;  // wide plan: settle order = (dist, okey)
   std::vector<uint32_t> ignored; // sorted link ids this run skipped
   static constexpr uint64_t kUnreachable = ~0ull;
 
   bool reached(uint32_t v) const { return v < dist.size() && dist[v] != kUnreachable; }
+  // DijkstraQ's settle order between two reached nodes (LinkState.h:483-535)
+  bool settlesBefore(uint32_t u, uint32_t v) const {
+    if (exact && okey.empty()) {
+      return order[u] < order[v];
+    }
+    const uint64_t du = dist[u], dv = dist[v];
+    if (du != dv) {
+      return du < dv;
+    }
+    return okey.empty() ? u < v : okey[u] < okey[v];
+  }
   template <class Fn>
   void forEachNextHop(uint32_t v, Fn&& fn) const {
     const uint64_t* m = nh.data() + (size_t)v * words;

@@ -2277,6 +2277,421 @@ __global__ __launch_bounds__(64) void spf_exact_kernel(ExactArgs a) {
   }
 }
 
+// -------------------------------------------------------------- wide kernel
+//
+// 64-bit distances for the metric graphs the 32-bit plans cannot take
+// (metric-0 links, or sums that may pass 2^32), one 1024-thread workgroup per
+// query, in parallel where the literal replay above is one thread:
+//  1. distances: near-far label-correcting SSSP over the u64 HBM row
+//     (pending bitmap in LDS, atomicMin on the row, the band [.., T) advances
+//     to the smallest pending distance + delta).  Any processing order
+//     reaches the unique fixpoint for non-negative metrics;
+//  2. settle keys: DijkstraQ extracts DISCOVERED nodes by (metric, name)
+//     (LinkState.h:483-535), so only plateaus of equal distance joined by
+//     usable metric-0 edges depart from (distance, id) order.  The plateau
+//     nodes that take part -- tails of such edges reached from below ("active
+//     seeds") and nodes reached only over metric-0 edges -- are replayed by
+//     one lane with a heap keyed (distance, id).  Passive nodes keep key
+//     id<<32; a replayed node gets (M<<32)|2^31|j, M the largest id replayed
+//     so far on its plateau, j its replay index.  A passive node p is
+//     extracted before a replayed node x iff p < M(x) (every passive of the
+//     plateau is in the heap from the start and never discovers anything), so
+//     (distance, key) order IS the reference's settle order;
+//  3. next hops: NH(v) = union over usable tight in-edges u->v with u settled
+//     before v of (u == src ? bit(v) : NH(u)) (LinkState.cpp:846-867; the
+//     source settles first, so its "directly connected" rule always fires),
+//     propagated in Kahn rounds over that DAG: a count of outstanding
+//     in-edges per node, 64-bit atomicOr of the masks.
+// The literal replay stays only for graphs whose metrics wrap (negative i32
+// metrics as uint64, where Dijkstra's order is not a fixpoint).
+
+constexpr uint32_t kWideBlock = 1024;
+constexpr uint32_t kWideG = 8; // lanes per node in the edge loops
+
+struct WideArgs {
+  const uint32_t* row;
+  const uint32_t* col;
+  const uint64_t* w64;
+  const uint32_t* link;
+  const uint32_t* rev;
+  const uint32_t* slot;
+  const uint32_t* trbits;
+  const uint32_t* zero_e; // half-edges with metric 0
+  const uint32_t* src;
+  const uint32_t* ign_off;
+  const uint32_t* ign;
+  const uint64_t* nh_off;
+  const uint32_t* nh_w;
+  uint64_t* dist_out; // [nq][V]
+  uint64_t* nh_out;
+  uint64_t* key_out;  // [nq][V] settle keys, or null
+  uint32_t* scratch;  // per workgroup: wide_stride(V, nbw) words
+  uint64_t delta;
+  uint32_t V, nq, nbw, n_zero, unit, want_nh;
+};
+
+// per-workgroup scratch: two queues, counts, heap [V] u32; keys [V] u64;
+// active / discovered / replayed bitmaps [nbw]
+__host__ __device__ inline size_t wide_stride(uint32_t V, uint32_t nbw) {
+  return (6 * (size_t)V + 3 * (size_t)nbw + 3) & ~(size_t)3;
+}
+
+__device__ __forceinline__ uint64_t ld_coh64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool wd_usable(const uint32_t* tr, uint32_t u, uint32_t s) {
+  return u == s || ((tr[u >> 5] >> (u & 31)) & 1u);
+}
+
+__device__ __forceinline__ bool wd_bit(const uint32_t* b, uint32_t v) {
+  return (ld_coh(b + (v >> 5)) >> (v & 31)) & 1u;
+}
+
+// x is discovered before its plateau starts: the source, or the head of a
+// usable tight in-edge from a smaller distance
+__device__ bool wd_seed(
+    const WideArgs& a, const uint64_t* d, uint32_t x, uint32_t s,
+    const uint32_t* ignp, uint32_t nign) {
+  if (x == s) {
+    return true;
+  }
+  const uint64_t dx = ld_coh64(d + x);
+  for (uint32_t e = a.row[x]; e < a.row[x + 1]; ++e) {
+    const uint32_t u = a.col[e];
+    if (!wd_usable(a.trbits, u, s) || (nign && in_sorted(ignp, nign, a.link[e]))) {
+      continue;
+    }
+    const uint64_t du = ld_coh64(d + u);
+    if (du < dx && du + a.w64[a.rev[e]] == dx) {
+      return true;
+    }
+  }
+  return false;
+}
+
+// Workgroup barrier for lanes that talk through GLOBAL memory: a plain
+// __syncthreads() only drains LDS traffic (s_waitcnt lgkmcnt), so stores and
+// non-returning atomics of other waves may still be on their way to L2.
+// Draining vmcnt first puts them in L2 (one XCD's L2 serves the whole
+// workgroup, so no agent-scope L2 writeback is needed); readers of data other
+// waves wrote use L1-bypassing loads (ld_coh / ld_coh64).
+__device__ __forceinline__ void wide_sync() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kWideBlock) void spf_wide_kernel(WideArgs a) {
+  extern __shared__ uint32_t wlds[];
+  uint32_t* pend = wlds; // [nbw]
+  __shared__ uint32_t s_qlen;
+  __shared__ unsigned long long s_min;
+  constexpr uint32_t BS = kWideBlock;
+  const uint32_t V = a.V, nbw = a.nbw, tid = threadIdx.x;
+  const uint32_t gl = tid % kWideG, gi = tid / kWideG;
+  uint32_t* ws = a.scratch + (size_t)blockIdx.x * wide_stride(V, nbw);
+  uint32_t* qa = ws;
+  uint32_t* qb = ws + V;
+  uint32_t* cnt = ws + 2 * (size_t)V;
+  uint32_t* heap = ws + 3 * (size_t)V;
+  uint64_t* kx = (uint64_t*)(ws + 4 * (size_t)V);
+  uint32_t* act = ws + 6 * (size_t)V;
+  uint32_t* disc = act + nbw;
+  uint32_t* mem = disc + nbw;
+  const bool zplat = a.n_zero && !a.unit;
+
+  for (uint32_t q = blockIdx.x; q < a.nq; q += gridDim.x) {
+    const uint32_t s = a.src[q];
+    uint64_t* d = a.dist_out + (size_t)q * V;
+    const uint32_t ilo = a.ign_off ? a.ign_off[q] : 0;
+    const uint32_t nign = a.ign_off ? a.ign_off[q + 1] - ilo : 0;
+    const uint32_t* ignp = a.ign ? a.ign + ilo : nullptr;
+    for (uint32_t v = tid; v < V; v += BS) {
+      d[v] = SPF_UNREACHABLE;
+    }
+    for (uint32_t w = tid; w < nbw; w += BS) {
+      pend[w] = 0;
+      act[w] = 0;
+      disc[w] = 0;
+      mem[w] = 0;
+    }
+    wide_sync();
+    if (tid == 0) {
+      d[s] = 0;
+      pend[s >> 5] = 1u << (s & 31);
+    }
+    wide_sync();
+
+    // ---- 1. distances (near-far)
+    uint64_t T = a.delta;
+    for (;;) {
+      if (tid == 0) {
+        s_qlen = 0;
+        s_min = SPF_UNREACHABLE;
+      }
+      wide_sync();
+      uint64_t lmin = SPF_UNREACHABLE;
+      for (uint32_t w = tid; w < nbw; w += BS) {
+        uint32_t b = pend[w];
+        if (!b) {
+          continue;
+        }
+        uint32_t keep = 0;
+        while (b) {
+          const uint32_t k = __ffs(b) - 1;
+          b &= b - 1;
+          const uint32_t v = w * 32 + k;
+          const uint64_t dv = ld_coh64(d + v);
+          if (dv < T) {
+            qa[atomicAdd(&s_qlen, 1u)] = v;
+          } else {
+            keep |= 1u << k;
+            lmin = min(lmin, dv);
+          }
+        }
+        pend[w] = keep;
+      }
+      for (int o = 32; o > 0; o >>= 1) {
+        lmin = min(lmin, (uint64_t)__shfl_xor((unsigned long long)lmin, o, 64));
+      }
+      if ((tid & 63) == 0 && lmin != SPF_UNREACHABLE) {
+        atomicMin(&s_min, (unsigned long long)lmin);
+      }
+      wide_sync();
+      const uint32_t n = s_qlen;
+      if (n == 0) {
+        const uint64_t m = s_min;
+        wide_sync();
+        if (m == SPF_UNREACHABLE) {
+          break;
+        }
+        T = m + a.delta;
+        continue;
+      }
+      for (uint32_t i = gi; i < n; i += BS / kWideG) {
+        const uint32_t u = ld_coh(qa + i);
+        if (!wd_usable(a.trbits, u, s)) {
+          continue;
+        }
+        const uint64_t du = ld_coh64(d + u);
+        for (uint32_t e = a.row[u] + gl; e < a.row[u + 1]; e += kWideG) {
+          if (nign && in_sorted(ignp, nign, a.link[e])) {
+            continue;
+          }
+          const uint32_t v = a.col[e];
+          const uint64_t c = du + (a.unit ? 1ull : a.w64[e]);
+          if (c < ld_coh64(d + v)) {
+            const uint64_t old =
+                atomicMin((unsigned long long*)(d + v), (unsigned long long)c);
+            if (c < old) {
+              atomicOr(&pend[v >> 5], 1u << (v & 31));
+            }
+          }
+        }
+      }
+      wide_sync();
+    }
+
+    // ---- 2. settle keys of metric-0 plateaus
+    if (zplat) {
+      for (uint32_t i = tid; i < a.n_zero; i += BS) {
+        const uint32_t e = a.zero_e[i];
+        const uint32_t u = a.col[a.rev[e]], v = a.col[e];
+        if (!wd_usable(a.trbits, u, s) || (nign && in_sorted(ignp, nign, a.link[e]))) {
+          continue;
+        }
+        const uint64_t du = ld_coh64(d + u);
+        if (du != SPF_UNREACHABLE && du == ld_coh64(d + v)) {
+          atomicOr(&act[u >> 5], 1u << (u & 31));
+        }
+      }
+      if (tid == 0) {
+        s_qlen = 0;
+      }
+      wide_sync();
+      for (uint32_t w = tid; w < nbw; w += BS) {
+        uint32_t b = ld_coh(act + w);
+        while (b) {
+          const uint32_t x = w * 32 + (__ffs(b) - 1);
+          b &= b - 1;
+          if (wd_seed(a, d, x, s, ignp, nign)) {
+            heap[atomicAdd(&s_qlen, 1u)] = x;
+            atomicOr(&disc[x >> 5], 1u << (x & 31));
+          }
+        }
+      }
+      wide_sync();
+      if (tid == 0) {
+        // other lanes wrote the heap: drop stale L1 lines first
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        uint32_t n = s_qlen;
+        auto before = [&](uint32_t x, uint32_t y) {
+          const uint64_t dx = ld_coh64(d + x), dy = ld_coh64(d + y);
+          return dx < dy || (dx == dy && x < y);
+        };
+        auto sift_down = [&](uint32_t i) {
+          const uint32_t x = heap[i];
+          for (;;) {
+            uint32_t c = 2 * i + 1;
+            if (c >= n) {
+              break;
+            }
+            if (c + 1 < n && before(heap[c + 1], heap[c])) {
+              ++c;
+            }
+            if (!before(heap[c], x)) {
+              break;
+            }
+            heap[i] = heap[c];
+            i = c;
+          }
+          heap[i] = x;
+        };
+        for (uint32_t i = n / 2; i-- > 0;) {
+          sift_down(i);
+        }
+        uint64_t curD = SPF_UNREACHABLE;
+        uint32_t M = 0, j = 0;
+        while (n) {
+          const uint32_t x = heap[0];
+          if (--n) {
+            heap[0] = heap[n];
+            sift_down(0);
+          }
+          const uint64_t dx = ld_coh64(d + x);
+          if (dx != curD) {
+            curD = dx;
+            M = 0;
+          }
+          M = max(M, x);
+          kx[x] = ((uint64_t)M << 32) | 0x80000000ull | j++;
+          atomicOr(&mem[x >> 5], 1u << (x & 31));
+          if (!wd_usable(a.trbits, x, s)) {
+            continue;
+          }
+          for (uint32_t e = a.row[x]; e < a.row[x + 1]; ++e) {
+            if (a.w64[e] != 0 || (nign && in_sorted(ignp, nign, a.link[e]))) {
+              continue;
+            }
+            const uint32_t y = a.col[e];
+            if (ld_coh64(d + y) != dx || wd_bit(disc, y)) {
+              continue;
+            }
+            atomicOr(&disc[y >> 5], 1u << (y & 31));
+            if (wd_seed(a, d, y, s, ignp, nign)) {
+              continue; // a passive seed: already in the plateau's heap
+            }
+            uint32_t i = n++;
+            while (i > 0) { // sift up
+              const uint32_t p = (i - 1) >> 1;
+              if (!before(y, heap[p])) {
+                break;
+              }
+              heap[i] = heap[p];
+              i = p;
+            }
+            heap[i] = y;
+          }
+        }
+      }
+      wide_sync();
+    }
+    auto key = [&](uint32_t v) -> uint64_t {
+      return (zplat && wd_bit(mem, v)) ? ld_coh64(kx + v) : ((uint64_t)v << 32);
+    };
+
+    // ---- 3. next hops (Kahn rounds over the settle-ordered tight DAG)
+    if (a.want_nh) {
+      const uint32_t W = a.nh_w[q];
+      uint64_t* nh = a.nh_out + a.nh_off[q];
+      for (uint32_t v = tid; v < V; v += BS) {
+        const uint64_t dv = ld_coh64(d + v);
+        uint32_t c = 0;
+        if (dv != SPF_UNREACHABLE && v != s) {
+          for (uint32_t e = a.row[v]; e < a.row[v + 1]; ++e) {
+            const uint32_t u = a.col[e];
+            if (!wd_usable(a.trbits, u, s) || (nign && in_sorted(ignp, nign, a.link[e]))) {
+              continue;
+            }
+            const uint64_t du = ld_coh64(d + u);
+            const uint64_t wu = a.unit ? 1ull : a.w64[a.rev[e]];
+            if (du == SPF_UNREACHABLE || du + wu != dv) {
+              continue;
+            }
+            if (wu == 0 && !(key(u) < key(v))) {
+              continue;
+            }
+            ++c;
+          }
+        }
+        cnt[v] = c;
+      }
+      if (tid == 0) {
+        qa[0] = s;
+      }
+      wide_sync();
+      uint32_t n = 1;
+      uint32_t *cur = qa, *nxt = qb;
+      while (n) {
+        if (tid == 0) {
+          s_qlen = 0;
+        }
+        wide_sync();
+        for (uint32_t i = gi; i < n; i += BS / kWideG) {
+          const uint32_t u = ld_coh(cur + i);
+          if (!wd_usable(a.trbits, u, s)) {
+            continue;
+          }
+          const uint64_t du = ld_coh64(d + u);
+          const uint64_t ku = key(u);
+          for (uint32_t e = a.row[u] + gl; e < a.row[u + 1]; e += kWideG) {
+            const uint32_t v = a.col[e];
+            if (v == s || (nign && in_sorted(ignp, nign, a.link[e]))) {
+              continue;
+            }
+            const uint64_t w = a.unit ? 1ull : a.w64[e];
+            const uint64_t dv = ld_coh64(d + v);
+            if (dv == SPF_UNREACHABLE || du + w != dv || (w == 0 && !(ku < key(v)))) {
+              continue;
+            }
+            if (u == s) {
+              const uint32_t sl = a.slot[e];
+              atomicOr((unsigned long long*)(nh + (size_t)v * W + (sl >> 6)),
+                       1ull << (sl & 63));
+            } else {
+              for (uint32_t k = 0; k < W; ++k) {
+                const uint64_t m = ld_coh64(nh + (size_t)u * W + k);
+                if (m) {
+                  atomicOr((unsigned long long*)(nh + (size_t)v * W + k),
+                           (unsigned long long)m);
+                }
+              }
+            }
+            if (atomicSub(cnt + v, 1u) == 1u) {
+              nxt[atomicAdd(&s_qlen, 1u)] = v;
+            }
+          }
+        }
+        wide_sync();
+        n = s_qlen;
+        uint32_t* t = cur;
+        cur = nxt;
+        nxt = t;
+        wide_sync();
+      }
+    }
+
+    // ---- 4. settle keys out (SPF_F_ORDER)
+    if (a.key_out) {
+      uint64_t* ko = a.key_out + (size_t)q * V;
+      for (uint32_t v = tid; v < V; v += BS) {
+        ko[v] = ld_coh64(d + v) == SPF_UNREACHABLE ? SPF_UNREACHABLE : key(v);
+      }
+    }
+    wide_sync();
+  }
+}
+
 // ------------------------------------------------ what-if screen (config 5)
 //
 // Removing a link changes an SPF only if one of its half-edges u->v is a
@@ -2644,7 +3059,9 @@ struct spf_graph {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   uint32_t V = 0, E = 0, L = 0, nbw = 0;
-  bool exact = false;     // metric runs need the exact kernel
+  bool exact = false;     // metric runs need 64-bit rows (wide or literal plan)
+  bool wrap = false;      // a metric above 2^31-1 (negative i32): literal replay
+  uint32_t n_zero = 0;    // half-edges with metric 0 (wide plan plateaus)
   uint32_t uniform = 0;   // every metric equals this value (0 = mixed)
   uint32_t G = 8;
   int num_cus = 256;
@@ -2658,6 +3075,8 @@ struct spf_graph {
            *d_nbrs = nullptr, *d_nbr_w = nullptr;
   uint64_t* d_w64 = nullptr;
   uint32_t* d_link_half = nullptr; // [2L] half-edges of each link (what-if screen)
+  uint32_t* d_zero_e = nullptr;    // [n_zero] half-edges with metric 0
+  uint64_t wide_delta = 1;         // wide plan band width (mean metric)
   // out-edges packed as head | metric << cw_bits (one u32 per edge) when
   // both fit; cw_bits = 0: not packed
   uint32_t* d_cw = nullptr;
@@ -2666,7 +3085,7 @@ struct spf_graph {
 };
 
 // How a batch is computed.
-enum class DistPlan { SsspLds, SsspGmem, BfsLds, BfsGmem, MsBfs, Dstep, MsDstep, Exact };
+enum class DistPlan { SsspLds, SsspGmem, BfsLds, BfsGmem, MsBfs, Dstep, MsDstep, Wide, Exact };
 enum class NhPlan { None, Inline, Rows, Levels };
 
 struct spf_query {
@@ -2705,6 +3124,7 @@ struct spf_query {
   uint64_t* d_nh_off = nullptr;
   void* d_dist = nullptr;
   uint64_t* d_nh = nullptr;
+  uint64_t* d_key = nullptr; // wide plan settle keys (SPF_F_ORDER)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t evm = nullptr; // after the distance stage, before next hops
   bool ran = false;
@@ -2739,7 +3159,8 @@ void free_graph(spf_graph* g) {
        {(void*)g->d_row, (void*)g->d_col, (void*)g->d_wout, (void*)g->d_win,
         (void*)g->d_link, (void*)g->d_rev, (void*)g->d_slot, (void*)g->d_tr,
         (void*)g->d_w64, (void*)g->d_nbr_off, (void*)g->d_nbrs,
-        (void*)g->d_nbr_w, (void*)g->d_link_half, (void*)g->d_cw}) {
+        (void*)g->d_nbr_w, (void*)g->d_link_half, (void*)g->d_cw,
+        (void*)g->d_zero_e}) {
     if (p) {
       (void)hipFree(p);
     }
@@ -2761,7 +3182,7 @@ void free_query(spf_query* q) {
         (void*)q->d_nh_off, q->d_dist, (void*)q->d_nh, (void*)q->d_row_of,
         (void*)q->d_lvl, (void*)q->d_flags, (void*)q->d_perm,
         (void*)q->d_slab, (void*)q->d_msd, (void*)q->d_base_of,
-        (void*)q->d_skip}) {
+        (void*)q->d_skip, (void*)q->d_key}) {
     if (p) {
       (void)hipFree(p);
     }
@@ -2801,28 +3222,51 @@ int upload_weights(spf_graph* g) {
       }
     }, 1);
   };
-  std::vector<uint64_t> wmax(nth, 0);
-  std::vector<uint8_t> wexact(nth, 0);
+  std::vector<uint64_t> wmax(nth, 0), wsum(nth, 0);
+  std::vector<uint8_t> wwrap(nth, 0);
+  std::vector<std::vector<uint32_t>> zeros(nth);
   blocks([&](uint32_t u, unsigned w) {
     for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
       const uint64_t m = g->w64[e];
-      if (m == 0 || m > 0x7FFFFFFFull) {
-        wexact[w] = 1;
+      if (m > 0x7FFFFFFFull) {
+        wwrap[w] = 1;
+      } else {
+        wsum[w] += m;
+      }
+      if (m == 0) {
+        zeros[w].push_back(e);
       }
       wmax[w] = std::max(wmax[w], m);
     }
   });
-  uint64_t maxw = 0;
-  bool exact = false;
+  uint64_t maxw = 0, sumw = 0;
+  bool wrap = false;
+  std::vector<uint32_t> zero_e;
   for (unsigned w = 0; w < nth; ++w) {
     maxw = std::max(maxw, wmax[w]);
-    exact = exact || wexact[w];
+    sumw += wsum[w];
+    wrap = wrap || wwrap[w];
+    zero_e.insert(zero_e.end(), zeros[w].begin(), zeros[w].end());
   }
+  std::sort(zero_e.begin(), zero_e.end());
+  bool exact = wrap || !zero_e.empty();
   if (!exact && V > 1 && maxw > 0 &&
       (unsigned __int128)maxw * (V - 1) >= 0xFFFFFFFFull) {
     exact = true;
   }
   g->exact = exact;
+  g->wrap = wrap;
+  g->n_zero = (uint32_t)zero_e.size();
+  // wide plan band: the mean metric (near-far's delta ~ a typical edge)
+  g->wide_delta = E ? std::max<uint64_t>(1, sumw / E) : 1;
+  if (g->d_zero_e) {
+    (void)hipFree(g->d_zero_e);
+    g->d_zero_e = nullptr;
+  }
+  if (!zero_e.empty()) {
+    HIP_TRY(hipMalloc((void**)&g->d_zero_e, zero_e.size() * 4));
+    HIP_TRY(hipMemcpy(g->d_zero_e, zero_e.data(), zero_e.size() * 4, hipMemcpyHostToDevice));
+  }
   g->uniform = 0;
   if (!exact && E) {
     const uint64_t c = g->w64[0];
@@ -3470,7 +3914,13 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
   // ---- plan: which kernels compute this batch
   std::vector<int32_t> row_of;
   std::vector<uint32_t> msd_perm;
-  const bool exact =(g->exact && !unit) || want_order;
+  // metrics that wrap (negative i32 as uint64): the literal DijkstraQ
+  // replay; metric 0 / sums past 32 bits / a settle order: the wide plan
+  // (OPENR_SPF_LITERAL=1 forces the replay on any 64-bit graph: measurement)
+  const char* lit_env = getenv("OPENR_SPF_LITERAL");
+  const bool literal =
+      (g->wrap && !unit) || (g->exact && !unit && lit_env && atoi(lit_env) == 1);
+  const bool exact = (g->exact && !unit) || want_order;
   const bool uniform = unit || g->uniform != 0;
   bool rows_ok = false;
   if (want_nh && !exact && !has_ign) {
@@ -3493,9 +3943,17 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       row_of.clear();
     }
   }
-  if (exact || (want_nh && !rows_ok && maxw > 16)) {
+  if (literal) {
     q->dist = DistPlan::Exact;
     q->nh = want_nh ? NhPlan::Inline : NhPlan::None;
+  } else if (exact || (want_nh && !rows_ok && maxw > 16)) {
+    q->dist = DistPlan::Wide;
+    q->nh = want_nh ? NhPlan::Inline : NhPlan::None;
+    q->lds_bytes = (size_t)g->nbw * 4;
+    if (q->lds_bytes + 64 > kLdsLimit) {
+      return bail(fail(SPF_E_UNSUPPORTED, "wide plan: pending bitmap exceeds LDS"));
+    }
+    q->grid = std::min<uint32_t>(std::max<uint32_t>(nq, 1), (uint32_t)g->num_cus * 2);
   } else {
     q->nh = !want_nh ? NhPlan::None : (rows_ok ? NhPlan::Rows : NhPlan::Inline);
     // weighted graph whose distance row does not fit LDS: delta-stepping
@@ -3629,7 +4087,8 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     return bail(s);
   }
   const bool ex = q->dist == DistPlan::Exact;
-  const size_t dist_bytes = ex ? (size_t)nq * V * 8 : (size_t)nq * q->Vp * 4;
+  const bool wide = q->dist == DistPlan::Wide;
+  const size_t dist_bytes = (ex || wide) ? (size_t)nq * V * 8 : (size_t)nq * q->Vp * 4;
   if (dist_bytes && hipMalloc(&q->d_dist, dist_bytes) != hipSuccess) {
     return bail(fail(SPF_E_NOMEM, "distance rows"));
   }
@@ -3653,6 +4112,13 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     if (hipMalloc((void**)&q->d_scratch, (size_t)nq * V * 8) != hipSuccess ||
         hipMalloc((void**)&q->d_order, (size_t)nq * V * 4) != hipSuccess) {
       return bail(fail(SPF_E_NOMEM, "exact-kernel scratch"));
+    }
+  }
+  if (wide && (size_t)nq * V) {
+    if (hipMalloc((void**)&q->d_scratch, (size_t)q->grid * wide_stride(V, g->nbw) * 4) !=
+            hipSuccess ||
+        (want_order && hipMalloc((void**)&q->d_key, (size_t)nq * V * 8) != hipSuccess)) {
+      return bail(fail(SPF_E_NOMEM, "wide-plan scratch"));
     }
   }
   // what-if screen (OPENR_SPF_WHATIF_SCREEN=0 disables): batches with
@@ -4060,6 +4526,53 @@ int launch_exact(spf_query* q) {
   return SPF_OK;
 }
 
+// 64-bit distance rows (literal replay or wide plan)
+inline bool rows64(const spf_query* q) {
+  return q->dist == DistPlan::Exact || q->dist == DistPlan::Wide;
+}
+
+int launch_wide(spf_query* q) {
+  spf_graph* g = q->g;
+  WideArgs a;
+  a.row = g->d_row;
+  a.col = g->d_col;
+  a.w64 = g->d_w64;
+  a.link = g->d_link;
+  a.rev = g->d_rev;
+  a.slot = g->d_slot;
+  a.trbits = g->d_tr;
+  a.zero_e = g->d_zero_e;
+  a.src = q->d_src;
+  a.ign_off = q->d_ign_off;
+  a.ign = q->d_ign;
+  a.nh_off = q->d_nh_off;
+  a.nh_w = q->d_nh_w;
+  a.dist_out = (uint64_t*)q->d_dist;
+  a.nh_out = q->d_nh;
+  a.key_out = q->d_key;
+  a.scratch = q->d_scratch;
+  a.V = g->V;
+  a.nq = q->nq;
+  a.nbw = g->nbw;
+  a.unit = (q->flags & SPF_F_UNIT_METRIC) ? 1 : 0;
+  a.n_zero = a.unit ? 0 : g->n_zero;
+  a.delta = a.unit ? 1 : g->wide_delta;
+  if (const char* dv = getenv("OPENR_SPF_WIDE_DELTA")) {
+    a.delta = std::max<uint64_t>(1, strtoull(dv, nullptr, 10));
+  }
+  a.want_nh = (q->flags & SPF_F_NEXTHOPS) ? 1 : 0;
+  if (g->nbw * 32 < g->V) {
+    return fail(SPF_E_INVALID, "bitmap words do not cover the nodes");
+  }
+  if (q->d_nh && q->nh_total) {
+    HIP_TRY(hipMemsetAsync(q->d_nh, 0, q->nh_total * 8, g->stream));
+  }
+  hipLaunchKernelGGL(spf_wide_kernel, dim3(q->grid), dim3(kWideBlock), q->lds_bytes,
+                     g->stream, a);
+  HIP_TRY(hipGetLastError());
+  return SPF_OK;
+}
+
 // Event between the distance kernel and the next-hop kernel of a two-stage
 // plan, so spf_query_stage_ms can split the device time per kernel.
 int mark_stage(spf_query* q) {
@@ -4119,6 +4632,8 @@ int run_plan(spf_query* q) {
   switch (q->dist) {
   case DistPlan::Exact:
     return launch_exact(q);
+  case DistPlan::Wide:
+    return launch_wide(q);
   case DistPlan::Dstep:
     return launch_dstep(q);
   case DistPlan::MsDstep:
@@ -4280,6 +4795,8 @@ const char* spf_query_kernel_name(const spf_query* q) {
     return "dstep";
   case DistPlan::MsDstep:
     return "msdstep";
+  case DistPlan::Wide:
+    return "wide";
   default:
     return "exact";
   }
@@ -4304,6 +4821,11 @@ int spf_query_dist(spf_query* q, uint32_t i, uint64_t* out) {
         out[v] = SPF_UNREACHABLE;
       }
     }
+    return SPF_OK;
+  }
+  if (q->dist == DistPlan::Wide) {
+    HIP_TRY(hipMemcpy(out, (uint64_t*)q->d_dist + (size_t)i * V, V * 8ull,
+                      hipMemcpyDeviceToHost));
     return SPF_OK;
   }
   std::vector<uint32_t> d(V);
@@ -4337,12 +4859,52 @@ int spf_query_nexthops(spf_query* q, uint32_t i, uint64_t* out) {
   return SPF_OK;
 }
 
+int spf_query_order_keys(spf_query* q, uint32_t i, uint64_t* out) {
+  SPF_ABI_RANGE("spf_query_order_keys");
+  if (!q || !out || i >= q->nq || !(q->flags & SPF_F_ORDER)) {
+    return fail(SPF_E_INVALID, "no settle order for this row");
+  }
+  if (q->dist != DistPlan::Wide) {
+    return fail(SPF_E_UNSUPPORTED, "settle keys come from the wide plan; use spf_query_order");
+  }
+  HIP_TRY(hipSetDevice(q->g->device));
+  HIP_TRY(hipStreamSynchronize(q->g->stream));
+  HIP_TRY(hipMemcpy(out, q->d_key + (size_t)i * q->g->V, q->g->V * 8ull,
+                    hipMemcpyDeviceToHost));
+  return SPF_OK;
+}
+
 int spf_query_order(spf_query* q, uint32_t i, uint32_t* out) {
-  if (!q || !out || i >= q->nq || q->dist != DistPlan::Exact) {
+  SPF_ABI_RANGE("spf_query_order");
+  if (!q || !out || i >= q->nq ||
+      !(q->dist == DistPlan::Exact || (q->dist == DistPlan::Wide && q->d_key))) {
     return fail(SPF_E_INVALID, "no settle order for this row");
   }
   HIP_TRY(hipSetDevice(q->g->device));
   HIP_TRY(hipStreamSynchronize(q->g->stream));
+  if (q->dist == DistPlan::Wide) {
+    // settle rank = position in (distance, key) order of the reached nodes
+    const uint32_t V = q->g->V;
+    std::vector<uint64_t> d(V), k(V);
+    HIP_TRY(hipMemcpy(d.data(), (uint64_t*)q->d_dist + (size_t)i * V, V * 8ull,
+                      hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(k.data(), q->d_key + (size_t)i * V, V * 8ull, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> idx;
+    idx.reserve(V);
+    for (uint32_t v = 0; v < V; ++v) {
+      out[v] = kInf32;
+      if (d[v] != SPF_UNREACHABLE) {
+        idx.push_back(v);
+      }
+    }
+    std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
+      return d[a] != d[b] ? d[a] < d[b] : k[a] < k[b];
+    });
+    for (uint32_t r = 0; r < idx.size(); ++r) {
+      out[idx[r]] = r;
+    }
+    return SPF_OK;
+  }
   HIP_TRY(hipMemcpy(out, q->d_order + (size_t)i * q->g->V, q->g->V * 4ull,
                     hipMemcpyDeviceToHost));
   return SPF_OK;
@@ -4358,7 +4920,7 @@ int spf_query_device_rows(
     *dist_rows = q->d_dist;
   }
   if (dist_elem_bytes) {
-    *dist_elem_bytes = q->dist == DistPlan::Exact ? 8 : 4;
+    *dist_elem_bytes = rows64(q) ? 8 : 4;
   }
   if (nh_rows) {
     *nh_rows = q->d_nh;
@@ -4382,7 +4944,7 @@ int spf_query_fetch_rows(
   if ((uint64_t)first + count > q->nq) {
     return fail(SPF_E_INVALID, "row range out of bounds");
   }
-  if (q->dist == DistPlan::Exact) {
+  if (rows64(q)) {
     return fail(SPF_E_UNSUPPORTED, "64-bit distance rows: use spf_query_dist");
   }
   const size_t V = q->g->V;
@@ -4438,7 +5000,7 @@ uint32_t spf_query_row_stride(const spf_query* q) {
   if (!q) {
     return 0;
   }
-  return q->dist == DistPlan::Exact ? q->g->V : q->Vp;
+  return rows64(q) ? q->g->V : q->Vp;
 }
 
 } // extern "C"
@@ -4610,7 +5172,7 @@ int spf_query_scatter_rows(
   if (!q->ran) {
     return fail(SPF_E_INVALID, "query has not run");
   }
-  if (q->dist == DistPlan::Exact) {
+  if (rows64(q)) {
     return fail(SPF_E_UNSUPPORTED, "64-bit distance rows: use spf_query_dist");
   }
   const uint32_t V = q->g->V;
@@ -4825,7 +5387,7 @@ int spf_route_table_create(
   if (!(q->flags & SPF_F_NEXTHOPS) || (q->flags & SPF_F_UNIT_METRIC) || q->has_ign) {
     return fail(SPF_E_INVALID, "route tables need a metric query with next hops and no ignore lists");
   }
-  if (q->dist == DistPlan::Exact) {
+  if (rows64(q)) {
     return fail(SPF_E_UNSUPPORTED, "64-bit distance rows");
   }
   const spf_graph* g = q->g;

@@ -7,10 +7,11 @@ One step = one pass of the hot path over one batch: every source of the
 fabric (9,976 single-source SPFs with ECMP next-hop sets), inputs (device CSR)
 resident in HBM before the timed region, outputs (distance rows + next-hop
 masks, ~1.4 GB) written to HBM.  Multi-GPU (one process per GPU, launched by
-torch.distributed.run): weak scaling — rank r computes the all-sources table
-of drain scenario r (rank 0: no drain; rank r > 0: one RSW drained), no
-collective on the data path.  `value` = SPFs of all ranks / max-over-ranks
-step time.
+torch.distributed.run; or --sharded on one GPU): STRONG scaling of the one
+9,976-source table through the engine's own multi-GPU path (spf_cluster /
+spf_table: contiguous source blocks per GPU, in-place RCCL all-gather of the
+rows and next-hop masks over xGMI).  `value` = 9,976 SPFs / max-over-ranks
+step time, gather included.
 
 Roofline: the dominant kernel of the step (the one with the larger average
 device time over the timed launches, HIP events on the engine's stream) is
@@ -403,13 +404,14 @@ def all_nodes_route_table(topo, device, reps=3):
         walls.append((time.perf_counter() - t0) * 1e3)
         spf.append(table.spf_ms)
         rt.append(table.route_ms)
-    V, P = table.num_nodes, table.num_prefixes
+    V, P, NL = table.num_nodes, table.num_prefixes, table.num_label_columns
     routes = table.count_routes()
     solver = E.SpfSolver("2-0-0", True, False)
     names = sorted(topo.names)
     bad = 0
     for node in ("2-0-0", names[len(names) // 2], names[-1]):
-        if table.routes(node) != solver.buildRouteDb(node, areas, ps)["unicast"]:
+        db = solver.buildRouteDb(node, areas, ps)
+        if table.routes(node) != db["unicast"] or table.mpls_routes(node) != db["mpls"]:
             bad += 1
     n_mat, us_mat = table.routes_timed("2-0-0")
     # network-wide route delta of one RSW drain (DecisionBenchmark's churn):
@@ -436,14 +438,15 @@ def all_nodes_route_table(topo, device, reps=3):
     lw = (deg + 63) // 64
     nbr = np.array([len(set(csr.col[csr.row_ptr[u]:csr.row_ptr[u + 1]].tolist())) for u in range(V)])
     nw = np.maximum(1, (nbr + 63) // 64)
-    alg = int(P * (12 * V + 8 * int(lw.sum()) + 8 * int(nw.sum())))
+    alg = int((P + NL) * (12 * V + 8 * int(lw.sum()) + 8 * int(nw.sum())))
     med = lambda x: sorted(x)[len(x) // 2]  # noqa: E731
     k_ms = med(rt)
     rt_traffic, rt_src = pmc_traffic_largest("spf_route_table_kernel")
     return {
-        "what": "unicast RouteDb of every node of the fabric at once: AllNodesRouteTable = all-sources "
-                "SPF + next hops, then spf_route_table_kernel (selectEcmpOpenr per node x prefix)",
-        "nodes": V, "prefixes": P, "routes": int(routes),
+        "what": "unicast + node-label MPLS RouteDb of every node of the fabric at once: "
+                "AllNodesRouteTable = all-sources SPF + next hops, then spf_route_table_kernel "
+                "(selectEcmpOpenr per node x prefix, getNextHopsWithMetric per node x labelled node)",
+        "nodes": V, "prefixes": P, "node_label_columns": NL, "routes": int(routes),
         "build_ms_median": round(med(walls), 2), "spf_ms_median": round(med(spf), 3),
         "route_kernel_ms_median": round(k_ms, 3),
         "route_kernel_roofline": {"bound": "hbm", "algorithmic_bytes": alg,
@@ -456,7 +459,7 @@ def all_nodes_route_table(topo, device, reps=3):
             "what": f"RSW {topo.names[rsw]} drained: table rebuilt + spf_route_table_diff_kernel = "
                     "getRouteDelta of every node at once",
             "table_rebuild_ms": round((t1 - t0) * 1e3, 2), "diff_ms": round((t2 - t1) * 1e3, 3),
-            "changed_routes": int(changed.sum()), "nodes_with_changes": int((changed > 0).sum()),
+            "changed_cells": int(changed.sum()), "nodes_with_changes": int((changed > 0).sum()),
             "parity_check": "ok" if delta_ok else "2-0-0 delta differs from getRouteDelta",
         },
     }
@@ -963,6 +966,83 @@ def wan_table_repair(topo, csr, sas, world, rank, local, dist):
             "events": events, "parity_check": check}
 
 
+def wide_plan(device=0):
+    """The wide plan (spf_wide_kernel) on the two shapes that used to send a
+    whole area to the one-thread-per-query literal replay:
+    the fabric with ONE metric-0 link (all 9,976 sources + next hops; the
+    literal replay timed on 64 sources beside it) and the 100k WAN with
+    metrics up to 10^6 (maxw * (V-1) >= 2^32; 2,048 distance rows).  Parity:
+    2 fabric rows against the DijkstraQ replay, 2 WAN rows against scipy."""
+    import numpy as np
+    import scipy.sparse as sp
+    import scipy.sparse.csgraph as cg
+
+    from openr_amd import abi
+    from openr_amd import topologies as TP
+    from oracle import spf_py
+
+    def timed(g, srcs, flags, reps=2):
+        q = g.query(srcs, flags)
+        best = None
+        for _ in range(reps):
+            q.run()
+            ms = q.elapsed_ms()
+            best = ms if best is None else min(best, ms)
+        return q, best
+
+    out = {}
+    topo = TP.fabric(10000)
+    k = len(topo.links) // 2
+    a, b, _, _ = topo.links[k]
+    topo.links[k] = (a, b, 0, 0)
+    csr = topo.csr()
+    g = abi.Graph(csr, device=device)
+    V = csr.num_nodes
+    srcs = np.arange(V, dtype=np.uint32)
+    q, ms = timed(g, srcs, abi.SPF_F_NEXTHOPS)
+    bad = 0
+    for i in (0, V // 2):
+        ref = spf_py.run_spf(csr, int(srcs[i]), True)
+        d = q.dist(i)
+        sets = q.nexthop_sets(i, int(srcs[i]))
+        bad += sum(int(d[v]) != m or (v != srcs[i] and sets[v] != nhs)
+                   for v, (m, nhs, _, _) in ref.items())
+    os.environ["OPENR_SPF_LITERAL"] = "1"
+    try:
+        ql, ms_l = timed(g, srcs[:64], abi.SPF_F_NEXTHOPS, reps=1)
+    finally:
+        del os.environ["OPENR_SPF_LITERAL"]
+    out["fabric_one_metric0_link"] = {
+        "sources": V, "kernel": q.kernel, "ms": round(ms, 2), "value": round(V / (ms / 1e3), 1),
+        "unit": "SPF/s", "literal_replay_ms_64_sources": round(ms_l, 2),
+        "parity_check": "ok" if bad == 0 else f"{bad} mismatches"}
+    q.close()
+    ql.close()
+    g.close()
+    topo = TP.wan(100000, 1000000, wmax=1_000_000)
+    csr = topo.csr()
+    g = abi.Graph(csr, device=device)
+    V = csr.num_nodes
+    S = 2048
+    srcs = np.arange(0, V, V // S, dtype=np.uint32)[:S]
+    q, ms = timed(g, srcs, 0)
+    A = sp.csr_matrix((csr.metric.astype(np.float64), csr.col, csr.row_ptr), shape=(V, V))
+    D = cg.dijkstra(A, indices=[int(srcs[0]), int(srcs[-1])])
+    bad = 0
+    for kk, i in enumerate((0, S - 1)):
+        ref = np.where(np.isfinite(D[kk]), D[kk], -1).astype(np.int64)
+        got = q.dist(i).astype(np.int64)
+        got[q.dist(i) == abi.SPF_UNREACHABLE] = -1
+        bad += int((ref != got).sum())
+    out["wan100k_metrics_to_1e6"] = {
+        "sources": S, "kernel": q.kernel, "ms": round(ms, 2), "value": round(S / (ms / 1e3), 1),
+        "unit": "SPF/s", "all_sources_s_est": round(ms / S * V / 1e3, 2),
+        "parity_check": "ok" if bad == 0 else f"{bad} mismatches"}
+    q.close()
+    g.close()
+    return out
+
+
 def cluster_for(world, rank, local, dist):
     """The engine's RCCL communicator for this rank (include/openr_spf.h
     spf_cluster_create_rank): rank 0 makes the id, torch.distributed hands
@@ -1294,6 +1374,10 @@ def main():
             out["publication_ingest"] = publication_ingest(topo)
         except Exception as e:
             out["publication_ingest"] = {"error": repr(e)}
+        try:
+            out["wide_plan"] = wide_plan(local)
+        except Exception as e:
+            out["wide_plan"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         one = cpu_baseline(topo, args.cpu_sample)
         t_per = 1.0 / one["value"] if one.get("value") else None

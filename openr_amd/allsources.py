@@ -139,6 +139,20 @@ def exchange_rows(table, local_rows, n: int, group=None):
     return int(keep.sum().item())
 
 
+def needs_64bit_rows(csr) -> bool:
+    """Host restatement of spf_graph_needs_exact for metric runs (the
+    engine's upload_weights rule): a metric-0 or wrapping (> 2^31 - 1) metric,
+    or maxw * (V - 1) >= 2^32.  Checked BEFORE any state changes."""
+    import numpy as np
+
+    m = np.asarray(csr.metric, dtype=np.uint64)
+    if m.size == 0:
+        return False
+    if (m == 0).any() or (m > np.uint64(0x7FFFFFFF)).any():
+        return True
+    return int(m.max()) * max(csr.num_nodes - 1, 0) >= 0xFFFFFFFF
+
+
 @dataclass
 class RepairRun:
     """One incremental table update on one rank (ShardedAllSources.update)."""
@@ -277,6 +291,10 @@ class ShardedAllSources:
             raise ValueError("node set changed: node ids are not shared, rebuild the table")
         out = RepairRun()
         multi = self.world > 1
+        if needs_64bit_rows(new_csr):
+            # refused before anything changes: the table, graph and query
+            # still describe the old topology and stay usable
+            raise abi.SpfError("all-sources tables need 32-bit sums (no metric 0 / 64-bit metrics)")
         if multi:
             dist.barrier(group=self.group)
         torch.cuda.synchronize(self.device)
@@ -312,8 +330,6 @@ class ShardedAllSources:
             self.graph.close()
             self.graph = graph
         self.csr = new_csr
-        if self.graph.needs_exact:
-            raise abi.SpfError("all-sources tables need 32-bit sums (no metric 0 / 64-bit metrics)")
         t2 = time.perf_counter()
         block = self.local_block()
         base = self.rank * self.cap if self.gather else 0

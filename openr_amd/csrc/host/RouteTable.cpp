@@ -3,6 +3,7 @@
 #include "RouteTable.h"
 
 #include <algorithm>
+#include <set>
 #include <stdexcept>
 
 #include "Engine.h"
@@ -93,6 +94,41 @@ AllNodesRouteTable::AllNodesRouteTable(
       annOff.push_back((uint32_t)ann.size());
     }
   }
+  // node-label columns (Decision.cpp:415-481): one pseudo-prefix per (valid
+  // label, owner in the graph), owners of a label by name; the cell of node
+  // s is getNextHopsWithMetric(s, {owner}) with LFA off
+  {
+    std::map<int32_t, std::vector<std::string>> byLabel;
+    for (const auto& [node, db] : ls.getAdjacencyDatabases()) {
+      if (db.nodeLabel == 0 || !isMplsLabelValid(db.nodeLabel) || !ids_.count(node)) {
+        continue;
+      }
+      byLabel[db.nodeLabel].push_back(node);
+    }
+    for (auto& [label, owners] : byLabel) {
+      std::sort(owners.begin(), owners.end());
+      auto& cols = labelCols_[label];
+      for (const auto& n : owners) {
+        cols.push_back((uint32_t)(prefixes_.size() + owners_.size()));
+        owners_.push_back(LabelOwner{label, ids_.at(n)});
+        ann.push_back(ids_.at(n));
+        annOff.push_back((uint32_t)ann.size());
+      }
+    }
+  }
+  // adjacency labels of every node (Decision.cpp:511-534), values copied
+  adjLabels_.resize(names_.size());
+  for (uint32_t i = 0; i < names_.size(); ++i) {
+    for (const auto& link : ls.linksFromNode(names_[i])) {
+      const int32_t label = link->getAdjLabelFromNode(names_[i]);
+      if (label == 0 || !isMplsLabelValid(label)) {
+        continue;
+      }
+      adjLabels_[i].push_back(AdjLabel{
+          label, link->getNhV6FromNode(names_[i]), link->getIfaceFromNode(names_[i]),
+          (int32_t)link->getMetricFromNode(names_[i]), link->getArea()});
+    }
+  }
   // own snapshot of the device graph: the table outlives LinkState changes
   spf_graph_desc d{};
   d.num_nodes = (uint32_t)eng.names.size();
@@ -134,8 +170,8 @@ AllNodesRouteTable::AllNodesRouteTable(
     cleanup("spf_query_run", s);
   }
   if ((s = spf_route_table_create(
-           query_, (uint32_t)prefixes_.size(), annOff.data(), ann.empty() ? nullptr : ann.data(),
-           &table_)) != SPF_OK) {
+           query_, (uint32_t)(prefixes_.size() + owners_.size()), annOff.data(),
+           ann.empty() ? nullptr : ann.data(), &table_)) != SPF_OK) {
     cleanup("spf_route_table_create", s);
   }
   if ((s = spf_route_table_run(table_)) != SPF_OK) {
@@ -156,17 +192,18 @@ AllNodesRouteTable::~AllNodesRouteTable() {
 
 uint64_t AllNodesRouteTable::countRoutes() const {
   uint64_t n = 0;
-  std::vector<uint32_t> metric(prefixes_.size()), best(prefixes_.size());
+  const size_t C = prefixes_.size() + owners_.size();
+  std::vector<uint32_t> metric(C), best(C);
   std::vector<uint64_t> links;
   for (uint32_t i = 0; i < names_.size(); ++i) {
     const int w = spf_route_table_link_words(table_, i);
-    links.resize(std::max<size_t>(1, prefixes_.size() * (size_t)std::max(w, 0)));
+    links.resize(std::max<size_t>(1, C * (size_t)std::max(w, 0)));
     if (int s = spf_route_table_fetch(table_, i, metric.data(), best.data(), links.data());
         s != SPF_OK) {
       tableFailure("spf_route_table_fetch", s);
     }
-    for (uint32_t m : metric) {
-      n += m != 0xFFFFFFFFu;
+    for (size_t p = 0; p < prefixes_.size(); ++p) {
+      n += metric[p] != 0xFFFFFFFFu;
     }
   }
   return n;
@@ -178,7 +215,7 @@ AllNodesRouteTable::Row AllNodesRouteTable::fetchRow(uint32_t i) const {
   if (w < 0) {
     tableFailure("spf_route_table_link_words", w);
   }
-  const size_t P = prefixes_.size();
+  const size_t P = prefixes_.size() + owners_.size();
   r.W = (size_t)w;
   r.metric.resize(P);
   r.best.resize(P);
@@ -234,9 +271,97 @@ std::unordered_map<thrift::IpPrefix, RibUnicastEntry> AllNodesRouteTable::routes
   return out;
 }
 
+std::optional<RibMplsEntry> AllNodesRouteTable::nodeLabelEntry(
+    uint32_t i, const Row& r, int32_t label) const {
+  auto lc = labelCols_.find(label);
+  if (lc == labelCols_.end()) {
+    return std::nullopt;
+  }
+  // the smallest-named owner that is this node (POP_AND_LOOKUP) or that it
+  // reaches (an unreachable owner inserts nothing and blocks nothing)
+  for (const uint32_t col : lc->second) {
+    const LabelOwner& o = owners_[col - prefixes_.size()];
+    if (o.id == i) {
+      thrift::NextHopThrift nh;
+      nh.address.addr = std::string(16, '\0'); // "::"
+      nh.area = area_;
+      nh.mplsAction = createMplsAction(thrift::MplsActionCode::POP_AND_LOOKUP);
+      return RibMplsEntry(label, {nh});
+    }
+    if (r.metric[col] == 0xFFFFFFFFu) {
+      continue;
+    }
+    const std::string& node = names_[i];
+    const std::string& owner = names_[o.id];
+    const uint32_t e0 = row_[i];
+    std::unordered_set<thrift::NextHopThrift> nhs;
+    for (size_t k = 0; k < r.W; ++k) {
+      uint64_t m = r.links[col * r.W + k];
+      while (m) {
+        const uint32_t j = (uint32_t)(k * 64 + __builtin_ctzll(m));
+        m &= m - 1;
+        const Link& l = *halfLink_[e0 + j];
+        const bool php = l.getOtherNodeName(node) == owner;
+        nhs.insert(createNextHop(
+            l.getNhV6FromNode(node), l.getIfaceFromNode(node), (int32_t)r.metric[col],
+            createMplsAction(
+                php ? thrift::MplsActionCode::PHP : thrift::MplsActionCode::SWAP,
+                php ? std::nullopt : std::optional<int32_t>(label)),
+            false, l.getArea()));
+      }
+    }
+    return RibMplsEntry(label, std::move(nhs));
+  }
+  return std::nullopt;
+}
+
+std::optional<RibMplsEntry> AllNodesRouteTable::mplsEntry(
+    uint32_t i, const Row& r, int32_t label) const {
+  if (auto e = nodeLabelEntry(i, r, label)) {
+    return e;
+  }
+  for (const AdjLabel& a : adjLabels_[i]) {
+    if (a.label == label) {
+      return RibMplsEntry(
+          label,
+          {createNextHop(a.nhV6, a.iface, a.metric, createMplsAction(thrift::MplsActionCode::PHP),
+                         false, a.area)});
+    }
+  }
+  return std::nullopt;
+}
+
+std::unordered_map<int32_t, RibMplsEntry> AllNodesRouteTable::mplsRoutes(
+    const std::string& node) const {
+  std::unordered_map<int32_t, RibMplsEntry> out;
+  auto it = ids_.find(node);
+  if (it == ids_.end()) {
+    return out;
+  }
+  const uint32_t i = it->second;
+  const Row r = owners_.empty() ? Row{} : fetchRow(i);
+  for (const auto& [label, cols] : labelCols_) {
+    if (auto e = nodeLabelEntry(i, r, label)) {
+      out.emplace(label, std::move(*e));
+    }
+  }
+  for (const AdjLabel& a : adjLabels_[i]) {
+    if (!out.count(a.label)) {
+      out.emplace(a.label, *mplsEntry(i, r, a.label));
+    }
+  }
+  return out;
+}
+
 std::vector<uint32_t> AllNodesRouteTable::diff(const AllNodesRouteTable& older) {
-  if (older.names_ != names_ || older.prefixes_ != prefixes_ || older.row_ != row_) {
-    throw std::invalid_argument("AllNodesRouteTable::diff: different nodes, prefixes or links");
+  bool sameOwners = older.owners_.size() == owners_.size();
+  for (size_t k = 0; sameOwners && k < owners_.size(); ++k) {
+    sameOwners = older.owners_[k].label == owners_[k].label && older.owners_[k].id == owners_[k].id;
+  }
+  if (older.names_ != names_ || older.prefixes_ != prefixes_ || older.row_ != row_ ||
+      !sameOwners) {
+    throw std::invalid_argument(
+        "AllNodesRouteTable::diff: different nodes, prefixes, node labels or links");
   }
   std::vector<uint32_t> changed(names_.size());
   if (int s = spf_route_table_diff(older.table_, table_, changed.data()); s != SPF_OK) {
@@ -247,7 +372,33 @@ std::vector<uint32_t> AllNodesRouteTable::diff(const AllNodesRouteTable& older) 
     tableFailure("spf_route_table_diff", s);
   }
   diffed_ = true;
+  older_ = &older;
   return changed;
+}
+
+std::pair<uint32_t, uint32_t> AllNodesRouteTable::changedSplit(const std::string& node) const {
+  if (!diffed_) {
+    throw std::logic_error("AllNodesRouteTable::changedSplit: no diff has run");
+  }
+  auto it = ids_.find(node);
+  const size_t P = prefixes_.size(), C = P + owners_.size();
+  if (it == ids_.end() || !C) {
+    return {0, 0};
+  }
+  std::vector<uint64_t> bits((C + 63) / 64);
+  if (int s = spf_route_table_changed(table_, it->second, bits.data()); s != SPF_OK) {
+    tableFailure("spf_route_table_changed", s);
+  }
+  uint32_t uni = 0, lab = 0;
+  for (size_t k = 0; k < bits.size(); ++k) {
+    uint64_t m = bits[k];
+    while (m) {
+      const size_t p = k * 64 + __builtin_ctzll(m);
+      m &= m - 1;
+      (p < P ? uni : lab) += 1;
+    }
+  }
+  return {uni, lab};
 }
 
 DecisionRouteUpdate AllNodesRouteTable::delta(const std::string& node) const {
@@ -256,31 +407,56 @@ DecisionRouteUpdate AllNodesRouteTable::delta(const std::string& node) const {
   if (!diffed_) {
     throw std::logic_error("AllNodesRouteTable::delta: no diff has run");
   }
-  if (it == ids_.end() || prefixes_.empty()) {
+  if (it == ids_.end()) {
     return u;
   }
-  const size_t P = prefixes_.size();
-  std::vector<uint64_t> bits((P + 63) / 64);
-  if (int s = spf_route_table_changed(table_, it->second, bits.data()); s != SPF_OK) {
-    tableFailure("spf_route_table_changed", s);
+  const uint32_t i = it->second;
+  const size_t P = prefixes_.size(), C = P + owners_.size();
+  std::vector<uint64_t> bits((C + 63) / 64);
+  if (C) {
+    if (int s = spf_route_table_changed(table_, i, bits.data()); s != SPF_OK) {
+      tableFailure("spf_route_table_changed", s);
+    }
   }
   bool any = false;
   for (uint64_t b : bits) {
     any |= b != 0;
   }
-  if (!any) {
+  // MPLS candidates: labels of changed label columns + adjacency labels
+  std::set<int32_t> labels;
+  for (const AdjLabel& a : adjLabels_[i]) {
+    labels.insert(a.label);
+  }
+  for (const AdjLabel& a : older_->adjLabels_[i]) {
+    labels.insert(a.label);
+  }
+  if (!any && labels.empty()) {
     return u;
   }
-  const Row r = fetchRow(it->second);
+  const Row r = C ? fetchRow(i) : Row{};
   for (size_t k = 0; k < bits.size(); ++k) {
     uint64_t m = bits[k];
     while (m) {
       const size_t p = k * 64 + __builtin_ctzll(m);
       m &= m - 1;
-      if (r.metric[p] == 0xFFFFFFFFu) {
+      if (p >= P) {
+        labels.insert(owners_[p - P].label);
+      } else if (r.metric[p] == 0xFFFFFFFFu) {
         u.unicastRoutesToDelete.push_back(prefixes_[p]);
       } else {
-        u.unicastRoutesToUpdate.push_back(materialise(node, it->second, r, p));
+        u.unicastRoutesToUpdate.push_back(materialise(node, i, r, p));
+      }
+    }
+  }
+  if (!labels.empty()) {
+    const Row o = C ? older_->fetchRow(i) : Row{};
+    for (const int32_t label : labels) {
+      auto ne = mplsEntry(i, r, label);
+      auto oe = older_->mplsEntry(i, o, label);
+      if (ne && (!oe || !(*oe == *ne))) {
+        u.mplsRoutesToUpdate.push_back(std::move(*ne));
+      } else if (!ne && oe) {
+        u.mplsRoutesToDelete.push_back(label);
       }
     }
   }

@@ -16,12 +16,23 @@
 // entries SpfSolver::buildRouteDb(node) produces for those prefixes
 // (tests/test_route_table.py).
 //
+// MPLS (Decision.cpp:415-534, this area, LFA off): every (node label, owner)
+// pair is one more column of the same kernel pass -- a pseudo-prefix
+// announced by the owner alone, so its cell is getNextHopsWithMetric(node,
+// {owner}) -- and mplsRoutes(node) turns the cells into POP_AND_LOOKUP (own
+// label) / PHP (next hop is the owner) / SWAP routes with the reference's
+// collision rule (the smallest-named owner the node itself is or reaches),
+// then adds the PHP routes of the node's adjacency labels (a node label
+// keeps its entry when an adjacency label repeats it).
+//
 // The table owns its device graph, query and rows (a snapshot): it stays
 // valid across later LinkState changes and answers for the topology it was
 // built from.
 #pragma once
 
+#include <map>
 #include <memory>
+#include <optional>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -50,15 +61,24 @@ class AllNodesRouteTable {
 
   // The unicast routes of `node` (empty if the node is not in the area).
   std::unordered_map<thrift::IpPrefix, RibUnicastEntry> routes(const std::string& node) const;
+  // The MPLS routes of `node` (node labels + adjacency labels, see above).
+  std::unordered_map<int32_t, RibMplsEntry> mplsRoutes(const std::string& node) const;
+  size_t numLabelColumns() const { return owners_.size(); }
 
   // Network-wide route delta against an older table over the same graph
-  // layout and prefixes (spf_route_table_diff): per node (id order, see
-  // nodeName) the number of prefixes whose route changed.  Throws
+  // layout, prefixes and node labels (spf_route_table_diff): per node (id
+  // order, see nodeName) the number of changed columns -- unicast prefixes
+  // and node-label columns (changedSplit separates them).  Throws
   // std::invalid_argument when the layouts differ.
   std::vector<uint32_t> diff(const AllNodesRouteTable& older);
-  // The unicast part of getRouteDelta(routes(node), older.routes(node))
+  // (changed unicast prefixes, changed node-label columns) of `node` from
+  // the last diff
+  std::pair<uint32_t, uint32_t> changedSplit(const std::string& node) const;
+  // getRouteDelta({routes, mplsRoutes}(node), the same of `older`)
   // (Decision.cpp:47-85) from the last diff: changed routes materialised,
-  // vanished ones deleted.
+  // vanished ones deleted.  MPLS candidates are the labels of changed label
+  // columns and the node's adjacency labels, compared entry by entry against
+  // `older` (which must outlive this call).
   DecisionRouteUpdate delta(const std::string& node) const;
   const std::string& nodeName(uint32_t id) const { return names_.at(id); }
 
@@ -70,6 +90,10 @@ class AllNodesRouteTable {
   };
   Row fetchRow(uint32_t i) const;
   RibUnicastEntry materialise(const std::string& node, uint32_t i, const Row& r, size_t p) const;
+  // the MPLS entry of `label` at node i: the node-label winner, else the
+  // first adjacency label of that value
+  std::optional<RibMplsEntry> mplsEntry(uint32_t i, const Row& r, int32_t label) const;
+  std::optional<RibMplsEntry> nodeLabelEntry(uint32_t i, const Row& r, int32_t label) const;
 
   struct Announcer {
     uint32_t id;
@@ -83,6 +107,23 @@ class AllNodesRouteTable {
   std::vector<std::shared_ptr<Link>> halfLink_; // half-edge -> Link
   std::vector<thrift::IpPrefix> prefixes_;
   std::vector<std::vector<Announcer>> announcers_;
+  // node-label columns: column prefixes_.size() + k is owners_[k]
+  struct LabelOwner {
+    int32_t label;
+    uint32_t id;
+  };
+  std::vector<LabelOwner> owners_;
+  std::map<int32_t, std::vector<uint32_t>> labelCols_; // label -> owner columns by name
+  // adjacency labels of every node, linksFromNode order (values copied)
+  struct AdjLabel {
+    int32_t label;
+    thrift::BinaryAddress nhV6;
+    std::string iface;
+    int32_t metric;
+    std::string area;
+  };
+  std::vector<std::vector<AdjLabel>> adjLabels_;
+  const AllNodesRouteTable* older_{nullptr};
   spf_graph* graph_{nullptr};
   spf_query* query_{nullptr};
   spf_route_table* table_{nullptr};

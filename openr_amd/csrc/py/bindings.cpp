@@ -349,8 +349,32 @@ PYBIND11_MODULE(_openr_spf, m) {
         py::object unicast = all["unicast"]; // owned before `all` goes away
         return unicast;
       })
-      .def("diff", &AllNodesRouteTable::diff, py::arg("older"))
+      .def_property_readonly("num_label_columns", &AllNodesRouteTable::numLabelColumns)
+      .def("mpls_routes", [](const AllNodesRouteTable& t, const std::string& node) {
+        DecisionRouteDb db;
+        db.mplsEntries = t.mplsRoutes(node);
+        py::dict all = routeDbToPy(db);
+        py::object mpls = all["mpls"];
+        return mpls;
+      })
+      .def("delta_mpls", [](const AllNodesRouteTable& t, const std::string& node) {
+        // (updated MPLS routes as mpls_routes() renders them, deleted labels)
+        const DecisionRouteUpdate u = t.delta(node);
+        DecisionRouteDb db;
+        for (const auto& e : u.mplsRoutesToUpdate) {
+          db.mplsEntries.emplace(e.label, e);
+        }
+        py::dict all = routeDbToPy(db);
+        py::object upd = all["mpls"];
+        py::list del;
+        for (int32_t l : u.mplsRoutesToDelete) {
+          del.append(l);
+        }
+        return py::make_tuple(upd, del);
+      })
+      .def("diff", &AllNodesRouteTable::diff, py::arg("older"), py::keep_alive<1, 2>())
       .def("node_name", &AllNodesRouteTable::nodeName)
+      .def("changed_split", &AllNodesRouteTable::changedSplit)
       .def("delta", [](const AllNodesRouteTable& t, const std::string& node) {
         // (updated unicast routes as routes() renders them, deleted prefixes)
         const DecisionRouteUpdate u = t.delta(node);

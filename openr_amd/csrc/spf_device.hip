@@ -462,7 +462,11 @@ struct DstepArgs {
   SsspArgs s;
   uint32_t shift = 5; // processing bucket width 2^shift
   uint32_t fshift = 0; // LDS bucket bytes quantise d >> fshift (fshift <= shift)
-  uint32_t noret = 0;  // bit 0: atomicMin without return, bit 1: coherent gathers
+  uint32_t noret = 0;  // bit 0: atomicMin without return, bit 1: coherent gathers,
+                       // bit 2: bucket bytes lowered at relaxation time (no
+                       // refresh reads), bit 3: no gather into unreached nodes
+                       // (packed pass only; skipping every gather would mark
+                       // unimproved nodes and ping-pong along tight edges)
   // OPENR_SPF_DSTEP_STATS: per-launch event counts of the push-only pass
   // (expansions, edges, bucket-filtered, gathers, atomics, improvements,
   // relax rounds, refreshed nodes)
@@ -813,6 +817,8 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
           nhrow[i] = 0;
         }
       }
+      // the row's initial stores land before any wave's atomics
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
         dist[src] = 0;
@@ -906,7 +912,13 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
             }
 #pragma unroll
             for (uint32_t j = 0; j < N; ++j) {
+              // bytes lowered in place (bit 2): 255 = nothing relaxed into v
+              // yet, so d[v] is unreached or about to drop to a value a racing
+              // lane is writing; atomicMin never raises, so skipping the read
+              // costs at most one redundant mark
+              const bool nogather = PK && (da.noret & 8u) && v[j] != kInf32 && bkt[v[j]] == 255;
               dv[j] = v[j] == kInf32 ? 0u
+                      : nogather ? kInf32
                       : ((PK || (LBK && (da.noret & 2u))) ? ld_coh(dist + v[j]) : dist[v[j]]);
             }
 #pragma unroll
@@ -921,7 +933,23 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
                 // a mark lost to a racing lower write only re-expands v once
                 // with its current distance (the refresh below reads it)
                 atomicMin(&dist[v[j]], c[j]);
-                atomicOr(&act[v[j] >> 5], 1u << (v[j] & 31));
+                // bytes lowered in place (bit 2): the improved node goes
+                // straight to the pending set (compaction only reads it after
+                // the phase barrier), no refresh pass over `act`
+                atomicOr(PK && (da.noret & 4u) ? &pend[v[j] >> 5] : &act[v[j] >> 5],
+                         1u << (v[j] & 31));
+                if constexpr (PK) {
+                  if (da.noret & 4u) {
+                    // d[v] <= c once the atomic lands, so bucket(c) is an
+                    // upper bound of v's bucket whatever order racing lanes
+                    // store in: the settled filter stays exact and sharpens
+                    // within the phase
+                    const uint8_t b = (uint8_t)min(c[j] >> shift, 254u);
+                    if (b < bkt[v[j]]) {
+                      bkt[v[j]] = b;
+                    }
+                  }
+                }
               } else if (atomicMin(&dist[v[j]], c[j]) > c[j]) {
                 st[5] += stats;
                 atomicOr(LBK ? &act[v[j] >> 5] : &pend[v[j] >> 5], 1u << (v[j] & 31));
@@ -978,12 +1006,15 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
             }
           }
         }
+        // non-returning atomics of every wave reach L2 before the next
+        // phase reads distances (a barrier alone drains LDS traffic only)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if constexpr (LBK) {
           // refresh straight from the marked words: each thread owns words
           // tid, tid + BS, ... (sole writer of those pend words in this
           // phase); four coherent distance reads in flight per step
-          for (uint32_t w = tid; w < nbw; w += BS) {
+          for (uint32_t w = tid; w < nbw && !(PK && (da.noret & 4u)); w += BS) {
             uint32_t b = act[w];
             if (!b) {
               continue;
@@ -3517,9 +3548,11 @@ void dstep_tune(spf_graph* g, spf_query* q, bool push_only) {
     fs = q->dstep_shift - std::min(fine, q->dstep_shift);
   }
   q->dstep_fshift = fs;
-  q->dstep_noret = 3;
+  // bits 2-3 (bytes lowered at relaxation time, no gather into unreached
+  // nodes): 14.9 -> 14.0 us/SPF on the 100k WAN (profiles/quick_wan.py)
+  q->dstep_noret = 15;
   if (const char* env = getenv("OPENR_SPF_DSTEP_NORET")) {
-    q->dstep_noret = (uint32_t)std::max(0, std::min(3, atoi(env)));
+    q->dstep_noret = (uint32_t)std::max(0, std::min(15, atoi(env)));
   }
   q->dstep_pack = g->cw_bits ? 2 : 0;
   if (const char* env = getenv("OPENR_SPF_DSTEP_PACK")) {
@@ -4277,7 +4310,7 @@ int launch_dstep_t(spf_query* q) {
   auto kern = q->dstep_lbk ? spf_dstep_kernel<WMAX, IGN, BS, true>
                            : spf_dstep_kernel<WMAX, IGN, BS, false>;
   if constexpr (WMAX == 0) {
-    if (q->dstep_lbk && d.cwvec && d.noret == 3) {
+    if (q->dstep_lbk && d.cwvec && (d.noret & 3u) == 3u) {
       kern = spf_dstep_kernel<WMAX, IGN, BS, true, false, true>;
     }
   }

@@ -155,3 +155,22 @@ def test_sharded_all_sources_engine(gpu_ready):
         for v in range(V):
             assert int(row[v]) == (ref[v][0] if v in ref else 0xFFFFFFFF)
     sas.close()
+
+
+def test_needs_64bit_rows_matches_engine_rule():
+    """ShardedAllSources.update refuses a topology that needs 64-bit rows
+    BEFORE touching its table / graph / query: the host rule
+    mirrors the engine's upload_weights (metric 0, a wrapping metric, or
+    maxw * (V - 1) >= 2^32)."""
+    from openr_amd import abi
+    from openr_amd.allsources import needs_64bit_rows
+
+    def csr(links, V=4):
+        return abi.Csr.from_links(V, links)
+
+    assert not needs_64bit_rows(csr([(0, 1, 1, 1), (1, 2, 5, 7), (2, 3, 9, 9)]))
+    assert needs_64bit_rows(csr([(0, 1, 0, 1), (1, 2, 5, 7)]))
+    assert needs_64bit_rows(csr([(0, 1, (1 << 64) - 5, 1)]))
+    big = (1 << 32) // 3 + 1  # maxw * (V - 1) >= 2^32 at V = 4
+    assert needs_64bit_rows(csr([(0, 1, big, 1)]))
+    assert not needs_64bit_rows(csr([(0, 1, big - 2, 1)]))

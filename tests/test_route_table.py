@@ -126,7 +126,9 @@ def test_route_table_diff_equals_route_delta(E, O, seed):
     for i, c in enumerate(changed):
         node = t1.node_name(i)
         upd, dele = t1.delta(node)
-        assert len(upd) + len(dele) == c, node
+        uni, lab = t1.changed_split(node)
+        assert uni + lab == c, node
+        assert len(upd) + len(dele) == uni, node
         # device delta == delta of the table rows == getRouteDelta of the host RouteDbs
         assert (upd, sorted(dele)) == _delta_py(t1.routes(node), t0.routes(node)), node
         after = osolver.buildRouteDb(node, oareas, ops)
@@ -134,4 +136,116 @@ def test_route_table_diff_equals_route_delta(E, O, seed):
         a = _ecmp_only(after["unicast"]) if after else {}
         assert (upd, sorted(dele)) == _delta_py(a, b), node
         total += c
+    assert total > 0
+
+
+def _label_network(seed, n_nodes=40, n_links=90):
+    """Random network whose node labels collide (17 distinct values over the
+    nodes), one invalid label, adjacency labels that repeat a node label and
+    each other (the emplace-first rules of Decision.cpp:483-534)."""
+    import random
+
+    names, adj_dbs, prefix_dbs = RZ.random_network(
+        1300 + seed, n_nodes=n_nodes, n_links=n_links, overload_prob=0.12, link_overload_prob=0.06
+    )
+    # no SR_MPLS prefixes: a KSP2 label stack through the node with the
+    # invalid label is the reference's fatal CHECK (createMplsAction)
+    for pdb in prefix_dbs:
+        pdb.prefixEntries = [e for e in pdb.prefixEntries if int(e.forwardingType) == 0]
+    rng = random.Random(seed)
+    for k, db in enumerate(adj_dbs["0"]):
+        db.nodeLabel = 101 + (k % 17)
+        if k == 3:
+            db.nodeLabel = 1 << 21  # invalid: skipped
+        for adj in db.adjacencies:
+            r = rng.random()
+            if r < 0.05:
+                adj.adjLabel = 101 + rng.randrange(17)  # repeats a node label
+            elif r < 0.1:
+                adj.adjLabel = 60000  # repeated adjacency label
+            elif r < 0.13:
+                adj.adjLabel = 0  # not SR
+    return names, adj_dbs, prefix_dbs
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_route_table_mpls_matches_build_route_db(E, O, seed):
+    """Every node's MPLS routes from the table (node-label columns of the same
+    device pass + adjacency labels) == the CPU oracle's buildRouteDb mpls
+    entries: POP_AND_LOOKUP / PHP / SWAP, label collisions (smallest-named
+    owner the node reaches), invalid labels, adjacency-label precedence."""
+    names, adj_dbs, prefix_dbs = _label_network(seed)
+    areas, ps = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    oareas, ops = RZ.load(O, adj_dbs, prefix_dbs, seed)
+    table = E.AllNodesRouteTable(areas, "0", ps, True)
+    assert table.num_label_columns > 17
+    solver = O.SpfSolver(names[0], True, False)
+    checked = 0
+    for node in names:
+        db = solver.buildRouteDb(node, oareas, ops)
+        got = table.mpls_routes(node)
+        if db is None:
+            assert got == {}, node
+            continue
+        assert got == db["mpls"], node
+        checked += len(got)
+    assert checked > 0
+
+
+def test_route_table_mpls_fabric(E, O):
+    from openr_amd import topologies as TP
+
+    topo = TP.fabric(600)
+    dbs = topo.adj_dbs(overloaded=[5, 77])
+    built = {}
+    for M in (E, O):
+        areas = M.AreaLinkStates()
+        ls = areas.add("0")
+        for db in dbs:
+            ls.updateAdjacencyDatabase(db)
+        ps = M.PrefixState()
+        for pdb in topo.prefix_dbs("0"):
+            ps.updatePrefixDatabase(pdb)
+        built[M] = (areas, ps)
+    table = E.AllNodesRouteTable(built[E][0], "0", built[E][1], True)
+    assert table.num_label_columns == topo.num_nodes
+    solver = O.SpfSolver("2-0-0", False, False)
+    for node in sorted(topo.names)[:: max(1, topo.num_nodes // 20)] + ["2-0-0"]:
+        db = solver.buildRouteDb(node, *built[O])
+        assert table.mpls_routes(node) == db["mpls"], node
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_route_table_delta_mpls_equals_route_delta(E, O, seed):
+    """Overload / metric / adjacency-label churn on the same links: the MPLS
+    part of the table delta of every node == getRouteDelta of the oracle's
+    RouteDbs before and after."""
+    import random
+
+    names, adj_dbs, prefix_dbs = _label_network(seed)
+    areas, ps = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    oareas, ops = RZ.load(O, adj_dbs, prefix_dbs, seed)
+    osolver = O.SpfSolver(names[0], True, False)
+    before = {n: osolver.buildRouteDb(n, oareas, ops) for n in names}
+    t0 = E.AllNodesRouteTable(areas, "0", ps, True)
+    rng = random.Random(seed)
+    for db in rng.sample(adj_dbs["0"], 4):
+        db.isOverloaded = not db.isOverloaded
+        if db.adjacencies:
+            db.adjacencies[0].metric += rng.randint(1, 9)
+            db.adjacencies[-1].adjLabel = 70000 + rng.randrange(50)
+    areas, ps = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    oareas, ops = RZ.load(O, adj_dbs, prefix_dbs, seed)
+    t1 = E.AllNodesRouteTable(areas, "0", ps, True)
+    t1.diff(t0)
+    total = 0
+    for node in names:
+        upd, dele = t1.delta_mpls(node)
+        after = osolver.buildRouteDb(node, oareas, ops)
+        b = before[node]["mpls"] if before.get(node) else {}
+        a = after["mpls"] if after else {}
+        want_upd = {k: v for k, v in a.items() if b.get(k) != v}
+        want_del = sorted(k for k in b if k not in a)
+        assert (upd, sorted(dele)) == (want_upd, want_del), node
+        total += len(upd) + len(dele)
     assert total > 0

@@ -489,6 +489,9 @@ struct DstepArgs {
   const uint32_t* cw = nullptr;
   uint32_t cwbits = 0;
   uint32_t cwvec = 0; // read cw as 16-byte chunks (padded to 4 edges)
+  // PK: sources beyond the first gridDim.x are claimed from this counter
+  // (zeroed per launch), so the workgroups finish together
+  uint32_t* qctr = nullptr;
 };
 
 
@@ -757,7 +760,18 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
   }
   __syncthreads();
 
-  for (uint32_t q = blockIdx.x; q < a.nq; q += gridDim.x) {
+  auto next_query = [&](uint32_t q) -> uint32_t {
+    if (!da.qctr) {
+      return q + gridDim.x;
+    }
+    __syncthreads(); // every lane has read ctl[kCtlWords - 2] of this query
+    if (tid == 0) {
+      ctl[kCtlWords - 2] = gridDim.x + atomicAdd(da.qctr, 1u);
+    }
+    __syncthreads();
+    return ctl[kCtlWords - 2];
+  };
+  for (uint32_t q = blockIdx.x; q < a.nq; q = next_query(q)) {
     if (a.skip && a.skip[q]) {
       continue; // uniform per block
     }
@@ -833,6 +847,11 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
 
     for (;;) {
       uint32_t qlen;
+      if (tid == 0) {
+        // next queue index a group claims (the first two per group are
+        // static); ordered before the relax loop by the compaction barriers
+        ctl[kCtlWords - 1] = 2 * ngrp;
+      }
       if constexpr (LBK) {
         qlen = compact_bucket<BS>(pend, BktLds{bkt}, cur, nbw, queue, ctl + 1);
       } else {
@@ -873,7 +892,10 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
           ndu = ld_coh(dist + nu);
         }
         uint32_t nnu = grp + ngrp < qlen ? queue[grp + ngrp] : kInf32;
-        for (uint32_t i = grp; i < qlen; i += ngrp) {
+        // PK: groups claim further nodes from an LDS counter (a group that
+        // drew light nodes takes more), so a phase ends with the last NODE,
+        // not with the heaviest static share of a group
+        for (uint32_t i = grp; PK ? nu != kInf32 : i < qlen; i += ngrp) {
           const uint32_t u = nu, du = ndu, beg = nbeg, end = nend;
           nu = nnu;
           if (nu != kInf32) {
@@ -881,7 +903,16 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
             nend = a.row[nu + 1];
             ndu = ld_coh(dist + nu);
           }
-          nnu = i + 2 * ngrp < qlen ? queue[i + 2 * ngrp] : kInf32;
+          if constexpr (PK) {
+            uint32_t nx = 0;
+            if (lg == 0) {
+              nx = atomicAdd(&ctl[kCtlWords - 1], 1u);
+            }
+            nx = (uint32_t)__shfl((int)nx, (int)((tid & 63u) & ~(G - 1u)), 64);
+            nnu = nx < qlen ? queue[nx] : kInf32;
+          } else {
+            nnu = i + 2 * ngrp < qlen ? queue[i + 2 * ngrp] : kInf32;
+          }
           if (u != src && !((a.trbits[u >> 5] >> (u & 31)) & 1u)) {
             continue; // overloaded: recorded but never transited
           }
@@ -1045,7 +1076,9 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
             }
           }
           st[6] += stats && tid == 0;
-          __syncthreads();
+          if (!(PK && (da.noret & 4u))) {
+            __syncthreads(); // refresh pass ran (uniform condition)
+          }
         }
         continue;
       }
@@ -3156,6 +3189,7 @@ struct spf_query {
   void* d_dist = nullptr;
   uint64_t* d_nh = nullptr;
   uint64_t* d_key = nullptr; // wide plan settle keys (SPF_F_ORDER)
+  uint32_t* d_qctr = nullptr; // dstep source-claim counter
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t evm = nullptr; // after the distance stage, before next hops
   bool ran = false;
@@ -3213,7 +3247,7 @@ void free_query(spf_query* q) {
         (void*)q->d_nh_off, q->d_dist, (void*)q->d_nh, (void*)q->d_row_of,
         (void*)q->d_lvl, (void*)q->d_flags, (void*)q->d_perm,
         (void*)q->d_slab, (void*)q->d_msd, (void*)q->d_base_of,
-        (void*)q->d_skip, (void*)q->d_key}) {
+        (void*)q->d_skip, (void*)q->d_key, (void*)q->d_qctr}) {
     if (p) {
       (void)hipFree(p);
     }
@@ -4312,6 +4346,13 @@ int launch_dstep_t(spf_query* q) {
   if constexpr (WMAX == 0) {
     if (q->dstep_lbk && d.cwvec && (d.noret & 3u) == 3u) {
       kern = spf_dstep_kernel<WMAX, IGN, BS, true, false, true>;
+      if (q->nq > q->grid) {
+        if (!q->d_qctr) {
+          HIP_TRY(hipMalloc((void**)&q->d_qctr, 4));
+        }
+        HIP_TRY(hipMemsetAsync(q->d_qctr, 0, 4, g->stream));
+        d.qctr = q->d_qctr;
+      }
     }
   }
   const size_t lds = q->lds_bytes;

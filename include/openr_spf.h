@@ -265,6 +265,14 @@ typedef struct spf_route_table spf_route_table;
 int spf_route_table_create(
     spf_query* q, uint32_t num_prefixes, const uint32_t* ann_offsets,
     const uint32_t* announcers, spf_route_table** out);
+/* flags of spf_route_table_create_ex */
+#define SPF_RT_LFA 0x1u /* loop-free alternates (computeLfaPaths_, Decision.cpp:1146-1175):
+                           every up link to a shortest-path or LFA next-hop node, each with
+                           its own metric (spf_route_table_fetch_link_metrics); needs every
+                           neighbour's row in the query (all sources) */
+int spf_route_table_create_ex(
+    spf_query* q, uint32_t num_prefixes, const uint32_t* ann_offsets,
+    const uint32_t* announcers, uint32_t flags, spf_route_table** out);
 int spf_route_table_destroy(spf_route_table* t);
 /* Enqueue spf_route_table_kernel after the query's last run (asynchronous,
  * graph stream). */
@@ -275,6 +283,11 @@ int spf_route_table_link_words(const spf_route_table* t, uint32_t i);
 /* Row i to host: metric[P], best[P], links[P * link_words(i)]. */
 int spf_route_table_fetch(
     spf_route_table* t, uint32_t i, uint32_t* metric, uint32_t* best, uint64_t* links);
+
+/* SPF_RT_LFA tables: the metric of every link of row i's source per prefix,
+ * out[p * deg + j] (deg = up links of the source in CSR order), set where bit
+ * j of the cell's link mask is; the diff compares these too. */
+int spf_route_table_fetch_link_metrics(spf_route_table* t, uint32_t i, uint32_t* out);
 
 /* Network-wide route delta: compare two tables built
  * over graphs with the same CSR layout (e.g. before and after an overload or

@@ -52,6 +52,8 @@ EXPORTED_SYMBOLS = (
     "spf_query_nexthops",
     "spf_query_order",
     "spf_query_order_keys",
+    "spf_route_table_create_ex",
+    "spf_route_table_fetch_link_metrics",
     "spf_query_device_rows",
     "spf_query_row_stride",
     "spf_query_fetch_rows",

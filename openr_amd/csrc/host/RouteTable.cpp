@@ -20,8 +20,8 @@ namespace {
 } // namespace
 
 AllNodesRouteTable::AllNodesRouteTable(
-    const LinkState& ls, const PrefixState& ps, bool enableV4)
-    : area_(ls.getArea()), enableV4_(enableV4) {
+    const LinkState& ls, const PrefixState& ps, bool enableV4, bool computeLfa)
+    : area_(ls.getArea()), enableV4_(enableV4), lfa_(computeLfa) {
   LinkState::Engine& eng = ls.engine();
   if (eng.exact) {
     throw std::invalid_argument(
@@ -169,9 +169,9 @@ AllNodesRouteTable::AllNodesRouteTable(
   if ((s = spf_query_run(query_)) != SPF_OK) {
     cleanup("spf_query_run", s);
   }
-  if ((s = spf_route_table_create(
+  if ((s = spf_route_table_create_ex(
            query_, (uint32_t)(prefixes_.size() + owners_.size()), annOff.data(),
-           ann.empty() ? nullptr : ann.data(), &table_)) != SPF_OK) {
+           ann.empty() ? nullptr : ann.data(), lfa_ ? SPF_RT_LFA : 0u, &table_)) != SPF_OK) {
     cleanup("spf_route_table_create", s);
   }
   if ((s = spf_route_table_run(table_)) != SPF_OK) {
@@ -224,6 +224,13 @@ AllNodesRouteTable::Row AllNodesRouteTable::fetchRow(uint32_t i) const {
       s != SPF_OK) {
     tableFailure("spf_route_table_fetch", s);
   }
+  if (lfa_) {
+    r.deg = row_[i + 1] - row_[i];
+    r.lmet.resize(std::max<size_t>(1, P * r.deg));
+    if (int s = spf_route_table_fetch_link_metrics(table_, i, r.lmet.data()); s != SPF_OK) {
+      tableFailure("spf_route_table_fetch_link_metrics", s);
+    }
+  }
   return r;
 }
 
@@ -240,7 +247,7 @@ RibUnicastEntry AllNodesRouteTable::materialise(
       const Link& l = *halfLink_[e0 + j];
       nhs.insert(createNextHop(
           isV4 ? l.getNhV4FromNode(node) : l.getNhV6FromNode(node), l.getIfaceFromNode(node),
-          (int32_t)r.metric[p], std::nullopt, false, l.getArea()));
+          (int32_t)r.linkMetric(p, j), std::nullopt, false, l.getArea()));
     }
   }
   const thrift::PrefixEntry* bestEntry = nullptr;
@@ -303,7 +310,7 @@ std::optional<RibMplsEntry> AllNodesRouteTable::nodeLabelEntry(
         const Link& l = *halfLink_[e0 + j];
         const bool php = l.getOtherNodeName(node) == owner;
         nhs.insert(createNextHop(
-            l.getNhV6FromNode(node), l.getIfaceFromNode(node), (int32_t)r.metric[col],
+            l.getNhV6FromNode(node), l.getIfaceFromNode(node), (int32_t)r.linkMetric(col, j),
             createMplsAction(
                 php ? thrift::MplsActionCode::PHP : thrift::MplsActionCode::SWAP,
                 php ? std::nullopt : std::optional<int32_t>(label)),
@@ -359,7 +366,7 @@ std::vector<uint32_t> AllNodesRouteTable::diff(const AllNodesRouteTable& older) 
     sameOwners = older.owners_[k].label == owners_[k].label && older.owners_[k].id == owners_[k].id;
   }
   if (older.names_ != names_ || older.prefixes_ != prefixes_ || older.row_ != row_ ||
-      !sameOwners) {
+      !sameOwners || older.lfa_ != lfa_) {
     throw std::invalid_argument(
         "AllNodesRouteTable::diff: different nodes, prefixes, node labels or links");
   }

@@ -46,7 +46,10 @@ namespace openr {
 
 class AllNodesRouteTable {
  public:
-  AllNodesRouteTable(const LinkState& ls, const PrefixState& ps, bool enableV4 = true);
+  // computeLfa: SpfSolver's computeLfaPaths (loop-free alternates as extra
+  // next hops with their own metrics, Decision.cpp:1146-1175)
+  AllNodesRouteTable(
+      const LinkState& ls, const PrefixState& ps, bool enableV4 = true, bool computeLfa = false);
   ~AllNodesRouteTable();
   AllNodesRouteTable(const AllNodesRouteTable&) = delete;
   AllNodesRouteTable& operator=(const AllNodesRouteTable&) = delete;
@@ -86,7 +89,12 @@ class AllNodesRouteTable {
   struct Row {
     std::vector<uint32_t> metric, best;
     std::vector<uint64_t> links;
-    size_t W = 0;
+    std::vector<uint32_t> lmet; // LFA: per-link metrics [cols][deg]
+    size_t W = 0, deg = 0;
+    // metric of link j of cell p (LFA: its own, else the cell's)
+    uint32_t linkMetric(size_t p, uint32_t j) const {
+      return lmet.empty() ? metric[p] : lmet[p * deg + j];
+    }
   };
   Row fetchRow(uint32_t i) const;
   RibUnicastEntry materialise(const std::string& node, uint32_t i, const Row& r, size_t p) const;
@@ -101,6 +109,7 @@ class AllNodesRouteTable {
   };
   std::string area_;
   bool enableV4_;
+  bool lfa_;
   std::vector<std::string> names_;
   std::unordered_map<std::string, uint32_t> ids_;
   std::vector<uint32_t> row_;                 // CSR row offsets of the snapshot

@@ -332,11 +332,11 @@ PYBIND11_MODULE(_openr_spf, m) {
 
   py::class_<AllNodesRouteTable>(m, "AllNodesRouteTable")
       .def(py::init([](const AreaMapHolder& areas, const std::string& area, const PrefixState& ps,
-                       bool enableV4) {
-             return std::make_unique<AllNodesRouteTable>(areas.map.at(area), ps, enableV4);
+                       bool enableV4, bool lfa) {
+             return std::make_unique<AllNodesRouteTable>(areas.map.at(area), ps, enableV4, lfa);
            }),
            py::arg("areas"), py::arg("area"), py::arg("prefix_state"), py::arg("enable_v4") = true,
-           py::keep_alive<1, 2>())
+           py::arg("lfa") = false, py::keep_alive<1, 2>())
       .def_property_readonly("num_nodes", &AllNodesRouteTable::numNodes)
       .def_property_readonly("num_prefixes", &AllNodesRouteTable::numPrefixes)
       .def_property_readonly("spf_ms", &AllNodesRouteTable::spfMs)

@@ -2938,13 +2938,19 @@ struct RouteTableArgs {
   uint32_t* metric_out; // [nq][P]
   uint32_t* best_out;   // [nq][P]
   uint64_t* link_out;
-  uint32_t Vp, P, nq;
+  // SPF_RT_LFA: query row of every node, per-link metrics [P][deg] per row
+  const int32_t* row_of;
+  const uint64_t* lm_off;
+  uint32_t* lmet_out;
+  uint32_t Vp, P, nq, lfa;
 };
 
 __global__ __launch_bounds__(256) void spf_route_table_kernel(RouteTableArgs a) {
   __shared__ uint32_t st_nbr[kRtStage];
   __shared__ uint32_t st_w[kRtStage];
   __shared__ uint32_t st_slot[kRtStage];
+  __shared__ uint32_t st_slotall[kRtStage]; // LFA: slot of every link
+  __shared__ uint32_t st_dns[kRtStage];     // LFA: d(nbr, s)
   for (uint32_t q = blockIdx.x; q < a.nq; q += gridDim.x) {
     const uint32_t s = a.src[q];
     const uint32_t* d = a.dist + (size_t)q * a.Vp;
@@ -2963,6 +2969,10 @@ __global__ __launch_bounds__(256) void spf_route_table_kernel(RouteTableArgs a) 
         st_nbr[j] = nb;
         st_w[j] = a.wout[e0 + j];
         st_slot[j] = a.wout[e0 + j] == d[nb] ? a.slot[e0 + j] : kInf32;
+        if (a.lfa) {
+          st_slotall[j] = a.slot[e0 + j];
+          st_dns[j] = a.dist[(size_t)a.row_of[nb] * a.Vp + s];
+        }
       }
     }
     __syncthreads();
@@ -2982,11 +2992,15 @@ __global__ __launch_bounds__(256) void spf_route_table_kernel(RouteTableArgs a) 
       }
       const size_t o = (size_t)q * a.P + p;
       uint64_t* lkp = lk + (size_t)p * WL;
+      uint32_t* lm = a.lfa ? a.lmet_out + a.lm_off[q] + (size_t)p * deg : nullptr;
       if (self || reach == 0) {
         a.metric_out[o] = kInf32;
         a.best_out[o] = kInf32;
         for (uint32_t k = 0; k < WL; ++k) {
           lkp[k] = 0;
+        }
+        for (uint32_t j = 0; lm && j < deg; ++j) {
+          lm[j] = kInf32;
         }
         continue;
       }
@@ -3019,6 +3033,42 @@ __global__ __launch_bounds__(256) void spf_route_table_kernel(RouteTableArgs a) 
               }
             }
           }
+        }
+        if (a.lfa) {
+          // getNextHopsWithMetric with LFA (Decision.cpp:1126-1175) and
+          // getNextHopsThrift without the shortest-metric filter: every up
+          // link to a next-hop node n, metric w(link) + value(n), value =
+          // mn - d(s, n) for shortest-path next hops, lowered to d(n, x) for
+          // any destination x with d(n, x) < mn + d(n, s) (RFC 5286)
+          for (uint32_t k = 0; k < WL; ++k) {
+            uint64_t out = 0;
+            const uint32_t j1 = min(deg, 64 * k + 64);
+            for (uint32_t j = 64 * k; j < j1; ++j) {
+              const uint32_t n = st_nbr[j], sl = st_slotall[j];
+              uint64_t w = 0;
+#pragma unroll
+              for (uint32_t kk = 0; kk < kRtMaskWords; ++kk) {
+                w = (sl >> 6) == kk ? m[kk] : w;
+              }
+              uint32_t v = ((w >> (sl & 63)) & 1ull) ? mn - d[n] : kInf32;
+              const uint32_t* rn = a.dist + (size_t)a.row_of[n] * a.Vp;
+              const uint64_t lim = (uint64_t)mn + st_dns[j];
+              for (uint32_t i = lo; i < hi; ++i) {
+                const uint32_t x = a.ann[i];
+                if (d[x] == kInf32 || (filt && !((a.trbits[x >> 5] >> (x & 31)) & 1u))) {
+                  continue;
+                }
+                const uint32_t dx = rn[x];
+                if (dx != kInf32 && (uint64_t)dx < lim) {
+                  v = min(v, dx);
+                }
+              }
+              lm[j] = v == kInf32 ? kInf32 : st_w[j] + v;
+              out |= (uint64_t)(v != kInf32) << (j & 63);
+            }
+            lkp[k] = out;
+          }
+          continue;
         }
         for (uint32_t k = 0; k < WL; ++k) {
           uint64_t out = 0;
@@ -3077,7 +3127,9 @@ __global__ __launch_bounds__(256) void spf_route_table_diff_kernel(
     const uint64_t* __restrict__ la, const uint32_t* __restrict__ mb,
     const uint32_t* __restrict__ bb, const uint64_t* __restrict__ lb,
     const uint64_t* __restrict__ lk_off, uint32_t P, uint32_t nq, uint32_t pw,
-    uint64_t* __restrict__ bits, uint32_t* __restrict__ count) {
+    uint64_t* __restrict__ bits, uint32_t* __restrict__ count,
+    const uint32_t* __restrict__ lma, const uint32_t* __restrict__ lmb,
+    const uint64_t* __restrict__ lm_off) {
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   for (uint32_t q = blockIdx.x; q < nq; q += gridDim.x) {
     const uint32_t WL = P ? (uint32_t)((lk_off[q + 1] - lk_off[q]) / P) : 0;
@@ -3092,6 +3144,13 @@ __global__ __launch_bounds__(256) void spf_route_table_diff_kernel(
         ch = ma[o] != mb[o] || ba[o] != bb[o];
         for (uint32_t k = 0; k < WL && !ch; ++k) {
           ch = la_q[(size_t)p * WL + k] != lb_q[(size_t)p * WL + k];
+        }
+        if (lma && !ch) { // LFA tables: per-link metrics too
+          const uint64_t deg = (lm_off[q + 1] - lm_off[q]) / P;
+          const size_t b0 = lm_off[q] + (size_t)p * deg;
+          for (uint64_t j = 0; j < deg && !ch; ++j) {
+            ch = lma[b0 + j] != lmb[b0 + j];
+          }
         }
       }
       const uint64_t word = __ballot(ch);
@@ -5424,6 +5483,12 @@ struct spf_route_table {
   // spf_route_table_diff against an older table: changed-cell bitmap
   uint64_t* d_diff = nullptr;
   uint32_t* d_count = nullptr;
+  // SPF_RT_LFA
+  bool lfa = false;
+  std::vector<uint64_t> lm_off; // [nq + 1] per-link metric offsets (P * deg)
+  uint64_t* d_lm_off = nullptr;
+  uint32_t* d_lmet = nullptr;
+  int32_t* d_row_of = nullptr;
 };
 
 namespace {
@@ -5433,7 +5498,8 @@ void free_route_table(spf_route_table* t) {
   }
   (void)hipSetDevice(t->q->g->device);
   for (void* p : {(void*)t->d_ann_off, (void*)t->d_ann, (void*)t->d_metric, (void*)t->d_best,
-                  (void*)t->d_lk_off, (void*)t->d_links, (void*)t->d_diff, (void*)t->d_count}) {
+                  (void*)t->d_lk_off, (void*)t->d_links, (void*)t->d_diff, (void*)t->d_count,
+                  (void*)t->d_lm_off, (void*)t->d_lmet, (void*)t->d_row_of}) {
     if (p) {
       (void)hipFree(p);
     }
@@ -5453,6 +5519,12 @@ extern "C" {
 int spf_route_table_create(
     spf_query* q, uint32_t num_prefixes, const uint32_t* ann_offsets,
     const uint32_t* announcers, spf_route_table** out) {
+  return spf_route_table_create_ex(q, num_prefixes, ann_offsets, announcers, 0, out);
+}
+
+int spf_route_table_create_ex(
+    spf_query* q, uint32_t num_prefixes, const uint32_t* ann_offsets,
+    const uint32_t* announcers, uint32_t flags, spf_route_table** out) {
   SPF_ABI_RANGE("spf_route_table_create");
   if (!q || !out || (num_prefixes && !ann_offsets)) {
     return fail(SPF_E_INVALID, "null argument");
@@ -5485,18 +5557,54 @@ int spf_route_table_create(
   std::vector<uint32_t> src(q->nq);
   HIP_TRY(hipSetDevice(g->device));
   HIP_TRY(hipMemcpy(src.data(), q->d_src, (size_t)q->nq * 4, hipMemcpyDeviceToHost));
+  const bool lfa = flags & SPF_RT_LFA;
+  std::vector<int32_t> row_of;
+  if (lfa) {
+    // every neighbour's row must be in the batch, every source on the
+    // staged register path (degree <= kRtStage, <= 256 distinct neighbours)
+    row_of.assign(g->V, -1);
+    for (uint32_t i = q->nq; i-- > 0;) {
+      row_of[src[i]] = (int32_t)i;
+    }
+    for (uint32_t i = 0; i < q->nq; ++i) {
+      const uint32_t s0 = src[i];
+      if (g->row[s0 + 1] - g->row[s0] > kRtStage || q->nh_w[i] > kRtMaskWords) {
+        return fail(SPF_E_UNSUPPORTED, "LFA route table: a source with more than 1024 links "
+                                       "or 256 neighbours");
+      }
+      for (uint32_t e = g->row[s0]; e < g->row[s0 + 1]; ++e) {
+        if (row_of[g->col[e]] < 0) {
+          return fail(SPF_E_UNSUPPORTED, "LFA route table: a neighbour's row is not in the batch");
+        }
+      }
+    }
+  }
   auto* t = new spf_route_table();
   t->q = q;
   t->P = num_prefixes;
+  t->lfa = lfa;
   t->lk_off.assign(q->nq + 1, 0);
+  t->lm_off.assign(q->nq + 1, 0);
   for (uint32_t i = 0; i < q->nq; ++i) {
     const uint32_t deg = g->row[src[i] + 1] - g->row[src[i]];
     t->lk_off[i + 1] = t->lk_off[i] + (uint64_t)num_prefixes * ((deg + 63) / 64);
+    t->lm_off[i + 1] = t->lm_off[i] + (lfa ? (uint64_t)num_prefixes * deg : 0);
   }
   auto bail = [&](int st) {
     free_route_table(t);
     return st;
   };
+  if (lfa) {
+    int s1 = SPF_OK;
+    if ((s1 = dev_upload(&t->d_row_of, row_of.data(), row_of.size())) ||
+        (s1 = dev_upload(&t->d_lm_off, t->lm_off.data(), t->lm_off.size()))) {
+      return bail(s1);
+    }
+    if (t->lm_off.back() &&
+        hipMalloc((void**)&t->d_lmet, t->lm_off.back() * 4) != hipSuccess) {
+      return bail(fail(SPF_E_NOMEM, "LFA link metrics"));
+    }
+  }
   const size_t cells = (size_t)q->nq * num_prefixes;
   std::vector<uint32_t> off(ann_offsets, ann_offsets + num_prefixes + 1);
   if (num_prefixes == 0) {
@@ -5558,6 +5666,10 @@ int spf_route_table_run(spf_route_table* t) {
     a.metric_out = t->d_metric;
     a.best_out = t->d_best;
     a.link_out = t->d_links;
+    a.row_of = t->d_row_of;
+    a.lm_off = t->d_lm_off;
+    a.lmet_out = t->d_lmet;
+    a.lfa = t->lfa ? 1u : 0u;
     a.Vp = q->Vp;
     a.P = t->P;
     a.nq = q->nq;
@@ -5614,6 +5726,31 @@ int spf_route_table_fetch(
   return SPF_OK;
 }
 
+int spf_route_table_fetch_link_metrics(spf_route_table* t, uint32_t i, uint32_t* out) {
+  SPF_ABI_RANGE("spf_route_table_fetch_link_metrics");
+  if (!t || i >= t->q->nq) {
+    return fail(SPF_E_INVALID, "bad argument");
+  }
+  if (!t->lfa) {
+    return fail(SPF_E_INVALID, "not an LFA table (every next hop has the cell metric)");
+  }
+  if (!t->ran) {
+    return fail(SPF_E_INVALID, "table has not run");
+  }
+  const uint64_t n = t->lm_off[i + 1] - t->lm_off[i];
+  if (!n) {
+    return SPF_OK;
+  }
+  if (!out) {
+    return fail(SPF_E_INVALID, "null out");
+  }
+  spf_graph* g = t->q->g;
+  HIP_TRY(hipSetDevice(g->device));
+  HIP_TRY(hipStreamSynchronize(g->stream));
+  HIP_TRY(hipMemcpy(out, t->d_lmet + t->lm_off[i], n * 4, hipMemcpyDeviceToHost));
+  return SPF_OK;
+}
+
 } // extern "C"
 
 extern "C" {
@@ -5629,7 +5766,8 @@ int spf_route_table_diff(spf_route_table* older, spf_route_table* newer, uint32_
   const spf_graph* ga = older->q->g;
   const spf_graph* gb = newer->q->g;
   if (ga->device != gb->device || older->q->nq != newer->q->nq || older->P != newer->P ||
-      older->lk_off != newer->lk_off || ga->row != gb->row || ga->col != gb->col) {
+      older->lk_off != newer->lk_off || ga->row != gb->row || ga->col != gb->col ||
+      older->lfa != newer->lfa) {
     return fail(SPF_E_UNSUPPORTED,
                 "tables differ in rows, prefixes or link layout (rematerialise instead)");
   }
@@ -5652,7 +5790,8 @@ int spf_route_table_diff(spf_route_table* older, spf_route_table* newer, uint32_
     hipLaunchKernelGGL(spf_route_table_diff_kernel, dim3(grid), dim3(256), 0, gb->stream,
                        older->d_metric, older->d_best, older->d_links, newer->d_metric,
                        newer->d_best, newer->d_links, newer->d_lk_off, P, nq, pw,
-                       newer->d_diff, newer->d_count);
+                       newer->d_diff, newer->d_count, older->d_lmet, newer->d_lmet,
+                       newer->d_lm_off);
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipMemcpyAsync(changed, newer->d_count, (size_t)nq * 4, hipMemcpyDeviceToHost,

@@ -249,3 +249,81 @@ def test_route_table_delta_mpls_equals_route_delta(E, O, seed):
         assert (upd, sorted(dele)) == (want_upd, want_del), node
         total += len(upd) + len(dele)
     assert total > 0
+
+
+@pytest.mark.parametrize("seed", range(5))
+@pytest.mark.parametrize("v4", [True, False])
+def test_route_table_lfa_matches_build_route_db(E, O, seed, v4):
+    """computeLfaPaths on (SpfSolver(..., computeLfaPaths=true)): every node's
+    unicast AND MPLS routes from the LFA table (shortest-path and
+    loop-free-alternate next hops, each with its own metric, RFC 5286
+    condition d(n, x) < d(s, x) + d(n, s)) == the CPU oracle's buildRouteDb."""
+    names, adj_dbs, prefix_dbs = RZ.random_network(
+        1700 + seed, n_nodes=40, n_links=100, overload_prob=0.12, link_overload_prob=0.05
+    )
+    areas, ps = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    oareas, ops = RZ.load(O, adj_dbs, prefix_dbs, seed)
+    table = E.AllNodesRouteTable(areas, "0", ps, v4, True)
+    solver = O.SpfSolver(names[0], v4, True)
+    checked = lfa_hops = 0
+    for node in names:
+        db = solver.buildRouteDb(node, oareas, ops)
+        got, mpls = table.routes(node), table.mpls_routes(node)
+        if db is None:
+            assert got == {} and mpls == {}, node
+            continue
+        want = _ecmp_only(db["unicast"])
+        assert got == want, node
+        assert mpls == db["mpls"], node
+        checked += len(got)
+    assert checked > 0
+    # LFA adds next hops somewhere: the LFA table differs from the plain one
+    plain = E.AllNodesRouteTable(areas, "0", ps, v4, False)
+    for node in names:
+        a, b = table.routes(node), plain.routes(node)
+        lfa_hops += sum(1 for k in a if a[k] != b.get(k))
+    assert lfa_hops > 0
+
+
+def test_route_table_lfa_fabric_and_delta(E, O):
+    """Fabric LFA table against the oracle on sampled nodes, then an RSW drain:
+    the LFA table delta of every node == getRouteDelta of the oracle."""
+    from openr_amd import topologies as TP
+
+    topo = TP.fabric(600)
+    dbs = topo.adj_dbs(overloaded=[5])
+
+    def load(M, dbs):
+        areas = M.AreaLinkStates()
+        ls = areas.add("0")
+        for db in dbs:
+            ls.updateAdjacencyDatabase(db)
+        ps = M.PrefixState()
+        for pdb in topo.prefix_dbs("0"):
+            ps.updatePrefixDatabase(pdb)
+        return areas, ps
+
+    ea, eps = load(E, dbs)
+    oa, ops = load(O, dbs)
+    t0 = E.AllNodesRouteTable(ea, "0", eps, False, True)
+    solver = O.SpfSolver("2-0-0", False, True)
+    sample = sorted(topo.names)[:: max(1, topo.num_nodes // 12)] + ["2-0-0"]
+    before = {}
+    for node in sample:
+        db = solver.buildRouteDb(node, oa, ops)
+        assert t0.routes(node) == db["unicast"], node
+        assert t0.mpls_routes(node) == db["mpls"], node
+        before[node] = db
+    rsw = next(i for i, n in enumerate(topo.names) if n.startswith("3-"))
+    dbs2 = topo.adj_dbs(overloaded=[5, rsw])
+    ea2, eps2 = load(E, dbs2)
+    oa2, ops2 = load(O, dbs2)
+    t1 = E.AllNodesRouteTable(ea2, "0", eps2, False, True)
+    t1.diff(t0)
+    for node in sample:
+        after = solver.buildRouteDb(node, oa2, ops2)
+        upd, dele = t1.delta(node)
+        assert (upd, sorted(dele)) == _delta_py(after["unicast"], before[node]["unicast"]), node
+        mu, md = t1.delta_mpls(node)
+        want_u = {k: v for k, v in after["mpls"].items() if before[node]["mpls"].get(k) != v}
+        assert (mu, sorted(md)) == (want_u, sorted(k for k in before[node]["mpls"] if k not in after["mpls"])), node

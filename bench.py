@@ -414,6 +414,18 @@ def all_nodes_route_table(topo, device, reps=3):
         if table.routes(node) != db["unicast"] or table.mpls_routes(node) != db["mpls"]:
             bad += 1
     n_mat, us_mat = table.routes_timed("2-0-0")
+    # the same table with loop-free alternates (SPF_RT_LFA): per-link metrics
+    # for every (node, column, up link) -- (P + labels) x E cells
+    lfa_walls, lfa_rt = [], []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        lt = E.AllNodesRouteTable(areas, "0", ps, True, True)
+        lfa_walls.append((time.perf_counter() - t0) * 1e3)
+        lfa_rt.append(lt.route_ms)
+    lsolver = E.SpfSolver("2-0-0", True, True)
+    ldb = lsolver.buildRouteDb("2-0-0", areas, ps)
+    lfa_ok = lt.routes("2-0-0") == ldb["unicast"] and lt.mpls_routes("2-0-0") == ldb["mpls"]
+    del lt
     # network-wide route delta of one RSW drain (DecisionBenchmark's churn):
     # rebuild the table on the drained topology, diff it on the device
     rsw = next(i for i, n in enumerate(topo.names) if n.startswith("3-"))
@@ -455,6 +467,10 @@ def all_nodes_route_table(topo, device, reps=3):
                                   "traffic": rt_traffic, "traffic_source": rt_src},
         "materialise_one_node_ms": round(us_mat / 1e3, 3), "materialised_routes": n_mat,
         "parity_check": "ok" if bad == 0 else f"{bad} nodes differ",
+        "lfa_table": {"what": "same table with loop-free alternates (SPF_RT_LFA, per-link metrics)",
+                      "build_ms_min": round(min(lfa_walls), 2),
+                      "route_kernel_ms_min": round(min(lfa_rt), 3),
+                      "parity_check": "ok" if lfa_ok else "2-0-0 differs from buildRouteDb(LFA)"},
         "drain_delta": {
             "what": f"RSW {topo.names[rsw]} drained: table rebuilt + spf_route_table_diff_kernel = "
                     "getRouteDelta of every node at once",

@@ -776,6 +776,101 @@ void pathLinksOf(
 
 } // namespace
 
+namespace {
+
+// OPENR_SPF_MEMO_SCREEN=0: drop the whole memo on every change (the
+// reference's behaviour, LinkState.cpp:712-715)
+bool memoScreenEnabled() {
+  static const bool on = [] {
+    const char* e = getenv("OPENR_SPF_MEMO_SCREEN");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
+// The table screen rule (spf_table_screen) on one host view:
+// the view keeps its distances AND next hops exactly unless some delta in
+// scope of its source is a tight edge that disappears or an edge at least as
+// good as the current distance of its head.
+bool screenHit(const SpfView& view, const std::vector<spf_edge_delta>& ds) {
+  const uint32_t s = view.src;
+  for (const auto& d : ds) {
+    if ((d.scope == SPF_SCOPE_TAIL_ONLY && s != d.tail) ||
+        (d.scope == SPF_SCOPE_NOT_TAIL && s == d.tail)) {
+      continue;
+    }
+    const uint64_t du = view.dist[d.tail];
+    if (du == SpfView::kUnreachable) {
+      continue;
+    }
+    const uint64_t dv = view.dist[d.head];
+    const uint64_t c = du + (view.useLinkMetric ? d.metric : 1ull);
+    if (d.kind == SPF_DELTA_REMOVED ? c == dv : (dv == SpfView::kUnreachable || c <= dv)) {
+      return true;
+    }
+  }
+  return false;
+}
+
+// keep the views of `memo` the deltas cannot touch, drop the rest
+template <class Map>
+void screenMemo(Map& memo, Map& into, const std::vector<spf_edge_delta>& ds) {
+  int64_t kept = 0, dropped = 0;
+  for (auto& [id, view] : memo) {
+    if (view && !screenHit(*view, ds)) {
+      into.emplace(id, std::move(view));
+      ++kept;
+    } else {
+      ++dropped;
+    }
+  }
+  memo.clear();
+  Counters::add("decision.spf_memo_kept", kept);
+  Counters::add("decision.spf_memo_dropped", dropped);
+}
+
+spf_graph_desc engineDesc(const LinkState::Engine& eng, const uint64_t* metric) {
+  spf_graph_desc d{};
+  d.num_nodes = (uint32_t)eng.names.size();
+  d.num_edges = (uint32_t)eng.col.size();
+  d.row_ptr = eng.row.data();
+  d.col = eng.col.data();
+  d.metric = metric;
+  d.link_id = eng.linkId.data();
+  d.rev = eng.rev.data();
+  d.node_overloaded = eng.overloaded.data();
+  d.num_links = (uint32_t)eng.links.size();
+  return d;
+}
+
+// Memo views of a retired engine that survive a structural change: same
+// nodes (ids = name ranks), deltas = spf_graph_diff of the two CSRs (unit
+// metrics for the hop-count memo), the screen rule per view.
+void adoptScreenedViews(LinkState::Engine& old, LinkState::Engine& neu) {
+  if (old.names != neu.names || old.exact || neu.exact) {
+    return;
+  }
+  for (int k = 0; k < 2; ++k) {
+    if (old.memo[k].empty()) {
+      continue;
+    }
+    const std::vector<uint64_t> onesOld(old.col.size(), 1), onesNew(neu.col.size(), 1);
+    const spf_graph_desc a = engineDesc(old, k ? old.metric.data() : onesOld.data());
+    const spf_graph_desc b = engineDesc(neu, k ? neu.metric.data() : onesNew.data());
+    uint32_t n = 0;
+    if (spf_graph_diff(&a, &b, nullptr, 0, &n) != SPF_OK) {
+      return;
+    }
+    std::vector<spf_edge_delta> ds(n);
+    if (n && spf_graph_diff(&a, &b, ds.data(), n, &n) != SPF_OK) {
+      return;
+    }
+    screenMemo(old.memo[k], neu.memo[k], ds);
+  }
+}
+
+} // namespace
+
 LinkState::Engine& LinkState::engine() const {
   if (!engine_) {
     engine_ = std::make_unique<Engine>();
@@ -788,6 +883,10 @@ LinkState::Engine& LinkState::engine() const {
         std::chrono::duration_cast<std::chrono::microseconds>(
             std::chrono::steady_clock::now() - t0)
             .count());
+    if (retired_) {
+      adoptScreenedViews(*retired_, *engine_);
+      retired_.reset();
+    }
   }
   return *engine_;
 }
@@ -828,6 +927,12 @@ void LinkState::clearMemo() const {
   spfResultsHops_.clear();
   kthPathResults_.clear();
   if (engine_) {
+    // a built engine retires with its memo: the next graph build keeps the
+    // views no edge delta can touch (selective invalidation, SURVEY §8(f)
+    // row 2); the reference drops them all (LinkState.cpp:712-715)
+    if (engine_->built && memoScreenEnabled()) {
+      retired_ = std::move(engine_);
+    }
     engine_.reset(); // drop the device graph: the topology changed
   }
 }
@@ -863,21 +968,53 @@ void LinkState::patchMemo(
     edges.push_back(e);
     metrics.push_back(link->getMetricFromNode(from));
   }
+  // edge deltas of this patch for the memo screen (metric memo / hop memo),
+  // taken before the host mirrors change: a metric change is its half-edge
+  // REMOVED at the old and ADDED at the new metric; a transit flip of x is
+  // every out-edge of x REMOVED / ADDED for sources other than x
+  std::vector<spf_edge_delta> dMetric, dHops;
+  std::unordered_map<uint32_t, uint64_t> newMetric;
+  for (size_t i = 0; i < edges.size(); ++i) {
+    newMetric[edges[i]] = metrics[i];
+    const uint32_t e = edges[i];
+    const uint32_t u = eng.col[eng.rev[e]], v = eng.col[e];
+    dMetric.push_back({u, v, eng.metric[e], SPF_DELTA_REMOVED, SPF_SCOPE_ALL});
+    dMetric.push_back({u, v, metrics[i], SPF_DELTA_ADDED, SPF_SCOPE_ALL});
+  }
   bool transit = false;
   for (const auto& n : transitNodes) {
     auto it = eng.ids.find(n);
     if (it == eng.ids.end()) {
       continue; // not in the graph: no transit bit to flip
     }
+    const uint32_t x = it->second;
     const uint8_t ov = isNodeOverloaded(n) ? 1 : 0;
-    transit |= eng.overloaded[it->second] != ov;
-    eng.overloaded[it->second] = ov;
+    if (eng.overloaded[x] != ov) {
+      transit = true;
+      const uint32_t kind = ov ? SPF_DELTA_REMOVED : SPF_DELTA_ADDED;
+      for (uint32_t e = eng.row[x]; e < eng.row[x + 1]; ++e) {
+        auto nm = newMetric.find(e);
+        const uint64_t w = ov || nm == newMetric.end() ? eng.metric[e] : nm->second;
+        dMetric.push_back({x, eng.col[e], w, kind, SPF_SCOPE_NOT_TAIL});
+        dHops.push_back({x, eng.col[e], 1, kind, SPF_SCOPE_NOT_TAIL});
+      }
+    }
+    eng.overloaded[x] = ov;
   }
   spfResultsMetric_.clear();
   spfResultsHops_.clear();
   kthPathResults_.clear();
+  if (memoScreenEnabled() && !eng.exact) {
+    for (int k = 0; k < 2; ++k) {
+      std::remove_reference_t<decltype(eng.memo[0])> keep;
+      screenMemo(eng.memo[k], keep, k ? dMetric : dHops);
+      eng.memo[k] = std::move(keep);
+    }
+  }
   for (auto& m : eng.memo) {
-    m.clear();
+    if (!memoScreenEnabled() || eng.exact) {
+      m.clear();
+    }
   }
   for (auto& m : eng.prefetched) {
     m.clear();

@@ -425,6 +425,9 @@ class LinkState {
   };
   mutable std::unique_ptr<KthFillLocks> kthFill_ = std::make_unique<KthFillLocks>();
   mutable std::unique_ptr<Engine> engine_;
+  // the engine a structural change retired: the next graph build keeps its
+  // memo views whose shortest-path DAG no edge delta touches (screenMemo)
+  mutable std::unique_ptr<Engine> retired_;
 };
 
 // Process-wide counters mirroring the fb303 keys the reference bumps

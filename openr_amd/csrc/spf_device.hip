@@ -2076,8 +2076,10 @@ __device__ __forceinline__ void nl_body(
 // dependent staging loads (nbrs -> row_of / transit) are paid once per
 // block instead of once per 1024-node chunk, and a block keeps up to
 // kNlUnroll independent row loads in flight per thread per chunk.
+// Sources with more than kNlStage distinct neighbours: the word-outer
+// order, staging 64 neighbours per word.
 template <bool WIDE>
-__device__ __forceinline__ void nl_body_multi(
+__device__ __forceinline__ void nl_body_multi_staged(
     const NhLevelsArgs& a, uint32_t q, uint32_t s, uint32_t c0, uint32_t c1,
     uint32_t* st_row, uint32_t* st_node) {
   const uint32_t Wm = a.nh_w[q];
@@ -2161,13 +2163,122 @@ __device__ __forceinline__ void nl_body_multi(
   }
 }
 
-// Write traffic: sources with Wm > 1 mask words store word w of 4 nodes per
-// thread in pass w, i.e. 8-byte pieces at a stride of 8*Wm bytes, so their
-// cache lines are written Wm times, partially (PMC: 1.31 GB written for
-// 0.95 GB of masks on the fabric).  Keeping all words of a node in registers
-// and writing each row once (r02 experiment) removed the excess writes but
-// cost occupancy (91 VGPRs) and time: 0.70 -> 0.82 ms in one launch, 0.92 ms
-// as two launches split by word count.  The per-word pass stays.
+template <bool WIDE>
+__device__ __forceinline__ void nl_body_multi(
+    const NhLevelsArgs& a, uint32_t q, uint32_t s, uint32_t c0, uint32_t c1,
+    uint32_t* st_row, uint32_t* st_node) {
+  const uint32_t Wm = a.nh_w[q];
+  uint64_t* nhrow = a.nh_out + a.nh_off[q];
+  const uint32_t none = WIDE ? kInf32 : 255u;
+  const uint64_t step = WIDE ? (uint64_t)a.scale : 1ull;
+  const uint32_t beg = a.nbr_off[s], n = a.nbr_off[s + 1] - beg;
+  // every neighbour staged once (n <= kNlStage; bigger sources take
+  // nl_body_multi_staged); the words of a chunk are then computed back to back,
+  // so the partial-line stores of a multi-word row meet in L2 before the
+  // line leaves (the word-outer order wrote each line Wm times), and the
+  // source's own level row is loaded once per chunk, not once per word
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < n; t += kNlThreads) {
+    const uint32_t f = a.nbrs[beg + t];
+    const uint32_t tf = (a.trbits[f >> 5] >> (f & 31)) & 1u;
+    st_row[t] = (uint32_t)a.row_of[f];
+    st_node[t] = f | (tf << 31);
+  }
+  __syncthreads();
+  for (uint32_t c = c0; c < c1; ++c) {
+    const uint32_t v0 = c * kNlChunk + threadIdx.x * kNlPer;
+    if (v0 >= a.V) {
+      break;
+    }
+    uint32_t ls[4];
+    nl_load<WIDE>(a, q, v0, ls);
+    bool live[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      live[i] = ls[i] != none && ls[i] != 0;
+    }
+    for (uint32_t w = 0; w < Wm; ++w) {
+      const uint32_t jlo = w * 64, jhi = min(n, jlo + 64);
+      uint64_t acc[4] = {0, 0, 0, 0};
+      uint32_t t = jlo;
+      for (; t + kNlUnroll <= jhi; t += kNlUnroll) {
+        uint32_t lf[kNlUnroll][4];
+#pragma unroll
+        for (uint32_t u = 0; u < kNlUnroll; ++u) {
+          nl_load<WIDE>(a, st_row[t + u], v0, lf[u]);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kNlUnroll; ++u) {
+          const uint32_t nd = st_node[t + u];
+          const uint32_t f = nd & 0x7FFFFFFFu;
+          const bool tf = nd >> 31;
+          const uint64_t bit = 1ull << ((t + u) & 63);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (live[i] && lf[u][i] != none && (uint64_t)lf[u][i] + step == (uint64_t)ls[i] &&
+                (tf || v0 + i == f)) {
+              acc[i] |= bit;
+            }
+          }
+        }
+      }
+      for (; t < jhi; ++t) {
+        uint32_t lf[4];
+        nl_load<WIDE>(a, st_row[t], v0, lf);
+        const uint32_t nd = st_node[t];
+        const uint32_t f = nd & 0x7FFFFFFFu;
+        const bool tf = nd >> 31;
+        const uint64_t bit = 1ull << (t & 63);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (live[i] && lf[i] != none && (uint64_t)lf[i] + step == (uint64_t)ls[i] &&
+              (tf || v0 + i == f)) {
+            acc[i] |= bit;
+          }
+        }
+      }
+      const uint32_t wv0 = v0 - 4 * (threadIdx.x & 63u); // first node of the wave
+      if (Wm == 1 && wv0 + 256 <= a.V) {
+        // each store instruction of the wave covers 1 KB contiguously: lane L
+        // writes nodes wv0 + 2L, +1 (store 0) and wv0 + 128 + 2L, +1 (store
+        // 1), fetched from the lanes that computed them (a lane's own four
+        // nodes at a 32-byte stride left every line half-written per store)
+        const uint32_t L = threadIdx.x & 63u;
+        const int a0 = (int)(L >> 1), a1 = (int)(32u + (L >> 1));
+        const bool odd = L & 1u;
+        auto sh = [](uint64_t x, int lane) {
+          return (uint64_t)__shfl((unsigned long long)x, lane, 64);
+        };
+        const uint64_t p0 = sh(acc[0], a0), p1 = sh(acc[1], a0), p2 = sh(acc[2], a0),
+                       p3 = sh(acc[3], a0);
+        const uint64_t r0 = sh(acc[0], a1), r1 = sh(acc[1], a1), r2 = sh(acc[2], a1),
+                       r3 = sh(acc[3], a1);
+        ulonglong2* o = reinterpret_cast<ulonglong2*>(nhrow + wv0);
+        o[L] = odd ? make_ulonglong2(p2, p3) : make_ulonglong2(p0, p1);
+        o[64 + L] = odd ? make_ulonglong2(r2, r3) : make_ulonglong2(r0, r1);
+      } else if (Wm == 1 && v0 + 4 <= a.V) {
+        ulonglong2* o = reinterpret_cast<ulonglong2*>(nhrow + v0);
+        o[0] = make_ulonglong2(acc[0], acc[1]);
+        o[1] = make_ulonglong2(acc[2], acc[3]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (v0 + i < a.V) {
+            nhrow[(size_t)(v0 + i) * Wm + w] = acc[i];
+          }
+        }
+      }
+    }
+  }
+}
+
+// Write traffic: a multi-word row (Wm > 1) is stored as 8-byte pieces at a
+// stride of 8*Wm bytes; with the word loop outside the chunk loop every line
+// was written Wm times, partially (PMC: 1.31 GB written for 0.95 GB of masks
+// on the fabric).  Keeping all words in registers (r02 experiment) cost
+// occupancy (91 VGPRs, 0.70 -> 0.82 ms); computing the words of a chunk back
+// to back (nl_body_multi) keeps one word of accumulators live and lets L2
+// merge the pieces of a line.
 // chunks of 1024 nodes swept by one block (measured on the fabric: 2 ->
 // 0.676 ms, 4 -> 0.682, 16 = whole rows -> 0.710; kNlUnroll 4 / 16 slower)
 #ifndef OPENR_NL_CPB
@@ -2175,7 +2286,9 @@ __device__ __forceinline__ void nl_body_multi(
 #endif
 constexpr uint32_t kNlChunksPerBlock = OPENR_NL_CPB;
 
-__global__ __launch_bounds__(kNlThreads) void spf_nh_levels_kernel(NhLevelsArgs a) {
+// six waves per SIMD (<= 80 VGPRs), as before the chunk-inner word loop
+__global__ __launch_bounds__(kNlThreads) __attribute__((amdgpu_waves_per_eu(6)))
+void spf_nh_levels_kernel(NhLevelsArgs a) {
   __shared__ uint32_t st_row[kNlStage];
   __shared__ uint32_t st_node[kNlStage];
   const uint32_t nchunks = (a.V + kNlChunk - 1) / kNlChunk;
@@ -2184,10 +2297,13 @@ __global__ __launch_bounds__(kNlThreads) void spf_nh_levels_kernel(NhLevelsArgs 
   const uint32_t s = a.src[q];
   const uint32_t c0 = cb * kNlChunksPerBlock;
   const uint32_t c1 = min(nchunks, c0 + kNlChunksPerBlock);
+  const bool big = a.nbr_off[s + 1] - a.nbr_off[s] > kNlStage; // uniform per block
   if (a.flags[0] != 0) {
-    nl_body_multi<true>(a, q, s, c0, c1, st_row, st_node);
+    big ? nl_body_multi_staged<true>(a, q, s, c0, c1, st_row, st_node)
+        : nl_body_multi<true>(a, q, s, c0, c1, st_row, st_node);
   } else {
-    nl_body_multi<false>(a, q, s, c0, c1, st_row, st_node);
+    big ? nl_body_multi_staged<false>(a, q, s, c0, c1, st_row, st_node)
+        : nl_body_multi<false>(a, q, s, c0, c1, st_row, st_node);
   }
 }
 

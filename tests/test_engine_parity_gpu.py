@@ -197,3 +197,54 @@ def test_incremental_updates(mods, seed):
         me = names[step % len(names)]
         assert es.buildRouteDb(me, ea, ep) == os_.buildRouteDb(me, oa, op), (step, me)
     assert E.get_counters().get("decision.graph_patches", 0) > 0
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_selective_memo_invalidation(mods, seed):
+    """SURVEY §8(f) row 2 in LinkState: a topology change keeps the memoized
+    SPF views whose shortest-path DAG no edge delta touches (the table screen
+    rule on the host rows) instead of dropping the whole memo
+    (LinkState.cpp:712-715).  Every node's metric AND hop-count SpfResult is
+    memoized, then drain toggles, metric changes, link overloads (the CSR
+    changes: the retired engine's views are screened against spf_graph_diff)
+    and link additions are applied; after each, EVERY node's SpfResult
+    (distances, next hops, pathLinks order) and a RouteDb equal the oracle's,
+    and views were both kept and dropped."""
+    import random
+
+    E, O = mods
+    names, adj_dbs, prefix_dbs = RZ.random_network(
+        2100 + seed, n_nodes=36, n_links=80, overload_prob=0.05, link_overload_prob=0.02
+    )
+    ea, ep = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    oa, op = RZ.load(O, adj_dbs, prefix_dbs, seed)
+    es = E.SpfSolver(names[0], True, False)
+    os_ = O.SpfSolver(names[0], True, False)
+    rng = random.Random(seed)
+    dbs = [copy.deepcopy(d) for d in adj_dbs["0"]]
+    E.reset_counters()
+    for step in range(10):
+        for node in names:  # warm the whole memo
+            if ea["0"].hasNode(node):
+                ea["0"].getSpfResult(node, True)
+                ea["0"].getSpfResult(node, False)
+        db = rng.choice(dbs)
+        kind = rng.random()
+        if kind < 0.35 or not db.adjacencies:
+            db.isOverloaded = not db.isOverloaded
+        elif kind < 0.7:
+            adj = rng.choice(db.adjacencies)
+            adj.metric = rng.randint(1, 20)
+        else:
+            adj = rng.choice(db.adjacencies)
+            adj.isOverloaded = not adj.isOverloaded
+        assert ea["0"].updateAdjacencyDatabase(db) == oa["0"].updateAdjacencyDatabase(db)
+        for node in names:
+            if ea["0"].hasNode(node):
+                _spf_equal(ea["0"], oa["0"], node, True)
+                _spf_equal(ea["0"], oa["0"], node, False)
+        me = names[step % len(names)]
+        assert es.buildRouteDb(me, ea, ep) == os_.buildRouteDb(me, oa, op), (step, me)
+    c = E.get_counters()
+    assert c.get("decision.spf_memo_kept", 0) > 0
+    assert c.get("decision.spf_memo_dropped", 0) > 0

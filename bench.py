@@ -133,6 +133,21 @@ def pmc_traffic_largest(kernel_name):
     return None, None
 
 
+def pmc_traffic_smallest(kernel_name):
+    """HBM bytes of the smallest dispatch of `kernel_name` in the committed
+    PMC passes (a kernel launched in two modes: the plain one)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        k = d.get("kernels", {}).get(kernel_name)
+        if k and "hbm_bytes_smallest_launch" in k:
+            return int(k["hbm_bytes_smallest_launch"]), os.path.relpath(f, ROOT)
+    return None, None
+
+
 def host_cores():
     """Host threads this process may use: the GPU box gives one GPU's share
     (16) of a larger machine whose nproc shows every CPU."""
@@ -453,7 +468,8 @@ def all_nodes_route_table(topo, device, reps=3):
     alg = int((P + NL) * (12 * V + 8 * int(lw.sum()) + 8 * int(nw.sum())))
     med = lambda x: sorted(x)[len(x) // 2]  # noqa: E731
     k_ms = med(rt)
-    rt_traffic, rt_src = pmc_traffic_largest("spf_route_table_kernel")
+    # the plain (non-LFA) launches are the smallest of the profiled ones
+    rt_traffic, rt_src = pmc_traffic_smallest("spf_route_table_kernel")
     return {
         "what": "unicast + node-label MPLS RouteDb of every node of the fabric at once: "
                 "AllNodesRouteTable = all-sources SPF + next hops, then spf_route_table_kernel "

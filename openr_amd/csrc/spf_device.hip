@@ -42,6 +42,7 @@
 #include <functional>
 #include <queue>
 #include <string>
+#include <mutex>
 #include <unordered_map>
 #include <vector>
 
@@ -3379,6 +3380,91 @@ struct spf_query {
 
 namespace {
 
+// Process-wide caching allocator for the per-query buffers: a RouteDb build
+// creates and destroys a few small queries (the node, its LFA neighbours,
+// KSP2 second passes), and hipMalloc / hipFree per buffer cost more than
+// the SPFs of a small area.  Blocks are power-of-two size classes per
+// device; blocks above kPoolMaxBlock (all-sources tables) and anything past
+// kPoolMaxCached cached bytes go straight back to the driver.
+constexpr size_t kPoolMaxBlock = 64ull << 20;
+constexpr size_t kPoolMaxCached = 1ull << 30;
+struct DevPool {
+  std::mutex mu;
+  std::unordered_map<size_t, std::vector<void*>> free;
+  std::unordered_map<void*, size_t> cls; // live pool blocks -> size class
+  size_t cached = 0;
+};
+DevPool& dev_pool() {
+  static std::mutex m;
+  static std::unordered_map<int, std::unique_ptr<DevPool>> pools;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> g(m);
+  auto& p = pools[dev];
+  if (!p) {
+    p = std::make_unique<DevPool>();
+  }
+  return *p;
+}
+hipError_t pool_malloc(void** p, size_t n) {
+  if (n > kPoolMaxBlock) {
+    return hipMalloc(p, n);
+  }
+  size_t c = 256;
+  while (c < n) {
+    c <<= 1;
+  }
+  DevPool& P = dev_pool();
+  {
+    std::lock_guard<std::mutex> g(P.mu);
+    auto& v = P.free[c];
+    if (!v.empty()) {
+      *p = v.back();
+      v.pop_back();
+      P.cached -= c;
+      P.cls[*p] = c;
+      return hipSuccess;
+    }
+  }
+  const hipError_t e = hipMalloc(p, c);
+  if (e == hipSuccess) {
+    std::lock_guard<std::mutex> g(P.mu);
+    P.cls[*p] = c;
+  }
+  return e;
+}
+// callers make sure no queued work still reads `p`
+void pool_free(void* p) {
+  if (!p) {
+    return;
+  }
+  DevPool& P = dev_pool();
+  {
+    std::lock_guard<std::mutex> g(P.mu);
+    auto it = P.cls.find(p);
+    if (it != P.cls.end()) {
+      const size_t c = it->second;
+      P.cls.erase(it);
+      if (P.cached + c <= kPoolMaxCached) {
+        P.free[c].push_back(p);
+        P.cached += c;
+        return;
+      }
+    }
+  }
+  (void)hipFree(p);
+}
+template <typename T>
+int dev_upload_q(T** dst, const T* src, size_t n) {
+  *dst = nullptr;
+  if (n == 0) {
+    return SPF_OK;
+  }
+  HIP_TRY(pool_malloc((void**)dst, n * sizeof(T)));
+  HIP_TRY(hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice));
+  return SPF_OK;
+}
+
 template <typename T>
 int dev_upload(T** dst, const T* src, size_t n) {
   *dst = nullptr;
@@ -3416,16 +3502,16 @@ void free_query(spf_query* q) {
     return;
   }
   (void)hipSetDevice(q->g->device);
+  // the buffers go back to the pool: nothing queued may still use them
+  (void)hipStreamSynchronize(q->g->stream);
   for (void* p :
        {(void*)q->d_src, (void*)q->d_ign_off, (void*)q->d_ign,
         (void*)q->d_nh_w, (void*)q->d_order, (void*)q->d_scratch,
         (void*)q->d_nh_off, q->d_dist, (void*)q->d_nh, (void*)q->d_row_of,
         (void*)q->d_lvl, (void*)q->d_flags, (void*)q->d_perm,
         (void*)q->d_slab, (void*)q->d_msd, (void*)q->d_base_of,
-        (void*)q->d_skip, (void*)q->d_key, (void*)q->d_qctr}) {
-    if (p) {
-      (void)hipFree(p);
-    }
+        (void*)q->d_skip, (void*)q->d_key, (void*)q->d_qctr, (void*)q->d_scatter}) {
+    pool_free(p);
   }
   if (q->base) {
     free_query(q->base);
@@ -4299,67 +4385,67 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     return bail(fail(SPF_E_DEVICE, "hipSetDevice failed"));
   }
   int s = SPF_OK;
-  if ((s = dev_upload(&q->d_src, desc->sources, nq))) {
+  if ((s = dev_upload_q(&q->d_src, desc->sources, nq))) {
     return bail(s);
   }
   if (q->dist == DistPlan::MsBfs) {
-    if (hipMalloc((void**)&q->d_lvl, (size_t)nq * q->Vp8) != hipSuccess ||
-        hipMalloc((void**)&q->d_flags, 16) != hipSuccess) {
+    if (pool_malloc((void**)&q->d_lvl, (size_t)nq * q->Vp8) != hipSuccess ||
+        pool_malloc((void**)&q->d_flags, 16) != hipSuccess) {
       return bail(fail(SPF_E_NOMEM, "level rows"));
     }
   }
   if (has_ign) {
     const uint32_t total = desc->ignore_offsets[nq];
-    if ((s = dev_upload(&q->d_ign_off, desc->ignore_offsets, nq + 1)) ||
-        (s = dev_upload(&q->d_ign, desc->ignore_links, total))) {
+    if ((s = dev_upload_q(&q->d_ign_off, desc->ignore_offsets, nq + 1)) ||
+        (s = dev_upload_q(&q->d_ign, desc->ignore_links, total))) {
       return bail(s);
     }
   }
   if (want_nh) {
-    if ((s = dev_upload(&q->d_nh_off, q->nh_off.data(), nq)) ||
-        (s = dev_upload(&q->d_nh_w, q->nh_w.data(), nq))) {
+    if ((s = dev_upload_q(&q->d_nh_off, q->nh_off.data(), nq)) ||
+        (s = dev_upload_q(&q->d_nh_w, q->nh_w.data(), nq))) {
       return bail(s);
     }
     if (q->nh_total &&
-        hipMalloc((void**)&q->d_nh, q->nh_total * 8) != hipSuccess) {
+        pool_malloc((void**)&q->d_nh, q->nh_total * 8) != hipSuccess) {
       return bail(fail(SPF_E_NOMEM, "next-hop rows"));
     }
   }
-  if (!row_of.empty() && (s = dev_upload(&q->d_row_of, row_of.data(), V))) {
+  if (!row_of.empty() && (s = dev_upload_q(&q->d_row_of, row_of.data(), V))) {
     return bail(s);
   }
   const bool ex = q->dist == DistPlan::Exact;
   const bool wide = q->dist == DistPlan::Wide;
   const size_t dist_bytes = (ex || wide) ? (size_t)nq * V * 8 : (size_t)nq * q->Vp * 4;
-  if (dist_bytes && hipMalloc(&q->d_dist, dist_bytes) != hipSuccess) {
+  if (dist_bytes && pool_malloc(&q->d_dist, dist_bytes) != hipSuccess) {
     return bail(fail(SPF_E_NOMEM, "distance rows"));
   }
   if ((q->dist == DistPlan::SsspGmem || q->dist == DistPlan::BfsGmem ||
        q->dist == DistPlan::Dstep) &&
-      hipMalloc((void**)&q->d_scratch, (size_t)q->grid * V * 4) !=
+      pool_malloc((void**)&q->d_scratch, (size_t)q->grid * V * 4) !=
           hipSuccess) {
     return bail(fail(SPF_E_NOMEM, "queue scratch"));
   }
   if (q->dist == DistPlan::MsDstep) {
     const size_t gv = (size_t)q->grid * V;
-    if ((s = dev_upload(&q->d_perm, msd_perm.data(), msd_perm.size()))) {
+    if ((s = dev_upload_q(&q->d_perm, msd_perm.data(), msd_perm.size()))) {
       return bail(s);
     }
-    if (hipMalloc((void**)&q->d_slab, gv * kMsdK * 4) != hipSuccess ||
-        hipMalloc((void**)&q->d_msd, gv * 4 * 4) != hipSuccess) {
+    if (pool_malloc((void**)&q->d_slab, gv * kMsdK * 4) != hipSuccess ||
+        pool_malloc((void**)&q->d_msd, gv * 4 * 4) != hipSuccess) {
       return bail(fail(SPF_E_NOMEM, "multi-source slab"));
     }
   }
   if (ex && (size_t)nq * V) {
-    if (hipMalloc((void**)&q->d_scratch, (size_t)nq * V * 8) != hipSuccess ||
-        hipMalloc((void**)&q->d_order, (size_t)nq * V * 4) != hipSuccess) {
+    if (pool_malloc((void**)&q->d_scratch, (size_t)nq * V * 8) != hipSuccess ||
+        pool_malloc((void**)&q->d_order, (size_t)nq * V * 4) != hipSuccess) {
       return bail(fail(SPF_E_NOMEM, "exact-kernel scratch"));
     }
   }
   if (wide && (size_t)nq * V) {
-    if (hipMalloc((void**)&q->d_scratch, (size_t)q->grid * wide_stride(V, g->nbw) * 4) !=
+    if (pool_malloc((void**)&q->d_scratch, (size_t)q->grid * wide_stride(V, g->nbw) * 4) !=
             hipSuccess ||
-        (want_order && hipMalloc((void**)&q->d_key, (size_t)nq * V * 8) != hipSuccess)) {
+        (want_order && pool_malloc((void**)&q->d_key, (size_t)nq * V * 8) != hipSuccess)) {
       return bail(fail(SPF_E_NOMEM, "wide-plan scratch"));
     }
   }
@@ -4386,10 +4472,10 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       bd.sources = base_srcs.data();
       bd.flags = desc->flags;
       if ((s = spf_query_create(g, &bd, &q->base)) ||
-          (s = dev_upload(&q->d_base_of, base_of.data(), nq))) {
+          (s = dev_upload_q(&q->d_base_of, base_of.data(), nq))) {
         return bail(s);
       }
-      if (hipMalloc((void**)&q->d_skip, (size_t)nq * 4) != hipSuccess) {
+      if (pool_malloc((void**)&q->d_skip, (size_t)nq * 4) != hipSuccess) {
         return bail(fail(SPF_E_NOMEM, "what-if screen flags"));
       }
     }
@@ -4523,7 +4609,7 @@ int launch_dstep_t(spf_query* q) {
       kern = spf_dstep_kernel<WMAX, IGN, BS, true, false, true>;
       if (q->nq > q->grid) {
         if (!q->d_qctr) {
-          HIP_TRY(hipMalloc((void**)&q->d_qctr, 4));
+          HIP_TRY(pool_malloc((void**)&q->d_qctr, 4));
         }
         HIP_TRY(hipMemsetAsync(q->d_qctr, 0, 4, g->stream));
         d.qctr = q->d_qctr;
@@ -5433,7 +5519,7 @@ int spf_query_scatter_rows(
   }
   HIP_TRY(hipSetDevice(q->g->device));
   if (!q->d_scatter) {
-    HIP_TRY(hipMalloc((void**)&q->d_scatter, (size_t)q->nq * 4));
+    HIP_TRY(pool_malloc((void**)&q->d_scatter, (size_t)q->nq * 4));
   }
   // the previous scatter of this query may still read d_scatter
   HIP_TRY(hipStreamSynchronize(q->g->stream));

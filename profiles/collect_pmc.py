@@ -67,6 +67,9 @@ def main(fetch_dir, write_dir, out):
             # the largest dispatch (kernels launched at several sizes, e.g.
             # a warm-up batch before the measured one)
             ent["hbm_bytes_largest_launch"] = int(round((2.0 * max(f) + max(w)) * 1024.0))
+            # and the smallest (a kernel run in two modes, e.g. the route
+            # table with and without LFA columns)
+            ent["hbm_bytes_smallest_launch"] = int(round((2.0 * min(f) + min(w)) * 1024.0))
             ent["dispatches"] = len(f)
         kernels[k] = ent
     json.dump(

@@ -240,6 +240,18 @@ int spf_table_repair(
     spf_graph* g, uint32_t* rows, size_t pitch, uint32_t num_rows,
     const uint32_t* sources, const uint32_t* row_idx,
     const spf_edge_delta* deltas, uint32_t n_deltas);
+/* Next-hop masks of `num` sources straight from a device table of uint32
+ * distance rows (rows[row_of[x]] = node x's row, pitch elements apart): the
+ * rule of the all-sources plans (spf_nh_rows_kernel) — bit b of NH(s, v) set
+ * iff s's b-th distinct neighbour f has w(s, f) + d(f, v) == d(s, v), f
+ * transit or f == v (LinkState.cpp:846-870).  Every source and every
+ * neighbour of a source needs a row (row_of[x] >= 0).  Source i's V * W_i
+ * words go to masks + mask_off[i] (device), W_i = ceil(nbrs(s_i) / 64) (at
+ * least 1).  The repaired rows of spf_table_repair get their next hops back
+ * this way.  Synchronous. */
+int spf_table_nexthops(
+    spf_graph* g, const uint32_t* rows, size_t pitch, const int32_t* row_of, uint32_t num,
+    const uint32_t* sources, uint64_t* masks, const uint64_t* mask_off);
 /* Copy distance row i of the query (uint32, as spf_query_fetch_rows) to
  * row dst_rows[i] of the device table `table` (pitch bytes apart), for every
  * query, in one kernel on the graph stream (asynchronous). */

@@ -53,6 +53,7 @@ EXPORTED_SYMBOLS = (
     "spf_query_order",
     "spf_query_order_keys",
     "spf_route_table_create_ex",
+    "spf_table_nexthops",
     "spf_route_table_fetch_link_metrics",
     "spf_query_device_rows",
     "spf_query_row_stride",
@@ -229,6 +230,8 @@ def load():
         ),
         "spf_query_scatter_rows": (C.c_int, [vp, pu32, vp, C.c_size_t]),
         "spf_table_repair": (C.c_int, [vp, vp, C.c_size_t, u32, pu32, pu32, vp, u32]),
+        "spf_table_nexthops": (
+            C.c_int, [vp, vp, C.c_size_t, C.POINTER(C.c_int32), u32, pu32, vp, pu64]),
         "spf_cluster_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
         "spf_cluster_create_local": (C.c_int, [u32, C.POINTER(C.c_int), C.POINTER(vp)]),
         "spf_cluster_create_rank": (C.c_int, [u32, u32, C.POINTER(C.c_uint8), C.c_int, C.POINTER(vp)]),
@@ -345,6 +348,12 @@ class Graph:
     def needs_exact(self) -> bool:
         return bool(load().spf_graph_needs_exact(self.h))
 
+    def num_nbrs(self, node: int) -> int:
+        n = load().spf_graph_num_nbrs(self.h, node)
+        if n < 0:
+            _check(n, "spf_graph_num_nbrs")
+        return int(n)
+
     def nbrs(self, node: int) -> np.ndarray:
         lib = load()
         n = lib.spf_graph_num_nbrs(self.h, node)
@@ -388,6 +397,16 @@ class Graph:
         )
         return out[: len(src)]
 
+    def table_nexthops(self, rows_ptr: int, pitch: int, row_of, sources, masks_ptr: int, mask_off):
+        """Next-hop masks of `sources` from a device distance table
+        (spf_table_nexthops); row_of[x] = table row of node x (-1 = none)."""
+        ro = np.ascontiguousarray(row_of, dtype=np.int32)
+        src = np.ascontiguousarray(sources, dtype=np.uint32)
+        off = np.ascontiguousarray(mask_off, dtype=np.uint64)
+        _check(load().spf_table_nexthops(self.h, rows_ptr, pitch, _p(ro, C.c_int32), len(src),
+                                         _p(src, C.c_uint32), masks_ptr, _p(off, C.c_uint64)),
+               "table_nexthops")
+
     def table_repair(self, rows_ptr: int, pitch: int, sources, row_idx, deltas) -> bool:
         """Repair device rows in place after `deltas` (spf_table_repair).
         False when the engine cannot (SPF_E_UNSUPPORTED): recompute instead."""
@@ -402,6 +421,19 @@ class Graph:
             return False
         _check(st, "table_repair")
         return True
+
+
+def mask_layout(graph: "Graph", sources) -> tuple:
+    """(nh_words per source, word offset per source, total words) of packed
+    next-hop mask rows: V * W words per source rounded up to 4 (32 bytes),
+    the layout of spf_query masks."""
+    V = graph.V
+    words = np.array([max(1, (graph.num_nbrs(int(s)) + 63) // 64) for s in sources], dtype=np.uint64)
+    sizes = (words * np.uint64(V) + np.uint64(3)) & ~np.uint64(3)
+    off = np.zeros(len(sources), dtype=np.uint64)
+    if len(sources):
+        off[1:] = np.cumsum(sizes)[:-1]
+    return words, off, int(sizes.sum())
 
 
 def graph_diff(before: "Csr", after: "Csr") -> np.ndarray:

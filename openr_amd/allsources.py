@@ -168,6 +168,7 @@ class RepairRun:
     wall_ms: float = 0.0     # barrier to barrier
     graph_patched: bool = False  # device graph patched in place (same links)
     relaxed: bool = False    # rows repaired in place (spf_table_repair), not recomputed
+    extra: dict = field(default_factory=dict)
 
 
 @dataclass
@@ -194,7 +195,7 @@ class ShardedAllSources:
     SURVEY §8(e): a RouteDb needs only its own row).
     """
 
-    def __init__(self, csr, sources=None, group=None, device=None, gather=True):
+    def __init__(self, csr, sources=None, group=None, device=None, gather=True, nexthops=False):
         import numpy as np
         import torch
         import torch.distributed as dist
@@ -223,6 +224,37 @@ class ShardedAllSources:
         self.csr = csr
         self.sources = src
         self.table = torch.full((rows, self.V), -1, dtype=torch.int32, device=f"cuda:{self.device}")
+        # next-hop masks of every source (spf_table_nexthops from the table
+        # rows; one rank: a source's neighbours' rows must all be local)
+        self.nexthops = nexthops
+        self.masks = None
+        if nexthops:
+            if self.world > 1 or self.n != self.V:
+                raise ValueError("next-hop tables need one rank and every node as a source")
+            self._mask_layout()
+
+    def _mask_layout(self):
+        import numpy as np
+        import torch
+
+        from openr_amd import abi
+
+        self.mask_words, self.mask_off, total = abi.mask_layout(self.graph, self.sources)
+        self.masks = torch.zeros(max(total, 1), dtype=torch.int64, device=f"cuda:{self.device}")
+        self.row_of = np.full(self.V, -1, dtype=np.int32)
+        self.row_of[self.sources] = np.arange(self.n, dtype=np.int32)
+
+    def _refresh_masks(self, idx):
+        """Masks of sources[idx] from the current table rows."""
+        if len(idx):
+            self.graph.table_nexthops(self.table.data_ptr(), self.V, self.row_of,
+                                      self.sources[idx], self.masks.data_ptr(), self.mask_off[idx])
+
+    def nexthop_masks(self, i):
+        """[V, W] uint64 next-hop masks of source i (host copy)."""
+        W = int(self.mask_words[i])
+        o = int(self.mask_off[i])
+        return self.masks[o : o + self.V * W].cpu().numpy().view("uint64").reshape(self.V, W)
 
     def local_block(self):
         if not self.gather:
@@ -257,6 +289,11 @@ class ShardedAllSources:
                 gather_rows(self.local_block(), self.n, group=self.group, out=self.table)
                 torch.cuda.synchronize(self.device)
             t2 = time.perf_counter()
+            if self.nexthops:
+                import numpy as np
+
+                self._refresh_masks(np.arange(self.n))
+                out.extra["nexthops_ms"] = (time.perf_counter() - t2) * 1e3
         if multi:
             dist.barrier(group=self.group)
         out.wall_ms = (time.perf_counter() - t0) * 1e3
@@ -372,6 +409,17 @@ class ShardedAllSources:
             dist.all_reduce(t, group=self.group)
             total = int(t.item())
         t5 = time.perf_counter()
+        if self.nexthops:
+            # next hops of the repaired sources (a source the screen passed
+            # keeps them: they are defined by its tight edges alone); a link
+            # set change can add / drop a source's neighbours, which moves
+            # its mask bits, so then every source is recomputed
+            if out.graph_patched:
+                self._refresh_masks(hit)
+            else:
+                self._mask_layout()
+                self._refresh_masks(np.arange(self.n))
+            out.extra["nexthops_ms"] = (time.perf_counter() - t5) * 1e3
         if multi:
             dist.barrier(group=self.group)
         out.affected_total = total

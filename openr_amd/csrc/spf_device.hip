@@ -1709,7 +1709,28 @@ struct NhRowsArgs {
   uint32_t nq;
   uint32_t nchunks;
   uint32_t unit;
+  // spf_table_nexthops: the source's own row is row_of[src] (else row q),
+  // and rows may be unaligned / unpadded (scalar loads within V)
+  uint32_t table = 0;
 };
+
+// four consecutive row entries from v0 (16-byte load on padded, aligned
+// rows; scalar loads within V otherwise)
+__device__ __forceinline__ void nh_ld4(
+    const NhRowsArgs& a, const uint32_t* rowp, uint32_t v0, uint32_t (&o)[4]) {
+  if (!a.table) {
+    const uint4 x = *reinterpret_cast<const uint4*>(rowp + v0);
+    o[0] = x.x;
+    o[1] = x.y;
+    o[2] = x.z;
+    o[3] = x.w;
+    return;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    o[k] = v0 + k < a.V ? rowp[v0 + k] : kInf32;
+  }
+}
 
 constexpr uint32_t kNhThreads = 256;
 constexpr uint32_t kNhPerThread = 4;
@@ -1725,8 +1746,8 @@ __global__ __launch_bounds__(kNhThreads) void spf_nh_rows_kernel(NhRowsArgs a) {
   }
   const uint32_t Wm = a.nh_w[q];
   uint64_t* nhrow = a.nh_out + a.nh_off[q];
-  const uint4 ds = *reinterpret_cast<const uint4*>(a.dist + (size_t)q * a.Vp + v0);
-  const uint32_t dsv[4] = {ds.x, ds.y, ds.z, ds.w};
+  uint32_t dsv[4];
+  nh_ld4(a, a.dist + (size_t)(a.table ? (uint32_t)a.row_of[s] : q) * a.Vp, v0, dsv);
   const uint32_t beg = a.nbr_off[s], n = a.nbr_off[s + 1] - beg;
   for (uint32_t w = 0; w < Wm; ++w) {
     uint64_t acc[4] = {0, 0, 0, 0};
@@ -1736,8 +1757,8 @@ __global__ __launch_bounds__(kNhThreads) void spf_nh_rows_kernel(NhRowsArgs a) {
       const uint64_t wf = a.unit ? 1ull : (uint64_t)a.nbr_w[beg + j];
       const bool tf = (a.trbits[f >> 5] >> (f & 31)) & 1u;
       const int32_t r = a.row_of[f];
-      const uint4 df = *reinterpret_cast<const uint4*>(a.dist + (size_t)r * a.Vp + v0);
-      const uint32_t dfv[4] = {df.x, df.y, df.z, df.w};
+      uint32_t dfv[4];
+      nh_ld4(a, a.dist + (size_t)r * a.Vp, v0, dfv);
       const uint64_t bit = 1ull << (j & 63);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -5535,6 +5556,88 @@ int spf_query_scatter_rows(
 } // extern "C"
 
 extern "C" {
+
+int spf_table_nexthops(
+    spf_graph* g, const uint32_t* rows, size_t pitch, const int32_t* row_of, uint32_t num,
+    const uint32_t* sources, uint64_t* masks, const uint64_t* mask_off) {
+  SPF_ABI_RANGE("spf_table_nexthops");
+  if (!g || (num && (!rows || !row_of || !sources || !masks || !mask_off))) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  if (num == 0 || g->V == 0) {
+    return SPF_OK;
+  }
+  if (g->exact) {
+    return fail(SPF_E_UNSUPPORTED, "64-bit rows");
+  }
+  if (pitch < g->V || pitch > 0xFFFFFFFFull) {
+    return fail(SPF_E_INVALID, "pitch");
+  }
+  const uint32_t V = g->V;
+  // every source's row and every neighbour's row must be in the table
+  for (uint32_t i = 0; i < num; ++i) {
+    const uint32_t s0 = sources[i];
+    if (s0 >= V || row_of[s0] < 0) {
+      return fail(SPF_E_INVALID, "source without a table row");
+    }
+    for (uint32_t k = g->nbr_off[s0]; k < g->nbr_off[s0 + 1]; ++k) {
+      if (row_of[g->nbrs[k]] < 0) {
+        return fail(SPF_E_INVALID, "neighbour without a table row");
+      }
+    }
+  }
+  std::vector<uint32_t> nw(num);
+  for (uint32_t i = 0; i < num; ++i) {
+    const uint32_t nn = g->nbr_off[sources[i] + 1] - g->nbr_off[sources[i]];
+    nw[i] = std::max<uint32_t>(1, (nn + 63) / 64);
+  }
+  HIP_TRY(hipSetDevice(g->device));
+  uint32_t *d_src = nullptr, *d_w = nullptr;
+  int32_t* d_row_of = nullptr;
+  uint64_t* d_off = nullptr;
+  int st = SPF_OK;
+  auto release = [&]() {
+    (void)hipStreamSynchronize(g->stream);
+    pool_free(d_src);
+    pool_free(d_w);
+    pool_free(d_row_of);
+    pool_free(d_off);
+  };
+  if ((st = dev_upload_q(&d_src, sources, num)) || (st = dev_upload_q(&d_w, nw.data(), num)) ||
+      (st = dev_upload_q(&d_row_of, row_of, V)) || (st = dev_upload_q(&d_off, mask_off, num))) {
+    release();
+    return st;
+  }
+  NhRowsArgs a;
+  a.nbr_off = g->d_nbr_off;
+  a.nbrs = g->d_nbrs;
+  a.nbr_w = g->d_nbr_w;
+  a.trbits = g->d_tr;
+  a.src = d_src;
+  a.row_of = d_row_of;
+  a.dist = rows;
+  a.nh_off = d_off;
+  a.nh_w = d_w;
+  a.nh_out = masks;
+  a.V = V;
+  a.Vp = (uint32_t)pitch;
+  a.nq = num;
+  a.nchunks = (V + kNhChunk - 1) / kNhChunk;
+  a.unit = 0;
+  a.table = 1;
+  const uint64_t blocks = (uint64_t)a.nchunks * num;
+  if (blocks > 0x7FFFFFFFull) {
+    release();
+    return fail(SPF_E_UNSUPPORTED, "too many rows for one next-hop pass");
+  }
+  hipLaunchKernelGGL(spf_nh_rows_kernel, dim3((uint32_t)blocks), dim3(kNhThreads), 0, g->stream, a);
+  const hipError_t le = hipGetLastError();
+  release(); // waits for the pass: the index buffers go back to the pool
+  if (le != hipSuccess) {
+    return fail(SPF_E_DEVICE, std::string("spf_nh_rows_kernel: ") + hipGetErrorString(le));
+  }
+  return SPF_OK;
+}
 
 int spf_table_repair(
     spf_graph* g, uint32_t* rows, size_t pitch, uint32_t num_rows,

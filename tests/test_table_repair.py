@@ -400,3 +400,53 @@ def test_repair_equals_full_recompute(gpu_ready, V, L, wmax, nsrc, expect_kernel
     sas.run()
     assert (sas.table.cpu().numpy().view(np.uint32)[: len(srcs)] == _full_table(csr, srcs)).all()
     sas.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("V,L,wmax", [(1500, 5000, 40), (2500, 9000, 1)])
+def test_repaired_table_next_hops(gpu_ready, V, L, wmax):
+    """SURVEY §8(f) row 2 with next hops: ShardedAllSources(nexthops=True)
+    keeps a next-hop mask table beside the distance rows; after each churn
+    event the repaired sources' masks are rebuilt from the table rows
+    (spf_table_nexthops, the all-sources rows rule) and EVERY source's masks
+    equal a fresh engine query's on the new graph, sampled sources the
+    literal DijkstraQ replay's next-hop sets."""
+    import torch
+
+    from oracle import spf_py
+
+    rng = random.Random(V * 7 + L)
+    links = _random_links(V, L, rng, wmax=wmax)
+    ov = np.zeros(V, dtype=np.uint8)
+    csr = abi.Csr.from_links(V, links, ov)
+    torch.cuda.set_device(0)
+    sas = AS.ShardedAllSources(csr, nexthops=True)
+    sas.run()
+    srcs = np.arange(V, dtype=np.uint32)
+
+    def check(csr, tag):
+        g = abi.Graph(csr)
+        q = g.query(srcs, abi.SPF_F_NEXTHOPS).run()
+        for i in range(V):
+            assert (sas.nexthop_masks(i) == q.nexthops(i)).all(), (tag, i)
+        for i in rng.sample(range(V), 3):
+            ref = spf_py.run_spf(csr, i, True)
+            nb = g.nbrs(i)
+            m = sas.nexthop_masks(i)
+            for v, (_, nhs, _, _) in ref.items():
+                if v == i:
+                    continue
+                got = {int(nb[w * 64 + b]) for w in range(m.shape[1]) for b in range(64)
+                       if (int(m[v, w]) >> b) & 1}
+                assert got == set(nhs), (tag, i, v)
+        q.close()
+        g.close()
+
+    check(csr, "initial")
+    for kinds in (["down"], ["metric_down"], ["drain"], ["metric_up"], ["up", "down"]):
+        links, ov = _churn(V, links, ov, rng, kinds, wmax=wmax)
+        csr = abi.Csr.from_links(V, links, ov)
+        rep = sas.update(csr)
+        assert "nexthops_ms" in rep.extra
+        check(csr, kinds)
+    sas.close()

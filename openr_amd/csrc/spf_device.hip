@@ -3387,6 +3387,7 @@ struct spf_query {
   uint64_t* d_nh = nullptr;
   uint64_t* d_key = nullptr; // wide plan settle keys (SPF_F_ORDER)
   uint32_t* d_qctr = nullptr; // dstep source-claim counter
+  void* d_pack = nullptr;     // the batch's index arrays (one pooled block)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t evm = nullptr; // after the distance stage, before next hops
   bool ran = false;
@@ -3475,6 +3476,40 @@ void pool_free(void* p) {
   }
   (void)hipFree(p);
 }
+// Recycled HIP events of finished queries (per device; a query records up
+// to 3 + 3 * kHist of them).
+std::mutex g_ev_mu;
+std::unordered_map<int, std::vector<hipEvent_t>> g_ev_free;
+hipError_t ev_get(hipEvent_t* e) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  {
+    std::lock_guard<std::mutex> g(g_ev_mu);
+    auto& v = g_ev_free[dev];
+    if (!v.empty()) {
+      *e = v.back();
+      v.pop_back();
+      return hipSuccess;
+    }
+  }
+  return hipEventCreate(e);
+}
+// callers make sure the event has completed (the stream was synchronised)
+void ev_put(hipEvent_t e) {
+  if (!e) {
+    return;
+  }
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> g(g_ev_mu);
+  auto& v = g_ev_free[dev];
+  if (v.size() < 4096) {
+    v.push_back(e);
+    return;
+  }
+  (void)hipEventDestroy(e);
+}
+
 template <typename T>
 int dev_upload_q(T** dst, const T* src, size_t n) {
   *dst = nullptr;
@@ -3525,10 +3560,10 @@ void free_query(spf_query* q) {
   (void)hipSetDevice(q->g->device);
   // the buffers go back to the pool: nothing queued may still use them
   (void)hipStreamSynchronize(q->g->stream);
+  // d_src, d_ign_off, d_ign, d_nh_off, d_nh_w, d_row_of live in d_pack
   for (void* p :
-       {(void*)q->d_src, (void*)q->d_ign_off, (void*)q->d_ign,
-        (void*)q->d_nh_w, (void*)q->d_order, (void*)q->d_scratch,
-        (void*)q->d_nh_off, q->d_dist, (void*)q->d_nh, (void*)q->d_row_of,
+       {q->d_pack, (void*)q->d_order, (void*)q->d_scratch,
+        q->d_dist, (void*)q->d_nh,
         (void*)q->d_lvl, (void*)q->d_flags, (void*)q->d_perm,
         (void*)q->d_slab, (void*)q->d_msd, (void*)q->d_base_of,
         (void*)q->d_skip, (void*)q->d_key, (void*)q->d_qctr, (void*)q->d_scatter}) {
@@ -3538,18 +3573,18 @@ void free_query(spf_query* q) {
     free_query(q->base);
   }
   if (q->ev0) {
-    (void)hipEventDestroy(q->ev0);
+    ev_put(q->ev0);
   }
   if (q->ev1) {
-    (void)hipEventDestroy(q->ev1);
+    ev_put(q->ev1);
   }
   if (q->evm) {
-    (void)hipEventDestroy(q->evm);
+    ev_put(q->evm);
   }
   for (auto& h : q->hist) {
     for (hipEvent_t e : h) {
       if (e) {
-        (void)hipEventDestroy(e);
+        ev_put(e);
       }
     }
   }
@@ -4133,9 +4168,11 @@ int spf_graph_set_transit(spf_graph* g, const uint8_t* node_overloaded) {
     }
   }
   HIP_TRY(hipSetDevice(g->device));
-  HIP_TRY(hipStreamSynchronize(g->stream));
-  HIP_TRY(hipMemcpy(g->d_tr, g->trbits.data(), g->trbits.size() * 4,
-                    hipMemcpyHostToDevice));
+  // ordered on the graph stream: kernels queued before read the old bits,
+  // kernels queued after the new ones (a pageable source is staged before
+  // the call returns, so trbits may change again right away)
+  HIP_TRY(hipMemcpyAsync(g->d_tr, g->trbits.data(), g->trbits.size() * 4,
+                         hipMemcpyHostToDevice, g->stream));
   return SPF_OK;
 }
 
@@ -4406,8 +4443,56 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     return bail(fail(SPF_E_DEVICE, "hipSetDevice failed"));
   }
   int s = SPF_OK;
-  if ((s = dev_upload_q(&q->d_src, desc->sources, nq))) {
-    return bail(s);
+  // every index array of the batch in ONE pooled block and ONE copy (a
+  // RouteDb build creates small batches whose separate blocking uploads
+  // cost more than their SPFs): sources, ignore lists, mask offsets / words,
+  // the rows plan's node -> row map, each at a 256-byte aligned offset
+  {
+    size_t off = 0;
+    auto seg = [&](size_t bytes) {
+      const size_t o = off;
+      off += (bytes + 255) & ~(size_t)255;
+      return o;
+    };
+    const uint32_t total_ign = has_ign ? desc->ignore_offsets[nq] : 0;
+    const size_t o_src = seg((size_t)nq * 4);
+    const size_t o_ioff = has_ign ? seg((size_t)(nq + 1) * 4) : 0;
+    const size_t o_ign = has_ign ? seg((size_t)total_ign * 4) : 0;
+    const size_t o_nhoff = want_nh ? seg((size_t)nq * 8) : 0;
+    const size_t o_nhw = want_nh ? seg((size_t)nq * 4) : 0;
+    const size_t o_rowof = !row_of.empty() ? seg((size_t)V * 4) : 0;
+    if (off) {
+      std::vector<uint8_t> host(off, 0);
+      std::memcpy(host.data() + o_src, desc->sources, (size_t)nq * 4);
+      if (has_ign) {
+        std::memcpy(host.data() + o_ioff, desc->ignore_offsets, (size_t)(nq + 1) * 4);
+        std::memcpy(host.data() + o_ign, desc->ignore_links, (size_t)total_ign * 4);
+      }
+      if (want_nh) {
+        std::memcpy(host.data() + o_nhoff, q->nh_off.data(), (size_t)nq * 8);
+        std::memcpy(host.data() + o_nhw, q->nh_w.data(), (size_t)nq * 4);
+      }
+      if (!row_of.empty()) {
+        std::memcpy(host.data() + o_rowof, row_of.data(), (size_t)V * 4);
+      }
+      if (pool_malloc(&q->d_pack, off) != hipSuccess ||
+          hipMemcpy(q->d_pack, host.data(), off, hipMemcpyHostToDevice) != hipSuccess) {
+        return bail(fail(SPF_E_NOMEM, "batch index arrays"));
+      }
+      uint8_t* base = static_cast<uint8_t*>(q->d_pack);
+      q->d_src = nq ? reinterpret_cast<uint32_t*>(base + o_src) : nullptr;
+      if (has_ign) {
+        q->d_ign_off = reinterpret_cast<uint32_t*>(base + o_ioff);
+        q->d_ign = total_ign ? reinterpret_cast<uint32_t*>(base + o_ign) : nullptr;
+      }
+      if (want_nh && nq) {
+        q->d_nh_off = reinterpret_cast<uint64_t*>(base + o_nhoff);
+        q->d_nh_w = reinterpret_cast<uint32_t*>(base + o_nhw);
+      }
+      if (!row_of.empty()) {
+        q->d_row_of = reinterpret_cast<int32_t*>(base + o_rowof);
+      }
+    }
   }
   if (q->dist == DistPlan::MsBfs) {
     if (pool_malloc((void**)&q->d_lvl, (size_t)nq * q->Vp8) != hipSuccess ||
@@ -4415,25 +4500,11 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       return bail(fail(SPF_E_NOMEM, "level rows"));
     }
   }
-  if (has_ign) {
-    const uint32_t total = desc->ignore_offsets[nq];
-    if ((s = dev_upload_q(&q->d_ign_off, desc->ignore_offsets, nq + 1)) ||
-        (s = dev_upload_q(&q->d_ign, desc->ignore_links, total))) {
-      return bail(s);
-    }
-  }
   if (want_nh) {
-    if ((s = dev_upload_q(&q->d_nh_off, q->nh_off.data(), nq)) ||
-        (s = dev_upload_q(&q->d_nh_w, q->nh_w.data(), nq))) {
-      return bail(s);
-    }
     if (q->nh_total &&
         pool_malloc((void**)&q->d_nh, q->nh_total * 8) != hipSuccess) {
       return bail(fail(SPF_E_NOMEM, "next-hop rows"));
     }
-  }
-  if (!row_of.empty() && (s = dev_upload_q(&q->d_row_of, row_of.data(), V))) {
-    return bail(s);
   }
   const bool ex = q->dist == DistPlan::Exact;
   const bool wide = q->dist == DistPlan::Wide;
@@ -4501,9 +4572,8 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       }
     }
   }
-  if (hipEventCreate(&q->ev0) != hipSuccess ||
-      hipEventCreate(&q->ev1) != hipSuccess ||
-      hipEventCreate(&q->evm) != hipSuccess) {
+  if (ev_get(&q->ev0) != hipSuccess || ev_get(&q->ev1) != hipSuccess ||
+      ev_get(&q->evm) != hipSuccess) {
     return bail(fail(SPF_E_DEVICE, "hipEventCreate failed"));
   }
   *out = q;
@@ -5057,7 +5127,7 @@ int spf_query_run(spf_query* q) {
   const uint32_t h = q->runs % spf_query::kHist;
   if (!q->hist[h][0]) {
     for (auto& e : q->hist[h]) {
-      HIP_TRY(hipEventCreate(&e));
+      HIP_TRY(ev_get(&e));
     }
   }
   HIP_TRY(hipEventRecord(q->ev0, g->stream));

@@ -270,10 +270,11 @@ def cpu_baseline(topo, sample):
     }
 
 
-def _rebuild_loop(M, topo, iters, timed, fwd=(0, 0)):
+def _rebuild_loop(M, topo, iters, timed, fwd=(0, 0), after_cold=None):
     """DecisionBenchmark BM_DecisionFabric loop (DecisionBenchmark.cpp:
     600-626): toggle an RSW's overload bit, rebuild the RouteDb of "2-0-0".
-    fwd = (PrefixForwardingType, PrefixForwardingAlgorithm) of every prefix."""
+    fwd = (PrefixForwardingType, PrefixForwardingAlgorithm) of every prefix;
+    after_cold() runs once the cold build is done (counter reset)."""
     areas = M.AreaLinkStates()
     ls = areas.add("0")
     dbs = topo.adj_dbs()
@@ -284,6 +285,8 @@ def _rebuild_loop(M, topo, iters, timed, fwd=(0, 0)):
         ps.updatePrefixDatabase(pdb)
     solver = M.SpfSolver("2-0-0", False, False)
     timed(solver, areas, ps)  # cold build (device graph for the engine)
+    if after_cold:
+        after_cold()
     rsw = [i for i, n in enumerate(topo.names) if n.startswith("3-")]
     tot, upd, bld, rel = [], [], [], []
     routes = 0
@@ -373,15 +376,17 @@ def route_db_rebuild_ms(topo, device, iters=5):
         nu, nm, us, free_us = solver.buildRouteDbTimed("2-0-0", areas, ps)
         return nu + nm, us, free_us
 
-    E.reset_counters()
-    out = _rebuild_loop(E, topo, iters, timed)
+    out = _rebuild_loop(E, topo, iters, timed, after_cold=E.reset_counters)
     c = E.get_counters()
     n = max(1, c.get("decision.route_build_runs", 1))
+    # warm builds only (counters reset after the cold build)
     out["per_build_us"] = {
         k.split(".", 1)[1]: round(c.get(k, 0) / n, 1)
         for k in ("decision.graph_build_us", "decision.graph_upload_us",
                   "decision.spf_batch_us", "decision.spf_device_us",
-                  "decision.route_prefetch_us")
+                  "decision.route_prefetch_us", "decision.route_prefix_pool_us",
+                  "decision.route_merge_us", "decision.route_label_us",
+                  "decision.route_release_us")
     }
     out["node"] = "2-0-0"
     out["what"] = "adj-db update (RSW overload toggle) + buildRouteDb, LFA off"
@@ -513,16 +518,19 @@ def ksp2_route_db(topo, device, iters=2):
         nu, nm, us, free_us = solver.buildRouteDbTimed("2-0-0", areas, ps)
         return nu + nm, us, free_us
 
-    E.reset_counters()
     out = _rebuild_loop(E, topo, iters, timed, (T.PrefixForwardingType.SR_MPLS,
-                                                T.PrefixForwardingAlgorithm.KSP2_ED_ECMP))
+                                                T.PrefixForwardingAlgorithm.KSP2_ED_ECMP),
+                        after_cold=E.reset_counters)
     c = E.get_counters()
     n = max(1, c.get("decision.route_build_runs", 1))
     out["per_build"] = {
         "spf_runs": round(c.get("decision.spf_runs", 0) / n, 1),
         **{k.split(".", 1)[1]: round(c.get(k, 0) / n, 1)
            for k in ("decision.route_prefetch_us", "decision.spf_batch_us", "decision.spf_device_us",
-                     "decision.route_prefix_pool_us", "decision.route_merge_us")},
+                     "decision.route_prefix_pool_us", "decision.route_merge_us",
+                     "decision.route_label_us", "decision.route_release_us",
+                     "decision.kth_trace_us", "decision.kth_memo_clear_us", "decision.kth2_trace_us",
+                     "decision.spf_memo_kept", "decision.spf_memo_dropped")},
     }
     out["what"] = ("adj-db update (RSW overload toggle) + buildRouteDb of 2-0-0, all prefixes "
                    "SR_MPLS/KSP2_ED_ECMP (k=1 + k=2 paths to every node)")

@@ -42,7 +42,9 @@ struct LinkState::Engine {
   std::map<std::pair<uint32_t, uint32_t>, std::unique_ptr<SpfView>> kthPrefetch;
   std::unordered_map<std::string, std::unique_ptr<SpfView>> isolated;
   // spfView may be called from the RouteDb worker threads of one build:
-  // memo hits take viewMu shared, fills (and kthPrefetch) exclusive; every
+  // memo hits take viewMu shared, fills (and kthPrefetch inserts) exclusive;
+  // a k = 2 fill moves its own prefetched view out under the shared lock
+  // (the emptied entry stays until the next topology change); every
   // device call of this graph is serialised by devMu (the C ABI is
   // single-threaded per graph)
   std::shared_mutex viewMu;

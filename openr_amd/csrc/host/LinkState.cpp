@@ -903,8 +903,7 @@ LinkState::LinkState(LinkState&& o) noexcept
       adjacencyDatabases_(std::move(o.adjacencyDatabases_)),
       spfResultsMetric_(std::move(o.spfResultsMetric_)),
       spfResultsHops_(std::move(o.spfResultsHops_)),
-      kthPathResults_(std::move(o.kthPathResults_)),
-      kthMu_(std::move(o.kthMu_)),
+      kth_(std::move(o.kth_)),
       kthFill_(std::move(o.kthFill_)),
       engine_(std::move(o.engine_)),
       topoGen_(o.topoGen_) {}
@@ -921,11 +920,18 @@ bool LinkState::LinkPtrEqual::operator()(
   return *lhs == *rhs;
 }
 
+void LinkState::clearKthMemo() const {
+  for (auto& stripe : *kth_) {
+    stripe.ids.clear();
+    stripe.paths.clear();
+  }
+}
+
 void LinkState::clearMemo() const {
   ++topoGen_;
   spfResultsMetric_.clear();
   spfResultsHops_.clear();
-  kthPathResults_.clear();
+  clearKthMemo();
   if (engine_) {
     // a built engine retires with its memo: the next graph build keeps the
     // views no edge delta can touch (selective invalidation, SURVEY §8(f)
@@ -1001,9 +1007,14 @@ void LinkState::patchMemo(
     }
     eng.overloaded[x] = ov;
   }
+  const auto tClear = std::chrono::steady_clock::now();
   spfResultsMetric_.clear();
   spfResultsHops_.clear();
-  kthPathResults_.clear();
+  clearKthMemo();
+  Counters::add("decision.kth_memo_clear_us",
+                std::chrono::duration_cast<std::chrono::microseconds>(
+                    std::chrono::steady_clock::now() - tClear)
+                    .count());
   if (memoScreenEnabled() && !eng.exact) {
     for (int k = 0; k < 2; ++k) {
       std::remove_reference_t<decltype(eng.memo[0])> keep;
@@ -1539,7 +1550,10 @@ LinkStateMetric LinkState::getMaxHopsToNode(const std::string& nodeName) const {
 // The reference's greedy edge-disjoint DFS (traceOnePath, LinkState.cpp:
 // 398-419), with two memos that keep its result and order exactly:
 //  * preds: pathLinksOf(v) depends on the SPF result and v only, so it is
-//    computed once per node per getKthPaths call instead of on every visit;
+//    computed once per node per SPF view -- and kept across the getKthPaths
+//    calls of one thread that trace over the same view (every k = 1 trace of
+//    one source reads the source's own SPF), keyed by (view serial, topology
+//    generation, engine);
 //  * dead: a node whose search failed has had every predecessor link
 //    inserted into linksToIgnore (the loop only stops early on success, and
 //    links are never removed), so any later search from it fails with no
@@ -1549,22 +1563,34 @@ LinkStateMetric LinkState::getMaxHopsToNode(const std::string& nodeName) const {
 // getKthPaths call, LinkState.cpp:776-786) is a link-id stamp array here:
 // same membership, no hashing or allocation per link.
 struct LinkState::TraceMemo {
-  std::vector<uint32_t> stamp;   // == epoch: preds[v] valid
+  std::vector<uint32_t> stamp;   // == predEpoch: preds[v] valid
   std::vector<uint32_t> visited; // == epoch: link id taken by some trace
-  std::vector<uint8_t> dead;
+  std::vector<uint32_t> dead;    // == epoch: search from v failed
   std::vector<std::vector<std::pair<uint32_t, uint32_t>>> preds;
-  uint32_t epoch = 0;
-  void reset(uint32_t V, uint32_t L) {
+  uint32_t epoch = 0, predEpoch = 0;
+  uint64_t viewSerial = 0, viewGen = 0;
+  const void* viewEngine = nullptr;
+  void reset(uint32_t V, uint32_t L, const SpfView& view, uint64_t gen, const void* eng) {
     if (stamp.size() != V || visited.size() != L) {
       stamp.assign(V, 0);
       visited.assign(L, 0);
+      dead.assign(V, 0);
       preds.assign(V, {});
-      epoch = 0;
+      epoch = predEpoch = 0;
+      viewEngine = nullptr;
     }
-    dead.assign(V, 0);
+    if (view.serial != viewSerial || gen != viewGen || eng != viewEngine) {
+      viewSerial = view.serial;
+      viewGen = gen;
+      viewEngine = eng;
+      if (++predEpoch == 0) {
+        std::fill(stamp.begin(), stamp.end(), 0);
+        predEpoch = 1;
+      }
+    }
     if (++epoch == 0) {
-      std::fill(stamp.begin(), stamp.end(), 0);
       std::fill(visited.begin(), visited.end(), 0);
+      std::fill(dead.begin(), dead.end(), 0);
       epoch = 1;
     }
   }
@@ -1577,44 +1603,49 @@ struct LinkState::TraceMemo {
   }
 };
 
-std::optional<LinkState::Path> LinkState::traceOnePath(
-    uint32_t src, uint32_t dest, const SpfView& result, TraceMemo& memo) const {
+bool LinkState::traceOnePath(
+    uint32_t src, uint32_t dest, const SpfView& result, TraceMemo& memo,
+    std::vector<uint32_t>& links) const {
+  // appends the path's links (src -> dest order) on success only
   if (src == dest) {
-    return Path{};
+    return true;
   }
-  if (memo.dead[dest]) {
-    return std::nullopt;
+  if (memo.dead[dest] == memo.epoch) {
+    return false;
   }
   const auto& eng = *engine_;
   auto& preds = memo.preds[dest];
-  if (memo.stamp[dest] != memo.epoch) {
+  if (memo.stamp[dest] != memo.predEpoch) {
     pathLinksOf(eng, result, dest, preds);
-    memo.stamp[dest] = memo.epoch;
+    memo.stamp[dest] = memo.predEpoch;
   }
   for (size_t i = 0; i < preds.size(); ++i) {
     const auto [eu, u] = preds[i];
     const uint32_t lid = eng.linkId[eu];
-    if (memo.take(lid)) {
-      if (auto path = traceOnePath(src, u, result, memo)) {
-        path->push_back(eng.links[lid]);
-        return path;
-      }
+    if (memo.take(lid) && traceOnePath(src, u, result, memo, links)) {
+      links.push_back(lid);
+      return true;
     }
   }
-  memo.dead[dest] = 1;
-  return std::nullopt;
+  memo.dead[dest] = memo.epoch;
+  return false;
 }
 
-std::vector<LinkState::Path> const& LinkState::getKthPaths(
+const Link& LinkState::linkOfId(uint32_t id) const {
+  return *engine().links.at(id);
+}
+
+const LinkState::KthPathIds& LinkState::kthPathIds(
     const std::string& src, const std::string& dest, size_t k) const {
   if (k < 1) {
     throw std::invalid_argument("getKthPaths: k must be >= 1");
   }
   KthKey key{src, dest, k};
-  auto lookup = [&]() -> const std::vector<Path>* {
-    std::shared_lock<std::shared_mutex> rd(*kthMu_);
-    auto found = kthPathResults_.find(key);
-    return found == kthPathResults_.end() ? nullptr : &found->second;
+  KthStripe& stripe = kthStripe(key);
+  auto lookup = [&]() -> const KthPathIds* {
+    std::shared_lock<std::shared_mutex> rd(stripe.mu);
+    auto found = stripe.ids.find(key);
+    return found == stripe.ids.end() ? nullptr : &found->second;
   };
   if (auto hit = lookup()) {
     return *hit;
@@ -1627,26 +1658,18 @@ std::vector<LinkState::Path> const& LinkState::getKthPaths(
   if (auto hit = lookup()) {
     return *hit;
   }
-  // linksToIgnore of the reference (LinkState.cpp:766-775), as the sorted
-  // ids of the links on the paths of ranks < k (every path link is an up
-  // link of the device graph)
+  // linksToIgnore of the reference (LinkState.cpp:766-775): the sorted ids
+  // of the links on the paths of ranks < k
   auto& eng = engine();
   std::vector<uint32_t> ign;
-  bool anyLink = false;
   for (size_t i = 1; i < k; ++i) {
-    for (const auto& path : getKthPaths(src, dest, i)) {
-      for (const auto& link : path) {
-        anyLink = true;
-        auto li = eng.linkIndex.find(link.get());
-        if (li != eng.linkIndex.end()) {
-          ign.push_back(li->second);
-        }
-      }
-    }
+    const auto& lower = kthPathIds(src, dest, i);
+    ign.insert(ign.end(), lower.links.begin(), lower.links.end());
   }
+  const bool anyLink = !ign.empty();
   std::sort(ign.begin(), ign.end());
   ign.erase(std::unique(ign.begin(), ign.end()), ign.end());
-  std::vector<Path> paths;
+  KthPathIds paths;
   const SpfView* res = nullptr;
   std::unique_ptr<SpfView> second;
   if (!anyLink) {
@@ -1656,11 +1679,13 @@ std::vector<LinkState::Path> const& LinkState::getKthPaths(
     if (sid != eng.ids.end()) {
       auto did = eng.ids.find(dest);
       if (did != eng.ids.end()) {
-        std::unique_lock<std::shared_mutex> wr(eng.viewMu);
+        // only this key's fill holder takes its prefetched view, and
+        // kthPrefetch changes shape only under the exclusive lock: moving the
+        // view out (the emptied entry stays) needs the shared lock alone
+        std::shared_lock<std::shared_mutex> rd(eng.viewMu);
         auto pit = eng.kthPrefetch.find({sid->second, did->second});
-        if (pit != eng.kthPrefetch.end() && pit->second->ignored == ign) {
+        if (pit != eng.kthPrefetch.end() && pit->second && pit->second->ignored == ign) {
           second = std::move(pit->second);
-          eng.kthPrefetch.erase(pit);
         }
       }
       if (!second) {
@@ -1672,20 +1697,55 @@ std::vector<LinkState::Path> const& LinkState::getKthPaths(
     }
     Counters::add("decision.spf_runs", 1);
   }
+  const auto tTrace = std::chrono::steady_clock::now();
   if (res && res->src != ~0u) {
     auto did = eng.ids.find(dest);
     if (did != eng.ids.end() && res->reached(did->second)) {
       thread_local TraceMemo memo;
-      memo.reset((uint32_t)eng.names.size(), (uint32_t)eng.links.size());
-      auto path = traceOnePath(res->src, did->second, *res, memo);
-      while (path && !path->empty()) {
-        paths.push_back(std::move(*path));
-        path = traceOnePath(res->src, did->second, *res, memo);
+      memo.reset((uint32_t)eng.names.size(), (uint32_t)eng.links.size(), *res, topoGen_, &eng);
+      // successive traces until one fails or is empty (src == dest)
+      for (;;) {
+        const size_t before = paths.links.size();
+        if (!traceOnePath(res->src, did->second, *res, memo, paths.links) ||
+            paths.links.size() == before) {
+          break;
+        }
+        paths.off.push_back((uint32_t)paths.links.size());
       }
     }
   }
-  std::unique_lock<std::shared_mutex> wr(*kthMu_);
-  return kthPathResults_.emplace(std::move(key), std::move(paths)).first->second;
+  if (k >= 2) {
+    // summed over the calling threads
+    Counters::add("decision.kth2_trace_us",
+                  std::chrono::duration_cast<std::chrono::microseconds>(
+                      std::chrono::steady_clock::now() - tTrace)
+                      .count());
+  }
+  std::unique_lock<std::shared_mutex> wr(stripe.mu);
+  return stripe.ids.emplace(std::move(key), std::move(paths)).first->second;
+}
+
+std::vector<LinkState::Path> const& LinkState::getKthPaths(
+    const std::string& src, const std::string& dest, size_t k) const {
+  const KthPathIds& ids = kthPathIds(src, dest, k);
+  KthKey key{src, dest, k};
+  KthStripe& stripe = kthStripe(key);
+  {
+    std::shared_lock<std::shared_mutex> rd(stripe.mu);
+    auto found = stripe.paths.find(key);
+    if (found != stripe.paths.end()) {
+      return found->second;
+    }
+  }
+  const auto& eng = engine();
+  std::vector<Path> paths(ids.size());
+  for (size_t i = 0; i < ids.size(); ++i) {
+    for (const uint32_t* l = ids.begin(i); l != ids.end(i); ++l) {
+      paths[i].push_back(eng.links[*l]);
+    }
+  }
+  std::unique_lock<std::shared_mutex> wr(stripe.mu);
+  return stripe.paths.emplace(std::move(key), std::move(paths)).first->second;
 }
 
 void LinkState::prefetchKthPaths(
@@ -1698,7 +1758,6 @@ void LinkState::prefetchKthPaths(
   // destinations whose second pass is still to run
   std::vector<std::pair<const std::string*, uint32_t>> todo;
   {
-    std::shared_lock<std::shared_mutex> rk(*kthMu_);
     std::shared_lock<std::shared_mutex> rv(eng.viewMu);
     std::unordered_set<uint32_t> seen;
     for (const auto& d : dests) {
@@ -1706,8 +1765,15 @@ void LinkState::prefetchKthPaths(
       if (did == eng.ids.end() || !seen.insert(did->second).second) {
         continue;
       }
-      if (kthPathResults_.count(KthKey{src, d, 2}) ||
-          eng.kthPrefetch.count({sid->second, did->second})) {
+      const KthKey k2{src, d, 2};
+      KthStripe& stripe = kthStripe(k2);
+      bool known;
+      {
+        std::shared_lock<std::shared_mutex> rk(stripe.mu);
+        known = stripe.ids.count(k2) > 0;
+      }
+      auto pf = eng.kthPrefetch.find({sid->second, did->second});
+      if (known || (pf != eng.kthPrefetch.end() && pf->second)) {
         continue;
       }
       todo.emplace_back(&d, did->second);
@@ -1720,19 +1786,17 @@ void LinkState::prefetchKthPaths(
   // k = 1 paths of every destination (independent traces over the same
   // row: host worker pool), then their links as the ignore lists
   std::vector<std::vector<uint32_t>> ignAll(todo.size());
+  const auto tTrace = std::chrono::steady_clock::now();
   parallelFor(todo.size(), hostThreads(todo.size(), 32), [&](size_t i, unsigned) {
     auto& ign = ignAll[i];
-    for (const auto& path : getKthPaths(src, *todo[i].first, 1)) {
-      for (const auto& link : path) {
-        auto li = eng.linkIndex.find(link.get());
-        if (li != eng.linkIndex.end()) {
-          ign.push_back(li->second);
-        }
-      }
-    }
+    ign = kthPathIds(src, *todo[i].first, 1).links;
     std::sort(ign.begin(), ign.end());
     ign.erase(std::unique(ign.begin(), ign.end()), ign.end());
   });
+  Counters::add("decision.kth_trace_us",
+                std::chrono::duration_cast<std::chrono::microseconds>(
+                    std::chrono::steady_clock::now() - tTrace)
+                    .count());
   std::vector<uint32_t> sources;
   std::vector<uint32_t> dstIds;
   std::vector<std::vector<uint32_t>> lists;

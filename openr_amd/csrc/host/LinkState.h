@@ -26,6 +26,8 @@
 #include <mutex>
 #include <shared_mutex>
 #include <string>
+#include <array>
+#include <atomic>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -161,7 +163,13 @@ class DistRow {
   size_t n_{0};
 };
 
+inline uint64_t nextSpfViewSerial() {
+  static std::atomic<uint64_t> serial{0};
+  return ++serial;
+}
+
 struct SpfView {
+  uint64_t serial{nextSpfViewSerial()}; // identity for per-view caches
   uint32_t src{0};            // node id (name rank) of the source
   bool useLinkMetric{true};
   bool exact{false};          // settle order came from the exact kernel
@@ -313,6 +321,20 @@ class LinkState {
   // path A is a contiguous sub-path of B (reference: LinkState.h:395-410)
   static bool pathAInPathB(Path const& a, Path const& b);
 
+  // Flat form of getKthPaths' result, the form it is computed and memoized
+  // in: path i is links [begin(i), end(i)), device-graph link ids (linkOfId)
+  // in path order.  Same paths in the same order, no Link refcounts touched;
+  // valid until the next topology change.
+  struct KthPathIds {
+    std::vector<uint32_t> off{0};
+    std::vector<uint32_t> links;
+    size_t size() const { return off.size() - 1; }
+    const uint32_t* begin(size_t i) const { return links.data() + off[i]; }
+    const uint32_t* end(size_t i) const { return links.data() + off[i + 1]; }
+  };
+  const KthPathIds& kthPathIds(const std::string& src, const std::string& dest, size_t k) const;
+  const Link& linkOfId(uint32_t id) const;
+
   // ---- MI355X engine extensions (not part of the reference API) ----
 
   // Flat SPF of `node`, memoized like getSpfResult (shares its spf_runs
@@ -376,8 +398,9 @@ class LinkState {
       const std::vector<std::pair<std::shared_ptr<Link>, std::string>>& metricPatches) const;
   Engine& engine() const;
   struct TraceMemo; // per getKthPaths call (LinkState.cpp)
-  std::optional<Path> traceOnePath(
-      uint32_t src, uint32_t dest, const SpfView& result, TraceMemo& memo) const;
+  bool traceOnePath(
+      uint32_t src, uint32_t dest, const SpfView& result, TraceMemo& memo,
+      std::vector<uint32_t>& links) const;
   void addLink(std::shared_ptr<Link> link);
   void removeLink(std::shared_ptr<Link> link);
   void removeNode(const std::string& nodeName);
@@ -411,11 +434,24 @@ class LinkState {
   struct KthKeyHash {
     size_t operator()(const KthKey& key) const;
   };
-  mutable std::unordered_map<KthKey, std::vector<Path>, KthKeyHash> kthPathResults_;
-  // getKthPaths / spfView may be called from the worker threads of one
-  // RouteDb build (Parallel.h): memo hits share the lock, fills take it
-  mutable std::unique_ptr<std::shared_mutex> kthMu_ = std::make_unique<std::shared_mutex>();
-  // once-only fills of kthPathResults_ (the reference memo runs each
+  // The paths of (src, dst, k) as link ids, and their reference form
+  // (materialised on the first getKthPaths of the key).  getKthPaths / spfView
+  // may be called from the worker threads of one RouteDb build (Parallel.h):
+  // the memo is split into stripes by key hash, each with its own lock (memo
+  // hits share it, fills take it), so the threads of a build seldom meet.
+  struct KthStripe {
+    std::shared_mutex mu;
+    std::unordered_map<KthKey, KthPathIds, KthKeyHash> ids;
+    std::unordered_map<KthKey, std::vector<Path>, KthKeyHash> paths;
+  };
+  static constexpr size_t kKthStripes = 64;
+  mutable std::unique_ptr<std::array<KthStripe, kKthStripes>> kth_ =
+      std::make_unique<std::array<KthStripe, kKthStripes>>();
+  KthStripe& kthStripe(const KthKey& key) const {
+    return (*kth_)[KthKeyHash{}(key) % kKthStripes];
+  }
+  void clearKthMemo() const;
+  // once-only fills of kthIds_ (the reference memo runs each
   // (src, dst, k) once, and decision.spf_runs counts it once): a fill holds
   // the stripe of its key; stripes are per k (k = 1, 2; one lock for k >= 3)
   // and a k-fill only ever takes stripes of smaller k, so there is no cycle

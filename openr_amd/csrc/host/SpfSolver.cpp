@@ -58,25 +58,41 @@ thrift::RouteDatabase DecisionRouteDb::toThrift() const {
   return db;
 }
 
+static size_t routeShardOf(const thrift::IpPrefix& prefix, unsigned shards) {
+  return std::hash<thrift::IpPrefix>()(prefix) % shards;
+}
+
+static size_t routeShardOf(int32_t label, unsigned shards) {
+  return (uint32_t)label % shards;
+}
+
 void releaseRouteDb(DecisionRouteDb&& db) {
   // The per-route payload (next-hop sets, prefix entries) is most of the
-  // memory and was allocated by the build's workers: free it on the same
-  // pool, bucket range by bucket range, then drop the emptied maps.  (A
-  // background reaper thread was measured worse: its frees contend with the
-  // next build's allocations, 113 -> 121 ms per fabric rebuild.)
+  // memory.  Each worker frees the routes of one shard: the routes buildRouteDb
+  // built on one worker (Parallel.h routeShards), whose memory sits in that
+  // worker's malloc arena, so the frees do not contend for arena locks.  The
+  // emptied maps are dropped afterwards.  (A background reaper thread was
+  // measured worse: its frees contend with the next build's allocations,
+  // 113 -> 121 ms per fabric rebuild.)
   const auto t0 = std::chrono::steady_clock::now();
   auto& u = db.unicastEntries;
-  parallelFor(u.bucket_count(), hostThreads(u.size(), 256), [&](size_t b, unsigned) {
-    for (auto it = u.begin(b); it != u.end(b); ++it) {
-      RibUnicastEntry dead(std::move(it->second));
+  const unsigned us = routeShards(u.size());
+  parallelShards(us, [&](unsigned s) {
+    for (auto& kv : u) {
+      if (routeShardOf(kv.first, us) == s) {
+        RibUnicastEntry dead(std::move(kv.second));
+      }
     }
-  }, 64);
+  });
   auto& m = db.mplsEntries;
-  parallelFor(m.bucket_count(), hostThreads(m.size(), 256), [&](size_t b, unsigned) {
-    for (auto it = m.begin(b); it != m.end(b); ++it) {
-      RibMplsEntry dead(std::move(it->second));
+  const unsigned ms = routeShards(m.size());
+  parallelShards(ms, [&](unsigned s) {
+    for (auto& kv : m) {
+      if (routeShardOf(kv.first, ms) == s) {
+        RibMplsEntry dead(std::move(kv.second));
+      }
     }
-  }, 64);
+  });
   DecisionRouteDb gone(std::move(db));
   Counters::add("decision.route_releases", 1);
   Counters::add(
@@ -471,31 +487,45 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
   // Open/R ECMP and SR-MPLS KSP2 prefixes only read the prefetched SPF rows
   // and the (thread-safe) path memo: one worker pool, per-worker route maps
   // merged afterwards (prefixes are distinct keys)
-  const unsigned threads = hostThreads(work.size());
+  // Prefixes go to route shards (one per worker, Parallel.h) so that
+  // releaseRouteDb frees each shard on one thread too
+  const unsigned shards = routeShards(work.size());
+  std::vector<std::vector<uint32_t>> shardWork(shards);
+  for (size_t i = 0; i < work.size(); ++i) {
+    shardWork[routeShardOf(*work[i].prefix, shards)].push_back((uint32_t)i);
+  }
   for (const auto& [area, ls] : areaLinkStates) {
     myLinks(myNodeName, area, ls); // fill the per-build cache before the workers read it
   }
-  std::vector<std::unordered_map<thrift::IpPrefix, RibUnicastEntry>> parts(threads);
+  std::vector<std::unordered_map<thrift::IpPrefix, RibUnicastEntry>> parts(shards);
   const auto tpar = std::chrono::steady_clock::now();
-  parallelFor(work.size(), threads, [&](size_t i, unsigned w) {
-    const PrefixWork& x = work[i];
-    if (x.srMpls) {
-      const auto nodes = getBestAnnouncingNodes(
-          myNodeName, *x.prefix, *x.entries, x.hasBGP, true, areaLinkStates);
-      if (!nodes.success || nodes.nodes.empty()) {
-        return;
+  parallelShards(shards, [&](unsigned s) {
+    for (const uint32_t i : shardWork[s]) {
+      const PrefixWork& x = work[i];
+      if (x.srMpls) {
+        const auto nodes = getBestAnnouncingNodes(
+            myNodeName, *x.prefix, *x.entries, x.hasBGP, true, areaLinkStates);
+        if (!nodes.success || nodes.nodes.empty()) {
+          continue;
+        }
+        selectKsp2(
+            parts[s], *x.prefix, myNodeName, nodes, *x.entries, x.hasBGP, areaLinkStates,
+            prefixState, x.algo);
+      } else {
+        selectEcmpOpenr(parts[s], myNodeName, *x.prefix, *x.entries, x.isV4, areaLinkStates);
       }
-      selectKsp2(
-          parts[w], *x.prefix, myNodeName, nodes, *x.entries, x.hasBGP, areaLinkStates,
-          prefixState, x.algo);
-    } else {
-      selectEcmpOpenr(parts[w], myNodeName, *x.prefix, *x.entries, x.isV4, areaLinkStates);
     }
   });
   const auto tmerge = std::chrono::steady_clock::now();
+  // move the workers' map nodes themselves (no re-allocation on this thread)
+  size_t built = routeDb.unicastEntries.size();
+  for (const auto& part : parts) {
+    built += part.size();
+  }
+  routeDb.unicastEntries.reserve(built);
   for (auto& part : parts) {
-    for (auto& kv : part) {
-      routeDb.unicastEntries.emplace(kv.first, std::move(kv.second));
+    while (!part.empty()) {
+      routeDb.unicastEntries.insert(part.extract(part.begin()));
     }
   }
   Counters::add("decision.route_prefix_pool_us",
@@ -509,6 +539,7 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
   // Labels held by a single (other) node are expanded on the worker pool
   // first; the sequential pass below applies the collision rule and uses
   // those results, computing colliding labels in place as the reference does.
+  const auto tlabel = std::chrono::steady_clock::now();
   std::unordered_map<int32_t, uint32_t> labelUse;
   for (const auto& [area, ls] : areaLinkStates) {
     for (const auto& [_, adjDb] : ls.getAdjacencyDatabases()) {
@@ -533,20 +564,35 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
     }
   }
   std::vector<std::optional<RibMplsEntry>> labelDone(labelJobs.size());
-  parallelFor(labelJobs.size(), hostThreads(labelJobs.size()), [&](size_t i, unsigned) {
-    const auto& db = *labelJobs[i].db;
-    const auto metricNhs =
-        getNextHopsWithMetric(myNodeName, {db.thisNodeName}, false, areaLinkStates);
-    if (metricNhs.second.empty()) {
-      return; // counted as no_route_to_label by the sequential pass
+  const unsigned labelShards = routeShards(labelJobs.size());
+  std::vector<std::vector<uint32_t>> labelShardJobs(labelShards);
+  for (size_t i = 0; i < labelJobs.size(); ++i) {
+    labelShardJobs[routeShardOf(labelJobs[i].db->nodeLabel, labelShards)].push_back((uint32_t)i);
+  }
+  parallelShards(labelShards, [&](unsigned s) {
+    for (const uint32_t i : labelShardJobs[s]) {
+      const auto& db = *labelJobs[i].db;
+      const auto metricNhs =
+          getNextHopsWithMetric(myNodeName, {db.thisNodeName}, false, areaLinkStates);
+      if (metricNhs.second.empty()) {
+        continue; // counted as no_route_to_label by the sequential pass
+      }
+      labelDone[i].emplace(
+          db.nodeLabel,
+          getNextHopsThrift(
+              myNodeName, {db.thisNodeName}, false, false, metricNhs.first,
+              metricNhs.second, db.nodeLabel, areaLinkStates, {*labelJobs[i].area}));
     }
-    labelDone[i].emplace(
-        db.nodeLabel,
-        getNextHopsThrift(
-            myNodeName, {db.thisNodeName}, false, false, metricNhs.first, metricNhs.second,
-            db.nodeLabel, areaLinkStates, {*labelJobs[i].area}));
   });
-  std::unordered_map<int32_t, std::pair<std::string, RibMplsEntry>> labelToNode;
+  // label -> node holding it so far; the entries go straight into the RouteDb
+  auto& mplsEntries = routeDb.mplsEntries;
+  mplsEntries.reserve(labelJobs.size() + 64);
+  std::unordered_map<int32_t, const std::string*> labelOwner;
+  labelOwner.reserve(labelJobs.size() + 64);
+  auto claimLabel = [&](int32_t label, const std::string& node, RibMplsEntry&& entry) {
+    labelOwner[label] = &node;
+    mplsEntries.insert_or_assign(label, std::move(entry));
+  };
   for (const auto& [area, ls] : areaLinkStates) {
     for (const auto& [_, adjDb] : ls.getAdjacencyDatabases()) {
       const int32_t topLabel = adjDb.nodeLabel;
@@ -557,10 +603,10 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
         Counters::add("decision.skipped_mpls_route", 1);
         continue;
       }
-      auto it = labelToNode.find(topLabel);
-      if (it != labelToNode.end()) {
+      auto it = labelOwner.find(topLabel);
+      if (it != labelOwner.end()) {
         Counters::add("decision.duplicate_node_label", 1);
-        if (it->second.first < adjDb.thisNodeName) {
+        if (*it->second < adjDb.thisNodeName) {
           continue;
         }
       }
@@ -569,9 +615,7 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
         nh.address.addr = std::string(16, '\0'); // "::"
         nh.area = area;
         nh.mplsAction = createMplsAction(thrift::MplsActionCode::POP_AND_LOOKUP);
-        labelToNode.erase(topLabel);
-        labelToNode.emplace(
-            topLabel, std::make_pair(adjDb.thisNodeName, RibMplsEntry(topLabel, {nh})));
+        claimLabel(topLabel, adjDb.thisNodeName, RibMplsEntry(topLabel, {nh}));
         continue;
       }
       auto job = labelJobOf.find(&adjDb);
@@ -581,9 +625,7 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
           Counters::add("decision.no_route_to_label", 1);
           continue;
         }
-        labelToNode.erase(topLabel);
-        labelToNode.emplace(
-            topLabel, std::make_pair(adjDb.thisNodeName, std::move(*done)));
+        claimLabel(topLabel, adjDb.thisNodeName, std::move(*done));
         continue;
       }
       const auto metricNhs =
@@ -592,20 +634,14 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
         Counters::add("decision.no_route_to_label", 1);
         continue;
       }
-      labelToNode.erase(topLabel);
-      labelToNode.emplace(
-          topLabel,
-          std::make_pair(
-              adjDb.thisNodeName,
-              RibMplsEntry(
-                  topLabel,
-                  getNextHopsThrift(
-                      myNodeName, {adjDb.thisNodeName}, false, false, metricNhs.first,
-                      metricNhs.second, topLabel, areaLinkStates, {area}))));
+      claimLabel(
+          topLabel, adjDb.thisNodeName,
+          RibMplsEntry(
+              topLabel,
+              getNextHopsThrift(
+                  myNodeName, {adjDb.thisNodeName}, false, false, metricNhs.first,
+                  metricNhs.second, topLabel, areaLinkStates, {area})));
     }
-  }
-  for (auto& [label, nodeAndEntry] : labelToNode) {
-    routeDb.mplsEntries.emplace(label, std::move(nodeAndEntry.second));
   }
 
   // adjacency-label PHP routes of our own links
@@ -630,6 +666,10 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
     }
   }
 
+  Counters::add("decision.route_label_us",
+                std::chrono::duration_cast<std::chrono::microseconds>(
+                    std::chrono::steady_clock::now() - tlabel)
+                    .count());
   const auto elapsed = std::chrono::steady_clock::now() - t0;
   Counters::add(
       "decision.route_build_us",
@@ -862,7 +902,34 @@ void SpfSolver::SpfSolverImpl::selectKsp2(
     thrift::PrefixForwardingAlgorithm algo) {
   RibUnicastEntry entry(prefix);
   bool selfNodeContained = false;
-  std::vector<LinkState::Path> paths;
+  // the chosen paths as link-id spans of their area's flat kth-path memo
+  struct PathRef {
+    const LinkState* ls;
+    const uint32_t* first;
+    const uint32_t* last;
+    size_t size() const { return (size_t)(last - first); }
+  };
+  std::vector<PathRef> paths;
+  // LinkState::pathAInPathB on link ids: links of one area are equal iff
+  // their ids are; links of different areas compare by value
+  auto sameLink = [](const PathRef& a, uint32_t la, const PathRef& b, uint32_t lb) {
+    return a.ls == b.ls ? la == lb : a.ls->linkOfId(la) == b.ls->linkOfId(lb);
+  };
+  auto aInB = [&](const PathRef& a, const PathRef& b) {
+    if (a.size() > b.size()) {
+      return false;
+    }
+    for (size_t start = 0; start + a.size() <= b.size(); ++start) {
+      size_t k = 0;
+      while (k < a.size() && sameLink(a, a.first[k], b, b.first[start + k])) {
+        ++k;
+      }
+      if (k == a.size()) {
+        return true;
+      }
+    }
+    return false;
+  };
 
   for (const auto& [_, ls] : areaLinkStates) {
     for (const auto& node : best.nodes) {
@@ -870,21 +937,24 @@ void SpfSolver::SpfSolverImpl::selectKsp2(
         selfNodeContained = true;
         continue;
       }
-      for (const auto& path : ls.getKthPaths(myNodeName, node, 1)) {
-        paths.push_back(path);
+      const auto& first = ls.kthPathIds(myNodeName, node, 1);
+      for (size_t i = 0; i < first.size(); ++i) {
+        paths.push_back({&ls, first.begin(i), first.end(i)});
       }
     }
     if (algo == thrift::PrefixForwardingAlgorithm::KSP2_ED_ECMP) {
       // drop second paths that contain a first path (anycast double spray)
       const size_t firstPaths = paths.size();
       for (const auto& node : best.nodes) {
-        for (const auto& secPath : ls.getKthPaths(myNodeName, node, 2)) {
+        const auto& second = ls.kthPathIds(myNodeName, node, 2);
+        for (size_t j = 0; j < second.size(); ++j) {
+          const PathRef sec{&ls, second.begin(j), second.end(j)};
           bool contained = false;
           for (size_t i = 0; i < firstPaths && !contained; ++i) {
-            contained = LinkState::pathAInPathB(paths[i], secPath);
+            contained = aInB(paths[i], sec);
           }
           if (!contained) {
-            paths.push_back(secPath);
+            paths.push_back(sec);
           }
         }
       }
@@ -894,37 +964,45 @@ void SpfSolver::SpfSolverImpl::selectKsp2(
     return;
   }
 
+  // one next hop per (path, area): the path's cost and its label stack --
+  // the node labels of the hops after the first (PHP), last hop on top of
+  // the destination's prepend label (Decision.cpp:1000-1047)
   const bool isV4Prefix = prefix.prefixAddress.addr.size() == 4;
+  std::vector<int32_t> hopLabels;
   for (const auto& path : paths) {
+    if (path.size() == 0) {
+      throw std::logic_error("selectKsp2: empty path");
+    }
+    const Link& firstLink = path.ls->linkOfId(path.first[0]);
     for (const auto& [area, ls] : areaLinkStates) {
+      const auto& adjDbs = ls.getAdjacencyDatabases();
       Metric cost = 0;
-      std::list<int32_t> labels;
-      std::string nextNode = myNodeName;
-      for (const auto& link : path) {
-        cost += link->getMetricFromNode(nextNode);
-        nextNode = link->getOtherNodeName(nextNode);
-        labels.push_front(ls.getAdjacencyDatabases().at(nextNode).nodeLabel);
+      const std::string* at = &myNodeName;
+      hopLabels.clear();
+      for (const uint32_t* l = path.first; l != path.last; ++l) {
+        const Link& link = path.ls->linkOfId(*l);
+        cost += link.getMetricFromNode(*at);
+        at = &link.getOtherNodeName(*at);
+        hopLabels.push_back(adjDbs.at(*at).nodeLabel);
       }
-      labels.pop_back(); // PHP: the first hop's label is not pushed
-      const auto& destEntry = prefixEntries.at(nextNode).at(area);
+      const auto& destEntry = prefixEntries.at(*at).at(area);
+      std::vector<int32_t> labels;
+      labels.reserve(hopLabels.size());
       if (destEntry.prependLabel) {
-        labels.push_front(*destEntry.prependLabel); // bottom of stack
+        labels.push_back(*destEntry.prependLabel); // bottom of stack
       }
-      if (path.empty()) {
-        throw std::logic_error("selectKsp2: empty path");
+      for (size_t h = hopLabels.size(); h-- > 1;) {
+        labels.push_back(hopLabels[h]);
       }
-      const auto& firstLink = path.front();
       std::optional<thrift::MplsAction> action;
       if (!labels.empty()) {
-        action = createMplsAction(
-            thrift::MplsActionCode::PUSH, std::nullopt,
-            std::vector<int32_t>(labels.begin(), labels.end()));
+        action = createMplsAction(thrift::MplsActionCode::PUSH, std::nullopt, std::move(labels));
       }
       entry.nexthops.insert(createNextHop(
-          isV4Prefix ? firstLink->getNhV4FromNode(myNodeName)
-                     : firstLink->getNhV6FromNode(myNodeName),
-          firstLink->getIfaceFromNode(myNodeName), (int32_t)cost, action, true,
-          firstLink->getArea()));
+          isV4Prefix ? firstLink.getNhV4FromNode(myNodeName)
+                     : firstLink.getNhV6FromNode(myNodeName),
+          firstLink.getIfaceFromNode(myNodeName), (int32_t)cost, action, true,
+          firstLink.getArea()));
     }
   }
 

@@ -1553,7 +1553,11 @@ LinkStateMetric LinkState::getMaxHopsToNode(const std::string& nodeName) const {
 //    computed once per node per SPF view -- and kept across the getKthPaths
 //    calls of one thread that trace over the same view (every k = 1 trace of
 //    one source reads the source's own SPF), keyed by (view serial, topology
-//    generation, engine);
+//    generation, engine).  A k = 2 trace runs over an ignore-list SPF that
+//    differs from the source's own SPF at few nodes: pathLinksOf(v) reads
+//    dist[v], the in-neighbours' dist and the ignore list at v only, so every
+//    node whose dist, in-neighbours' dist and in-links all match the
+//    source's SPF takes the source view's (cached) predecessors;
 //  * dead: a node whose search failed has had every predecessor link
 //    inserted into linksToIgnore (the loop only stops early on success, and
 //    links are never removed), so any later search from it fails with no
@@ -1563,36 +1567,96 @@ LinkStateMetric LinkState::getMaxHopsToNode(const std::string& nodeName) const {
 // getKthPaths call, LinkState.cpp:776-786) is a link-id stamp array here:
 // same membership, no hashing or allocation per link.
 struct LinkState::TraceMemo {
-  std::vector<uint32_t> stamp;   // == predEpoch: preds[v] valid
-  std::vector<uint32_t> visited; // == epoch: link id taken by some trace
-  std::vector<uint32_t> dead;    // == epoch: search from v failed
-  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> preds;
-  uint32_t epoch = 0, predEpoch = 0;
-  uint64_t viewSerial = 0, viewGen = 0;
-  const void* viewEngine = nullptr;
-  void reset(uint32_t V, uint32_t L, const SpfView& view, uint64_t gen, const void* eng) {
-    if (stamp.size() != V || visited.size() != L) {
-      stamp.assign(V, 0);
-      visited.assign(L, 0);
-      dead.assign(V, 0);
-      preds.assign(V, {});
-      epoch = predEpoch = 0;
-      viewEngine = nullptr;
-    }
-    if (view.serial != viewSerial || gen != viewGen || eng != viewEngine) {
-      viewSerial = view.serial;
-      viewGen = gen;
-      viewEngine = eng;
-      if (++predEpoch == 0) {
-        std::fill(stamp.begin(), stamp.end(), 0);
-        predEpoch = 1;
+  using Preds = std::vector<std::pair<uint32_t, uint32_t>>;
+  // pathLinksOf of one view, per node, valid while stamp[v] == epoch
+  struct PredCache {
+    std::vector<uint32_t> stamp;
+    std::vector<Preds> preds;
+    uint32_t epoch = 0;
+    uint64_t serial = 0, gen = 0;
+    const void* eng = nullptr;
+    void bind(uint32_t V, const SpfView& view, uint64_t g, const void* e) {
+      if (stamp.size() != V) {
+        stamp.assign(V, 0);
+        preds.assign(V, {});
+        epoch = 0;
+        eng = nullptr;
+      }
+      if (view.serial != serial || g != gen || e != eng) {
+        serial = view.serial;
+        gen = g;
+        eng = e;
+        if (++epoch == 0) {
+          std::fill(stamp.begin(), stamp.end(), 0);
+          epoch = 1;
+        }
       }
     }
+    const Preds& get(const LinkState::Engine& en, const SpfView& view, uint32_t v) {
+      if (stamp[v] != epoch) {
+        pathLinksOf(en, view, v, preds[v]);
+        stamp[v] = epoch;
+      }
+      return preds[v];
+    }
+  };
+  PredCache own;  // the traced view
+  PredCache base; // the source's own SPF (k >= 2 traces)
+  const SpfView* baseView = nullptr;
+  std::vector<uint32_t> visited; // == epoch: link id taken by some trace
+  std::vector<uint32_t> dead;    // == epoch: search from v failed
+  std::vector<uint32_t> changed; // == epoch: v does not take base's preds
+  uint32_t epoch = 0;
+  void reset(uint32_t V, uint32_t L, const SpfView& view, uint64_t gen, const void* eng) {
+    if (visited.size() != L || dead.size() != V) {
+      visited.assign(L, 0);
+      dead.assign(V, 0);
+      changed.assign(V, 0);
+      epoch = 0;
+    }
+    own.bind(V, view, gen, eng);
+    baseView = nullptr;
     if (++epoch == 0) {
       std::fill(visited.begin(), visited.end(), 0);
       std::fill(dead.begin(), dead.end(), 0);
+      std::fill(changed.begin(), changed.end(), 0);
       epoch = 1;
     }
+  }
+  // trace `view` (an ignore-list SPF of the same source) with the source's
+  // own SPF `src` as the base: mark the nodes whose predecessors may differ
+  void useBase(const LinkState::Engine& en, const SpfView& view, const SpfView& src,
+               uint64_t gen) {
+    const uint32_t V = (uint32_t)dead.size();
+    base.bind(V, src, gen, &en);
+    baseView = &src;
+    auto mark = [&](uint32_t x) {
+      changed[x] = epoch;
+      for (uint32_t e = en.row[x]; e < en.row[x + 1]; ++e) {
+        changed[en.col[e]] = epoch; // x is an in-neighbour of col[e]
+      }
+    };
+    const uint32_t* a = view.dist.raw32();
+    const uint32_t* b = src.dist.raw32();
+    for (uint32_t x = 0; x < V; ++x) {
+      if (a && b ? a[x] != b[x] : view.dist[x] != src.dist[x]) {
+        mark(x);
+      }
+    }
+    for (const uint32_t lid : view.ignored) {
+      for (const uint32_t h : en.halves[lid]) {
+        if (h != ~0u) {
+          changed[en.col[h]] = epoch;
+          changed[en.col[en.rev[h]]] = epoch;
+        }
+      }
+    }
+  }
+  const Preds& preds(const LinkState::Engine& en, const SpfView& view, uint32_t v) {
+    if (baseView && changed[v] != epoch) {
+      return base.get(en, *baseView, v);
+    }
+    return own.get(en, view, v);
   }
   bool take(uint32_t lid) {
     if (visited[lid] == epoch) {
@@ -1614,11 +1678,7 @@ bool LinkState::traceOnePath(
     return false;
   }
   const auto& eng = *engine_;
-  auto& preds = memo.preds[dest];
-  if (memo.stamp[dest] != memo.predEpoch) {
-    pathLinksOf(eng, result, dest, preds);
-    memo.stamp[dest] = memo.predEpoch;
-  }
+  const auto& preds = memo.preds(eng, result, dest);
   for (size_t i = 0; i < preds.size(); ++i) {
     const auto [eu, u] = preds[i];
     const uint32_t lid = eng.linkId[eu];
@@ -1703,6 +1763,22 @@ const LinkState::KthPathIds& LinkState::kthPathIds(
     if (did != eng.ids.end() && res->reached(did->second)) {
       thread_local TraceMemo memo;
       memo.reset((uint32_t)eng.names.size(), (uint32_t)eng.links.size(), *res, topoGen_, &eng);
+      if (second && !second->exact && second->okey.empty() && second->useLinkMetric) {
+        // the source's own SPF, if memoized (looking it up runs nothing)
+        const SpfView* own = nullptr;
+        {
+          std::shared_lock<std::shared_mutex> rd(eng.viewMu);
+          auto it = eng.memo[1].find(res->src);
+          if (it != eng.memo[1].end()) {
+            own = it->second.get();
+          }
+        }
+        if (own && !own->exact && own->okey.empty() && own->useLinkMetric &&
+            own->ignored.empty() &&
+            own->src == res->src && own->dist.size() == res->dist.size()) {
+          memo.useBase(eng, *res, *own, topoGen_);
+        }
+      }
       // successive traces until one fails or is empty (src == dest)
       for (;;) {
         const size_t before = paths.links.size();

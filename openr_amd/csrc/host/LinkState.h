@@ -134,6 +134,8 @@ class Link {
 class DistRow {
  public:
   static constexpr uint64_t kUnreachable = ~0ull;
+  // the 32-bit row this view shares, or nullptr (64-bit row)
+  const uint32_t* raw32() const { return d32_; }
   uint64_t operator[](size_t v) const {
     if (d32_) {
       const uint32_t x = d32_[v];

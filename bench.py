@@ -386,8 +386,12 @@ def route_db_rebuild_ms(topo, device, iters=5):
                   "decision.spf_batch_us", "decision.spf_device_us",
                   "decision.route_prefetch_us", "decision.route_prefix_pool_us",
                   "decision.route_merge_us", "decision.route_label_us",
-                  "decision.route_release_us")
+                  "decision.route_label_pool_us", "decision.route_release_us",
+                  "decision.ecmp_best_us", "decision.ecmp_nhnodes_us",
+                  "decision.ecmp_thrift_us", "decision.ecmp_insert_us")
     }
+    out["builds_counted"] = n
+    out["releases_counted"] = c.get("decision.route_releases", 0)
     out["node"] = "2-0-0"
     out["what"] = "adj-db update (RSW overload toggle) + buildRouteDb, LFA off"
     return out

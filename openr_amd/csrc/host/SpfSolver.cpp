@@ -67,30 +67,34 @@ static size_t routeShardOf(int32_t label, unsigned shards) {
 }
 
 void releaseRouteDb(DecisionRouteDb&& db) {
-  // The per-route payload (next-hop sets, prefix entries) is most of the
-  // memory.  Each worker frees the routes of one shard: the routes buildRouteDb
-  // built on one worker (Parallel.h routeShards), whose memory sits in that
+  // Each worker frees the routes of one shard: the routes buildRouteDb built
+  // on one worker (Parallel.h routeShards), whose memory sits in that
   // worker's malloc arena, so the frees do not contend for arena locks.  The
-  // emptied maps are dropped afterwards.  (A background reaper thread was
-  // measured worse: its frees contend with the next build's allocations,
-  // 113 -> 121 ms per fabric rebuild.)
+  // map nodes are unlinked here first (one pass, no frees) and destroyed,
+  // payload and node together, by the shard workers.  (A background reaper
+  // thread was measured worse: its frees contend with the next build's
+  // allocations, 113 -> 121 ms per fabric rebuild.)
   const auto t0 = std::chrono::steady_clock::now();
   auto& u = db.unicastEntries;
   const unsigned us = routeShards(u.size());
-  parallelShards(us, [&](unsigned s) {
-    for (auto& kv : u) {
-      if (routeShardOf(kv.first, us) == s) {
-        RibUnicastEntry dead(std::move(kv.second));
-      }
-    }
-  });
+  std::vector<std::vector<decltype(u.extract(u.begin()))>> uNodes(us);
+  while (!u.empty()) {
+    auto node = u.extract(u.begin());
+    uNodes[routeShardOf(node.key(), us)].push_back(std::move(node));
+  }
   auto& m = db.mplsEntries;
   const unsigned ms = routeShards(m.size());
-  parallelShards(ms, [&](unsigned s) {
-    for (auto& kv : m) {
-      if (routeShardOf(kv.first, ms) == s) {
-        RibMplsEntry dead(std::move(kv.second));
-      }
+  std::vector<std::vector<decltype(m.extract(m.begin()))>> mNodes(ms);
+  while (!m.empty()) {
+    auto node = m.extract(m.begin());
+    mNodes[routeShardOf(node.key(), ms)].push_back(std::move(node));
+  }
+  parallelShards(std::max(us, ms), [&](unsigned s) {
+    if (s < us) {
+      uNodes[s].clear();
+    }
+    if (s < ms) {
+      mNodes[s].clear();
     }
   });
   DecisionRouteDb gone(std::move(db));
@@ -197,6 +201,29 @@ class SpfRead {
   const SpfView& view_;
   const std::vector<std::string>& names_;
 };
+
+// Per-thread phase clocks of selectEcmpOpenr (summed over workers, flushed
+// into counters once per route shard).
+struct EcmpClock {
+  int64_t ns[4] = {0, 0, 0, 0}; // best nodes, next-hop nodes, thrift, insert
+  void flush() {
+    static const char* kKeys[4] = {
+        "decision.ecmp_best_us", "decision.ecmp_nhnodes_us", "decision.ecmp_thrift_us",
+        "decision.ecmp_insert_us"};
+    for (int i = 0; i < 4; ++i) {
+      if (ns[i]) {
+        Counters::add(kKeys[i], ns[i] / 1000);
+        ns[i] = 0;
+      }
+    }
+  }
+};
+thread_local EcmpClock tEcmpClock;
+inline int64_t nowNs() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
 
 } // namespace
 
@@ -515,6 +542,7 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
         selectEcmpOpenr(parts[s], myNodeName, *x.prefix, *x.entries, x.isV4, areaLinkStates);
       }
     }
+    tEcmpClock.flush();
   });
   const auto tmerge = std::chrono::steady_clock::now();
   // move the workers' map nodes themselves (no re-allocation on this thread)
@@ -536,112 +564,119 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
                     .count());
 
   // node-label MPLS routes: on a label collision the smaller node name wins.
-  // Labels held by a single (other) node are expanded on the worker pool
-  // first; the sequential pass below applies the collision rule and uses
-  // those results, computing colliding labels in place as the reference does.
+  // Labels held by a single (other) node cannot collide: they are expanded
+  // on the worker pool straight into per-shard route maps (spliced into the
+  // RouteDb like the unicast routes).  The sequential pass applies the
+  // collision rule to the rest, computing in place as the reference does.
   const auto tlabel = std::chrono::steady_clock::now();
-  std::unordered_map<int32_t, uint32_t> labelUse;
-  for (const auto& [area, ls] : areaLinkStates) {
-    for (const auto& [_, adjDb] : ls.getAdjacencyDatabases()) {
-      if (adjDb.nodeLabel != 0 && isMplsLabelValid(adjDb.nodeLabel)) {
-        ++labelUse[adjDb.nodeLabel];
-      }
-    }
-  }
-  struct LabelJob {
+  struct LabelItem {
+    int32_t label;
     const std::string* area;
     const thrift::AdjacencyDatabase* db;
   };
-  std::vector<LabelJob> labelJobs;
-  std::unordered_map<const thrift::AdjacencyDatabase*, size_t> labelJobOf;
+  std::vector<LabelItem> labelItems; // valid labels, adjacency-database order
   for (const auto& [area, ls] : areaLinkStates) {
     for (const auto& [_, adjDb] : ls.getAdjacencyDatabases()) {
-      if (adjDb.nodeLabel != 0 && isMplsLabelValid(adjDb.nodeLabel) &&
-          labelUse[adjDb.nodeLabel] == 1 && adjDb.thisNodeName != myNodeName) {
-        labelJobOf.emplace(&adjDb, labelJobs.size());
-        labelJobs.push_back({&area, &adjDb});
-      }
-    }
-  }
-  std::vector<std::optional<RibMplsEntry>> labelDone(labelJobs.size());
-  const unsigned labelShards = routeShards(labelJobs.size());
-  std::vector<std::vector<uint32_t>> labelShardJobs(labelShards);
-  for (size_t i = 0; i < labelJobs.size(); ++i) {
-    labelShardJobs[routeShardOf(labelJobs[i].db->nodeLabel, labelShards)].push_back((uint32_t)i);
-  }
-  parallelShards(labelShards, [&](unsigned s) {
-    for (const uint32_t i : labelShardJobs[s]) {
-      const auto& db = *labelJobs[i].db;
-      const auto metricNhs =
-          getNextHopsWithMetric(myNodeName, {db.thisNodeName}, false, areaLinkStates);
-      if (metricNhs.second.empty()) {
-        continue; // counted as no_route_to_label by the sequential pass
-      }
-      labelDone[i].emplace(
-          db.nodeLabel,
-          getNextHopsThrift(
-              myNodeName, {db.thisNodeName}, false, false, metricNhs.first,
-              metricNhs.second, db.nodeLabel, areaLinkStates, {*labelJobs[i].area}));
-    }
-  });
-  // label -> node holding it so far; the entries go straight into the RouteDb
-  auto& mplsEntries = routeDb.mplsEntries;
-  mplsEntries.reserve(labelJobs.size() + 64);
-  std::unordered_map<int32_t, const std::string*> labelOwner;
-  labelOwner.reserve(labelJobs.size() + 64);
-  auto claimLabel = [&](int32_t label, const std::string& node, RibMplsEntry&& entry) {
-    labelOwner[label] = &node;
-    mplsEntries.insert_or_assign(label, std::move(entry));
-  };
-  for (const auto& [area, ls] : areaLinkStates) {
-    for (const auto& [_, adjDb] : ls.getAdjacencyDatabases()) {
-      const int32_t topLabel = adjDb.nodeLabel;
-      if (topLabel == 0) {
+      if (adjDb.nodeLabel == 0) {
         continue; // not SR
       }
-      if (!isMplsLabelValid(topLabel)) {
+      if (!isMplsLabelValid(adjDb.nodeLabel)) {
         Counters::add("decision.skipped_mpls_route", 1);
         continue;
       }
-      auto it = labelOwner.find(topLabel);
-      if (it != labelOwner.end()) {
-        Counters::add("decision.duplicate_node_label", 1);
-        if (*it->second < adjDb.thisNodeName) {
-          continue;
-        }
-      }
-      if (adjDb.thisNodeName == myNodeName) {
-        thrift::NextHopThrift nh;
-        nh.address.addr = std::string(16, '\0'); // "::"
-        nh.area = area;
-        nh.mplsAction = createMplsAction(thrift::MplsActionCode::POP_AND_LOOKUP);
-        claimLabel(topLabel, adjDb.thisNodeName, RibMplsEntry(topLabel, {nh}));
-        continue;
-      }
-      auto job = labelJobOf.find(&adjDb);
-      if (job != labelJobOf.end()) {
-        auto& done = labelDone[job->second];
-        if (!done) {
-          Counters::add("decision.no_route_to_label", 1);
-          continue;
-        }
-        claimLabel(topLabel, adjDb.thisNodeName, std::move(*done));
-        continue;
-      }
+      labelItems.push_back({adjDb.nodeLabel, &area, &adjDb});
+    }
+  }
+  std::unordered_map<int32_t, uint32_t> labelUse;
+  labelUse.reserve(labelItems.size());
+  for (const auto& it : labelItems) {
+    ++labelUse[it.label];
+  }
+  std::vector<uint8_t> single(labelItems.size(), 0);
+  std::vector<uint32_t> labelJobs;
+  for (size_t i = 0; i < labelItems.size(); ++i) {
+    if (labelUse[labelItems[i].label] == 1 && labelItems[i].db->thisNodeName != myNodeName) {
+      single[i] = 1;
+      labelJobs.push_back((uint32_t)i);
+    }
+  }
+  const unsigned labelShards = routeShards(labelJobs.size());
+  std::vector<std::vector<uint32_t>> labelShardJobs(labelShards);
+  for (const uint32_t i : labelJobs) {
+    labelShardJobs[routeShardOf(labelItems[i].label, labelShards)].push_back(i);
+  }
+  std::vector<std::unordered_map<int32_t, RibMplsEntry>> labelParts(labelShards);
+  const auto tLabelPool = std::chrono::steady_clock::now();
+  parallelShards(labelShards, [&](unsigned s) {
+    for (const uint32_t i : labelShardJobs[s]) {
+      const auto& db = *labelItems[i].db;
       const auto metricNhs =
-          getNextHopsWithMetric(myNodeName, {adjDb.thisNodeName}, false, areaLinkStates);
+          getNextHopsWithMetric(myNodeName, {db.thisNodeName}, false, areaLinkStates);
       if (metricNhs.second.empty()) {
         Counters::add("decision.no_route_to_label", 1);
         continue;
       }
-      claimLabel(
-          topLabel, adjDb.thisNodeName,
+      labelParts[s].emplace(
+          db.nodeLabel,
           RibMplsEntry(
-              topLabel,
+              db.nodeLabel,
               getNextHopsThrift(
-                  myNodeName, {adjDb.thisNodeName}, false, false, metricNhs.first,
-                  metricNhs.second, topLabel, areaLinkStates, {area})));
+                  myNodeName, {db.thisNodeName}, false, false, metricNhs.first,
+                  metricNhs.second, db.nodeLabel, areaLinkStates, {*labelItems[i].area})));
     }
+  });
+  Counters::add("decision.route_label_pool_us",
+                std::chrono::duration_cast<std::chrono::microseconds>(
+                    std::chrono::steady_clock::now() - tLabelPool)
+                    .count());
+  auto& mplsEntries = routeDb.mplsEntries;
+  mplsEntries.reserve(labelItems.size() + 64);
+  for (auto& part : labelParts) {
+    while (!part.empty()) {
+      mplsEntries.insert(part.extract(part.begin()));
+    }
+  }
+  // label -> node holding it so far (colliding labels and our own)
+  std::unordered_map<int32_t, const std::string*> labelOwner;
+  auto claimLabel = [&](int32_t label, const std::string& node, RibMplsEntry&& entry) {
+    labelOwner[label] = &node;
+    mplsEntries.insert_or_assign(label, std::move(entry));
+  };
+  for (size_t i = 0; i < labelItems.size(); ++i) {
+    if (single[i]) {
+      continue;
+    }
+    const int32_t topLabel = labelItems[i].label;
+    const auto& adjDb = *labelItems[i].db;
+    const std::string& area = *labelItems[i].area;
+    auto it = labelOwner.find(topLabel);
+    if (it != labelOwner.end()) {
+      Counters::add("decision.duplicate_node_label", 1);
+      if (*it->second < adjDb.thisNodeName) {
+        continue;
+      }
+    }
+    if (adjDb.thisNodeName == myNodeName) {
+      thrift::NextHopThrift nh;
+      nh.address.addr = std::string(16, '\0'); // "::"
+      nh.area = area;
+      nh.mplsAction = createMplsAction(thrift::MplsActionCode::POP_AND_LOOKUP);
+      claimLabel(topLabel, adjDb.thisNodeName, RibMplsEntry(topLabel, {nh}));
+      continue;
+    }
+    const auto metricNhs =
+        getNextHopsWithMetric(myNodeName, {adjDb.thisNodeName}, false, areaLinkStates);
+    if (metricNhs.second.empty()) {
+      Counters::add("decision.no_route_to_label", 1);
+      continue;
+    }
+    claimLabel(
+        topLabel, adjDb.thisNodeName,
+        RibMplsEntry(
+            topLabel,
+            getNextHopsThrift(
+                myNodeName, {adjDb.thisNodeName}, false, false, metricNhs.first,
+                metricNhs.second, topLabel, areaLinkStates, {area})));
   }
 
   // adjacency-label PHP routes of our own links
@@ -830,8 +865,16 @@ void SpfSolver::SpfSolverImpl::selectEcmpOpenr(
     const thrift::PrefixEntries& prefixEntries,
     bool isV4,
     AreaLinkStates const& areaLinkStates) {
+  auto& clk = tEcmpClock;
+  int64_t t = nowNs();
+  auto lap = [&](int i) {
+    const int64_t n = nowNs();
+    clk.ns[i] += n - t;
+    t = n;
+  };
   const auto ret =
       getBestAnnouncingNodes(myNodeName, prefix, prefixEntries, false, false, areaLinkStates);
+  lap(0);
   if (!ret.success) {
     return;
   }
@@ -839,6 +882,7 @@ void SpfSolver::SpfSolverImpl::selectEcmpOpenr(
       getPrefixForwardingType(prefixEntries) == thrift::PrefixForwardingType::SR_MPLS;
   const auto metricNhs =
       getNextHopsWithMetric(myNodeName, ret.nodes, perDestination, areaLinkStates);
+  lap(1);
   if (metricNhs.second.empty()) {
     Counters::add("decision.no_route_to_prefix", 1);
     return;
@@ -850,7 +894,9 @@ void SpfSolver::SpfSolverImpl::selectEcmpOpenr(
           std::nullopt, areaLinkStates, ret.areas),
       prefixEntries.at(ret.bestNode).at(ret.bestArea),
       ret.bestArea);
+  lap(2);
   unicastEntries.emplace(prefix, std::move(entry));
+  lap(3);
 }
 
 void SpfSolver::SpfSolverImpl::selectEcmpBgp(

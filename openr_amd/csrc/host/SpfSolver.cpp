@@ -12,6 +12,7 @@
 
 #include "SpfSolver.h"
 
+#include <atomic>
 #include <chrono>
 #include <memory>
 #include <string_view>
@@ -158,6 +159,9 @@ class SpfRead {
  public:
   SpfRead(const LinkState& ls, const std::string& src, bool useLinkMetric = true)
       : ls_(ls), src_(src), view_(ls.spfView(src, useLinkMetric)), names_(ls.nodeNames()) {}
+  // over an already resolved (link-metric) view of src
+  SpfRead(const LinkState& ls, const std::string& src, const SpfView& view)
+      : ls_(ls), src_(src), view_(view), names_(ls.nodeNames()) {}
 
   std::optional<Metric> metric(const std::string& node) const {
     if (view_.src == ~0u) {
@@ -341,8 +345,12 @@ class SpfSolver::SpfSolverImpl {
     const std::string* iface;
   };
   struct MyLinks {
+    std::string node;
     std::vector<MyLink> links;
     std::unordered_map<std::string_view, std::vector<uint32_t>> byNbr;
+    // node's own link-metric SPF view, resolved on first read (spfView's
+    // memo lock is then off the per-prefix path of the worker pool)
+    mutable std::atomic<const SpfView*> view{nullptr};
   };
   const MyLinks& myLinks(
       const std::string& myNodeName, const std::string& area, const LinkState& ls) const {
@@ -350,7 +358,8 @@ class SpfSolver::SpfSolverImpl {
     if (it != myLinks_.end()) {
       return it->second;
     }
-    MyLinks v;
+    MyLinks& v = myLinks_[area];
+    v.node = myNodeName;
     for (const auto& link : ls.linksFromNode(myNodeName)) {
       const std::string& nbr = link->getOtherNodeName(myNodeName);
       v.byNbr[std::string_view(nbr)].push_back((uint32_t)v.links.size());
@@ -359,9 +368,22 @@ class SpfSolver::SpfSolverImpl {
           link->getMetricFromNode(myNodeName), &link->getNhV4FromNode(myNodeName),
           &link->getNhV6FromNode(myNodeName), &link->getIfaceFromNode(myNodeName)});
     }
-    return myLinks_.emplace(area, std::move(v)).first->second;
+    return v;
   }
   mutable std::unordered_map<std::string, MyLinks> myLinks_;
+  // SpfRead of myNodeName's own SPF in `area` (the per-build cached view)
+  SpfRead myRead(const std::string& myNodeName, const std::string& area, const LinkState& ls) const {
+    auto it = myLinks_.find(area);
+    if (it == myLinks_.end() || it->second.node != myNodeName) {
+      return SpfRead(ls, myNodeName);
+    }
+    const SpfView* v = it->second.view.load(std::memory_order_acquire);
+    if (!v) {
+      v = &ls.spfView(myNodeName, true);
+      it->second.view.store(v, std::memory_order_release);
+    }
+    return SpfRead(ls, myNodeName, *v);
+  }
 
   thrift::StaticRoutes staticRoutes_;
   std::vector<thrift::RouteDatabaseDelta> staticRoutesUpdates_;
@@ -731,7 +753,7 @@ BestPathCalResult SpfSolver::SpfSolverImpl::getBestAnnouncingNodes(
     }
     for (const auto& [node, byArea] : prefixEntries) {
       for (const auto& [area, entry] : byArea) {
-        SpfRead mine(areaLinkStates.at(area), myNodeName);
+        const SpfRead mine = myRead(myNodeName, area, areaLinkStates.at(area));
         if (!mine.metric(node)) {
           continue; // unreachable announcer
         }
@@ -1094,8 +1116,8 @@ std::pair<Metric, NextHopNodes> SpfSolver::SpfSolverImpl::getNextHopsWithMetric(
   NextHopNodes nextHopNodes;
   Metric shortestMetric = std::numeric_limits<Metric>::max();
 
-  for (const auto& [_, ls] : areaLinkStates) {
-    SpfRead mine(ls, myNodeName);
+  for (const auto& [areaName, ls] : areaLinkStates) {
+    const SpfRead mine = myRead(myNodeName, areaName, ls);
     // closest announcers in this area
     Metric areaMin = std::numeric_limits<Metric>::max();
     std::vector<const std::string*> minCostNodes;

@@ -534,6 +534,7 @@ def ksp2_route_db(topo, device, iters=2):
                      "decision.route_prefix_pool_us", "decision.route_merge_us",
                      "decision.route_label_us", "decision.route_release_us",
                      "decision.kth_trace_us", "decision.kth_memo_clear_us", "decision.kth2_trace_us",
+                     "decision.kth2_base_us",
                      "decision.spf_memo_kept", "decision.spf_memo_dropped")},
     }
     out["what"] = ("adj-db update (RSW overload toggle) + buildRouteDb of 2-0-0, all prefixes "

@@ -13,6 +13,7 @@
 #include "Engine.h"
 
 #include <chrono>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <shared_mutex>
@@ -1638,9 +1639,25 @@ struct LinkState::TraceMemo {
     };
     const uint32_t* a = view.dist.raw32();
     const uint32_t* b = src.dist.raw32();
-    for (uint32_t x = 0; x < V; ++x) {
-      if (a && b ? a[x] != b[x] : view.dist[x] != src.dist[x]) {
-        mark(x);
+    if (a && b) {
+      // the rows differ at few nodes: skip equal 256-byte chunks (memcmp)
+      constexpr uint32_t kChunk = 64;
+      for (uint32_t x0 = 0; x0 < V; x0 += kChunk) {
+        const uint32_t n = std::min(kChunk, V - x0);
+        if (std::memcmp(a + x0, b + x0, (size_t)n * sizeof(uint32_t)) == 0) {
+          continue;
+        }
+        for (uint32_t x = x0; x < x0 + n; ++x) {
+          if (a[x] != b[x]) {
+            mark(x);
+          }
+        }
+      }
+    } else {
+      for (uint32_t x = 0; x < V; ++x) {
+        if (view.dist[x] != src.dist[x]) {
+          mark(x);
+        }
       }
     }
     for (const uint32_t lid : view.ignored) {
@@ -1776,7 +1793,12 @@ const LinkState::KthPathIds& LinkState::kthPathIds(
         if (own && !own->exact && own->okey.empty() && own->useLinkMetric &&
             own->ignored.empty() &&
             own->src == res->src && own->dist.size() == res->dist.size()) {
+          const auto tBase = std::chrono::steady_clock::now();
           memo.useBase(eng, *res, *own, topoGen_);
+          Counters::add("decision.kth2_base_us",
+                        std::chrono::duration_cast<std::chrono::microseconds>(
+                            std::chrono::steady_clock::now() - tBase)
+                            .count());
         }
       }
       // successive traces until one fails or is empty (src == dest)

@@ -534,7 +534,8 @@ def ksp2_route_db(topo, device, iters=2):
                      "decision.route_prefix_pool_us", "decision.route_merge_us",
                      "decision.route_label_us", "decision.route_release_us",
                      "decision.kth_trace_us", "decision.kth_memo_clear_us", "decision.kth2_trace_us",
-                     "decision.kth2_base_us",
+                     "decision.kth2_base_us", "decision.ksp2_best_us", "decision.ksp2_paths_us",
+                     "decision.ksp2_nexthops_us", "decision.ksp2_rest_us",
                      "decision.spf_memo_kept", "decision.spf_memo_dropped")},
     }
     out["what"] = ("adj-db update (RSW overload toggle) + buildRouteDb of 2-0-0, all prefixes "

@@ -458,7 +458,7 @@ class LinkState {
   // the stripe of its key; stripes are per k (k = 1, 2; one lock for k >= 3)
   // and a k-fill only ever takes stripes of smaller k, so there is no cycle
   struct KthFillLocks {
-    static constexpr size_t kStripes = 64;
+    static constexpr size_t kStripes = 1024; // a fill holds its stripe for a whole trace
     std::mutex k1[kStripes], k2[kStripes], kN;
   };
   mutable std::unique_ptr<KthFillLocks> kthFill_ = std::make_unique<KthFillLocks>();

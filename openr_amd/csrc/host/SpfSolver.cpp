@@ -209,12 +209,15 @@ class SpfRead {
 // Per-thread phase clocks of selectEcmpOpenr (summed over workers, flushed
 // into counters once per route shard).
 struct EcmpClock {
-  int64_t ns[4] = {0, 0, 0, 0}; // best nodes, next-hop nodes, thrift, insert
+  // ECMP: best nodes, next-hop nodes, thrift, insert; KSP2: best nodes,
+  // paths (k = 1, 2), next hops + label stacks, rest
+  int64_t ns[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   void flush() {
-    static const char* kKeys[4] = {
+    static const char* kKeys[8] = {
         "decision.ecmp_best_us", "decision.ecmp_nhnodes_us", "decision.ecmp_thrift_us",
-        "decision.ecmp_insert_us"};
-    for (int i = 0; i < 4; ++i) {
+        "decision.ecmp_insert_us", "decision.ksp2_best_us", "decision.ksp2_paths_us",
+        "decision.ksp2_nexthops_us", "decision.ksp2_rest_us"};
+    for (int i = 0; i < 8; ++i) {
       if (ns[i]) {
         Counters::add(kKeys[i], ns[i] / 1000);
         ns[i] = 0;
@@ -552,8 +555,10 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
     for (const uint32_t i : shardWork[s]) {
       const PrefixWork& x = work[i];
       if (x.srMpls) {
+        const int64_t tb = nowNs();
         const auto nodes = getBestAnnouncingNodes(
             myNodeName, *x.prefix, *x.entries, x.hasBGP, true, areaLinkStates);
+        tEcmpClock.ns[4] += nowNs() - tb;
         if (!nodes.success || nodes.nodes.empty()) {
           continue;
         }
@@ -968,6 +973,13 @@ void SpfSolver::SpfSolverImpl::selectKsp2(
     AreaLinkStates const& areaLinkStates,
     PrefixState const& prefixState,
     thrift::PrefixForwardingAlgorithm algo) {
+  auto& clk = tEcmpClock;
+  int64_t tk = nowNs();
+  auto lap = [&](int i) {
+    const int64_t n = nowNs();
+    clk.ns[i] += n - tk;
+    tk = n;
+  };
   RibUnicastEntry entry(prefix);
   bool selfNodeContained = false;
   // the chosen paths as link-id spans of their area's flat kth-path memo
@@ -1028,6 +1040,7 @@ void SpfSolver::SpfSolverImpl::selectKsp2(
       }
     }
   }
+  lap(5);
   if (paths.empty()) {
     return;
   }
@@ -1074,6 +1087,7 @@ void SpfSolver::SpfSolverImpl::selectKsp2(
     }
   }
 
+  lap(6);
   int staticNexthops = 0;
   if (selfNodeContained) {
     const auto& mine = prefixEntries.at(myNodeName);
@@ -1106,6 +1120,7 @@ void SpfSolver::SpfSolverImpl::selectKsp2(
     }
   }
   unicastEntries.emplace(prefix, std::move(entry));
+  lap(7);
 }
 
 std::pair<Metric, NextHopNodes> SpfSolver::SpfSolverImpl::getNextHopsWithMetric(

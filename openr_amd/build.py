@@ -1,9 +1,15 @@
 """Build recipe for the MI355X SPF engine (in-tree, no JIT cache):
 
-  libopenr_spf.so        hipcc --offload-arch=gfx950  csrc/spf_device.hip
-  _openr_spf*.so         g++ host C++ (LinkState / SpfSolver / PrefixState)
-                         + pybind11 bindings, linked to libopenr_spf.so
+  libopenr_spf.so        the C ABI: hipcc --offload-arch=gfx950
+                         csrc/spf_device.hip + csrc/spf_cluster.hip (RCCL, roctx)
+  libopenr_decision.so   the host layer (LinkState / PrefixState / SpfSolver /
+                         AllNodesRouteTable / PublicationIngest), g++
+  decision_consumer      a standalone Decision-style C++ caller
+  _openr_spf*.so         pybind11 bindings of the host layer (tests / bench),
+                         linked to libopenr_decision.so + libopenr_spf.so
 
+The first three commands are READ from INTEGRATION.md's "Build recipe"
+block (the recipe a maintainer follows is the one this repo builds with).
 Run `python -m openr_amd.build` (or __graft_entry__.build()).  Targets are
 rebuilt only when a source is newer than the output.
 """
@@ -12,6 +18,8 @@ from __future__ import annotations
 
 import glob
 import os
+import re
+import shlex
 import subprocess
 import sys
 import sysconfig
@@ -24,7 +32,37 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("OPENR_SPF_ARCH", "gfx950")
 
 LIB = os.path.join(HERE, "libopenr_spf.so")
+DECISION = os.path.join(HERE, "libopenr_decision.so")
+CONSUMER = os.path.join(HERE, "decision_consumer")
 EXT = os.path.join(HERE, "_openr_spf" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def recipe(out=HERE, repo=ROOT):
+    """INTEGRATION.md's build recipe: {"engine" | "host" | "consumer": argv},
+    with $REPO / $OUT substituted."""
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    head = "### Build recipe"
+    block = text[text.index(head):].split("```sh\n", 1)[1].split("```", 1)[0]
+    cmds, cur = {}, None
+    for line in block.splitlines():
+        m = re.match(r"# recipe: (\w+)", line)
+        if m:
+            cur = m.group(1)
+            cmds[cur] = ""
+            continue
+        if cur is not None and line.strip() and not line.lstrip().startswith("#"):
+            cmds[cur] += " " + line.strip().rstrip("\\")
+    out_cmds = {}
+    for k, v in cmds.items():
+        v = v.replace("$REPO", repo).replace("$OUT", out)
+        out_cmds[k] = shlex.split(v)
+    if set(out_cmds) != {"engine", "host", "consumer"}:
+        raise RuntimeError(f"INTEGRATION.md recipe has steps {sorted(out_cmds)}")
+    return out_cmds
+
+
+def _recipe_sources(argv):
+    return [a for a in argv if a.endswith((".hip", ".cpp"))]
 
 
 def _newer(target, sources):
@@ -40,38 +78,30 @@ def _run(cmd):
 
 
 def build_device(force=False):
-    srcs = [os.path.join(CSRC, "spf_device.hip"), os.path.join(CSRC, "spf_cluster.hip"),
-            os.path.join(INC, "openr_spf.h")]
+    cmd = recipe()["engine"]
+    srcs = _recipe_sources(cmd) + [os.path.join(INC, "openr_spf.h")]
     if force or _newer(LIB, srcs):
-        _run(
-            [
-                HIPCC,
-                f"--offload-arch={ARCH}",
-                "-O3",
-                "-std=c++17",
-                "-shared",
-                "-fPIC",
-                f"-I{INC}",
-                "-o",
-                LIB,
-                srcs[0],
-                srcs[1],
-                "-L/opt/rocm/lib",
-                "-lrccl",
-                "-lrocprofiler-sdk-roctx",
-                "-Wl,-rpath,/opt/rocm/lib",
-            ]
-        )
+        _run(cmd)
     return LIB
+
+
+def build_decision(force=False):
+    """libopenr_decision.so (host layer) and the standalone consumer."""
+    r = recipe()
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "host", "*.h"))) + [os.path.join(INC, "openr_spf.h")]
+    if force or _newer(DECISION, _recipe_sources(r["host"]) + hdrs + [LIB]):
+        _run(r["host"])
+    if force or _newer(CONSUMER, _recipe_sources(r["consumer"]) + hdrs + [DECISION]):
+        _run(r["consumer"])
+    return DECISION
 
 
 def build_host(force=False):
     import pybind11
 
-    host = sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "host", "*.h")))
     bind = os.path.join(CSRC, "py", "bindings.cpp")
-    if force or _newer(EXT, host + hdrs + [bind, LIB, os.path.join(INC, "openr_spf.h")]):
+    if force or _newer(EXT, hdrs + [bind, LIB, DECISION, os.path.join(INC, "openr_spf.h")]):
         _run(
             [
                 os.environ.get("CXX", "g++"),
@@ -84,11 +114,11 @@ def build_host(force=False):
                 f"-I{INC}",
                 f"-I{pybind11.get_include()}",
                 f"-I{sysconfig.get_paths()['include']}",
-                *host,
                 bind,
                 "-o",
                 EXT,
                 f"-L{HERE}",
+                "-lopenr_decision",
                 "-lopenr_spf",
                 "-Wl,-rpath,$ORIGIN",
             ]
@@ -98,6 +128,7 @@ def build_host(force=False):
 
 def build(force=False):
     build_device(force)
+    build_decision(force)
     build_host(force)
 
 

@@ -73,6 +73,16 @@ void Counters::add(const std::string& key, int64_t v) {
   counterMap()[key] += v;
   ++sampleMap()[key];
 }
+void Counters::addSamples(const std::string& key, int64_t sum, int64_t samples) {
+  std::lock_guard<std::mutex> g(counterMutex());
+  counterMap()[key] += sum;
+  sampleMap()[key] += samples;
+}
+int64_t Counters::samples(const std::string& key) {
+  std::lock_guard<std::mutex> g(counterMutex());
+  auto it = sampleMap().find(key);
+  return it == sampleMap().end() ? 0 : it->second;
+}
 std::unordered_map<std::string, int64_t> Counters::fb303Snapshot() {
   std::lock_guard<std::mutex> g(counterMutex());
   std::unordered_map<std::string, int64_t> out;
@@ -907,6 +917,7 @@ LinkState::LinkState(LinkState&& o) noexcept
       kth_(std::move(o.kth_)),
       kthFill_(std::move(o.kthFill_)),
       engine_(std::move(o.engine_)),
+      retired_(std::move(o.retired_)),
       topoGen_(o.topoGen_) {}
 
 size_t LinkState::LinkPtrHash::operator()(const std::shared_ptr<Link>& l) const {
@@ -944,7 +955,13 @@ void LinkState::clearMemo() const {
   }
 }
 
-void LinkState::invalidate() const { clearMemo(); }
+// Drop the device graph and every memoized result, retired ones included
+// (nothing is screened or adopted by the next build).
+void LinkState::invalidate() const {
+  clearMemo();
+  retired_.reset();
+  engine_.reset();
+}
 
 // Topology change that keeps the set of up links: drop every SPF memo but
 // keep the device graph, patching node transit bits / link metrics in place
@@ -1473,7 +1490,8 @@ std::unique_ptr<LinkState::SpfBatch> LinkState::runSpfBatch(
   batch->gen_ = topoGen_;
   batch->src_ = src;
   const size_t nq = linksToIgnore.size();
-  Counters::add("decision.spf_runs", (int64_t)nq);
+  // one COUNT sample per SPF, as the reference's per-runSpf addStatValue
+  Counters::addSamples("decision.spf_runs", (int64_t)nq, (int64_t)nq);
   auto sid = eng.ids.find(src);
   if (sid == eng.ids.end()) {
     // unknown source: every result holds only the source itself
@@ -1727,6 +1745,16 @@ const LinkState::KthPathIds& LinkState::kthPathIds(
   if (auto hit = lookup()) {
     return *hit;
   }
+  // linksToIgnore of the reference (LinkState.cpp:766-775): the sorted ids
+  // of the links on the paths of ranks < k.  Filled BEFORE this key's fill
+  // lock is taken, so a fill never holds a lock while it recurses (every
+  // k >= 3 shares one fill lock; k = 4 recursing into k = 3 under it would
+  // lock it twice on one thread).
+  std::vector<uint32_t> ign;
+  for (size_t i = 1; i < k; ++i) {
+    const auto& lower = kthPathIds(src, dest, i);
+    ign.insert(ign.end(), lower.links.begin(), lower.links.end());
+  }
   // once-only fill: concurrent callers of the same key wait for the first
   std::mutex& fillMu = k == 1 ? kthFill_->k1[KthKeyHash{}(key) % KthFillLocks::kStripes]
       : k == 2 ? kthFill_->k2[KthKeyHash{}(key) % KthFillLocks::kStripes]
@@ -1735,14 +1763,7 @@ const LinkState::KthPathIds& LinkState::kthPathIds(
   if (auto hit = lookup()) {
     return *hit;
   }
-  // linksToIgnore of the reference (LinkState.cpp:766-775): the sorted ids
-  // of the links on the paths of ranks < k
   auto& eng = engine();
-  std::vector<uint32_t> ign;
-  for (size_t i = 1; i < k; ++i) {
-    const auto& lower = kthPathIds(src, dest, i);
-    ign.insert(ign.end(), lower.links.begin(), lower.links.end());
-  }
   const bool anyLink = !ign.empty();
   std::sort(ign.begin(), ign.end());
   ign.erase(std::unique(ign.begin(), ign.end()), ign.end());

@@ -455,8 +455,9 @@ class LinkState {
   void clearKthMemo() const;
   // once-only fills of kthIds_ (the reference memo runs each
   // (src, dst, k) once, and decision.spf_runs counts it once): a fill holds
-  // the stripe of its key; stripes are per k (k = 1, 2; one lock for k >= 3)
-  // and a k-fill only ever takes stripes of smaller k, so there is no cycle
+  // the stripe of its key; stripes are per k (k = 1, 2; one lock for k >= 3).
+  // The lower-rank paths a k-fill needs are filled before it takes its lock,
+  // so no thread ever holds two fill locks (no cycle, no re-entry)
   struct KthFillLocks {
     static constexpr size_t kStripes = 1024; // a fill holds its stripe for a whole trace
     std::mutex k1[kStripes], k2[kStripes], kN;
@@ -478,6 +479,9 @@ class LinkState {
 // the windowed names carry the all-time value.
 struct Counters {
   static void add(const std::string& key, int64_t v);
+  // `samples` add() calls of total value `sum` in one step (a batch of SPFs)
+  static void addSamples(const std::string& key, int64_t sum, int64_t samples);
+  static int64_t samples(const std::string& key);
   static int64_t get(const std::string& key);
   static std::unordered_map<std::string, int64_t> snapshot();
   static std::unordered_map<std::string, int64_t> fb303Snapshot();

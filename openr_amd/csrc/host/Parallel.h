@@ -77,9 +77,8 @@ void parallelFor(size_t n, unsigned threads, Fn&& fn, size_t chunk = 16) {
 // (releaseRouteDb), by the one worker that takes its shard, so the frees of
 // a shard land in the malloc arena its builder allocated from instead of
 // every releasing thread taking every arena's lock (fabric 2-0-0, ~20k routes
-// x ~40 next hops: release 67 ms on dynamically scheduled buckets).  Build
-// and release agree on the shard count because both derive it from the route
-// count with the same rule.
+// x ~40 next hops: release 67 ms on dynamically scheduled buckets).  The
+// build records its shard counts in the RouteDb and the release reuses them.
 inline unsigned routeShards(size_t routes) { return hostThreads(routes, 64); }
 
 // fn(shard) for every shard in [0, shards), one shard per work item.

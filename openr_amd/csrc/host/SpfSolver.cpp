@@ -68,23 +68,27 @@ static size_t routeShardOf(int32_t label, unsigned shards) {
 }
 
 void releaseRouteDb(DecisionRouteDb&& db) {
-  // Each worker frees the routes of one shard: the routes buildRouteDb built
-  // on one worker (Parallel.h routeShards), whose memory sits in that
-  // worker's malloc arena, so the frees do not contend for arena locks.  The
+  // Each worker frees the routes of one shard, with the shard split the
+  // build used (recorded in the RouteDb): a shard's routes were allocated by
+  // one build worker, so they come from one malloc arena and the frees of
+  // different workers mostly take different arena locks.  Shards are handed
+  // out dynamically in both passes, so the freeing thread is not guaranteed
+  // to be the allocating one; the measured gain (fabric release 67 -> 13-22
+  // ms) is for this split on the bench's route mix and 16 host threads.  The
   // map nodes are unlinked here first (one pass, no frees) and destroyed,
   // payload and node together, by the shard workers.  (A background reaper
   // thread was measured worse: its frees contend with the next build's
   // allocations, 113 -> 121 ms per fabric rebuild.)
   const auto t0 = std::chrono::steady_clock::now();
   auto& u = db.unicastEntries;
-  const unsigned us = routeShards(u.size());
+  const unsigned us = db.unicastShards ? db.unicastShards : routeShards(u.size());
   std::vector<std::vector<decltype(u.extract(u.begin()))>> uNodes(us);
   while (!u.empty()) {
     auto node = u.extract(u.begin());
     uNodes[routeShardOf(node.key(), us)].push_back(std::move(node));
   }
   auto& m = db.mplsEntries;
-  const unsigned ms = routeShards(m.size());
+  const unsigned ms = db.mplsShards ? db.mplsShards : routeShards(m.size());
   std::vector<std::vector<decltype(m.extract(m.begin()))>> mNodes(ms);
   while (!m.empty()) {
     auto node = m.extract(m.begin());
@@ -542,6 +546,7 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
   // Prefixes go to route shards (one per worker, Parallel.h) so that
   // releaseRouteDb frees each shard on one thread too
   const unsigned shards = routeShards(work.size());
+  routeDb.unicastShards = shards;
   std::vector<std::vector<uint32_t>> shardWork(shards);
   for (size_t i = 0; i < work.size(); ++i) {
     shardWork[routeShardOf(*work[i].prefix, shards)].push_back((uint32_t)i);
@@ -628,6 +633,7 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
     }
   }
   const unsigned labelShards = routeShards(labelJobs.size());
+  routeDb.mplsShards = labelShards;
   std::vector<std::vector<uint32_t>> labelShardJobs(labelShards);
   for (const uint32_t i : labelJobs) {
     labelShardJobs[routeShardOf(labelItems[i].label, labelShards)].push_back(i);

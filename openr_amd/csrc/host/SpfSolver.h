@@ -75,6 +75,9 @@ struct DecisionRouteDb {
   std::unordered_map<thrift::IpPrefix, RibUnicastEntry> unicastEntries;
   std::unordered_map<int32_t, RibMplsEntry> mplsEntries;
   thrift::RouteDatabase toThrift() const;
+  // route shards buildRouteDb used (Parallel.h routeShards): releaseRouteDb
+  // frees with the same split (0 = derive it from the route count)
+  unsigned unicastShards{0}, mplsShards{0};
 };
 
 struct DecisionRouteUpdate {

@@ -1338,6 +1338,80 @@ PYBIND11_MODULE(_oracle_ref, m) {
       py::arg("row"), py::arg("col"), py::arg("w"), py::arg("link"), py::arg("overloaded"),
       py::arg("sources"), py::arg("ign_off") = py::none(), py::arg("ign") = py::none(),
       py::arg("use_metric") = true, py::arg("want_nh") = true, py::arg("threads") = 1);
+  // The same four summary numbers computed from an ENGINE's output (checker
+  // side of the config-2 golden, tests/golden/summary.py): rows32 uint32
+  // [Q, V] (0xFFFFFFFF = unreached), masks = the queries' next-hop masks back
+  // to back (query q at mask_off[q], V * words words), nbr_ids[nbr_off[q] ..]
+  // = the node id of each mask bit of query q.  Multi-threaded so every
+  // fabric source gets its full mix, not a sample.
+  m.def(
+      "rows_summary",
+      [](py::array_t<uint32_t, py::array::c_style> rows, py::array_t<uint64_t, py::array::c_style> masks,
+         py::array_t<uint64_t, py::array::c_style> maskOff, py::array_t<uint32_t, py::array::c_style> nbrOff,
+         py::array_t<uint32_t, py::array::c_style> nbrIds, unsigned threads) {
+        if (rows.ndim() != 2) throw std::invalid_argument("rows_summary: rows must be [Q, V]");
+        const ssize_t Q = rows.shape(0), V = rows.shape(1);
+        if (maskOff.size() != Q + 1 || nbrOff.size() != Q + 1)
+          throw std::invalid_argument("rows_summary: offsets must have Q + 1 entries");
+        if ((ssize_t)maskOff.data()[Q] > masks.size())
+          throw std::invalid_argument("rows_summary: masks shorter than mask_off[Q]");
+        if ((ssize_t)nbrOff.data()[Q] > nbrIds.size())
+          throw std::invalid_argument("rows_summary: nbr_ids shorter than nbr_off[Q]");
+        py::array_t<uint64_t> res({Q, (ssize_t)4});
+        uint64_t* out = res.mutable_data();
+        const uint32_t* R = rows.data();
+        const uint64_t* M = masks.data();
+        const uint64_t* MO = maskOff.data();
+        const uint32_t* NO = nbrOff.data();
+        const uint32_t* NI = nbrIds.data();
+        std::string err;
+        {
+          py::gil_scoped_release rel;
+          std::atomic<ssize_t> next{0};
+          std::mutex errMu;
+          auto worker = [&]() {
+            for (ssize_t q; (q = next.fetch_add(1)) < Q;) {
+              const uint32_t* r = R + (size_t)q * V;
+              const uint64_t words = (MO[q + 1] - MO[q]) / (uint64_t)std::max<ssize_t>(V, 1);
+              const uint32_t nn = NO[q + 1] - NO[q];
+              uint64_t reached = 0, sum = 0, pairs = 0, mix = 0;
+              for (ssize_t v = 0; v < V; ++v) {
+                if (r[v] == 0xFFFFFFFFu) continue;
+                ++reached;
+                sum += r[v];
+                mix += csr::splitmix64(((uint64_t)r[v] << 24) ^ (uint64_t)v);
+              }
+              for (ssize_t v = 0; v < V; ++v) {
+                const uint64_t* m = M + MO[q] + (uint64_t)v * words;
+                for (uint64_t w = 0; w < words; ++w) {
+                  for (uint64_t b = m[w]; b; b &= b - 1) {
+                    const uint32_t bit = (uint32_t)(w * 64 + __builtin_ctzll(b));
+                    if (bit >= nn) {
+                      std::lock_guard<std::mutex> g(errMu);
+                      err = "rows_summary: mask bit beyond the source's neighbours";
+                      continue;
+                    }
+                    ++pairs;
+                    mix += csr::splitmix64((((uint64_t)v + 1) << 32) | NI[NO[q] + bit]);
+                  }
+                }
+              }
+              out[q * 4 + 0] = reached;
+              out[q * 4 + 1] = sum;
+              out[q * 4 + 2] = pairs;
+              out[q * 4 + 3] = mix;
+            }
+          };
+          std::vector<std::thread> pool;
+          for (unsigned t = 1; t < std::max(1u, threads); ++t) pool.emplace_back(worker);
+          worker();
+          for (auto& t : pool) t.join();
+        }
+        if (!err.empty()) throw std::invalid_argument(err);
+        return res;
+      },
+      py::arg("rows"), py::arg("masks"), py::arg("mask_off"), py::arg("nbr_off"), py::arg("nbr_ids"),
+      py::arg("threads") = 1);
   // distance rows (uint64 [Q, V], ~0 = unreached) of a few sources
   m.def(
       "csr_spf_rows",

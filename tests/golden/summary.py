@@ -55,6 +55,28 @@ def summary_from_spf_result(res, names_by_rank):
 _POP8 = np.array([bin(i).count("1") for i in range(256)], dtype=np.uint8)
 
 
+def summaries_full(rows32, masks, words, nbrs, threads=None):
+    """Every query's four numbers (mix included) from the engine's rows,
+    computed by the oracle extension's multi-threaded rows_summary (checker
+    code, oracle/ref_decision.cpp) -- the pure numpy path below is too slow
+    to expand every (node, next hop) pair of a 9,976-source batch."""
+    import os
+
+    from oracle import _oracle_ref as O
+
+    Q, V = rows32.shape
+    words = np.asarray(words, dtype=np.uint64)
+    mask_off = np.zeros(Q + 1, dtype=np.uint64)
+    mask_off[1:] = np.cumsum(np.uint64(V) * words)
+    nbr_off = np.zeros(Q + 1, dtype=np.uint32)
+    nbr_off[1:] = np.cumsum([len(n) for n in nbrs])
+    nbr_ids = np.concatenate([np.asarray(n, dtype=np.uint32) for n in nbrs] or [np.zeros(0, np.uint32)])
+    if len(nbr_ids) == 0:
+        nbr_ids = np.zeros(1, dtype=np.uint32)
+    return O.rows_summary(np.ascontiguousarray(rows32, dtype=np.uint32), np.ascontiguousarray(masks),
+                          mask_off, nbr_off, nbr_ids, threads or min(16, os.cpu_count() or 1))
+
+
 def summaries_from_rows(rows32, masks, words, nbrs, mix_rows=()):
     """Engine output of a batch -> uint64 [Q, 4].
 

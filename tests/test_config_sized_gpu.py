@@ -4,10 +4,10 @@ itself cross-checked there against the reference-style oracle and the literal
 DijkstraQ replay) and against size-independent properties.
 
   config 2  all 9,976 fabric sources in ONE batch (the msbfs+levels plan):
-            per-source (reached, sum of distances, next-hop pairs) for every
-            source, the order-free mix of every (node, distance) and (node,
-            next hop) pair for 512 sampled sources, the reference-form digest
-            of the 8 fabric_sampled.json sources.
+            per-source (reached, sum of distances, next-hop pairs) AND the
+            order-free mix of every (node, distance) and (node, next hop) pair
+            for EVERY source, the reference-form digest of the 8
+            fabric_sampled.json sources.
   config 3  the 100k-node / 1M-link WAN, all 100,000 sources through
             ShardedAllSources (world 1, push-only delta-stepping): the
             reference's own checksum of row n0, 32 sampled rows by sha256, and
@@ -27,7 +27,7 @@ import numpy as np
 import pytest
 
 from tests.golden.make_golden import FABRIC_SOURCES, digest, spf_canon
-from tests.golden.summary import summaries_from_rows
+from tests.golden.summary import summaries_from_rows, summaries_full
 
 pytestmark = pytest.mark.gpu
 
@@ -35,6 +35,7 @@ GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def _batch_summaries(q, g, sources, mix_rows):
+    """mix_rows=None: every query's mix (oracle rows_summary, threaded)."""
     n = len(sources)
     V = g.V
     rows = np.empty((n, V), dtype=np.uint32)
@@ -48,12 +49,16 @@ def _batch_summaries(q, g, sources, mix_rows):
         if s not in nbr_cache:
             nbr_cache[s] = g.nbrs(s)
         nbrs.append(nbr_cache[s])
+    if mix_rows is None:
+        return summaries_full(rows, masks, words, nbrs)
     return summaries_from_rows(rows, masks, words, nbrs, mix_rows)
 
 
 def _check_summary(got, want, mix_rows, what):
     bad = np.nonzero((got[:, :3] != want[:, :3]).any(axis=1))[0]
     assert len(bad) == 0, f"{what}: {len(bad)} queries differ, first {bad[:5].tolist()}"
+    if mix_rows is None:
+        mix_rows = range(len(want))
     mr = np.asarray(sorted(mix_rows), dtype=np.int64)
     bad = mr[got[mr, 3] != want[mr, 3]]
     assert len(bad) == 0, f"{what}: mix differs for queries {bad[:5].tolist()}"
@@ -74,9 +79,8 @@ def test_config2_fabric_all_sources_msbfs(gpu_ready):
     q.run()
     _, names_by_rank = topo.rank()
     sampled_ids = [names_by_rank.index(s) for s in FABRIC_SOURCES]
-    mix_rows = sorted(set(range(0, V, V // 512)) | set(sampled_ids))
-    got = _batch_summaries(q, g, sources, mix_rows)
-    _check_summary(got, want, mix_rows, "fabric all-sources")
+    got = _batch_summaries(q, g, sources, None)  # every source's full mix
+    _check_summary(got, want, None, "fabric all-sources")
     gold = json.load(open(os.path.join(GOLD, "fabric_sampled.json")))
     for src, sid in zip(FABRIC_SOURCES, sampled_ids):
         d = q.dist(sid)
@@ -156,10 +160,8 @@ def test_config5_whatif_batch_c_abi(gpu_ready):
         g = abi.Graph(csr)
         srcs = np.full(n, sid, dtype=np.uint32)
         q = g.query(srcs, abi.SPF_F_NEXTHOPS, ignore=[[int(l)] for l in links]).run()
-        mix_rows = sorted(set(range(0, n, 16)) | {s["query"] for m in meta["areas"] if m["area"] == area
-                                                  for s in m["sampled"]})
-        got = _batch_summaries(q, g, srcs, mix_rows)
-        _check_summary(got, want[off:off + n], mix_rows, f"what-if area {area}")
+        got = _batch_summaries(q, g, srcs, None)  # every query's full mix
+        _check_summary(got, want[off:off + n], None, f"what-if area {area}")
         off += n
         q.close()
         g.close()

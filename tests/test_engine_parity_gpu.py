@@ -248,3 +248,52 @@ def test_selective_memo_invalidation(mods, seed):
     c = E.get_counters()
     assert c.get("decision.spf_memo_kept", 0) > 0
     assert c.get("decision.spf_memo_dropped", 0) > 0
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_kth_paths_beyond_two(mods, seed):
+    """getKthPaths accepts any k (LinkState.cpp:760-789: linksToIgnore = the
+    links of every lower rank).  k = 5 asked FIRST on a fresh LinkState fills
+    ranks 1..4 on the way (a k >= 3 fill used to re-lock its own
+    fill lock); then k = 3, 4 hit the memo.  Paths equal the oracle's."""
+    E, O = mods
+    names, adj_dbs, prefix_dbs = RZ.random_network(800 + seed, n_nodes=20, n_links=70)
+    ea, _ = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    oa, _ = RZ.load(O, adj_dbs, prefix_dbs, seed)
+    src = names[0]
+    for d in names[1:8]:
+        for k in (5, 3, 4, 1, 2):
+            assert _paths(ea["0"], src, d, k) == _paths(oa["0"], src, d, k), (d, k)
+
+
+def test_spf_runs_fb303_count_per_spf(mods):
+    """decision.spf_runs is a COUNT stat bumped once per runSpf (LinkState.cpp:
+    813): a what-if batch of n queries exports .count == n, equal to the sum."""
+    E, _ = mods
+    names, adj_dbs, prefix_dbs = RZ.random_network(9, n_nodes=20, n_links=40)
+    ea, _ = RZ.load(E, adj_dbs, prefix_dbs, 1)
+    ls = ea["0"]
+    links = list(ls.linksFromNode(names[0]))
+    E.reset_counters()
+    ls.runSpfBatch(names[0], [[l] for l in links], True)
+    got = E.get_counters()["decision.spf_runs"]
+    assert got == len(links)
+    assert E.get_fb303_counters()["decision.spf_runs.count"] == got
+
+
+def test_invalidate_drops_every_view(mods):
+    """LinkState::invalidate releases the device graph and every memoized
+    result: the next getSpfResult runs a new SPF (spf_runs + 1) and still
+    equals the oracle's."""
+    E, O = mods
+    names, adj_dbs, prefix_dbs = RZ.random_network(10, n_nodes=20, n_links=40)
+    ea, _ = RZ.load(E, adj_dbs, prefix_dbs, 1)
+    oa, _ = RZ.load(O, adj_dbs, prefix_dbs, 1)
+    ls = ea["0"]
+    ls.getSpfResult(names[0], True)
+    E.reset_counters()
+    ls.getSpfResult(names[0], True)
+    assert E.get_counters().get("decision.spf_runs", 0) == 0  # memo hit
+    ls.invalidate()
+    _spf_equal(ls, oa["0"], names[0], True)
+    assert E.get_counters().get("decision.spf_runs", 0) == 1

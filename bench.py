@@ -174,24 +174,75 @@ def _oracle_spf_worker(args):
 
 
 def _roofline(kernel, avg_ms, alg_bytes, traffic, traffic_src):
-    """Roofline of the dominant kernel: `achieved` / `frac` from the PMC HBM
-    bytes per launch (rocprofv3 FETCH_SIZE/WRITE_SIZE of this code, committed
-    under profiles/) over the launch time measured live here; the compulsory
-    (algorithmic) bytes and their rate are reported beside them."""
+    """Roofline of the dominant kernel: `achieved` / `frac` = ALGORITHMIC
+    bytes per launch (the compulsory bytes DESIGN.md §3 restates for this
+    kernel) over its launch time measured live here (HIP events on the
+    engine's stream).  The rocprofv3 PMC HBM bytes of the same launch
+    (profiles/<round>/pmc_traffic.json) are `traffic`; `traffic_frac` is the
+    bandwidth they spent and `traffic_over_algorithmic` the waste factor."""
     out = {"bound": "hbm", "kernel": kernel, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "avg_launch_ms": avg_ms, "traffic": traffic, "traffic_source": traffic_src,
-           "algorithmic_bytes": alg_bytes}
-    if traffic and avg_ms:
-        a = traffic / (avg_ms / 1e3) / 1e9
-        out.update(achieved=round(a, 1), frac=round(a / HBM_PEAK_GBS, 4),
-                   basis="PMC HBM bytes per launch / live HIP-event launch time")
+           "avg_launch_ms": avg_ms, "algorithmic_bytes": alg_bytes, "traffic": traffic,
+           "traffic_source": traffic_src}
     if alg_bytes and avg_ms:
         a = alg_bytes / (avg_ms / 1e3) / 1e9
-        out.update(algorithmic_achieved=round(a, 1), algorithmic_frac=round(a / HBM_PEAK_GBS, 4))
-        if "achieved" not in out:
-            out.update(achieved=out["algorithmic_achieved"], frac=out["algorithmic_frac"],
-                       basis="algorithmic bytes (no PMC profile of this kernel committed)")
+        out.update(achieved=round(a, 1), frac=round(a / HBM_PEAK_GBS, 4),
+                   basis="algorithmic bytes per launch / live HIP-event launch time")
+    if traffic and avg_ms:
+        t = traffic / (avg_ms / 1e3) / 1e9
+        out.update(traffic_achieved=round(t, 1), traffic_frac=round(t / HBM_PEAK_GBS, 4))
+        if alg_bytes:
+            out["traffic_over_algorithmic"] = round(traffic / alg_bytes, 3)
     return out
+
+
+def _routedb_golden():
+    """Oracle-made RouteDbs of "2-0-0" (tests/golden/make_routedb_golden.py)."""
+    from tests.golden import routes as R
+
+    return R, R.load(os.path.join(ROOT, "tests", "golden", "fabric_routedb.json.gz"))
+
+
+def _golden_state(R, gold, section, state):
+    """Per-route hashes of one golden state (base, or base + its delta)."""
+    sec = gold[section]
+    if state == "base":
+        return sec["base"]["hashes"]
+    return R.apply_delta(sec["base"]["hashes"], sec[state]["delta_vs_base"])
+
+
+def _check_routedb(R, got_db, want, what):
+    try:
+        R.compare(R.route_hashes(got_db), want, what)
+        return None
+    except AssertionError as e:
+        return str(e)
+
+
+def _routedb_parity(section, ls, solver, areas, ps, dbs, topo, node="2-0-0"):
+    """The bench's RouteDb against the oracle's golden: the base state, then
+    the first overload toggle of the timed loop (applied and reverted)."""
+    R, gold = _routedb_golden()
+    if gold["node"] != node:
+        return f"golden is for {gold['node']}"
+    errs = []
+    e = _check_routedb(R, solver.buildRouteDb(node, areas, ps), _golden_state(R, gold, section, "base"),
+                       f"{section} base")
+    if e:
+        errs.append(e)
+    rsw = [i for i, n in enumerate(topo.names) if n.startswith("3-")][0]
+    state = f"overload:{topo.names[rsw]}"
+    if state in gold[section]:
+        dbs[rsw].isOverloaded = True
+        ls.updateAdjacencyDatabase(dbs[rsw])
+        e = _check_routedb(R, solver.buildRouteDb(node, areas, ps), _golden_state(R, gold, section, state),
+                           f"{section} {state}")
+        if e:
+            errs.append(e)
+        dbs[rsw].isOverloaded = False
+        ls.updateAdjacencyDatabase(dbs[rsw])
+    else:
+        errs.append(f"golden lacks {section}/{state}")
+    return "ok (oracle golden: base + " + state + ")" if not errs else "; ".join(errs)
 
 
 def cpu_baseline_all_cores(topo, num_sws, per_core_s=12.0, t_per_spf=None):
@@ -270,7 +321,7 @@ def cpu_baseline(topo, sample):
     }
 
 
-def _rebuild_loop(M, topo, iters, timed, fwd=(0, 0), after_cold=None):
+def _rebuild_loop(M, topo, iters, timed, fwd=(0, 0), after_cold=None, check=None):
     """DecisionBenchmark BM_DecisionFabric loop (DecisionBenchmark.cpp:
     600-626): toggle an RSW's overload bit, rebuild the RouteDb of "2-0-0".
     fwd = (PrefixForwardingType, PrefixForwardingAlgorithm) of every prefix;
@@ -308,6 +359,12 @@ def _rebuild_loop(M, topo, iters, timed, fwd=(0, 0), after_cold=None):
     med = lambda x: round(sorted(x)[len(x) // 2], 3)  # noqa: E731
     out = {"ms_median": med(tot), "update_ms_median": med(upd),
            "build_ms_median": med(bld), "routes": routes, "samples": len(tot)}
+    if check is not None:
+        # after the timed loop, on the same LinkState / solver (untimed)
+        try:
+            out["parity_check"] = check(ls, solver, areas, ps, dbs)
+        except Exception as e:  # reported, never silently replaced
+            out["parity_check"] = f"error: {e!r}"
     if rel:
         # freeing the old RouteDb (releaseRouteDb, in ms_median)
         out["release_ms_median"] = med(rel)
@@ -376,8 +433,14 @@ def route_db_rebuild_ms(topo, device, iters=5):
         nu, nm, us, free_us = solver.buildRouteDbTimed("2-0-0", areas, ps)
         return nu + nm, us, free_us
 
-    out = _rebuild_loop(E, topo, iters, timed, after_cold=E.reset_counters)
-    c = E.get_counters()
+    counters = {}
+
+    def check(ls, solver, areas, ps, dbs):
+        counters.update(E.get_counters())  # the timed builds' counters, before the check's
+        return _routedb_parity("sp_ecmp", ls, solver, areas, ps, dbs, topo)
+
+    out = _rebuild_loop(E, topo, iters, timed, after_cold=E.reset_counters, check=check)
+    c = counters or E.get_counters()
     n = max(1, c.get("decision.route_build_runs", 1))
     # warm builds only (counters reset after the cold build)
     out["per_build_us"] = {
@@ -395,11 +458,6 @@ def route_db_rebuild_ms(topo, device, iters=5):
     out["node"] = "2-0-0"
     out["what"] = "adj-db update (RSW overload toggle) + buildRouteDb, LFA off"
     return out
-
-
-def _unicast_delta(new, old):
-    """getRouteDelta (Decision.cpp:47-85) over unicast route dicts."""
-    return {k: v for k, v in new.items() if old.get(k) != v}, sorted(k for k in old if k not in new)
 
 
 def all_nodes_route_table(topo, device, reps=3):
@@ -430,13 +488,21 @@ def all_nodes_route_table(topo, device, reps=3):
         rt.append(table.route_ms)
     V, P, NL = table.num_nodes, table.num_prefixes, table.num_label_columns
     routes = table.count_routes()
-    solver = E.SpfSolver("2-0-0", True, False)
+    # parity against the ORACLE's RouteDbs (tests/golden/fabric_routedb.json.gz),
+    # not against this engine's own buildRouteDb
+    R, gold = _routedb_golden()
     names = sorted(topo.names)
-    bad = 0
+    bad = []
     for node in ("2-0-0", names[len(names) // 2], names[-1]):
-        db = solver.buildRouteDb(node, areas, ps)
-        if table.routes(node) != db["unicast"] or table.mpls_routes(node) != db["mpls"]:
-            bad += 1
+        got = R.route_hashes({"unicast": table.routes(node), "mpls": table.mpls_routes(node)})
+        if node == gold["node"]:
+            e = _check_routedb(R, {"unicast": table.routes(node), "mpls": table.mpls_routes(node)},
+                               _golden_state(R, gold, "sp_ecmp", "base"), node)
+            if e:
+                bad.append(e)
+        elif R.digest(got) != gold["nodes"][node]["digest"]:
+            bad.append(f"{node}: digest differs ({len(got['unicast'])} unicast, {len(got['mpls'])} mpls "
+                       f"vs {gold['nodes'][node]['num_unicast']}, {gold['nodes'][node]['num_mpls']})")
     n_mat, us_mat = table.routes_timed("2-0-0")
     # the same table with loop-free alternates (SPF_RT_LFA): per-link metrics
     # for every (node, column, up link) -- (P + labels) x E cells
@@ -446,9 +512,8 @@ def all_nodes_route_table(topo, device, reps=3):
         lt = E.AllNodesRouteTable(areas, "0", ps, True, True)
         lfa_walls.append((time.perf_counter() - t0) * 1e3)
         lfa_rt.append(lt.route_ms)
-    lsolver = E.SpfSolver("2-0-0", True, True)
-    ldb = lsolver.buildRouteDb("2-0-0", areas, ps)
-    lfa_ok = lt.routes("2-0-0") == ldb["unicast"] and lt.mpls_routes("2-0-0") == ldb["mpls"]
+    lfa_err = _check_routedb(R, {"unicast": lt.routes("2-0-0"), "mpls": lt.mpls_routes("2-0-0")},
+                             _golden_state(R, gold, "sp_ecmp_lfa", "base"), "LFA 2-0-0")
     del lt
     # network-wide route delta of one RSW drain (DecisionBenchmark's churn):
     # rebuild the table on the drained topology, diff it on the device
@@ -463,8 +528,13 @@ def all_nodes_route_table(topo, device, reps=3):
     t2 = time.perf_counter()
     changed = np.asarray(changed, dtype=np.int64)
     upd, dele = drained.delta("2-0-0")
-    delta_ok = (upd, sorted(dele)) == _unicast_delta(solver.buildRouteDb("2-0-0", areas, ps)["unicast"],
-                                                     table.routes("2-0-0"))
+    # the oracle's getRouteDelta of this drain: the golden overload state's
+    # delta vs base (unicast part)
+    state = f"overload:{topo.names[rsw]}"
+    want = gold["sp_ecmp"][state]["delta_vs_base"]["unicast"] if state in gold["sp_ecmp"] else None
+    got = {R.key_str(k): R.route_hash(v) for k, v in upd.items()}
+    got.update({R.key_str(k): None for k in dele})
+    delta_ok = want is not None and got == want
     # algorithmic bytes of spf_route_table_kernel per launch: per (node,
     # prefix) cell the metric + best words written, the link mask written
     # (8 B x link words of the node), the announcer's distance read and its
@@ -491,17 +561,20 @@ def all_nodes_route_table(topo, device, reps=3):
                                   "unit": "GB/s", "frac": round(alg / (k_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                                   "traffic": rt_traffic, "traffic_source": rt_src},
         "materialise_one_node_ms": round(us_mat / 1e3, 3), "materialised_routes": n_mat,
-        "parity_check": "ok" if bad == 0 else f"{bad} nodes differ",
+        "parity_check": "ok (oracle goldens: 2-0-0 per route, 2 more nodes by digest)" if not bad
+                        else "; ".join(bad),
         "lfa_table": {"what": "same table with loop-free alternates (SPF_RT_LFA, per-link metrics)",
                       "build_ms_min": round(min(lfa_walls), 2),
                       "route_kernel_ms_min": round(min(lfa_rt), 3),
-                      "parity_check": "ok" if lfa_ok else "2-0-0 differs from buildRouteDb(LFA)"},
+                      "parity_check": "ok (oracle golden)" if not lfa_err else lfa_err},
         "drain_delta": {
             "what": f"RSW {topo.names[rsw]} drained: table rebuilt + spf_route_table_diff_kernel = "
                     "getRouteDelta of every node at once",
             "table_rebuild_ms": round((t1 - t0) * 1e3, 2), "diff_ms": round((t2 - t1) * 1e3, 3),
             "changed_cells": int(changed.sum()), "nodes_with_changes": int((changed > 0).sum()),
-            "parity_check": "ok" if delta_ok else "2-0-0 delta differs from getRouteDelta",
+            "parity_check": "ok (oracle golden delta)" if delta_ok
+                            else f"2-0-0 delta differs from the oracle's ({len(got)} vs "
+                                 f"{None if want is None else len(want)} routes)",
         },
     }
 
@@ -522,10 +595,16 @@ def ksp2_route_db(topo, device, iters=2):
         nu, nm, us, free_us = solver.buildRouteDbTimed("2-0-0", areas, ps)
         return nu + nm, us, free_us
 
+    counters = {}
+
+    def check(ls, solver, areas, ps, dbs):
+        counters.update(E.get_counters())  # the timed builds' counters, before the check's
+        return _routedb_parity("ksp2", ls, solver, areas, ps, dbs, topo)
+
     out = _rebuild_loop(E, topo, iters, timed, (T.PrefixForwardingType.SR_MPLS,
                                                 T.PrefixForwardingAlgorithm.KSP2_ED_ECMP),
-                        after_cold=E.reset_counters)
-    c = E.get_counters()
+                        after_cold=E.reset_counters, check=check)
+    c = counters or E.get_counters()
     n = max(1, c.get("decision.route_build_runs", 1))
     out["per_build"] = {
         "spf_runs": round(c.get("decision.spf_runs", 0) / n, 1),

@@ -376,6 +376,35 @@ int spf_table_device_buffers(
     spf_table* t, uint32_t local, void** rows, void** masks, uint64_t* mask_cap_words);
 int spf_table_kernel_name(spf_table* t, uint32_t local, const char** name);
 
+/* ---- persistent cluster graphs + query tables ----
+ * One spf_graph per local device of a cluster, created once per area and
+ * topology and kept across batches (the host LinkState patches it with the
+ * same overload / metric churn as its single-device graph), instead of one
+ * graph upload per device per table.  Over it, spf_table_create_q shards ANY
+ * query batch -- with per-query ignore lists -- over the ranks in contiguous
+ * blocks: KSP2 second passes by destination (LinkState::getKthPaths k = 2,
+ * runSpf(src, true, linksToIgnore) at LinkState.cpp:776-777), what-if by
+ * failed link (runSpf with linksToIgnore, LinkState.cpp:842-847), LFA by
+ * neighbour (getSpfResult per neighbour, Decision.cpp:1145-1174). */
+typedef struct spf_cgraph spf_cgraph;
+int spf_cgraph_create(spf_cluster* c, const spf_graph_desc* desc, spf_cgraph** out);
+int spf_cgraph_destroy(spf_cgraph* g);
+int spf_cgraph_set_transit(spf_cgraph* g, const uint8_t* node_overloaded);
+int spf_cgraph_patch_metrics(
+    spf_cgraph* g, uint32_t n, const uint32_t* edge_idx, const uint64_t* metric);
+/* The graph of local device `local` (NULL if out of range), e.g. for
+ * spf_graph_num_nbrs / spf_graph_nbrs. */
+spf_graph* spf_cgraph_device_graph(spf_cgraph* g, uint32_t local);
+/* A table over `g` from a full query description: desc->sources /
+ * ignore_offsets / ignore_links as in spf_query_create (offsets of the whole
+ * batch; each rank's block gets its slice), desc->flags SPF_F_UNIT_METRIC /
+ * SPF_F_NEXTHOPS, plus the SPF_T_GATHER_* bits in `flags`.  The table
+ * borrows the graphs (destroy the table before the cgraph).  Rows of 64-bit
+ * plans (spf_table_fetch_rows -> SPF_E_UNSUPPORTED) are left to the caller's
+ * single-device path. */
+int spf_table_create_q(
+    spf_cgraph* g, const spf_query_desc* desc, uint32_t flags, spf_table** out);
+
 #ifdef __cplusplus
 }
 #endif

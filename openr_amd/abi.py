@@ -89,6 +89,12 @@ EXPORTED_SYMBOLS = (
     "spf_table_fetch_nexthops",
     "spf_table_device_buffers",
     "spf_table_kernel_name",
+    "spf_cgraph_create",
+    "spf_cgraph_destroy",
+    "spf_cgraph_set_transit",
+    "spf_cgraph_patch_metrics",
+    "spf_cgraph_device_graph",
+    "spf_table_create_q",
 )
 
 SPF_CLUSTER_ID_BYTES = 128
@@ -161,6 +167,31 @@ class _QueryDesc(C.Structure):
         ("ignore_links", C.POINTER(C.c_uint32)),
         ("flags", C.c_uint32),
     ]
+
+
+def _query_desc(src, flags, ignore=None):
+    """spf_query_desc of uint32 sources and optional per-query ignore lists
+    (link ids; sorted and de-duplicated here).  Returns (desc, keep-alive)."""
+    keep = [src]
+    ioff = ilinks = None
+    if ignore is not None:
+        offs = [0]
+        flat = []
+        for lst in ignore:
+            s = sorted(set(int(x) for x in lst))
+            flat.extend(s)
+            offs.append(len(flat))
+        ioff = np.asarray(offs, dtype=np.uint32)
+        ilinks = np.asarray(flat if flat else [0], dtype=np.uint32)
+        keep += [ioff, ilinks]
+    d = _QueryDesc(
+        len(src),
+        _p(src, C.c_uint32),
+        _p(ioff, C.c_uint32) if ioff is not None else None,
+        _p(ilinks, C.c_uint32) if ilinks is not None else None,
+        flags,
+    )
+    return d, keep
 
 
 _lib = None
@@ -250,6 +281,12 @@ def load():
         "spf_table_fetch_nexthops": (C.c_int, [vp, u32, u32, pu64]),
         "spf_table_device_buffers": (C.c_int, [vp, u32, C.POINTER(vp), C.POINTER(vp), pu64]),
         "spf_table_kernel_name": (C.c_int, [vp, u32, C.POINTER(C.c_char_p)]),
+        "spf_cgraph_create": (C.c_int, [vp, C.POINTER(_GraphDesc), C.POINTER(vp)]),
+        "spf_cgraph_destroy": (C.c_int, [vp]),
+        "spf_cgraph_set_transit": (C.c_int, [vp, C.POINTER(C.c_uint8)]),
+        "spf_cgraph_patch_metrics": (C.c_int, [vp, u32, pu32, pu64]),
+        "spf_cgraph_device_graph": (vp, [vp, u32]),
+        "spf_table_create_q": (C.c_int, [vp, C.POINTER(_QueryDesc), u32, C.POINTER(vp)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -458,25 +495,7 @@ class Query:
         lib = load()
         self.graph = graph
         src = np.ascontiguousarray(sources, dtype=np.uint32)
-        keep = [src]
-        ioff = ilinks = None
-        if ignore is not None:
-            offs = [0]
-            flat = []
-            for lst in ignore:
-                s = sorted(set(int(x) for x in lst))
-                flat.extend(s)
-                offs.append(len(flat))
-            ioff = np.asarray(offs, dtype=np.uint32)
-            ilinks = np.asarray(flat if flat else [0], dtype=np.uint32)
-            keep += [ioff, ilinks]
-        d = _QueryDesc(
-            len(src),
-            _p(src, C.c_uint32),
-            _p(ioff, C.c_uint32) if ioff is not None else None,
-            _p(ilinks, C.c_uint32) if ilinks is not None else None,
-            flags,
-        )
+        d, keep = _query_desc(src, flags, ignore)
         h = C.c_void_p()
         _check(lib.spf_query_create(graph.h, C.byref(d), C.byref(h)), "spf_query_create")
         self.h = h
@@ -674,22 +693,68 @@ class Cluster:
             pass
 
 
-class Table:
-    """All-sources table sharded over a Cluster (spf_table_*)."""
+class ClusterGraph:
+    """One persistent spf_graph per local device of a Cluster (spf_cgraph_*)."""
 
-    def __init__(self, cluster: Cluster, csr: "Csr", sources, flags):
+    def __init__(self, cluster: Cluster, csr: "Csr"):
         lib = load()
         self.cluster = cluster
         self.V = csr.num_nodes
-        src = np.ascontiguousarray(sources, dtype=np.uint32)
         d, keep = _graph_desc(csr, 0)
         h = C.c_void_p()
-        _check_cl(lib.spf_table_create(cluster.h, C.byref(d), len(src), _p(src, C.c_uint32), flags,
-                                       C.byref(h)), "spf_table_create")
+        _check_cl(lib.spf_cgraph_create(cluster.h, C.byref(d), C.byref(h)), "spf_cgraph_create")
+        self.h = h
+        self._keep = keep
+
+    def close(self):
+        if self.h:
+            load().spf_cgraph_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_transit(self, overloaded):
+        ov = np.ascontiguousarray(overloaded, dtype=np.uint8)
+        _check_cl(load().spf_cgraph_set_transit(self.h, _p(ov, C.c_uint8)), "spf_cgraph_set_transit")
+
+    def patch_metrics(self, edges, metrics):
+        e = np.ascontiguousarray(edges, dtype=np.uint32)
+        m = np.ascontiguousarray(metrics, dtype=np.uint64)
+        _check_cl(load().spf_cgraph_patch_metrics(self.h, len(e), _p(e, C.c_uint32), _p(m, C.c_uint64)),
+                  "spf_cgraph_patch_metrics")
+
+    def table(self, sources, flags, ignore=None, gather=0):
+        return Table(self.cluster, None, sources, flags | gather, cgraph=self, ignore=ignore)
+
+
+class Table:
+    """All-sources table sharded over a Cluster (spf_table_*); with `cgraph`
+    a query table over persistent cluster graphs (spf_table_create_q), whose
+    queries may carry ignore lists (one list of link ids per query)."""
+
+    def __init__(self, cluster: Cluster, csr: "Csr", sources, flags, cgraph=None, ignore=None):
+        lib = load()
+        self.cluster = cluster
+        src = np.ascontiguousarray(sources, dtype=np.uint32)
+        h = C.c_void_p()
+        if cgraph is None:
+            self.V = csr.num_nodes
+            d, keep = _graph_desc(csr, 0)
+            _check_cl(lib.spf_table_create(cluster.h, C.byref(d), len(src), _p(src, C.c_uint32), flags,
+                                           C.byref(h)), "spf_table_create")
+        else:
+            self.V = cgraph.V
+            qd, keep = _query_desc(src, flags & 0xFF, ignore)
+            _check_cl(lib.spf_table_create_q(cgraph.h, C.byref(qd), flags & ~0xFF, C.byref(h)),
+                      "spf_table_create_q")
         self.h = h
         self.n = len(src)
         self.flags = flags
-        self._keep = (keep, src)
+        self._keep = (keep, src, cgraph)
 
     def close(self):
         if self.h:

@@ -30,6 +30,11 @@ struct LinkState::Engine {
   std::unordered_map<const Link*, uint32_t> linkIndex;
   std::vector<std::array<uint32_t, 2>> halves; // link id -> half-edge from first/second node
   spf_graph* graph{nullptr};
+  // the same graph on every device of the multi-GPU fan-out (setSpfDevices),
+  // created on the first fanned-out batch and patched with the same churn as
+  // `graph`; cgraphGen = the cluster generation it was built for
+  spf_cgraph* cgraph{nullptr};
+  uint64_t cgraphGen{0};
   // host block the 32-bit rows of a batch land in (runBatch): reused while no
   // view of an earlier batch holds it, so big batches (the KSP2 second
   // passes: 9,975 x 9,976 rows on the fabric) skip the zero fill and the
@@ -51,6 +56,9 @@ struct LinkState::Engine {
   std::mutex devMu;
 
   ~Engine() {
+    if (cgraph) {
+      spf_cgraph_destroy(cgraph);
+    }
     if (graph) {
       spf_graph_destroy(graph);
     }

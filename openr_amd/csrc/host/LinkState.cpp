@@ -129,6 +129,9 @@ struct ClusterState {
   // not destroyed at process exit: RCCL / HIP teardown from a static
   // destructor can run after the runtime's own exit handlers
   spf_cluster* cluster{nullptr};
+  // bumped whenever the device set changes: an Engine's cluster graph of an
+  // older generation is rebuilt for the new devices
+  uint64_t gen{1};
 };
 ClusterState& clusterState() {
   static ClusterState s;
@@ -147,7 +150,17 @@ void setSpfDevices(const std::vector<int>& devices) {
     cs.cluster = nullptr;
   }
   cs.devices = devices;
+  ++cs.gen;
 }
+
+namespace {
+std::atomic<size_t>& clusterMin() {
+  static std::atomic<size_t> n{kClusterMinSources};
+  return n;
+}
+} // namespace
+void setClusterMinSources(size_t n) { clusterMin().store(std::max<size_t>(1, n)); }
+size_t clusterMinSources() { return clusterMin().load(); }
 
 std::vector<int> getSpfDevices() {
   auto& cs = clusterState();
@@ -653,12 +666,18 @@ std::vector<std::unique_ptr<SpfView>> runBatch(
   return out;
 }
 
-// The multi-GPU fan-out of one all-sources batch (setSpfDevices): the
-// sources are split over the cluster's devices in one spf_table run and every
-// block comes back to the host from the device that computed it.  Same
+// The multi-GPU fan-out of one batch (setSpfDevices): the queries are split
+// over the cluster's devices in one spf_table run over the engine's
+// persistent cluster graph (one upload per device per topology, patched in
+// place by patchMemo), each block with its slice of the ignore lists, and
+// every block comes back to the host from the device that computed it.  Same
 // views as runBatch (32-bit rows shared from one block, next-hop masks).
+// Returns no views when a block's plan keeps 64-bit rows (a source with more
+// than 1,024 neighbours, SPF_E_UNSUPPORTED from the row fetch): the caller
+// runs the batch on its single device instead.
 std::vector<std::unique_ptr<SpfView>> runBatchCluster(
-    LinkState::Engine& eng, const std::vector<uint32_t>& sources, bool useLinkMetric) {
+    LinkState::Engine& eng, const std::vector<uint32_t>& sources, bool useLinkMetric,
+    bool wantNextHops, const std::vector<std::vector<uint32_t>>* ignore) {
   const auto tBatch = std::chrono::steady_clock::now();
   auto& cs = clusterState();
   std::lock_guard<std::mutex> g(cs.mu);
@@ -673,16 +692,6 @@ std::vector<std::unique_ptr<SpfView>> runBatchCluster(
   }
   const uint32_t V = (uint32_t)eng.names.size();
   const uint32_t nq = (uint32_t)sources.size();
-  spf_graph_desc d{};
-  d.num_nodes = V;
-  d.num_edges = (uint32_t)eng.col.size();
-  d.row_ptr = eng.row.data();
-  d.col = eng.col.data();
-  d.metric = eng.metric.data();
-  d.link_id = eng.linkId.data();
-  d.rev = eng.rev.data();
-  d.node_overloaded = eng.overloaded.data();
-  d.num_links = (uint32_t)eng.links.size();
   spf_table* t = nullptr;
   auto check = [&](int s, const char* what) {
     if (s != SPF_OK) {
@@ -694,26 +703,71 @@ std::vector<std::unique_ptr<SpfView>> runBatchCluster(
           " (" + spf_cluster_last_error() + " / " + spf_last_error_detail() + ")");
     }
   };
-  check(spf_table_create(cs.cluster, &d, nq, sources.data(),
-                         SPF_F_NEXTHOPS | (useLinkMetric ? 0u : SPF_F_UNIT_METRIC), &t),
-        "spf_table_create");
+  if (eng.cgraph && eng.cgraphGen != cs.gen) {
+    spf_cgraph_destroy(eng.cgraph); // built for another device set
+    eng.cgraph = nullptr;
+  }
+  if (!eng.cgraph) {
+    spf_graph_desc d{};
+    d.num_nodes = V;
+    d.num_edges = (uint32_t)eng.col.size();
+    d.row_ptr = eng.row.data();
+    d.col = eng.col.data();
+    d.metric = eng.metric.data();
+    d.link_id = eng.linkId.data();
+    d.rev = eng.rev.data();
+    d.node_overloaded = eng.overloaded.data();
+    d.num_links = (uint32_t)eng.links.size();
+    const auto tc = std::chrono::steady_clock::now();
+    check(spf_cgraph_create(cs.cluster, &d, &eng.cgraph), "spf_cgraph_create");
+    eng.cgraphGen = cs.gen;
+    Counters::add("decision.cluster_graph_uploads", 1);
+    Counters::add("decision.cluster_graph_upload_us",
+                  std::chrono::duration_cast<std::chrono::microseconds>(
+                      std::chrono::steady_clock::now() - tc)
+                      .count());
+  }
+  std::vector<uint32_t> ioff, ilinks;
+  spf_query_desc qd{};
+  qd.num_queries = nq;
+  qd.sources = sources.data();
+  qd.flags = (wantNextHops ? SPF_F_NEXTHOPS : 0u) | (useLinkMetric ? 0u : SPF_F_UNIT_METRIC);
+  if (ignore) {
+    ioff.push_back(0);
+    for (const auto& l : *ignore) {
+      ilinks.insert(ilinks.end(), l.begin(), l.end());
+      ioff.push_back((uint32_t)ilinks.size());
+    }
+    qd.ignore_offsets = ioff.data();
+    qd.ignore_links = ilinks.data();
+  }
+  check(spf_table_create_q(eng.cgraph, &qd, 0, &t), "spf_table_create_q");
   check(spf_table_run(t), "spf_table_run");
   check(spf_table_sync(t), "spf_table_sync");
   float cm = 0, gm = 0;
   check(spf_table_elapsed_ms(t, &cm, &gm), "spf_table_elapsed_ms");
   eng.lastMs = cm + gm;
   Counters::add("decision.spf_device_us", (int64_t)(eng.lastMs * 1000.0f));
-  Counters::add("decision.spf_cluster_batches", 1);
   auto rows32 = std::make_shared<std::vector<uint32_t>>((size_t)nq * V);
-  check(spf_table_fetch_rows(t, 0, nq, rows32->data()), "spf_table_fetch_rows");
-  std::vector<uint32_t> words(nq);
-  std::vector<uint64_t> maskOff(nq + 1, 0);
-  for (uint32_t i = 0; i < nq; ++i) {
-    words[i] = (uint32_t)spf_table_nh_words(t, i);
-    maskOff[i + 1] = maskOff[i] + (uint64_t)V * words[i];
+  if (const int s = spf_table_fetch_rows(t, 0, nq, rows32->data()); s == SPF_E_UNSUPPORTED) {
+    spf_table_destroy(t); // 64-bit rows in some block: the caller's single-device path
+    Counters::add("decision.spf_cluster_fallbacks", 1);
+    return {};
+  } else {
+    check(s, "spf_table_fetch_rows");
   }
-  std::vector<uint64_t> masks(maskOff[nq]);
-  check(spf_table_fetch_nexthops(t, 0, nq, masks.data()), "spf_table_fetch_nexthops");
+  Counters::add("decision.spf_cluster_batches", 1);
+  std::vector<uint32_t> words(nq, 1);
+  std::vector<uint64_t> maskOff(nq + 1, 0);
+  std::vector<uint64_t> masks;
+  if (wantNextHops) {
+    for (uint32_t i = 0; i < nq; ++i) {
+      words[i] = (uint32_t)spf_table_nh_words(t, i);
+      maskOff[i + 1] = maskOff[i] + (uint64_t)V * words[i];
+    }
+    masks.resize(maskOff[nq]);
+    check(spf_table_fetch_nexthops(t, 0, nq, masks.data()), "spf_table_fetch_nexthops");
+  }
   spf_table_destroy(t);
   t = nullptr;
   std::vector<std::unique_ptr<SpfView>> out(nq);
@@ -722,12 +776,17 @@ std::vector<std::unique_ptr<SpfView>> runBatchCluster(
     view->src = sources[i];
     view->useLinkMetric = useLinkMetric;
     view->dist.share32(rows32, i * V, V);
-    view->words = words[i];
-    view->nh.assign(masks.begin() + maskOff[i], masks.begin() + maskOff[i + 1]);
-    const int nn = spf_graph_num_nbrs(eng.graph, sources[i]);
-    view->nbrs.resize(std::max(nn, 0));
-    if (nn > 0) {
-      spf_graph_nbrs(eng.graph, sources[i], view->nbrs.data());
+    if (wantNextHops) {
+      view->words = words[i];
+      view->nh.assign(masks.begin() + maskOff[i], masks.begin() + maskOff[i + 1]);
+      const int nn = spf_graph_num_nbrs(eng.graph, sources[i]);
+      view->nbrs.resize(std::max(nn, 0));
+      if (nn > 0) {
+        spf_graph_nbrs(eng.graph, sources[i], view->nbrs.data());
+      }
+    }
+    if (ignore) {
+      view->ignored = (*ignore)[i];
     }
     out[i] = std::move(view);
   }, 8);
@@ -739,6 +798,22 @@ std::vector<std::unique_ptr<SpfView>> runBatchCluster(
     Counters::add("decision.spf_ms", (int64_t)(batchMs / (double)nq));
   }
   return out;
+}
+
+// One device batch on the fan-out devices when they are configured and the
+// batch is big enough (kClusterMinSources) on a 32-bit plan, else (or when a
+// block needs 64-bit rows) on the area's own device.  Caller holds devMu.
+std::vector<std::unique_ptr<SpfView>> runBatchAuto(
+    LinkState::Engine& eng, const std::vector<uint32_t>& sources, bool useLinkMetric,
+    bool wantNextHops, const std::vector<std::vector<uint32_t>>* ignore) {
+  if (sources.size() >= clusterMinSources() && !(eng.exact && useLinkMetric) &&
+      !getSpfDevices().empty()) {
+    auto views = runBatchCluster(eng, sources, useLinkMetric, wantNextHops, ignore);
+    if (!views.empty()) {
+      return views;
+    }
+  }
+  return runBatch(eng, sources, useLinkMetric, wantNextHops, ignore);
 }
 
 // Predecessors of v in the reference's pathLinks order: usable in-links whose
@@ -1061,6 +1136,12 @@ void LinkState::patchMemo(
       if (s != SPF_OK) {
         engineFailure("spf_graph_set_transit", s);
       }
+      if (eng.cgraph) {
+        const int c = spf_cgraph_set_transit(eng.cgraph, eng.overloaded.data());
+        if (c != SPF_OK) {
+          engineFailure("spf_cgraph_set_transit", c);
+        }
+      }
     }
     if (!edges.empty()) {
       for (size_t i = 0; i < edges.size(); ++i) {
@@ -1070,6 +1151,13 @@ void LinkState::patchMemo(
           eng.graph, (uint32_t)edges.size(), edges.data(), metrics.data());
       if (s != SPF_OK) {
         engineFailure("spf_graph_patch_metrics", s);
+      }
+      if (eng.cgraph) {
+        const int c = spf_cgraph_patch_metrics(
+            eng.cgraph, (uint32_t)edges.size(), edges.data(), metrics.data());
+        if (c != SPF_OK) {
+          engineFailure("spf_cgraph_patch_metrics", c);
+        }
       }
       eng.exact = spf_graph_needs_exact(eng.graph) != 0;
     }
@@ -1437,10 +1525,7 @@ void LinkState::prefetchSpf(const std::vector<std::string>& nodes, bool useLinkM
     return;
   }
   // the multi-GPU fan-out for big batches on the fast (32-bit) plans
-  const bool fanOut = !getSpfDevices().empty() && todo.size() >= kClusterMinSources &&
-      !(eng.exact && useLinkMetric);
-  auto views = fanOut ? runBatchCluster(eng, todo, useLinkMetric)
-                      : runBatch(eng, todo, useLinkMetric, true, nullptr);
+  auto views = runBatchAuto(eng, todo, useLinkMetric, true, nullptr);
   for (size_t i = 0; i < todo.size(); ++i) {
     pre.emplace(todo[i], std::move(views[i]));
   }
@@ -1526,7 +1611,7 @@ std::unique_ptr<LinkState::SpfBatch> LinkState::runSpfBatch(
   std::vector<uint32_t> sources(nq, sid->second);
   {
     std::lock_guard<std::mutex> dev(eng.devMu);
-    batch->views_ = runBatch(eng, sources, useLinkMetric, true, &lists);
+    batch->views_ = runBatchAuto(eng, sources, useLinkMetric, true, &lists);
   }
   return batch;
 }
@@ -1932,8 +2017,10 @@ void LinkState::prefetchKthPaths(
   }
   std::vector<std::unique_ptr<SpfView>> views;
   {
+    // the second passes of many destinations: fanned out by destination
+    // when devices are configured (distances only: a trace reads no masks)
     std::lock_guard<std::mutex> dev(eng.devMu);
-    views = runBatch(eng, sources, true, false, &lists);
+    views = runBatchAuto(eng, sources, true, false, &lists);
   }
   std::unique_lock<std::shared_mutex> wr(eng.viewMu);
   for (size_t i = 0; i < views.size(); ++i) {

@@ -492,14 +492,20 @@ struct Counters {
 void setSpfDevice(int device);
 int getSpfDevice();
 // Devices of the multi-GPU fan-out: when non-empty,
-// LinkState::prefetchSpf batches of at least kClusterMinSources sources
-// (all-sources views, every node's RouteDb) are split over these devices in
-// one call (spf_cluster_create_local + spf_table_*, one RCCL communicator per
-// device) and every block's rows come back to the host from its own device.
-// Empty (the default) = everything on getSpfDevice().
+// every device batch of at least clusterMinSources() queries on a 32-bit plan
+// -- prefetchSpf (all-sources views, a RouteDb's node + LFA neighbours),
+// prefetchKthPaths (the KSP2 second passes, by destination), runSpfBatch
+// (what-if link failures) -- is split over these devices in one call
+// (spf_cluster_create_local + a persistent spf_cgraph per area + one
+// spf_table_create_q per batch, ignore lists sliced per block) and every
+// block's rows come back to the host from its own device.  Empty (the
+// default) = everything on getSpfDevice().
 void setSpfDevices(const std::vector<int>& devices);
 std::vector<int> getSpfDevices();
 constexpr size_t kClusterMinSources = 64;
+// the fan-out threshold (default kClusterMinSources; tests lower it)
+void setClusterMinSources(size_t n);
+size_t clusterMinSources();
 
 } // namespace openr
 

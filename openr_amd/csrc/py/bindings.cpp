@@ -157,6 +157,8 @@ PYBIND11_MODULE(_openr_spf, m) {
   m.def("set_spf_device", &setSpfDevice);
   m.def("get_spf_device", &getSpfDevice);
   m.def("set_spf_devices", &setSpfDevices);
+  m.def("set_cluster_min_sources", &setClusterMinSources);
+  m.def("cluster_min_sources", &clusterMinSources);
   m.def("get_spf_devices", &getSpfDevices);
   m.def("get_counters", [] {
     py::dict d;

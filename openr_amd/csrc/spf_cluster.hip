@@ -85,8 +85,15 @@ struct spf_cluster {
   std::vector<ncclComm_t> comms;
 };
 
+struct spf_cgraph {
+  spf_cluster* c = nullptr;
+  uint32_t V = 0;
+  std::vector<spf_graph*> g; // one per local device, c->devices order
+};
+
 struct spf_table {
   spf_cluster* c = nullptr;
+  bool borrowed = false; // graphs belong to an spf_cgraph (not destroyed here)
   uint32_t V = 0, n = 0, flags = 0, cap = 0;
   std::vector<uint32_t> sources;
   std::vector<uint32_t> words;       // next-hop words per source
@@ -98,6 +105,7 @@ struct spf_table {
     uint32_t rank = 0;
     spf_graph* g = nullptr;
     spf_query* q = nullptr;
+    std::vector<uint32_t> ign_off; // this block's ignore offsets, rebased to 0
     uint32_t* rows = nullptr;  // gathered rows [world * cap][V] (GATHER_ROWS)
     uint64_t* masks = nullptr; // gathered masks [world * mask_cap] (GATHER_NEXTHOPS)
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
@@ -232,7 +240,7 @@ static void free_table(spf_table* t) {
     if (L.q) {
       spf_query_destroy(L.q);
     }
-    if (L.g) {
+    if (L.g && !t->borrowed) {
       spf_graph_destroy(L.g);
     }
     if (L.rows) {
@@ -257,25 +265,96 @@ int spf_table_destroy(spf_table* t) {
   return SPF_OK;
 }
 
-int spf_table_create(
-    spf_cluster* c, const spf_graph_desc* desc, uint32_t num_sources, const uint32_t* sources,
-    uint32_t flags, spf_table** out) {
-  SPF_ABI_RANGE_CLUSTER("spf_table_create");
-  if (!c || !desc || !out || (num_sources && !sources)) {
-    return cfail(SPF_E_INVALID, "spf_table_create: null argument");
+// ---- persistent per-device graphs (spf_cgraph) ----
+
+int spf_cgraph_create(spf_cluster* c, const spf_graph_desc* desc, spf_cgraph** out) {
+  SPF_ABI_RANGE_CLUSTER("spf_cgraph_create");
+  if (!c || !desc || !out) {
+    return cfail(SPF_E_INVALID, "spf_cgraph_create: null argument");
   }
+  auto cg = std::make_unique<spf_cgraph>();
+  cg->c = c;
+  cg->V = desc->num_nodes;
+  for (int dev : c->devices) {
+    spf_graph_desc gd = *desc;
+    gd.device = dev;
+    spf_graph* g = nullptr;
+    const int s = spf_graph_create(&gd, &g);
+    if (s != SPF_OK) {
+      spf_cgraph_destroy(cg.release());
+      return s;
+    }
+    cg->g.push_back(g);
+  }
+  *out = cg.release();
+  return SPF_OK;
+}
+
+int spf_cgraph_destroy(spf_cgraph* cg) {
+  if (!cg) {
+    return SPF_OK;
+  }
+  for (spf_graph* g : cg->g) {
+    spf_graph_destroy(g);
+  }
+  delete cg;
+  return SPF_OK;
+}
+
+int spf_cgraph_set_transit(spf_cgraph* cg, const uint8_t* node_overloaded) {
+  if (!cg) {
+    return cfail(SPF_E_INVALID, "spf_cgraph_set_transit: null graph");
+  }
+  for (spf_graph* g : cg->g) {
+    CL_TRY(spf_graph_set_transit(g, node_overloaded));
+  }
+  return SPF_OK;
+}
+
+int spf_cgraph_patch_metrics(
+    spf_cgraph* cg, uint32_t n, const uint32_t* edge_idx, const uint64_t* metric) {
+  if (!cg) {
+    return cfail(SPF_E_INVALID, "spf_cgraph_patch_metrics: null graph");
+  }
+  for (spf_graph* g : cg->g) {
+    CL_TRY(spf_graph_patch_metrics(g, n, edge_idx, metric));
+  }
+  return SPF_OK;
+}
+
+spf_graph* spf_cgraph_device_graph(spf_cgraph* cg, uint32_t local) {
+  return cg && local < cg->g.size() ? cg->g[local] : nullptr;
+}
+
+// The table of queries qd over per-device graphs `graphs` (local device
+// order): contiguous query blocks per rank, each block with its own slice of
+// the ignore lists (rebased offsets), one spf_query per local block.
+static int table_init(
+    spf_table* t, spf_cluster* c, const std::vector<spf_graph*>& graphs, uint32_t V,
+    const spf_query_desc* qd_all, uint32_t flags) {
+  const uint32_t num_sources = qd_all->num_queries;
+  const uint32_t* sources = qd_all->sources;
   const uint32_t qflags = flags & (SPF_F_UNIT_METRIC | SPF_F_NEXTHOPS);
   if ((flags & SPF_T_GATHER_NEXTHOPS) && !(flags & SPF_F_NEXTHOPS)) {
     return cfail(SPF_E_INVALID, "spf_table_create: GATHER_NEXTHOPS needs SPF_F_NEXTHOPS");
   }
+  if (num_sources && !sources) {
+    return cfail(SPF_E_INVALID, "spf_table_create: null sources");
+  }
   for (uint32_t i = 0; i < num_sources; ++i) {
-    if (sources[i] >= desc->num_nodes) {
+    if (sources[i] >= V) {
       return cfail(SPF_E_INVALID, "spf_table_create: source out of range");
     }
   }
-  std::unique_ptr<spf_table, void (*)(spf_table*)> t(new spf_table, free_table);
+  const uint32_t* ioff = qd_all->ignore_offsets;
+  if (ioff && (!qd_all->ignore_links && ioff[num_sources] > 0)) {
+    return cfail(SPF_E_INVALID, "spf_table_create: ignore offsets without links");
+  }
+  if (ioff && ioff[0] != 0) {
+    return cfail(SPF_E_INVALID, "spf_table_create: ignore_offsets[0] != 0");
+  }
   t->c = c;
-  t->V = desc->num_nodes;
+  t->V = V;
   t->n = num_sources;
   t->flags = flags;
   t->sources.assign(sources, sources + num_sources);
@@ -283,12 +362,9 @@ int spf_table_create(
   t->block_first.resize(c->world + 1);
   t->local.resize(c->devices.size());
   for (size_t d = 0; d < c->devices.size(); ++d) {
-    auto& L = t->local[d];
-    L.device = c->devices[d];
-    L.rank = c->first_rank + (uint32_t)d;
-    spf_graph_desc gd = *desc;
-    gd.device = L.device;
-    CL_TRY(spf_graph_create(&gd, &L.g));
+    t->local[d].device = c->devices[d];
+    t->local[d].rank = c->first_rank + (uint32_t)d;
+    t->local[d].g = graphs[d];
   }
   // next-hop words of every source (the gathered mask layout needs all of
   // them; distinct neighbour counts come from the graph, any device)
@@ -303,7 +379,7 @@ int spf_table_create(
     }
   }
   t->mask_off.resize(num_sources);
-  CL_TRY(spf_table_layout(num_sources, c->world, t->V, t->words.data(), t->block_first.data(),
+  CL_TRY(spf_table_layout(num_sources, c->world, V, t->words.data(), t->block_first.data(),
                           t->mask_off.data(), &t->mask_cap));
   for (auto& L : t->local) {
     CL_HIP(hipSetDevice(L.device));
@@ -313,6 +389,14 @@ int spf_table_create(
       qd.num_queries = (uint32_t)count;
       qd.sources = t->sources.data() + first;
       qd.flags = qflags;
+      if (ioff) {
+        L.ign_off.resize(count + 1);
+        for (uint64_t i = 0; i <= count; ++i) {
+          L.ign_off[i] = ioff[first + i] - ioff[first];
+        }
+        qd.ignore_offsets = L.ign_off.data();
+        qd.ignore_links = qd_all->ignore_links + ioff[first];
+      }
       CL_TRY(spf_query_create(L.g, &qd, &L.q));
     }
     if (flags & SPF_T_GATHER_ROWS) {
@@ -325,6 +409,56 @@ int spf_table_create(
     CL_HIP(hipEventCreate(&L.e1));
     CL_HIP(hipEventCreate(&L.e2));
   }
+  return SPF_OK;
+}
+
+int spf_table_create(
+    spf_cluster* c, const spf_graph_desc* desc, uint32_t num_sources, const uint32_t* sources,
+    uint32_t flags, spf_table** out) {
+  SPF_ABI_RANGE_CLUSTER("spf_table_create");
+  if (!c || !desc || !out || (num_sources && !sources)) {
+    return cfail(SPF_E_INVALID, "spf_table_create: null argument");
+  }
+  std::unique_ptr<spf_table, void (*)(spf_table*)> t(new spf_table, free_table);
+  std::vector<spf_graph*> graphs;
+  for (int dev : c->devices) {
+    spf_graph_desc gd = *desc;
+    gd.device = dev;
+    spf_graph* g = nullptr;
+    const int s = spf_graph_create(&gd, &g);
+    if (s != SPF_OK) {
+      for (spf_graph* x : graphs) {
+        spf_graph_destroy(x);
+      }
+      return s;
+    }
+    graphs.push_back(g);
+  }
+  // the table owns these graphs from here on (free_table destroys them)
+  t->local.resize(graphs.size());
+  for (size_t d = 0; d < graphs.size(); ++d) {
+    t->local[d].g = graphs[d];
+  }
+  spf_query_desc qd{};
+  qd.num_queries = num_sources;
+  qd.sources = sources;
+  CL_TRY(table_init(t.get(), c, graphs, desc->num_nodes, &qd, flags));
+  *out = t.release();
+  return SPF_OK;
+}
+
+int spf_table_create_q(spf_cgraph* cg, const spf_query_desc* qd, uint32_t flags, spf_table** out) {
+  SPF_ABI_RANGE_CLUSTER("spf_table_create_q");
+  if (!cg || !qd || !out) {
+    return cfail(SPF_E_INVALID, "spf_table_create_q: null argument");
+  }
+  if (qd->flags & SPF_F_ORDER) {
+    return cfail(SPF_E_UNSUPPORTED, "spf_table_create_q: settle order is single-device");
+  }
+  std::unique_ptr<spf_table, void (*)(spf_table*)> t(new spf_table, free_table);
+  t->borrowed = true;
+  CL_TRY(table_init(t.get(), cg->c, cg->g, cg->V, qd,
+                    flags | (qd->flags & (SPF_F_UNIT_METRIC | SPF_F_NEXTHOPS))));
   *out = t.release();
   return SPF_OK;
 }

@@ -78,6 +78,12 @@ constexpr uint32_t kSettled = 0xFFFFFFFEu;
 
 thread_local std::string g_last_error;
 
+// 0/1 switch from the environment (A/B knobs of the measured variants)
+uint32_t env_flag(const char* name, uint32_t dflt) {
+  const char* v = getenv(name);
+  return v ? (uint32_t)(atoi(v) != 0) : dflt;
+}
+
 int fail(int code, const std::string& what) {
   g_last_error = what;
   return code;
@@ -1965,6 +1971,8 @@ struct NhLevelsArgs {
   uint32_t Vp8;
   uint32_t nq;
   uint32_t scale;
+  uint32_t xcd_swizzle; // 1: XCD-aware block order (OPENR_NL_XCD, default on)
+  uint32_t held_words;  // 1: 2/3-word masks stored node-major from registers (OPENR_NL_HELD)
 };
 
 constexpr uint32_t kNlThreads = 256;
@@ -2185,20 +2193,23 @@ __device__ __forceinline__ void nl_body_multi_staged(
   }
 }
 
-template <bool WIDE>
+// WM = the source's mask words when it is 2 or 3 (finished words are held in
+// registers and a lane's four nodes x WM words leave as one contiguous
+// 32*WM-byte run, so every line of the row is written whole by one wave);
+// WM = 1 the single-word path (wave-contiguous 1 KB stores); WM = 0 any width
+// (word-strided 8-byte stores).
+template <bool WIDE, uint32_t WM>
 __device__ __forceinline__ void nl_body_multi(
     const NhLevelsArgs& a, uint32_t q, uint32_t s, uint32_t c0, uint32_t c1,
     uint32_t* st_row, uint32_t* st_node) {
-  const uint32_t Wm = a.nh_w[q];
+  const uint32_t Wm = WM ? WM : a.nh_w[q];
   uint64_t* nhrow = a.nh_out + a.nh_off[q];
   const uint32_t none = WIDE ? kInf32 : 255u;
   const uint64_t step = WIDE ? (uint64_t)a.scale : 1ull;
   const uint32_t beg = a.nbr_off[s], n = a.nbr_off[s + 1] - beg;
   // every neighbour staged once (n <= kNlStage; bigger sources take
-  // nl_body_multi_staged); the words of a chunk are then computed back to back,
-  // so the partial-line stores of a multi-word row meet in L2 before the
-  // line leaves (the word-outer order wrote each line Wm times), and the
-  // source's own level row is loaded once per chunk, not once per word
+  // nl_body_multi_staged); the words of a chunk are then computed back to back
+  // and the source's own level row is loaded once per chunk, not once per word
   __syncthreads();
   for (uint32_t t = threadIdx.x; t < n; t += kNlThreads) {
     const uint32_t f = a.nbrs[beg + t];
@@ -2219,6 +2230,7 @@ __device__ __forceinline__ void nl_body_multi(
     for (int i = 0; i < 4; ++i) {
       live[i] = ls[i] != none && ls[i] != 0;
     }
+    uint64_t held[WM > 1 ? WM : 1][4];
     for (uint32_t w = 0; w < Wm; ++w) {
       const uint32_t jlo = w * 64, jhi = min(n, jlo + 64);
       uint64_t acc[4] = {0, 0, 0, 0};
@@ -2259,8 +2271,20 @@ __device__ __forceinline__ void nl_body_multi(
           }
         }
       }
+      if constexpr (WM > 1) {
+#pragma unroll
+        for (uint32_t ww = 0; ww < WM; ++ww) {
+          if (ww == w) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              held[ww][i] = acc[i];
+            }
+          }
+        }
+        continue;
+      }
       const uint32_t wv0 = v0 - 4 * (threadIdx.x & 63u); // first node of the wave
-      if (Wm == 1 && wv0 + 256 <= a.V) {
+      if (WM == 1 && wv0 + 256 <= a.V) {
         // each store instruction of the wave covers 1 KB contiguously: lane L
         // writes nodes wv0 + 2L, +1 (store 0) and wv0 + 128 + 2L, +1 (store
         // 1), fetched from the lanes that computed them (a lane's own four
@@ -2291,6 +2315,34 @@ __device__ __forceinline__ void nl_body_multi(
         }
       }
     }
+    if constexpr (WM > 1) {
+      // node-major: node v0 + i, word ww at (v0 + i) * WM + ww
+      if (v0 + 4 <= a.V) {
+        ulonglong2* o = reinterpret_cast<ulonglong2*>(nhrow + (size_t)v0 * WM);
+        uint64_t flat[4 * WM];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (uint32_t ww = 0; ww < WM; ++ww) {
+            flat[i * WM + ww] = held[ww][i];
+          }
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 2 * WM; ++k) {
+          o[k] = make_ulonglong2(flat[2 * k], flat[2 * k + 1]);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (v0 + i < a.V) {
+#pragma unroll
+            for (uint32_t ww = 0; ww < WM; ++ww) {
+              nhrow[(size_t)(v0 + i) * WM + ww] = held[ww][i];
+            }
+          }
+        }
+      }
+    }
   }
 }
 
@@ -2308,24 +2360,55 @@ __device__ __forceinline__ void nl_body_multi(
 #endif
 constexpr uint32_t kNlChunksPerBlock = OPENR_NL_CPB;
 
+// Logical block of a launch of n blocks such that consecutive logical blocks
+// share an XCD (blocks b and b + 8 are dealt to one XCD, MI355X_MICROARCH
+// "Workgroup dispatch"): XCD x of the round-robin deal gets the contiguous
+// logical range [x*q + min(x, r), ...), q = n / 8, r = n % 8.  Speed only
+// (L2 locality), never correctness: every logical block is still run once.
+__device__ __forceinline__ uint32_t xcd_logical_block(uint32_t b, uint32_t n) {
+  const uint32_t x = b & 7u, i = b >> 3, qn = n >> 3, r = n & 7u;
+  return x * qn + min(x, r) + i;
+}
+
 // six waves per SIMD (<= 80 VGPRs), as before the chunk-inner word loop
 __global__ __launch_bounds__(kNlThreads) __attribute__((amdgpu_waves_per_eu(6)))
 void spf_nh_levels_kernel(NhLevelsArgs a) {
   __shared__ uint32_t st_row[kNlStage];
   __shared__ uint32_t st_node[kNlStage];
   const uint32_t nchunks = (a.V + kNlChunk - 1) / kNlChunk;
-  const uint32_t cb = blockIdx.x / a.nq;
-  const uint32_t q = blockIdx.x - cb * a.nq;
+  // sources of one pod / plane are adjacent name ranks and share neighbours:
+  // run them on one XCD so its L2 serves their neighbours' level rows (the
+  // 8 FSWs of a pod all read its 48 RSW rows; dealt round-robin they fetched
+  // each RSW row once per XCD)
+  const uint32_t bid = a.xcd_swizzle ? xcd_logical_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint32_t cb = bid / a.nq;
+  const uint32_t q = bid - cb * a.nq;
   const uint32_t s = a.src[q];
   const uint32_t c0 = cb * kNlChunksPerBlock;
   const uint32_t c1 = min(nchunks, c0 + kNlChunksPerBlock);
-  const bool big = a.nbr_off[s + 1] - a.nbr_off[s] > kNlStage; // uniform per block
+  const uint32_t deg = a.nbr_off[s + 1] - a.nbr_off[s];
+  const bool big = deg > kNlStage; // uniform per block
+  const uint32_t wm = a.nh_w[q];
   if (a.flags[0] != 0) {
-    big ? nl_body_multi_staged<true>(a, q, s, c0, c1, st_row, st_node)
-        : nl_body_multi<true>(a, q, s, c0, c1, st_row, st_node);
+    if (big) {
+      nl_body_multi_staged<true>(a, q, s, c0, c1, st_row, st_node);
+    } else if (wm == 1) {
+      nl_body_multi<true, 1>(a, q, s, c0, c1, st_row, st_node);
+    } else {
+      nl_body_multi<true, 0>(a, q, s, c0, c1, st_row, st_node);
+    }
   } else {
-    big ? nl_body_multi_staged<false>(a, q, s, c0, c1, st_row, st_node)
-        : nl_body_multi<false>(a, q, s, c0, c1, st_row, st_node);
+    if (big) {
+      nl_body_multi_staged<false>(a, q, s, c0, c1, st_row, st_node);
+    } else if (wm == 1) {
+      nl_body_multi<false, 1>(a, q, s, c0, c1, st_row, st_node);
+    } else if (wm == 2 && a.held_words) {
+      nl_body_multi<false, 2>(a, q, s, c0, c1, st_row, st_node);
+    } else if (wm == 3 && a.held_words) {
+      nl_body_multi<false, 3>(a, q, s, c0, c1, st_row, st_node);
+    } else {
+      nl_body_multi<false, 0>(a, q, s, c0, c1, st_row, st_node);
+    }
   }
 }
 
@@ -4907,6 +4990,8 @@ int launch_nh_levels(spf_query* q, bool unit) {
   a.Vp8 = q->Vp8;
   a.nq = q->nq;
   a.scale = unit ? 1u : g->uniform;
+  a.xcd_swizzle = env_flag("OPENR_NL_XCD", 1);
+  a.held_words = env_flag("OPENR_NL_HELD", 1);
   const uint32_t nchunks = (g->V + kNlChunk - 1) / kNlChunk;
   const uint64_t blocks =
       (uint64_t)((nchunks + kNlChunksPerBlock - 1) / kNlChunksPerBlock) * q->nq;

@@ -147,3 +147,107 @@ def test_linkstate_prefetch_fans_out(gpu_ready):
                 assert list(a[k][2]) == list(b[k][2]), (node, k)
     finally:
         E.set_spf_devices([])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["local", "rank"])
+def test_query_table_ignore_lists_persistent_graph(gpu_ready, mode):
+    """spf_table_create_q over a persistent spf_cgraph: per-query ignore
+    lists (KSP2 second passes / what-if / LFA batches, LinkState.cpp:776-777,
+    842-847) sliced per block give the single-device query's rows and masks
+    exactly; the same cgraph serves later tables after in-place transit and
+    metric patches (no re-upload)."""
+    csr = _random_csr(2500, 9000, 21)
+    rng = np.random.default_rng(5)
+    n = 300
+    sources = rng.integers(0, csr.num_nodes, n).astype(np.uint32)
+    ignore = [sorted(set(int(x) for x in rng.integers(0, csr.num_links, int(rng.integers(0, 40)))))
+              for _ in range(n)]
+    c = abi.Cluster([0]) if mode == "local" else abi.Cluster(
+        world=1, rank=0, uid=abi.cluster_unique_id(), device=0)
+    cg = abi.ClusterGraph(c, csr)
+    g = abi.Graph(csr)
+    for step in range(3):
+        for flags in (abi.SPF_F_NEXTHOPS, abi.SPF_F_NEXTHOPS | abi.SPF_F_UNIT_METRIC, 0):
+            t = cg.table(sources, flags, ignore=ignore).run()
+            q = g.query(sources, flags, ignore=ignore).run()
+            rows = np.empty((n, csr.num_nodes), dtype=np.uint32)
+            q.fetch_rows(0, n, rows.ctypes.data, csr.num_nodes * 4, on_device=False)
+            assert (t.fetch_rows(0, n) == rows).all(), (step, flags)
+            if flags & abi.SPF_F_NEXTHOPS:
+                assert (t.fetch_nexthops(0, n) == q.fetch_nexthops(0, n)).all(), (step, flags)
+            q.close()
+            t.close()
+        # churn on both graphs: drain toggles and metric changes in place
+        ov = (rng.random(csr.num_nodes) < 0.05).astype(np.uint8)
+        cg.set_transit(ov)
+        g.set_transit(ov)
+        e = rng.choice(len(csr.col), 50, replace=False).astype(np.uint32)
+        m = rng.integers(1, 20, 50).astype(np.uint64)
+        cg.patch_metrics(e, m)
+        g.patch_metrics(e, m)
+    g.close()
+    cg.close()
+    c.close()
+
+
+@pytest.mark.gpu
+def test_linkstate_batches_fan_out_with_ignore_lists(gpu_ready):
+    """The drop-in with setSpfDevices: what-if batches (runSpfBatch), KSP2
+    second passes (prefetchKthPaths) and LFA neighbour batches (prefetchSpf)
+    all run through the persistent cluster graph -- one upload, patched by
+    drain churn -- and every SpfResult / RouteDb equals the oracle's."""
+    import copy
+
+    import openr_amd._openr_spf as E
+    from oracle import build
+    from openr_amd import thrift as T
+    from tests import randomized as RZ
+
+    build.build()
+    from oracle import _oracle_ref as O
+
+    names, adj_dbs, prefix_dbs = RZ.random_network(91, n_nodes=60, n_links=150)
+    for pdb in prefix_dbs:  # SR-MPLS KSP2 for half the prefixes
+        for i, e in enumerate(pdb.prefixEntries):
+            if i % 2 == 0:
+                e.forwardingType = T.PrefixForwardingType.SR_MPLS
+                e.forwardingAlgorithm = T.PrefixForwardingAlgorithm.KSP2_ED_ECMP
+    ea, ep = RZ.load(E, adj_dbs, prefix_dbs, 1)
+    oa, op = RZ.load(O, adj_dbs, prefix_dbs, 1)
+    E.set_spf_devices([0])
+    E.set_cluster_min_sources(4)
+    try:
+        E.reset_counters()
+        me = names[0]
+        links = list(ea["0"].linksFromNode(me))
+        by_key = {tuple(l.key()): l for l in oa["0"].linksFromNode(me)}
+        olinks = [by_key[tuple(l.key())] for l in links]
+        batch = ea["0"].runSpfBatch(me, [[l] for l in links], True)
+        for i, ol in enumerate(olinks):
+            want = oa["0"].runSpfIgnoring(me, [ol], True)
+            got = batch.result(i)
+            assert got.keys() == want.keys()
+            for k in got:
+                assert got[k][0] == want[k][0] and got[k][1] == want[k][1], (i, k)
+        for lfa in (False, True):
+            es = E.SpfSolver(me, True, lfa)
+            os_ = O.SpfSolver(me, True, lfa)
+            assert es.buildRouteDb(me, ea, ep) == os_.buildRouteDb(me, oa, op), lfa
+        c = E.get_counters()
+        assert c.get("decision.spf_cluster_batches", 0) >= 3
+        assert c.get("decision.cluster_graph_uploads", 0) == 1
+        # drain churn patches the cluster graph in place
+        dbs = [copy.deepcopy(d) for d in adj_dbs["0"]]
+        for step in range(3):
+            db = dbs[(step * 17) % len(dbs)]
+            db.isOverloaded = not db.isOverloaded
+            ea["0"].updateAdjacencyDatabase(db)
+            oa["0"].updateAdjacencyDatabase(db)
+            es = E.SpfSolver(me, True, True)
+            os_ = O.SpfSolver(me, True, True)
+            assert es.buildRouteDb(me, ea, ep) == os_.buildRouteDb(me, oa, op), step
+        assert E.get_counters().get("decision.cluster_graph_uploads", 0) == 1
+    finally:
+        E.set_cluster_min_sources(64)
+        E.set_spf_devices([])

@@ -135,6 +135,30 @@ def test_config3_wan100k_all_sources_sharded(gpu_ready):
     sas.close()
 
 
+def test_config3_wan100k_all_sources_spf_table(gpu_ready):
+    """Config 3 through the in-ABI multi-GPU path (spf_cluster + spf_cgraph +
+    spf_table_create_q, world 1, rows all-gathered into the rank slots):
+    the reference's checksum of row n0 and the 32 golden rows."""
+    from openr_amd import abi
+    from openr_amd import topologies as TP
+
+    gold = json.load(open(os.path.join(GOLD, "wan100k_rows.json")))["rows"]
+    anchor = [a for a in json.load(open(os.path.join(GOLD, "wan_anchors.json")))["anchors"]
+              if a["V"] == 100000 and a["S"] == 1][0]
+    csr = TP.wan(100000, 1000000).csr()
+    c = abi.Cluster([0])
+    cg = abi.ClusterGraph(c, csr)
+    t = cg.table(np.arange(csr.num_nodes, dtype=np.uint32), 0, gather=abi.SPF_T_GATHER_ROWS).run()
+    assert t.kernel(0) == "dstep"
+    assert int(t.fetch_rows(0, 1)[0].astype(np.int64).sum()) == anchor["sum_dist"]
+    for r in gold:
+        row = t.fetch_rows(r["src"], 1)[0]
+        assert hashlib.sha256(row.tobytes()).hexdigest() == r["sha256"], r["src"]
+    t.close()
+    cg.close()
+    c.close()
+
+
 def _two_area():
     from openr_amd import topologies as TP
 
@@ -168,13 +192,24 @@ def test_config5_whatif_batch_c_abi(gpu_ready):
     assert off == len(want) == 8192
 
 
-def test_config5_whatif_multi_area_linkstate(gpu_ready):
+@pytest.mark.parametrize("fan_out", [False, True])
+def test_config5_whatif_multi_area_linkstate(gpu_ready, fan_out):
     """The same failures through the drop-in: one AreaLinkStates holding both
     areas, LinkState::runSpfBatch(border, {link}) per area, sampled results
-    materialised in the reference's SpfResult form."""
+    materialised in the reference's SpfResult form; fan_out: through the
+    multi-GPU path (setSpfDevices, the cluster graph, ignore lists sliced per
+    block)."""
     import openr_amd._openr_spf as E
     from openr_amd import topologies as TP
 
+    E.set_spf_devices([0] if fan_out else [])
+    try:
+        _config5_linkstate(E, TP, fan_out)
+    finally:
+        E.set_spf_devices([])
+
+
+def _config5_linkstate(E, TP, fan_out):
     meta, want, areas = _two_area()
     la = E.AreaLinkStates()
     for area, topo, _ in areas:
@@ -193,6 +228,7 @@ def test_config5_whatif_multi_area_linkstate(gpu_ready):
         batch = ls.runSpfBatch(TP.WHATIF_BORDER, ign, True)
         assert len(batch) == len(links)
         assert E.get_counters()["decision.spf_runs"] == len(links)
+        assert (E.get_counters().get("decision.spf_cluster_batches", 0) == 1) == fan_out
         _, names_by_rank = topo.rank()
         for s in m["sampled"]:
             res = batch.result(s["query"])

@@ -18,7 +18,8 @@ def _abi_symbols():
     import re
 
     text = open(os.path.join(ROOT, "include", "openr_spf.h")).read()
-    return sorted(set(re.findall(r"^(?:int|void|const char\*|uint32_t|void\*)\s+\*?(spf_\w+)\(", text, re.M)))
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(spf_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_recipe_builds_links_and_runs(tmp_path):

@@ -1,0 +1,117 @@
+"""Full-size RouteDb parity (BASELINE configs[1] "full RouteDb rebuild" and
+configs[3]): the engine's RouteDb of the DecisionBenchmark node "2-0-0" on
+fabric_full(10000) equals, route by route, the CPU oracle's
+(tests/golden/fabric_routedb.json.gz, made by make_routedb_golden.py):
+
+  * every prefix IP / SP_ECMP, LFA off -- the base state and every RSW
+    overload state of the bench's rebuild loop (DecisionBenchmark.cpp:
+    600-626), reached by toggling on ONE LinkState the way the loop does;
+  * LFA on (Decision.cpp:1146-1175);
+  * every prefix SR_MPLS / KSP2_ED_ECMP: k = 1 and k = 2 edge-disjoint paths
+    to all 9,975 destinations (LinkState.cpp:760-789, selectKsp2
+    Decision.cpp:909-1066), base and first overload toggle;
+  * the SP_ECMP RouteDbs of two more nodes (digests).
+The golden file's own consistency is checked on the CPU."""
+
+import os
+
+import pytest
+
+from tests.golden import routes as R
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fabric_routedb.json.gz")
+NODE = "2-0-0"
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return R.load(GOLD)
+
+
+def state(gold, section, name):
+    sec = gold[section]
+    if name == "base":
+        return sec["base"]["hashes"]
+    return R.apply_delta(sec["base"]["hashes"], sec[name]["delta_vs_base"])
+
+
+def test_golden_is_self_consistent(gold):
+    """CPU: the digests and counts match the per-route hashes they summarise."""
+    for section in ("sp_ecmp", "sp_ecmp_lfa", "ksp2"):
+        for name, st in gold[section].items():
+            h = state(gold, section, name)
+            assert R.digest(h) == st["digest"], (section, name)
+            assert len(h["unicast"]) == st["num_unicast"] and len(h["mpls"]) == st["num_mpls"]
+    base = gold["sp_ecmp"]["base"]
+    assert base["num_unicast"] == 9975  # every other node's loopback
+    assert gold["ksp2"]["base"]["num_unicast"] == 9975
+    # the rebuild loop's toggles really change routes
+    assert any(st.get("delta_vs_base", {}).get("unicast") for st in gold["sp_ecmp"].values())
+
+
+def _load(E, topo, fwd=(0, 0)):
+    areas = E.AreaLinkStates()
+    ls = areas.add("0")
+    dbs = topo.adj_dbs()
+    for db in dbs:
+        ls.updateAdjacencyDatabase(db)
+    ps = E.PrefixState()
+    for pdb in topo.prefix_dbs("0", *fwd):
+        ps.updatePrefixDatabase(pdb)
+    return areas, ls, ps, dbs
+
+
+def _walk_states(E, gold, section, fwd, lfa, states):
+    from openr_amd import topologies as TP
+
+    topo = TP.fabric(10000)
+    areas, ls, ps, dbs = _load(E, topo, fwd)
+    solver = E.SpfSolver(NODE, False, lfa)
+    idx = {n: i for i, n in enumerate(topo.names)}
+    for name in states:
+        if name != "base":
+            i = idx[name.split(":", 1)[1]]
+            dbs[i].isOverloaded = True
+            ls.updateAdjacencyDatabase(dbs[i])
+        R.compare(R.route_hashes(solver.buildRouteDb(NODE, areas, ps)), state(gold, section, name),
+                  f"{section} {name}")
+        if name != "base":
+            dbs[i].isOverloaded = False
+            ls.updateAdjacencyDatabase(dbs[i])
+
+
+@pytest.mark.gpu
+def test_fabric_sp_ecmp_route_db_every_loop_state(gpu_ready, gold):
+    import openr_amd._openr_spf as E
+
+    names = ["base"] + [k for k in gold["sp_ecmp"] if k != "base"] + ["base"]
+    _walk_states(E, gold, "sp_ecmp", (0, 0), False, names)
+
+
+@pytest.mark.gpu
+def test_fabric_sp_ecmp_lfa_route_db(gpu_ready, gold):
+    import openr_amd._openr_spf as E
+
+    _walk_states(E, gold, "sp_ecmp_lfa", (0, 0), True, ["base"])
+
+
+@pytest.mark.gpu
+def test_fabric_ksp2_route_db_all_destinations(gpu_ready, gold):
+    import openr_amd._openr_spf as E
+    from openr_amd import thrift as T
+
+    fwd = (T.PrefixForwardingType.SR_MPLS, T.PrefixForwardingAlgorithm.KSP2_ED_ECMP)
+    names = ["base"] + [k for k in gold["ksp2"] if k != "base"] + ["base"]
+    _walk_states(E, gold, "ksp2", fwd, False, names)
+
+
+@pytest.mark.gpu
+def test_fabric_other_nodes_route_db(gpu_ready, gold):
+    import openr_amd._openr_spf as E
+    from openr_amd import topologies as TP
+
+    topo = TP.fabric(10000)
+    areas, ls, ps, _ = _load(E, topo)
+    for node, want in gold["nodes"].items():
+        h = R.route_hashes(E.SpfSolver(node, False, False).buildRouteDb(node, areas, ps))
+        assert R.digest(h) == want["digest"], (node, len(h["unicast"]), want["num_unicast"])

@@ -58,6 +58,9 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-full", action="store_true",
+                   help="time BASELINE.md §3 line A fully on all host cores: config 2 (every fabric "
+                        "source) and config 4 (getKthPaths k=1,2 to every destination); minutes")
     p.add_argument("--no-route-db", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=0, help="oracle sources (0 = auto ~15 s)")
     p.add_argument("--num-sws", type=int, default=10000)
@@ -158,6 +161,61 @@ def host_cores():
     return max(1, min(16, n))
 
 
+def host_cpu_model():
+    """The host CPU's model name (recorded beside `cores`)."""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+
+    return platform.processor() or "unknown"
+
+
+def _ksp2_worker(args):
+    """One host process of the full config-4 line A: the oracle's LinkState
+    for the fabric, then getKthPaths(2-0-0, d, 1) and (…, 2) for its share
+    of the destinations (k = 2 runs an un-memoized runSpf per destination,
+    LinkState.cpp:776-777)."""
+    num_sws, dests = args
+    from oracle import _oracle_ref as O
+    from openr_amd import topologies as TP
+
+    topo = TP.fabric(num_sws)
+    ls = O.LinkState("0")
+    for db in topo.adj_dbs():
+        ls.updateAdjacencyDatabase(db)
+    ls.getSpfResult("2-0-0", True)
+    t0 = time.perf_counter()
+    paths = 0
+    for d in dests:
+        paths += len(ls.getKthPaths("2-0-0", d, 1)) + len(ls.getKthPaths("2-0-0", d, 2))
+    return time.perf_counter() - t0, paths, len(dests)
+
+
+def ksp2_cpu_full(topo, num_sws):
+    """BASELINE.md §3 line A for config 4, timed fully: every destination of
+    2-0-0 on every host core (destinations dealt round-robin to one process
+    per core); wall = the slowest process."""
+    import multiprocessing as mp
+
+    from oracle import build as obuild
+
+    obuild.build()
+    cores = host_cores()
+    names = sorted(n for n in topo.names if n != "2-0-0")
+    chunks = [names[i::cores] for i in range(cores)]
+    with mp.get_context("spawn").Pool(cores) as pool:
+        res = pool.map(_ksp2_worker, [(num_sws, c) for c in chunks])
+    wall = max(r[0] for r in res)
+    return {"build_s": round(wall, 2), "destinations": len(names), "paths": sum(r[1] for r in res),
+            "cores": cores, "kind": "port", "cpu_model": host_cpu_model(),
+            "sample": f"ALL {len(names)} destinations of 2-0-0, oracle/ref_decision.cpp getKthPaths "
+                      f"k=1,2 over {cores} processes (one per core); slowest process {wall:.1f} s"}
+
+
 def _oracle_spf_worker(args):
     """One host process of the all-cores reference-style baseline: the
     oracle's LinkState for the fabric, then uncached runSpf of its sources."""
@@ -245,7 +303,7 @@ def _routedb_parity(section, ls, solver, areas, ps, dbs, topo, node="2-0-0"):
     return "ok (oracle golden: base + " + state + ")" if not errs else "; ".join(errs)
 
 
-def cpu_baseline_all_cores(topo, num_sws, per_core_s=12.0, t_per_spf=None):
+def cpu_baseline_all_cores(topo, num_sws, per_core_s=12.0, t_per_spf=None, full=False):
     """The reference-style oracle runSpf on every host core (one process per
     core, sources dealt round-robin), plus the optimised flat CPU
     restatement (oracle/csr_spf.h, int CSR + binary heap + next-hop bitsets)
@@ -263,7 +321,7 @@ def cpu_baseline_all_cores(topo, num_sws, per_core_s=12.0, t_per_spf=None):
     names = sorted(topo.names)
     per = max(4, int(per_core_s / max(t_per_spf or 0.09, 1e-4)))
     step = max(1, len(names) // (per * cores))
-    pick = names[::step][: per * cores]
+    pick = names if full else names[::step][: per * cores]
     chunks = [pick[i::cores] for i in range(cores)]
     ctx = mp.get_context("spawn")
     with ctx.Pool(cores) as pool:
@@ -279,13 +337,14 @@ def cpu_baseline_all_cores(topo, num_sws, per_core_s=12.0, t_per_spf=None):
     return {
         "reference_style": {
             "value": round(nspf / wall, 2), "unit": "SPF/s", "cores": cores, "kind": "port",
-            "sample": f"{nspf} fabric sources over {cores} processes (one per core), uncached runSpf "
-                      f"(oracle/ref_decision.cpp, reference data structures); slowest process {wall:.1f} s"},
+            "sample": f"{'ALL ' if full else ''}{nspf} fabric sources over {cores} processes (one per "
+                      f"core), uncached runSpf (oracle/ref_decision.cpp, reference data structures); "
+                      f"slowest process {wall:.1f} s", "cpu_model": host_cpu_model()},
         "optimised": {
             "value": round(csr.num_nodes / opt_s, 1), "unit": "SPF/s", "cores": cores, "kind": "port",
             "sample": f"all {csr.num_nodes} fabric sources with ECMP next-hop sets, oracle/csr_spf.h "
                       f"(int CSR, binary heap, next-hop bitsets) on {cores} threads, {opt_s:.2f} s",
-            "checksum_pairs": int(S[:, 2].sum())},
+            "checksum_pairs": int(S[:, 2].sum()), "cpu_model": host_cpu_model()},
     }
 
 
@@ -615,6 +674,8 @@ def ksp2_route_db(topo, device, iters=2):
                      "decision.kth_trace_us", "decision.kth_memo_clear_us", "decision.kth2_trace_us",
                      "decision.kth2_base_us", "decision.ksp2_best_us", "decision.ksp2_paths_us",
                      "decision.ksp2_nexthops_us", "decision.ksp2_rest_us",
+                     "decision.kth2_device_trace_us", "decision.kth2_device_traces",
+                     "decision.kth2_device_overflows",
                      "decision.spf_memo_kept", "decision.spf_memo_dropped")},
     }
     out["what"] = ("adj-db update (RSW overload toggle) + buildRouteDb of 2-0-0, all prefixes "
@@ -650,7 +711,7 @@ def ksp2_cpu_sample(topo, sample=12):
                       f"extrapolated x{len(names)} destinations"}
 
 
-def whatif_batch(world, rank, local, dist, steps=3):
+def whatif_batch(world, rank, local, dist, steps=3, cpu_lines=True):
     """BASELINE configs[4]: 8,192 single-link-failure SPFs (runSpf with
     linksToIgnore = {link}, LinkState.cpp:806-880) from the border node
     "2-0-0" of two areas: area A = the 10k fabric, area B = the 10k-node /
@@ -731,6 +792,28 @@ def whatif_batch(world, rank, local, dist, steps=3):
         q.close()
     for _, g, _ in graphs:
         g.close()
+    cpu = None
+    if rank == 0 and cpu_lines:
+        # BASELINE.md §3 line B: oracle/csr_spf.h (int CSR, binary heap,
+        # next-hop bitsets) over ALL 8,192 queries on every host core
+        from oracle import build as obuild
+
+        obuild.build()
+        from oracle import _oracle_ref as O
+
+        cores = host_cores()
+        tc = time.perf_counter()
+        for a, (csr, src, links) in enumerate(areas):
+            n = len(links)
+            O.csr_spf_summary(csr.row_ptr, csr.col, csr.metric.astype(np.uint64), csr.link_id,
+                              csr.overloaded, np.full(n, src, dtype=np.uint32),
+                              np.arange(n + 1, dtype=np.uint32), links.astype(np.uint32), True, True,
+                              cores)
+        cpu_s = time.perf_counter() - tc
+        cpu = {"value": round(len(allq) / cpu_s, 1), "unit": "SPF/s", "cores": cores,
+               "kind": "port", "cpu_model": host_cpu_model(),
+               "sample": f"ALL {len(allq)} what-if queries (both areas, ECMP next hops), "
+                         f"oracle/csr_spf.h on {cores} threads, {cpu_s:.2f} s"}
     return {
         "config": "BASELINE configs[4]: 8,192 single-link-failure SPFs with ECMP next hops from the "
                   "border node 2-0-0 of two areas: A = fabric (9,976 nodes), B = WAN-10k, 4,096 links each",
@@ -738,6 +821,7 @@ def whatif_batch(world, rank, local, dist, steps=3):
         "ms": round(ms, 3), "device_ms": round(dev_ms, 3),
         "value": round(len(allq) / (ms / 1e3), 1), "unit": "SPF/s",
         "parity_check": check,
+        **({"cpu_baseline_optimised_all_cores": cpu} if cpu else {}),
     }
 
 
@@ -950,6 +1034,30 @@ def wan_all_sources(args, world, rank, local, dist):
                "sample": f"{S} sources, scipy.sparse.csgraph.dijkstra (C binary-heap Dijkstra over the "
                          "same CSR), single thread; the reference's own runSpf needs ~587 s/SPF here "
                          "(SURVEY §6, reMake per strict improvement)"}
+        if not args.no_cpu_baseline:
+            # BASELINE.md §3 line B on every host core: oracle/csr_spf.h
+            # distances over a fixed source sample, extrapolated to all sources
+            from oracle import build as obuild
+
+            obuild.build()
+            from oracle import _oracle_ref as O
+
+            cores = host_cores()
+            Sa = 48 * cores
+            smp = np.arange(0, V, max(1, V // Sa), dtype=np.uint32)[:Sa]
+            tc = time.perf_counter()
+            Sm = O.csr_spf_summary(csr.row_ptr, csr.col, csr.metric.astype(np.uint64), csr.link_id,
+                                   csr.overloaded, smp, None, None, True, False, cores)
+            all_s = time.perf_counter() - tc
+            cpu["optimised_all_cores"] = {
+                "anchor_check": (None if not (want and int(smp[0]) == 0)
+                                 else "ok" if int(Sm[0, 1]) == want[0] else "mismatch"),
+                "value": round(len(smp) / all_s, 1), "unit": "SPF/s", "cores": cores, "kind": "port",
+                "cpu_model": host_cpu_model(),
+                "all_sources_s_extrapolated": round(all_s / len(smp) * V, 1),
+                "sample": f"{len(smp)} sources (every {V // len(smp)}th), oracle/csr_spf.h distances "
+                          f"(int CSR, binary heap) on {cores} threads, {all_s:.2f} s; extrapolated "
+                          f"x{V / len(smp):.0f} to all sources"}
     repair = None if args.no_repair else wan_table_repair(topo, csr, sas, world, rank, local, dist)
     sas.close()
     table_bytes = n * V * 4
@@ -1475,7 +1583,8 @@ def main():
             out["wan_all_sources"] = {"error": repr(e)}
     if not args.no_whatif:
         try:
-            out["whatif_batch"] = whatif_batch(world, rank, local, dist)
+            out["whatif_batch"] = whatif_batch(world, rank, local, dist,
+                                               cpu_lines=not args.no_cpu_baseline)
         except Exception as e:
             out["whatif_batch"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_route_db:
@@ -1507,7 +1616,7 @@ def main():
         one = cpu_baseline(topo, args.cpu_sample)
         t_per = 1.0 / one["value"] if one.get("value") else None
         try:
-            allc = cpu_baseline_all_cores(topo, args.num_sws, t_per_spf=t_per)
+            allc = cpu_baseline_all_cores(topo, args.num_sws, t_per_spf=t_per, full=args.cpu_full)
             out["cpu_baseline"] = dict(allc["reference_style"])
             out["cpu_baseline"]["single_core"] = one
             out["cpu_baseline"]["optimised_all_cores"] = allc["optimised"]
@@ -1522,6 +1631,12 @@ def main():
             out["cpu_baseline"]["ksp2"] = ksp2_cpu_sample(topo)
         except Exception as e:
             out["cpu_baseline"]["ksp2"] = {"error": repr(e)}
+        if args.cpu_full:
+            try:
+                out["cpu_baseline"]["ksp2_full"] = ksp2_cpu_full(topo, args.num_sws)
+            except Exception as e:
+                out["cpu_baseline"]["ksp2_full"] = {"error": repr(e)}
+        out["cpu_baseline"]["cpu_model"] = host_cpu_model()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -179,6 +179,28 @@ uint32_t spf_query_row_stride(const spf_query* q);
  * caller materialises (NodeSpfResult::nextHops, LinkState.h:203-257). */
 int spf_query_fetch_nexthops(
     spf_query* q, uint32_t first, uint32_t count, uint64_t* dst);
+/* getKthPaths' trace loop on the device (LinkState.cpp:776-786 over
+ * traceOnePath, :398-419): for queries [first, first+count), repeated
+ * traceOnePath from the query's source to dests[i] over the query's own
+ * distance row and ignore list, sharing one visited-link set, until a trace
+ * fails — the KSP2 second passes of a RouteDb build (SpfSolver
+ * selectKsp2 -> getKthPaths(src, dst, 2)) without their rows leaving HBM.
+ * Same paths in the same order as the reference (pathLinks order: tail
+ * settle rank, then linksFromNode order).  Per query i (host arrays):
+ * path_count[i] paths and link_count[i] links in them, or path_count[i] =
+ * SPF_TRACE_OVERFLOW when the visited set, the recursion stack or the
+ * 1,024-link output of the query was exceeded (trace that query on the
+ * host).  The paths stay on the device until spf_query_trace_fetch.
+ * SPF_E_UNSUPPORTED for 64-bit (exact) rows. */
+#define SPF_TRACE_OVERFLOW 0xFFFFFFFFu
+int spf_query_trace_paths(
+    spf_query* q, uint32_t first, uint32_t count, const uint32_t* dests, uint32_t* path_count,
+    uint32_t* link_count);
+/* The last trace's paths, packed in query order (overflowed queries
+ * skipped): links[] holds Σ link_count link ids, each path src -> dst;
+ * ends[] holds Σ path_count end offsets, each relative to its query's first
+ * link. */
+int spf_query_trace_fetch(spf_query* q, uint32_t* links, uint32_t* ends);
 
 /* ---- incremental all-sources tables ----
  * The reference drops every memoized SpfResult on any topology change
@@ -369,6 +391,14 @@ int spf_table_nh_words(const spf_table* t, uint32_t i);
  * words each. */
 int spf_table_fetch_rows(spf_table* t, uint32_t first, uint32_t count, uint32_t* dst);
 int spf_table_fetch_nexthops(spf_table* t, uint32_t first, uint32_t count, uint64_t* dst);
+/* spf_query_trace_paths over every local block of the table (each block on
+ * its device, concurrently); dests and the counts are indexed by table
+ * query.  Other ranks' blocks are not traced (their counts are 0).  Then
+ * spf_table_trace_fetch packs the local blocks' paths in table-query order,
+ * as spf_query_trace_fetch does. */
+int spf_table_trace_paths(
+    spf_table* t, const uint32_t* dests, uint32_t* path_count, uint32_t* link_count);
+int spf_table_trace_fetch(spf_table* t, uint32_t* links, uint32_t* ends);
 /* Gathered buffers on local device `local`: rows [world * cap][V] uint32
  * (cap = ceil(n / world)), masks [world * mask_cap] uint64; NULL when that
  * gather is off. */

@@ -21,6 +21,7 @@ LIB_PATH = os.environ.get("OPENR_SPF_LIB") or os.path.join(_HERE, "libopenr_spf.
 SPF_OK = 0
 SPF_E_UNSUPPORTED = -4
 SPF_UNREACHABLE = (1 << 64) - 1
+SPF_TRACE_OVERFLOW = 0xFFFFFFFF
 SPF_F_UNIT_METRIC = 0x1
 SPF_F_NEXTHOPS = 0x2
 SPF_F_ORDER = 0x4
@@ -59,6 +60,8 @@ EXPORTED_SYMBOLS = (
     "spf_query_row_stride",
     "spf_query_fetch_rows",
     "spf_query_fetch_nexthops",
+    "spf_query_trace_paths",
+    "spf_query_trace_fetch",
     "spf_graph_diff",
     "spf_table_screen",
     "spf_query_scatter_rows",
@@ -87,6 +90,8 @@ EXPORTED_SYMBOLS = (
     "spf_table_nh_words",
     "spf_table_fetch_rows",
     "spf_table_fetch_nexthops",
+    "spf_table_trace_paths",
+    "spf_table_trace_fetch",
     "spf_table_device_buffers",
     "spf_table_kernel_name",
     "spf_cgraph_create",
@@ -247,6 +252,8 @@ def load():
         "spf_query_row_stride": (u32, [vp]),
         "spf_query_fetch_rows": (C.c_int, [vp, u32, u32, vp, C.c_size_t, C.c_int]),
         "spf_query_fetch_nexthops": (C.c_int, [vp, u32, u32, pu64]),
+        "spf_query_trace_paths": (C.c_int, [vp, u32, u32, pu32, pu32, pu32]),
+        "spf_query_trace_fetch": (C.c_int, [vp, pu32, pu32]),
         "spf_query_device_rows": (
             C.c_int,
             [vp, C.POINTER(vp), pu32, C.POINTER(vp), pu64],
@@ -279,6 +286,8 @@ def load():
         "spf_table_nh_words": (C.c_int, [vp, u32]),
         "spf_table_fetch_rows": (C.c_int, [vp, u32, u32, pu32]),
         "spf_table_fetch_nexthops": (C.c_int, [vp, u32, u32, pu64]),
+        "spf_table_trace_paths": (C.c_int, [vp, pu32, pu32, pu32]),
+        "spf_table_trace_fetch": (C.c_int, [vp, pu32, pu32]),
         "spf_table_device_buffers": (C.c_int, [vp, u32, C.POINTER(vp), C.POINTER(vp), pu64]),
         "spf_table_kernel_name": (C.c_int, [vp, u32, C.POINTER(C.c_char_p)]),
         "spf_cgraph_create": (C.c_int, [vp, C.POINTER(_GraphDesc), C.POINTER(vp)]),
@@ -490,6 +499,27 @@ def graph_diff(before: "Csr", after: "Csr") -> np.ndarray:
     return out[: n.value]
 
 
+def _unpack_traces(n, pc, lc, fetch):
+    ok = pc[:n] != SPF_TRACE_OVERFLOW
+    links = np.zeros(max(int(lc[:n][ok].sum()), 1), dtype=np.uint32)
+    ends = np.zeros(max(int(pc[:n][ok].sum()), 1), dtype=np.uint32)
+    fetch(links, ends)
+    out, lo, po = [], 0, 0
+    for i in range(n):
+        if not ok[i]:
+            out.append(None)
+            continue
+        paths, a = [], 0
+        for j in range(int(pc[i])):
+            b = int(ends[po + j])
+            paths.append([int(x) for x in links[lo + a : lo + b]])
+            a = b
+        out.append(paths)
+        lo += int(lc[i])
+        po += int(pc[i])
+    return out
+
+
 class Query:
     def __init__(self, graph: Graph, sources, flags, ignore=None):
         lib = load()
@@ -614,6 +644,20 @@ class Query:
         _check(load().spf_query_fetch_nexthops(self.h, first, count, _p(out, C.c_uint64)),
                "fetch_nexthops")
         return out[:n]
+
+    def trace_paths(self, dests, first: int = 0):
+        """getKthPaths' trace loop on the device (spf_query_trace_paths +
+        spf_query_trace_fetch): per query, a list of paths (each a list of
+        link ids, src -> dst), or None when the device trace overflowed."""
+        d = np.ascontiguousarray(dests, dtype=np.uint32)
+        n = len(d)
+        pc = np.zeros(max(n, 1), dtype=np.uint32)
+        lc = np.zeros(max(n, 1), dtype=np.uint32)
+        lib = load()
+        _check(lib.spf_query_trace_paths(self.h, first, n, _p(d, C.c_uint32), _p(pc, C.c_uint32),
+                                         _p(lc, C.c_uint32)), "trace_paths")
+        return _unpack_traces(n, pc, lc, lambda L, E: _check(
+            lib.spf_query_trace_fetch(self.h, _p(L, C.c_uint32), _p(E, C.c_uint32)), "trace_fetch"))
 
     def device_rows(self):
         dp = C.c_void_p()
@@ -806,6 +850,20 @@ class Table:
         _check_cl(load().spf_table_fetch_nexthops(self.h, first, count, _p(out, C.c_uint64)),
                   "spf_table_fetch_nexthops")
         return out[:n]
+
+    def trace_paths(self, dests):
+        """spf_table_trace_paths + spf_table_trace_fetch: per table query,
+        its paths (lists of link ids) or None (overflow: trace on the host)."""
+        d = np.ascontiguousarray(dests, dtype=np.uint32)
+        n = len(d)
+        pc = np.zeros(max(n, 1), dtype=np.uint32)
+        lc = np.zeros(max(n, 1), dtype=np.uint32)
+        lib = load()
+        _check_cl(lib.spf_table_trace_paths(self.h, _p(d, C.c_uint32), _p(pc, C.c_uint32),
+                                            _p(lc, C.c_uint32)), "spf_table_trace_paths")
+        return _unpack_traces(n, pc, lc, lambda L, E: _check_cl(
+            lib.spf_table_trace_fetch(self.h, _p(L, C.c_uint32), _p(E, C.c_uint32)),
+            "spf_table_trace_fetch"))
 
     def device_buffers(self, local: int = 0):
         r, m = C.c_void_p(), C.c_void_p()

@@ -139,10 +139,47 @@ def exchange_rows(table, local_rows, n: int, group=None):
     return int(keep.sum().item())
 
 
+def transit_hop_bound(csr) -> int:
+    """Host restatement of the engine's transit_hop_bound (spf_device.hip):
+    2 * eccentricity of the highest-degree transit node r under the transit
+    rule (a node is expanded iff it is r or not overloaded), or 0 when r does
+    not reach every node (or no node may be transited)."""
+    import numpy as np
+
+    V = int(csr.num_nodes)
+    row = np.asarray(csr.row_ptr, dtype=np.int64)
+    col = np.asarray(csr.col, dtype=np.int64)
+    transit = np.asarray(csr.overloaded, dtype=np.uint8) == 0
+    if V == 0 or not transit.any():
+        return 0
+    deg = np.diff(row)
+    cand = np.where(transit)[0]
+    r = int(cand[np.argmax(deg[cand])])  # first of the largest degree
+    seen = np.zeros(V, dtype=bool)
+    seen[r] = True
+    cur = np.array([r], dtype=np.int64)
+    depth = 0
+    while cur.size:
+        exp = cur[(cur == r) | transit[cur]]
+        if exp.size == 0:
+            break
+        lo, hi = row[exp], row[exp + 1]
+        idx = np.repeat(hi - (hi - lo).cumsum(), hi - lo) + np.arange((hi - lo).sum())
+        nb = np.unique(col[idx]) if idx.size else idx
+        nb = nb[~seen[nb]]
+        if nb.size == 0:
+            break
+        seen[nb] = True
+        depth += 1
+        cur = nb
+    return 2 * depth if seen.all() else 0
+
+
 def needs_64bit_rows(csr) -> bool:
     """Host restatement of spf_graph_needs_exact for metric runs (the
-    engine's upload_weights rule): a metric-0 or wrapping (> 2^31 - 1) metric,
-    or maxw * (V - 1) >= 2^32.  Checked BEFORE any state changes."""
+    engine's refresh_exact rule): a metric-0 or wrapping (> 2^31 - 1) metric,
+    or maxw * (V - 1) >= 2^32 - 1 AND no transit hop bound h with
+    maxw * (h + 1) < 2^32 - 1.  Checked BEFORE any state changes."""
     import numpy as np
 
     m = np.asarray(csr.metric, dtype=np.uint64)
@@ -150,7 +187,11 @@ def needs_64bit_rows(csr) -> bool:
         return False
     if (m == 0).any() or (m > np.uint64(0x7FFFFFFF)).any():
         return True
-    return int(m.max()) * max(csr.num_nodes - 1, 0) >= 0xFFFFFFFF
+    maxw = int(m.max())
+    if maxw * max(csr.num_nodes - 1, 0) < 0xFFFFFFFF:
+        return False
+    h = transit_hop_bound(csr)
+    return not (h and maxw * (h + 1) < 0xFFFFFFFF)
 
 
 @dataclass

@@ -13,6 +13,7 @@
 #include "Engine.h"
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -816,6 +817,195 @@ std::vector<std::unique_ptr<SpfView>> runBatchAuto(
   return runBatch(eng, sources, useLinkMetric, wantNextHops, ignore);
 }
 
+// KSP2 second passes with their traces on the device (getKthPaths k = 2,
+// LinkState.cpp:760-789): one ignore-list SPF per destination, then
+// spf_query_trace_paths / spf_table_trace_paths over the rows where they lie,
+// so only link-id paths come back (no 4*V-byte row per destination).  count[i]
+// = SPF_TRACE_OVERFLOW marks a query the device could not trace: its row is
+// returned in rows[i] for the host trace.  Caller holds devMu; the batch is
+// 32-bit (the caller checks !eng.exact).
+struct DeviceTraces {
+  std::vector<uint32_t> count, linkCount; // per query (count: SPF_TRACE_OVERFLOW)
+  std::vector<uint32_t> links, ends;      // packed (spf_query_trace_fetch)
+  std::vector<std::unique_ptr<SpfView>> rows; // overflowed queries only
+  bool unsupported = false; // 64-bit rows in some block: use runBatchAuto
+};
+
+bool deviceTraceEnabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("OPENR_KSP2_DEVICE_TRACE");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
+DeviceTraces traceSecondPasses(
+    LinkState::Engine& eng, const std::vector<uint32_t>& sources,
+    const std::vector<uint32_t>& dests, const std::vector<std::vector<uint32_t>>& lists) {
+  const auto tBatch = std::chrono::steady_clock::now();
+  const uint32_t V = (uint32_t)eng.names.size();
+  const uint32_t nq = (uint32_t)sources.size();
+  DeviceTraces out;
+  out.count.assign(nq, 0);
+  out.linkCount.assign(nq, 0);
+  out.rows.resize(nq);
+  auto sizeOutputs = [&] {
+    size_t nl = 0, np = 0;
+    for (uint32_t i = 0; i < nq; ++i) {
+      if (out.count[i] != SPF_TRACE_OVERFLOW) {
+        nl += out.linkCount[i];
+        np += out.count[i];
+      }
+    }
+    out.links.resize(nl);
+    out.ends.resize(np);
+  };
+  std::vector<uint32_t> ioff{0}, ilinks;
+  for (const auto& l : lists) {
+    ilinks.insert(ilinks.end(), l.begin(), l.end());
+    ioff.push_back((uint32_t)ilinks.size());
+  }
+  spf_query_desc qd{};
+  qd.num_queries = nq;
+  qd.sources = sources.data();
+  qd.flags = 0; // link metrics, distances only: a trace reads no masks
+  qd.ignore_offsets = ioff.data();
+  qd.ignore_links = ilinks.data();
+  auto rowView = [&](size_t i, const std::shared_ptr<std::vector<uint32_t>>& row) {
+    auto view = std::make_unique<SpfView>();
+    view->src = sources[i];
+    view->useLinkMetric = true;
+    view->dist.share32(row, 0, V);
+    view->ignored = lists[i];
+    return view;
+  };
+  const bool cluster = nq >= clusterMinSources() && !getSpfDevices().empty();
+  if (cluster) {
+    auto& cs = clusterState();
+    std::lock_guard<std::mutex> g(cs.mu);
+    if (!cs.cluster) {
+      const int c = spf_cluster_create_local(
+          (uint32_t)cs.devices.size(), cs.devices.data(), &cs.cluster);
+      if (c != SPF_OK) {
+        engineFailure("spf_cluster_create_local", c);
+      }
+    }
+    if (eng.cgraph && eng.cgraphGen != cs.gen) {
+      spf_cgraph_destroy(eng.cgraph);
+      eng.cgraph = nullptr;
+    }
+    if (!eng.cgraph) {
+      spf_graph_desc d{};
+      d.num_nodes = V;
+      d.num_edges = (uint32_t)eng.col.size();
+      d.row_ptr = eng.row.data();
+      d.col = eng.col.data();
+      d.metric = eng.metric.data();
+      d.link_id = eng.linkId.data();
+      d.rev = eng.rev.data();
+      d.node_overloaded = eng.overloaded.data();
+      d.num_links = (uint32_t)eng.links.size();
+      if (const int c = spf_cgraph_create(cs.cluster, &d, &eng.cgraph); c != SPF_OK) {
+        engineFailure("spf_cgraph_create", c);
+      }
+      eng.cgraphGen = cs.gen;
+      Counters::add("decision.cluster_graph_uploads", 1);
+    }
+    spf_table* t = nullptr;
+    int st = spf_table_create_q(eng.cgraph, &qd, 0, &t);
+    struct TGuard {
+      spf_table* t;
+      ~TGuard() {
+        if (t) {
+          spf_table_destroy(t);
+        }
+      }
+    } tg{t};
+    if (st == SPF_OK && (st = spf_table_run(t)) == SPF_OK && (st = spf_table_sync(t)) == SPF_OK) {
+      float cm = 0, gm = 0;
+      spf_table_elapsed_ms(t, &cm, &gm);
+      eng.lastMs = cm + gm;
+      Counters::add("decision.spf_device_us", (int64_t)(eng.lastMs * 1000.0f));
+      const auto tTr = std::chrono::steady_clock::now();
+      st = spf_table_trace_paths(t, dests.data(), out.count.data(), out.linkCount.data());
+      if (st == SPF_E_UNSUPPORTED) {
+        out.unsupported = true;
+        return out;
+      }
+      if (st == SPF_OK) {
+        sizeOutputs();
+        st = spf_table_trace_fetch(t, out.links.data(), out.ends.data());
+      }
+      Counters::add("decision.kth2_device_trace_us",
+                    std::chrono::duration_cast<std::chrono::microseconds>(
+                        std::chrono::steady_clock::now() - tTr)
+                        .count());
+    }
+    if (st != SPF_OK) {
+      engineFailure("spf_table (KSP2 device traces)", st);
+    }
+    Counters::add("decision.spf_cluster_batches", 1);
+    for (uint32_t i = 0; i < nq; ++i) {
+      if (out.count[i] == SPF_TRACE_OVERFLOW) {
+        auto row = std::make_shared<std::vector<uint32_t>>(V);
+        if (const int c = spf_table_fetch_rows(t, i, 1, row->data()); c != SPF_OK) {
+          engineFailure("spf_table_fetch_rows", c);
+        }
+        out.rows[i] = rowView(i, row);
+      }
+    }
+  } else {
+    spf_query* q = nullptr;
+    int s = spf_query_create(eng.graph, &qd, &q);
+    if (s != SPF_OK) {
+      engineFailure("spf_query_create", s);
+    }
+    struct Guard {
+      spf_query* q;
+      ~Guard() { spf_query_destroy(q); }
+    } guard{q};
+    if ((s = spf_query_run(q)) != SPF_OK || (s = spf_query_sync(q)) != SPF_OK) {
+      engineFailure("spf_query_run", s);
+    }
+    spf_query_elapsed_ms(q, &eng.lastMs);
+    Counters::add("decision.spf_device_us", (int64_t)(eng.lastMs * 1000.0f));
+    const auto tTr = std::chrono::steady_clock::now();
+    s = spf_query_trace_paths(q, 0, nq, dests.data(), out.count.data(), out.linkCount.data());
+    if (s == SPF_E_UNSUPPORTED) {
+      out.unsupported = true;
+      return out;
+    }
+    if (s != SPF_OK) {
+      engineFailure("spf_query_trace_paths", s);
+    }
+    sizeOutputs();
+    if ((s = spf_query_trace_fetch(q, out.links.data(), out.ends.data())) != SPF_OK) {
+      engineFailure("spf_query_trace_fetch", s);
+    }
+    Counters::add("decision.kth2_device_trace_us",
+                  std::chrono::duration_cast<std::chrono::microseconds>(
+                      std::chrono::steady_clock::now() - tTr)
+                      .count());
+    for (uint32_t i = 0; i < nq; ++i) {
+      if (out.count[i] == SPF_TRACE_OVERFLOW) {
+        auto row = std::make_shared<std::vector<uint32_t>>(V);
+        if ((s = spf_query_fetch_rows(q, i, 1, row->data(), (size_t)V * 4, 0)) != SPF_OK) {
+          engineFailure("spf_query_fetch_rows", s);
+        }
+        out.rows[i] = rowView(i, row);
+      }
+    }
+  }
+  const double batchMs =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tBatch)
+          .count();
+  Counters::add("decision.spf_batch_us", (int64_t)(batchMs * 1000.0));
+  for (uint32_t i = 0; i < nq; ++i) {
+    Counters::add("decision.spf_ms", (int64_t)(batchMs / (double)nq));
+  }
+  return out;
+}
+
 // Predecessors of v in the reference's pathLinks order: usable in-links whose
 // tail is the source or transit, is settled before v and is tight; sorted by
 // the tail's settle rank, then by the tail's linksFromNode() order.
@@ -1159,8 +1349,9 @@ void LinkState::patchMemo(
           engineFailure("spf_cgraph_patch_metrics", c);
         }
       }
-      eng.exact = spf_graph_needs_exact(eng.graph) != 0;
     }
+    // metrics and transit bits both feed the 32-bit row bound (refresh_exact)
+    eng.exact = spf_graph_needs_exact(eng.graph) != 0;
   } catch (...) {
     clearMemo();
     throw;
@@ -2016,7 +2207,58 @@ void LinkState::prefetchKthPaths(
     return;
   }
   std::vector<std::unique_ptr<SpfView>> views;
-  {
+  bool traced = false;
+  if (!eng.exact && deviceTraceEnabled()) {
+    // second passes AND their traces on the device (fanned out by
+    // destination when devices are configured): the (src, dst, 2) memo
+    // entries are filled here, as the fill in kthPathIds would (one counted
+    // runSpf each, LinkState.cpp:776-777); overflowed traces keep their row
+    // for the host trace
+    DeviceTraces tr;
+    {
+      std::lock_guard<std::mutex> dev(eng.devMu);
+      tr = traceSecondPasses(eng, sources, dstIds, lists);
+    }
+    traced = !tr.unsupported;
+    if (!traced) {
+      tr.count.clear();
+    }
+    const std::string* dstName = nullptr;
+    size_t j = 0, lo = 0, po = 0;
+    uint64_t overflowed = 0;
+    for (size_t i = 0; i < tr.count.size(); ++i) {
+      if (tr.count[i] == SPF_TRACE_OVERFLOW) {
+        ++overflowed;
+        continue;
+      }
+      while (todo[j].second != dstIds[i]) {
+        ++j; // todo and dstIds are in the same order (dstIds skips entries)
+      }
+      dstName = todo[j].first;
+      KthPathIds paths;
+      const uint32_t* L = tr.links.data() + lo;
+      const uint32_t* E = tr.ends.data() + po;
+      paths.links.assign(L, L + tr.linkCount[i]);
+      paths.off.reserve(tr.count[i] + 1);
+      for (uint32_t p = 0; p < tr.count[i]; ++p) {
+        paths.off.push_back(E[p]);
+      }
+      lo += tr.linkCount[i];
+      po += tr.count[i];
+      KthKey key{src, *dstName, 2};
+      KthStripe& stripe = kthStripe(key);
+      std::unique_lock<std::shared_mutex> wr(stripe.mu);
+      if (stripe.ids.emplace(std::move(key), std::move(paths)).second) {
+        Counters::add("decision.spf_runs", 1);
+      }
+    }
+    if (traced) {
+      views = std::move(tr.rows);
+      Counters::add("decision.kth2_device_traces", (int64_t)(tr.count.size() - overflowed));
+      Counters::add("decision.kth2_device_overflows", (int64_t)overflowed);
+    }
+  }
+  if (!traced) {
     // the second passes of many destinations: fanned out by destination
     // when devices are configured (distances only: a trace reads no masks)
     std::lock_guard<std::mutex> dev(eng.devMu);
@@ -2024,7 +2266,9 @@ void LinkState::prefetchKthPaths(
   }
   std::unique_lock<std::shared_mutex> wr(eng.viewMu);
   for (size_t i = 0; i < views.size(); ++i) {
-    eng.kthPrefetch[{sid->second, dstIds[i]}] = std::move(views[i]);
+    if (views[i]) {
+      eng.kthPrefetch[{sid->second, dstIds[i]}] = std::move(views[i]);
+    }
   }
 }
 

@@ -27,6 +27,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "openr_spf.h"
@@ -112,6 +113,9 @@ struct spf_table {
   };
   std::vector<Local> local;
   bool ran = false;
+  // spf_table_trace_paths: packed offsets of each local block's paths
+  bool traced = false;
+  std::vector<uint64_t> trace_link_base, trace_path_base;
 };
 
 extern "C" {
@@ -612,6 +616,102 @@ int spf_table_fetch_rows(spf_table* t, uint32_t first, uint32_t count, uint32_t*
                                   (size_t)t->V * sizeof(uint32_t), 0));
     }
     i = bend;
+  }
+  return SPF_OK;
+}
+
+int spf_table_trace_paths(
+    spf_table* t, const uint32_t* dests, uint32_t* path_count, uint32_t* link_count) {
+  SPF_ABI_RANGE_CLUSTER("spf_table_trace_paths");
+  if (!t || (t->n && (!dests || !path_count || !link_count))) {
+    return cfail(SPF_E_INVALID, "spf_table_trace_paths: null argument");
+  }
+  if (!t->ran) {
+    return cfail(SPF_E_INVALID, "spf_table_trace_paths: table has not run");
+  }
+  std::fill(path_count, path_count + t->n, 0u);
+  std::fill(link_count, link_count + t->n, 0u);
+  // every local block on its own device, concurrently (each call waits for
+  // its own graph stream only)
+  std::vector<int> st(t->local.size(), SPF_OK);
+  std::vector<std::string> why(t->local.size());
+  std::vector<std::thread> th;
+  for (size_t j = 0; j < t->local.size(); ++j) {
+    const auto& L = t->local[j];
+    if (!L.q) {
+      continue;
+    }
+    const uint64_t first = t->block_first[L.rank];
+    const uint32_t count = (uint32_t)(t->block_first[L.rank + 1] - first);
+    th.emplace_back([&, j, first, count] {
+      if (hipSetDevice(t->local[j].device) != hipSuccess) {
+        st[j] = SPF_E_DEVICE;
+        return;
+      }
+      st[j] = spf_query_trace_paths(t->local[j].q, 0, count, dests + first, path_count + first,
+                                    link_count + first);
+      if (st[j] != SPF_OK) {
+        why[j] = spf_last_error_detail();
+      }
+    });
+  }
+  for (auto& x : th) {
+    x.join();
+  }
+  for (size_t j = 0; j < st.size(); ++j) {
+    if (st[j] != SPF_OK) {
+      return cfail(st[j], "spf_table_trace_paths: " + why[j]);
+    }
+  }
+  // packed offsets of every local block (table-query order)
+  t->trace_link_base.assign(t->local.size(), 0);
+  t->trace_path_base.assign(t->local.size(), 0);
+  std::vector<uint64_t> lsum(t->n + 1, 0), psum(t->n + 1, 0);
+  for (uint32_t i = 0; i < t->n; ++i) {
+    const bool ok = path_count[i] != SPF_TRACE_OVERFLOW;
+    lsum[i + 1] = lsum[i] + (ok ? link_count[i] : 0);
+    psum[i + 1] = psum[i] + (ok ? path_count[i] : 0);
+  }
+  for (size_t j = 0; j < t->local.size(); ++j) {
+    const uint64_t first = t->block_first[t->local[j].rank];
+    t->trace_link_base[j] = lsum[first];
+    t->trace_path_base[j] = psum[first];
+  }
+  t->traced = true;
+  return SPF_OK;
+}
+
+int spf_table_trace_fetch(spf_table* t, uint32_t* links, uint32_t* ends) {
+  SPF_ABI_RANGE_CLUSTER("spf_table_trace_fetch");
+  if (!t || !t->traced) {
+    return cfail(SPF_E_INVALID, "spf_table_trace_fetch: no trace to fetch");
+  }
+  std::vector<int> st(t->local.size(), SPF_OK);
+  std::vector<std::string> why(t->local.size());
+  std::vector<std::thread> th;
+  for (size_t j = 0; j < t->local.size(); ++j) {
+    if (!t->local[j].q) {
+      continue;
+    }
+    th.emplace_back([&, j] {
+      if (hipSetDevice(t->local[j].device) != hipSuccess) {
+        st[j] = SPF_E_DEVICE;
+        return;
+      }
+      st[j] = spf_query_trace_fetch(t->local[j].q, links ? links + t->trace_link_base[j] : nullptr,
+                                    ends ? ends + t->trace_path_base[j] : nullptr);
+      if (st[j] != SPF_OK) {
+        why[j] = spf_last_error_detail();
+      }
+    });
+  }
+  for (auto& x : th) {
+    x.join();
+  }
+  for (size_t j = 0; j < st.size(); ++j) {
+    if (st[j] != SPF_OK) {
+      return cfail(st[j], "spf_table_trace_fetch: " + why[j]);
+    }
   }
   return SPF_OK;
 }

@@ -1810,6 +1810,13 @@ constexpr uint32_t kMsMaxK = 16; // nodes per thread -> V <= 16384
 struct MsBfsArgs {
   const uint32_t* row;
   const uint32_t* col;
+  // sliced-ELL copy of the CSR (one slice = the 64 nodes of one wave's
+  // k-th node slot): edge j of lane L of slice c is word j % 4 of uint4
+  // sell4[(sell_off[c] + j / 4) * 64 + L]; short rows are padded with the
+  // node itself, whose frontier bits are a subset of its visited bits and so
+  // drop out of `acc & ~vis`.  nullptr: the plain CSR loop.
+  const uint4* sell4;
+  const uint32_t* sell_off; // [slices + 1] in 64-uint4 groups
   const uint32_t* trbits;
   const uint32_t* src;
   uint32_t* dist_out; // [nq][Vp]
@@ -1843,7 +1850,7 @@ __device__ __forceinline__ void ms_record(
   }
 }
 
-template <typename MT, uint32_t KMAX>
+template <typename MT, uint32_t KMAX, bool SELL>
 __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
   extern __shared__ __align__(16) unsigned char ms_smem[];
   constexpr uint32_t B = sizeof(MT) * 8;
@@ -1872,9 +1879,13 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
     }
     __syncthreads();
     MT vis[KMAX];
+    uint32_t trm = 0; // bit k: this thread's k-th node may be transited
 #pragma unroll
     for (uint32_t k = 0; k < KMAX; ++k) {
       const uint32_t v = tid + k * kMsThreads;
+      if (k < K && v < V) {
+        trm |= ((a.trbits[v >> 5] >> (v & 31)) & 1u) << k;
+      }
       vis[k] = (k < K && v < V) ? cur[v] : (MT)0;
       if (k < K && v < V && vis[k]) {
         ms_record<MT>(a, q0, v, vis[k], 0); // level 0 = the sources
@@ -1894,7 +1905,26 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
           continue;
         }
         MT nw = 0;
-        if (vis[k] != full) {
+        if (SELL && vis[k] != full) {
+          // a wave reads 1 KB of its slice per load instead of one line per lane
+          const uint32_t c = __builtin_amdgcn_readfirstlane(v >> 6);
+          const uint32_t g0 = __builtin_amdgcn_readfirstlane(a.sell_off[c]);
+          const uint32_t g1 = __builtin_amdgcn_readfirstlane(a.sell_off[c + 1]);
+          const uint4* p = a.sell4 + (size_t)g0 * 64 + (tid & 63u);
+          MT acc = 0;
+          uint32_t g = g0;
+          for (; g + 2 <= g1; g += 2, p += 128) {
+            const uint4 c0 = p[0], c1 = p[64];
+            acc |= cur[c0.x] | cur[c0.y] | cur[c0.z] | cur[c0.w] | cur[c1.x] | cur[c1.y] |
+                   cur[c1.z] | cur[c1.w];
+          }
+          if (g < g1) {
+            const uint4 c0 = p[0];
+            acc |= cur[c0.x] | cur[c0.y] | cur[c0.z] | cur[c0.w];
+          }
+          nw = acc & ~vis[k];
+          vis[k] |= nw;
+        } else if (!SELL && vis[k] != full) {
           const uint32_t beg = a.row[v], end = a.row[v + 1];
           MT acc = 0;
           uint32_t e = beg;
@@ -1918,7 +1948,7 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
           vis[k] |= nw;
         }
         any |= nw != 0;
-        const bool transit = (a.trbits[v >> 5] >> (v & 31)) & 1u;
+        const bool transit = (trm >> k) & 1u;
         nxt[v] = transit ? nw : (MT)0;
         if (nw) {
           ms_record<MT>(a, q0, v, nw, L);
@@ -1971,7 +2001,7 @@ struct NhLevelsArgs {
   uint32_t Vp8;
   uint32_t nq;
   uint32_t scale;
-  uint32_t xcd_swizzle; // 1: XCD-aware block order (OPENR_NL_XCD, default on)
+  uint32_t xcd_swizzle; // 1: XCD-aware block order (OPENR_NL_XCD; default off: 0.69 -> 0.92 ms on the fabric, profiles/r03b)
   uint32_t held_words;  // 1: 2/3-word masks stored node-major from registers (OPENR_NL_HELD)
 };
 
@@ -2368,6 +2398,198 @@ constexpr uint32_t kNlChunksPerBlock = OPENR_NL_CPB;
 __device__ __forceinline__ uint32_t xcd_logical_block(uint32_t b, uint32_t n) {
   const uint32_t x = b & 7u, i = b >> 3, qn = n >> 3, r = n & 7u;
   return x * qn + min(x, r) + i;
+}
+
+// Byte-SIMD (SWAR) next-hop pass.  The compare of spf_nh_levels_kernel,
+// lvl(n, v) + 1 == lvl(s, v), costs ~8 VALU ops per (neighbour, node): at
+// Σ deg(s) * V = 2.3G pairs on the fabric that alone is ~0.5 ms of the
+// chip's VALU issue.  Here a lane owns 16 nodes (one 16-byte load per
+// neighbour row) and compares 4 level bytes per 32-bit op: with t = lvl(s, v)
+// - 1 bytewise, a neighbour matches node v iff byte v of lvl(n, .) ^ t is 0
+// and v is live (lvl(s, v) not 0 = the source, not 255 = unreached).  The
+// zero-byte test leaves 0x80 in each matching byte; neighbour j = 8g + k of
+// a 64-neighbour mask word ORs it, shifted right by 7 - k, into accumulator
+// P[g], so byte i of P[0..7] is node i's mask word, 8 bits per P — a 4x4 byte
+// transpose (v_perm) per group of four P hands each node its 64-bit word.
+// ~7 VALU ops per (neighbour, 4 nodes).  Non-transit neighbours (drained,
+// LinkState.cpp:829-836) match only the node they are (v == n), a uniform
+// per-neighbour bit staged with the list.  One 128-thread block per source,
+// each wave sweeping 1024-node chunks; mask words are staged 64 neighbours at
+// a time, so any degree works.  A BFS deeper than 254 levels (flags[0]) takes
+// the generic 32-bit-row compare in the same launch.
+constexpr uint32_t kNsThreads = 128;
+constexpr uint32_t kNsNodes = 16;
+constexpr uint32_t kNsChunk = 64 * kNsNodes;
+
+__device__ __forceinline__ uint32_t swar_zero_bytes(uint32_t x) {
+  return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu); // 0x80 per zero byte
+}
+
+// byte i of p0..p3 -> out[i] = (p0.i, p1.i, p2.i, p3.i)
+__device__ __forceinline__ void swar_transpose4(
+    uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3, uint32_t (&out)[4]) {
+  const uint32_t t0 = __builtin_amdgcn_perm(p1, p0, 0x05010400u);
+  const uint32_t t1 = __builtin_amdgcn_perm(p1, p0, 0x07030602u);
+  const uint32_t t2 = __builtin_amdgcn_perm(p3, p2, 0x05010400u);
+  const uint32_t t3 = __builtin_amdgcn_perm(p3, p2, 0x07030602u);
+  out[0] = __builtin_amdgcn_perm(t2, t0, 0x05040100u);
+  out[1] = __builtin_amdgcn_perm(t2, t0, 0x07060302u);
+  out[2] = __builtin_amdgcn_perm(t3, t1, 0x05040100u);
+  out[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
+}
+
+// the generic branch (a BFS deeper than 254 levels): 32-bit rows, one node
+// at a time; out of line so its registers do not weigh on the byte path
+__device__ __noinline__ void nl_swar_deep(
+    const NhLevelsArgs& a, uint32_t q, uint32_t v0, uint32_t w, uint32_t Wm, uint32_t cnt,
+    uint64_t ntmask, const uint32_t* st_row, const uint32_t* st_node, uint64_t* nhrow) {
+  for (uint32_t i = 0; i < kNsNodes; ++i) {
+    const uint32_t v = v0 + i;
+    if (v >= a.V) {
+      break;
+    }
+    uint64_t acc = 0;
+    const uint32_t ds = a.dist[(size_t)q * a.Vp + v];
+    if (ds != kInf32 && ds != 0) {
+      for (uint32_t j = 0; j < cnt; ++j) {
+        // st_row holds level-row byte offsets (row * Vp8)
+        const uint32_t df = a.dist[(size_t)(st_row[j] / a.Vp8) * a.Vp + v];
+        const bool tr = !((ntmask >> j) & 1u) || st_node[j] == v;
+        if (df != kInf32 && (uint64_t)df + a.scale == (uint64_t)ds && tr) {
+          acc |= 1ull << j;
+        }
+      }
+    }
+    nhrow[(size_t)v * Wm + w] = acc;
+  }
+}
+
+__global__ __launch_bounds__(kNsThreads) __attribute__((amdgpu_waves_per_eu(4)))
+void spf_nh_levels_swar_kernel(NhLevelsArgs a) {
+  __shared__ uint32_t st_row[64];
+  __shared__ uint32_t st_node[64];
+  __shared__ uint32_t st_nt[2]; // non-transit neighbours of the staged word
+  const uint32_t q = blockIdx.x;
+  const uint32_t s = a.src[q];
+  const uint32_t Wm = a.nh_w[q];
+  uint64_t* nhrow = a.nh_out + a.nh_off[q];
+  const uint32_t beg = a.nbr_off[s], n = a.nbr_off[s + 1] - beg;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t nchunks = (a.V + kNsChunk - 1) / kNsChunk;
+  const bool deep = a.flags[0] != 0; // uniform
+  const uint8_t* lvl_s = a.lvl + (size_t)q * a.Vp8;
+  for (uint32_t w = 0; w < Wm; ++w) {
+    const uint32_t jlo = w * 64, cnt = min(64u, n - min(n, jlo));
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      bool nt = false;
+      if (threadIdx.x < cnt) {
+        const uint32_t f = a.nbrs[beg + jlo + threadIdx.x];
+        nt = !((a.trbits[f >> 5] >> (f & 31)) & 1u);
+        st_row[threadIdx.x] = (uint32_t)a.row_of[f] * a.Vp8;
+        st_node[threadIdx.x] = f;
+      }
+      const uint64_t b = __ballot(nt);
+      if (threadIdx.x == 0) {
+        st_nt[0] = (uint32_t)b;
+        st_nt[1] = (uint32_t)(b >> 32);
+      }
+    }
+    __syncthreads();
+    // readfirstlane returns int: widen through uint32_t (no sign extension)
+    const uint64_t ntmask =
+        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(st_nt[1]) << 32) |
+        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(st_nt[0]);
+    const uint32_t ngroups = (cnt + 7) / 8;
+    for (uint32_t c = wv; c < nchunks; c += kNsThreads / 64) {
+      const uint32_t v0 = c * kNsChunk + lane * kNsNodes;
+      if (deep) {
+        nl_swar_deep(a, q, v0, w, Wm, cnt, ntmask, st_row, st_node, nhrow);
+        continue;
+      }
+      const bool active = v0 < a.V;
+      uint4 ls = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+      if (active) {
+        ls = *reinterpret_cast<const uint4*>(lvl_s + v0);
+      }
+      const uint32_t lsw[4] = {ls.x, ls.y, ls.z, ls.w};
+      uint32_t tgt[4], live[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        // bytewise ls - 1 (no borrow across bytes), live = not 0, not 255
+        tgt[k] = ((lsw[k] | 0x80808080u) - 0x01010101u) ^ (~lsw[k] & 0x80808080u);
+        live[k] = 0x80808080u & ~(swar_zero_bytes(lsw[k]) | swar_zero_bytes(~lsw[k]));
+      }
+      uint32_t P[4][8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+          P[k][g] = 0;
+        }
+      }
+      if (active) {
+#pragma unroll
+        for (uint32_t g = 0; g < 8; ++g) {
+          if (g < ngroups) {
+            uint4 lf[8];
+#pragma unroll
+            for (uint32_t kk = 0; kk < 8; ++kk) {
+              lf[kk] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+              if (8 * g + kk < cnt) {
+                lf[kk] = *reinterpret_cast<const uint4*>(a.lvl + st_row[8 * g + kk] + v0);
+              }
+            }
+            const uint32_t ntg = (uint32_t)(ntmask >> (8 * g)) & 0xFFu;
+#pragma unroll
+            for (uint32_t kk = 0; kk < 8; ++kk) {
+              const uint32_t lw[4] = {lf[kk].x, lf[kk].y, lf[kk].z, lf[kk].w};
+              uint32_t m[4];
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                m[k] = live[k] & swar_zero_bytes(lw[k] ^ tgt[k]);
+              }
+              if ((ntg >> kk) & 1u) {
+                // a drained neighbour is a next hop only to itself
+                const uint32_t f = st_node[8 * g + kk];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                  const uint32_t r = f - (v0 + 4u * k);
+                  m[k] &= r < 4u ? (0x80u << (8u * r)) : 0u;
+                }
+              }
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                P[k][g] |= m[k] >> (7u - kk);
+              }
+            }
+          }
+        }
+      }
+      if (!active) {
+        continue;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint32_t lo[4], hi[4];
+        swar_transpose4(P[k][0], P[k][1], P[k][2], P[k][3], lo);
+        swar_transpose4(P[k][4], P[k][5], P[k][6], P[k][7], hi);
+        const uint32_t vk = v0 + 4u * k;
+        if (Wm == 1 && vk + 4 <= a.V) {
+          ulonglong2* o = reinterpret_cast<ulonglong2*>(nhrow + vk);
+          o[0] = make_ulonglong2(((uint64_t)hi[0] << 32) | lo[0], ((uint64_t)hi[1] << 32) | lo[1]);
+          o[1] = make_ulonglong2(((uint64_t)hi[2] << 32) | lo[2], ((uint64_t)hi[3] << 32) | lo[3]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (vk + i < a.V) {
+              nhrow[(size_t)(vk + i) * Wm + w] = ((uint64_t)hi[i] << 32) | lo[i];
+            }
+          }
+        }
+      }
+    }
+  }
 }
 
 // six waves per SIMD (<= 80 VGPRs), as before the chunk-inner word loop
@@ -3386,6 +3608,304 @@ __global__ __launch_bounds__(256) void spf_route_table_diff_kernel(
   }
 }
 
+// ------------------------------------------------ k-th path traces (KSP2)
+//
+// getKthPaths' trace loop (LinkState.cpp:776-786) over one query row: repeated
+// traceOnePath (LinkState.cpp:398-419) from the query's source to its
+// destination with one visited-link set, until a trace fails.  One wave per
+// query; the recursion is an explicit stack in LDS whose frames hold a
+// cursor into the node's pathLinks order.  pathLinks(v) = the usable tight
+// in-links u -> v (u reached, u the source or transit, link not ignored,
+// d[u] + w(u->v) == d[v]) ordered by the tail's settle rank (d[u], u) and then
+// by the half-edge's position in u's row (linksFromNode(u) order); on the
+// 32-bit plans every metric is >= 1, so each such tail settles before v.  A
+// frame's next pathLink is the smallest key (d[u] << 32 | u, half-edge + 1)
+// above its cursor: the wave scans v's in-edges 64 at a time and reduces.
+// Visited links live in a per-wave open-addressing set in LDS (64 slots
+// probed per step); nodes whose search failed in a second one (the host
+// trace's `dead` memo: every pathLink of such a node is already visited, so a
+// repeat search fails with no side effect).  A query whose set, stack or
+// output would overflow reports kTraceOverflow and is traced on the host.
+constexpr uint32_t kTraceWaves = 4;      // queries per 256-thread block
+constexpr uint32_t kTraceHash = 1024;    // visited-link slots per wave (<= 1/2 full)
+constexpr uint32_t kTraceDead = 512;     // failed-node slots per wave
+constexpr uint32_t kTraceDepth = 128;    // recursion frames per wave
+constexpr uint32_t kTraceOverflow = 0xFFFFFFFFu;
+constexpr uint32_t kTraceCap = 1024;     // links (and paths) per query
+constexpr uint32_t kTraceEmpty = 0xFFFFFFFFu;
+
+struct TraceArgs {
+  const uint32_t* row;
+  const uint32_t* col;
+  const uint32_t* rev;
+  const uint32_t* link;
+  const uint32_t* wout;
+  const uint32_t* trbits;
+  const uint32_t* src;     // [nq]
+  const uint32_t* dst;     // [nq]
+  const uint32_t* ign_off; // [nq + 1] or nullptr
+  const uint32_t* ign;
+  const uint32_t* dist;    // [nq][Vp]
+  uint32_t* out_n;         // [nq] paths, or kTraceOverflow
+  uint32_t* out_len;       // [nq] links of all its paths
+  uint32_t* out_links;     // [nq][cap] link ids, paths back to back (src -> dst)
+  uint32_t* out_ends;      // [nq][cap] end offset of each path in out_links
+  uint32_t Vp;
+  uint32_t nq;
+  uint32_t cap;
+  uint32_t unit;
+};
+
+__device__ __forceinline__ uint32_t trace_hash(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+// wave-uniform insert of key into a linear-probing set of `cap` slots:
+// 1 = inserted, 0 = present, -1 = full (more than half the slots used)
+template <uint32_t CAP>
+__device__ __forceinline__ int trace_set_insert(uint32_t* set, uint32_t& used, uint32_t key,
+                                                uint32_t lane) {
+  uint32_t h = trace_hash(key);
+  for (uint32_t probe = 0; probe < CAP; probe += 64, h += 64) {
+    const uint32_t slot = (h + lane) & (CAP - 1);
+    const uint32_t x = set[slot];
+    if (__ballot(x == key)) {
+      return 0;
+    }
+    const uint64_t empty = __ballot(x == kTraceEmpty);
+    if (empty) {
+      if (2 * (used + 1) > CAP) {
+        return -1;
+      }
+      const uint32_t first = (uint32_t)__builtin_ctzll(empty);
+      if (lane == first) {
+        set[slot] = key;
+      }
+      ++used;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      return 1;
+    }
+  }
+  return -1;
+}
+
+template <uint32_t CAP>
+__device__ __forceinline__ bool trace_set_has(const uint32_t* set, uint32_t key, uint32_t lane) {
+  uint32_t h = trace_hash(key);
+  for (uint32_t probe = 0; probe < CAP; probe += 64, h += 64) {
+    const uint32_t x = set[(h + lane) & (CAP - 1)];
+    if (__ballot(x == key)) {
+      return true;
+    }
+    if (__ballot(x == kTraceEmpty)) {
+      return false;
+    }
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(64 * kTraceWaves) void spf_trace_paths_kernel(TraceArgs a) {
+  __shared__ uint32_t vis_s[kTraceWaves][kTraceHash];
+  __shared__ uint32_t dead_s[kTraceWaves][kTraceDead];
+  __shared__ uint64_t cp_s[kTraceWaves][kTraceDepth];
+  __shared__ uint32_t ce_s[kTraceWaves][kTraceDepth];
+  __shared__ uint32_t node_s[kTraceWaves][kTraceDepth];
+  __shared__ uint32_t lnk_s[kTraceWaves][kTraceDepth];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t q = blockIdx.x * kTraceWaves + wv;
+  if (q >= a.nq) {
+    return; // whole wave: no block-level barrier below
+  }
+  uint32_t* vis = vis_s[wv];
+  uint32_t* dead = dead_s[wv];
+  uint64_t* cp = cp_s[wv];
+  uint32_t* ce = ce_s[wv];
+  uint32_t* node = node_s[wv];
+  uint32_t* lnk = lnk_s[wv];
+  for (uint32_t i = lane; i < kTraceHash; i += 64) {
+    vis[i] = kTraceEmpty;
+  }
+  for (uint32_t i = lane; i < kTraceDead; i += 64) {
+    dead[i] = kTraceEmpty;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t s = a.src[q], d = a.dst[q];
+  const uint32_t* dist = a.dist + (size_t)q * a.Vp;
+  const uint32_t ilo = a.ign_off ? a.ign_off[q] : 0u;
+  const uint32_t ihi = a.ign_off ? a.ign_off[q + 1] : 0u;
+  uint32_t* out_links = a.out_links + (size_t)q * a.cap;
+  uint32_t* out_ends = a.out_ends + (size_t)q * a.cap;
+  uint32_t npaths = 0, nl = 0, vused = 0, dused = 0;
+  bool overflow = false;
+  if (s != d && dist[d] != kInf32) {
+    for (;;) { // one traceOnePath per iteration
+      uint32_t depth = 0;
+      node[0] = d;
+      cp[0] = 0;
+      ce[0] = 0;
+      bool found = false;
+      for (;;) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t v = node[depth];
+        const uint64_t ccp = cp[depth];
+        const uint32_t cce = ce[depth];
+        const uint64_t dv = dist[v];
+        // next pathLink of v after the cursor (ccp, cce)
+        uint64_t bp = ~0ull;
+        uint32_t bk = kInf32, be = kInf32;
+        const uint32_t e0 = a.row[v], e1 = a.row[v + 1];
+        for (uint32_t base = e0; base < e1; base += 64) {
+          const uint32_t e = base + lane;
+          uint64_t p = ~0ull;
+          uint32_t k2 = kInf32;
+          if (e < e1) {
+            const uint32_t u = a.col[e];
+            const uint32_t du = dist[u];
+            bool ok = du != kInf32 && (u == s || ((a.trbits[u >> 5] >> (u & 31)) & 1u));
+            uint32_t eu = 0;
+            if (ok) {
+              eu = a.rev[e];
+              const uint64_t w = a.unit ? 1ull : (uint64_t)a.wout[eu];
+              ok = (uint64_t)du + w == dv;
+            }
+            if (ok && ihi > ilo) {
+              const uint32_t l = a.link[e];
+              for (uint32_t i = ilo; i < ihi; ++i) {
+                if (a.ign[i] == l) {
+                  ok = false;
+                  break;
+                }
+              }
+            }
+            if (ok) {
+              const uint64_t pk = ((uint64_t)du << 32) | u;
+              if (pk > ccp || (pk == ccp && eu + 1 > cce)) {
+                p = pk;
+                k2 = eu + 1;
+              }
+            }
+          }
+          if (p < bp || (p == bp && k2 < bk)) {
+            bp = p;
+            bk = k2;
+            be = e;
+          }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+          const uint64_t op = (uint64_t)__shfl_xor((unsigned long long)bp, off, 64);
+          const uint32_t ok2 = (uint32_t)__shfl_xor((int)bk, off, 64);
+          const uint32_t oe = (uint32_t)__shfl_xor((int)be, off, 64);
+          if (op < bp || (op == bp && ok2 < bk)) {
+            bp = op;
+            bk = ok2;
+            be = oe;
+          }
+        }
+        if (bp == ~0ull) {
+          // v exhausted: the search from v fails (dead memo, best effort)
+          if (trace_set_insert<kTraceDead>(dead, dused, v, lane) < 0) {
+            dused = kTraceDead; // full: stop recording (an optimisation only)
+          }
+          if (depth == 0) {
+            break;
+          }
+          --depth;
+          continue;
+        }
+        cp[depth] = bp;
+        ce[depth] = bk;
+        const uint32_t l = a.link[be];
+        const int ins = trace_set_insert<kTraceHash>(vis, vused, l, lane);
+        if (ins < 0) {
+          overflow = true;
+          break;
+        }
+        if (ins == 0) {
+          continue; // link already taken by some trace
+        }
+        lnk[depth] = l;
+        const uint32_t u = a.col[be];
+        if (u == s) {
+          found = true;
+          break;
+        }
+        if (trace_set_has<kTraceDead>(dead, u, lane)) {
+          continue; // the recursive search fails at once
+        }
+        if (depth + 1 >= kTraceDepth) {
+          overflow = true;
+          break;
+        }
+        ++depth;
+        node[depth] = u;
+        cp[depth] = 0;
+        ce[depth] = 0;
+      }
+      if (overflow || !found) {
+        break;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t len = depth + 1;
+      if (nl + len > a.cap || npaths + 1 > a.cap) {
+        overflow = true;
+        break;
+      }
+      // frames deepest first: the path runs src -> dst
+      for (uint32_t i = lane; i < len; i += 64) {
+        out_links[nl + i] = lnk[depth - i];
+      }
+      nl += len;
+      if (lane == 0) {
+        out_ends[npaths] = nl;
+      }
+      ++npaths;
+    }
+  }
+  if (lane == 0) {
+    a.out_n[q] = overflow ? kTraceOverflow : npaths;
+    a.out_len[q] = overflow ? 0u : nl;
+  }
+}
+
+struct TracePackArgs {
+  const uint32_t* out_n;
+  const uint32_t* out_len;
+  const uint32_t* links;
+  const uint32_t* ends;
+  const uint32_t* off_links;
+  const uint32_t* off_ends;
+  uint32_t* dst_links;
+  uint32_t* dst_ends;
+  uint32_t cap;
+  uint32_t nq;
+};
+
+// trace scratch [nq][cap] -> packed arrays (offsets from the host scan)
+__global__ __launch_bounds__(64) void spf_trace_pack_kernel(TracePackArgs a) {
+  const uint32_t q = blockIdx.x;
+  const uint32_t n = a.out_n[q];
+  if (n == kTraceOverflow) {
+    return;
+  }
+  const uint32_t len = a.out_len[q];
+  for (uint32_t i = threadIdx.x; i < len; i += 64) {
+    a.dst_links[a.off_links[q] + i] = a.links[(size_t)q * a.cap + i];
+  }
+  for (uint32_t i = threadIdx.x; i < n; i += 64) {
+    a.dst_ends[a.off_ends[q] + i] = a.ends[(size_t)q * a.cap + i];
+  }
+}
+
 __global__ void fill_u32_kernel(uint32_t* p, size_t n, uint32_t v) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -3426,6 +3946,11 @@ struct spf_graph {
   uint32_t* d_cw = nullptr;
   uint32_t cw_bits = 0;
   uint64_t ecc_est = 0; // graph_ecc cache (0 = not computed)
+  uint64_t maxw = 0;       // largest metric (refresh_exact)
+  bool hop_bounded = false; // 32-bit rows justified by transit_hop_bound
+  // sliced-ELL CSR for the MS-BFS pull (MsBfsArgs::sell4), V <= 16 Ki only
+  uint4* d_sell = nullptr;
+  uint32_t* d_sell_off = nullptr;
 };
 
 // How a batch is computed.
@@ -3470,6 +3995,13 @@ struct spf_query {
   uint64_t* d_nh = nullptr;
   uint64_t* d_key = nullptr; // wide plan settle keys (SPF_F_ORDER)
   uint32_t* d_qctr = nullptr; // dstep source-claim counter
+  // k-th path traces (spf_query_trace_paths): device scratch and the last
+  // trace's per-query path / link counts
+  uint32_t* d_trace = nullptr;
+  size_t trace_words = 0;
+  uint32_t trace_n = 0, trace_cap = 0;
+  uint64_t trace_links = 0, trace_paths = 0;
+  std::vector<uint32_t> trace_pc, trace_lc;
   void* d_pack = nullptr;     // the batch's index arrays (one pooled block)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t evm = nullptr; // after the distance stage, before next hops
@@ -3649,7 +4181,8 @@ void free_query(spf_query* q) {
         q->d_dist, (void*)q->d_nh,
         (void*)q->d_lvl, (void*)q->d_flags, (void*)q->d_perm,
         (void*)q->d_slab, (void*)q->d_msd, (void*)q->d_base_of,
-        (void*)q->d_skip, (void*)q->d_key, (void*)q->d_qctr, (void*)q->d_scatter}) {
+        (void*)q->d_skip, (void*)q->d_key, (void*)q->d_qctr, (void*)q->d_scatter,
+        (void*)q->d_trace}) {
     pool_free(p);
   }
   if (q->base) {
@@ -3672,6 +4205,79 @@ void free_query(spf_query* q) {
     }
   }
   delete q;
+}
+
+// Upper bound on the hop count of some valid path from any node to any node
+// it reaches: 2 * ecc(r) for a transit hub r whose transit-only BFS (a node
+// is expanded iff it is r or may be transited, LinkState.cpp:829-836)
+// reaches every node.  For a source s and a node v it reaches, the BFS tree
+// paths s <- r and r -> v have transit interiors and r is transit, so their
+// concatenation is a walk the SPF from s may take (the source is exempt) of
+// at most 2 * ecc(r) links.  0 = no such hub (no transit node, or the hub
+// does not reach every node: partitioned by drained nodes).
+uint64_t transit_hop_bound(const std::vector<uint32_t>& row, const std::vector<uint32_t>& col,
+                           const std::vector<uint32_t>& trbits, uint32_t V) {
+  auto transit = [&](uint32_t v) { return (trbits[v >> 5] >> (v & 31)) & 1u; };
+  uint32_t r = kInf32, best = 0;
+  for (uint32_t v = 0; v < V; ++v) {
+    const uint32_t d = row[v + 1] - row[v];
+    if (transit(v) && (r == kInf32 || d > best)) {
+      r = v;
+      best = d;
+    }
+  }
+  if (r == kInf32) {
+    return 0;
+  }
+  std::vector<uint32_t> lvl(V, kInf32), cur{r}, nxt;
+  lvl[r] = 0;
+  uint32_t reached = 1, depth = 0;
+  while (!cur.empty()) {
+    nxt.clear();
+    for (uint32_t u : cur) {
+      if (u != r && !transit(u)) {
+        continue;
+      }
+      for (uint32_t e = row[u]; e < row[u + 1]; ++e) {
+        const uint32_t v = col[e];
+        if (lvl[v] == kInf32) {
+          lvl[v] = depth + 1;
+          nxt.push_back(v);
+          ++reached;
+        }
+      }
+    }
+    if (!nxt.empty()) {
+      ++depth;
+    }
+    cur.swap(nxt);
+  }
+  return reached == V ? 2ull * depth : 0;
+}
+
+// g->exact: the batch needs 64-bit rows (wide / literal plans).  A metric 0
+// or a wrapping metric always does; otherwise 32-bit rows are exact when no
+// distance (nor distance + one link) can reach 2^32 - 1 (kInf32): first the
+// coarse maxw * (V - 1) bound, then maxw * (transit_hop_bound + 1), so a
+// WAN with metrics to 10^6 keeps the 32-bit plans.  Re-run when transit bits
+// change (a drain can lengthen paths).
+void refresh_exact(spf_graph* g) {
+  const uint32_t V = g->V;
+  const uint64_t maxw = g->maxw;
+  bool exact = g->wrap || g->n_zero > 0;
+  g->hop_bounded = false;
+  if (!exact && V > 1 && maxw > 0 &&
+      (unsigned __int128)maxw * (V - 1) >= 0xFFFFFFFFull) {
+    const uint64_t h = env_flag("OPENR_SPF_HOP_BOUND", 1)
+                           ? transit_hop_bound(g->row, g->col, g->trbits, V)
+                           : 0;
+    if (h && (unsigned __int128)maxw * (h + 1) < 0xFFFFFFFFull) {
+      g->hop_bounded = true;
+    } else {
+      exact = true;
+    }
+  }
+  g->exact = exact;
 }
 
 // fast-path weights, exactness, uniformity and per-neighbour cheapest metric
@@ -3714,14 +4320,11 @@ int upload_weights(spf_graph* g) {
     zero_e.insert(zero_e.end(), zeros[w].begin(), zeros[w].end());
   }
   std::sort(zero_e.begin(), zero_e.end());
-  bool exact = wrap || !zero_e.empty();
-  if (!exact && V > 1 && maxw > 0 &&
-      (unsigned __int128)maxw * (V - 1) >= 0xFFFFFFFFull) {
-    exact = true;
-  }
-  g->exact = exact;
   g->wrap = wrap;
   g->n_zero = (uint32_t)zero_e.size();
+  g->maxw = maxw;
+  refresh_exact(g);
+  const bool exact = g->exact;
   // wide plan band: the mean metric (near-far's delta ~ a typical edge)
   g->wide_delta = E ? std::max<uint64_t>(1, sumw / E) : 1;
   if (g->d_zero_e) {
@@ -3797,6 +4400,42 @@ int upload_weights(spf_graph* g) {
     g->cw_bits = bits;
   }
   return SPF_OK;
+}
+
+// Sliced-ELL copy of the CSR for spf_msbfs_kernel: slice c = nodes
+// [64c, 64c + 64) (one wave's node slot), width = the slice's largest degree
+// rounded up to 4; lane L's edge j sits in word j % 4 of the uint4 at group
+// sell_off[c] + j / 4, so one wave load covers 1 KB.  Rows are padded with
+// the node's own id (harmless in the pull, see MsBfsArgs).  Name ranks keep
+// nodes of one role (SSW / FSW / RSW) adjacent, so the padding is small
+// (fabric: 232,512 edges -> 233,472 slots).
+int upload_sell(spf_graph* g) {
+  const uint32_t V = g->V, ns = (V + 63) / 64;
+  std::vector<uint32_t> off(ns + 1, 0);
+  for (uint32_t c = 0; c < ns; ++c) {
+    uint32_t w = 0;
+    for (uint32_t v = 64 * c; v < std::min(V, 64 * c + 64); ++v) {
+      w = std::max(w, g->row[v + 1] - g->row[v]);
+    }
+    off[c + 1] = off[c] + (w + 3) / 4;
+  }
+  std::vector<uint32_t> sell((size_t)off[ns] * 256);
+  for (uint32_t c = 0; c < ns; ++c) {
+    const uint32_t groups = off[c + 1] - off[c];
+    for (uint32_t L = 0; L < 64; ++L) {
+      const uint32_t v = 64 * c + L;
+      const uint32_t deg = v < V ? g->row[v + 1] - g->row[v] : 0;
+      for (uint32_t j = 0; j < groups * 4; ++j) {
+        const uint32_t x = j < deg ? g->col[g->row[v] + j] : (v < V ? v : 0);
+        sell[((size_t)(off[c] + j / 4) * 64 + L) * 4 + (j & 3)] = x;
+      }
+    }
+  }
+  int s = dev_upload(&g->d_sell_off, off.data(), off.size());
+  if (s == SPF_OK && !sell.empty()) {
+    s = dev_upload((uint32_t**)&g->d_sell, sell.data(), sell.size());
+  }
+  return s;
 }
 
 inline size_t lds_ctl_bytes(const spf_graph* g, uint32_t ign_cap) {
@@ -4229,6 +4868,9 @@ int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
       return bail(s);
     }
   }
+  if (V && V <= kMsThreads * kMsMaxK && (s = upload_sell(g))) {
+    return bail(s);
+  }
   *out = g;
   return SPF_OK;
 }
@@ -4256,6 +4898,10 @@ int spf_graph_set_transit(spf_graph* g, const uint8_t* node_overloaded) {
   // the call returns, so trbits may change again right away)
   HIP_TRY(hipMemcpyAsync(g->d_tr, g->trbits.data(), g->trbits.size() * 4,
                          hipMemcpyHostToDevice, g->stream));
+  if (g->hop_bounded || (g->maxw && !g->wrap && !g->n_zero &&
+                         (unsigned __int128)g->maxw * (g->V - 1) >= 0xFFFFFFFFull)) {
+    refresh_exact(g); // the hop bound depends on which nodes may be transited
+  }
   return SPF_OK;
 }
 
@@ -4926,6 +5572,9 @@ int launch_msbfs(spf_query* q, bool unit) {
   MsBfsArgs a;
   a.row = g->d_row;
   a.col = g->d_col;
+  const bool sell = g->d_sell && env_flag("OPENR_MS_SELL", 1);
+  a.sell4 = g->d_sell;
+  a.sell_off = g->d_sell_off;
   a.trbits = g->d_tr;
   a.src = q->d_src;
   a.dist_out = (uint32_t*)q->d_dist;
@@ -4939,7 +5588,9 @@ int launch_msbfs(spf_query* q, bool unit) {
   HIP_TRY(hipMemsetAsync(q->d_flags, 0, 16, g->stream));
   const uint32_t K = (g->V + kMsThreads - 1) / kMsThreads;
   const void* kern = nullptr;
-#define MS_PICK(MT, KM) kern = (const void*)spf_msbfs_kernel<MT, KM>
+#define MS_PICK(MT, KM)                                                            \
+  kern = sell ? (const void*)spf_msbfs_kernel<MT, KM, true>                        \
+              : (const void*)spf_msbfs_kernel<MT, KM, false>
   if (q->ms_bits == 64) {
     if (K <= 4) {
       MS_PICK(uint64_t, 4);
@@ -4990,13 +5641,19 @@ int launch_nh_levels(spf_query* q, bool unit) {
   a.Vp8 = q->Vp8;
   a.nq = q->nq;
   a.scale = unit ? 1u : g->uniform;
-  a.xcd_swizzle = env_flag("OPENR_NL_XCD", 1);
+  a.xcd_swizzle = env_flag("OPENR_NL_XCD", 0);
   a.held_words = env_flag("OPENR_NL_HELD", 1);
   const uint32_t nchunks = (g->V + kNlChunk - 1) / kNlChunk;
   const uint64_t blocks =
       (uint64_t)((nchunks + kNlChunksPerBlock - 1) / kNlChunksPerBlock) * q->nq;
   if (blocks > 0x7FFFFFFFull) {
     return fail(SPF_E_UNSUPPORTED, "batch too large for the next-hop pass");
+  }
+  if (env_flag("OPENR_NL_SWAR", 1)) {
+    hipLaunchKernelGGL(spf_nh_levels_swar_kernel, dim3(q->nq), dim3(kNsThreads), 0,
+                       g->stream, a);
+    HIP_TRY(hipGetLastError());
+    return SPF_OK;
   }
   hipLaunchKernelGGL(spf_nh_levels_kernel, dim3((uint32_t)blocks),
                      dim3(kNlThreads), 0, g->stream, a);
@@ -5473,6 +6130,150 @@ int spf_query_fetch_rows(
   if (!dst_on_device) {
     HIP_TRY(hipStreamSynchronize(q->g->stream));
   }
+  return SPF_OK;
+}
+
+int spf_query_trace_paths(
+    spf_query* q, uint32_t first, uint32_t count, const uint32_t* dests, uint32_t* path_count,
+    uint32_t* link_count) {
+  SPF_ABI_RANGE("spf_query_trace_paths");
+  if (!q || (count && (!dests || !path_count || !link_count))) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  if (!q->ran) {
+    return fail(SPF_E_INVALID, "query has not run");
+  }
+  if ((uint64_t)first + count > q->nq) {
+    return fail(SPF_E_INVALID, "query range out of bounds");
+  }
+  if (rows64(q)) {
+    return fail(SPF_E_UNSUPPORTED, "64-bit distance rows (settle keys): trace on the host");
+  }
+  const spf_graph* g = q->g;
+  for (uint32_t i = 0; i < count; ++i) {
+    if (dests[i] >= g->V) {
+      return fail(SPF_E_INVALID, "destination out of range");
+    }
+  }
+  q->trace_n = 0;
+  q->trace_links = 0;
+  q->trace_paths = 0;
+  if (count == 0) {
+    return SPF_OK;
+  }
+  HIP_TRY(hipSetDevice(g->device));
+  // scratch: dests | out_n | out_len | links [count][cap] | ends [count][cap]
+  // (OPENR_SPF_TRACE_CAP lowers the per-query capacity: overflow tests)
+  const uint32_t cap = std::max<uint32_t>(1, std::min(kTraceCap, env_flag("OPENR_SPF_TRACE_CAP", kTraceCap)));
+  q->trace_cap = cap;
+  const size_t cells = (size_t)count * cap;
+  const size_t words = 3 * (size_t)count + 2 * cells;
+  if (q->d_trace && q->trace_words < words) {
+    HIP_TRY(hipStreamSynchronize(g->stream));
+    pool_free(q->d_trace);
+    q->d_trace = nullptr;
+  }
+  if (!q->d_trace) {
+    HIP_TRY(pool_malloc((void**)&q->d_trace, words * 4));
+    q->trace_words = words;
+  }
+  uint32_t* buf = q->d_trace;
+  HIP_TRY(hipMemcpyAsync(buf, dests, (size_t)count * 4, hipMemcpyHostToDevice, g->stream));
+  TraceArgs a;
+  a.row = g->d_row;
+  a.col = g->d_col;
+  a.rev = g->d_rev;
+  a.link = g->d_link;
+  a.wout = g->d_wout;
+  a.trbits = g->d_tr;
+  a.src = q->d_src + first;
+  a.dst = buf;
+  a.ign_off = q->d_ign_off ? q->d_ign_off + first : nullptr;
+  a.ign = q->d_ign;
+  a.dist = (const uint32_t*)q->d_dist + (size_t)first * q->Vp;
+  a.out_n = buf + count;
+  a.out_len = buf + 2 * (size_t)count;
+  a.out_links = buf + 3 * (size_t)count;
+  a.out_ends = buf + 3 * (size_t)count + cells;
+  a.Vp = q->Vp;
+  a.nq = count;
+  a.cap = cap;
+  a.unit = (q->flags & SPF_F_UNIT_METRIC) ? 1u : 0u;
+  hipLaunchKernelGGL(spf_trace_paths_kernel, dim3((count + kTraceWaves - 1) / kTraceWaves),
+                     dim3(64 * kTraceWaves), 0, g->stream, a);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(path_count, a.out_n, (size_t)count * 4, hipMemcpyDeviceToHost,
+                         g->stream));
+  HIP_TRY(hipMemcpyAsync(link_count, a.out_len, (size_t)count * 4, hipMemcpyDeviceToHost,
+                         g->stream));
+  HIP_TRY(hipStreamSynchronize(g->stream));
+  q->trace_n = count;
+  q->trace_pc.assign(path_count, path_count + count);
+  q->trace_lc.assign(link_count, link_count + count);
+  for (uint32_t i = 0; i < count; ++i) {
+    if (path_count[i] != SPF_TRACE_OVERFLOW) {
+      q->trace_links += link_count[i];
+      q->trace_paths += path_count[i];
+    }
+  }
+  return SPF_OK;
+}
+
+int spf_query_trace_fetch(spf_query* q, uint32_t* links, uint32_t* ends) {
+  SPF_ABI_RANGE("spf_query_trace_fetch");
+  if (!q || (q->trace_links && !links) || (q->trace_paths && !ends)) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  const uint32_t count = q->trace_n;
+  if (count == 0 || (q->trace_links == 0 && q->trace_paths == 0)) {
+    return SPF_OK;
+  }
+  spf_graph* g = q->g;
+  HIP_TRY(hipSetDevice(g->device));
+  // destination offsets of every query's links and ends (host scan), then
+  // one pack kernel and two copies
+  std::vector<uint32_t> off(2 * (size_t)count);
+  uint64_t lo = 0, po = 0;
+  for (uint32_t i = 0; i < count; ++i) {
+    const bool ok = q->trace_pc[i] != SPF_TRACE_OVERFLOW;
+    off[i] = (uint32_t)lo;
+    off[count + i] = (uint32_t)po;
+    lo += ok ? q->trace_lc[i] : 0;
+    po += ok ? q->trace_pc[i] : 0;
+  }
+  uint32_t* pk = nullptr; // offsets [2 * count] | links [lo] | ends [po]
+  HIP_TRY(pool_malloc((void**)&pk, (2 * (size_t)count + lo + po) * 4));
+  struct Free {
+    uint32_t* p;
+    hipStream_t st;
+    ~Free() {
+      (void)hipStreamSynchronize(st);
+      pool_free(p);
+    }
+  } guard{pk, g->stream};
+  HIP_TRY(hipMemcpyAsync(pk, off.data(), off.size() * 4, hipMemcpyHostToDevice, g->stream));
+  const size_t cells = (size_t)count * q->trace_cap;
+  uint32_t* buf = q->d_trace;
+  TracePackArgs a;
+  a.out_n = buf + count;
+  a.out_len = buf + 2 * (size_t)count;
+  a.links = buf + 3 * (size_t)count;
+  a.ends = buf + 3 * (size_t)count + cells;
+  a.off_links = pk;
+  a.off_ends = pk + count;
+  a.dst_links = pk + 2 * (size_t)count;
+  a.dst_ends = pk + 2 * (size_t)count + lo;
+  a.cap = q->trace_cap;
+  a.nq = count;
+  hipLaunchKernelGGL(spf_trace_pack_kernel, dim3(count), dim3(64), 0, g->stream, a);
+  HIP_TRY(hipGetLastError());
+  if (lo) {
+    HIP_TRY(hipMemcpyAsync(links, a.dst_links, lo * 4, hipMemcpyDeviceToHost, g->stream));
+  }
+  if (po) {
+    HIP_TRY(hipMemcpyAsync(ends, a.dst_ends, po * 4, hipMemcpyDeviceToHost, g->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(g->stream));
   return SPF_OK;
 }
 

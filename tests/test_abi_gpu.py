@@ -443,3 +443,119 @@ def test_whatif_screen_matches_full_runs(gpu_ready, weighted, monkeypatch):
         assert (q.dist(i) == r.dist(i)).all(), i
         assert (q.nexthops(i) == r.nexthops(i)).all(), i
     check_query(csr, q, srcs, True, ignore=ign, rows={0, 5, 6, 310, 499})
+
+
+@pytest.mark.parametrize("V,L,wmax", [(300, 1200, 10 ** 8), (20000, 80000, 10 ** 6)])
+def test_hop_bound_keeps_32bit_rows(gpu_ready, V, L, wmax, monkeypatch):
+    """Large metrics whose coarse bound maxw * (V - 1) passes 2^32 still run
+    the 32-bit plans when maxw * (transit hop bound + 1) fits (refresh_exact):
+    same rows as the literal replay, drained nodes included; the 64-bit
+    plan (OPENR_SPF_HOP_BOUND=0) agrees bit for bit."""
+    from openr_amd.allsources import needs_64bit_rows
+
+    rng = random.Random(V)
+    links = random_links(rng, V, L, wmin=1, wmax=wmax, parallel=0.01)
+    ov = np.zeros(V, dtype=np.uint8)
+    ov[rng.sample(range(V), V // 100)] = 1
+    csr = abi.Csr.from_links(V, links, overloaded=ov)
+    assert wmax * (V - 1) >= 1 << 32
+    g = abi.Graph(csr)
+    assert not g.needs_exact
+    assert not needs_64bit_rows(csr)
+    srcs = [0, 1, V - 1] + [rng.randrange(V) for _ in range(5)]
+    q = g.query(srcs, abi.SPF_F_NEXTHOPS).run()
+    assert q.kernel != "wide"
+    rows = set(range(len(srcs))) if V <= 1000 else {0, 2}
+    check_query(csr, q, srcs, True, rows=rows)
+    monkeypatch.setenv("OPENR_SPF_HOP_BOUND", "0")
+    g64 = abi.Graph(csr)
+    assert g64.needs_exact
+    w = g64.query(srcs, abi.SPF_F_NEXTHOPS).run()
+    assert w.kernel == "wide"
+    for i in range(len(srcs)):
+        assert (w.dist(i) == q.dist(i)).all(), i
+        assert w.nexthop_sets(i, srcs[i]) == q.nexthop_sets(i, srcs[i]), i
+
+
+def test_hop_bound_follows_drains(gpu_ready):
+    """A drain that partitions the transit graph withdraws the hop bound
+    (spf_graph_set_transit re-runs refresh_exact); undraining restores it."""
+    # star 0 - {1..8} plus 9 - 8: hub 0, ecc 2 -> bound 4 hops; 5w fits in
+    # 32 bits, the coarse 9w does not
+    w = (1 << 32) // 7
+    links = [(0, v, w, w) for v in range(1, 9)] + [(8, 9, w, w)]
+    csr = abi.Csr.from_links(10, links)
+    g = abi.Graph(csr)
+    assert not g.needs_exact
+    ov = np.zeros(10, dtype=np.uint8)
+    ov[8] = 1
+    g.set_transit(ov)
+    assert g.needs_exact  # the hub no longer reaches 9
+    g.set_transit(np.zeros(10, dtype=np.uint8))
+    assert not g.needs_exact
+
+
+@pytest.mark.parametrize("sell", ["0", "1"])
+def test_msbfs_sliced_ell_matches_csr(gpu_ready, sell, monkeypatch):
+    """MS-BFS over the sliced-ELL copy of the CSR (upload_sell) and over the
+    plain CSR: identical distance and next-hop rows, checked against the
+    literal replay on a few sources (irregular degrees, drained nodes, parallel
+    links, a ragged last slice)."""
+    monkeypatch.setenv("OPENR_MS_SELL", sell)
+    rng = random.Random(77)
+    V = 3001
+    links = random_links(rng, V, 9000, wmin=1, wmax=1, parallel=0.05)
+    links += [(5, v, 1, 1) for v in range(100, 400)]  # a hub: a wide slice
+    ov = np.zeros(V, dtype=np.uint8)
+    ov[rng.sample(range(V), 30)] = 1
+    csr = abi.Csr.from_links(V, links, overloaded=ov)
+    g = abi.Graph(csr)
+    srcs = np.arange(V, dtype=np.uint32)
+    q = g.query(srcs, abi.SPF_F_NEXTHOPS | abi.SPF_F_UNIT_METRIC).run()
+    assert q.kernel == "msbfs+levels"
+    check_query(csr, q, [int(s) for s in srcs], False, rows={0, 5, 17, 1500, V - 1})
+    monkeypatch.setenv("OPENR_MS_SELL", "1" if sell == "0" else "0")
+    r = g.query(srcs, abi.SPF_F_NEXTHOPS | abi.SPF_F_UNIT_METRIC).run()
+    for i in range(0, V, 97):
+        assert (q.dist(i) == r.dist(i)).all(), i
+        assert (q.nexthops(i) == r.nexthops(i)).all(), i
+
+
+@pytest.mark.parametrize("case", ["random", "hubs", "deep"])
+def test_nh_levels_swar_matches_scalar(gpu_ready, case, monkeypatch):
+    """The byte-SIMD next-hop pass (spf_nh_levels_swar_kernel) against the
+    per-node pass (spf_nh_levels_kernel) on the same MS-BFS rows, and both
+    against the literal replay on a few sources: drained neighbours (next
+    hop only to themselves), sources with 1-3 mask words, a ragged last
+    chunk, and a BFS deeper than 254 levels (the 32-bit-row branch)."""
+    rng = random.Random({"random": 5, "hubs": 6, "deep": 7}[case])
+    if case == "deep":
+        V = 700  # a 600-node chain hanging off a random core: levels > 255
+        links = random_links(rng, 100, 400, wmin=1, wmax=1, parallel=0.0)
+        links += [(99 + i, 100 + i, 1, 1) for i in range(600)]
+    else:
+        V = 2500 if case == "random" else 1300
+        links = random_links(rng, V, 7000, wmin=1, wmax=1, parallel=0.03)
+        if case == "hubs":
+            links += [(7, v, 1, 1) for v in range(100, 260)]  # 3 mask words
+            links += [(8, v, 1, 1) for v in range(300, 400)]  # 2 mask words
+    ov = np.zeros(V, dtype=np.uint8)
+    ov[rng.sample(range(V), V // 40)] = 1
+    csr = abi.Csr.from_links(V, links, overloaded=ov)
+    g = abi.Graph(csr)
+    srcs = np.arange(V, dtype=np.uint32)
+    flags = abi.SPF_F_NEXTHOPS | abi.SPF_F_UNIT_METRIC
+    monkeypatch.setenv("OPENR_NL_SWAR", "1")
+    a = g.query(srcs, flags).run()
+    assert a.kernel == "msbfs+levels"
+    monkeypatch.setenv("OPENR_NL_SWAR", "0")
+    b = g.query(srcs, flags).run()
+    for i in range(V):
+        assert a.nh_words(i) == b.nh_words(i)
+    ma = a.fetch_nexthops(0, V)
+    mb = b.fetch_nexthops(0, V)
+    if not (ma == mb).all():
+        bad = int(np.flatnonzero(ma != mb)[0])
+        pytest.fail(f"mask word {bad} differs: {ma[bad]:#x} vs {mb[bad]:#x}")
+    probe = [0, 7, 8, V - 1, V // 2] if case != "deep" else [0, 99, 650, 699]
+    check_query(csr, a, [int(s) for s in srcs], False, rows=set(probe))

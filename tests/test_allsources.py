@@ -174,3 +174,24 @@ def test_needs_64bit_rows_matches_engine_rule():
     big = (1 << 32) // 3 + 1  # maxw * (V - 1) >= 2^32 at V = 4
     assert needs_64bit_rows(csr([(0, 1, big, 1)]))
     assert not needs_64bit_rows(csr([(0, 1, big - 2, 1)]))
+
+
+def test_transit_hop_bound_rule():
+    """The 32-bit row bound's hop count (spf_device.hip transit_hop_bound):
+    2 * eccentricity of the first highest-degree transit node, 0 when a drain
+    cuts a node off from it."""
+    import numpy as np
+
+    from openr_amd import abi
+    from openr_amd.allsources import needs_64bit_rows, transit_hop_bound
+
+    star = [(0, v, 1, 1) for v in range(1, 9)] + [(8, 9, 1, 1)]
+    csr = abi.Csr.from_links(10, star)
+    assert transit_hop_bound(csr) == 4
+    ov = np.zeros(10, dtype=np.uint8)
+    ov[8] = 1
+    assert transit_hop_bound(abi.Csr.from_links(10, star, overloaded=ov)) == 0
+    w = (1 << 32) // 7  # 5w fits, 9w (the coarse V - 1 bound) does not
+    big = [(a, b, w, w) for (a, b, _, _) in star]
+    assert not needs_64bit_rows(abi.Csr.from_links(10, big))
+    assert needs_64bit_rows(abi.Csr.from_links(10, big, overloaded=ov))

@@ -16,7 +16,8 @@ step time, gather included.
 Roofline: the dominant kernel of the step (the one with the larger average
 device time over the timed launches, HIP events on the engine's stream) is
 priced by its ALGORITHMIC bytes per launch:
-  spf_nh_levels_kernel  sum_q [ V*(1 + nbrs(q)) * b + 8*V*W_q ]
+  spf_nh_levels_held_kernel (or spf_nh_levels_kernel)
+                        sum_q [ V*(1 + nbrs(q)) * b + 8*V*W_q ]
                          (own level row + one row per distinct neighbour of
                           the source, b = 1 byte per 8-bit level, 4 if the
                           32-bit rows are used; next-hop mask row written)
@@ -43,8 +44,12 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 
+# the next-hop stage of the MS-BFS plan: the byte-SIMD held-word kernel
+# (+ spf_nh_levels_swar_kernel for sources with > 3 mask words, none on the
+# fabric) unless OPENR_NL_SWAR=0 selects the per-node spf_nh_levels_kernel
+_NL = "spf_nh_levels_kernel" if os.environ.get("OPENR_NL_SWAR") == "0" else "spf_nh_levels_held_kernel"
 KERNELS = {
-    "msbfs+levels": ("spf_msbfs_kernel", "spf_nh_levels_kernel"),
+    "msbfs+levels": ("spf_msbfs_kernel", _NL),
     "bfs+rows": ("spf_bfs_kernel", "spf_nh_rows_kernel"),
     "bfs-gmem+rows": ("spf_bfs_kernel", "spf_nh_rows_kernel"),
     "lds+rows": ("spf_sssp_kernel", "spf_nh_rows_kernel"),

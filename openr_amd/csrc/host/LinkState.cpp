@@ -831,12 +831,12 @@ struct DeviceTraces {
   bool unsupported = false; // 64-bit rows in some block: use runBatchAuto
 };
 
+// opt-in (OPENR_KSP2_DEVICE_TRACE=1): on the fabric the device traces cost
+// more than the host pool's (profiles/r03d: 59 ms of device DFS, 632 of
+// 9,975 traces overflowing to the host, KSP2 loop 219 ms vs 174-189 ms)
 bool deviceTraceEnabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("OPENR_KSP2_DEVICE_TRACE");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on;
+  const char* e = std::getenv("OPENR_KSP2_DEVICE_TRACE");
+  return e && std::atoi(e) != 0;
 }
 
 DeviceTraces traceSecondPasses(

@@ -1827,6 +1827,7 @@ struct MsBfsArgs {
   uint32_t Vp8;
   uint32_t nq;
   uint32_t scale;
+  uint32_t wrec; // 1: wave-cooperative row stores (ms_record_wave)
 };
 
 // Write each (source, node) distance the moment its bit appears (one store
@@ -1847,6 +1848,37 @@ __device__ __forceinline__ void ms_record(
     bits &= bits - 1;
     a.dist_out[(size_t)(q0 + s) * a.Vp + v] = d;
     a.lvl_out[(size_t)(q0 + s) * a.Vp8 + v] = l8;
+  }
+}
+
+// Wave-cooperative form (OPENR_MS_WREC, default): the lanes' bit sets are
+// OR-reduced over the wave and the wave walks the union bit by bit, so every
+// store instruction writes source s's row at the wave's 64 consecutive nodes
+// (256 contiguous bytes of distances, 64 of levels) instead of 64 lanes
+// scattering into 64 different rows.  Every lane of the wave must call it.
+template <typename MT>
+__device__ __forceinline__ void ms_record_wave(
+    const MsBfsArgs& a, uint32_t q0, uint32_t v, MT bits, uint32_t level) {
+  uint64_t w = (uint64_t)bits;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    w |= (uint64_t)__shfl_xor((unsigned long long)w, off, 64);
+  }
+  if (!w) {
+    return;
+  }
+  const uint32_t d = level * a.scale;
+  const uint8_t l8 = level < 255 ? (uint8_t)level : (uint8_t)255;
+  if (level >= 255 && bits) {
+    atomicOr(a.flags, 1u);
+  }
+  while (w) {
+    const uint32_t s = (uint32_t)__builtin_ctzll((unsigned long long)w);
+    w &= w - 1;
+    if (((uint64_t)bits >> s) & 1u) {
+      a.dist_out[(size_t)(q0 + s) * a.Vp + v] = d;
+      a.lvl_out[(size_t)(q0 + s) * a.Vp8 + v] = l8;
+    }
   }
 }
 
@@ -1887,8 +1919,12 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
         trm |= ((a.trbits[v >> 5] >> (v & 31)) & 1u) << k;
       }
       vis[k] = (k < K && v < V) ? cur[v] : (MT)0;
-      if (k < K && v < V && vis[k]) {
-        ms_record<MT>(a, q0, v, vis[k], 0); // level 0 = the sources
+      if (a.wrec) {
+        if (k < K) {
+          ms_record_wave<MT>(a, q0, v, vis[k], 0); // level 0 = the sources
+        }
+      } else if (k < K && v < V && vis[k]) {
+        ms_record<MT>(a, q0, v, vis[k], 0);
       }
     }
     uint32_t level = 0;
@@ -1901,11 +1937,12 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
         // opaque to the optimizer: keeps per-node addressing from being
         // hoisted out of the level loop (KMAX copies of it spill VGPRs)
         asm volatile("" : "+v"(v));
-        if (k >= K || v >= V) {
-          continue;
+        if (k >= K) {
+          continue; // uniform
         }
+        const bool valid = v < V;
         MT nw = 0;
-        if (SELL && vis[k] != full) {
+        if (SELL && valid && vis[k] != full) {
           // a wave reads 1 KB of its slice per load instead of one line per lane
           const uint32_t c = __builtin_amdgcn_readfirstlane(v >> 6);
           const uint32_t g0 = __builtin_amdgcn_readfirstlane(a.sell_off[c]);
@@ -1924,7 +1961,7 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
           }
           nw = acc & ~vis[k];
           vis[k] |= nw;
-        } else if (!SELL && vis[k] != full) {
+        } else if (!SELL && valid && vis[k] != full) {
           const uint32_t beg = a.row[v], end = a.row[v + 1];
           MT acc = 0;
           uint32_t e = beg;
@@ -1949,8 +1986,12 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
         }
         any |= nw != 0;
         const bool transit = (trm >> k) & 1u;
-        nxt[v] = transit ? nw : (MT)0;
-        if (nw) {
+        if (valid) {
+          nxt[v] = transit ? nw : (MT)0;
+        }
+        if (a.wrec) {
+          ms_record_wave<MT>(a, q0, v, nw, L);
+        } else if (nw) {
           ms_record<MT>(a, q0, v, nw, L);
         }
       }
@@ -1967,7 +2008,25 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
 #pragma unroll
     for (uint32_t k = 0; k < KMAX; ++k) {
       const uint32_t v = tid + k * kMsThreads;
-      if (k < K && v < V) {
+      if (a.wrec) {
+        if (k < K) {
+          // unreached pairs as one more "level" whose value is the sentinel
+          const MT miss = v < V ? (full & ~vis[k]) : (MT)0;
+          uint64_t w = (uint64_t)miss;
+#pragma unroll
+          for (int off = 32; off >= 1; off >>= 1) {
+            w |= (uint64_t)__shfl_xor((unsigned long long)w, off, 64);
+          }
+          while (w) {
+            const uint32_t s = (uint32_t)__builtin_ctzll((unsigned long long)w);
+            w &= w - 1;
+            if (((uint64_t)miss >> s) & 1u) {
+              a.dist_out[(size_t)(q0 + s) * a.Vp + v] = kInf32;
+              a.lvl_out[(size_t)(q0 + s) * a.Vp8 + v] = 255;
+            }
+          }
+        }
+      } else if (k < K && v < V) {
         MT miss = full & ~vis[k];
         while (miss) {
           const uint32_t s = (uint32_t)__builtin_ctzll((unsigned long long)miss);
@@ -2464,19 +2523,152 @@ __device__ __noinline__ void nl_swar_deep(
   }
 }
 
+// The SWAR pass for sources with at most kNsHeldMax mask words (every
+// fabric source): all neighbours are staged once; a lane owns four nodes in
+// each of the chunk's four 256-node segments (4-byte loads, 256 contiguous
+// bytes per wave per neighbour row), computes every word of its four nodes
+// back to back and stores the 4 x Wm words as one contiguous 32*Wm-byte run,
+// so a wave writes 2*Wm KB of mask row contiguously per segment (the per-lane
+// 16-node layout stored 16-byte pieces 128 bytes apart: twice the L2 write
+// requests, profiles/r03e).
+constexpr uint32_t kNsHeldMax = 3;
+constexpr uint32_t kNsHeldThreads = 256; // one block per (source, 1024-node chunk)
+
+__device__ __forceinline__ void nl_swar_held(
+    const NhLevelsArgs& a, uint32_t q, uint32_t c, uint32_t Wm, uint32_t n, uint32_t beg,
+    uint64_t* nhrow, const uint8_t* lvl_s, uint32_t* st_row, uint32_t* st_node, uint32_t* st_nt) {
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  for (uint32_t t = threadIdx.x; t < 64 * kNsHeldMax; t += kNsHeldThreads) {
+    bool nt = false;
+    if (t < n) {
+      const uint32_t f = a.nbrs[beg + t];
+      nt = !((a.trbits[f >> 5] >> (f & 31)) & 1u);
+      st_row[t] = (uint32_t)a.row_of[f] * a.Vp8;
+      st_node[t] = f;
+    }
+    const uint64_t b = __ballot(nt);
+    if (lane == 0) {
+      st_nt[2 * (t >> 6)] = (uint32_t)b;
+      st_nt[2 * (t >> 6) + 1] = (uint32_t)(b >> 32);
+    }
+  }
+  __syncthreads();
+  {
+    {
+      const uint32_t v0 = c * kNsChunk + wv * 256 + 4 * lane;
+      if (v0 >= a.V) {
+        return;
+      }
+      const uint32_t ls = *reinterpret_cast<const uint32_t*>(lvl_s + v0);
+      const uint32_t tgt = ((ls | 0x80808080u) - 0x01010101u) ^ (~ls & 0x80808080u);
+      const uint32_t live =
+          0x80808080u & ~(swar_zero_bytes(ls) | swar_zero_bytes(~ls));
+      uint64_t held[kNsHeldMax][4];
+#pragma unroll 1
+      for (uint32_t w = 0; w < Wm; ++w) {
+        {
+          const uint32_t jlo = 64 * w, cnt = min(64u, n - min(n, jlo));
+          const uint64_t ntmask =
+              ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(st_nt[2 * w + 1]) << 32) |
+              (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(st_nt[2 * w]);
+          uint32_t P[8];
+#pragma unroll
+          for (int g = 0; g < 8; ++g) {
+            P[g] = 0;
+          }
+#pragma unroll
+          for (uint32_t g = 0; g < 8; ++g) {
+            if (8 * g < cnt) {
+              uint32_t lf[8];
+#pragma unroll
+              for (uint32_t kk = 0; kk < 8; ++kk) {
+                lf[kk] = 0xFFFFFFFFu;
+                if (8 * g + kk < cnt) {
+                  lf[kk] = *reinterpret_cast<const uint32_t*>(a.lvl + st_row[jlo + 8 * g + kk] + v0);
+                }
+              }
+              const uint32_t ntg = (uint32_t)(ntmask >> (8 * g)) & 0xFFu;
+#pragma unroll
+              for (uint32_t kk = 0; kk < 8; ++kk) {
+                uint32_t m = live & swar_zero_bytes(lf[kk] ^ tgt);
+                if ((ntg >> kk) & 1u) {
+                  // a drained neighbour is a next hop only to itself
+                  const uint32_t r = st_node[jlo + 8 * g + kk] - v0;
+                  m &= r < 4u ? (0x80u << (8u * r)) : 0u;
+                }
+                P[g] |= m >> (7u - kk);
+              }
+            }
+          }
+          uint32_t lo[4], hi[4];
+          swar_transpose4(P[0], P[1], P[2], P[3], lo);
+          swar_transpose4(P[4], P[5], P[6], P[7], hi);
+#pragma unroll
+          for (uint32_t ww = 0; ww < kNsHeldMax; ++ww) {
+            if (ww == w) { // static register indices
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                held[ww][i] = ((uint64_t)hi[i] << 32) | lo[i];
+              }
+            }
+          }
+        }
+      }
+      // node-major: node v0 + i, word w at (v0 + i) * Wm + w
+      if (v0 + 4 <= a.V) {
+        ulonglong2* o = reinterpret_cast<ulonglong2*>(nhrow + (size_t)v0 * Wm);
+        if (Wm == 1) {
+          o[0] = make_ulonglong2(held[0][0], held[0][1]);
+          o[1] = make_ulonglong2(held[0][2], held[0][3]);
+        } else if (Wm == 2) {
+          o[0] = make_ulonglong2(held[0][0], held[1][0]);
+          o[1] = make_ulonglong2(held[0][1], held[1][1]);
+          o[2] = make_ulonglong2(held[0][2], held[1][2]);
+          o[3] = make_ulonglong2(held[0][3], held[1][3]);
+        } else {
+          o[0] = make_ulonglong2(held[0][0], held[1][0]);
+          o[1] = make_ulonglong2(held[2][0], held[0][1]);
+          o[2] = make_ulonglong2(held[1][1], held[2][1]);
+          o[3] = make_ulonglong2(held[0][2], held[1][2]);
+          o[4] = make_ulonglong2(held[2][2], held[0][3]);
+          o[5] = make_ulonglong2(held[1][3], held[2][3]);
+        }
+      } else {
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {
+          if (v0 + i < a.V) {
+#pragma unroll
+            for (uint32_t w = 0; w < kNsHeldMax; ++w) {
+              if (w < Wm) {
+                nhrow[(size_t)(v0 + i) * Wm + w] = held[w][i];
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(kNsThreads) __attribute__((amdgpu_waves_per_eu(4)))
-void spf_nh_levels_swar_kernel(NhLevelsArgs a) {
+void spf_nh_levels_swar_kernel(NhLevelsArgs a, const uint32_t* big, uint32_t nbig) {
   __shared__ uint32_t st_row[64];
   __shared__ uint32_t st_node[64];
   __shared__ uint32_t st_nt[2]; // non-transit neighbours of the staged word
-  const uint32_t q = blockIdx.x;
+  const bool deep = a.flags[0] != 0; // uniform
+  // sources with more than kNsHeldMax words (or every source of a deep BFS;
+  // the held kernel takes the rest)
+  for (uint32_t bi = blockIdx.x;; bi += gridDim.x) {
+  if (deep ? bi >= a.nq : bi >= nbig) {
+    break;
+  }
+  const uint32_t q = deep ? bi : big[bi];
   const uint32_t s = a.src[q];
   const uint32_t Wm = a.nh_w[q];
   uint64_t* nhrow = a.nh_out + a.nh_off[q];
   const uint32_t beg = a.nbr_off[s], n = a.nbr_off[s + 1] - beg;
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t nchunks = (a.V + kNsChunk - 1) / kNsChunk;
-  const bool deep = a.flags[0] != 0; // uniform
   const uint8_t* lvl_s = a.lvl + (size_t)q * a.Vp8;
   for (uint32_t w = 0; w < Wm; ++w) {
     const uint32_t jlo = w * 64, cnt = min(64u, n - min(n, jlo));
@@ -2590,6 +2782,28 @@ void spf_nh_levels_swar_kernel(NhLevelsArgs a) {
       }
     }
   }
+  __syncthreads(); // the next source restages the neighbour list
+  }
+}
+
+// Sources with at most kNsHeldMax mask words (all of the fabric's), unless the
+// BFS went deeper than 254 levels (then spf_nh_levels_swar_kernel takes all).
+__global__ __launch_bounds__(kNsHeldThreads) void spf_nh_levels_held_kernel(NhLevelsArgs a) {
+  __shared__ uint32_t st_row[kNsHeldMax * 64];
+  __shared__ uint32_t st_node[kNsHeldMax * 64];
+  __shared__ uint32_t st_nt[2 * kNsHeldMax];
+  // consecutive blocks: consecutive sources at the same chunk (neighbouring
+  // name ranks share neighbours, so their row reads meet in L2)
+  const uint32_t c = blockIdx.x / a.nq;
+  const uint32_t q = blockIdx.x - c * a.nq;
+  const uint32_t Wm = a.nh_w[q];
+  if (a.flags[0] != 0 || Wm > kNsHeldMax) {
+    return;
+  }
+  const uint32_t s = a.src[q];
+  const uint32_t beg = a.nbr_off[s], n = a.nbr_off[s + 1] - beg;
+  nl_swar_held(a, q, c, Wm, n, beg, a.nh_out + a.nh_off[q], a.lvl + (size_t)q * a.Vp8, st_row,
+               st_node, st_nt);
 }
 
 // six waves per SIMD (<= 80 VGPRs), as before the chunk-inner word loop
@@ -3995,6 +4209,8 @@ struct spf_query {
   uint64_t* d_nh = nullptr;
   uint64_t* d_key = nullptr; // wide plan settle keys (SPF_F_ORDER)
   uint32_t* d_qctr = nullptr; // dstep source-claim counter
+  uint32_t* d_big = nullptr;  // nh_levels: queries with more than kNsHeldMax mask words
+  uint32_t nbig = 0;
   // k-th path traces (spf_query_trace_paths): device scratch and the last
   // trace's per-query path / link counts
   uint32_t* d_trace = nullptr;
@@ -4182,7 +4398,7 @@ void free_query(spf_query* q) {
         (void*)q->d_lvl, (void*)q->d_flags, (void*)q->d_perm,
         (void*)q->d_slab, (void*)q->d_msd, (void*)q->d_base_of,
         (void*)q->d_skip, (void*)q->d_key, (void*)q->d_qctr, (void*)q->d_scatter,
-        (void*)q->d_trace}) {
+        (void*)q->d_trace, (void*)q->d_big}) {
     pool_free(p);
   }
   if (q->base) {
@@ -5223,6 +5439,18 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       }
     }
   }
+  if (q->dist == DistPlan::MsBfs && q->nh == NhPlan::Levels) {
+    std::vector<uint32_t> big;
+    for (uint32_t i = 0; i < nq; ++i) {
+      if (q->nh_w[i] > kNsHeldMax) {
+        big.push_back(i);
+      }
+    }
+    q->nbig = (uint32_t)big.size();
+    if (!big.empty() && dev_upload_q(&q->d_big, big.data(), big.size()) != SPF_OK) {
+      return bail(fail(SPF_E_NOMEM, "next-hop source list"));
+    }
+  }
   if (q->dist == DistPlan::MsBfs) {
     if (pool_malloc((void**)&q->d_lvl, (size_t)nq * q->Vp8) != hipSuccess ||
         pool_malloc((void**)&q->d_flags, 16) != hipSuccess) {
@@ -5585,6 +5813,7 @@ int launch_msbfs(spf_query* q, bool unit) {
   a.Vp8 = q->Vp8;
   a.nq = q->nq;
   a.scale = unit ? 1u : g->uniform;
+  a.wrec = env_flag("OPENR_MS_WREC", 0); // measured slower (0.212 -> 0.232 ms, profiles/r03g)
   HIP_TRY(hipMemsetAsync(q->d_flags, 0, 16, g->stream));
   const uint32_t K = (g->V + kMsThreads - 1) / kMsThreads;
   const void* kern = nullptr;
@@ -5650,8 +5879,18 @@ int launch_nh_levels(spf_query* q, bool unit) {
     return fail(SPF_E_UNSUPPORTED, "batch too large for the next-hop pass");
   }
   if (env_flag("OPENR_NL_SWAR", 1)) {
-    hipLaunchKernelGGL(spf_nh_levels_swar_kernel, dim3(q->nq), dim3(kNsThreads), 0,
-                       g->stream, a);
+    // held kernel: every source with <= kNsHeldMax mask words; the generic
+    // byte kernel: the rest (q->d_big), or every source after a deep BFS
+    const uint64_t hblocks = (uint64_t)q->nq * ((g->V + kNsChunk - 1) / kNsChunk);
+    if (hblocks > 0x7FFFFFFFull) {
+      return fail(SPF_E_UNSUPPORTED, "batch too large for the next-hop pass");
+    }
+    hipLaunchKernelGGL(spf_nh_levels_held_kernel, dim3((uint32_t)hblocks),
+                       dim3(kNsHeldThreads), 0, g->stream, a);
+    HIP_TRY(hipGetLastError());
+    const uint32_t grid = std::max<uint32_t>(q->nbig, std::min<uint32_t>(q->nq, 1024));
+    hipLaunchKernelGGL(spf_nh_levels_swar_kernel, dim3(grid), dim3(kNsThreads), 0, g->stream,
+                       a, (const uint32_t*)q->d_big, q->nbig);
     HIP_TRY(hipGetLastError());
     return SPF_OK;
   }

@@ -495,13 +495,15 @@ def test_hop_bound_follows_drains(gpu_ready):
     assert not g.needs_exact
 
 
-@pytest.mark.parametrize("sell", ["0", "1"])
-def test_msbfs_sliced_ell_matches_csr(gpu_ready, sell, monkeypatch):
+@pytest.mark.parametrize("sell,wrec", [("0", "1"), ("1", "1"), ("1", "0")])
+def test_msbfs_sliced_ell_matches_csr(gpu_ready, sell, wrec, monkeypatch):
     """MS-BFS over the sliced-ELL copy of the CSR (upload_sell) and over the
-    plain CSR: identical distance and next-hop rows, checked against the
-    literal replay on a few sources (irregular degrees, drained nodes, parallel
-    links, a ragged last slice)."""
+    plain CSR, with wave-cooperative or per-lane row stores: identical
+    distance and next-hop rows, checked against the literal replay on a few
+    sources (irregular degrees, drained nodes, parallel links, a ragged last
+    slice)."""
     monkeypatch.setenv("OPENR_MS_SELL", sell)
+    monkeypatch.setenv("OPENR_MS_WREC", wrec)
     rng = random.Random(77)
     V = 3001
     links = random_links(rng, V, 9000, wmin=1, wmax=1, parallel=0.05)
@@ -515,6 +517,7 @@ def test_msbfs_sliced_ell_matches_csr(gpu_ready, sell, monkeypatch):
     assert q.kernel == "msbfs+levels"
     check_query(csr, q, [int(s) for s in srcs], False, rows={0, 5, 17, 1500, V - 1})
     monkeypatch.setenv("OPENR_MS_SELL", "1" if sell == "0" else "0")
+    monkeypatch.setenv("OPENR_MS_WREC", "1" if wrec == "0" else "0")
     r = g.query(srcs, abi.SPF_F_NEXTHOPS | abi.SPF_F_UNIT_METRIC).run()
     for i in range(0, V, 97):
         assert (q.dist(i) == r.dist(i)).all(), i

@@ -251,3 +251,32 @@ def test_linkstate_batches_fan_out_with_ignore_lists(gpu_ready):
     finally:
         E.set_cluster_min_sources(64)
         E.set_spf_devices([])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["local", "rank"])
+def test_query_table_trace_paths(gpu_ready, mode):
+    """spf_table_trace_paths / spf_table_trace_fetch: the KSP2 second-pass
+    traces of a query table (one source, per-destination ignore lists = the
+    first paths' links) equal the single-device query's traces in table
+    order, overflowed entries included."""
+    csr = _random_csr(1500, 6000, 31, wmax=4)
+    g = abi.Graph(csr)
+    src = 7
+    dsts = np.arange(0, csr.num_nodes, 3, dtype=np.uint32)
+    dsts = dsts[dsts != src]
+    first = g.query(np.full(len(dsts), src, dtype=np.uint32), 0).run().trace_paths(dsts)
+    keep = [i for i, p in enumerate(first) if p]
+    ign = [sorted({l for p in first[i] for l in p}) for i in keep]
+    srcs = np.full(len(keep), src, dtype=np.uint32)
+    d2 = dsts[keep]
+    want = g.query(srcs, 0, ignore=ign).run().trace_paths(d2)
+    c = abi.Cluster([0]) if mode == "local" else abi.Cluster(
+        world=1, rank=0, uid=abi.cluster_unique_id(), device=0)
+    cg = abi.ClusterGraph(c, csr)
+    t = cg.table(srcs, 0, ignore=ign).run()
+    assert t.trace_paths(d2) == want
+    t.close()
+    cg.close()
+    c.close()
+    g.close()

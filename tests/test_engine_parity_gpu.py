@@ -297,3 +297,23 @@ def test_invalidate_drops_every_view(mods):
     ls.invalidate()
     _spf_equal(ls, oa["0"], names[0], True)
     assert E.get_counters().get("decision.spf_runs", 0) == 1
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_ksp2_route_db_device_traces(mods, seed, monkeypatch):
+    """KSP2 RouteDbs with the k = 2 traces on the device
+    (OPENR_KSP2_DEVICE_TRACE=1, spf_query_trace_paths) equal the oracle's,
+    spf_runs included (one counted runSpf per (src, dst, 2) key)."""
+    monkeypatch.setenv("OPENR_KSP2_DEVICE_TRACE", "1")
+    monkeypatch.setenv("OPENR_SPF_TRACE_CAP", "6")  # some traces overflow to the host
+    E, O = mods
+    names, adj_dbs, prefix_dbs = RZ.random_network(700 + seed, n_nodes=30, n_links=80)
+    ea, ep = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    oa, op = RZ.load(O, adj_dbs, prefix_dbs, seed)
+    E.reset_counters()
+    O.reset_counters()
+    es = E.SpfSolver(names[0], True, False)
+    os_ = O.SpfSolver(names[0], True, False)
+    for node in names[:6]:
+        assert es.buildRouteDb(node, ea, ep) == os_.buildRouteDb(node, oa, op), node
+    assert E.get_counters().get("decision.spf_runs") == O.get_counters().get("decision.spf_runs")

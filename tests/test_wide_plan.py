@@ -197,15 +197,19 @@ def _csr_arrays(csr):
     )
 
 
-def test_wan_large_metrics_vs_flat_oracle(gpu_ready):
+@pytest.mark.parametrize("hop_bound", ["1", "0"])
+def test_wan_large_metrics_vs_flat_oracle(gpu_ready, hop_bound, monkeypatch):
     """A 20k-node WAN-like graph with metrics up to 10^6 (maxw * (V-1) >=
     2^32): distance rows and next-hop summaries of sampled sources against
-    the flat CPU restatement (uint64 sums)."""
+    the flat CPU restatement (uint64 sums) -- on the 32-bit plans the
+    transit hop bound admits (maxw * (hop bound + 1) < 2^32), and on the
+    wide plan with the bound disabled."""
     from oracle import build
 
     build.build()
     from oracle import _oracle_ref as O
 
+    monkeypatch.setenv("OPENR_SPF_HOP_BOUND", hop_bound)
     rng = random.Random(41)
     V = 20000
     links = random_links(rng, V, 100000, wmin=1, wmax=1_000_000, parallel=0.01)
@@ -213,10 +217,10 @@ def test_wan_large_metrics_vs_flat_oracle(gpu_ready):
     ov[rng.sample(range(V), 100)] = 1
     csr = abi.Csr.from_links(V, links, overloaded=ov)
     g = abi.Graph(csr)
-    assert g.needs_exact
+    assert g.needs_exact == (hop_bound == "0")
     srcs = np.array(rng.sample(range(V), 24), dtype=np.uint32)
     q = g.query(srcs, abi.SPF_F_NEXTHOPS).run()
-    assert q.kernel == "wide"
+    assert (q.kernel == "wide") == (hop_bound == "0")
     row, col, w, link, ovl = _csr_arrays(csr)
     ref = O.csr_spf_rows(row, col, w, link, ovl, srcs, True, 4)
     for i in range(len(srcs)):

@@ -2793,9 +2793,11 @@ __global__ __launch_bounds__(kNsHeldThreads) void spf_nh_levels_held_kernel(NhLe
   __shared__ uint32_t st_node[kNsHeldMax * 64];
   __shared__ uint32_t st_nt[2 * kNsHeldMax];
   // consecutive blocks: consecutive sources at the same chunk (neighbouring
-  // name ranks share neighbours, so their row reads meet in L2)
-  const uint32_t c = blockIdx.x / a.nq;
-  const uint32_t q = blockIdx.x - c * a.nq;
+  // name ranks share neighbours, so their row reads meet in L2); with
+  // OPENR_NL_XCD=1 consecutive logical blocks also share an XCD
+  const uint32_t bid = a.xcd_swizzle ? xcd_logical_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint32_t c = bid / a.nq;
+  const uint32_t q = bid - c * a.nq;
   const uint32_t Wm = a.nh_w[q];
   if (a.flags[0] != 0 || Wm > kNsHeldMax) {
     return;
@@ -4120,6 +4122,30 @@ __global__ __launch_bounds__(64) void spf_trace_pack_kernel(TracePackArgs a) {
   }
 }
 
+struct PatchArgs {
+  const uint32_t* pk;   // (index, value) pairs per u32 array, then (index, lo, hi)
+  uint32_t* dst32[4];
+  uint32_t n32[4];
+  uint32_t off32[4];
+  uint64_t* dst64;
+  uint32_t n64;
+  uint32_t off64;
+};
+
+// scatter of a metric patch's words (spf_graph_patch_metrics, sparse path)
+__global__ void spf_patch_words_kernel(PatchArgs a) {
+  for (int k = 0; k < 4; ++k) {
+    for (uint32_t i = threadIdx.x; i < a.n32[k]; i += blockDim.x) {
+      const uint32_t* p = a.pk + a.off32[k] + 2 * i;
+      a.dst32[k][p[0]] = p[1];
+    }
+  }
+  for (uint32_t i = threadIdx.x; i < a.n64; i += blockDim.x) {
+    const uint32_t* p = a.pk + a.off64 + 3 * i;
+    a.dst64[p[0]] = ((uint64_t)p[2] << 32) | p[1];
+  }
+}
+
 __global__ void fill_u32_kernel(uint32_t* p, size_t n, uint32_t v) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -4174,6 +4200,7 @@ enum class NhPlan { None, Inline, Rows, Levels };
 struct spf_query {
   spf_graph* g = nullptr;
   uint32_t nq = 0, flags = 0;
+  uint32_t nrows = 0; // distance / level rows computed: nq + MS-BFS helper sources
   DistPlan dist = DistPlan::SsspLds;
   NhPlan nh = NhPlan::None;
   int wmax = 0;
@@ -4654,6 +4681,128 @@ int upload_sell(spf_graph* g) {
   return s;
 }
 
+// A few metrics changed (adjacency churn, LinkState.cpp:621-660): patch the
+// host mirrors and scatter only the device words those edges feed — w64[e],
+// wout[e], win[rev[e]], the cheapest-link metric of e's neighbour slot and
+// the packed edge word — instead of upload_weights' full recompute and
+// upload (26 ms per event on the WAN-100k, bench table_repair).  The graph
+// scalars (maxw, mean metric, uniformity, exactness) come from one parallel
+// scan of w64.  SPF_E_UNSUPPORTED (nothing changed) when the patch would
+// change the set of metric-0 edges, the wrap flag or the packed-edge layout:
+// the caller then runs upload_weights.
+int patch_weights_sparse(spf_graph* g, uint32_t n, const uint32_t* edge_idx, const uint64_t* m) {
+  const uint32_t E = g->E;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t o = g->w64[edge_idx[i]], w = m[i];
+    if ((o == 0) != (w == 0) || (o > 0x7FFFFFFFull) != (w > 0x7FFFFFFFull)) {
+      return SPF_E_UNSUPPORTED; // zero-edge list / wrap flag change
+    }
+    if (g->cw_bits && w >= (1ull << (32 - g->cw_bits))) {
+      return SPF_E_UNSUPPORTED; // no longer packable
+    }
+  }
+  HIP_TRY(hipStreamSynchronize(g->stream)); // queued kernels read the old words
+  for (uint32_t i = 0; i < n; ++i) {
+    g->w64[edge_idx[i]] = m[i];
+  }
+  // scalars: one parallel scan (maxw / sum / uniformity)
+  const unsigned nth = openr::hostThreads(E, 1u << 16);
+  const size_t chunk = (E + nth - 1) / std::max(1u, nth);
+  std::vector<uint64_t> wmax(nth, 0), wsum(nth, 0);
+  std::vector<uint8_t> same(nth, 1);
+  const uint64_t c0 = E ? g->w64[0] : 0;
+  openr::parallelFor(nth, nth, [&](size_t t, unsigned) {
+    const size_t lo = t * chunk, hi = std::min<size_t>(E, lo + chunk);
+    uint64_t mx = 0, sm = 0;
+    bool eq = true;
+    for (size_t e = lo; e < hi; ++e) {
+      const uint64_t w = g->w64[e];
+      mx = std::max(mx, w);
+      sm += w <= 0x7FFFFFFFull ? w : 0;
+      eq = eq && w == c0;
+    }
+    wmax[t] = mx;
+    wsum[t] = sm;
+    same[t] = eq;
+  }, 1);
+  uint64_t maxw = 0, sumw = 0;
+  bool uni = true;
+  for (unsigned t = 0; t < nth; ++t) {
+    maxw = std::max(maxw, wmax[t]);
+    sumw += wsum[t];
+    uni = uni && same[t];
+  }
+  g->maxw = maxw;
+  refresh_exact(g);
+  g->wide_delta = E ? std::max<uint64_t>(1, sumw / E) : 1;
+  g->uniform = (!g->exact && E && uni) ? (uint32_t)c0 : 0;
+  // the device words (u32 index, u32 lo, u32 hi) per array, one upload
+  std::vector<uint32_t> pk;
+  uint32_t counts[5] = {0, 0, 0, 0, 0};
+  std::vector<uint32_t> lists[5];
+  std::vector<uint64_t> vals64;
+  std::vector<uint32_t> idx64;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t e = edge_idx[i];
+    const uint64_t w = g->w64[e];
+    const uint32_t w32 = (uint32_t)std::min<uint64_t>(w, 0xFFFFFFFFull);
+    idx64.push_back(e);
+    vals64.push_back(w);
+    lists[0].push_back(e);
+    lists[0].push_back(w32); // wout[e]
+    lists[1].push_back(g->rev[e]);
+    lists[1].push_back(w32); // win[rev[e]]
+    // cheapest usable link to the neighbour of slot[e] (parallel links)
+    uint32_t u = (uint32_t)(std::upper_bound(g->row.begin(), g->row.end(), e) - g->row.begin()) - 1;
+    uint32_t best = 0xFFFFFFFFu;
+    for (uint32_t f = g->row[u]; f < g->row[u + 1]; ++f) {
+      if (g->slot[f] == g->slot[e]) {
+        best = std::min<uint32_t>(best, (uint32_t)std::min<uint64_t>(g->w64[f], 0xFFFFFFFFull));
+      }
+    }
+    const uint32_t ns = g->nbr_off[u] + g->slot[e];
+    g->nbr_w[ns] = best;
+    lists[2].push_back(ns);
+    lists[2].push_back(best);
+    if (g->cw_bits) {
+      lists[3].push_back(e);
+      lists[3].push_back(g->col[e] | (w32 << g->cw_bits));
+    }
+  }
+  PatchArgs a{};
+  uint32_t* arrays[4] = {g->d_wout, g->d_win, g->d_nbr_w, g->d_cw};
+  size_t off = 0;
+  for (int k = 0; k < 4; ++k) {
+    counts[k] = (uint32_t)(lists[k].size() / 2);
+    a.dst32[k] = arrays[k];
+    a.n32[k] = arrays[k] ? counts[k] : 0;
+    a.off32[k] = (uint32_t)off;
+    pk.insert(pk.end(), lists[k].begin(), lists[k].end());
+    off = pk.size();
+  }
+  const size_t o64 = pk.size();
+  for (uint32_t i = 0; i < n; ++i) {
+    pk.push_back(idx64[i]);
+    pk.push_back((uint32_t)vals64[i]);
+    pk.push_back((uint32_t)(vals64[i] >> 32));
+  }
+  a.dst64 = g->d_w64;
+  a.n64 = n;
+  a.off64 = (uint32_t)o64;
+  uint32_t* d = nullptr;
+  HIP_TRY(pool_malloc((void**)&d, pk.size() * 4));
+  HIP_TRY(hipMemcpyAsync(d, pk.data(), pk.size() * 4, hipMemcpyHostToDevice, g->stream));
+  a.pk = d;
+  hipLaunchKernelGGL(spf_patch_words_kernel, dim3(1), dim3(256), 0, g->stream, a);
+  const hipError_t le = hipGetLastError();
+  const hipError_t se = hipStreamSynchronize(g->stream); // pk is host memory too
+  pool_free(d);
+  HIP_TRY(le);
+  HIP_TRY(se);
+  g->ecc_est = 0; // dstep tuning re-estimates the eccentricity
+  return SPF_OK;
+}
+
 inline size_t lds_ctl_bytes(const spf_graph* g, uint32_t ign_cap) {
   return (3 * (size_t)g->nbw + kCtlWords + ign_cap) * sizeof(uint32_t);
 }
@@ -5132,10 +5281,16 @@ int spf_graph_patch_metrics(
       return fail(SPF_E_INVALID, "edge index out of range");
     }
   }
+  HIP_TRY(hipSetDevice(g->device));
+  if (n && (uint64_t)n * 64 <= g->E && env_flag("OPENR_SPF_PATCH_INPLACE", 1)) {
+    const int st = patch_weights_sparse(g, n, edge_idx, m);
+    if (st != SPF_E_UNSUPPORTED) {
+      return st;
+    }
+  }
   for (uint32_t i = 0; i < n; ++i) {
     g->w64[edge_idx[i]] = m[i];
   }
-  HIP_TRY(hipSetDevice(g->device));
   HIP_TRY(hipStreamSynchronize(g->stream));
   return upload_weights(g);
 }
@@ -5244,6 +5399,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
 
   // ---- plan: which kernels compute this batch
   std::vector<int32_t> row_of;
+  std::vector<uint32_t> helpers; // MS-BFS helper sources (rows nq, nq+1, ...)
   std::vector<uint32_t> msd_perm;
   // metrics that wrap (negative i32 as uint64): the literal DijkstraQ
   // replay; metric 0 / sums past 32 bits / a settle order: the wide plan
@@ -5269,6 +5425,35 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
           break;
         }
       }
+    }
+    // an MS-BFS batch whose sources' neighbours lie outside it (one rank's
+    // block of a sharded all-sources table): the missing neighbours ride
+    // along as helper sources — their level rows are computed after the
+    // batch's own rows and serve only the next-hop pass — instead of the
+    // batch dropping to per-source SSSP (fabric block of 1,247 sources:
+    // 1.93 ms on the lds plan, profiles/r03j)
+    const bool msbfs_candidate = !rows_ok && uniform && !literal && nq >= 32 &&
+                                 V <= kMsThreads * kMsMaxK &&
+                                 2 * (size_t)V * 4 <= kLdsLimit &&
+                                 !(getenv("OPENR_SPF_MSBFS") && atoi(getenv("OPENR_SPF_MSBFS")) == 0) &&
+                                 env_flag("OPENR_SPF_MSBFS_HELPERS", 1);
+    if (msbfs_candidate) {
+      // no bound on the helper count: it is < V, and one MS-BFS pass over
+      // the batch and all its helpers still beats per-source SSSP on the
+      // batch alone (a 64-source workgroup costs about one source's SSSP)
+      std::vector<uint32_t> extra;
+      for (uint32_t i = 0; i < nq; ++i) {
+        const uint32_t s = desc->sources[i];
+        for (uint32_t k = g->nbr_off[s]; k < g->nbr_off[s + 1]; ++k) {
+          const uint32_t f = g->nbrs[k];
+          if (row_of[f] < 0) {
+            row_of[f] = (int32_t)(nq + extra.size());
+            extra.push_back(f);
+          }
+        }
+      }
+      rows_ok = true;
+      helpers = std::move(extra);
     }
     if (!rows_ok) {
       row_of.clear();
@@ -5374,7 +5559,8 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       q->dist = DistPlan::MsBfs;
       q->ms_bits = width;
       q->lds_bytes = 2 * (size_t)V * (width / 8); // frontier double buffer
-      const uint32_t nbatch = (nq + width - 1) / width;
+      const uint32_t nrows = nq + (uint32_t)helpers.size();
+      const uint32_t nbatch = (nrows + width - 1) / width;
       const uint32_t per_cu = (uint32_t)std::max<size_t>(
           1, std::min<size_t>(2048 / kMsThreads, kLdsLimit / std::max<size_t>(q->lds_bytes, 1)));
       q->grid = std::min<uint32_t>(nbatch, (uint32_t)g->num_cus * per_cu);
@@ -5383,6 +5569,10 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       }
     }
   }
+  if (!helpers.empty() && !(q->dist == DistPlan::MsBfs && q->nh == NhPlan::Levels)) {
+    return bail(fail(SPF_E_INVALID, "internal: helper sources outside the MS-BFS plan"));
+  }
+  q->nrows = nq + (uint32_t)helpers.size();
 
   if (hipSetDevice(g->device) != hipSuccess) {
     return bail(fail(SPF_E_DEVICE, "hipSetDevice failed"));
@@ -5400,7 +5590,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       return o;
     };
     const uint32_t total_ign = has_ign ? desc->ignore_offsets[nq] : 0;
-    const size_t o_src = seg((size_t)nq * 4);
+    const size_t o_src = seg((size_t)q->nrows * 4);
     const size_t o_ioff = has_ign ? seg((size_t)(nq + 1) * 4) : 0;
     const size_t o_ign = has_ign ? seg((size_t)total_ign * 4) : 0;
     const size_t o_nhoff = want_nh ? seg((size_t)nq * 8) : 0;
@@ -5409,6 +5599,9 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     if (off) {
       std::vector<uint8_t> host(off, 0);
       std::memcpy(host.data() + o_src, desc->sources, (size_t)nq * 4);
+      if (!helpers.empty()) {
+        std::memcpy(host.data() + o_src + (size_t)nq * 4, helpers.data(), helpers.size() * 4);
+      }
       if (has_ign) {
         std::memcpy(host.data() + o_ioff, desc->ignore_offsets, (size_t)(nq + 1) * 4);
         std::memcpy(host.data() + o_ign, desc->ignore_links, (size_t)total_ign * 4);
@@ -5452,7 +5645,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     }
   }
   if (q->dist == DistPlan::MsBfs) {
-    if (pool_malloc((void**)&q->d_lvl, (size_t)nq * q->Vp8) != hipSuccess ||
+    if (pool_malloc((void**)&q->d_lvl, (size_t)q->nrows * q->Vp8) != hipSuccess ||
         pool_malloc((void**)&q->d_flags, 16) != hipSuccess) {
       return bail(fail(SPF_E_NOMEM, "level rows"));
     }
@@ -5465,7 +5658,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
   }
   const bool ex = q->dist == DistPlan::Exact;
   const bool wide = q->dist == DistPlan::Wide;
-  const size_t dist_bytes = (ex || wide) ? (size_t)nq * V * 8 : (size_t)nq * q->Vp * 4;
+  const size_t dist_bytes = (ex || wide) ? (size_t)nq * V * 8 : (size_t)q->nrows * q->Vp * 4;
   if (dist_bytes && pool_malloc(&q->d_dist, dist_bytes) != hipSuccess) {
     return bail(fail(SPF_E_NOMEM, "distance rows"));
   }
@@ -5811,7 +6004,7 @@ int launch_msbfs(spf_query* q, bool unit) {
   a.V = g->V;
   a.Vp = q->Vp;
   a.Vp8 = q->Vp8;
-  a.nq = q->nq;
+  a.nq = q->nrows; // the batch + its helper sources
   a.scale = unit ? 1u : g->uniform;
   a.wrec = env_flag("OPENR_MS_WREC", 0); // measured slower (0.212 -> 0.232 ms, profiles/r03g)
   HIP_TRY(hipMemsetAsync(q->d_flags, 0, 16, g->stream));
@@ -5982,9 +6175,15 @@ int launch_wide(spf_query* q) {
 
 // Event between the distance kernel and the next-hop kernel of a two-stage
 // plan, so spf_query_stage_ms can split the device time per kernel.
+// A what-if baseline (q->base) runs through run_plan alone, without
+// spf_query_run's per-run events: nothing to mark then.
 int mark_stage(spf_query* q) {
+  hipEvent_t h = q->hist[q->runs % spf_query::kHist][1];
+  if (!h) {
+    return SPF_OK;
+  }
   HIP_TRY(hipEventRecord(q->evm, q->g->stream));
-  HIP_TRY(hipEventRecord(q->hist[q->runs % spf_query::kHist][1], q->g->stream));
+  HIP_TRY(hipEventRecord(h, q->g->stream));
   q->two_stage = true;
   return SPF_OK;
 }

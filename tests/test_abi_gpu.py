@@ -562,3 +562,83 @@ def test_nh_levels_swar_matches_scalar(gpu_ready, case, monkeypatch):
         pytest.fail(f"mask word {bad} differs: {ma[bad]:#x} vs {mb[bad]:#x}")
     probe = [0, 7, 8, V - 1, V // 2] if case != "deep" else [0, 99, 650, 699]
     check_query(csr, a, [int(s) for s in srcs], False, rows=set(probe))
+
+
+@pytest.mark.parametrize("case", ["weighted", "uniform", "large"])
+def test_sparse_metric_patch_equals_fresh_graph(gpu_ready, case, monkeypatch):
+    """spf_graph_patch_metrics' sparse path (a few edges: only their device
+    words are scattered, scalars rescanned) gives the same rows and masks as
+    a graph created from the patched CSR, and as the full re-upload
+    (OPENR_SPF_PATCH_INPLACE=0): weighted / uniform-metric (the patch breaks
+    and then restores uniformity, i.e. the MS-BFS plan) / delta-stepping
+    graphs, parallel links (cheapest-neighbour metric), drained nodes."""
+    rng = random.Random({"weighted": 51, "uniform": 52, "large": 53}[case])
+    V = {"weighted": 400, "uniform": 2000, "large": 40000}[case]
+    wmax = 1 if case == "uniform" else 30
+    links = random_links(rng, V, 4 * V, wmin=1, wmax=wmax, parallel=0.05)
+    ov = np.zeros(V, dtype=np.uint8)
+    ov[rng.sample(range(V), V // 50)] = 1
+    csr = abi.Csr.from_links(V, links, overloaded=ov)
+    srcs = [0, 1, V // 2, V - 1] if case != "uniform" else list(range(64))
+    flags = abi.SPF_F_NEXTHOPS
+    for inplace in ("1", "0"):
+        monkeypatch.setenv("OPENR_SPF_PATCH_INPLACE", inplace)
+        g = abi.Graph(csr)
+        metric = csr.metric.copy()
+        for step in range(3):
+            E = len(metric)
+            k = 6
+            e = np.array(rng.sample(range(E), k), dtype=np.uint32)
+            if case == "uniform" and step == 2:
+                m = np.ones(k, dtype=np.uint64)  # restore: uniform again below
+                e = np.flatnonzero(metric != 1).astype(np.uint32)[:64]
+                m = np.ones(len(e), dtype=np.uint64)
+            else:
+                m = np.array([rng.randint(1, 40) for _ in range(k)], dtype=np.uint64)
+            g.patch_metrics(e, m)
+            metric[e] = m
+            fresh_csr = abi.Csr(csr.num_nodes, csr.row_ptr, csr.col, metric.copy(), csr.link_id,
+                                csr.rev, csr.overloaded, csr.num_links)
+            f = abi.Graph(fresh_csr)
+            assert g.needs_exact == f.needs_exact
+            a = g.query(srcs, flags).run()
+            b = f.query(srcs, flags).run()
+            assert a.kernel == b.kernel, (step, a.kernel, b.kernel)
+            for i in range(len(srcs)):
+                assert (a.dist(i) == b.dist(i)).all(), (inplace, step, i)
+                assert (a.nexthops(i) == b.nexthops(i)).all(), (inplace, step, i)
+            check_query(fresh_csr, a, srcs, True, rows={0, len(srcs) - 1} if V > 1000 else None)
+            a.close()
+            b.close()
+            f.close()
+        g.close()
+
+
+@pytest.mark.parametrize("block", [(0, 700), (1300, 1900), (2900, 3001)])
+def test_msbfs_block_with_helper_sources(gpu_ready, block):
+    """One rank's block of an all-sources table (sources whose neighbours lie
+    outside the block): the MS-BFS plan computes the missing neighbours' level
+    rows as helper sources, so the block keeps msbfs+levels, and its rows and
+    masks equal the full batch's rows for the same sources."""
+    rng = random.Random(91)
+    V = 3001
+    links = random_links(rng, V, 9000, wmin=1, wmax=1, parallel=0.03)
+    ov = np.zeros(V, dtype=np.uint8)
+    ov[rng.sample(range(V), 40)] = 1
+    csr = abi.Csr.from_links(V, links, overloaded=ov)
+    g = abi.Graph(csr)
+    flags = abi.SPF_F_NEXTHOPS | abi.SPF_F_UNIT_METRIC
+    full = g.query(np.arange(V, dtype=np.uint32), flags).run()
+    lo, hi = block
+    srcs = np.arange(lo, hi, dtype=np.uint32)
+    q = g.query(srcs, flags).run()
+    assert q.kernel == "msbfs+levels"
+    n = hi - lo
+    got = np.empty((n, V), dtype=np.uint32)
+    want = np.empty((n, V), dtype=np.uint32)
+    q.fetch_rows(0, n, got.ctypes.data, V * 4, on_device=False)
+    full.fetch_rows(lo, n, want.ctypes.data, V * 4, on_device=False)
+    assert (got == want).all()
+    for i in range(0, n, 37):
+        assert (q.nexthops(i) == full.nexthops(lo + i)).all(), i
+    check_query(csr, q, [int(s) for s in srcs], False, rows={0, n - 1})

@@ -1554,6 +1554,12 @@ def fabric_single(args, topo, world, rank, local, dist):
 
 def main():
     args = parse()
+    # everything but the final JSON line goes to stderr: RCCL's init banner
+    # ("RCCL version : ...") and any library chatter write to fd 1 directly,
+    # and the contract is ONE JSON line on rank 0's stdout
+    json_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     import numpy as np
     import torch
 
@@ -1642,8 +1648,9 @@ def main():
             except Exception as e:
                 out["cpu_baseline"]["ksp2_full"] = {"error": repr(e)}
         out["cpu_baseline"]["cpu_model"] = host_cpu_model()
+    sys.stdout.flush()
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist:
         dist.destroy_process_group()
 

@@ -96,15 +96,37 @@ int spf_device_count(void);
 const char* spf_error_string(int status);
 const char* spf_last_error_detail(void); /* thread-local text of last error */
 
+/* ---- device memory (tables a host driver owns, e.g. AllSourcesTable) ---- */
+#define SPF_COPY_D2H 0
+#define SPF_COPY_H2D 1
+#define SPF_COPY_D2D 2
+int spf_device_alloc(int device, size_t bytes, void** out);
+int spf_device_free(int device, void* p);
+/* synchronous copy on `device` (SPF_COPY_*) */
+int spf_device_memcpy(int device, void* dst, const void* src, size_t bytes, int kind);
+
 /* ---- graph ---- */
 int spf_graph_create(const spf_graph_desc* desc, spf_graph** out);
 int spf_graph_destroy(spf_graph* g);
 /* Replace the per-node transit bits (overload/drain) in place: node
  * overload toggles are the common churn (DecisionBenchmark.cpp:600-626). */
 int spf_graph_set_transit(spf_graph* g, const uint8_t* node_overloaded);
-/* Patch metrics of existing half-edges in place (metric churn, a7 deltas). */
+/* Patch metrics of existing half-edges in place (metric churn, a7 deltas).
+ * A few edges (n * 64 <= E): only their device words are rewritten. */
 int spf_graph_patch_metrics(
     spf_graph* g, uint32_t n, const uint32_t* edge_idx, const uint64_t* metric);
+/* Take half-edges down (up[i] = 0) or bring them back up (1) with the given
+ * metrics, in place: link removal / re-addition (LinkState.cpp:421-434
+ * removeLink / addLink; the reference drops its whole memo, :712-715) without
+ * a new device graph.  A down half-edge stays at its CSR position as a
+ * self-loop of its tail (never relaxed, never tight).  Distance queries
+ * only: a graph changed this way refuses SPF_F_NEXTHOPS / SPF_F_ORDER
+ * (SPF_E_UNSUPPORTED; its distinct-neighbour lists still hold the old
+ * heads) — rebuild it for those.  SPF_E_UNSUPPORTED too for 64-bit graphs,
+ * metric 0, or metrics the packed edge words cannot hold. */
+int spf_graph_set_edges(
+    spf_graph* g, uint32_t n, const uint32_t* edge_idx, const uint8_t* up,
+    const uint64_t* metric);
 /* Work of this graph is enqueued on `stream` (a hipStream_t, NULL = the
  * graph's own stream). */
 int spf_graph_set_stream(spf_graph* g, void* stream);

@@ -31,10 +31,14 @@ EXPORTED_SYMBOLS = (
     "spf_device_count",
     "spf_error_string",
     "spf_last_error_detail",
+    "spf_device_alloc",
+    "spf_device_free",
+    "spf_device_memcpy",
     "spf_graph_create",
     "spf_graph_destroy",
     "spf_graph_set_transit",
     "spf_graph_patch_metrics",
+    "spf_graph_set_edges",
     "spf_graph_set_stream",
     "spf_graph_get_stream",
     "spf_graph_needs_exact",
@@ -222,9 +226,13 @@ def load():
         "spf_error_string": (C.c_char_p, [C.c_int]),
         "spf_last_error_detail": (C.c_char_p, []),
         "spf_graph_create": (C.c_int, [C.POINTER(_GraphDesc), C.POINTER(vp)]),
+        "spf_device_alloc": (C.c_int, [C.c_int, C.c_size_t, C.POINTER(vp)]),
+        "spf_device_free": (C.c_int, [C.c_int, vp]),
+        "spf_device_memcpy": (C.c_int, [C.c_int, vp, vp, C.c_size_t, C.c_int]),
         "spf_graph_destroy": (C.c_int, [vp]),
         "spf_graph_set_transit": (C.c_int, [vp, C.POINTER(C.c_uint8)]),
         "spf_graph_patch_metrics": (C.c_int, [vp, u32, pu32, pu64]),
+        "spf_graph_set_edges": (C.c_int, [vp, u32, pu32, C.POINTER(C.c_uint8), pu64]),
         "spf_graph_set_stream": (C.c_int, [vp, vp]),
         "spf_graph_get_stream": (vp, [vp]),
         "spf_graph_needs_exact": (C.c_int, [vp]),
@@ -412,6 +420,14 @@ class Graph:
     def set_transit(self, overloaded):
         ov = np.ascontiguousarray(overloaded, dtype=np.uint8)
         _check(load().spf_graph_set_transit(self.h, _p(ov, C.c_uint8)), "transit")
+
+    def set_edges(self, edges, up, metrics):
+        """Half-edges down (up=0) / back up (1) in place (spf_graph_set_edges)."""
+        e = np.ascontiguousarray(edges, dtype=np.uint32)
+        u = np.ascontiguousarray(up, dtype=np.uint8)
+        m = np.ascontiguousarray(metrics, dtype=np.uint64)
+        _check(load().spf_graph_set_edges(self.h, len(e), _p(e, C.c_uint32), _p(u, C.c_uint8),
+                                          _p(m, C.c_uint64)), "set_edges")
 
     def patch_metrics(self, edges, metrics):
         """Metrics of existing half-edges, in place (spf_graph_patch_metrics)."""

@@ -253,6 +253,7 @@ class ShardedAllSources:
         self.first, self.count = shard(self.n, self.world, self.rank)
         self.cap = shard_cap(self.n, self.world)
         self.graph = abi.Graph(csr, device=self.device)
+        self._layout(csr)
         if self.graph.needs_exact:
             raise abi.SpfError("all-sources tables need 32-bit sums (no metric 0 / 64-bit metrics)")
         self.stream = torch.cuda.Stream(device=self.device)
@@ -345,6 +346,55 @@ class ShardedAllSources:
             out.fetch_ms = ev0.elapsed_time(ev1)
         return out
 
+    def _layout(self, csr):
+        """Half-edge layout of the resident device graph: heads as created,
+        which half-edges are up, their current metrics (spf_graph_set_edges
+        keeps down half-edges in place)."""
+        import numpy as np
+
+        self._lay_row = np.asarray(csr.row_ptr, dtype=np.int64)
+        self._lay_col = np.asarray(csr.col, dtype=np.uint32).copy()
+        self._lay_up = np.ones(len(csr.col), dtype=bool)
+        self._lay_w = np.asarray(csr.metric, dtype=np.uint64).copy()
+
+    def _links_in_place(self, deltas):
+        """Map link-set deltas (spf_graph_diff: REMOVED / ADDED half-edges
+        (tail, head, metric), multiset per tail) onto the resident layout:
+        a removed half-edge is an up slot (tail, head, metric) going down, an
+        added one a down slot (tail, head) coming back up with its metric.
+        None when some added half-edge has no down slot (a new link: rebuild)
+        or a metric is 0 / past 2^31 - 1 (64-bit graphs rebuild too)."""
+        import numpy as np
+
+        from openr_amd import abi
+
+        SCOPE_NOT_TAIL = 2
+        up = self._lay_up.copy()
+        w = self._lay_w.copy()
+        touched = {}
+        order = sorted((d for d in deltas if int(d["scope"]) != SCOPE_NOT_TAIL),
+                       key=lambda d: int(d["kind"]) != abi.SPF_DELTA_REMOVED)
+        for d in order:
+            u, v, m, kind = int(d["tail"]), int(d["head"]), int(d["metric"]), int(d["kind"])
+            if m == 0 or m > 0x7FFFFFFF:
+                return None
+            lo, hi = int(self._lay_row[u]), int(self._lay_row[u + 1])
+            cols = self._lay_col[lo:hi]
+            if kind == abi.SPF_DELTA_REMOVED:
+                cand = np.nonzero((cols == v) & up[lo:hi] & (w[lo:hi] == np.uint64(m)))[0]
+            else:
+                cand = np.nonzero((cols == v) & ~up[lo:hi])[0]
+            if len(cand) == 0:
+                return None
+            e = lo + int(cand[0])
+            up[e] = kind != abi.SPF_DELTA_REMOVED
+            if kind != abi.SPF_DELTA_REMOVED:
+                w[e] = m
+            touched[e] = None
+        self._lay_up, self._lay_w = up, w
+        e = np.fromiter(touched.keys(), dtype=np.uint32, count=len(touched))
+        return e, up[e].astype(np.uint8), w[e]
+
     def update(self, new_csr) -> RepairRun:
         """Repair the table after a topology change instead of recomputing
         every source (the reference clears its whole SPF
@@ -393,7 +443,15 @@ class ShardedAllSources:
             and np.array_equal(old.link_id, new_csr.link_id)
             and np.array_equal(old.rev, new_csr.rev)
         )
-        if same_links:
+        # the resident graph's layout is the old CSR's unless links were
+        # taken down / up in place before
+        layout_is_old = bool(self._lay_up.all()) and len(self._lay_col) == len(old.col) and \
+            np.array_equal(self._lay_row, old.row_ptr) and np.array_equal(self._lay_col, old.col)
+        inplace = None
+        if (not (same_links and layout_is_old) and not self.nexthops
+                and os.environ.get("OPENR_SPF_LINKS_INPLACE", "1") != "0"):
+            inplace = self._links_in_place(deltas)
+        if same_links and layout_is_old:
             # metric / drain churn: patch the resident device graph in place
             ch = np.nonzero(old.metric != new_csr.metric)[0]
             if len(ch):
@@ -401,12 +459,23 @@ class ShardedAllSources:
             if not np.array_equal(old.overloaded, new_csr.overloaded):
                 self.graph.set_transit(new_csr.overloaded)
             self.graph.csr = new_csr
+            self._lay_w = new_csr.metric.astype(np.uint64).copy()
+            out.graph_patched = True
+        elif inplace is not None:
+            # links down / back up: the half-edges stay at their positions of
+            # the resident graph (spf_graph_set_edges), transit bits as above
+            e, up, w = inplace
+            if len(e):
+                self.graph.set_edges(e, up, w)
+            if not np.array_equal(old.overloaded, new_csr.overloaded):
+                self.graph.set_transit(new_csr.overloaded)
             out.graph_patched = True
         else:
             graph = abi.Graph(new_csr, device=self.device)
             graph.set_stream(self.stream.cuda_stream)
             self.graph.close()
             self.graph = graph
+            self._layout(new_csr)
         self.csr = new_csr
         t2 = time.perf_counter()
         block = self.local_block()

@@ -1,0 +1,377 @@
+// AllSourcesTable.cpp — see AllSourcesTable.h.
+#include "AllSourcesTable.h"
+
+#include <algorithm>
+#include <chrono>
+#include <stdexcept>
+
+#include "Engine.h"
+
+namespace openr {
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+double msSince(Clock::time_point t) {
+  return std::chrono::duration<double, std::milli>(Clock::now() - t).count();
+}
+
+void check(int s, const char* what) {
+  if (s != SPF_OK) {
+    throw std::runtime_error(std::string("MI355X SPF engine failure in ") + what + ": " +
+                             spf_error_string(s) + " (" + spf_last_error_detail() + ")");
+  }
+}
+
+} // namespace
+
+spf_graph_desc AllSourcesTable::Csr::desc(int device) const {
+  spf_graph_desc d{};
+  d.num_nodes = (uint32_t)overloaded.size();
+  d.num_edges = (uint32_t)col.size();
+  d.row_ptr = row.data();
+  d.col = col.data();
+  d.metric = metric.data();
+  d.link_id = linkId.data();
+  d.rev = rev.data();
+  d.node_overloaded = overloaded.data();
+  d.num_links = numLinks;
+  d.device = device;
+  return d;
+}
+
+AllSourcesTable::Csr AllSourcesTable::snapshot(const LinkState& ls) const {
+  LinkState::Engine& eng = ls.engine(); // builds the flat CSR if needed
+  Csr c;
+  c.row = eng.row;
+  c.col = eng.col;
+  c.linkId = eng.linkId;
+  c.rev = eng.rev;
+  c.metric = eng.metric;
+  c.overloaded = eng.overloaded;
+  c.numLinks = (uint32_t)eng.links.size();
+  if (eng.names != names_ && !names_.empty()) {
+    throw std::invalid_argument("AllSourcesTable::update: the node set changed, rebuild the table");
+  }
+  return c;
+}
+
+AllSourcesTable::AllSourcesTable(const LinkState& ls, std::vector<int> devices) {
+  LinkState::Engine& eng = ls.engine();
+  if (eng.exact) {
+    throw std::invalid_argument(
+        "AllSourcesTable: metric 0 / 64-bit sums need 64-bit rows (the exact kernels)");
+  }
+  names_ = eng.names;
+  ids_ = eng.ids;
+  cur_ = snapshot(ls);
+  if (devices.empty()) {
+    devices = getSpfDevices();
+  }
+  if (devices.empty()) {
+    devices = {0};
+  }
+  const uint32_t V = (uint32_t)names_.size();
+  const uint32_t n = (uint32_t)devices.size();
+  // contiguous source blocks (spf_table_layout's split: n / world each, the
+  // first n % world one more)
+  uint32_t first = 0;
+  try {
+    for (uint32_t r = 0; r < n; ++r) {
+      Block b;
+      b.device = devices[r];
+      b.first = first;
+      b.count = V / n + (r < V % n ? 1 : 0);
+      first += b.count;
+      b.sources.resize(b.count);
+      for (uint32_t i = 0; i < b.count; ++i) {
+        b.sources[i] = b.first + i;
+      }
+      if (b.count) {
+        void* p = nullptr;
+        check(spf_device_alloc(b.device, (size_t)b.count * V * 4, &p), "spf_device_alloc");
+        b.rows = static_cast<uint32_t*>(p);
+      }
+      blocks_.push_back(std::move(b));
+    }
+    buildGraphs(cur_);
+    recompute();
+  } catch (...) {
+    for (auto& b : blocks_) {
+      if (b.graph) {
+        spf_graph_destroy(b.graph);
+      }
+      spf_device_free(b.device, b.rows);
+    }
+    throw;
+  }
+}
+
+AllSourcesTable::~AllSourcesTable() {
+  for (auto& b : blocks_) {
+    if (b.graph) {
+      spf_graph_destroy(b.graph);
+    }
+    spf_device_free(b.device, b.rows);
+  }
+}
+
+void AllSourcesTable::buildGraphs(const Csr& c) {
+  for (auto& b : blocks_) {
+    spf_graph* g = nullptr;
+    const spf_graph_desc d = c.desc(b.device);
+    check(spf_graph_create(&d, &g), "spf_graph_create");
+    if (b.graph) {
+      spf_graph_destroy(b.graph);
+    }
+    b.graph = g;
+  }
+  layRow_ = c.row;
+  layCol_ = c.col;
+  layUp_.assign(c.col.size(), 1);
+  layW_ = c.metric;
+}
+
+// rows of `idx` (block-local row indices) recomputed: one batch query; the
+// whole block lands in place (fetch_rows), a subset is scattered
+void AllSourcesTable::computeBlock(Block& b, const std::vector<uint32_t>& idx, bool scatter) {
+  if (idx.empty()) {
+    return;
+  }
+  const uint32_t V = (uint32_t)names_.size();
+  std::vector<uint32_t> srcs(idx.size());
+  for (size_t i = 0; i < idx.size(); ++i) {
+    srcs[i] = b.sources[idx[i]];
+  }
+  spf_query_desc qd{};
+  qd.num_queries = (uint32_t)srcs.size();
+  qd.sources = srcs.data();
+  qd.flags = 0;
+  spf_query* q = nullptr;
+  check(spf_query_create(b.graph, &qd, &q), "spf_query_create");
+  struct Guard {
+    spf_query* q;
+    ~Guard() { spf_query_destroy(q); }
+  } guard{q};
+  check(spf_query_run(q), "spf_query_run");
+  if (scatter) {
+    check(spf_query_scatter_rows(q, idx.data(), b.rows, (size_t)V * 4), "spf_query_scatter_rows");
+  } else {
+    check(spf_query_fetch_rows(q, 0, qd.num_queries, b.rows, (size_t)V * 4, 1),
+          "spf_query_fetch_rows");
+  }
+  check(spf_query_sync(q), "spf_query_sync");
+  float ms = 0;
+  spf_query_elapsed_ms(q, &ms);
+  lastSpfMs_ = std::max(lastSpfMs_, (double)ms);
+}
+
+void AllSourcesTable::recompute() {
+  lastSpfMs_ = 0;
+  for (auto& b : blocks_) {
+    std::vector<uint32_t> all(b.count);
+    for (uint32_t i = 0; i < b.count; ++i) {
+      all[i] = i;
+    }
+    computeBlock(b, all, false);
+  }
+}
+
+// Link-set deltas onto the resident layout (the C++ form of
+// allsources.ShardedAllSources._links_in_place): a REMOVED half-edge
+// (tail, head, metric) is an up slot going down, an ADDED one a down slot
+// (tail, head) coming back up; false when an added half-edge has no down
+// slot (a new link) or a metric is 0 / wraps.
+bool AllSourcesTable::linksInPlace(
+    const std::vector<spf_edge_delta>& deltas, std::vector<uint32_t>& edges,
+    std::vector<uint8_t>& up, std::vector<uint64_t>& w) {
+  std::vector<uint8_t> lu = layUp_;
+  std::vector<uint64_t> lw = layW_;
+  std::vector<uint8_t> touched(layCol_.size(), 0);
+  for (int pass = 0; pass < 2; ++pass) { // REMOVED first (a metric change is both)
+    const uint32_t kind = pass == 0 ? SPF_DELTA_REMOVED : SPF_DELTA_ADDED;
+    for (const auto& d : deltas) {
+      if (d.scope == SPF_SCOPE_NOT_TAIL || d.kind != kind) {
+        continue; // transit flips are set_transit's
+      }
+      if (d.metric == 0 || d.metric > 0x7FFFFFFFull) {
+        return false;
+      }
+      uint32_t hit = ~0u;
+      for (uint32_t e = layRow_[d.tail]; e < layRow_[d.tail + 1]; ++e) {
+        if (layCol_[e] != d.head) {
+          continue;
+        }
+        if (kind == SPF_DELTA_REMOVED ? (lu[e] && lw[e] == d.metric) : !lu[e]) {
+          hit = e;
+          break;
+        }
+      }
+      if (hit == ~0u) {
+        return false;
+      }
+      lu[hit] = kind == SPF_DELTA_ADDED;
+      if (kind == SPF_DELTA_ADDED) {
+        lw[hit] = d.metric;
+      }
+      touched[hit] = 1;
+    }
+  }
+  edges.clear();
+  up.clear();
+  w.clear();
+  for (uint32_t e = 0; e < touched.size(); ++e) {
+    if (touched[e]) {
+      edges.push_back(e);
+      up.push_back(lu[e]);
+      w.push_back(lw[e]);
+    }
+  }
+  layUp_ = std::move(lu);
+  layW_ = std::move(lw);
+  return true;
+}
+
+AllSourcesTable::UpdateStats AllSourcesTable::update(const LinkState& ls) {
+  UpdateStats st;
+  const auto t0 = Clock::now();
+  if (ls.engine().exact) {
+    throw std::invalid_argument("AllSourcesTable::update: the new topology needs 64-bit rows");
+  }
+  Csr nc = snapshot(ls);
+  const uint32_t V = (uint32_t)names_.size();
+  // edge deltas
+  std::vector<spf_edge_delta> deltas;
+  {
+    const spf_graph_desc a = cur_.desc(0), b = nc.desc(0);
+    uint32_t n = 0;
+    check(spf_graph_diff(&a, &b, nullptr, 0, &n), "spf_graph_diff");
+    deltas.resize(n);
+    if (n) {
+      check(spf_graph_diff(&a, &b, deltas.data(), n, &n), "spf_graph_diff");
+    }
+  }
+  st.deltas = (uint32_t)deltas.size();
+  st.diffMs = msSince(t0);
+  // device graphs: in place when the link set is the layout's, or links went
+  // down / came back up; rebuilt for a new link
+  const auto tg = Clock::now();
+  const bool sameLinks = nc.row == cur_.row && nc.col == cur_.col && nc.linkId == cur_.linkId &&
+                         nc.rev == cur_.rev;
+  const bool layoutIsCur = std::all_of(layUp_.begin(), layUp_.end(), [](uint8_t x) { return x; }) &&
+                           layRow_ == cur_.row && layCol_ == cur_.col;
+  const bool transit = nc.overloaded != cur_.overloaded;
+  std::vector<uint32_t> edges;
+  std::vector<uint8_t> up;
+  std::vector<uint64_t> w;
+  if (sameLinks && layoutIsCur) {
+    std::vector<uint32_t> ch;
+    std::vector<uint64_t> cm;
+    for (uint32_t e = 0; e < nc.metric.size(); ++e) {
+      if (nc.metric[e] != cur_.metric[e]) {
+        ch.push_back(e);
+        cm.push_back(nc.metric[e]);
+      }
+    }
+    for (auto& b : blocks_) {
+      if (!ch.empty()) {
+        check(spf_graph_patch_metrics(b.graph, (uint32_t)ch.size(), ch.data(), cm.data()),
+              "spf_graph_patch_metrics");
+      }
+      if (transit) {
+        check(spf_graph_set_transit(b.graph, nc.overloaded.data()), "spf_graph_set_transit");
+      }
+    }
+    layW_ = nc.metric;
+    st.graphPatched = true;
+  } else if (linksInPlace(deltas, edges, up, w)) {
+    for (auto& b : blocks_) {
+      if (!edges.empty()) {
+        check(spf_graph_set_edges(b.graph, (uint32_t)edges.size(), edges.data(), up.data(),
+                                  w.data()),
+              "spf_graph_set_edges");
+      }
+      if (transit) {
+        check(spf_graph_set_transit(b.graph, nc.overloaded.data()), "spf_graph_set_transit");
+      }
+    }
+    st.graphPatched = true;
+  } else {
+    buildGraphs(nc);
+  }
+  cur_ = std::move(nc);
+  st.graphMs = msSince(tg);
+  if (spf_graph_needs_exact(blocks_.front().graph)) {
+    throw std::invalid_argument("AllSourcesTable::update: the new topology needs 64-bit rows");
+  }
+  // screen, then repair (or recompute) the affected rows of each block
+  lastSpfMs_ = 0;
+  bool anyRelaxed = false, anyRecomputed = false;
+  for (auto& b : blocks_) {
+    if (!b.count || deltas.empty()) {
+      continue;
+    }
+    const auto ts = Clock::now();
+    std::vector<uint8_t> hit(b.count, 0);
+    check(spf_table_screen(b.graph, b.rows, V, b.count, b.sources.data(), deltas.data(),
+                           (uint32_t)deltas.size(), hit.data()),
+          "spf_table_screen");
+    st.screenMs += msSince(ts);
+    std::vector<uint32_t> idx, srcs;
+    for (uint32_t i = 0; i < b.count; ++i) {
+      if (hit[i]) {
+        idx.push_back(i);
+        srcs.push_back(b.sources[i]);
+      }
+    }
+    st.affected += (uint32_t)idx.size();
+    if (idx.empty()) {
+      continue;
+    }
+    const auto tr = Clock::now();
+    const int s = spf_table_repair(b.graph, b.rows, V, (uint32_t)idx.size(), srcs.data(),
+                                   idx.data(), deltas.data(), (uint32_t)deltas.size());
+    if (s == SPF_OK) {
+      anyRelaxed = true;
+    } else if (s == SPF_E_UNSUPPORTED) {
+      computeBlock(b, idx, true);
+      anyRecomputed = true;
+    } else {
+      check(s, "spf_table_repair");
+    }
+    st.spfMs += msSince(tr);
+  }
+  st.relaxed = anyRelaxed && !anyRecomputed;
+  st.wallMs = msSince(t0);
+  return st;
+}
+
+std::vector<uint32_t> AllSourcesTable::row(const std::string& src) const {
+  const auto it = ids_.find(src);
+  if (it == ids_.end()) {
+    throw std::out_of_range("AllSourcesTable::row: unknown node " + src);
+  }
+  const uint32_t V = (uint32_t)names_.size();
+  for (const auto& b : blocks_) {
+    if (it->second >= b.first && it->second < b.first + b.count) {
+      std::vector<uint32_t> out(V);
+      check(spf_device_memcpy(b.device, out.data(), b.rows + (size_t)(it->second - b.first) * V,
+                              (size_t)V * 4, SPF_COPY_D2H),
+            "spf_device_memcpy");
+      return out;
+    }
+  }
+  throw std::out_of_range("AllSourcesTable::row: no block holds " + src);
+}
+
+std::optional<uint64_t> AllSourcesTable::distance(const std::string& src,
+                                                  const std::string& dst) const {
+  const auto dit = ids_.find(dst);
+  if (dit == ids_.end()) {
+    return std::nullopt;
+  }
+  const uint32_t d = row(src)[dit->second];
+  return d == 0xFFFFFFFFu ? std::nullopt : std::optional<uint64_t>(d);
+}
+
+} // namespace openr

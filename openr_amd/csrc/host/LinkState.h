@@ -387,6 +387,8 @@ class LinkState {
 
   struct Engine; // device graph + flat memo (Engine.h)
   friend class AllNodesRouteTable; // reads the device graph (RouteTable.h)
+  friend class AllSourcesTable;    // reads the flat CSR (AllSourcesTable.h)
+  friend class AllAreasRouteTable; // checks the graph's row width (RouteTable.h)
 
  private:
   void clearMemo() const;

@@ -20,7 +20,8 @@ namespace {
 } // namespace
 
 AllNodesRouteTable::AllNodesRouteTable(
-    const LinkState& ls, const PrefixState& ps, bool enableV4, bool computeLfa)
+    const LinkState& ls, const PrefixState& ps, bool enableV4, bool computeLfa,
+    const std::unordered_set<std::string>* borderNodes)
     : area_(ls.getArea()), enableV4_(enableV4), lfa_(computeLfa) {
   LinkState::Engine& eng = ls.engine();
   if (eng.exact) {
@@ -37,14 +38,16 @@ AllNodesRouteTable::AllNodesRouteTable(
   // eligible prefixes (Decision.cpp:313-412 restricted to selectEcmpOpenr)
   std::vector<uint32_t> annOff{0}, ann;
   for (const auto& [prefix, entries] : ps.prefixes()) {
-    bool otherArea = false, bgp = false;
+    bool otherArea = false, bgp = false, inArea = false, borderAnn = false;
     for (const auto& [node, byArea] : entries) {
       for (const auto& [area, entry] : byArea) {
         otherArea |= area != area_;
+        inArea |= area == area_;
+        borderAnn |= area == area_ && borderNodes && borderNodes->count(node);
         bgp |= entry.type == thrift::PrefixType::BGP;
       }
     }
-    if (otherArea || bgp || entries.empty()) {
+    if (bgp || entries.empty() || (otherArea && !borderNodes) || !inArea || borderAnn) {
       continue;
     }
     if (prefix.prefixAddress.addr.size() == 4 && !enableV4_) {
@@ -57,10 +60,11 @@ AllNodesRouteTable::AllNodesRouteTable(
     std::vector<Announcer> as;
     for (const auto& [node, byArea] : entries) {
       auto it = ids_.find(node);
-      if (it == ids_.end()) {
-        continue; // not in the graph: never reachable
+      auto ea = byArea.find(area_);
+      if (it == ids_.end() || ea == byArea.end()) {
+        continue; // not in the graph / announced in another area: never reachable
       }
-      as.push_back(Announcer{it->second, byArea.at(area_)});
+      as.push_back(Announcer{it->second, ea->second});
     }
     prefixes_.push_back(prefix);
     announcers_.push_back(std::move(as));
@@ -469,4 +473,100 @@ DecisionRouteUpdate AllNodesRouteTable::delta(const std::string& node) const {
   }
   return u;
 }
+
+AllAreasRouteTable::AllAreasRouteTable(
+    const std::unordered_map<std::string, LinkState>& areas, const PrefixState& ps,
+    bool enableV4, bool computeLfa, bool bgpDryRun, bool bgpUseIgpMetric, bool prefetchAll)
+    : areas_(areas),
+      ps_(ps),
+      enableV4_(enableV4),
+      lfa_(computeLfa),
+      bgpDryRun_(bgpDryRun),
+      bgpIgp_(bgpUseIgpMetric) {
+  // nodes of every area (hasNode, LinkState.h) -> border nodes (>= 2 areas)
+  std::unordered_map<std::string, std::vector<std::string>> areasOf;
+  for (const auto& [area, ls] : areas_) {
+    for (const auto& [node, _] : ls.getAdjacencyDatabases()) {
+      if (ls.hasNode(node)) {
+        areasOf[node].push_back(area);
+      }
+    }
+  }
+  for (const auto& [node, as] : areasOf) {
+    if (as.size() > 1) {
+      border_.insert(node);
+    } else {
+      home_[node] = as.front();
+    }
+  }
+  const bool multi = areas_.size() > 1;
+  for (const auto& [area, ls] : areas_) {
+    if (ls.engine().exact) {
+      continue; // metric 0 / 64-bit sums: this area stays on the host path
+    }
+    auto t = std::make_unique<AllNodesRouteTable>(ls, ps, enableV4, computeLfa,
+                                                  multi ? &border_ : nullptr);
+    auto& served = served_[area];
+    for (const auto& p : t->prefixes()) {
+      served.insert(p);
+    }
+    rest_[area] = served.size() < ps.prefixes().size();
+    tables_[area] = std::move(t);
+    if (prefetchAll) {
+      // the host share then reads resident rows only (one batch per area)
+      std::vector<std::string> all;
+      for (const auto& [node, as] : areasOf) {
+        if (std::find(as.begin(), as.end(), area) != as.end()) {
+          all.push_back(node);
+        }
+      }
+      ls.prefetchSpf(all, true);
+    }
+  }
+}
+
+AllAreasRouteTable::~AllAreasRouteTable() = default;
+
+std::optional<DecisionRouteDb> AllAreasRouteTable::routeDb(const std::string& node) const {
+  lastTable_ = lastHost_ = 0;
+  bool known = false;
+  for (const auto& [_, ls] : areas_) {
+    known |= ls.hasNode(node);
+  }
+  if (!known) {
+    return std::nullopt;
+  }
+  SpfSolver solver(node, enableV4_, lfa_, false, bgpDryRun_, bgpIgp_);
+  const auto h = home_.find(node);
+  const auto t = h == home_.end() ? tables_.end() : tables_.find(h->second);
+  if (t == tables_.end()) {
+    // border node (or an area the kernel does not take): the host path
+    auto db = solver.buildRouteDb(node, areas_, ps_);
+    if (db) {
+      lastHost_ = db->unicastEntries.size() + db->mplsEntries.size();
+    }
+    return db;
+  }
+  const bool single = areas_.size() == 1;
+  DecisionRouteDb db;
+  db.unicastEntries = t->second->routes(node);
+  if (single) {
+    db.mplsEntries = t->second->mplsRoutes(node);
+  }
+  lastTable_ = db.unicastEntries.size() + db.mplsEntries.size();
+  if (!single || rest_.at(h->second)) {
+    auto part = solver.buildRouteDbPartial(node, areas_, ps_, served_.at(h->second), !single);
+    if (part) {
+      lastHost_ = part->unicastEntries.size() + (single ? 0 : part->mplsEntries.size());
+      for (auto& [p, e] : part->unicastEntries) {
+        db.unicastEntries.emplace(p, std::move(e));
+      }
+      if (!single) {
+        db.mplsEntries = std::move(part->mplsEntries);
+      }
+    }
+  }
+  return db;
+}
+
 } // namespace openr

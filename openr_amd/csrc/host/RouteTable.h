@@ -35,6 +35,7 @@
 #include <optional>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "LinkState.h"
@@ -48,8 +49,14 @@ class AllNodesRouteTable {
  public:
   // computeLfa: SpfSolver's computeLfaPaths (loop-free alternates as extra
   // next hops with their own metrics, Decision.cpp:1146-1175)
+  // borderNodes (multi-area, see AllAreasRouteTable): non-null selects the
+  // prefixes this area's table can serve for its interior nodes -- entries
+  // in this area, none of them by a border node; the announcers are the
+  // in-area entries (for an interior node every other area's announcer is
+  // unreachable, Decision.cpp:555-579)
   AllNodesRouteTable(
-      const LinkState& ls, const PrefixState& ps, bool enableV4 = true, bool computeLfa = false);
+      const LinkState& ls, const PrefixState& ps, bool enableV4 = true, bool computeLfa = false,
+      const std::unordered_set<std::string>* borderNodes = nullptr);
   ~AllNodesRouteTable();
   AllNodesRouteTable(const AllNodesRouteTable&) = delete;
   AllNodesRouteTable& operator=(const AllNodesRouteTable&) = delete;
@@ -84,6 +91,8 @@ class AllNodesRouteTable {
   // `older` (which must outlive this call).
   DecisionRouteUpdate delta(const std::string& node) const;
   const std::string& nodeName(uint32_t id) const { return names_.at(id); }
+  // the unicast prefixes the kernel serves (routes() covers exactly these)
+  const std::vector<thrift::IpPrefix>& prefixes() const { return prefixes_; }
 
  private:
   struct Row {
@@ -138,6 +147,46 @@ class AllNodesRouteTable {
   spf_route_table* table_{nullptr};
   float spfMs_{0}, routeMs_{0};
   bool diffed_{false};
+};
+
+// Every node's COMPLETE RouteDb over all areas (SURVEY §8(f) row 1 beyond
+// one area and IGP prefixes): routeDb(node) == SpfSolver::buildRouteDb(node)
+// (Decision.cpp:291-542) for any configuration -- multi-area, BGP,
+// SR-MPLS / KSP2.  Device share: one AllNodesRouteTable per area (all-sources
+// SPF + spf_route_table_kernel) serves the IP / SP_ECMP Open/R prefixes of
+// the area's interior nodes (single area: every node, MPLS node labels
+// included); the host share is SpfSolver::buildRouteDbPartial over the
+// same LinkStates for what the kernel does not restate: border nodes (in two
+// or more areas: cross-area ECMP and drain rules), BGP prefixes (metric-
+// vector best path, Decision.cpp:714-866), SR-MPLS prefixes, prefixes a
+// border node announces, and the multi-area MPLS routes.  With
+// prefetchAll, every area's all-sources SPF views are computed in one
+// device batch up front, so the host share runs no SPF per node.
+class AllAreasRouteTable {
+ public:
+  AllAreasRouteTable(
+      const std::unordered_map<std::string, LinkState>& areas, const PrefixState& ps,
+      bool enableV4 = true, bool computeLfa = false, bool bgpDryRun = false,
+      bool bgpUseIgpMetric = false, bool prefetchAll = true);
+  ~AllAreasRouteTable();
+  // nullopt iff `node` is in no area (Decision.cpp:296-302)
+  std::optional<DecisionRouteDb> routeDb(const std::string& node) const;
+  // routes of the last routeDb() call that came from a device table / the host
+  size_t lastTableRoutes() const { return lastTable_; }
+  size_t lastHostRoutes() const { return lastHost_; }
+  bool isBorder(const std::string& node) const { return border_.count(node) > 0; }
+  size_t numTables() const { return tables_.size(); }
+
+ private:
+  const std::unordered_map<std::string, LinkState>& areas_;
+  const PrefixState& ps_;
+  bool enableV4_, lfa_, bgpDryRun_, bgpIgp_;
+  std::unordered_set<std::string> border_;
+  std::unordered_map<std::string, std::string> home_; // interior node -> its area
+  std::map<std::string, std::unique_ptr<AllNodesRouteTable>> tables_;
+  std::map<std::string, std::unordered_set<thrift::IpPrefix>> served_;
+  std::map<std::string, bool> rest_; // area -> some prefix is left to the host
+  mutable size_t lastTable_{0}, lastHost_{0};
 };
 
 } // namespace openr

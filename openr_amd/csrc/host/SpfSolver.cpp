@@ -242,6 +242,9 @@ inline int64_t nowNs() {
 
 class SpfSolver::SpfSolverImpl {
  public:
+  // buildRouteDbPartial: unicast prefixes to leave out, and whether to skip MPLS
+  const std::unordered_set<thrift::IpPrefix>* skipPrefixes_{nullptr};
+  bool skipMpls_{false};
   SpfSolverImpl(
       const std::string& myNodeName,
       bool enableV4,
@@ -502,6 +505,9 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
   };
   std::vector<PrefixWork> work;
   for (const auto& [prefix, prefixEntries] : prefixState.prefixes()) {
+    if (skipPrefixes_ && skipPrefixes_->count(prefix)) {
+      continue; // served by the caller (AllAreasRouteTable's device table)
+    }
     bool hasBGP = false, hasNonBGP = false, missingMv = false;
     for (const auto& [node, byArea] : prefixEntries) {
       for (const auto& [area, entry] : byArea) {
@@ -601,6 +607,9 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
   // RouteDb like the unicast routes).  The sequential pass applies the
   // collision rule to the rest, computing in place as the reference does.
   const auto tlabel = std::chrono::steady_clock::now();
+  if (skipMpls_) {
+    return routeDb; // unicast only (AllAreasRouteTable brings the MPLS routes)
+  }
   struct LabelItem {
     int32_t label;
     const std::string* area;
@@ -1309,6 +1318,24 @@ std::optional<DecisionRouteUpdate> SpfSolver::processStaticRouteUpdates() {
 }
 
 thrift::StaticRoutes const& SpfSolver::getStaticRoutes() { return impl_->getStaticRoutes(); }
+
+std::optional<DecisionRouteDb> SpfSolver::buildRouteDbPartial(
+    const std::string& myNodeName,
+    std::unordered_map<std::string, LinkState> const& areaLinkStates,
+    PrefixState const& prefixState,
+    const std::unordered_set<thrift::IpPrefix>& skipUnicast,
+    bool withMpls) {
+  impl_->skipPrefixes_ = &skipUnicast;
+  impl_->skipMpls_ = !withMpls;
+  struct Reset {
+    SpfSolverImpl* i;
+    ~Reset() {
+      i->skipPrefixes_ = nullptr;
+      i->skipMpls_ = false;
+    }
+  } reset{impl_.get()};
+  return impl_->buildRouteDb(myNodeName, areaLinkStates, prefixState);
+}
 
 std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
     const std::string& myNodeName,

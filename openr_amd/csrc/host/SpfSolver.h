@@ -130,6 +130,16 @@ class SpfSolver {
       std::unordered_map<std::string, LinkState> const& areaLinkStates,
       PrefixState const& prefixState);
 
+  // buildRouteDb without the unicast prefixes of `skipUnicast` and, with
+  // withMpls = false, without MPLS routes: the host share of a RouteDb whose
+  // other routes come from a device route table (AllAreasRouteTable)
+  std::optional<DecisionRouteDb> buildRouteDbPartial(
+      const std::string& myNodeName,
+      std::unordered_map<std::string, LinkState> const& areaLinkStates,
+      PrefixState const& prefixState,
+      const std::unordered_set<thrift::IpPrefix>& skipUnicast,
+      bool withMpls);
+
   class SpfSolverImpl;
 
  private:

@@ -9,6 +9,7 @@
 #include <chrono>
 #include <pybind11/stl.h>
 
+#include "../host/AllSourcesTable.h"
 #include "../host/LinkState.h"
 #include "../host/PrefixState.h"
 #include "../host/Publication.h"
@@ -331,6 +332,55 @@ PYBIND11_MODULE(_openr_spf, m) {
              return out;
            })
       .def("__len__", [](const AreaMapHolder& am) { return am.map.size(); });
+
+  py::class_<AllAreasRouteTable>(m, "AllAreasRouteTable")
+      .def(py::init([](const AreaMapHolder& areas, const PrefixState& ps, bool enableV4, bool lfa,
+                       bool bgpDryRun, bool bgpUseIgpMetric, bool prefetchAll) {
+             return std::make_unique<AllAreasRouteTable>(areas.map, ps, enableV4, lfa, bgpDryRun,
+                                                         bgpUseIgpMetric, prefetchAll);
+           }),
+           py::arg("areas"), py::arg("prefix_state"), py::arg("enable_v4") = true,
+           py::arg("lfa") = false, py::arg("bgp_dry_run") = false,
+           py::arg("bgp_use_igp_metric") = false, py::arg("prefetch_all") = true,
+           py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
+      .def("route_db", [](const AllAreasRouteTable& t, const std::string& node) -> py::object {
+        auto db = t.routeDb(node);
+        if (!db) {
+          return py::none();
+        }
+        return routeDbToPy(*db);
+      })
+      .def_property_readonly("last_table_routes", &AllAreasRouteTable::lastTableRoutes)
+      .def_property_readonly("last_host_routes", &AllAreasRouteTable::lastHostRoutes)
+      .def_property_readonly("num_tables", &AllAreasRouteTable::numTables)
+      .def("is_border", &AllAreasRouteTable::isBorder);
+
+  py::class_<AllSourcesTable>(m, "AllSourcesTable")
+      .def(py::init([](const AreaMapHolder& areas, const std::string& area, std::vector<int> devices) {
+             return std::make_unique<AllSourcesTable>(areas.map.at(area), devices);
+           }),
+           py::arg("areas"), py::arg("area"), py::arg("devices") = std::vector<int>{})
+      .def_property_readonly("num_nodes", &AllSourcesTable::numNodes)
+      .def_property_readonly("num_devices", &AllSourcesTable::numDevices)
+      .def_property_readonly("node_names", &AllSourcesTable::nodeNames)
+      .def_property_readonly("last_spf_ms", &AllSourcesTable::lastSpfMs)
+      .def("recompute", &AllSourcesTable::recompute)
+      .def("update", [](AllSourcesTable& t, const AreaMapHolder& areas, const std::string& area) {
+        const auto st = t.update(areas.map.at(area));
+        py::dict d;
+        d["deltas"] = st.deltas;
+        d["affected"] = st.affected;
+        d["graph_patched"] = st.graphPatched;
+        d["relaxed"] = st.relaxed;
+        d["diff_ms"] = st.diffMs;
+        d["graph_ms"] = st.graphMs;
+        d["screen_ms"] = st.screenMs;
+        d["spf_ms"] = st.spfMs;
+        d["wall_ms"] = st.wallMs;
+        return d;
+      })
+      .def("row", &AllSourcesTable::row)
+      .def("distance", &AllSourcesTable::distance);
 
   py::class_<AllNodesRouteTable>(m, "AllNodesRouteTable")
       .def(py::init([](const AreaMapHolder& areas, const std::string& area, const PrefixState& ps,

@@ -4122,11 +4122,12 @@ __global__ __launch_bounds__(64) void spf_trace_pack_kernel(TracePackArgs a) {
   }
 }
 
+constexpr int kPatch32 = 6; // wout, win, nbr_w, cw, col, sell (u32 words)
 struct PatchArgs {
   const uint32_t* pk;   // (index, value) pairs per u32 array, then (index, lo, hi)
-  uint32_t* dst32[4];
-  uint32_t n32[4];
-  uint32_t off32[4];
+  uint32_t* dst32[kPatch32];
+  uint32_t n32[kPatch32];
+  uint32_t off32[kPatch32];
   uint64_t* dst64;
   uint32_t n64;
   uint32_t off64;
@@ -4134,7 +4135,7 @@ struct PatchArgs {
 
 // scatter of a metric patch's words (spf_graph_patch_metrics, sparse path)
 __global__ void spf_patch_words_kernel(PatchArgs a) {
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < kPatch32; ++k) {
     for (uint32_t i = threadIdx.x; i < a.n32[k]; i += blockDim.x) {
       const uint32_t* p = a.pk + a.off32[k] + 2 * i;
       a.dst32[k][p[0]] = p[1];
@@ -4191,6 +4192,13 @@ struct spf_graph {
   // sliced-ELL CSR for the MS-BFS pull (MsBfsArgs::sell4), V <= 16 Ki only
   uint4* d_sell = nullptr;
   uint32_t* d_sell_off = nullptr;
+  std::vector<uint32_t> sell_off; // host copy (spf_graph_set_edges patches entries)
+  // spf_graph_set_edges: half-edges taken down in place are self-loops of
+  // their tail (col_orig keeps the head); next-hop queries are refused on
+  // such a graph (the distinct-neighbour lists still hold the old heads)
+  std::vector<uint32_t> col_orig;
+  std::vector<uint8_t> edge_up;
+  bool links_patched = false;
 };
 
 // How a batch is computed.
@@ -4674,6 +4682,7 @@ int upload_sell(spf_graph* g) {
       }
     }
   }
+  g->sell_off = off;
   int s = dev_upload(&g->d_sell_off, off.data(), off.size());
   if (s == SPF_OK && !sell.empty()) {
     s = dev_upload((uint32_t**)&g->d_sell, sell.data(), sell.size());
@@ -4772,6 +4781,10 @@ int patch_weights_sparse(spf_graph* g, uint32_t n, const uint32_t* edge_idx, con
   PatchArgs a{};
   uint32_t* arrays[4] = {g->d_wout, g->d_win, g->d_nbr_w, g->d_cw};
   size_t off = 0;
+  for (int k = 4; k < kPatch32; ++k) {
+    a.dst32[k] = nullptr;
+    a.n32[k] = 0;
+  }
   for (int k = 0; k < 4; ++k) {
     counts[k] = (uint32_t)(lists[k].size() / 2);
     a.dst32[k] = arrays[k];
@@ -5240,6 +5253,48 @@ int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
   return SPF_OK;
 }
 
+int spf_device_alloc(int device, size_t bytes, void** out) {
+  SPF_ABI_RANGE("spf_device_alloc");
+  if (!out) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  *out = nullptr;
+  if (device < 0 || device >= spf_device_count()) {
+    return fail(SPF_E_INVALID, "bad device ordinal");
+  }
+  HIP_TRY(hipSetDevice(device));
+  if (bytes && hipMalloc(out, bytes) != hipSuccess) {
+    *out = nullptr;
+    return fail(SPF_E_NOMEM, "device table");
+  }
+  return SPF_OK;
+}
+
+int spf_device_free(int device, void* p) {
+  SPF_ABI_RANGE("spf_device_free");
+  if (p) {
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipFree(p));
+  }
+  return SPF_OK;
+}
+
+int spf_device_memcpy(int device, void* dst, const void* src, size_t bytes, int kind) {
+  SPF_ABI_RANGE("spf_device_memcpy");
+  if (bytes && (!dst || !src)) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  if (!bytes) {
+    return SPF_OK;
+  }
+  HIP_TRY(hipSetDevice(device));
+  const hipMemcpyKind k = kind == SPF_COPY_D2H   ? hipMemcpyDeviceToHost
+                          : kind == SPF_COPY_H2D ? hipMemcpyHostToDevice
+                                                 : hipMemcpyDeviceToDevice;
+  HIP_TRY(hipMemcpy(dst, src, bytes, k));
+  return SPF_OK;
+}
+
 int spf_graph_destroy(spf_graph* g) {
   SPF_ABI_RANGE("spf_graph_destroy");
   free_graph(g);
@@ -5293,6 +5348,103 @@ int spf_graph_patch_metrics(
   }
   HIP_TRY(hipStreamSynchronize(g->stream));
   return upload_weights(g);
+}
+
+int spf_graph_set_edges(
+    spf_graph* g, uint32_t n, const uint32_t* edge_idx, const uint8_t* up,
+    const uint64_t* metric) {
+  SPF_ABI_RANGE("spf_graph_set_edges");
+  if (!g || (n && (!edge_idx || !up || !metric))) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  if (g->exact || g->wrap || g->n_zero) {
+    return fail(SPF_E_UNSUPPORTED, "in-place link changes need 32-bit rows and no metric 0");
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    if (edge_idx[i] >= g->E) {
+      return fail(SPF_E_INVALID, "edge index out of range");
+    }
+    if (metric[i] == 0 || metric[i] > 0x7FFFFFFFull ||
+        (g->cw_bits && metric[i] >= (1ull << (32 - g->cw_bits)))) {
+      return fail(SPF_E_UNSUPPORTED, "metric outside the in-place range (0, wrap or unpackable)");
+    }
+  }
+  if (g->col_orig.empty()) {
+    g->col_orig = g->col;
+    g->edge_up.assign(g->E, 1);
+  }
+  HIP_TRY(hipSetDevice(g->device));
+  HIP_TRY(hipStreamSynchronize(g->stream)); // queued kernels read the old words
+  std::vector<uint32_t> lists[kPatch32];
+  std::vector<uint32_t> w64l;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t e = edge_idx[i];
+    const uint32_t u =
+        (uint32_t)(std::upper_bound(g->row.begin(), g->row.end(), e) - g->row.begin()) - 1;
+    g->edge_up[e] = up[i] ? 1 : 0;
+    // a down half-edge is a self-loop of its tail with a positive metric:
+    // d[u] + w > d[u], so it never relaxes, is never tight, and the pull
+    // reads u's own frontier bits (a subset of its visited bits)
+    g->col[e] = up[i] ? g->col_orig[e] : u;
+    g->w64[e] = metric[i];
+    const uint32_t w32 = (uint32_t)metric[i];
+    lists[0].insert(lists[0].end(), {e, w32});           // wout[e]
+    lists[1].insert(lists[1].end(), {g->rev[e], w32});   // win[rev[e]]
+    if (g->cw_bits) {
+      lists[3].insert(lists[3].end(), {e, g->col[e] | (w32 << g->cw_bits)});
+    }
+    lists[4].insert(lists[4].end(), {e, g->col[e]});
+    if (g->d_sell) {
+      const uint32_t j = e - g->row[u], c = u >> 6, L = u & 63u;
+      const uint32_t idx = ((g->sell_off[c] + j / 4) * 64 + L) * 4 + (j & 3);
+      lists[5].insert(lists[5].end(), {idx, g->col[e]});
+    }
+    w64l.insert(w64l.end(), {e, (uint32_t)metric[i], (uint32_t)(metric[i] >> 32)});
+  }
+  // graph scalars: maxw / mean / uniformity and the 32-bit row bound (the
+  // transit hop bound reads the patched heads)
+  uint64_t maxw = 0, sumw = 0;
+  bool uni = true;
+  const uint64_t c0 = g->E ? g->w64[0] : 0;
+  for (uint32_t e = 0; e < g->E; ++e) {
+    maxw = std::max(maxw, g->w64[e]);
+    sumw += g->w64[e];
+    uni = uni && g->w64[e] == c0;
+  }
+  g->maxw = maxw;
+  refresh_exact(g);
+  g->wide_delta = g->E ? std::max<uint64_t>(1, sumw / g->E) : 1;
+  g->uniform = (!g->exact && g->E && uni) ? (uint32_t)c0 : 0;
+  g->ecc_est = 0;
+  g->links_patched = true;
+  PatchArgs a{};
+  uint32_t* arrays[kPatch32] = {g->d_wout, g->d_win, g->d_nbr_w, g->d_cw, g->d_col,
+                                reinterpret_cast<uint32_t*>(g->d_sell)};
+  std::vector<uint32_t> pk;
+  for (int k = 0; k < kPatch32; ++k) {
+    a.dst32[k] = arrays[k];
+    a.n32[k] = arrays[k] ? (uint32_t)(lists[k].size() / 2) : 0;
+    a.off32[k] = (uint32_t)pk.size();
+    pk.insert(pk.end(), lists[k].begin(), lists[k].end());
+  }
+  a.dst64 = g->d_w64;
+  a.n64 = n;
+  a.off64 = (uint32_t)pk.size();
+  pk.insert(pk.end(), w64l.begin(), w64l.end());
+  if (pk.empty()) {
+    return SPF_OK;
+  }
+  uint32_t* d = nullptr;
+  HIP_TRY(pool_malloc((void**)&d, pk.size() * 4));
+  HIP_TRY(hipMemcpyAsync(d, pk.data(), pk.size() * 4, hipMemcpyHostToDevice, g->stream));
+  a.pk = d;
+  hipLaunchKernelGGL(spf_patch_words_kernel, dim3(1), dim3(256), 0, g->stream, a);
+  const hipError_t le = hipGetLastError();
+  const hipError_t se = hipStreamSynchronize(g->stream);
+  pool_free(d);
+  HIP_TRY(le);
+  HIP_TRY(se);
+  return SPF_OK;
 }
 
 int spf_graph_set_stream(spf_graph* g, void* stream) {
@@ -5378,6 +5530,11 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
   const bool unit = desc->flags & SPF_F_UNIT_METRIC;
   const bool want_nh = desc->flags & SPF_F_NEXTHOPS;
   const bool want_order = desc->flags & SPF_F_ORDER;
+  if ((want_nh || want_order) && g->links_patched) {
+    return bail(fail(SPF_E_UNSUPPORTED,
+                     "next hops / settle order on a graph whose links were set in place "
+                     "(spf_graph_set_edges): rebuild the graph"));
+  }
 
   // next-hop mask geometry
   uint32_t maxw = 0;

@@ -1,0 +1,87 @@
+"""AllSourcesTable (csrc/host/AllSourcesTable.{h,cpp}): the C++ driver that
+keeps every source's distance row of an area resident in HBM under
+adjacency churn — spf_graph_diff, in-place graph
+patches (transit bits, metrics, links down / back up via
+spf_graph_set_edges; a new link rebuilds), spf_table_screen, then
+spf_table_repair or recompute.  After every churn step every row equals the
+oracle's runSpf metrics (oracle/ref_decision.cpp, LinkState.cpp:806-880)."""
+
+import copy
+import random
+
+import pytest
+
+from openr_amd import thrift as T
+from tests import randomized as RZ
+
+pytestmark = pytest.mark.gpu
+
+UNREACH = 0xFFFFFFFF
+
+
+@pytest.fixture(scope="module")
+def mods(gpu_ready):
+    from oracle import _oracle_ref
+    import openr_amd._openr_spf as E
+
+    return E, _oracle_ref
+
+
+def _check_rows(E, O, t, ea, oa):
+    names = list(t.node_names)
+    for src in names:
+        ref = oa["0"].getSpfResult(src, True)
+        row = t.row(src)
+        for j, dst in enumerate(names):
+            want = ref[dst][0] if dst in ref else UNREACH
+            assert row[j] == want, (src, dst, row[j], want)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_all_sources_table_under_churn(mods, seed):
+    E, O = mods
+    names, adj_dbs, prefix_dbs = RZ.random_network(
+        3100 + seed, n_nodes=40, n_links=100, overload_prob=0.05, link_overload_prob=0.03)
+    # every node keeps an adjacency db (the node set must not change)
+    have = {d.thisNodeName for d in adj_dbs["0"]}
+    for n in names:
+        if n not in have:
+            adj_dbs["0"].append(T.createAdjDb(n, [], 0, False, "0"))
+    ea, _ = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    oa, _ = RZ.load(O, adj_dbs, prefix_dbs, seed)
+    t = E.AllSourcesTable(ea, "0")
+    _check_rows(E, O, t, ea, oa)
+    rng = random.Random(seed)
+    dbs = {d.thisNodeName: copy.deepcopy(d) for d in adj_dbs["0"]}
+    kinds = {"patched": 0, "rebuilt": 0, "affected": 0}
+    for step in range(16):
+        db = rng.choice([d for d in dbs.values() if d.adjacencies] or list(dbs.values()))
+        r = rng.random()
+        if r < 0.25 or not db.adjacencies:
+            db.isOverloaded = not db.isOverloaded
+        elif r < 0.5:
+            rng.choice(db.adjacencies).metric = rng.randint(1, 20)
+        elif r < 0.85:
+            adj = rng.choice(db.adjacencies)  # link down / back up (flap)
+            adj.isOverloaded = not adj.isOverloaded
+        else:
+            # a brand-new link between two nodes (both sides advertise it)
+            a, b = rng.sample(sorted(dbs), 2)
+            k = 1000 + step
+            dbs[a].adjacencies.append(T.createAdjacency(
+                b, f"new_{a}_{k}", f"new_{b}_{k}", f"fe80::1:{k:x}", "10.9.9.1", rng.randint(1, 20), 0))
+            dbs[b].adjacencies.append(T.createAdjacency(
+                a, f"new_{b}_{k}", f"new_{a}_{k}", f"fe80::2:{k:x}", "10.9.9.2", rng.randint(1, 20), 0))
+            ea["0"].updateAdjacencyDatabase(dbs[a])
+            oa["0"].updateAdjacencyDatabase(dbs[a])
+            db = dbs[b]
+        ea["0"].updateAdjacencyDatabase(db)
+        oa["0"].updateAdjacencyDatabase(db)
+        st = t.update(ea, "0")
+        kinds["patched" if st["graph_patched"] else "rebuilt"] += 1
+        kinds["affected"] += st["affected"]
+        _check_rows(E, O, t, ea, oa)
+    assert kinds["patched"] > 0
+    # a full recompute on the patched graphs gives the same rows
+    t.recompute()
+    _check_rows(E, O, t, ea, oa)

@@ -327,3 +327,33 @@ def test_route_table_lfa_fabric_and_delta(E, O):
         mu, md = t1.delta_mpls(node)
         want_u = {k: v for k, v in after["mpls"].items() if before[node]["mpls"].get(k) != v}
         assert (mu, sorted(md)) == (want_u, sorted(k for k in before[node]["mpls"] if k not in after["mpls"])), node
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,areas,bgp", [(0, ("0",), True), (1, ("A", "B"), False),
+                                             (2, ("A", "B"), True), (3, ("A", "B", "C"), True)])
+def test_all_areas_route_table_equals_oracle(gpu_ready, seed, areas, bgp):
+    """AllAreasRouteTable: every node's complete RouteDb (multi-area, BGP
+    metric-vector prefixes, SR-MPLS / KSP2 prefixes, MPLS routes) equals the
+    oracle's buildRouteDb; interior nodes take their IP / SP_ECMP routes from
+    the per-area device tables, border nodes and the other prefixes from the
+    host path."""
+    from oracle import _oracle_ref as O
+    import openr_amd._openr_spf as E
+    from tests import randomized as RZ
+
+    names, adj_dbs, prefix_dbs = RZ.random_network(
+        4100 + seed, n_nodes=28, n_links=70, areas=areas, bgp=bgp)
+    ea, ep = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    oa, op = RZ.load(O, adj_dbs, prefix_dbs, seed)
+    for lfa in (False, True):
+        t = E.AllAreasRouteTable(ea, ep, True, lfa)
+        table_routes = 0
+        for node in names:
+            os_ = O.SpfSolver(node, True, lfa)
+            want = os_.buildRouteDb(node, oa, op)
+            got = t.route_db(node)
+            assert got == want, (node, lfa, t.is_border(node))
+            table_routes += t.last_table_routes
+        if any(not t.is_border(n) for n in names):
+            assert table_routes > 0  # the device tables served the interior nodes

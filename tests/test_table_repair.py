@@ -450,3 +450,62 @@ def test_repaired_table_next_hops(gpu_ready, V, L, wmax):
         assert "nexthops_ms" in rep.extra
         check(csr, kinds)
     sas.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("V,L,wmax", [(2500, 9000, 30), (2500, 9000, 1), (40000, 160000, 1000)])
+def test_link_flaps_patched_in_place(gpu_ready, V, L, wmax, monkeypatch):
+    """Link down / back up (and parallel-link churn) on a distance table keep
+    the resident device graph: the half-edges stay in place as self-loops
+    (spf_graph_set_edges) and the repaired table equals a full recompute and
+    the CPU oracle after every event -- flaps, metric changes on the patched
+    layout, drains, a brand-new link (that one rebuilds the graph), and the
+    same sequence with the in-place path disabled."""
+    import torch
+
+    for inplace in ("1", "0"):
+        monkeypatch.setenv("OPENR_SPF_LINKS_INPLACE", inplace)
+        rng = random.Random(V + L + wmax)
+        links = _random_links(V, L, rng, wmax=wmax)
+        ov = np.zeros(V, dtype=np.uint8)
+        csr = abi.Csr.from_links(V, links, ov)
+        srcs = np.asarray(sorted(rng.sample(range(V), min(V, 600))), dtype=np.uint32)
+        torch.cuda.set_device(0)
+        sas = AS.ShardedAllSources(csr, sources=srcs)
+        sas.run()
+        gone = []
+        steps = ["down", "down", "up", "metric", "drain", "up", "new", "down", "metric"]
+        for kind in steps:
+            if kind == "down":
+                i = rng.randrange(len(links))
+                gone.append((i, links.pop(i)))
+            elif kind == "up":
+                links.insert(*gone.pop())
+            elif kind == "metric":
+                i = rng.randrange(len(links))
+                u, v, a, b = links[i]
+                links[i] = (u, v, a + 1 + rng.randrange(wmax), b)
+            elif kind == "drain":
+                ov[rng.randrange(V)] ^= 1
+            elif kind == "new":
+                while True:
+                    u, v = rng.randrange(V), rng.randrange(V)
+                    if u != v:
+                        break
+                links.append((u, v, rng.randint(1, wmax), rng.randint(1, wmax)))
+            csr = abi.Csr.from_links(V, links, ov)
+            rep = sas.update(csr)
+            if inplace == "1" and kind in ("down", "up", "metric", "drain"):
+                assert rep.graph_patched, kind
+            if kind == "new":
+                assert not rep.graph_patched
+            got = sas.table.cpu().numpy().view(np.uint32)[: len(srcs)]
+            pick = np.asarray(sorted(rng.sample(range(len(srcs)), 32)))
+            assert (got[pick] == _oracle_rows(csr, srcs[pick])).all(), (inplace, kind)
+            if V <= 3000:
+                assert (got == _full_table(csr, srcs)).all(), (inplace, kind)
+        sas.run()  # a full pass over the patched layout
+        got = sas.table.cpu().numpy().view(np.uint32)[: len(srcs)]
+        pick = np.asarray(sorted(rng.sample(range(len(srcs)), 32)))
+        assert (got[pick] == _oracle_rows(csr, srcs[pick])).all()
+        sas.close()

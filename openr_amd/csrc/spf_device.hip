@@ -1805,7 +1805,8 @@ __global__ __launch_bounds__(kNhThreads) void spf_nh_rows_kernel(NhRowsArgs a) {
 #define OPENR_MS_UNROLL8 1
 #endif
 constexpr uint32_t kMsThreads = 1024;
-constexpr uint32_t kMsMaxK = 16; // nodes per thread -> V <= 16384
+constexpr uint32_t kMsMaxK = 20; // nodes per thread -> V <= 20480 (32-bit batches above 10,240 nodes: the
+                                 // double buffer is 2 * V * 4 B <= 160 KB of LDS)
 
 struct MsBfsArgs {
   const uint32_t* row;
@@ -6187,8 +6188,10 @@ int launch_msbfs(spf_query* q, bool unit) {
       MS_PICK(uint32_t, 8);
     } else if (K <= 12) {
       MS_PICK(uint32_t, 12);
-    } else {
+    } else if (K <= 16) {
       MS_PICK(uint32_t, 16);
+    } else {
+      MS_PICK(uint32_t, 20);
     }
   }
 #undef MS_PICK

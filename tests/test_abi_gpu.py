@@ -642,3 +642,21 @@ def test_msbfs_block_with_helper_sources(gpu_ready, block):
     for i in range(0, n, 37):
         assert (q.nexthops(i) == full.nexthops(lo + i)).all(), i
     check_query(csr, q, [int(s) for s in srcs], False, rows={0, n - 1})
+
+
+def test_msbfs_20k_nodes_32bit_batches(gpu_ready):
+    """Past 16 Ki nodes (fabric(20000): 20,000 nodes) the MS-BFS plan runs
+    32-source batches with 20 nodes per thread (the 2 * V * 4-byte frontier
+    double buffer still fits 160 KB of LDS): rows and masks against the
+    literal replay on sampled sources."""
+    rng = random.Random(2020)
+    V = 20000
+    links = random_links(rng, V, 60000, wmin=1, wmax=1, parallel=0.0)
+    ov = np.zeros(V, dtype=np.uint8)
+    ov[rng.sample(range(V), 200)] = 1
+    csr = abi.Csr.from_links(V, links, overloaded=ov)
+    g = abi.Graph(csr)
+    srcs = np.arange(0, V, 97, dtype=np.uint32)[:96]
+    q = g.query(srcs, abi.SPF_F_NEXTHOPS | abi.SPF_F_UNIT_METRIC).run()
+    assert q.kernel == "msbfs+levels"
+    check_query(csr, q, [int(s) for s in srcs], False, rows={0, 50, 95})

@@ -179,6 +179,30 @@ def host_cpu_model():
     return platform.processor() or "unknown"
 
 
+class _Heartbeat:
+    """Writes one stderr line a minute while a long host baseline runs, so a
+    supervisor watching the output does not take the run for hung."""
+
+    def __init__(self, what, every=60.0):
+        import threading
+
+        self.what, self.every, self.stop = what, every, threading.Event()
+        self.t0 = time.perf_counter()
+        self.thread = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        while not self.stop.wait(self.every):
+            print(f"[bench] {self.what}: {time.perf_counter() - self.t0:.0f} s", file=sys.stderr, flush=True)
+
+    def __enter__(self):
+        self.thread.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.thread.join()
+
+
 def _ksp2_worker(args):
     """One host process of the full config-4 line A: the oracle's LinkState
     for the fabric, then getKthPaths(2-0-0, d, 1) and (…, 2) for its share
@@ -212,7 +236,7 @@ def ksp2_cpu_full(topo, num_sws):
     cores = host_cores()
     names = sorted(n for n in topo.names if n != "2-0-0")
     chunks = [names[i::cores] for i in range(cores)]
-    with mp.get_context("spawn").Pool(cores) as pool:
+    with _Heartbeat("config-4 line A (all destinations)"), mp.get_context("spawn").Pool(cores) as pool:
         res = pool.map(_ksp2_worker, [(num_sws, c) for c in chunks])
     wall = max(r[0] for r in res)
     return {"build_s": round(wall, 2), "destinations": len(names), "paths": sum(r[1] for r in res),
@@ -329,7 +353,7 @@ def cpu_baseline_all_cores(topo, num_sws, per_core_s=12.0, t_per_spf=None, full=
     pick = names if full else names[::step][: per * cores]
     chunks = [pick[i::cores] for i in range(cores)]
     ctx = mp.get_context("spawn")
-    with ctx.Pool(cores) as pool:
+    with _Heartbeat("reference-style runSpf on all cores"), ctx.Pool(cores) as pool:
         res = pool.map(_oracle_spf_worker, [(num_sws, c) for c in chunks])
     wall = max(r[0] for r in res)
     nspf = sum(r[2] for r in res)

@@ -1829,6 +1829,10 @@ struct MsBfsArgs {
   uint32_t nq;
   uint32_t scale;
   uint32_t wrec; // 1: wave-cooperative row stores (ms_record_wave)
+  // zero-metric plan: (tail, head) pairs of the metric-0 half-edges this
+  // pass closes over at every level (ms_zero_close); nz = 0 elsewhere
+  const uint32_t* zlist;
+  uint32_t nz;
 };
 
 // Write each (source, node) distance the moment its bit appears (one store
@@ -1883,6 +1887,39 @@ __device__ __forceinline__ void ms_record_wave(
   }
 }
 
+// Metric-0 closure of one level (zero-metric plan): the head y
+// of a metric-0 half-edge x -> y reaches, at the SAME level, every source
+// whose bit x publishes at this level (fr = the level's published frontier:
+// transit nodes' new bits, or the sources' own bits at level 0).  The zero
+// links are node-disjoint, so one pass closes the level: y's gained bits
+// could only flow back to x, which already holds them.  Run by y's owner
+// lane (its visited mask lives in that lane's registers).
+template <typename MT, uint32_t KMAX>
+__device__ __forceinline__ void ms_zero_close(
+    const MsBfsArgs& a, uint32_t q0, MT* fr, MT (&vis)[KMAX], uint32_t trm, uint32_t level) {
+  for (uint32_t i = 0; i < a.nz; ++i) {
+    const uint32_t x = a.zlist[2 * i], y = a.zlist[2 * i + 1];
+    if ((y & (kMsThreads - 1)) != threadIdx.x) {
+      continue;
+    }
+    const uint32_t ky = y / kMsThreads;
+    const MT fx = fr[x];
+#pragma unroll
+    for (uint32_t k = 0; k < KMAX; ++k) {
+      if (k == ky) { // static register index
+        const MT gain = fx & ~vis[k];
+        if (gain) {
+          vis[k] |= gain;
+          if ((trm >> k) & 1u) {
+            fr[y] |= gain;
+          }
+          ms_record<MT>(a, q0, y, gain, level);
+        }
+      }
+    }
+  }
+}
+
 template <typename MT, uint32_t KMAX, bool SELL>
 __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
   extern __shared__ __align__(16) unsigned char ms_smem[];
@@ -1927,6 +1964,10 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
       } else if (k < K && v < V && vis[k]) {
         ms_record<MT>(a, q0, v, vis[k], 0);
       }
+    }
+    if (a.nz) {
+      ms_zero_close<MT, KMAX>(a, q0, cur, vis, trm, 0);
+      __syncthreads();
     }
     uint32_t level = 0;
     for (;;) {
@@ -2000,6 +2041,10 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
       if (!more) {
         break;
       }
+      if (a.nz) {
+        ms_zero_close<MT, KMAX>(a, q0, nxt, vis, trm, L);
+        __syncthreads();
+      }
       MT* t = cur;
       cur = nxt;
       nxt = t;
@@ -2063,6 +2108,12 @@ struct NhLevelsArgs {
   uint32_t scale;
   uint32_t xcd_swizzle; // 1: XCD-aware block order (OPENR_NL_XCD; default off: 0.69 -> 0.92 ms on the fabric, profiles/r03b)
   uint32_t held_words;  // 1: 2/3-word masks stored node-major from registers (OPENR_NL_HELD)
+  // zero-metric plan: source q reads its own and its neighbours' rows from
+  // variant table zvar[q] (lvl + zvar[q] * lvl_vstride, dist + zvar[q] *
+  // dist_vstride); nullptr: one table
+  const uint8_t* zvar;
+  uint64_t lvl_vstride;
+  uint64_t dist_vstride;
 };
 
 constexpr uint32_t kNlThreads = 256;
@@ -2501,19 +2552,20 @@ __device__ __forceinline__ void swar_transpose4(
 // the generic branch (a BFS deeper than 254 levels): 32-bit rows, one node
 // at a time; out of line so its registers do not weigh on the byte path
 __device__ __noinline__ void nl_swar_deep(
-    const NhLevelsArgs& a, uint32_t q, uint32_t v0, uint32_t w, uint32_t Wm, uint32_t cnt,
-    uint64_t ntmask, const uint32_t* st_row, const uint32_t* st_node, uint64_t* nhrow) {
+    const NhLevelsArgs& a, const uint32_t* dist, uint32_t q, uint32_t v0, uint32_t w, uint32_t Wm,
+    uint32_t cnt, uint64_t ntmask, const uint32_t* st_row, const uint32_t* st_node,
+    uint64_t* nhrow) {
   for (uint32_t i = 0; i < kNsNodes; ++i) {
     const uint32_t v = v0 + i;
     if (v >= a.V) {
       break;
     }
     uint64_t acc = 0;
-    const uint32_t ds = a.dist[(size_t)q * a.Vp + v];
+    const uint32_t ds = dist[(size_t)q * a.Vp + v];
     if (ds != kInf32 && ds != 0) {
       for (uint32_t j = 0; j < cnt; ++j) {
         // st_row holds level-row byte offsets (row * Vp8)
-        const uint32_t df = a.dist[(size_t)(st_row[j] / a.Vp8) * a.Vp + v];
+        const uint32_t df = dist[(size_t)(st_row[j] / a.Vp8) * a.Vp + v];
         const bool tr = !((ntmask >> j) & 1u) || st_node[j] == v;
         if (df != kInf32 && (uint64_t)df + a.scale == (uint64_t)ds && tr) {
           acc |= 1ull << j;
@@ -2536,8 +2588,9 @@ constexpr uint32_t kNsHeldMax = 3;
 constexpr uint32_t kNsHeldThreads = 256; // one block per (source, 1024-node chunk)
 
 __device__ __forceinline__ void nl_swar_held(
-    const NhLevelsArgs& a, uint32_t q, uint32_t c, uint32_t Wm, uint32_t n, uint32_t beg,
-    uint64_t* nhrow, const uint8_t* lvl_s, uint32_t* st_row, uint32_t* st_node, uint32_t* st_nt) {
+    const NhLevelsArgs& a, const uint8_t* lvl, uint32_t q, uint32_t c, uint32_t Wm, uint32_t n,
+    uint32_t beg, uint64_t* nhrow, const uint8_t* lvl_s, uint32_t* st_row, uint32_t* st_node,
+    uint32_t* st_nt) {
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   for (uint32_t t = threadIdx.x; t < 64 * kNsHeldMax; t += kNsHeldThreads) {
     bool nt = false;
@@ -2585,7 +2638,7 @@ __device__ __forceinline__ void nl_swar_held(
               for (uint32_t kk = 0; kk < 8; ++kk) {
                 lf[kk] = 0xFFFFFFFFu;
                 if (8 * g + kk < cnt) {
-                  lf[kk] = *reinterpret_cast<const uint32_t*>(a.lvl + st_row[jlo + 8 * g + kk] + v0);
+                  lf[kk] = *reinterpret_cast<const uint32_t*>(lvl + st_row[jlo + 8 * g + kk] + v0);
                 }
               }
               const uint32_t ntg = (uint32_t)(ntmask >> (8 * g)) & 0xFFu;
@@ -2670,7 +2723,10 @@ void spf_nh_levels_swar_kernel(NhLevelsArgs a, const uint32_t* big, uint32_t nbi
   const uint32_t beg = a.nbr_off[s], n = a.nbr_off[s + 1] - beg;
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t nchunks = (a.V + kNsChunk - 1) / kNsChunk;
-  const uint8_t* lvl_s = a.lvl + (size_t)q * a.Vp8;
+  const uint32_t zv = a.zvar ? a.zvar[q] : 0u;
+  const uint8_t* lvl = a.lvl + zv * a.lvl_vstride;
+  const uint32_t* dist = a.dist + zv * a.dist_vstride;
+  const uint8_t* lvl_s = lvl + (size_t)q * a.Vp8;
   for (uint32_t w = 0; w < Wm; ++w) {
     const uint32_t jlo = w * 64, cnt = min(64u, n - min(n, jlo));
     __syncthreads();
@@ -2697,7 +2753,7 @@ void spf_nh_levels_swar_kernel(NhLevelsArgs a, const uint32_t* big, uint32_t nbi
     for (uint32_t c = wv; c < nchunks; c += kNsThreads / 64) {
       const uint32_t v0 = c * kNsChunk + lane * kNsNodes;
       if (deep) {
-        nl_swar_deep(a, q, v0, w, Wm, cnt, ntmask, st_row, st_node, nhrow);
+        nl_swar_deep(a, dist, q, v0, w, Wm, cnt, ntmask, st_row, st_node, nhrow);
         continue;
       }
       const bool active = v0 < a.V;
@@ -2730,7 +2786,7 @@ void spf_nh_levels_swar_kernel(NhLevelsArgs a, const uint32_t* big, uint32_t nbi
             for (uint32_t kk = 0; kk < 8; ++kk) {
               lf[kk] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
               if (8 * g + kk < cnt) {
-                lf[kk] = *reinterpret_cast<const uint4*>(a.lvl + st_row[8 * g + kk] + v0);
+                lf[kk] = *reinterpret_cast<const uint4*>(lvl + st_row[8 * g + kk] + v0);
               }
             }
             const uint32_t ntg = (uint32_t)(ntmask >> (8 * g)) & 0xFFu;
@@ -2805,8 +2861,107 @@ __global__ __launch_bounds__(kNsHeldThreads) void spf_nh_levels_held_kernel(NhLe
   }
   const uint32_t s = a.src[q];
   const uint32_t beg = a.nbr_off[s], n = a.nbr_off[s + 1] - beg;
-  nl_swar_held(a, q, c, Wm, n, beg, a.nh_out + a.nh_off[q], a.lvl + (size_t)q * a.Vp8, st_row,
+  const uint8_t* lvl = a.lvl + (a.zvar ? a.zvar[q] * a.lvl_vstride : 0);
+  nl_swar_held(a, lvl, q, c, Wm, n, beg, a.nh_out + a.nh_off[q], lvl + (size_t)q * a.Vp8, st_row,
                st_node, st_nt);
+}
+
+// ------------------------------------------------- zero-metric plan helpers
+//
+// A uniform metric c plus a few node-disjoint metric-0 links (DESIGN.md §2,
+// "zero-metric plan").  DijkstraQ settles a plateau {a, b} (equal distance,
+// joined by a metric-0 link) in (metric, name) order among DISCOVERED nodes
+// (LinkState.h:483-535), and a node takes next hops only from neighbours
+// settled before it (LinkState.cpp:842-871), so the metric-0 half-edge from
+// the later-settled end into the earlier one never carries next hops.  For a
+// source s the reference's next hops are therefore the order-free
+// all-sources rule on G minus that half-edge; with k zero links there are
+// 2^k such graphs ("variants", bit i set: link i's b end settles first,
+// a -> b dropped; clear: b -> a dropped), and each gets its own MS-BFS
+// table.  spf_zvar_kernel picks each source's variant from the distances
+// (d = min over the variants, which is the distance in G): a plateau end is
+// discovered before the plateau starts iff it is the source or the head of
+// a usable tight in-edge of positive metric; two such ends settle by name
+// rank, else the discovered end first.
+
+struct ZvarArgs {
+  const uint32_t* row;
+  const uint32_t* col;
+  const uint32_t* win; // metric of the half-edge col[e] -> (row owner)
+  const uint32_t* trbits;
+  const uint32_t* src;
+  const uint32_t* dist;  // [nvar][nrows][Vp]
+  const uint32_t* links; // [nlinks][2] ends (a < b)
+  uint8_t* zvar;         // [nq]
+  uint64_t vstride;      // nrows * Vp
+  uint32_t Vp, nq, nvar, nlinks;
+};
+
+__global__ void spf_zvar_kernel(ZvarArgs a) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= a.nq) {
+    return;
+  }
+  const uint32_t s = a.src[q];
+  const uint32_t* d0 = a.dist + (size_t)q * a.Vp;
+  auto dmin = [&](uint32_t x) {
+    uint32_t m = kInf32;
+    for (uint32_t j = 0; j < a.nvar; ++j) {
+      m = min(m, d0[j * a.vstride + x]);
+    }
+    return m;
+  };
+  auto seed = [&](uint32_t x, uint32_t dx) {
+    if (x == s) {
+      return true;
+    }
+    for (uint32_t e = a.row[x]; e < a.row[x + 1]; ++e) {
+      const uint32_t u = a.col[e], w = a.win[e];
+      if (w == 0 || !(u == s || ((a.trbits[u >> 5] >> (u & 31)) & 1u))) {
+        continue;
+      }
+      const uint32_t du = dmin(u);
+      if (du != kInf32 && (uint64_t)du + w == dx) {
+        return true;
+      }
+    }
+    return false;
+  };
+  uint32_t var = 0;
+  for (uint32_t i = 0; i < a.nlinks; ++i) {
+    const uint32_t x = a.links[2 * i], y = a.links[2 * i + 1];
+    const uint32_t dx = dmin(x), dy = dmin(y);
+    if (dx == kInf32 || dx != dy) {
+      continue; // no plateau: either variant serves
+    }
+    const bool sx = seed(x, dx), sy = seed(y, dy);
+    if (sy && !sx) { // both discovered: x (the smaller rank) first
+      var |= 1u << i;
+    }
+  }
+  a.zvar[q] = (uint8_t)var;
+}
+
+// the output rows: source q's distances from its own variant table
+__global__ void spf_zrows_kernel(uint32_t* dist, const uint8_t* zvar, uint64_t vstride, uint32_t Vp) {
+  const uint32_t q = blockIdx.x;
+  const uint32_t zv = zvar[q];
+  if (!zv) {
+    return;
+  }
+  const uint4* in = reinterpret_cast<const uint4*>(dist + zv * vstride + (size_t)q * Vp);
+  uint4* out = reinterpret_cast<uint4*>(dist + (size_t)q * Vp);
+  for (uint32_t i = threadIdx.x; i < Vp / 4; i += blockDim.x) {
+    out[i] = in[i];
+  }
+}
+
+// a 64-bit distance row (wide plan) into a 32-bit one
+__global__ void spf_rows64to32_kernel(const uint64_t* in, uint32_t* out, uint32_t V) {
+  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < V; v += gridDim.x * blockDim.x) {
+    const uint64_t d = in[v];
+    out[v] = d == SPF_UNREACHABLE ? kInf32 : (uint32_t)d;
+  }
 }
 
 // six waves per SIMD (<= 80 VGPRs), as before the chunk-inner word loop
@@ -4247,6 +4402,17 @@ struct spf_query {
   uint32_t* d_qctr = nullptr; // dstep source-claim counter
   uint32_t* d_big = nullptr;  // nh_levels: queries with more than kNsHeldMax mask words
   uint32_t nbig = 0;
+  // zero-metric plan (spf_zvar_kernel): variant tables, their closure pairs
+  // (variant j: pairs [zoff[j], zoff[j+1]) of d_zl, then the links' ends at
+  // pair zoff[zvars]), each source's variant, and the wide-plan run of the
+  // sources with a metric-0 out-link (their first hop costs 0, outside the
+  // byte rule) whose rows replace this query's rows zfix_rows
+  uint32_t zvars = 0, zscale = 0, znlinks = 0;
+  std::vector<uint32_t> zoff;
+  uint32_t* d_zl = nullptr;
+  uint8_t* d_zvar = nullptr;
+  spf_query* zfix = nullptr;
+  std::vector<uint32_t> zfix_rows;
   // k-th path traces (spf_query_trace_paths): device scratch and the last
   // trace's per-query path / link counts
   uint32_t* d_trace = nullptr;
@@ -4434,11 +4600,14 @@ void free_query(spf_query* q) {
         (void*)q->d_lvl, (void*)q->d_flags, (void*)q->d_perm,
         (void*)q->d_slab, (void*)q->d_msd, (void*)q->d_base_of,
         (void*)q->d_skip, (void*)q->d_key, (void*)q->d_qctr, (void*)q->d_scatter,
-        (void*)q->d_trace, (void*)q->d_big}) {
+        (void*)q->d_trace, (void*)q->d_big, (void*)q->d_zl, (void*)q->d_zvar}) {
     pool_free(p);
   }
   if (q->base) {
     free_query(q->base);
+  }
+  if (q->zfix) {
+    free_query(q->zfix);
   }
   if (q->ev0) {
     ev_put(q->ev0);
@@ -5480,6 +5649,66 @@ int spf_graph_nbrs(const spf_graph* g, uint32_t node, uint32_t* out) {
   return SPF_OK;
 }
 
+namespace {
+
+// Zero-metric plan eligibility (spf_zvar_kernel): every metric is 0 or one
+// value c (c * V below 2^32 - 1), and the metric-0 half-edges join at most
+// kZeroLinks node pairs that share no node.  Parallel metric-0 links of one
+// pair count once (the plan reasons about the pair's settle order).
+constexpr uint32_t kZeroLinks = 3;
+struct ZeroLink {
+  uint32_t a, b; // a < b
+  bool ab, ba;   // a -> b / b -> a has metric 0
+};
+
+bool zero_plan_links(const spf_graph* g, std::vector<ZeroLink>& out, uint32_t& c) {
+  out.clear();
+  c = 0;
+  if (g->wrap || !g->n_zero || g->V < 2) {
+    return false;
+  }
+  for (uint32_t u = 0; u < g->V; ++u) {
+    for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
+      const uint64_t m = g->w64[e];
+      if (m != 0) {
+        if (c == 0) {
+          c = (uint32_t)m;
+        } else if (m != c) {
+          return false;
+        }
+        continue;
+      }
+      const uint32_t v = g->col[e];
+      if (v == u) {
+        return false;
+      }
+      const uint32_t a = std::min(u, v), b = std::max(u, v);
+      auto it = std::find_if(out.begin(), out.end(),
+                             [&](const ZeroLink& z) { return z.a == a && z.b == b; });
+      if (it == out.end()) {
+        if (out.size() == kZeroLinks) {
+          return false;
+        }
+        out.push_back({a, b, false, false});
+        it = out.end() - 1;
+      }
+      (u == a ? it->ab : it->ba) = true;
+    }
+  }
+  std::vector<uint32_t> ends;
+  for (const auto& z : out) {
+    ends.push_back(z.a);
+    ends.push_back(z.b);
+  }
+  std::sort(ends.begin(), ends.end());
+  if (std::adjacent_find(ends.begin(), ends.end()) != ends.end()) {
+    return false; // links share a node: a plateau of three or more nodes
+  }
+  return c != 0 && (uint64_t)c * g->V < 0xFFFFFFFFull && !out.empty();
+}
+
+} // namespace
+
 int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) {
   SPF_ABI_RANGE("spf_query_create");
   if (!g || !desc || !out) {
@@ -5565,8 +5794,17 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
   const char* lit_env = getenv("OPENR_SPF_LITERAL");
   const bool literal =
       (g->wrap && !unit) || (g->exact && !unit && lit_env && atoi(lit_env) == 1);
-  const bool exact = (g->exact && !unit) || want_order;
-  const bool uniform = unit || g->uniform != 0;
+  // metric-0 links on an otherwise uniform metric: MS-BFS variant tables
+  // (spf_zvar_kernel) instead of the wide plan (OPENR_SPF_ZERO_MSBFS=0: wide)
+  std::vector<ZeroLink> zlinks;
+  uint32_t zc = 0;
+  const bool zcand = !unit && !literal && !want_order && !has_ign && g->exact && g->n_zero &&
+                     nq >= 32 && V <= kMsThreads * kMsMaxK && 2 * (size_t)V * 4 <= kLdsLimit &&
+                     env_flag("OPENR_SPF_ZERO_MSBFS", 1) &&
+                     !(getenv("OPENR_SPF_MSBFS") && atoi(getenv("OPENR_SPF_MSBFS")) == 0) &&
+                     zero_plan_links(g, zlinks, zc);
+  const bool exact = ((g->exact && !unit) || want_order) && !zcand;
+  const bool uniform = unit || g->uniform != 0 || zcand;
   bool rows_ok = false;
   if (want_nh && !exact && !has_ign) {
     // next hops from distance rows need every neighbour's row in the batch
@@ -5730,7 +5968,72 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
   if (!helpers.empty() && !(q->dist == DistPlan::MsBfs && q->nh == NhPlan::Levels)) {
     return bail(fail(SPF_E_INVALID, "internal: helper sources outside the MS-BFS plan"));
   }
+  if (zcand && !(q->dist == DistPlan::MsBfs && (!want_nh || q->nh == NhPlan::Levels))) {
+    return bail(fail(SPF_E_INVALID, "internal: zero-metric plan outside MS-BFS"));
+  }
   q->nrows = nq + (uint32_t)helpers.size();
+  if (zcand) {
+    // next hops: one table per variant; distances alone: one table closed
+    // over every metric-0 half-edge
+    q->zvars = want_nh ? (1u << zlinks.size()) : 1u;
+    q->zscale = zc;
+    q->znlinks = (uint32_t)zlinks.size();
+    std::vector<uint32_t> zl;
+    for (uint32_t j = 0; j < q->zvars; ++j) {
+      q->zoff.push_back((uint32_t)(zl.size() / 2));
+      for (uint32_t i = 0; i < zlinks.size(); ++i) {
+        const ZeroLink& z = zlinks[i];
+        const bool bfirst = want_nh && ((j >> i) & 1u);
+        const bool afirst = want_nh && !((j >> i) & 1u);
+        if (z.ab && !bfirst) {
+          zl.push_back(z.a);
+          zl.push_back(z.b);
+        }
+        if (z.ba && !afirst) {
+          zl.push_back(z.b);
+          zl.push_back(z.a);
+        }
+      }
+    }
+    q->zoff.push_back((uint32_t)(zl.size() / 2));
+    for (const ZeroLink& z : zlinks) {
+      zl.push_back(z.a);
+      zl.push_back(z.b);
+    }
+    if (dev_upload_q(&q->d_zl, zl.data(), zl.size()) != SPF_OK) {
+      return bail(fail(SPF_E_NOMEM, "zero-metric closure lists"));
+    }
+    if (want_nh) {
+      if (pool_malloc((void**)&q->d_zvar, std::max<size_t>(nq, 16)) != hipSuccess) {
+        return bail(fail(SPF_E_NOMEM, "zero-metric variants"));
+      }
+      // sources whose first hop may cost 0: the wide plan, rows copied in
+      std::vector<uint32_t> fix;
+      for (uint32_t i = 0; i < nq; ++i) {
+        const uint32_t x = desc->sources[i];
+        for (const ZeroLink& z : zlinks) {
+          if ((x == z.a && z.ab) || (x == z.b && z.ba)) {
+            fix.push_back(x);
+            q->zfix_rows.push_back(i);
+            break;
+          }
+        }
+      }
+      if (!fix.empty()) {
+        spf_query_desc fd{};
+        fd.num_queries = (uint32_t)fix.size();
+        fd.sources = fix.data();
+        fd.flags = SPF_F_NEXTHOPS;
+        int fs = spf_query_create(g, &fd, &q->zfix);
+        if (fs != SPF_OK) {
+          return bail(fs);
+        }
+        if (q->zfix->dist != DistPlan::Wide) {
+          return bail(fail(SPF_E_INVALID, "internal: zero-metric fix-up outside the wide plan"));
+        }
+      }
+    }
+  }
 
   if (hipSetDevice(g->device) != hipSuccess) {
     return bail(fail(SPF_E_DEVICE, "hipSetDevice failed"));
@@ -5802,8 +6105,9 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       return bail(fail(SPF_E_NOMEM, "next-hop source list"));
     }
   }
+  const size_t ntab = std::max<uint32_t>(1, q->zvars); // MS-BFS tables (zero-metric variants)
   if (q->dist == DistPlan::MsBfs) {
-    if (pool_malloc((void**)&q->d_lvl, (size_t)q->nrows * q->Vp8) != hipSuccess ||
+    if (pool_malloc((void**)&q->d_lvl, ntab * q->nrows * q->Vp8) != hipSuccess ||
         pool_malloc((void**)&q->d_flags, 16) != hipSuccess) {
       return bail(fail(SPF_E_NOMEM, "level rows"));
     }
@@ -5816,7 +6120,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
   }
   const bool ex = q->dist == DistPlan::Exact;
   const bool wide = q->dist == DistPlan::Wide;
-  const size_t dist_bytes = (ex || wide) ? (size_t)nq * V * 8 : (size_t)q->nrows * q->Vp * 4;
+  const size_t dist_bytes = (ex || wide) ? (size_t)nq * V * 8 : ntab * q->nrows * q->Vp * 4;
   if (dist_bytes && pool_malloc(&q->d_dist, dist_bytes) != hipSuccess) {
     return bail(fail(SPF_E_NOMEM, "distance rows"));
   }
@@ -6163,8 +6467,10 @@ int launch_msbfs(spf_query* q, bool unit) {
   a.Vp = q->Vp;
   a.Vp8 = q->Vp8;
   a.nq = q->nrows; // the batch + its helper sources
-  a.scale = unit ? 1u : g->uniform;
+  a.scale = unit ? 1u : (q->zvars ? q->zscale : g->uniform);
   a.wrec = env_flag("OPENR_MS_WREC", 0); // measured slower (0.212 -> 0.232 ms, profiles/r03g)
+  a.zlist = nullptr;
+  a.nz = 0;
   HIP_TRY(hipMemsetAsync(q->d_flags, 0, 16, g->stream));
   const uint32_t K = (g->V + kMsThreads - 1) / kMsThreads;
   const void* kern = nullptr;
@@ -6197,12 +6503,44 @@ int launch_msbfs(spf_query* q, bool unit) {
 #undef MS_PICK
   HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)q->lds_bytes));
-  void* args[] = {&a};
-  HIP_TRY(hipLaunchKernel(kern, dim3(q->grid), dim3(kMsThreads), args,
-                          q->lds_bytes, g->stream));
-  HIP_TRY(hipGetLastError());
+  const uint32_t ntab = std::max<uint32_t>(1, q->zvars);
+  for (uint32_t j = 0; j < ntab; ++j) {
+    if (q->zvars) { // zero-metric variant j: its own table and closure pairs
+      a.dist_out = (uint32_t*)q->d_dist + (size_t)j * q->nrows * q->Vp;
+      a.lvl_out = q->d_lvl + (size_t)j * q->nrows * q->Vp8;
+      a.zlist = q->d_zl + 2 * (size_t)q->zoff[j];
+      a.nz = q->zoff[j + 1] - q->zoff[j];
+    }
+    void* args[] = {&a};
+    HIP_TRY(hipLaunchKernel(kern, dim3(q->grid), dim3(kMsThreads), args,
+                            q->lds_bytes, g->stream));
+    HIP_TRY(hipGetLastError());
+  }
+  if (q->zvars && q->d_zvar) {
+    ZvarArgs z;
+    z.row = g->d_row;
+    z.col = g->d_col;
+    z.win = g->d_win;
+    z.trbits = g->d_tr;
+    z.src = q->d_src;
+    z.dist = (const uint32_t*)q->d_dist;
+    z.links = q->d_zl + 2 * (size_t)q->zoff[q->zvars];
+    z.zvar = q->d_zvar;
+    z.vstride = (uint64_t)q->nrows * q->Vp;
+    z.Vp = q->Vp;
+    z.nq = q->nq;
+    z.nvar = q->zvars;
+    z.nlinks = q->znlinks;
+    hipLaunchKernelGGL(spf_zvar_kernel, dim3((q->nq + 255) / 256), dim3(256), 0, g->stream, z);
+    HIP_TRY(hipGetLastError());
+  }
   return SPF_OK;
 }
+
+// zero-metric plan, after the next-hop pass: every source's distance row from
+// its own variant table, then the wide-plan rows of the sources with a
+// metric-0 out-link
+int finish_zero_plan(spf_query* q);
 
 int launch_nh_levels(spf_query* q, bool unit) {
   spf_graph* g = q->g;
@@ -6222,16 +6560,19 @@ int launch_nh_levels(spf_query* q, bool unit) {
   a.Vp = q->Vp;
   a.Vp8 = q->Vp8;
   a.nq = q->nq;
-  a.scale = unit ? 1u : g->uniform;
+  a.scale = unit ? 1u : (q->zvars ? q->zscale : g->uniform);
   a.xcd_swizzle = env_flag("OPENR_NL_XCD", 0);
   a.held_words = env_flag("OPENR_NL_HELD", 1);
+  a.zvar = q->d_zvar;
+  a.lvl_vstride = (uint64_t)q->nrows * q->Vp8;
+  a.dist_vstride = (uint64_t)q->nrows * q->Vp;
   const uint32_t nchunks = (g->V + kNlChunk - 1) / kNlChunk;
   const uint64_t blocks =
       (uint64_t)((nchunks + kNlChunksPerBlock - 1) / kNlChunksPerBlock) * q->nq;
   if (blocks > 0x7FFFFFFFull) {
     return fail(SPF_E_UNSUPPORTED, "batch too large for the next-hop pass");
   }
-  if (env_flag("OPENR_NL_SWAR", 1)) {
+  if (env_flag("OPENR_NL_SWAR", 1) || q->d_zvar) {
     // held kernel: every source with <= kNsHeldMax mask words; the generic
     // byte kernel: the rest (q->d_big), or every source after a deep BFS
     const uint64_t hblocks = (uint64_t)q->nq * ((g->V + kNsChunk - 1) / kNsChunk);
@@ -6350,6 +6691,38 @@ int mark_stage(spf_query* q) {
 
 int run_plan(spf_query* q);
 
+int finish_zero_plan(spf_query* q) {
+  spf_graph* g = q->g;
+  if (!q->d_zvar) {
+    return SPF_OK; // distances alone: one table, already in place
+  }
+  hipLaunchKernelGGL(spf_zrows_kernel, dim3(q->nq), dim3(256), 0, g->stream, (uint32_t*)q->d_dist,
+                     (const uint8_t*)q->d_zvar, (uint64_t)q->nrows * q->Vp, q->Vp);
+  HIP_TRY(hipGetLastError());
+  if (!q->zfix) {
+    return SPF_OK;
+  }
+  spf_query* f = q->zfix;
+  int s = run_plan(f);
+  if (s != SPF_OK) {
+    return s;
+  }
+  const uint32_t V = g->V;
+  for (uint32_t j = 0; j < f->nq; ++j) {
+    const uint32_t i = q->zfix_rows[j];
+    if (f->nh_w[j] != q->nh_w[i]) {
+      return fail(SPF_E_INVALID, "internal: zero-metric fix-up mask width differs");
+    }
+    HIP_TRY(hipMemcpyAsync(q->d_nh + q->nh_off[i], f->d_nh + f->nh_off[j],
+                           (size_t)q->nh_w[i] * V * 8, hipMemcpyDeviceToDevice, g->stream));
+    hipLaunchKernelGGL(spf_rows64to32_kernel, dim3((V + 255) / 256), dim3(256), 0, g->stream,
+                       (const uint64_t*)f->d_dist + (size_t)j * V,
+                       (uint32_t*)q->d_dist + (size_t)i * q->Vp, V);
+    HIP_TRY(hipGetLastError());
+  }
+  return SPF_OK;
+}
+
 int run_screen(spf_query* q) {
   spf_query* b = q->base;
   spf_graph* g = q->g;
@@ -6411,6 +6784,9 @@ int run_plan(spf_query* q) {
       if (s == SPF_OK) {
         s = launch_nh_levels(q, unit);
       }
+    }
+    if (s == SPF_OK && q->zvars) {
+      s = finish_zero_plan(q);
     }
     return s;
   }
@@ -6556,6 +6932,9 @@ const char* spf_query_kernel_name(const spf_query* q) {
   case DistPlan::BfsGmem:
     return q->nh == NhPlan::Rows ? "bfs-gmem+rows" : "bfs-gmem";
   case DistPlan::MsBfs:
+    if (q->zvars) {
+      return q->nh == NhPlan::Levels ? "msbfs0+levels" : "msbfs0";
+    }
     return q->nh == NhPlan::Levels ? "msbfs+levels" : "msbfs";
   case DistPlan::Dstep:
     return "dstep";

@@ -1200,6 +1200,7 @@ def wan_table_repair(topo, csr, sas, world, rank, local, dist):
                        "screen_ms": round(float(t[2]), 2), "graph_ms": round(float(t[3]), 2),
                        "exchange_ms": round(float(t[4]), 2), "diff_ms": round(rep.diff_ms, 2),
                        "graph_patched_in_place": rep.graph_patched,
+                       "result_release_ms": round(rep.extra.get("release_ms", 0.0), 2),
                        "rows": "repaired in place (spf_table_repair)" if rep.relaxed else "recomputed"})
         cur = nxt
     check = None

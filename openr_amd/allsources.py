@@ -356,6 +356,7 @@ class ShardedAllSources:
         self._lay_col = np.asarray(csr.col, dtype=np.uint32).copy()
         self._lay_up = np.ones(len(csr.col), dtype=bool)
         self._lay_w = np.asarray(csr.metric, dtype=np.uint64).copy()
+        self._lay_is_csr = csr  # the layout is exactly this CSR's (no link set in place)
 
     def _links_in_place(self, deltas):
         """Map link-set deltas (spf_graph_diff: REMOVED / ADDED half-edges
@@ -369,9 +370,8 @@ class ShardedAllSources:
         from openr_amd import abi
 
         SCOPE_NOT_TAIL = 2
-        up = self._lay_up.copy()
-        w = self._lay_w.copy()
-        touched = {}
+        up0, w0 = self._lay_up, self._lay_w
+        touched = {}  # slot -> (up, metric), applied once every delta has mapped
         order = sorted((d for d in deltas if int(d["scope"]) != SCOPE_NOT_TAIL),
                        key=lambda d: int(d["kind"]) != abi.SPF_DELTA_REMOVED)
         for d in order:
@@ -380,20 +380,26 @@ class ShardedAllSources:
                 return None
             lo, hi = int(self._lay_row[u]), int(self._lay_row[u + 1])
             cols = self._lay_col[lo:hi]
+            up = up0[lo:hi].copy()
+            w = w0[lo:hi].copy()
+            for e, (eu, ew) in touched.items():
+                if lo <= e < hi:
+                    up[e - lo], w[e - lo] = eu, ew
             if kind == abi.SPF_DELTA_REMOVED:
-                cand = np.nonzero((cols == v) & up[lo:hi] & (w[lo:hi] == np.uint64(m)))[0]
+                cand = np.nonzero((cols == v) & up & (w == np.uint64(m)))[0]
             else:
-                cand = np.nonzero((cols == v) & ~up[lo:hi])[0]
+                cand = np.nonzero((cols == v) & ~up)[0]
             if len(cand) == 0:
                 return None
             e = lo + int(cand[0])
-            up[e] = kind != abi.SPF_DELTA_REMOVED
-            if kind != abi.SPF_DELTA_REMOVED:
-                w[e] = m
-            touched[e] = None
-        self._lay_up, self._lay_w = up, w
+            removed = kind == abi.SPF_DELTA_REMOVED
+            touched[e] = (not removed, int(w[e - lo]) if removed else m)
         e = np.fromiter(touched.keys(), dtype=np.uint32, count=len(touched))
-        return e, up[e].astype(np.uint8), w[e]
+        new_up = np.fromiter((t[0] for t in touched.values()), dtype=bool, count=len(touched))
+        new_w = np.fromiter((t[1] for t in touched.values()), dtype=np.uint64, count=len(touched))
+        up0[e] = new_up
+        w0[e] = new_w
+        return e, new_up.astype(np.uint8), new_w
 
     def update(self, new_csr) -> RepairRun:
         """Repair the table after a topology change instead of recomputing
@@ -433,20 +439,27 @@ class ShardedAllSources:
         # the full-batch query holds a result block the size of this rank's
         # table slot: release it before the repair allocates
         if self.query is not None:
+            tr = time.perf_counter()
             self.query.close()
             self.query = None
+            out.extra["release_ms"] = (time.perf_counter() - tr) * 1e3
         old = self.csr
+
+        def same(x, y):  # shared arrays (a metric / drain event) skip the compare
+            return x is y or np.array_equal(x, y)
+
         same_links = (
             len(old.col) == len(new_csr.col)
-            and np.array_equal(old.row_ptr, new_csr.row_ptr)
-            and np.array_equal(old.col, new_csr.col)
-            and np.array_equal(old.link_id, new_csr.link_id)
-            and np.array_equal(old.rev, new_csr.rev)
+            and same(old.row_ptr, new_csr.row_ptr)
+            and same(old.col, new_csr.col)
+            and same(old.link_id, new_csr.link_id)
+            and same(old.rev, new_csr.rev)
         )
         # the resident graph's layout is the old CSR's unless links were
         # taken down / up in place before
-        layout_is_old = bool(self._lay_up.all()) and len(self._lay_col) == len(old.col) and \
-            np.array_equal(self._lay_row, old.row_ptr) and np.array_equal(self._lay_col, old.col)
+        layout_is_old = self._lay_is_csr is old or (
+            bool(self._lay_up.all()) and len(self._lay_col) == len(old.col)
+            and np.array_equal(self._lay_row, old.row_ptr) and np.array_equal(self._lay_col, old.col))
         inplace = None
         if (not (same_links and layout_is_old) and not self.nexthops
                 and os.environ.get("OPENR_SPF_LINKS_INPLACE", "1") != "0"):
@@ -459,7 +472,8 @@ class ShardedAllSources:
             if not np.array_equal(old.overloaded, new_csr.overloaded):
                 self.graph.set_transit(new_csr.overloaded)
             self.graph.csr = new_csr
-            self._lay_w = new_csr.metric.astype(np.uint64).copy()
+            self._lay_w[ch] = new_csr.metric[ch]
+            self._lay_is_csr = new_csr
             out.graph_patched = True
         elif inplace is not None:
             # links down / back up: the half-edges stay at their positions of
@@ -467,6 +481,7 @@ class ShardedAllSources:
             e, up, w = inplace
             if len(e):
                 self.graph.set_edges(e, up, w)
+            self._lay_is_csr = None
             if not np.array_equal(old.overloaded, new_csr.overloaded):
                 self.graph.set_transit(new_csr.overloaded)
             out.graph_patched = True

@@ -4355,6 +4355,11 @@ struct spf_graph {
   std::vector<uint32_t> col_orig;
   std::vector<uint8_t> edge_up;
   bool links_patched = false;
+  // spf_table_repair's delta block + per-workgroup queues, kept between
+  // calls (a 100k-node graph needs 200 MB: allocating it per churn event
+  // cost more than the screen)
+  char* d_repair = nullptr;
+  size_t repair_bytes = 0;
 };
 
 // How a batch is computed.
@@ -4575,7 +4580,7 @@ void free_graph(spf_graph* g) {
         (void*)g->d_link, (void*)g->d_rev, (void*)g->d_slot, (void*)g->d_tr,
         (void*)g->d_w64, (void*)g->d_nbr_off, (void*)g->d_nbrs,
         (void*)g->d_nbr_w, (void*)g->d_link_half, (void*)g->d_cw,
-        (void*)g->d_zero_e}) {
+        (void*)g->d_zero_e, (void*)g->d_sell, (void*)g->d_sell_off, (void*)g->d_repair}) {
     if (p) {
       (void)hipFree(p);
     }
@@ -4869,22 +4874,11 @@ int upload_sell(spf_graph* g) {
 // scan of w64.  SPF_E_UNSUPPORTED (nothing changed) when the patch would
 // change the set of metric-0 edges, the wrap flag or the packed-edge layout:
 // the caller then runs upload_weights.
-int patch_weights_sparse(spf_graph* g, uint32_t n, const uint32_t* edge_idx, const uint64_t* m) {
+// graph scalars after an in-place metric / link patch: maxw, the wide-plan
+// band (mean metric), uniformity and the 32-bit row bound, in one parallel
+// scan of the host metrics
+void rescan_scalars(spf_graph* g) {
   const uint32_t E = g->E;
-  for (uint32_t i = 0; i < n; ++i) {
-    const uint64_t o = g->w64[edge_idx[i]], w = m[i];
-    if ((o == 0) != (w == 0) || (o > 0x7FFFFFFFull) != (w > 0x7FFFFFFFull)) {
-      return SPF_E_UNSUPPORTED; // zero-edge list / wrap flag change
-    }
-    if (g->cw_bits && w >= (1ull << (32 - g->cw_bits))) {
-      return SPF_E_UNSUPPORTED; // no longer packable
-    }
-  }
-  HIP_TRY(hipStreamSynchronize(g->stream)); // queued kernels read the old words
-  for (uint32_t i = 0; i < n; ++i) {
-    g->w64[edge_idx[i]] = m[i];
-  }
-  // scalars: one parallel scan (maxw / sum / uniformity)
   const unsigned nth = openr::hostThreads(E, 1u << 16);
   const size_t chunk = (E + nth - 1) / std::max(1u, nth);
   std::vector<uint64_t> wmax(nth, 0), wsum(nth, 0);
@@ -4915,6 +4909,24 @@ int patch_weights_sparse(spf_graph* g, uint32_t n, const uint32_t* edge_idx, con
   refresh_exact(g);
   g->wide_delta = E ? std::max<uint64_t>(1, sumw / E) : 1;
   g->uniform = (!g->exact && E && uni) ? (uint32_t)c0 : 0;
+}
+
+int patch_weights_sparse(spf_graph* g, uint32_t n, const uint32_t* edge_idx, const uint64_t* m) {
+  const uint32_t E = g->E;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t o = g->w64[edge_idx[i]], w = m[i];
+    if ((o == 0) != (w == 0) || (o > 0x7FFFFFFFull) != (w > 0x7FFFFFFFull)) {
+      return SPF_E_UNSUPPORTED; // zero-edge list / wrap flag change
+    }
+    if (g->cw_bits && w >= (1ull << (32 - g->cw_bits))) {
+      return SPF_E_UNSUPPORTED; // no longer packable
+    }
+  }
+  HIP_TRY(hipStreamSynchronize(g->stream)); // queued kernels read the old words
+  for (uint32_t i = 0; i < n; ++i) {
+    g->w64[edge_idx[i]] = m[i];
+  }
+  rescan_scalars(g);
   // the device words (u32 index, u32 lo, u32 hi) per array, one upload
   std::vector<uint32_t> pk;
   uint32_t counts[5] = {0, 0, 0, 0, 0};
@@ -5571,20 +5583,9 @@ int spf_graph_set_edges(
     }
     w64l.insert(w64l.end(), {e, (uint32_t)metric[i], (uint32_t)(metric[i] >> 32)});
   }
-  // graph scalars: maxw / mean / uniformity and the 32-bit row bound (the
-  // transit hop bound reads the patched heads)
-  uint64_t maxw = 0, sumw = 0;
-  bool uni = true;
-  const uint64_t c0 = g->E ? g->w64[0] : 0;
-  for (uint32_t e = 0; e < g->E; ++e) {
-    maxw = std::max(maxw, g->w64[e]);
-    sumw += g->w64[e];
-    uni = uni && g->w64[e] == c0;
-  }
-  g->maxw = maxw;
-  refresh_exact(g);
-  g->wide_delta = g->E ? std::max<uint64_t>(1, sumw / g->E) : 1;
-  g->uniform = (!g->exact && g->E && uni) ? (uint32_t)c0 : 0;
+  // graph scalars and the 32-bit row bound (the transit hop bound reads the
+  // patched heads)
+  rescan_scalars(g);
   g->ecc_est = 0;
   g->links_patched = true;
   PatchArgs a{};
@@ -7315,16 +7316,21 @@ int spf_graph_diff(
       return fail(SPF_E_INVALID, "malformed graph description");
     }
   }
-  uint64_t n = 0;
+  // node blocks in parallel, each into its own list; the lists are then
+  // concatenated in node order (the serial scan's output order)
+  const uint32_t nblk = (V + kHostBlock - 1) / kHostBlock;
+  std::vector<std::vector<spf_edge_delta>> found(nblk);
+  const unsigned nth =
+      openr::hostThreads((size_t)before->num_edges + after->num_edges, 1u << 16);
+  openr::parallelFor(nblk, nth, [&](size_t blk, unsigned) {
+  std::vector<spf_edge_delta>& lst = found[blk];
   auto emit = [&](uint32_t u, uint32_t v, uint64_t w, uint32_t kind, uint32_t scope) {
-    if (n < cap) {
-      out[n] = spf_edge_delta{u, v, w, kind, scope};
-    }
-    ++n;
+    lst.push_back(spf_edge_delta{u, v, w, kind, scope});
   };
   using HE = std::pair<uint32_t, uint64_t>; // (head, metric)
   std::vector<HE> a, b;
-  for (uint32_t u = 0; u < V; ++u) {
+  const uint32_t u1 = std::min<uint32_t>(V, (uint32_t)(blk + 1) * kHostBlock);
+  for (uint32_t u = (uint32_t)blk * kHostBlock; u < u1; ++u) {
     const bool trA = !before->node_overloaded[u], trB = !after->node_overloaded[u];
     const uint32_t ra = before->row_ptr[u], na = before->row_ptr[u + 1] - ra;
     const uint32_t rb = after->row_ptr[u], nb = after->row_ptr[u + 1] - rb;
@@ -7366,6 +7372,16 @@ int spf_graph_diff(
         ++i;
         ++j;
       }
+    }
+  }
+  }, 1);
+  uint64_t n = 0;
+  for (const auto& lst : found) {
+    for (const spf_edge_delta& d : lst) {
+      if (n < cap) {
+        out[n] = d;
+      }
+      ++n;
     }
   }
   if (n > 0xFFFFFFFFull) {
@@ -7642,8 +7658,17 @@ int spf_table_repair(
   if (nrem) {
     std::memcpy(h.data() + off64, rw.data(), (size_t)nrem * 8);
   }
-  char* d = nullptr;
-  HIP_TRY(hipMalloc((void**)&d, bytes));
+  if (g->repair_bytes < bytes) {
+    HIP_TRY(hipStreamSynchronize(g->stream));
+    if (g->d_repair) {
+      HIP_TRY(hipFree(g->d_repair));
+      g->d_repair = nullptr;
+      g->repair_bytes = 0;
+    }
+    HIP_TRY(hipMalloc((void**)&g->d_repair, bytes));
+    g->repair_bytes = bytes;
+  }
+  char* d = g->d_repair;
   int st = SPF_OK;
   if (hipMemcpyAsync(d, h.data(), meta, hipMemcpyHostToDevice, g->stream) != hipSuccess) {
     st = fail(SPF_E_DEVICE, "delta upload failed");
@@ -7702,7 +7727,6 @@ int spf_table_repair(
     }
   }
   (void)hipStreamSynchronize(g->stream);
-  (void)hipFree(d);
   return st;
 }
 

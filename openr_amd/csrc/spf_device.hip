@@ -6545,7 +6545,7 @@ int finish_zero_plan(spf_query* q);
 
 int launch_nh_levels(spf_query* q, bool unit) {
   spf_graph* g = q->g;
-  NhLevelsArgs a;
+  NhLevelsArgs a{};
   a.nbr_off = g->d_nbr_off;
   a.nbrs = g->d_nbrs;
   a.trbits = g->d_tr;

@@ -168,10 +168,13 @@ class SpfRead {
       : ls_(ls), src_(src), view_(view), names_(ls.nodeNames()) {}
 
   std::optional<Metric> metric(const std::string& node) const {
+    return metricById(ls_.nodeId(node), node);
+  }
+  // metric() with the node's id already looked up (ls.nodeId(node))
+  std::optional<Metric> metricById(std::optional<uint32_t> id, const std::string& node) const {
     if (view_.src == ~0u) {
       return node == src_ ? std::optional<Metric>(0) : std::nullopt;
     }
-    auto id = ls_.nodeId(node);
     if (!id || !view_.reached(*id)) {
       return std::nullopt;
     }
@@ -354,10 +357,19 @@ class SpfSolver::SpfSolverImpl {
     const thrift::BinaryAddress* nhV6;
     const std::string* iface;
   };
+  // a loop-free-alternate candidate: an up link's neighbour, its SPF view
+  // and its distance back to myNode (getNextHopsWithMetric's LFA loop)
+  struct LfaNbr {
+    const std::string* nbr;
+    SpfRead read;
+    std::optional<Metric> toHere;
+  };
   struct MyLinks {
     std::string node;
     std::vector<MyLink> links;
     std::unordered_map<std::string_view, std::vector<uint32_t>> byNbr;
+    // computeLfaPaths_: every up link of myNode in linksFromNode() order
+    std::vector<LfaNbr> lfa;
     // node's own link-metric SPF view, resolved on first read (spfView's
     // memo lock is then off the per-prefix path of the worker pool)
     mutable std::atomic<const SpfView*> view{nullptr};
@@ -377,8 +389,20 @@ class SpfSolver::SpfSolverImpl {
           link.get(), &nbr, std::string_view(nbr), link->isUp(),
           link->getMetricFromNode(myNodeName), &link->getNhV4FromNode(myNodeName),
           &link->getNhV6FromNode(myNodeName), &link->getIfaceFromNode(myNodeName)});
+      if (computeLfaPaths_ && link->isUp()) {
+        // the neighbour's view resolved once per build (prefetched), not per
+        // prefix and per neighbour under spfView's memo lock
+        SpfRead r(ls, nbr);
+        const auto toHere = r.metric(myNodeName);
+        v.lfa.push_back(LfaNbr{&nbr, std::move(r), toHere});
+      }
     }
     return v;
+  }
+  // the per-build cache of `area` if it was filled for myNodeName
+  const MyLinks* cachedLinks(const std::string& myNodeName, const std::string& area) const {
+    auto it = myLinks_.find(area);
+    return it != myLinks_.end() && it->second.node == myNodeName ? &it->second : nullptr;
   }
   mutable std::unordered_map<std::string, MyLinks> myLinks_;
   // SpfRead of myNodeName's own SPF in `area` (the per-build cached view)
@@ -1181,6 +1205,38 @@ std::pair<Metric, NextHopNodes> SpfSolver::SpfSolverImpl::getNextHopsWithMetric(
       });
     }
     if (computeLfaPaths_) {
+      if (const MyLinks* mls = cachedLinks(myNodeName, areaName)) {
+        // RFC 5286 loop-free alternates through every up neighbour (per-build
+        // neighbour views; each destination's id looked up once)
+        std::vector<std::pair<const std::string*, std::optional<uint32_t>>> dsts;
+        dsts.reserve(dstNodeNames.size());
+        for (const auto& dst : dstNodeNames) {
+          dsts.emplace_back(&dst, ls.nodeId(dst));
+        }
+        for (const LfaNbr& ln : mls->lfa) {
+          if (!ln.toHere) {
+            throw std::out_of_range("LFA: neighbour cannot reach " + myNodeName);
+          }
+          for (const auto& [dst, id] : dsts) {
+            const auto dNbr = ln.read.metricById(id, *dst);
+            if (!dNbr) {
+              continue;
+            }
+            if (*dNbr < shortestMetric + *ln.toHere) {
+              auto key = std::make_pair(
+                  std::string_view(*ln.nbr),
+                  perDestination ? std::string_view(*dst) : std::string_view(kNoDestName));
+              auto it = nextHopNodes.find(key);
+              if (it == nextHopNodes.end()) {
+                nextHopNodes.emplace(std::move(key), *dNbr);
+              } else if (it->second > *dNbr) {
+                it->second = *dNbr;
+              }
+            }
+          }
+        }
+        continue;
+      }
       // RFC 5286 loop-free alternates through every up neighbour
       for (const auto& link : ls.linksFromNode(myNodeName)) {
         if (!link->isUp()) {

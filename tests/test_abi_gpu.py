@@ -524,14 +524,15 @@ def test_msbfs_sliced_ell_matches_csr(gpu_ready, sell, wrec, monkeypatch):
         assert (q.nexthops(i) == r.nexthops(i)).all(), i
 
 
-@pytest.mark.parametrize("case", ["random", "hubs", "deep"])
+@pytest.mark.parametrize("case", ["random", "hubs", "wide_hubs", "deep"])
 def test_nh_levels_swar_matches_scalar(gpu_ready, case, monkeypatch):
-    """The byte-SIMD next-hop pass (spf_nh_levels_swar_kernel) against the
-    per-node pass (spf_nh_levels_kernel) on the same MS-BFS rows, and both
-    against the literal replay on a few sources: drained neighbours (next
-    hop only to themselves), sources with 1-3 mask words, a ragged last
+    """The byte-SIMD next-hop pass (spf_nh_levels_held_kernel, its 4-8 word
+    instance and spf_nh_levels_swar_kernel) against the per-node pass
+    (spf_nh_levels_kernel) on the same MS-BFS rows, and both against the
+    literal replay on a few sources: drained neighbours (next hop only to
+    themselves), sources with 1-3, 4-8 and more mask words, a ragged last
     chunk, and a BFS deeper than 254 levels (the 32-bit-row branch)."""
-    rng = random.Random({"random": 5, "hubs": 6, "deep": 7}[case])
+    rng = random.Random({"random": 5, "hubs": 6, "wide_hubs": 8, "deep": 7}[case])
     if case == "deep":
         V = 700  # a 600-node chain hanging off a random core: levels > 255
         links = random_links(rng, 100, 400, wmin=1, wmax=1, parallel=0.0)
@@ -542,6 +543,10 @@ def test_nh_levels_swar_matches_scalar(gpu_ready, case, monkeypatch):
         if case == "hubs":
             links += [(7, v, 1, 1) for v in range(100, 260)]  # 3 mask words
             links += [(8, v, 1, 1) for v in range(300, 400)]  # 2 mask words
+        if case == "wide_hubs":
+            links += [(7, v, 1, 1) for v in range(20, 300)]   # 5 mask words
+            links += [(8, v, 1, 1) for v in range(300, 800)]  # 8 mask words
+            links += [(9, v, 1, 1) for v in range(200, 800)]  # 10 mask words (generic)
     ov = np.zeros(V, dtype=np.uint8)
     ov[rng.sample(range(V), V // 40)] = 1
     csr = abi.Csr.from_links(V, links, overloaded=ov)
@@ -560,7 +565,7 @@ def test_nh_levels_swar_matches_scalar(gpu_ready, case, monkeypatch):
     if not (ma == mb).all():
         bad = int(np.flatnonzero(ma != mb)[0])
         pytest.fail(f"mask word {bad} differs: {ma[bad]:#x} vs {mb[bad]:#x}")
-    probe = [0, 7, 8, V - 1, V // 2] if case != "deep" else [0, 99, 650, 699]
+    probe = [0, 7, 8, 9, V - 1, V // 2] if case != "deep" else [0, 99, 650, 699]
     check_query(csr, a, [int(s) for s in srcs], False, rows=set(probe))
 
 

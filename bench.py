@@ -90,25 +90,34 @@ def distinct_nbrs(csr):
     return np.bincount(key // V, minlength=V)
 
 
-def nh_levels_bytes(csr, nbrs, nh_words, level_bytes=1):
-    """Compulsory bytes of one spf_nh_levels_kernel launch: every source's
-    level row read once (the rows of a source's neighbours are other
-    sources' rows: re-reads, served by L2 / MALL when the kernel is good) and
-    every next-hop mask row written once."""
+def lvl_only():
+    """The engine's default (OPENR_MS_LVL_ONLY, spf_device.hip lvl_only):
+    the next-hop pass, not the BFS, writes the u32 distance rows."""
+    return os.environ.get("OPENR_MS_LVL_ONLY", "1") != "0" and \
+        os.environ.get("OPENR_NL_SWAR", "1") != "0"
+
+
+def nh_levels_bytes(csr, nbrs, nh_words, level_bytes=1, dist_rows=False):
+    """Compulsory bytes of one next-hop pass launch: every source's level row
+    read once (the rows of a source's neighbours are other sources' rows:
+    re-reads, served by L2 / MALL when the kernel is good), every next-hop
+    mask row written once, and with `dist_rows` every source's u32 distance
+    row written once (lvl_only)."""
     import numpy as np
 
     V = csr.num_nodes
     w = np.asarray(nh_words, dtype=np.int64)
-    return int(V * level_bytes * len(w) + 8 * V * int(w.sum()))
+    return int(V * level_bytes * len(w) + 8 * V * int(w.sum()) + (4 * V * len(w) if dist_rows else 0))
 
 
-def msbfs_bytes(csr, nsrc, levels_per_batch):
-    """Compulsory bytes of one spf_msbfs_kernel launch: u32 distance + u8
-    level rows written once, the CSR read once per 64-source batch and
-    level (each level is one pull scan of the CSR for the whole batch)."""
+def msbfs_bytes(csr, nsrc, levels_per_batch, dist_rows=True):
+    """Compulsory bytes of one spf_msbfs_kernel launch: u8 level rows (and
+    u32 distance rows unless the next-hop pass writes them) written once,
+    the CSR read once per 64-source batch and level (each level is one pull
+    scan of the CSR for the whole batch)."""
     V = csr.num_nodes
     E = len(csr.col)
-    return int(5 * V * nsrc + sum(levels_per_batch) * (4 * E + 4 * (V + 1)))
+    return int((5 if dist_rows else 1) * V * nsrc + sum(levels_per_batch) * (4 * E + 4 * (V + 1)))
 
 
 def pmc_traffic(kernel_name):
@@ -1499,12 +1508,13 @@ def fabric_single(args, topo, world, rank, local, dist):
         lv = int(ecc.max()) + 2  # +1 level discovering nothing, +1 source level
         levels = [lv] * ((nsrc + 63) // 64)
     stages = {}
+    lo = kname == "msbfs+levels" and lvl_only()
     if nh_k:
-        b = nh_levels_bytes(csr, nbrs, nh_words) if "levels" in kname else None
+        b = nh_levels_bytes(csr, nbrs, nh_words, dist_rows=lo) if "levels" in kname else None
         stages[nh_k] = {"avg_ms": round(n_ms, 4), "algorithmic_bytes": b}
     stages[dist_k] = {
         "avg_ms": round(d_ms, 4),
-        "algorithmic_bytes": msbfs_bytes(csr, nsrc, levels) if levels else None,
+        "algorithmic_bytes": msbfs_bytes(csr, nsrc, levels, dist_rows=not lo) if levels else None,
     }
     dom = max(stages, key=lambda k: stages[k]["avg_ms"])
     dom_bytes = stages[dom]["algorithmic_bytes"]

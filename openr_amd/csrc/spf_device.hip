@@ -84,6 +84,12 @@ uint32_t env_flag(const char* name, uint32_t dflt) {
   return v ? (uint32_t)(atoi(v) != 0) : dflt;
 }
 
+// unsigned value from the environment (A/B knobs with a size)
+uint32_t env_u32(const char* name, uint32_t dflt) {
+  const char* v = getenv(name);
+  return v ? (uint32_t)strtoul(v, nullptr, 10) : dflt;
+}
+
 int fail(int code, const std::string& what) {
   g_last_error = what;
   return code;
@@ -1833,6 +1839,10 @@ struct MsBfsArgs {
   // pass closes over at every level (ms_zero_close); nz = 0 elsewhere
   const uint32_t* zlist;
   uint32_t nz;
+  // 1: distances below level 255 are left to the next-hop pass, which
+  // writes them from the level rows as coalesced 16-byte stores
+  // (OPENR_MS_LVL_ONLY); levels >= 255 and unreached pairs still go here
+  uint32_t lvl_only;
 };
 
 // Write each (source, node) distance the moment its bit appears (one store
@@ -1848,10 +1858,13 @@ __device__ __forceinline__ void ms_record(
   if (level >= 255 && bits) {
     atomicOr(a.flags, 1u);
   }
+  const bool wd = !a.lvl_only || level >= 255;
   while (bits) {
     const uint32_t s = (uint32_t)__builtin_ctzll((unsigned long long)bits);
     bits &= bits - 1;
-    a.dist_out[(size_t)(q0 + s) * a.Vp + v] = d;
+    if (wd) {
+      a.dist_out[(size_t)(q0 + s) * a.Vp + v] = d;
+    }
     a.lvl_out[(size_t)(q0 + s) * a.Vp8 + v] = l8;
   }
 }
@@ -1881,7 +1894,9 @@ __device__ __forceinline__ void ms_record_wave(
     const uint32_t s = (uint32_t)__builtin_ctzll((unsigned long long)w);
     w &= w - 1;
     if (((uint64_t)bits >> s) & 1u) {
-      a.dist_out[(size_t)(q0 + s) * a.Vp + v] = d;
+      if (!a.lvl_only || level >= 255) {
+        a.dist_out[(size_t)(q0 + s) * a.Vp + v] = d;
+      }
       a.lvl_out[(size_t)(q0 + s) * a.Vp8 + v] = l8;
     }
   }
@@ -2114,6 +2129,10 @@ struct NhLevelsArgs {
   const uint8_t* zvar;
   uint64_t lvl_vstride;
   uint64_t dist_vstride;
+  // MsBfsArgs::lvl_only: the pass writes each source's distances below
+  // level 255 (lvl * scale) into dist_w and reads neighbour distances from
+  // the level byte when it is below 255
+  uint32_t* dist_w;
 };
 
 constexpr uint32_t kNlThreads = 256;
@@ -2549,6 +2568,26 @@ __device__ __forceinline__ void swar_transpose4(
   out[3] = __builtin_amdgcn_perm(t3, t1, 0x07060302u);
 }
 
+// MsBfsArgs::lvl_only: source q's distances of nodes v0..v0+3 from their
+// level bytes (lvl * scale below 255; 255 = unreached or deep, written by
+// the BFS itself), one 16-byte store when all four are below 255
+__device__ __forceinline__ void nl_dist_from_levels(
+    const NhLevelsArgs& a, uint32_t q, uint32_t v0, uint32_t ls) {
+  uint32_t* dw = a.dist_w + (size_t)q * a.Vp + v0;
+  const uint32_t b[4] = {ls & 0xFFu, (ls >> 8) & 0xFFu, (ls >> 16) & 0xFFu, ls >> 24};
+  if (v0 + 4 <= a.V && b[0] < 255 && b[1] < 255 && b[2] < 255 && b[3] < 255) {
+    *reinterpret_cast<uint4*>(dw) =
+        make_uint4(b[0] * a.scale, b[1] * a.scale, b[2] * a.scale, b[3] * a.scale);
+    return;
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i) {
+    if (v0 + i < a.V && b[i] < 255) {
+      dw[i] = b[i] * a.scale;
+    }
+  }
+}
+
 // the generic branch (a BFS deeper than 254 levels): 32-bit rows, one node
 // at a time; out of line so its registers do not weigh on the byte path
 __device__ __noinline__ void nl_swar_deep(
@@ -2561,11 +2600,23 @@ __device__ __noinline__ void nl_swar_deep(
       break;
     }
     uint64_t acc = 0;
-    const uint32_t ds = dist[(size_t)q * a.Vp + v];
+    auto dget = [&](uint32_t row) {
+      if (a.dist_w) { // levels below 255 are not in the 32-bit rows
+        const uint32_t l = a.lvl[(size_t)row * a.Vp8 + v];
+        if (l < 255) {
+          return l * a.scale;
+        }
+      }
+      return dist[(size_t)row * a.Vp + v];
+    };
+    const uint32_t ds = dget(q);
+    if (a.dist_w && w == 0) {
+      a.dist_w[(size_t)q * a.Vp + v] = ds;
+    }
     if (ds != kInf32 && ds != 0) {
       for (uint32_t j = 0; j < cnt; ++j) {
         // st_row holds level-row byte offsets (row * Vp8)
-        const uint32_t df = dist[(size_t)(st_row[j] / a.Vp8) * a.Vp + v];
+        const uint32_t df = dget(st_row[j] / a.Vp8);
         const bool tr = !((ntmask >> j) & 1u) || st_node[j] == v;
         if (df != kInf32 && (uint64_t)df + a.scale == (uint64_t)ds && tr) {
           acc |= 1ull << j;
@@ -2585,14 +2636,15 @@ __device__ __noinline__ void nl_swar_deep(
 // 16-node layout stored 16-byte pieces 128 bytes apart: twice the L2 write
 // requests, profiles/r03e).
 constexpr uint32_t kNsHeldMax = 3;
-constexpr uint32_t kNsHeldThreads = 256; // one block per (source, 1024-node chunk)
+constexpr uint32_t kNsHeldWide = 8; // the held kernel's wide instance (4-8 words)
 
+template <uint32_t T, uint32_t H>
 __device__ __forceinline__ void nl_swar_held(
     const NhLevelsArgs& a, const uint8_t* lvl, uint32_t q, uint32_t c, uint32_t Wm, uint32_t n,
     uint32_t beg, uint64_t* nhrow, const uint8_t* lvl_s, uint32_t* st_row, uint32_t* st_node,
     uint32_t* st_nt) {
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  for (uint32_t t = threadIdx.x; t < 64 * kNsHeldMax; t += kNsHeldThreads) {
+  for (uint32_t t = threadIdx.x; t < 64 * H; t += T) {
     bool nt = false;
     if (t < n) {
       const uint32_t f = a.nbrs[beg + t];
@@ -2609,7 +2661,7 @@ __device__ __forceinline__ void nl_swar_held(
   __syncthreads();
   {
     {
-      const uint32_t v0 = c * kNsChunk + wv * 256 + 4 * lane;
+      const uint32_t v0 = c * (4 * T) + wv * 256 + 4 * lane;
       if (v0 >= a.V) {
         return;
       }
@@ -2617,7 +2669,10 @@ __device__ __forceinline__ void nl_swar_held(
       const uint32_t tgt = ((ls | 0x80808080u) - 0x01010101u) ^ (~ls & 0x80808080u);
       const uint32_t live =
           0x80808080u & ~(swar_zero_bytes(ls) | swar_zero_bytes(~ls));
-      uint64_t held[kNsHeldMax][4];
+      if (a.dist_w) {
+        nl_dist_from_levels(a, q, v0, ls);
+      }
+      uint64_t held[H][4];
 #pragma unroll 1
       for (uint32_t w = 0; w < Wm; ++w) {
         {
@@ -2658,7 +2713,7 @@ __device__ __forceinline__ void nl_swar_held(
           swar_transpose4(P[0], P[1], P[2], P[3], lo);
           swar_transpose4(P[4], P[5], P[6], P[7], hi);
 #pragma unroll
-          for (uint32_t ww = 0; ww < kNsHeldMax; ++ww) {
+          for (uint32_t ww = 0; ww < H; ++ww) {
             if (ww == w) { // static register indices
 #pragma unroll
               for (int i = 0; i < 4; ++i) {
@@ -2669,7 +2724,7 @@ __device__ __forceinline__ void nl_swar_held(
         }
       }
       // node-major: node v0 + i, word w at (v0 + i) * Wm + w
-      if (v0 + 4 <= a.V) {
+      if (H <= 3 && v0 + 4 <= a.V) {
         ulonglong2* o = reinterpret_cast<ulonglong2*>(nhrow + (size_t)v0 * Wm);
         if (Wm == 1) {
           o[0] = make_ulonglong2(held[0][0], held[0][1]);
@@ -2692,7 +2747,7 @@ __device__ __forceinline__ void nl_swar_held(
         for (uint32_t i = 0; i < 4; ++i) {
           if (v0 + i < a.V) {
 #pragma unroll
-            for (uint32_t w = 0; w < kNsHeldMax; ++w) {
+            for (uint32_t w = 0; w < H; ++w) {
               if (w < Wm) {
                 nhrow[(size_t)(v0 + i) * Wm + w] = held[w][i];
               }
@@ -2762,6 +2817,12 @@ void spf_nh_levels_swar_kernel(NhLevelsArgs a, const uint32_t* big, uint32_t nbi
         ls = *reinterpret_cast<const uint4*>(lvl_s + v0);
       }
       const uint32_t lsw[4] = {ls.x, ls.y, ls.z, ls.w};
+      if (a.dist_w && w == 0 && active) {
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+          nl_dist_from_levels(a, q, v0 + 4 * k, lsw[k]);
+        }
+      }
       uint32_t tgt[4], live[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -2845,24 +2906,30 @@ void spf_nh_levels_swar_kernel(NhLevelsArgs a, const uint32_t* big, uint32_t nbi
 
 // Sources with at most kNsHeldMax mask words (all of the fabric's), unless the
 // BFS went deeper than 254 levels (then spf_nh_levels_swar_kernel takes all).
-__global__ __launch_bounds__(kNsHeldThreads) void spf_nh_levels_held_kernel(NhLevelsArgs a) {
-  __shared__ uint32_t st_row[kNsHeldMax * 64];
-  __shared__ uint32_t st_node[kNsHeldMax * 64];
-  __shared__ uint32_t st_nt[2 * kNsHeldMax];
+// T threads per block, one block per (source, 4T-node chunk).  H = 3: the
+// sources with at most 3 mask words (all of the 10k fabric's); H = 8: the
+// sources with 4-8 words, listed in big[0, nmid) (a 20k fabric's SSWs)
+template <uint32_t T, uint32_t H>
+__global__ __launch_bounds__(T) void spf_nh_levels_held_kernel(
+    NhLevelsArgs a, const uint32_t* big, uint32_t nmid) {
+  __shared__ uint32_t st_row[H * 64];
+  __shared__ uint32_t st_node[H * 64];
+  __shared__ uint32_t st_nt[2 * H];
   // consecutive blocks: consecutive sources at the same chunk (neighbouring
   // name ranks share neighbours, so their row reads meet in L2); with
   // OPENR_NL_XCD=1 consecutive logical blocks also share an XCD
   const uint32_t bid = a.xcd_swizzle ? xcd_logical_block(blockIdx.x, gridDim.x) : blockIdx.x;
-  const uint32_t c = bid / a.nq;
-  const uint32_t q = bid - c * a.nq;
+  const uint32_t nsrc = H <= 3 ? a.nq : nmid;
+  const uint32_t c = bid / nsrc;
+  const uint32_t q = H <= 3 ? bid - c * nsrc : big[bid - c * nsrc];
   const uint32_t Wm = a.nh_w[q];
-  if (a.flags[0] != 0 || Wm > kNsHeldMax) {
+  if (a.flags[0] != 0 || Wm > H || (H > 3 && Wm <= 3)) {
     return;
   }
   const uint32_t s = a.src[q];
   const uint32_t beg = a.nbr_off[s], n = a.nbr_off[s + 1] - beg;
   const uint8_t* lvl = a.lvl + (a.zvar ? a.zvar[q] * a.lvl_vstride : 0);
-  nl_swar_held(a, lvl, q, c, Wm, n, beg, a.nh_out + a.nh_off[q], lvl + (size_t)q * a.Vp8, st_row,
+  nl_swar_held<T, H>(a, lvl, q, c, Wm, n, beg, a.nh_out + a.nh_off[q], lvl + (size_t)q * a.Vp8, st_row,
                st_node, st_nt);
 }
 
@@ -4407,6 +4474,7 @@ struct spf_query {
   uint32_t* d_qctr = nullptr; // dstep source-claim counter
   uint32_t* d_big = nullptr;  // nh_levels: queries with more than kNsHeldMax mask words
   uint32_t nbig = 0;
+  uint32_t nmid = 0;          // the first nmid of them have at most kNsHeldWide words
   // zero-metric plan (spf_zvar_kernel): variant tables, their closure pairs
   // (variant j: pairs [zoff[j], zoff[j+1]) of d_zl, then the links' ends at
   // pair zoff[zvars]), each source's variant, and the wide-plan run of the
@@ -6095,9 +6163,16 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     }
   }
   if (q->dist == DistPlan::MsBfs && q->nh == NhPlan::Levels) {
+    // 4-8 mask words first (the wide held kernel), then the rest (generic)
     std::vector<uint32_t> big;
     for (uint32_t i = 0; i < nq; ++i) {
-      if (q->nh_w[i] > kNsHeldMax) {
+      if (q->nh_w[i] > kNsHeldMax && q->nh_w[i] <= kNsHeldWide) {
+        big.push_back(i);
+      }
+    }
+    q->nmid = (uint32_t)big.size();
+    for (uint32_t i = 0; i < nq; ++i) {
+      if (q->nh_w[i] > kNsHeldWide) {
         big.push_back(i);
       }
     }
@@ -6451,6 +6526,17 @@ int launch_nh_rows(spf_query* q, bool unit) {
   return SPF_OK;
 }
 
+// distances below level 255 written by the next-hop pass from the level
+// rows (OPENR_MS_LVL_ONLY=0: by the BFS).  The BFS stores one 4-byte
+// distance per (source, node) bit as it appears, scattered over 64 rows;
+// the next-hop pass already reads each source's level row in order and
+// writes them as 16-byte runs: fabric msbfs 0.228 -> 0.155 ms, next hops
+// 0.451 -> 0.499 ms, step 0.691 -> 0.666 ms (profiles/r03w)
+inline bool lvl_only(const spf_query* q) {
+  return q->nh == NhPlan::Levels && !q->zvars && env_flag("OPENR_NL_SWAR", 1) &&
+         env_flag("OPENR_MS_LVL_ONLY", 1);
+}
+
 int launch_msbfs(spf_query* q, bool unit) {
   spf_graph* g = q->g;
   MsBfsArgs a;
@@ -6472,6 +6558,7 @@ int launch_msbfs(spf_query* q, bool unit) {
   a.wrec = env_flag("OPENR_MS_WREC", 0); // measured slower (0.212 -> 0.232 ms, profiles/r03g)
   a.zlist = nullptr;
   a.nz = 0;
+  a.lvl_only = lvl_only(q) ? 1u : 0u;
   HIP_TRY(hipMemsetAsync(q->d_flags, 0, 16, g->stream));
   const uint32_t K = (g->V + kMsThreads - 1) / kMsThreads;
   const void* kern = nullptr;
@@ -6567,6 +6654,7 @@ int launch_nh_levels(spf_query* q, bool unit) {
   a.zvar = q->d_zvar;
   a.lvl_vstride = (uint64_t)q->nrows * q->Vp8;
   a.dist_vstride = (uint64_t)q->nrows * q->Vp;
+  a.dist_w = lvl_only(q) ? (uint32_t*)q->d_dist : nullptr;
   const uint32_t nchunks = (g->V + kNlChunk - 1) / kNlChunk;
   const uint64_t blocks =
       (uint64_t)((nchunks + kNlChunksPerBlock - 1) / kNlChunksPerBlock) * q->nq;
@@ -6576,16 +6664,36 @@ int launch_nh_levels(spf_query* q, bool unit) {
   if (env_flag("OPENR_NL_SWAR", 1) || q->d_zvar) {
     // held kernel: every source with <= kNsHeldMax mask words; the generic
     // byte kernel: the rest (q->d_big), or every source after a deep BFS
-    const uint64_t hblocks = (uint64_t)q->nq * ((g->V + kNsChunk - 1) / kNsChunk);
+    // threads per block (OPENR_NL_HT = 256 / 512 / 1024; chunk = 4 nodes per thread)
+    const uint32_t ht = env_u32("OPENR_NL_HT", 256);
+    const uint32_t T = ht == 1024 ? 1024u : (ht == 512 ? 512u : 256u);
+    const uint64_t hblocks = (uint64_t)q->nq * ((g->V + 4 * T - 1) / (4 * T));
     if (hblocks > 0x7FFFFFFFull) {
       return fail(SPF_E_UNSUPPORTED, "batch too large for the next-hop pass");
     }
-    hipLaunchKernelGGL(spf_nh_levels_held_kernel, dim3((uint32_t)hblocks),
-                       dim3(kNsHeldThreads), 0, g->stream, a);
+    const uint32_t* nolist = nullptr;
+    if (T == 1024) {
+      hipLaunchKernelGGL((spf_nh_levels_held_kernel<1024, kNsHeldMax>), dim3((uint32_t)hblocks),
+                         dim3(1024), 0, g->stream, a, nolist, 0u);
+    } else if (T == 512) {
+      hipLaunchKernelGGL((spf_nh_levels_held_kernel<512, kNsHeldMax>), dim3((uint32_t)hblocks),
+                         dim3(512), 0, g->stream, a, nolist, 0u);
+    } else {
+      hipLaunchKernelGGL((spf_nh_levels_held_kernel<256, kNsHeldMax>), dim3((uint32_t)hblocks),
+                         dim3(256), 0, g->stream, a, nolist, 0u);
+    }
     HIP_TRY(hipGetLastError());
-    const uint32_t grid = std::max<uint32_t>(q->nbig, std::min<uint32_t>(q->nq, 1024));
+    if (q->nmid && env_flag("OPENR_NL_WIDE", 1)) {
+      // sources with 4-8 words: the same per-(source, chunk) pass
+      const uint64_t mblocks = (uint64_t)q->nmid * ((g->V + 1023) / 1024);
+      hipLaunchKernelGGL((spf_nh_levels_held_kernel<256, kNsHeldWide>), dim3((uint32_t)mblocks),
+                         dim3(256), 0, g->stream, a, (const uint32_t*)q->d_big, q->nmid);
+      HIP_TRY(hipGetLastError());
+    }
+    const uint32_t skip = env_flag("OPENR_NL_WIDE", 1) ? q->nmid : 0;
+    const uint32_t grid = std::max<uint32_t>(q->nbig - skip, std::min<uint32_t>(q->nq, 1024));
     hipLaunchKernelGGL(spf_nh_levels_swar_kernel, dim3(grid), dim3(kNsThreads), 0, g->stream,
-                       a, (const uint32_t*)q->d_big, q->nbig);
+                       a, (const uint32_t*)q->d_big + skip, q->nbig - skip);
     HIP_TRY(hipGetLastError());
     return SPF_OK;
   }

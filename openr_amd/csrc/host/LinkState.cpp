@@ -1198,10 +1198,16 @@ bool LinkState::LinkPtrEqual::operator()(
 }
 
 void LinkState::clearKthMemo() const {
+  // the stripes hold one entry per (src, dst, k) a KSP2 build filled (20k on
+  // the fabric): freed on the worker pool, one stripe per task
+  size_t n = 0;
   for (auto& stripe : *kth_) {
-    stripe.ids.clear();
-    stripe.paths.clear();
+    n += stripe.ids.size() + stripe.paths.size();
   }
+  openr::parallelFor(kKthStripes, openr::hostThreads(n, 2048), [&](size_t i, unsigned) {
+    (*kth_)[i].ids.clear();
+    (*kth_)[i].paths.clear();
+  }, 1);
 }
 
 void LinkState::clearMemo() const {

@@ -356,6 +356,7 @@ class ShardedAllSources:
         self._lay_col = np.asarray(csr.col, dtype=np.uint32).copy()
         self._lay_up = np.ones(len(csr.col), dtype=bool)
         self._lay_w = np.asarray(csr.metric, dtype=np.uint64).copy()
+        self._lay_rev = np.asarray(csr.rev, dtype=np.int64).copy()  # the other half of each link
         self._lay_is_csr = csr  # the layout is exactly this CSR's (no link set in place)
 
     def _links_in_place(self, deltas):
@@ -363,37 +364,57 @@ class ShardedAllSources:
         (tail, head, metric), multiset per tail) onto the resident layout:
         a removed half-edge is an up slot (tail, head, metric) going down, an
         added one a down slot (tail, head) coming back up with its metric.
-        None when some added half-edge has no down slot (a new link: rebuild)
-        or a metric is 0 / past 2^31 - 1 (64-bit graphs rebuild too)."""
+        Slots are chosen as LINK PAIRS: the pull kernels read a slot's head
+        together with win[e] = metric of its reverse half rev[e], so both
+        halves of a link must be up or down together.  An added half-edge
+        takes, in order of preference, the slot a removed delta of this same
+        update took down (a metric change), a slot whose other half this pass
+        already brought up, then any down slot; a layout in which some touched
+        slot's halves disagree afterwards (parallel links matched across
+        links) is refused.  None when some added half-edge has no down slot (a
+        new link: rebuild), the halves cannot be paired, or a metric is 0 /
+        past 2^31 - 1 (64-bit graphs rebuild too)."""
         import numpy as np
 
         from openr_amd import abi
 
         SCOPE_NOT_TAIL = 2
-        up0, w0 = self._lay_up, self._lay_w
+        up0, w0, rev = self._lay_up, self._lay_w, self._lay_rev
         touched = {}  # slot -> (up, metric), applied once every delta has mapped
+        removed_here = set()
         order = sorted((d for d in deltas if int(d["scope"]) != SCOPE_NOT_TAIL),
                        key=lambda d: int(d["kind"]) != abi.SPF_DELTA_REMOVED)
+
+        def state(e):
+            t = touched.get(e)
+            return (t[0], t[1]) if t is not None else (bool(up0[e]), int(w0[e]))
+
         for d in order:
             u, v, m, kind = int(d["tail"]), int(d["head"]), int(d["metric"]), int(d["kind"])
             if m == 0 or m > 0x7FFFFFFF:
                 return None
             lo, hi = int(self._lay_row[u]), int(self._lay_row[u + 1])
-            cols = self._lay_col[lo:hi]
-            up = up0[lo:hi].copy()
-            w = w0[lo:hi].copy()
-            for e, (eu, ew) in touched.items():
-                if lo <= e < hi:
-                    up[e - lo], w[e - lo] = eu, ew
-            if kind == abi.SPF_DELTA_REMOVED:
-                cand = np.nonzero((cols == v) & up & (w == np.uint64(m)))[0]
-            else:
-                cand = np.nonzero((cols == v) & ~up)[0]
-            if len(cand) == 0:
-                return None
-            e = lo + int(cand[0])
+            slots = [lo + int(k) for k in np.nonzero(self._lay_col[lo:hi] == v)[0]]
             removed = kind == abi.SPF_DELTA_REMOVED
-            touched[e] = (not removed, int(w[e - lo]) if removed else m)
+            if removed:
+                cand = [e for e in slots if state(e)[0] and state(e)[1] == m]
+            else:
+                down = [e for e in slots if not state(e)[0]]
+                cand = ([e for e in down if e in removed_here]
+                        + [e for e in down if e not in removed_here and int(rev[e]) in touched
+                           and touched[int(rev[e])][0]]
+                        + [e for e in down if e not in removed_here])
+            if not cand:
+                return None
+            e = cand[0]
+            if removed:
+                removed_here.add(e)
+                touched[e] = (False, state(e)[1])
+            else:
+                touched[e] = (True, m)
+        for e in list(touched):
+            if state(e)[0] != state(int(rev[e]))[0]:
+                return None  # the halves of a link disagree: rebuild
         e = np.fromiter(touched.keys(), dtype=np.uint32, count=len(touched))
         new_up = np.fromiter((t[0] for t in touched.values()), dtype=bool, count=len(touched))
         new_w = np.fromiter((t[1] for t in touched.values()), dtype=np.uint64, count=len(touched))

@@ -128,6 +128,7 @@ void AllSourcesTable::buildGraphs(const Csr& c) {
   }
   layRow_ = c.row;
   layCol_ = c.col;
+  layRev_ = c.rev;
   layUp_.assign(c.col.size(), 1);
   layW_ = c.metric;
 }
@@ -180,13 +181,20 @@ void AllSourcesTable::recompute() {
 // Link-set deltas onto the resident layout (the C++ form of
 // allsources.ShardedAllSources._links_in_place): a REMOVED half-edge
 // (tail, head, metric) is an up slot going down, an ADDED one a down slot
-// (tail, head) coming back up; false when an added half-edge has no down
-// slot (a new link) or a metric is 0 / wraps.
+// (tail, head) coming back up.  Slots are chosen as LINK PAIRS — the pull
+// kernels read a slot's head with win[e] = the metric of its reverse half
+// rev[e], so both halves of a link must be up or down together: an added
+// half-edge takes the slot a removed delta of this update took down (a
+// metric change), else a slot whose other half this pass brought up, else
+// any down slot, and a result whose touched slots disagree with their
+// reverse halves (parallel links matched across links) is refused.  false:
+// rebuild (a new link, unpairable halves, a metric 0 / past 2^31 - 1).
 bool AllSourcesTable::linksInPlace(
     const std::vector<spf_edge_delta>& deltas, std::vector<uint32_t>& edges,
     std::vector<uint8_t>& up, std::vector<uint64_t>& w) {
   std::vector<uint8_t> lu = layUp_;
   std::vector<uint64_t> lw = layW_;
+  // 1: touched by a REMOVED delta, 2: brought up by an ADDED one
   std::vector<uint8_t> touched(layCol_.size(), 0);
   for (int pass = 0; pass < 2; ++pass) { // REMOVED first (a metric change is both)
     const uint32_t kind = pass == 0 ? SPF_DELTA_REMOVED : SPF_DELTA_ADDED;
@@ -198,13 +206,25 @@ bool AllSourcesTable::linksInPlace(
         return false;
       }
       uint32_t hit = ~0u;
+      int rank = 3;
       for (uint32_t e = layRow_[d.tail]; e < layRow_[d.tail + 1]; ++e) {
         if (layCol_[e] != d.head) {
           continue;
         }
-        if (kind == SPF_DELTA_REMOVED ? (lu[e] && lw[e] == d.metric) : !lu[e]) {
+        if (kind == SPF_DELTA_REMOVED) {
+          if (lu[e] && lw[e] == d.metric) {
+            hit = e;
+            break;
+          }
+          continue;
+        }
+        if (lu[e]) {
+          continue;
+        }
+        const int r = (touched[e] & 1u) ? 0 : ((touched[layRev_[e]] & 2u) && lu[layRev_[e]]) ? 1 : 2;
+        if (r < rank) {
+          rank = r;
           hit = e;
-          break;
         }
       }
       if (hit == ~0u) {
@@ -214,7 +234,7 @@ bool AllSourcesTable::linksInPlace(
       if (kind == SPF_DELTA_ADDED) {
         lw[hit] = d.metric;
       }
-      touched[hit] = 1;
+      touched[hit] |= kind == SPF_DELTA_REMOVED ? 1u : 2u;
     }
   }
   edges.clear();
@@ -222,6 +242,9 @@ bool AllSourcesTable::linksInPlace(
   w.clear();
   for (uint32_t e = 0; e < touched.size(); ++e) {
     if (touched[e]) {
+      if (lu[e] != lu[layRev_[e]]) {
+        return false; // the halves of a link disagree
+      }
       edges.push_back(e);
       up.push_back(lu[e]);
       w.push_back(lw[e]);
@@ -239,6 +262,20 @@ AllSourcesTable::UpdateStats AllSourcesTable::update(const LinkState& ls) {
     throw std::invalid_argument("AllSourcesTable::update: the new topology needs 64-bit rows");
   }
   Csr nc = snapshot(ls);
+  if (stale_) {
+    // a failed update patched the graphs but left the old rows: start over
+    buildGraphs(nc);
+    cur_ = std::move(nc);
+    if (spf_graph_needs_exact(blocks_.front().graph)) {
+      throw std::invalid_argument("AllSourcesTable::update: the new topology needs 64-bit rows");
+    }
+    recompute();
+    stale_ = false;
+    st.affected = (uint32_t)names_.size();
+    st.spfMs = lastSpfMs_;
+    st.wallMs = msSince(t0);
+    return st;
+  }
   const uint32_t V = (uint32_t)names_.size();
   // edge deltas
   std::vector<spf_edge_delta> deltas;
@@ -302,6 +339,7 @@ AllSourcesTable::UpdateStats AllSourcesTable::update(const LinkState& ls) {
   cur_ = std::move(nc);
   st.graphMs = msSince(tg);
   if (spf_graph_needs_exact(blocks_.front().graph)) {
+    stale_ = true;
     throw std::invalid_argument("AllSourcesTable::update: the new topology needs 64-bit rows");
   }
   // screen, then repair (or recompute) the affected rows of each block
@@ -347,6 +385,9 @@ AllSourcesTable::UpdateStats AllSourcesTable::update(const LinkState& ls) {
 }
 
 std::vector<uint32_t> AllSourcesTable::row(const std::string& src) const {
+  if (stale_) {
+    throw std::logic_error("AllSourcesTable::row: the last update() failed, the rows are stale");
+  }
   const auto it = ids_.find(src);
   if (it == ids_.end()) {
     throw std::out_of_range("AllSourcesTable::row: unknown node " + src);

@@ -60,7 +60,9 @@ class AllSourcesTable {
   AllSourcesTable& operator=(const AllSourcesTable&) = delete;
 
   // Bring the rows to `ls`'s current topology (same node set; otherwise
-  // std::invalid_argument: rebuild the table).
+  // std::invalid_argument: rebuild the table).  A topology that needs 64-bit
+  // rows throws std::invalid_argument and leaves the table stale: row()
+  // throws std::logic_error until an update() to a 32-bit topology succeeds.
   UpdateStats update(const LinkState& ls);
   // Recompute every row on the current graphs (device time in lastSpfMs()).
   void recompute();
@@ -101,11 +103,15 @@ class AllSourcesTable {
   Csr cur_;
   // half-edge layout of the resident graphs (heads as created, up flags,
   // current metrics): links taken down / up in place keep their slots
-  std::vector<uint32_t> layRow_, layCol_;
+  std::vector<uint32_t> layRow_, layCol_, layRev_;
   std::vector<uint8_t> layUp_;
   std::vector<uint64_t> layW_;
   std::vector<Block> blocks_;
   double lastSpfMs_{0};
+  // an update() that threw after the graphs were patched (the new topology
+  // needs 64-bit rows) left rows of the old topology: the next update()
+  // rebuilds and recomputes, row() refuses until then
+  bool stale_{false};
 };
 
 } // namespace openr

@@ -747,16 +747,18 @@ std::vector<std::unique_ptr<SpfView>> runBatchCluster(
   check(spf_table_sync(t), "spf_table_sync");
   float cm = 0, gm = 0;
   check(spf_table_elapsed_ms(t, &cm, &gm), "spf_table_elapsed_ms");
-  eng.lastMs = cm + gm;
-  Counters::add("decision.spf_device_us", (int64_t)(eng.lastMs * 1000.0f));
   auto rows32 = std::make_shared<std::vector<uint32_t>>((size_t)nq * V);
   if (const int s = spf_table_fetch_rows(t, 0, nq, rows32->data()); s == SPF_E_UNSUPPORTED) {
-    spf_table_destroy(t); // 64-bit rows in some block: the caller's single-device path
+    // 64-bit rows in some block: the caller's single-device path runs the
+    // batch again and charges its own device time (not this run's)
+    spf_table_destroy(t);
     Counters::add("decision.spf_cluster_fallbacks", 1);
     return {};
   } else {
     check(s, "spf_table_fetch_rows");
   }
+  eng.lastMs = cm + gm;
+  Counters::add("decision.spf_device_us", (int64_t)(eng.lastMs * 1000.0f));
   Counters::add("decision.spf_cluster_batches", 1);
   std::vector<uint32_t> words(nq, 1);
   std::vector<uint64_t> maskOff(nq + 1, 0);

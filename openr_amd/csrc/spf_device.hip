@@ -505,6 +505,9 @@ struct DstepArgs {
   // PK: sources beyond the first gridDim.x are claimed from this counter
   // (zeroed per launch), so the workgroups finish together
   uint32_t* qctr = nullptr;
+  // run only queries qlist[0, *qcount) (nullptr: all nq)
+  const uint32_t* qlist = nullptr;
+  const uint32_t* qcount = nullptr;
 };
 
 
@@ -784,7 +787,11 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
     __syncthreads();
     return ctl[kCtlWords - 2];
   };
-  for (uint32_t q = blockIdx.x; q < a.nq; q = next_query(q)) {
+  // qlist: only the listed queries (*qcount of them, written by an earlier
+  // kernel of the stream: the LDS-row plan's overflows)
+  const uint32_t nqd = da.qcount ? *da.qcount : a.nq;
+  for (uint32_t qq = blockIdx.x; qq < nqd; qq = next_query(qq)) {
+    const uint32_t q = da.qlist ? da.qlist[qq] : qq;
     if (a.skip && a.skip[q]) {
       continue; // uniform per block
     }
@@ -1233,6 +1240,305 @@ __global__ __launch_bounds__(BS) void spf_dstep_kernel(DstepArgs da) {
     for (int k = 0; k < 8; ++k) {
       if (st[k]) {
         atomicAdd(&da.stats[k], (unsigned long long)st[k]);
+      }
+    }
+  }
+}
+
+// ----------------- LDS-resident delta-stepping (distance rows, 12-bit fields)
+//
+// The push-only pass above keeps the distance row in HBM: every relaxation
+// that the LDS bucket byte cannot decide gathers d[v] and improves it with
+// an HBM atomicMin (360k gathers + 278k atomics per SSSP on the 100k WAN,
+// 2.9x the algorithmic bytes).  When every distance a run can hold is small
+// (the WAN: metrics <= 1,000, eccentricity ~1,200) the whole row fits LDS as
+// 12-bit fields, five per 64-bit word (V <= 104k in 160 KB): relaxation is
+// then an LDS read + compare-and-swap, and HBM sees only the CSR stream and
+// one coalesced row store per source.
+//
+// Field value f: the node's tentative distance (0..kDlMaxDist), kDlUnreached
+// = not reached.  Buckets [lo, lo + width) are processed in order:
+//   SCAN   every field in [lo, hi] -> queue (two passes + block scan); none:
+//          jump lo to the smallest field above hi (none: done);
+//   EXPAND queued node u (the source, or a transit node: LinkState.cpp:829-836)
+//          relaxes its packed out-edges: c = f(u) + w; c < f(v) -> CAS the
+//          field down; a node lowered into [lo, hi] is queued again (the
+//          light-edge re-expansion of delta-stepping).  Phases repeat until no
+//          node of the bucket was lowered.
+// Values only decrease and every lowered node of the bucket is expanded
+// after its last drop, so the loop ends at the same fixpoint as runSpf
+// (Dijkstra where only the source or non-overloaded nodes
+// relax).  A relaxation that would store a value above kDlMaxDist into an
+// unreached node flags the source: its row is recomputed by the HBM-row
+// kernel (DstepArgs::qlist), so the plan is exact for any graph.
+constexpr uint32_t kDlUnreached = 0xFFFu;
+constexpr uint32_t kDlMaxDist = 0xFFEu;
+constexpr uint64_t kDlEmptyWord = 0x0FFFFFFFFFFFFFFFull; // five unreached fields
+constexpr uint32_t kDlCtl = 40; // control words after the field image
+
+struct DldsArgs {
+  const uint32_t* row;
+  const uint32_t* cw; // head | metric << cwbits, padded to 16-byte chunks
+  const uint32_t* trbits;
+  const uint32_t* src;
+  uint32_t* dist_out;  // [nq][Vp]
+  uint32_t* gscratch;  // [grid][2 * V] node queues
+  uint32_t* ovf_list;  // [nq] queries whose values left the 12-bit range
+  uint32_t* ovf_n;     // (count)
+  uint32_t* qctr;      // source-claim counter (zeroed per launch)
+  unsigned long long* stats; // OPENR_SPF_DSTEP_STATS (8 counters) or nullptr
+  uint32_t V, Vp, nq, cwbits, wshift;
+};
+
+__device__ __forceinline__ uint32_t dl_field(uint64_t x, uint32_t k) {
+  return (uint32_t)(x >> (12 * k)) & 0xFFFu;
+}
+
+template <uint32_t BS, uint32_t G>
+__global__ __launch_bounds__(BS) void spf_dlds_kernel(DldsArgs a) {
+  extern __shared__ __align__(16) uint64_t fld[];
+  const uint32_t V = a.V, nw = (V + 4) / 5;
+  uint32_t* ctl = reinterpret_cast<uint32_t*>(fld + nw);
+  // ctl[0..2] appended-node counters (rotating by phase), [3] overflow flag,
+  // [4] claimed query, [8, 8 + 2 * waves) scan scratch
+  uint32_t* scan = ctl + 8;
+  constexpr uint32_t kWv = BS / 64;
+  constexpr uint32_t ngrp = BS / G; // G lanes per expanded node
+  const uint32_t tid = threadIdx.x, lg = tid & (G - 1), grp = tid / G;
+  const uint32_t mask = (1u << a.cwbits) - 1u, width = 1u << a.wshift;
+  uint32_t* qa = a.gscratch + (size_t)blockIdx.x * 2 * V;
+  uint32_t* qb = qa + V;
+  const bool stats = a.stats != nullptr;
+  uint32_t st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  auto ld = [&](uint32_t w) -> uint64_t {
+    return __hip_atomic_load(fld + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+
+  uint32_t q = blockIdx.x;
+  while (q < a.nq) {
+    const uint32_t src = a.src[q];
+    for (uint32_t w = tid; w < nw; w += BS) {
+      fld[w] = kDlEmptyWord;
+    }
+    if (tid < 4) {
+      ctl[tid] = 0;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t w = src / 5, k = src % 5;
+      fld[w] &= ~(0xFFFull << (12 * k));
+    }
+    __syncthreads();
+    uint32_t lo = 0, len = 0, ph = 0;
+    bool rescan = true;
+    uint32_t* qc = qa;
+    uint32_t* qn = qb;
+    for (;;) {
+      const uint32_t hi = min(lo + width - 1u, kDlMaxDist);
+      if (rescan) {
+        // SCAN pass 1: fields in [lo, hi], smallest field above hi
+        uint32_t cnt = 0, mn = kInf32;
+        for (uint32_t w = tid; w < nw; w += BS) {
+          const uint64_t x = fld[w];
+#pragma unroll
+          for (uint32_t k = 0; k < 5; ++k) {
+            const uint32_t f = dl_field(x, k);
+            cnt += f >= lo && f <= hi;
+            if (f > hi && f != kDlUnreached) {
+              mn = min(mn, f);
+            }
+          }
+        }
+        mn = grp_min(mn, 64);
+        if ((tid & 63u) == 0) {
+          scan[kWv + (tid >> 6)] = mn;
+        }
+        uint32_t total;
+        uint32_t off = block_excl_scan<BS>(cnt, scan, &total);
+        if (total == 0) {
+          uint32_t m = kInf32;
+#pragma unroll
+          for (uint32_t i = 0; i < kWv; ++i) {
+            m = min(m, scan[kWv + i]);
+          }
+          __syncthreads(); // scan scratch reused by the next pass
+          if (m == kInf32) {
+            break;
+          }
+          lo = m & ~(width - 1u);
+          continue;
+        }
+        // SCAN pass 2: the bucket's nodes -> qa
+        for (uint32_t w = tid; w < nw; w += BS) {
+          const uint64_t x = fld[w];
+#pragma unroll
+          for (uint32_t k = 0; k < 5; ++k) {
+            const uint32_t f = dl_field(x, k);
+            if (f >= lo && f <= hi) {
+              qa[off++] = 5 * w + k;
+            }
+          }
+        }
+        st[6] += stats && tid == 0;
+        qc = qa;
+        qn = qb;
+        len = total;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+      // EXPAND qc[0, len): a group's next node id and its row range are
+      // loaded while the current node's edges are in flight
+      uint32_t* cnt = ctl + ph;
+      {
+        uint32_t i = grp;
+        uint32_t u = i < len ? qc[i] : kInf32;
+        uint32_t nu = i + ngrp < len ? qc[i + ngrp] : kInf32;
+        uint32_t beg = 0, end = 0, trb = 0;
+        if (u != kInf32) {
+          beg = a.row[u];
+          end = a.row[u + 1];
+          trb = a.trbits[u >> 5];
+        }
+        while (u != kInf32) {
+          const uint32_t nnu = i + 2 * ngrp < len ? qc[i + 2 * ngrp] : kInf32;
+          uint32_t nbeg = 0, nend = 0, ntrb = 0;
+          if (nu != kInf32) {
+            nbeg = a.row[nu];
+            nend = a.row[nu + 1];
+            ntrb = a.trbits[nu >> 5];
+          }
+          // the source, or a transit node (overloaded: recorded, never transited)
+          if (u == src || ((trb >> (u & 31)) & 1u)) {
+            const uint32_t du = dl_field(ld(u / 5), u % 5);
+            if (stats && lg == 0) {
+              st[0] += 1;
+              st[1] += end - beg;
+            }
+            for (uint32_t kc = (beg >> 2) + lg; 4 * kc < end; kc += 2 * G) {
+              uint32_t v[8], c[8];
+#pragma unroll
+              for (uint32_t h = 0; h < 2; ++h) {
+                const uint32_t kk = kc + h * G;
+                const uint4 x = 4 * kk < end ? reinterpret_cast<const uint4*>(a.cw)[kk]
+                                             : make_uint4(0, 0, 0, 0);
+                const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                  const uint32_t e = 4 * kk + j;
+                  const bool ok = e >= beg && e < end;
+                  v[4 * h + j] = ok ? (xs[j] & mask) : kInf32;
+                  c[4 * h + j] = du + (xs[j] >> a.cwbits);
+                }
+              }
+              uint64_t old[8];
+#pragma unroll
+              for (uint32_t j = 0; j < 8; ++j) {
+                old[j] = v[j] != kInf32 ? ld(v[j] / 5) : 0ull;
+              }
+#pragma unroll
+              for (uint32_t j = 0; j < 8; ++j) {
+                if (v[j] == kInf32) {
+                  continue;
+                }
+                const uint32_t w = v[j] / 5, sh = 12 * (v[j] % 5);
+                uint64_t o = old[j];
+                uint32_t cur = (uint32_t)(o >> sh) & 0xFFFu;
+                if (c[j] >= cur) {
+                  continue;
+                }
+                if (c[j] > kDlMaxDist) {
+                  ctl[3] = 1; // cur is kDlUnreached: the value does not fit
+                  continue;
+                }
+                bool done = false;
+                while (!done && c[j] < cur) {
+                  const uint64_t nv = (o & ~(0xFFFull << sh)) | ((uint64_t)c[j] << sh);
+                  const uint64_t p = atomicCAS((unsigned long long*)(fld + w),
+                                               (unsigned long long)o, (unsigned long long)nv);
+                  done = p == o;
+                  o = p;
+                  cur = (uint32_t)(o >> sh) & 0xFFFu;
+                }
+                st[4] += stats;
+                if (done) {
+                  st[5] += stats;
+                  if (c[j] <= hi) {
+                    // lowered into the bucket: expanded again next phase (a
+                    // full queue drops the id; the bucket is rescanned then)
+                    const uint32_t slot = atomicAdd(cnt, 1u);
+                    if (slot < V) {
+                      qn[slot] = v[j];
+                    }
+                  }
+                }
+              }
+            }
+          }
+          i += ngrp;
+          u = nu;
+          nu = nnu;
+          beg = nbeg;
+          end = nend;
+          trb = ntrb;
+        }
+      }
+      // the next phase's counter was last read two phases ago (before the
+      // previous phase's barrier): clear it for the next phase
+      const uint32_t ph2 = ph == 2 ? 0u : ph + 1u;
+      if (tid == 0) {
+        ctl[ph2] = 0;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const uint32_t n = *cnt;
+      ph = ph2;
+      st[7] += stats && tid == 0 ? n : 0u;
+      if (n == 0) {
+        // bucket settled
+        if (hi >= kDlMaxDist) {
+          break;
+        }
+        lo = hi + 1;
+        rescan = true;
+      } else if (n > V) {
+        rescan = true; // queue overflowed: the whole bucket again
+      } else {
+        uint32_t* t = qc;
+        qc = qn;
+        qn = t;
+        len = n;
+        rescan = false;
+      }
+    }
+    // the row: 16-byte stores of four nodes per lane
+    uint32_t* drow = a.dist_out + (size_t)q * a.Vp;
+    for (uint32_t v0 = 4 * tid; v0 < V; v0 += 4 * BS) {
+      uint32_t r[4];
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t v = v0 + j;
+        const uint32_t f = v < V ? dl_field(fld[v / 5], v % 5) : kDlUnreached;
+        r[j] = f == kDlUnreached ? kInf32 : f;
+      }
+      *reinterpret_cast<uint4*>(drow + v0) = make_uint4(r[0], r[1], r[2], r[3]);
+    }
+    __syncthreads(); // every lane read the fields and the overflow flag
+    if (tid == 0) {
+      if (ctl[3]) {
+        a.ovf_list[atomicAdd(a.ovf_n, 1u)] = q;
+      }
+      ctl[4] = gridDim.x + atomicAdd(a.qctr, 1u);
+    }
+    __syncthreads();
+    q = ctl[4];
+    __syncthreads();
+  }
+  if (stats) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (st[k]) {
+        atomicAdd(&a.stats[k], (unsigned long long)st[k]);
       }
     }
   }
@@ -4447,6 +4753,12 @@ struct spf_query {
   uint32_t dstep_fshift = 5; // bucket-byte resolution (dstep_tune)
   uint32_t dstep_noret = 0;  // relaxation mode bits (dstep_tune)
   uint32_t dstep_pack = 0;   // packed out-edges: 0 off, 1 scalar, 2 vector
+  // LDS-resident rows (spf_dlds_kernel) first, the HBM-row pass only for the
+  // sources whose values left the 12-bit range
+  bool dlds = false;
+  uint32_t dlds_shift = 4, dlds_grid = 0;
+  size_t dlds_lds = 0;
+  uint32_t* d_ovf = nullptr; // [0] overflow count, [1] claim counter, [2..] list
   uint32_t ign_cap = 0, grid = 0, Vp = 0, Vp8 = 0;
   uint8_t* d_lvl = nullptr;
   uint32_t* d_flags = nullptr;
@@ -4673,7 +4985,8 @@ void free_query(spf_query* q) {
         (void*)q->d_lvl, (void*)q->d_flags, (void*)q->d_perm,
         (void*)q->d_slab, (void*)q->d_msd, (void*)q->d_base_of,
         (void*)q->d_skip, (void*)q->d_key, (void*)q->d_qctr, (void*)q->d_scatter,
-        (void*)q->d_trace, (void*)q->d_big, (void*)q->d_zl, (void*)q->d_zvar}) {
+        (void*)q->d_trace, (void*)q->d_big, (void*)q->d_zl, (void*)q->d_zvar,
+        (void*)q->d_ovf}) {
     pool_free(p);
   }
   if (q->base) {
@@ -6001,6 +6314,21 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
         per_cu = std::max<uint32_t>(1, std::min<uint32_t>(per_cu, (uint32_t)atoi(pc)));
       }
       q->grid = std::min<uint32_t>(std::max<uint32_t>(nq, 1), (uint32_t)g->num_cus * per_cu);
+      // distance rows whose every value fits 12 bits (metrics <= 4,094; the
+      // kernel flags a source whose values do not, and the pass above redoes
+      // only those): the row lives in LDS (OPENR_SPF_DSTEP_LDSROW=0 disables)
+      const size_t dl_lds = (size_t)((V + 4) / 5) * 8 + kDlCtl * 4;
+      q->dlds = !want_nh && !has_ign && g->cw_bits && g->maxw <= kDlMaxDist &&
+                dl_lds <= kLdsLimit && env_flag("OPENR_SPF_DSTEP_LDSROW", 1);
+      if (q->dlds) {
+        q->dlds_lds = dl_lds;
+        q->dlds_grid = std::min<uint32_t>(std::max<uint32_t>(nq, 1), (uint32_t)g->num_cus);
+        // bucket width: the delta-stepping Delta (mean metric / mean degree)
+        q->dlds_shift = dstep_bucket_shift(g, true);
+        if (const char* env = getenv("OPENR_SPF_DSTEP_LSHIFT")) {
+          q->dlds_shift = (uint32_t)std::min(11, std::max(0, atoi(env)));
+        }
+      }
     } else if (ctl <= kLdsLimit) {
       q->dist = bfs ? DistPlan::BfsGmem : DistPlan::SsspGmem;
       q->lds_bytes = ctl;
@@ -6202,9 +6530,13 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
   }
   if ((q->dist == DistPlan::SsspGmem || q->dist == DistPlan::BfsGmem ||
        q->dist == DistPlan::Dstep) &&
-      pool_malloc((void**)&q->d_scratch, (size_t)q->grid * V * 4) !=
-          hipSuccess) {
+      pool_malloc((void**)&q->d_scratch,
+                  std::max<size_t>((size_t)q->grid, q->dlds ? 2 * (size_t)q->dlds_grid : 0) * V *
+                      4) != hipSuccess) {
     return bail(fail(SPF_E_NOMEM, "queue scratch"));
+  }
+  if (q->dlds && pool_malloc((void**)&q->d_ovf, ((size_t)nq + 2) * 4) != hipSuccess) {
+    return bail(fail(SPF_E_NOMEM, "overflow list"));
   }
   if (q->dist == DistPlan::MsDstep) {
     const size_t gv = (size_t)q->grid * V;
@@ -6395,6 +6727,11 @@ int launch_dstep_t(spf_query* q) {
       }
     }
   }
+  if (q->dlds) {
+    // after spf_dlds_kernel: only the sources it flagged
+    d.qcount = q->d_ovf;
+    d.qlist = q->d_ovf + 2;
+  }
   const size_t lds = q->lds_bytes;
   HIP_TRY(hipFuncSetAttribute(
       (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -6432,6 +6769,65 @@ int launch_dstep_bs(spf_query* q) {
   default:
     return ign ? launch_dstep_t<16, true, BS>(q) : launch_dstep_t<16, false, BS>(q);
   }
+}
+
+int launch_dlds(spf_query* q) {
+  spf_graph* g = q->g;
+  DldsArgs a{};
+  a.row = g->d_row;
+  a.cw = g->d_cw;
+  a.trbits = g->d_tr;
+  a.src = q->d_src;
+  a.dist_out = (uint32_t*)q->d_dist;
+  a.gscratch = q->d_scratch;
+  a.ovf_n = q->d_ovf;
+  a.qctr = q->d_ovf + 1;
+  a.ovf_list = q->d_ovf + 2;
+  a.V = g->V;
+  a.Vp = q->Vp;
+  a.nq = q->nq;
+  a.cwbits = g->cw_bits;
+  a.wshift = q->dlds_shift;
+  if (!g->d_cw || !g->cw_bits) {
+    return fail(SPF_E_INVALID, "internal: LDS-row plan without packed edges");
+  }
+  HIP_TRY(hipMemsetAsync(q->d_ovf, 0, 8, g->stream));
+  const char* st_env = getenv("OPENR_SPF_DSTEP_STATS");
+  if (st_env && atoi(st_env) == 1) {
+    HIP_TRY(hipMalloc((void**)&a.stats, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemsetAsync(a.stats, 0, 8 * sizeof(unsigned long long), g->stream));
+  }
+  auto kern = spf_dlds_kernel<1024, 4>;
+  switch (env_u32("OPENR_SPF_DSTEP_LG", 4)) {
+  case 1:
+    kern = spf_dlds_kernel<1024, 1>;
+    break;
+  case 2:
+    kern = spf_dlds_kernel<1024, 2>;
+    break;
+  case 8:
+    kern = spf_dlds_kernel<1024, 8>;
+    break;
+  default:
+    break;
+  }
+  HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)q->dlds_lds));
+  hipLaunchKernelGGL(kern, dim3(q->dlds_grid), dim3(1024), q->dlds_lds, g->stream, a);
+  HIP_TRY(hipGetLastError());
+  if (a.stats) {
+    unsigned long long h[8];
+    uint32_t novf = 0;
+    HIP_TRY(hipStreamSynchronize(g->stream));
+    HIP_TRY(hipMemcpy(h, a.stats, sizeof(h), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&novf, q->d_ovf, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipFree(a.stats));
+    fprintf(stderr,
+            "[dlds stats] nq=%u expand=%llu edges=%llu improving=%llu lowered=%llu "
+            "buckets=%llu requeued=%llu overflowed=%u\n",
+            q->nq, h[0], h[1], h[4], h[5], h[6], h[7], novf);
+  }
+  return SPF_OK;
 }
 
 // 1024-thread workgroups: one per CU with the LDS bucket image (2 when the
@@ -6882,8 +7278,10 @@ int run_plan(spf_query* q) {
     return launch_exact(q);
   case DistPlan::Wide:
     return launch_wide(q);
-  case DistPlan::Dstep:
-    return launch_dstep(q);
+  case DistPlan::Dstep: {
+    int s = q->dlds ? launch_dlds(q) : SPF_OK;
+    return s == SPF_OK ? launch_dstep(q) : s;
+  }
   case DistPlan::MsDstep:
     return launch_msdstep(q);
   case DistPlan::MsBfs: {
@@ -7046,7 +7444,7 @@ const char* spf_query_kernel_name(const spf_query* q) {
     }
     return q->nh == NhPlan::Levels ? "msbfs+levels" : "msbfs";
   case DistPlan::Dstep:
-    return "dstep";
+    return q->dlds ? "dstep-ldsrow" : "dstep";
   case DistPlan::MsDstep:
     return "msdstep";
   case DistPlan::Wide:
@@ -7626,6 +8024,11 @@ int spf_table_nexthops(
   }
   if (g->exact) {
     return fail(SPF_E_UNSUPPORTED, "64-bit rows");
+  }
+  if (g->links_patched) {
+    // the distinct-neighbour lists / cheapest metrics still describe the
+    // links before spf_graph_set_edges (as spf_query_create refuses)
+    return fail(SPF_E_UNSUPPORTED, "next hops on a graph whose links were set in place");
   }
   if (pitch < g->V || pitch > 0xFFFFFFFFull) {
     return fail(SPF_E_INVALID, "pitch");

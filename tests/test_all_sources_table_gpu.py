@@ -85,3 +85,78 @@ def test_all_sources_table_under_churn(mods, seed):
     # a full recompute on the patched graphs gives the same rows
     t.recompute()
     _check_rows(E, O, t, ea, oa)
+
+
+def _parallel_net():
+    """Ring n0..n9 (asymmetric metrics) plus THREE parallel links n0 - n1
+    (ifnames p0..p2, asymmetric metrics), so slots of one (tail, head) can be
+    matched across links."""
+    names = [f"n{i}" for i in range(10)]
+    adj = {n: [] for n in names}
+    k = 0
+
+    def link(a, b, wab, wba, tag):
+        nonlocal k
+        k += 1
+        adj[a].append(T.createAdjacency(b, f"{tag}_{a}", f"{tag}_{b}", f"fe80::{k}:1", "10.0.0.1", wab, 0))
+        adj[b].append(T.createAdjacency(a, f"{tag}_{b}", f"{tag}_{a}", f"fe80::{k}:2", "10.0.0.2", wba, 0))
+
+    for i in range(10):
+        link(names[i], names[(i + 1) % 10], 4 + i % 3, 5 + i % 2, f"r{i}")
+    for j, (wab, wba) in enumerate(((3, 9), (6, 2), (8, 8))):
+        link("n0", "n1", wab, wba, f"p{j}")
+    link("n3", "n7", 2, 3, "c")
+    return {"0": [T.createAdjDb(n, adj[n], 0, False, "0") for n in names]}
+
+
+def test_all_sources_table_parallel_link_flaps(mods):
+    """parallel links taken down / brought back / re-metered one
+    way while a sibling is down must keep both halves of every link on the
+    same slots (the pull kernels read win[e] = metric of rev[e]); every step
+    equals the oracle, and the graph stays patched in place when the halves
+    can be paired."""
+    E, O = mods
+    adj_dbs = _parallel_net()
+    ea, _ = RZ.load(E, adj_dbs, [], 0)
+    oa, _ = RZ.load(O, adj_dbs, [], 0)
+    t = E.AllSourcesTable(ea, "0")
+    _check_rows(E, O, t, ea, oa)
+    dbs = {d.thisNodeName: copy.deepcopy(d) for d in adj_dbs["0"]}
+
+    def adj_of(node, tag):
+        return next(a for a in dbs[node].adjacencies if a.ifName == f"{tag}_{node}")
+
+    def push(*nodes):
+        for n in nodes:
+            ea["0"].updateAdjacencyDatabase(dbs[n])
+            oa["0"].updateAdjacencyDatabase(dbs[n])
+        st = t.update(ea, "0")
+        _check_rows(E, O, t, ea, oa)
+        return st
+
+    patched = 0
+    # p0 and p1 down (both ends), then p1 back with new metrics on both ends
+    for tag in ("p0", "p1"):
+        adj_of("n0", tag).isOverloaded = True
+        adj_of("n1", tag).isOverloaded = True
+    patched += push("n0", "n1")["graph_patched"]
+    adj_of("n0", "p1").isOverloaded = False
+    adj_of("n1", "p1").isOverloaded = False
+    adj_of("n0", "p1").metric = 1
+    adj_of("n1", "p1").metric = 7
+    patched += push("n1", "n0")["graph_patched"]
+    # one-way metric change on p2 while p0 is still down
+    adj_of("n1", "p2").metric = 1
+    patched += push("n1")["graph_patched"]
+    # p1 down, p0 back up one end at a time
+    adj_of("n0", "p1").isOverloaded = True
+    adj_of("n1", "p1").isOverloaded = True
+    patched += push("n0", "n1")["graph_patched"]
+    adj_of("n1", "p0").isOverloaded = False
+    push("n1")  # still down: only n1 advertises it up
+    adj_of("n0", "p0").isOverloaded = False
+    adj_of("n0", "p0").metric = 2
+    patched += push("n0")["graph_patched"]
+    assert patched >= 3
+    t.recompute()
+    _check_rows(E, O, t, ea, oa)

@@ -97,17 +97,18 @@ def lvl_only():
         os.environ.get("OPENR_NL_SWAR", "1") != "0"
 
 
-def nh_levels_bytes(csr, nbrs, nh_words, level_bytes=1, dist_rows=False):
+def nh_levels_bytes(csr, nbrs, nh_bytes, level_bytes=1, dist_rows=False):
     """Compulsory bytes of one next-hop pass launch: every source's level row
     read once (the rows of a source's neighbours are other sources' rows:
     re-reads, served by L2 / MALL when the kernel is good), every next-hop
-    mask row written once, and with `dist_rows` every source's u32 distance
-    row written once (lvl_only)."""
+    mask row written once in the device layout (nh_bytes per node per source:
+    1 / 2 / 4 bytes up to 8 / 16 / 32 neighbours, else whole u64 words), and
+    with `dist_rows` every source's u32 distance row written once (lvl_only)."""
     import numpy as np
 
     V = csr.num_nodes
-    w = np.asarray(nh_words, dtype=np.int64)
-    return int(V * level_bytes * len(w) + 8 * V * int(w.sum()) + (4 * V * len(w) if dist_rows else 0))
+    b = np.asarray(nh_bytes, dtype=np.int64)
+    return int(V * level_bytes * len(b) + V * int(b.sum()) + (4 * V * len(b) if dist_rows else 0))
 
 
 def msbfs_bytes(csr, nsrc, levels_per_batch, dist_rows=True):
@@ -1462,6 +1463,7 @@ def fabric_single(args, topo, world, rank, local, dist):
     sources = np.arange(csr.num_nodes, dtype=np.uint32)
     q = g.query(sources, abi.SPF_F_NEXTHOPS)
     nh_words = [q.nh_words(i) for i in range(len(sources))]
+    nh_bytes = [q.nh_bytes(i) for i in range(len(sources))]
     for _ in range(args.warmup):
         q.run(sync=False)
     torch.cuda.synchronize()
@@ -1510,7 +1512,7 @@ def fabric_single(args, topo, world, rank, local, dist):
     stages = {}
     lo = kname == "msbfs+levels" and lvl_only()
     if nh_k:
-        b = nh_levels_bytes(csr, nbrs, nh_words, dist_rows=lo) if "levels" in kname else None
+        b = nh_levels_bytes(csr, nbrs, nh_bytes, dist_rows=lo) if "levels" in kname else None
         stages[nh_k] = {"avg_ms": round(n_ms, 4), "algorithmic_bytes": b}
     stages[dist_k] = {
         "avg_ms": round(d_ms, 4),
@@ -1527,7 +1529,7 @@ def fabric_single(args, topo, world, rank, local, dist):
     # compulsory bytes of the step (SURVEY §8(d) restated for
     # the bit-parallel plan): every output written once -- u32 distance row,
     # u8 level row, next-hop mask row per source -- and the CSR read once
-    floor_bytes = int(nsrc * 5 * csr.num_nodes + 8 * csr.num_nodes * int(np.sum(nh_words))
+    floor_bytes = int(nsrc * 5 * csr.num_nodes + csr.num_nodes * int(np.sum(nh_bytes))
                       + 4 * E + 4 * (csr.num_nodes + 1))
 
     # spot-check this run against the oracle restatement (3 sources, rank 0)

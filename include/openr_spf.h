@@ -166,8 +166,19 @@ const char* spf_query_kernel_name(const spf_query* q);
 int spf_query_dist(spf_query* q, uint32_t i, uint64_t* out /*[V]*/);
 /* Words per next-hop mask of query i (ceil(nbrs(src)/64), at least 1). */
 int spf_query_nh_words(const spf_query* q, uint32_t i);
-/* Next-hop masks of query i: out[v*W + w], W = spf_query_nh_words. */
+/* Next-hop masks of query i: out[v*W + w], W = spf_query_nh_words (host
+ * layout: u64 words, whatever the device layout). */
 int spf_query_nexthops(spf_query* q, uint32_t i, uint64_t* out /*[V*W]*/);
+/* Device layout of the next-hop masks (spf_query_device_rows): query i's row
+ * holds spf_query_nh_bytes(q, i) bytes per node, node-major, starting
+ * spf_query_nh_offset bytes into the block.  Bytes per node = 1, 2 or 4 for
+ * a source with at most 8, 16 or 32 distinct neighbours (bit j of that
+ * little-endian integer = the j-th neighbour, spf_graph_nbrs order), else
+ * 8 * nh_words (u64 words).  Rows start 32-byte aligned. */
+#define SPF_NH_BYTES(nbrs) \
+  ((nbrs) <= 8u ? 1u : (nbrs) <= 16u ? 2u : (nbrs) <= 32u ? 4u : 8u * (((nbrs) + 63u) / 64u))
+int spf_query_nh_bytes(const spf_query* q, uint32_t i);
+int spf_query_nh_offset(const spf_query* q, uint32_t i, uint64_t* byte_off);
 /* Settle rank of every node for query i (SPF_F_ORDER): the order in which the
  * reference's DijkstraQ extracts nodes; UINT32_MAX = not reached. */
 int spf_query_order(spf_query* q, uint32_t i, uint32_t* out /*[V]*/);
@@ -179,8 +190,10 @@ int spf_query_order(spf_query* q, uint32_t i, uint32_t* out /*[V]*/);
 int spf_query_order_keys(spf_query* q, uint32_t i, uint64_t* out /*[V]*/);
 /* Device pointers of the result rows (for RCCL gathers): dist rows are
  * uint32 (fast kernels) or uint64 (exact kernel), spf_query_row_stride
- * elements apart (V entries used per row).  Next-hop rows are packed:
- * query i starts at word sum_{j<i} roundup4(V * nh_words(j)). */
+ * elements apart (V entries used per row).  Next-hop rows are packed in the
+ * byte layout of spf_query_nh_bytes: query i starts at byte
+ * sum_{j<i} roundup32(V * nh_bytes(j)); *nh_total_words = the block's size
+ * in 8-byte words. */
 int spf_query_device_rows(
     spf_query* q, void** dist_rows, uint32_t* dist_elem_bytes,
     void** nh_rows, uint64_t* nh_total_words);
@@ -385,12 +398,13 @@ int spf_cluster_info(
 const char* spf_cluster_last_error(void);
 
 /* Host only: the block boundaries (block_first[world + 1]) and, when
- * mask_off is non-NULL, the word offset of every source's next-hop masks in
- * the gathered mask buffer (rank slots of *mask_cap words; within a slot the
- * block's sources back to back, V * nh_words[i] words each rounded up to 4).
- * nh_words may be NULL (one word each). */
+ * mask_off is non-NULL, the BYTE offset of every source's next-hop masks in
+ * the gathered mask buffer (rank slots of *mask_cap bytes; within a slot the
+ * block's sources back to back, V * nh_bytes[i] bytes each rounded up to 32:
+ * the device layout of spf_query_nh_bytes / SPF_NH_BYTES).  nh_bytes may be
+ * NULL (8 bytes = one word each). */
 int spf_table_layout(
-    uint32_t num_sources, uint32_t world, uint32_t num_nodes, const uint32_t* nh_words,
+    uint32_t num_sources, uint32_t world, uint32_t num_nodes, const uint32_t* nh_bytes,
     uint64_t* block_first, uint64_t* mask_off, uint64_t* mask_cap);
 /* One graph per local device from `desc` (desc->device ignored), the local
  * ranks' source blocks as queries.  flags: SPF_F_UNIT_METRIC,
@@ -407,6 +421,8 @@ int spf_table_sync(spf_table* t);
 int spf_table_elapsed_ms(spf_table* t, float* compute_ms, float* gather_ms);
 int spf_table_block(const spf_table* t, uint32_t rank, uint32_t* first, uint32_t* count);
 int spf_table_nh_words(const spf_table* t, uint32_t i);
+/* Device bytes per node of source i's masks in the gathered buffer. */
+int spf_table_nh_bytes(const spf_table* t, uint32_t i);
 /* Rows / masks of sources [first, first+count) to host memory (from the
  * local owner, or from the gathered copy; SPF_E_UNSUPPORTED for another
  * rank's rows without the gather flag).  Masks back to back, V * nh_words(i)
@@ -422,10 +438,10 @@ int spf_table_trace_paths(
     spf_table* t, const uint32_t* dests, uint32_t* path_count, uint32_t* link_count);
 int spf_table_trace_fetch(spf_table* t, uint32_t* links, uint32_t* ends);
 /* Gathered buffers on local device `local`: rows [world * cap][V] uint32
- * (cap = ceil(n / world)), masks [world * mask_cap] uint64; NULL when that
- * gather is off. */
+ * (cap = ceil(n / world)), masks [world * mask_cap] bytes in the layout of
+ * spf_table_layout; NULL when that gather is off. */
 int spf_table_device_buffers(
-    spf_table* t, uint32_t local, void** rows, void** masks, uint64_t* mask_cap_words);
+    spf_table* t, uint32_t local, void** rows, void** masks, uint64_t* mask_cap_bytes);
 int spf_table_kernel_name(spf_table* t, uint32_t local, const char** name);
 
 /* ---- persistent cluster graphs + query tables ----

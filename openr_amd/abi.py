@@ -54,6 +54,8 @@ EXPORTED_SYMBOLS = (
     "spf_query_kernel_name",
     "spf_query_dist",
     "spf_query_nh_words",
+    "spf_query_nh_bytes",
+    "spf_query_nh_offset",
     "spf_query_nexthops",
     "spf_query_order",
     "spf_query_order_keys",
@@ -92,6 +94,7 @@ EXPORTED_SYMBOLS = (
     "spf_table_elapsed_ms",
     "spf_table_block",
     "spf_table_nh_words",
+    "spf_table_nh_bytes",
     "spf_table_fetch_rows",
     "spf_table_fetch_nexthops",
     "spf_table_trace_paths",
@@ -254,6 +257,8 @@ def load():
         "spf_query_kernel_name": (C.c_char_p, [vp]),
         "spf_query_dist": (C.c_int, [vp, u32, pu64]),
         "spf_query_nh_words": (C.c_int, [vp, u32]),
+        "spf_query_nh_bytes": (C.c_int, [vp, u32]),
+        "spf_query_nh_offset": (C.c_int, [vp, u32, pu64]),
         "spf_query_nexthops": (C.c_int, [vp, u32, pu64]),
         "spf_query_order": (C.c_int, [vp, u32, pu32]),
         "spf_query_order_keys": (C.c_int, [vp, u32, pu64]),
@@ -292,6 +297,7 @@ def load():
         "spf_table_elapsed_ms": (C.c_int, [vp, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
         "spf_table_block": (C.c_int, [vp, u32, pu32, pu32]),
         "spf_table_nh_words": (C.c_int, [vp, u32]),
+        "spf_table_nh_bytes": (C.c_int, [vp, u32]),
         "spf_table_fetch_rows": (C.c_int, [vp, u32, u32, pu32]),
         "spf_table_fetch_nexthops": (C.c_int, [vp, u32, u32, pu64]),
         "spf_table_trace_paths": (C.c_int, [vp, pu32, pu32, pu32]),
@@ -601,6 +607,16 @@ class Query:
     def nh_words(self, i: int) -> int:
         return load().spf_query_nh_words(self.h, i)
 
+    def nh_bytes(self, i: int) -> int:
+        """Device bytes per node of query i's masks (SPF_NH_BYTES)."""
+        return load().spf_query_nh_bytes(self.h, i)
+
+    def nh_offset(self, i: int) -> int:
+        """Byte offset of query i's masks in device_rows()' mask block."""
+        o = C.c_uint64()
+        _check(load().spf_query_nh_offset(self.h, i, C.byref(o)), "nh_offset")
+        return o.value
+
     def nexthops(self, i: int) -> np.ndarray:
         W = self.nh_words(i)
         out = np.zeros(self.graph.V * W, dtype=np.uint64)
@@ -701,13 +717,19 @@ def _check_cl(status: int, what: str):
         )
 
 
-def table_layout(n: int, world: int, V: int, nh_words=None):
+def nh_bytes_for(nbrs: int) -> int:
+    """Device bytes per node of a source's next-hop masks (SPF_NH_BYTES)."""
+    return 1 if nbrs <= 8 else 2 if nbrs <= 16 else 4 if nbrs <= 32 else 8 * ((nbrs + 63) // 64)
+
+
+def table_layout(n: int, world: int, V: int, nh_bytes=None):
     """spf_table_layout (host only): (block_first uint64[world+1],
-    mask_off uint64[n], mask_cap words per rank slot)."""
+    mask_off uint64[n] BYTE offsets, mask_cap bytes per rank slot); nh_bytes
+    = device bytes per node of each source's masks (nh_bytes_for)."""
     bf = np.zeros(world + 1, dtype=np.uint64)
     mo = np.zeros(max(n, 1), dtype=np.uint64)
     cap = C.c_uint64()
-    w = None if nh_words is None else np.ascontiguousarray(nh_words, dtype=np.uint32)
+    w = None if nh_bytes is None else np.ascontiguousarray(nh_bytes, dtype=np.uint32)
     _check_cl(load().spf_table_layout(n, world, V, _p(w, C.c_uint32) if w is not None else None,
                                       _p(bf, C.c_uint64), _p(mo, C.c_uint64), C.byref(cap)),
               "spf_table_layout")
@@ -848,6 +870,9 @@ class Table:
 
     def nh_words(self, i: int) -> int:
         return load().spf_table_nh_words(self.h, i)
+
+    def nh_bytes(self, i: int) -> int:
+        return load().spf_table_nh_bytes(self.h, i)
 
     def kernel(self, local: int = 0) -> str:
         n = C.c_char_p()

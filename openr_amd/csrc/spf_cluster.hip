@@ -75,7 +75,7 @@ int cfail(int status, const std::string& what) {
     }                       \
   } while (0)
 
-uint64_t roundup4(uint64_t x) { return (x + 3) & ~3ull; }
+uint64_t roundup32(uint64_t x) { return (x + 31) & ~31ull; }
 
 } // namespace
 
@@ -97,10 +97,11 @@ struct spf_table {
   bool borrowed = false; // graphs belong to an spf_cgraph (not destroyed here)
   uint32_t V = 0, n = 0, flags = 0, cap = 0;
   std::vector<uint32_t> sources;
-  std::vector<uint32_t> words;       // next-hop words per source
+  std::vector<uint32_t> words;       // next-hop words per source (host layout)
+  std::vector<uint32_t> nbytes;      // mask bytes per node per source (device layout)
   std::vector<uint64_t> block_first; // [world + 1] source index boundaries
-  std::vector<uint64_t> mask_off;    // word offset of each source in the gathered masks
-  uint64_t mask_cap = 0;             // words per rank slot of the gathered masks
+  std::vector<uint64_t> mask_off;    // byte offset of each source in the gathered masks
+  uint64_t mask_cap = 0;             // bytes per rank slot of the gathered masks (x32)
   struct Local {
     int device = 0;
     uint32_t rank = 0;
@@ -108,7 +109,7 @@ struct spf_table {
     spf_query* q = nullptr;
     std::vector<uint32_t> ign_off; // this block's ignore offsets, rebased to 0
     uint32_t* rows = nullptr;  // gathered rows [world * cap][V] (GATHER_ROWS)
-    uint64_t* masks = nullptr; // gathered masks [world * mask_cap] (GATHER_NEXTHOPS)
+    uint8_t* masks = nullptr; // gathered masks [world * mask_cap bytes] (GATHER_NEXTHOPS)
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
   };
   std::vector<Local> local;
@@ -123,7 +124,7 @@ extern "C" {
 const char* spf_cluster_last_error(void) { return g_cluster_err.c_str(); }
 
 int spf_table_layout(
-    uint32_t num_sources, uint32_t world, uint32_t num_nodes, const uint32_t* nh_words,
+    uint32_t num_sources, uint32_t world, uint32_t num_nodes, const uint32_t* nh_bytes,
     uint64_t* block_first, uint64_t* mask_off, uint64_t* mask_cap) {
   if (world == 0 || !block_first) {
     return cfail(SPF_E_INVALID, "spf_table_layout: world == 0 or no block_first");
@@ -134,14 +135,15 @@ int spf_table_layout(
   }
   uint64_t cap = 0;
   for (uint32_t r = 0; r < world; ++r) {
-    uint64_t words = 0;
+    uint64_t bytes = 0;
     for (uint64_t i = block_first[r]; i < block_first[r + 1]; ++i) {
       if (mask_off) {
-        mask_off[i] = words; // within the slot; the slot base is added below
+        mask_off[i] = bytes; // within the slot; the slot base is added below
       }
-      words += roundup4((uint64_t)num_nodes * (nh_words ? nh_words[i] : 1));
+      // a query's row: V * nh_bytes rounded up to 32 bytes (spf_query_nh_offset)
+      bytes += roundup32((uint64_t)num_nodes * (nh_bytes ? nh_bytes[i] : 8u));
     }
-    cap = std::max(cap, words);
+    cap = std::max(cap, bytes);
   }
   if (mask_off) {
     for (uint32_t r = 0; r < world; ++r) {
@@ -373,6 +375,7 @@ static int table_init(
   // next-hop words of every source (the gathered mask layout needs all of
   // them; distinct neighbour counts come from the graph, any device)
   t->words.assign(num_sources, 1);
+  t->nbytes.assign(num_sources, 8);
   if (qflags & SPF_F_NEXTHOPS) {
     for (uint32_t i = 0; i < num_sources; ++i) {
       const int nb = spf_graph_num_nbrs(t->local[0].g, sources[i]);
@@ -380,10 +383,11 @@ static int table_init(
         return nb;
       }
       t->words[i] = std::max<uint32_t>(1, ((uint32_t)nb + 63) / 64);
+      t->nbytes[i] = SPF_NH_BYTES((uint32_t)nb);
     }
   }
   t->mask_off.resize(num_sources);
-  CL_TRY(spf_table_layout(num_sources, c->world, V, t->words.data(), t->block_first.data(),
+  CL_TRY(spf_table_layout(num_sources, c->world, V, t->nbytes.data(), t->block_first.data(),
                           t->mask_off.data(), &t->mask_cap));
   for (auto& L : t->local) {
     CL_HIP(hipSetDevice(L.device));
@@ -402,12 +406,23 @@ static int table_init(
         qd.ignore_links = qd_all->ignore_links + ioff[first];
       }
       CL_TRY(spf_query_create(L.g, &qd, &L.q));
+      if (qflags & SPF_F_NEXTHOPS) {
+        // the block's masks land in its slot as one copy: same layout
+        for (uint64_t i = 0; i < count; ++i) {
+          uint64_t o = 0;
+          CL_TRY(spf_query_nh_offset(L.q, (uint32_t)i, &o));
+          if (o + (uint64_t)L.rank * t->mask_cap != t->mask_off[first + i] ||
+              (uint32_t)spf_query_nh_bytes(L.q, (uint32_t)i) != t->nbytes[first + i]) {
+            return cfail(SPF_E_INVALID, "spf_table_create: query mask layout differs from the slot");
+          }
+        }
+      }
     }
     if (flags & SPF_T_GATHER_ROWS) {
       CL_HIP(hipMalloc((void**)&L.rows, (size_t)c->world * t->cap * t->V * sizeof(uint32_t)));
     }
     if (flags & SPF_T_GATHER_NEXTHOPS) {
-      CL_HIP(hipMalloc((void**)&L.masks, (size_t)c->world * t->mask_cap * sizeof(uint64_t)));
+      CL_HIP(hipMalloc((void**)&L.masks, (size_t)c->world * t->mask_cap));
     }
     CL_HIP(hipEventCreate(&L.e0));
     CL_HIP(hipEventCreate(&L.e1));
@@ -495,6 +510,7 @@ int spf_table_run(spf_table* t) {
         CL_TRY(spf_query_device_rows(L.q, &dr, &eb, &nh, &total));
         CL_HIP(hipMemcpyAsync(L.masks + (size_t)L.rank * t->mask_cap, nh,
                               total * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+        // (total * 8 = the query's byte layout, <= mask_cap)
       }
     }
     CL_HIP(hipEventRecord(L.e1, st));
@@ -512,7 +528,7 @@ int spf_table_run(spf_table* t) {
                               c->comms[d], st));
       }
       if (L.masks) {
-        CL_NCCL(ncclAllGather(L.masks + (size_t)L.rank * t->mask_cap, L.masks, t->mask_cap,
+        CL_NCCL(ncclAllGather(L.masks + (size_t)L.rank * t->mask_cap, L.masks, t->mask_cap / 8,
                               ncclUint64, c->comms[d], st));
       }
     }
@@ -577,6 +593,13 @@ int spf_table_nh_words(const spf_table* t, uint32_t i) {
     return cfail(SPF_E_INVALID, "spf_table_nh_words: bad index");
   }
   return (int)t->words[i];
+}
+
+int spf_table_nh_bytes(const spf_table* t, uint32_t i) {
+  if (!t || i >= t->n) {
+    return cfail(SPF_E_INVALID, "spf_table_nh_bytes: bad index");
+  }
+  return (int)t->nbytes[i];
 }
 
 // rank owning source index i
@@ -747,8 +770,21 @@ int spf_table_fetch_nexthops(spf_table* t, uint32_t first, uint32_t count, uint6
       uint64_t o = out;
       for (uint32_t k = i; k < bend; ++k) {
         const size_t w = (size_t)t->V * t->words[k];
-        CL_HIP(hipMemcpy(dst + o, L.masks + t->mask_off[k], w * sizeof(uint64_t),
-                         hipMemcpyDeviceToHost));
+        const uint32_t B = t->nbytes[k];
+        if (B >= 8) {
+          CL_HIP(hipMemcpy(dst + o, L.masks + t->mask_off[k], w * sizeof(uint64_t),
+                           hipMemcpyDeviceToHost));
+        } else {
+          // narrow row: one B-byte integer per node, widened to u64 words
+          std::vector<uint8_t> tmp((size_t)t->V * B);
+          CL_HIP(hipMemcpy(tmp.data(), L.masks + t->mask_off[k], tmp.size(),
+                           hipMemcpyDeviceToHost));
+          for (size_t v = 0; v < t->V; ++v) {
+            uint64_t x = 0;
+            std::memcpy(&x, tmp.data() + v * B, B);
+            dst[o + v] = x;
+          }
+        }
         o += w;
       }
     }
@@ -759,7 +795,7 @@ int spf_table_fetch_nexthops(spf_table* t, uint32_t first, uint32_t count, uint6
 }
 
 int spf_table_device_buffers(
-    spf_table* t, uint32_t local, void** rows, void** masks, uint64_t* mask_cap_words) {
+    spf_table* t, uint32_t local, void** rows, void** masks, uint64_t* mask_cap_bytes) {
   if (!t || local >= t->local.size()) {
     return cfail(SPF_E_INVALID, "spf_table_device_buffers: bad local index");
   }
@@ -769,8 +805,8 @@ int spf_table_device_buffers(
   if (masks) {
     *masks = t->local[local].masks;
   }
-  if (mask_cap_words) {
-    *mask_cap_words = t->mask_cap;
+  if (mask_cap_bytes) {
+    *mask_cap_bytes = t->mask_cap;
   }
   return SPF_OK;
 }

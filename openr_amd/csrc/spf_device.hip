@@ -73,6 +73,11 @@ constexpr uint32_t kHostBlock = 2048;
 constexpr uint32_t kCtlWords = 32;         // qlen + scan scratch (<= 16 waves + 1)
 constexpr size_t kLdsLimit = 160 * 1024;   // gfx950 LDS per CU
 constexpr uint32_t kIgnLdsMax = 2048;      // ignore-list entries staged in LDS
+// internal query flag (never in the ABI): next-hop output rows in the word
+// layout (8 * W bytes per node) whatever the neighbour count, for batches
+// whose rows another query copies into its working buffer (what-if
+// baselines, the zero-metric plan's wide-plan sources)
+constexpr uint32_t kQueryWideMasks = 0x80000000u;
 constexpr uint32_t kNotSeen = 0xFFFFFFFFu; // exact kernel heap states
 constexpr uint32_t kSettled = 0xFFFFFFFEu;
 
@@ -137,6 +142,71 @@ __device__ __forceinline__ bool in_sorted(
     }
   }
   return false;
+}
+
+// ---- next-hop mask rows (byte-strided layout of spf_query results)
+// A query's row holds B bytes per node: B = 1, 2, 4 for sources with at most
+// 8, 16, 32 distinct neighbours (bit j of the byte / short / word = the j-th
+// neighbour), else 8 * W with W = ceil(neighbours / 64) u64 words, node-major
+// (the original layout).  A fabric RSW (8 neighbours) thus writes one byte per
+// node instead of a 64-bit word (nh_bytes_for, include/openr_spf.h).
+__host__ __device__ __forceinline__ uint32_t nh_bytes_for(uint32_t nbrs) {
+  return nbrs <= 8 ? 1u : nbrs <= 16 ? 2u : nbrs <= 32 ? 4u : 8u * ((nbrs + 63) / 64);
+}
+
+// word w of node v's mask (w < W; narrow rows have one word)
+__device__ __forceinline__ uint64_t nh_load(const uint8_t* row, uint32_t B, uint32_t W,
+                                            uint32_t v, uint32_t w) {
+  if (B >= 8) {
+    return reinterpret_cast<const uint64_t*>(row)[(size_t)v * W + w];
+  }
+  if (B == 4) {
+    return reinterpret_cast<const uint32_t*>(row)[v];
+  }
+  if (B == 2) {
+    return reinterpret_cast<const uint16_t*>(row)[v];
+  }
+  return row[v];
+}
+
+__device__ __forceinline__ void nh_store(uint8_t* row, uint32_t B, uint32_t W, uint32_t v,
+                                         uint32_t w, uint64_t x) {
+  if (B >= 8) {
+    reinterpret_cast<uint64_t*>(row)[(size_t)v * W + w] = x;
+  } else if (B == 4) {
+    reinterpret_cast<uint32_t*>(row)[v] = (uint32_t)x;
+  } else if (B == 2) {
+    reinterpret_cast<uint16_t*>(row)[v] = (uint16_t)x;
+  } else {
+    row[v] = (uint8_t)x;
+  }
+}
+
+// single-word masks of nodes v0..v0+3 (v0 % 4 == 0) of a narrow row (B < 8):
+// one 4 / 8 / 16-byte store when all four nodes exist
+__device__ __forceinline__ void nh_store4_narrow(uint8_t* row, uint32_t B, uint32_t v0,
+                                                 uint32_t V, const uint64_t (&x)[4]) {
+  if (v0 + 4 <= V) {
+    if (B == 1) {
+      *reinterpret_cast<uint32_t*>(row + v0) =
+          (uint32_t)(x[0] & 0xFFu) | (uint32_t)(x[1] & 0xFFu) << 8 |
+          (uint32_t)(x[2] & 0xFFu) << 16 | (uint32_t)(x[3] & 0xFFu) << 24;
+    } else if (B == 2) {
+      *reinterpret_cast<uint2*>(row + 2 * (size_t)v0) =
+          make_uint2((uint32_t)(x[0] & 0xFFFFu) | (uint32_t)(x[1] & 0xFFFFu) << 16,
+                     (uint32_t)(x[2] & 0xFFFFu) | (uint32_t)(x[3] & 0xFFFFu) << 16);
+    } else {
+      *reinterpret_cast<uint4*>(row + 4 * (size_t)v0) =
+          make_uint4((uint32_t)x[0], (uint32_t)x[1], (uint32_t)x[2], (uint32_t)x[3]);
+    }
+    return;
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i) {
+    if (v0 + i < V) {
+      nh_store(row, B, 1, v0 + i, 0, x[i]);
+    }
+  }
 }
 
 // Exclusive scan of one value per thread over the workgroup.  `scan` holds
@@ -2422,6 +2492,12 @@ struct NhLevelsArgs {
   const uint64_t* nh_off;
   const uint32_t* nh_w;
   uint64_t* nh_out;
+  // the byte-strided output rows (nh_bytes_for) the SWAR kernels write
+  // directly; the word-layout kernels above write nh_out (a working buffer
+  // narrowed afterwards when the layouts differ)
+  uint8_t* nhb;
+  const uint64_t* nhb_off;
+  const uint32_t* nh_b;
   uint32_t V;
   uint32_t Vp;
   uint32_t Vp8;
@@ -2899,7 +2975,7 @@ __device__ __forceinline__ void nl_dist_from_levels(
 __device__ __noinline__ void nl_swar_deep(
     const NhLevelsArgs& a, const uint32_t* dist, uint32_t q, uint32_t v0, uint32_t w, uint32_t Wm,
     uint32_t cnt, uint64_t ntmask, const uint32_t* st_row, const uint32_t* st_node,
-    uint64_t* nhrow) {
+    uint8_t* nhrow, uint32_t B) {
   for (uint32_t i = 0; i < kNsNodes; ++i) {
     const uint32_t v = v0 + i;
     if (v >= a.V) {
@@ -2929,7 +3005,7 @@ __device__ __noinline__ void nl_swar_deep(
         }
       }
     }
-    nhrow[(size_t)v * Wm + w] = acc;
+    nh_store(nhrow, B, Wm, v, w, acc);
   }
 }
 
@@ -2947,8 +3023,9 @@ constexpr uint32_t kNsHeldWide = 8; // the held kernel's wide instance (4-8 word
 template <uint32_t T, uint32_t H>
 __device__ __forceinline__ void nl_swar_held(
     const NhLevelsArgs& a, const uint8_t* lvl, uint32_t q, uint32_t c, uint32_t Wm, uint32_t n,
-    uint32_t beg, uint64_t* nhrow, const uint8_t* lvl_s, uint32_t* st_row, uint32_t* st_node,
-    uint32_t* st_nt) {
+    uint32_t beg, uint8_t* nhrow_b, uint32_t B, const uint8_t* lvl_s, uint32_t* st_row,
+    uint32_t* st_node, uint32_t* st_nt) {
+  uint64_t* nhrow = reinterpret_cast<uint64_t*>(nhrow_b);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   for (uint32_t t = threadIdx.x; t < 64 * H; t += T) {
     bool nt = false;
@@ -3029,8 +3106,11 @@ __device__ __forceinline__ void nl_swar_held(
           }
         }
       }
-      // node-major: node v0 + i, word w at (v0 + i) * Wm + w
-      if (H <= 3 && v0 + 4 <= a.V) {
+      // node-major: node v0 + i, word w at (v0 + i) * Wm + w; narrow rows
+      // (B < 8 bytes per node, one word) as one 4 / 8 / 16-byte run
+      if (H <= 3 && B < 8) {
+        nh_store4_narrow(nhrow_b, B, v0, a.V, held[0]);
+      } else if (H <= 3 && v0 + 4 <= a.V) {
         ulonglong2* o = reinterpret_cast<ulonglong2*>(nhrow + (size_t)v0 * Wm);
         if (Wm == 1) {
           o[0] = make_ulonglong2(held[0][0], held[0][1]);
@@ -3080,7 +3160,9 @@ void spf_nh_levels_swar_kernel(NhLevelsArgs a, const uint32_t* big, uint32_t nbi
   const uint32_t q = deep ? bi : big[bi];
   const uint32_t s = a.src[q];
   const uint32_t Wm = a.nh_w[q];
-  uint64_t* nhrow = a.nh_out + a.nh_off[q];
+  uint8_t* nhrow_b = a.nhb + a.nhb_off[q];
+  const uint32_t B = a.nh_b[q];
+  uint64_t* nhrow = reinterpret_cast<uint64_t*>(nhrow_b);
   const uint32_t beg = a.nbr_off[s], n = a.nbr_off[s + 1] - beg;
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t nchunks = (a.V + kNsChunk - 1) / kNsChunk;
@@ -3114,7 +3196,7 @@ void spf_nh_levels_swar_kernel(NhLevelsArgs a, const uint32_t* big, uint32_t nbi
     for (uint32_t c = wv; c < nchunks; c += kNsThreads / 64) {
       const uint32_t v0 = c * kNsChunk + lane * kNsNodes;
       if (deep) {
-        nl_swar_deep(a, dist, q, v0, w, Wm, cnt, ntmask, st_row, st_node, nhrow);
+        nl_swar_deep(a, dist, q, v0, w, Wm, cnt, ntmask, st_row, st_node, nhrow_b, B);
         continue;
       }
       const bool active = v0 < a.V;
@@ -3191,7 +3273,11 @@ void spf_nh_levels_swar_kernel(NhLevelsArgs a, const uint32_t* big, uint32_t nbi
         swar_transpose4(P[k][0], P[k][1], P[k][2], P[k][3], lo);
         swar_transpose4(P[k][4], P[k][5], P[k][6], P[k][7], hi);
         const uint32_t vk = v0 + 4u * k;
-        if (Wm == 1 && vk + 4 <= a.V) {
+        if (B < 8) {
+          const uint64_t x4[4] = {((uint64_t)hi[0] << 32) | lo[0], ((uint64_t)hi[1] << 32) | lo[1],
+                                  ((uint64_t)hi[2] << 32) | lo[2], ((uint64_t)hi[3] << 32) | lo[3]};
+          nh_store4_narrow(nhrow_b, B, vk, a.V, x4);
+        } else if (Wm == 1 && vk + 4 <= a.V) {
           ulonglong2* o = reinterpret_cast<ulonglong2*>(nhrow + vk);
           o[0] = make_ulonglong2(((uint64_t)hi[0] << 32) | lo[0], ((uint64_t)hi[1] << 32) | lo[1]);
           o[1] = make_ulonglong2(((uint64_t)hi[2] << 32) | lo[2], ((uint64_t)hi[3] << 32) | lo[3]);
@@ -3235,8 +3321,56 @@ __global__ __launch_bounds__(T) void spf_nh_levels_held_kernel(
   const uint32_t s = a.src[q];
   const uint32_t beg = a.nbr_off[s], n = a.nbr_off[s + 1] - beg;
   const uint8_t* lvl = a.lvl + (a.zvar ? a.zvar[q] * a.lvl_vstride : 0);
-  nl_swar_held<T, H>(a, lvl, q, c, Wm, n, beg, a.nh_out + a.nh_off[q], lvl + (size_t)q * a.Vp8, st_row,
-               st_node, st_nt);
+  nl_swar_held<T, H>(a, lvl, q, c, Wm, n, beg, a.nhb + a.nhb_off[q], a.nh_b[q],
+                     lvl + (size_t)q * a.Vp8, st_row, st_node, st_nt);
+}
+
+// Working word rows -> byte-strided output rows, after a plan whose kernels
+// wrote the word layout (spf_query::narrow): one block per (query, 1,024
+// nodes), four nodes per thread; narrow rows (B < 8) keep the low 8 * B bits
+// of each node's single word, the others are copied word for word.  Per-query
+// offsets / widths from device arrays, or (off == nullptr) the scalars of one
+// row.
+struct NhNarrowArgs {
+  const uint64_t* src;
+  uint8_t* dst;
+  const uint64_t* src_off; // words
+  const uint64_t* dst_off; // bytes
+  const uint32_t* nb;
+  const uint32_t* nw;
+  uint64_t src_off1, dst_off1;
+  uint32_t nb1, nw1;
+  uint32_t V, nq;
+};
+
+__global__ __launch_bounds__(256) void spf_nh_narrow_kernel(NhNarrowArgs a) {
+  const uint32_t nch = (a.V + 1023) / 1024;
+  const uint32_t q = blockIdx.x / nch, c = blockIdx.x - q * nch;
+  if (q >= a.nq) {
+    return;
+  }
+  const bool list = a.src_off != nullptr;
+  const uint64_t* s = a.src + (list ? a.src_off[q] : a.src_off1);
+  uint8_t* d = a.dst + (list ? a.dst_off[q] : a.dst_off1);
+  const uint32_t B = list ? a.nb[q] : a.nb1, W = list ? a.nw[q] : a.nw1;
+  const uint32_t v0 = c * 1024 + 4 * threadIdx.x;
+  if (v0 >= a.V) {
+    return;
+  }
+  if (B < 8) {
+    uint64_t x[4];
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+      x[i] = v0 + i < a.V ? s[v0 + i] : 0ull;
+    }
+    nh_store4_narrow(d, B, v0, a.V, x);
+    return;
+  }
+  uint64_t* dw = reinterpret_cast<uint64_t*>(d);
+  const size_t e1 = (size_t)min(v0 + 4, a.V) * W;
+  for (size_t e = (size_t)v0 * W; e < e1; ++e) {
+    dw[e] = s[e];
+  }
 }
 
 // ------------------------------------------------- zero-metric plan helpers
@@ -4117,8 +4251,9 @@ struct RouteTableArgs {
   const uint32_t* trbits;
   const uint32_t* src;
   const uint32_t* dist; // query rows, stride Vp
-  const uint64_t* nh;
-  const uint64_t* nh_off;
+  const uint8_t* nh;      // byte-strided mask rows (nh_bytes_for)
+  const uint64_t* nh_off; // byte offset of each query's rows
+  const uint32_t* nh_b;   // bytes per node
   const uint32_t* nh_w;
   const uint32_t* ann_off; // [P+1]
   const uint32_t* ann;
@@ -4142,8 +4277,8 @@ __global__ __launch_bounds__(256) void spf_route_table_kernel(RouteTableArgs a) 
   for (uint32_t q = blockIdx.x; q < a.nq; q += gridDim.x) {
     const uint32_t s = a.src[q];
     const uint32_t* d = a.dist + (size_t)q * a.Vp;
-    const uint64_t* nhq = a.nh + a.nh_off[q];
-    const uint32_t W = a.nh_w[q];
+    const uint8_t* nhq = a.nh + a.nh_off[q];
+    const uint32_t W = a.nh_w[q], NB = a.nh_b[q];
     const uint32_t e0 = a.row[s], deg = a.row[s + 1] - e0;
     const uint32_t WL = (deg + 63) / 64;
     uint64_t* lk = a.link_out + a.lk_off[q];
@@ -4213,11 +4348,10 @@ __global__ __launch_bounds__(256) void spf_route_table_kernel(RouteTableArgs a) 
         for (uint32_t i = lo; i < hi; ++i) {
           const uint32_t x = a.ann[i];
           if (d[x] == mn && (!filt || ((a.trbits[x >> 5] >> (x & 31)) & 1u))) {
-            const uint64_t* mx = nhq + (size_t)x * W;
 #pragma unroll
             for (uint32_t k = 0; k < kRtMaskWords; ++k) {
               if (k < W) {
-                m[k] |= mx[k];
+                m[k] |= nh_load(nhq, NB, W, x, k);
               }
             }
           }
@@ -4293,7 +4427,7 @@ __global__ __launch_bounds__(256) void spf_route_table_kernel(RouteTableArgs a) 
           for (uint32_t i = lo; i < hi && !mm; ++i) {
             const uint32_t x = a.ann[i];
             if (d[x] == mn && (!filt || ((a.trbits[x >> 5] >> (x & 31)) & 1u))) {
-              mm = (nhq[(size_t)x * W + (sl >> 6)] >> (sl & 63)) & 1ull;
+              mm = (nh_load(nhq, NB, W, x, sl >> 6) >> (sl & 63)) & 1ull;
             }
           }
           out |= mm << (j & 63);
@@ -4764,9 +4898,26 @@ struct spf_query {
   uint32_t* d_flags = nullptr;
   size_t lds_bytes = 0;
   bool has_ign = false;
+  // next-hop masks.  Working layout (u64 words, nh_w[i] per node, query i at
+  // word nh_off[i], nh_total words in d_nh): what the SSSP / rows / wide /
+  // exact kernels read and write.  Output layout (byte-strided, nh_b[i] =
+  // nh_bytes_for(neighbours) bytes per node, query i at byte nhb_off[i],
+  // nhb_total bytes in d_nhb): what the ABI hands out.  The two coincide
+  // (d_nhb aliases d_nh) unless some source has at most 32 neighbours
+  // (`narrow`); then the SWAR next-hop kernels write d_nhb directly
+  // (`nh_direct`, no working buffer) and every other plan is narrowed by
+  // spf_nh_narrow_kernel after it ran.
   std::vector<uint64_t> nh_off;
   std::vector<uint32_t> nh_w;
   uint64_t nh_total = 0;
+  std::vector<uint64_t> nhb_off;
+  std::vector<uint32_t> nh_b;
+  uint64_t nhb_total = 0;
+  bool narrow = false, nh_direct = false;
+  bool nl_swar = true; // the byte-SIMD next-hop kernels (OPENR_NL_SWAR, read at creation)
+  uint8_t* d_nhb = nullptr;
+  uint64_t* d_nhb_off = nullptr;
+  uint32_t* d_nh_b = nullptr;
   uint32_t *d_src = nullptr, *d_ign_off = nullptr, *d_ign = nullptr,
            *d_nh_w = nullptr, *d_order = nullptr, *d_scratch = nullptr;
   int32_t* d_row_of = nullptr;
@@ -4928,6 +5079,16 @@ void ev_put(hipEvent_t e) {
   (void)hipEventDestroy(e);
 }
 
+// host copy of a narrow mask row (B = 1, 2, 4 bytes per node) as one u64
+// word per node (the ABI's host layout)
+void widen_masks(const uint8_t* src, size_t B, size_t V, uint64_t* out) {
+  for (size_t v = 0; v < V; ++v) {
+    uint64_t x = 0;
+    std::memcpy(&x, src + v * B, B); // little-endian: the low bytes of the word
+    out[v] = x;
+  }
+}
+
 template <typename T>
 int dev_upload_q(T** dst, const T* src, size_t n) {
   *dst = nullptr;
@@ -4986,7 +5147,7 @@ void free_query(spf_query* q) {
         (void*)q->d_slab, (void*)q->d_msd, (void*)q->d_base_of,
         (void*)q->d_skip, (void*)q->d_key, (void*)q->d_qctr, (void*)q->d_scatter,
         (void*)q->d_trace, (void*)q->d_big, (void*)q->d_zl, (void*)q->d_zvar,
-        (void*)q->d_ovf}) {
+        (void*)q->d_ovf, q->narrow ? (void*)q->d_nhb : nullptr}) {
     pool_free(p);
   }
   if (q->base) {
@@ -6148,22 +6309,32 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
                      "(spf_graph_set_edges): rebuild the graph"));
   }
 
-  // next-hop mask geometry
+  // next-hop mask geometry: the working word layout and the byte-strided
+  // output layout (kQueryWideMasks: output = working, for internal batches
+  // whose rows are copied into another query's working buffer)
   uint32_t maxw = 0;
   q->nh_off.assign(nq, 0);
   q->nh_w.assign(nq, 0);
+  q->nhb_off.assign(nq, 0);
+  q->nh_b.assign(nq, 0);
   if (want_nh) {
-    uint64_t off = 0;
+    uint64_t off = 0, boff = 0;
     for (uint32_t i = 0; i < nq; ++i) {
       const uint32_t s = desc->sources[i];
       const uint32_t nn = g->nbr_off[s + 1] - g->nbr_off[s];
       const uint32_t w = std::max<uint32_t>(1, (nn + 63) / 64);
+      const uint32_t b = (desc->flags & kQueryWideMasks) ? 8 * w : nh_bytes_for(nn);
       q->nh_off[i] = off;
       q->nh_w[i] = w;
       off += ((uint64_t)w * V + 3) & ~3ull; // 32-byte aligned rows
+      q->nhb_off[i] = boff;
+      q->nh_b[i] = b;
+      boff += ((uint64_t)b * V + 31) & ~31ull;
+      q->narrow = q->narrow || b < 8;
       maxw = std::max(maxw, w);
     }
     q->nh_total = off;
+    q->nhb_total = boff;
   }
 
   // ---- plan: which kernels compute this batch
@@ -6420,7 +6591,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
         spf_query_desc fd{};
         fd.num_queries = (uint32_t)fix.size();
         fd.sources = fix.data();
-        fd.flags = SPF_F_NEXTHOPS;
+        fd.flags = SPF_F_NEXTHOPS | kQueryWideMasks;
         int fs = spf_query_create(g, &fd, &q->zfix);
         if (fs != SPF_OK) {
           return bail(fs);
@@ -6453,6 +6624,8 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     const size_t o_ign = has_ign ? seg((size_t)total_ign * 4) : 0;
     const size_t o_nhoff = want_nh ? seg((size_t)nq * 8) : 0;
     const size_t o_nhw = want_nh ? seg((size_t)nq * 4) : 0;
+    const size_t o_nhboff = want_nh ? seg((size_t)nq * 8) : 0;
+    const size_t o_nhb = want_nh ? seg((size_t)nq * 4) : 0;
     const size_t o_rowof = !row_of.empty() ? seg((size_t)V * 4) : 0;
     if (off) {
       std::vector<uint8_t> host(off, 0);
@@ -6467,6 +6640,8 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       if (want_nh) {
         std::memcpy(host.data() + o_nhoff, q->nh_off.data(), (size_t)nq * 8);
         std::memcpy(host.data() + o_nhw, q->nh_w.data(), (size_t)nq * 4);
+        std::memcpy(host.data() + o_nhboff, q->nhb_off.data(), (size_t)nq * 8);
+        std::memcpy(host.data() + o_nhb, q->nh_b.data(), (size_t)nq * 4);
       }
       if (!row_of.empty()) {
         std::memcpy(host.data() + o_rowof, row_of.data(), (size_t)V * 4);
@@ -6484,6 +6659,8 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       if (want_nh && nq) {
         q->d_nh_off = reinterpret_cast<uint64_t*>(base + o_nhoff);
         q->d_nh_w = reinterpret_cast<uint32_t*>(base + o_nhw);
+        q->d_nhb_off = reinterpret_cast<uint64_t*>(base + o_nhboff);
+        q->d_nh_b = reinterpret_cast<uint32_t*>(base + o_nhb);
       }
       if (!row_of.empty()) {
         q->d_row_of = reinterpret_cast<int32_t*>(base + o_rowof);
@@ -6517,9 +6694,19 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     }
   }
   if (want_nh) {
-    if (q->nh_total &&
-        pool_malloc((void**)&q->d_nh, q->nh_total * 8) != hipSuccess) {
-      return bail(fail(SPF_E_NOMEM, "next-hop rows"));
+    // the SWAR next-hop kernels write the output layout themselves
+    q->nl_swar = env_flag("OPENR_NL_SWAR", 1) || q->zvars;
+    q->nh_direct = q->dist == DistPlan::MsBfs && q->nh == NhPlan::Levels && q->nl_swar;
+    if (!q->narrow) {
+      if (q->nh_total && pool_malloc((void**)&q->d_nh, q->nh_total * 8) != hipSuccess) {
+        return bail(fail(SPF_E_NOMEM, "next-hop rows"));
+      }
+      q->d_nhb = reinterpret_cast<uint8_t*>(q->d_nh);
+    } else {
+      if (pool_malloc((void**)&q->d_nhb, q->nhb_total) != hipSuccess ||
+          (!q->nh_direct && pool_malloc((void**)&q->d_nh, q->nh_total * 8) != hipSuccess)) {
+        return bail(fail(SPF_E_NOMEM, "next-hop rows"));
+      }
     }
   }
   const bool ex = q->dist == DistPlan::Exact;
@@ -6582,7 +6769,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       spf_query_desc bd{};
       bd.num_queries = (uint32_t)base_srcs.size();
       bd.sources = base_srcs.data();
-      bd.flags = desc->flags;
+      bd.flags = desc->flags | kQueryWideMasks;
       if ((s = spf_query_create(g, &bd, &q->base)) ||
           (s = dev_upload_q(&q->d_base_of, base_of.data(), nq))) {
         return bail(s);
@@ -7040,6 +7227,9 @@ int launch_nh_levels(spf_query* q, bool unit) {
   a.nh_off = q->d_nh_off;
   a.nh_w = q->d_nh_w;
   a.nh_out = q->d_nh;
+  a.nhb = q->d_nhb;
+  a.nhb_off = q->d_nhb_off;
+  a.nh_b = q->d_nh_b;
   a.V = g->V;
   a.Vp = q->Vp;
   a.Vp8 = q->Vp8;
@@ -7057,7 +7247,7 @@ int launch_nh_levels(spf_query* q, bool unit) {
   if (blocks > 0x7FFFFFFFull) {
     return fail(SPF_E_UNSUPPORTED, "batch too large for the next-hop pass");
   }
-  if (env_flag("OPENR_NL_SWAR", 1) || q->d_zvar) {
+  if (q->nl_swar) {
     // held kernel: every source with <= kNsHeldMax mask words; the generic
     // byte kernel: the rest (q->d_big), or every source after a deep BFS
     // threads per block (OPENR_NL_HT = 256 / 512 / 1024; chunk = 4 nodes per thread)
@@ -7218,8 +7408,24 @@ int finish_zero_plan(spf_query* q) {
     if (f->nh_w[j] != q->nh_w[i]) {
       return fail(SPF_E_INVALID, "internal: zero-metric fix-up mask width differs");
     }
-    HIP_TRY(hipMemcpyAsync(q->d_nh + q->nh_off[i], f->d_nh + f->nh_off[j],
-                           (size_t)q->nh_w[i] * V * 8, hipMemcpyDeviceToDevice, g->stream));
+    if (!q->narrow) {
+      HIP_TRY(hipMemcpyAsync(q->d_nh + q->nh_off[i], f->d_nh + f->nh_off[j],
+                             (size_t)q->nh_w[i] * V * 8, hipMemcpyDeviceToDevice, g->stream));
+    } else {
+      // f's rows are in the word layout (kQueryWideMasks): narrow row i
+      NhNarrowArgs na{};
+      na.src = f->d_nh;
+      na.dst = q->d_nhb;
+      na.src_off1 = f->nh_off[j];
+      na.dst_off1 = q->nhb_off[i];
+      na.nb1 = q->nh_b[i];
+      na.nw1 = q->nh_w[i];
+      na.V = V;
+      na.nq = 1;
+      hipLaunchKernelGGL(spf_nh_narrow_kernel, dim3((V + 1023) / 1024), dim3(256), 0, g->stream,
+                         na);
+      HIP_TRY(hipGetLastError());
+    }
     hipLaunchKernelGGL(spf_rows64to32_kernel, dim3((V + 255) / 256), dim3(256), 0, g->stream,
                        (const uint64_t*)f->d_dist + (size_t)j * V,
                        (uint32_t*)q->d_dist + (size_t)i * q->Vp, V);
@@ -7265,7 +7471,35 @@ int run_screen(spf_query* q) {
   return SPF_OK;
 }
 
+int run_plan_kernels(spf_query* q);
+
+// the plan's kernels, then (word-layout plans of a query with narrow rows)
+// the working rows narrowed into the output layout
 int run_plan(spf_query* q) {
+  const int s = run_plan_kernels(q);
+  if (s != SPF_OK || !q->narrow || q->nh_direct || !q->d_nh) {
+    return s;
+  }
+  NhNarrowArgs na{};
+  na.src = q->d_nh;
+  na.dst = q->d_nhb;
+  na.src_off = q->d_nh_off;
+  na.dst_off = q->d_nhb_off;
+  na.nb = q->d_nh_b;
+  na.nw = q->d_nh_w;
+  na.V = q->g->V;
+  na.nq = q->nq;
+  const uint64_t blocks = (uint64_t)q->nq * ((q->g->V + 1023) / 1024);
+  if (blocks > 0x7FFFFFFFull) {
+    return fail(SPF_E_UNSUPPORTED, "batch too large for the mask narrowing pass");
+  }
+  hipLaunchKernelGGL(spf_nh_narrow_kernel, dim3((uint32_t)blocks), dim3(256), 0, q->g->stream,
+                     na);
+  HIP_TRY(hipGetLastError());
+  return SPF_OK;
+}
+
+int run_plan_kernels(spf_query* q) {
   const bool unit = q->flags & SPF_F_UNIT_METRIC;
   if (q->base) {
     const int s = run_screen(q);
@@ -7503,11 +7737,29 @@ int spf_query_nexthops(spf_query* q, uint32_t i, uint64_t* out) {
   }
   HIP_TRY(hipSetDevice(q->g->device));
   HIP_TRY(hipStreamSynchronize(q->g->stream));
-  const size_t n = (size_t)q->nh_w[i] * q->g->V;
-  if (n) {
-    HIP_TRY(hipMemcpy(out, q->d_nh + q->nh_off[i], n * 8,
-                      hipMemcpyDeviceToHost));
+  const size_t V = q->g->V, W = q->nh_w[i], B = q->nh_b[i];
+  if (V && B >= 8) {
+    HIP_TRY(hipMemcpy(out, q->d_nhb + q->nhb_off[i], V * W * 8, hipMemcpyDeviceToHost));
+  } else if (V) {
+    std::vector<uint8_t> tmp(V * B);
+    HIP_TRY(hipMemcpy(tmp.data(), q->d_nhb + q->nhb_off[i], V * B, hipMemcpyDeviceToHost));
+    widen_masks(tmp.data(), B, V, out);
   }
+  return SPF_OK;
+}
+
+int spf_query_nh_bytes(const spf_query* q, uint32_t i) {
+  if (!q || i >= q->nq) {
+    return fail(SPF_E_INVALID, "bad query row");
+  }
+  return (int)q->nh_b[i];
+}
+
+int spf_query_nh_offset(const spf_query* q, uint32_t i, uint64_t* byte_off) {
+  if (!q || !byte_off || i >= q->nq) {
+    return fail(SPF_E_INVALID, "bad query row");
+  }
+  *byte_off = q->nhb_off[i];
   return SPF_OK;
 }
 
@@ -7575,10 +7827,10 @@ int spf_query_device_rows(
     *dist_elem_bytes = rows64(q) ? 8 : 4;
   }
   if (nh_rows) {
-    *nh_rows = q->d_nh;
+    *nh_rows = q->d_nhb;
   }
   if (nh_total_words) {
-    *nh_total_words = q->nh_total;
+    *nh_total_words = q->nhb_total / 8; // rows are 32-byte aligned
   }
   return SPF_OK;
 }
@@ -7777,16 +8029,21 @@ int spf_query_fetch_nexthops(
     return SPF_OK;
   }
   const size_t V = q->g->V;
-  const uint64_t lo = q->nh_off[first];
-  const uint64_t hi = first + count < q->nq ? q->nh_off[first + count] : q->nh_total;
-  std::vector<uint64_t> tmp(hi - lo);
+  const uint64_t lo = q->nhb_off[first];
+  const uint64_t hi = first + count < q->nq ? q->nhb_off[first + count] : q->nhb_total;
+  std::vector<uint8_t> tmp(hi - lo);
   HIP_TRY(hipSetDevice(q->g->device));
   HIP_TRY(hipStreamSynchronize(q->g->stream));
-  HIP_TRY(hipMemcpy(tmp.data(), q->d_nh + lo, (hi - lo) * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(tmp.data(), q->d_nhb + lo, hi - lo, hipMemcpyDeviceToHost));
   uint64_t out = 0;
   for (uint32_t i = first; i < first + count; ++i) {
     const size_t n = V * q->nh_w[i];
-    std::memcpy(dst + out, tmp.data() + (q->nh_off[i] - lo), n * 8);
+    const uint8_t* src = tmp.data() + (q->nhb_off[i] - lo);
+    if (q->nh_b[i] >= 8) {
+      std::memcpy(dst + out, src, n * 8);
+    } else {
+      widen_masks(src, q->nh_b[i], V, dst + out);
+    }
     out += n;
   }
   return SPF_OK;
@@ -8430,8 +8687,9 @@ int spf_route_table_run(spf_route_table* t) {
     a.trbits = g->d_tr;
     a.src = q->d_src;
     a.dist = (const uint32_t*)q->d_dist;
-    a.nh = q->d_nh;
-    a.nh_off = q->d_nh_off;
+    a.nh = q->d_nhb;
+    a.nh_off = q->d_nhb_off;
+    a.nh_b = q->d_nh_b;
     a.nh_w = q->d_nh_w;
     a.ann_off = t->d_ann_off;
     a.ann = t->d_ann;

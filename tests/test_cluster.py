@@ -18,18 +18,27 @@ from openr_amd import abi
 from openr_amd import allsources as AS
 
 
+def test_nh_bytes_rule():
+    """Device mask bytes per node (SPF_NH_BYTES): 1 / 2 / 4 bytes up to 8 / 16
+    / 32 neighbours (a fabric RSW's 8 neighbours: one byte per node), then
+    whole u64 words."""
+    want = {0: 1, 1: 1, 8: 1, 9: 2, 16: 2, 17: 4, 32: 4, 33: 8, 64: 8, 65: 16, 173: 24}
+    assert {n: abi.nh_bytes_for(n) for n in want} == want
+
+
 @pytest.mark.parametrize("n,world", [(10, 3), (9976, 8), (7, 8), (100000, 8), (1, 1), (0, 4)])
 def test_table_layout_blocks_match_shard(n, world):
     rng = np.random.default_rng(n + world)
     V = 37
-    words = rng.integers(1, 4, size=n).astype(np.uint32)
-    bf, mo, cap = abi.table_layout(n, world, V, words)
+    nbytes = rng.choice([1, 2, 4, 8, 16, 24], size=n).astype(np.uint32)
+    bf, mo, cap = abi.table_layout(n, world, V, nbytes)
     for r in range(world):
         first, count = AS.shard(n, world, r)
         assert (int(bf[r]), int(bf[r + 1] - bf[r])) == (first, count)
     assert int(bf[world]) == n
+    assert cap % 32 == 0
     # mask slots: equal-sized, every source inside its owner's slot, back to back
-    size = lambda i: ((V * int(words[i]) + 3) // 4) * 4  # noqa: E731
+    size = lambda i: ((V * int(nbytes[i]) + 31) // 32) * 32  # noqa: E731
     for r in range(world):
         off = r * cap
         for i in range(int(bf[r]), int(bf[r + 1])):
@@ -39,21 +48,21 @@ def test_table_layout_blocks_match_shard(n, world):
 
 
 def test_table_layout_gather_simulation():
-    """Rank r's packed masks (query order, each roundup4(V*W) words) placed in
-    slot r of an all-gather land where mask_off says."""
+    """Rank r's packed masks (query order, each roundup32(V*B) bytes) placed
+    in slot r of an all-gather land where mask_off says."""
     rng = np.random.default_rng(5)
     n, world, V = 23, 4, 11
-    words = rng.integers(1, 3, size=n).astype(np.uint32)
-    bf, mo, cap = abi.table_layout(n, world, V, words)
-    gathered = np.zeros(world * cap, dtype=np.uint64)
+    nbytes = rng.choice([1, 2, 4, 8, 16], size=n).astype(np.uint32)
+    bf, mo, cap = abi.table_layout(n, world, V, nbytes)
+    gathered = np.zeros(world * cap, dtype=np.uint8)
     truth = {}
     for r in range(world):
         packed = []
         for i in range(int(bf[r]), int(bf[r + 1])):
-            m = rng.integers(0, 2**63, size=V * int(words[i]), dtype=np.uint64)
+            m = rng.integers(0, 256, size=V * int(nbytes[i]), dtype=np.uint8)
             truth[i] = m
-            pad = (-len(m)) % 4
-            packed.append(np.concatenate([m, np.zeros(pad, dtype=np.uint64)]))
+            pad = (-len(m)) % 32
+            packed.append(np.concatenate([m, np.zeros(pad, dtype=np.uint8)]))
         if packed:
             blk = np.concatenate(packed)
             gathered[r * cap : r * cap + len(blk)] = blk  # ncclAllGather slot r
@@ -83,6 +92,7 @@ def _check_table_equals_query(t, g, csr, sources, flags):
     assert (t.fetch_rows(0, n) == rows).all()
     if flags & abi.SPF_F_NEXTHOPS:
         assert [t.nh_words(i) for i in range(n)] == [q.nh_words(i) for i in range(n)]
+        assert [t.nh_bytes(i) for i in range(n)] == [q.nh_bytes(i) for i in range(n)]
         assert (t.fetch_nexthops(0, n) == q.fetch_nexthops(0, n)).all()
     q.close()
 

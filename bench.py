@@ -136,6 +136,19 @@ def pmc_traffic(kernel_name):
     return None, None
 
 
+def wan_sssp_bytes(plan, V, E):
+    """Algorithmic bytes per SSSP of the WAN all-sources plan (SURVEY §8(d)
+    per-SSSP figure without the masks this distance-only pass does not
+    produce): the out-edges of every settled node read once, in the format
+    the kernel reads, the row pointers, and the u32 distance row written
+    once.  The LDS-row plan (spf_dlds_kernel) reads packed edges (head |
+    metric << bits, 4 bytes); the HBM-row pass spf_dstep_kernel is priced on
+    the separate head / metric arrays (8 bytes), as before."""
+    if plan == "dstep-ldsrow":
+        return 4 * E + 4 * (V + 1) + 4 * V, "spf_dlds_kernel (LDS-resident 12-bit rows, packed edges)"
+    return 8 * E + 4 * (V + 1) + 4 * V, "spf_dstep_kernel (push-only, LDS buckets)"
+
+
 def pmc_traffic_largest(kernel_name):
     """HBM bytes of the largest dispatch of `kernel_name` in the committed
     PMC passes (the measured launch, not a warm-up batch)."""
@@ -981,7 +994,7 @@ def wan_all_sources_table(args, world, rank, local, dist, cluster):
         check = "ok" if bad == 0 else f"{bad} mismatches"
     kernel = tab.kernel(0)
     tab.close()
-    per_sssp = 8 * E + 4 * (V + 1) + 4 * V
+    per_sssp, kdesc = wan_sssp_bytes(kernel, V, E)
     out = {
         "config": "BASELINE configs[2]: 100k-node / 1M-link WAN (SURVEY §8(d) row 3), all sources, "
                   f"one engine call over {world} GPU(s): contiguous source blocks + in-engine RCCL "
@@ -995,7 +1008,7 @@ def wan_all_sources_table(args, world, rank, local, dist, cluster):
         "gteps": round(V * E / (wall_ms / 1e3) / 1e9, 2),
         "table_bytes": V * V * 4,
         "gather_algbw_gbs": round(V * V * 4 / (gather_ms / 1e3) / 1e9, 1) if world > 1 and gather_ms else None,
-        "roofline": {"bound": "hbm", "kernel": "spf_dstep_kernel (push-only, LDS buckets)",
+        "roofline": {"bound": "hbm", "kernel": kdesc,
                      "algorithmic_bytes_per_sssp": per_sssp,
                      "algorithmic_achieved": round(V * per_sssp / (comp_ms / 1e3) / 1e9 / world, 1),
                      "algorithmic_frac": round(V * per_sssp / (comp_ms / 1e3) / 1e9 / world / HBM_PEAK_GBS, 4),
@@ -1104,10 +1117,10 @@ def wan_all_sources(args, world, rank, local, dist):
     # CSR row of every settled node read once (col + metric u32, row_ptr),
     # the distance row written once (SURVEY §8(d) per-SSSP figure without
     # the next-hop masks this distance-only pass does not produce)
-    per_sssp = 8 * E + 4 * (V + 1) + 4 * V
+    per_sssp, kdesc = wan_sssp_bytes(r.kernel, V, E)
     kernel_s = spf_ms / 1e3
     achieved = sas.count * per_sssp / kernel_s / 1e9 if kernel_s else None
-    traffic, traffic_src = pmc_traffic_largest("spf_dstep_kernel")
+    traffic, traffic_src = pmc_traffic_largest(kdesc.split()[0])
     out = {
         "config": "BASELINE configs[2]: 100k-node / 1M-link WAN (SURVEY §8(d) row 3), all sources, "
                   "contiguous source blocks per GPU, RCCL all-gather of uint32 rows",
@@ -1120,9 +1133,10 @@ def wan_all_sources(args, world, rank, local, dist):
         "gteps": round(n * E / (wall_ms / 1e3) / 1e9, 2),
         "table_bytes": table_bytes,
         "gather_algbw_gbs": round(table_bytes / (gather_ms / 1e3) / 1e9, 1) if world > 1 and gather_ms else None,
-        "roofline": {"bound": "hbm", "kernel": "spf_dstep_kernel (push-only, LDS buckets)",
+        "roofline": {"bound": "hbm", "kernel": kdesc,
                      # SURVEY §8(d) per-SSSP figure without masks: CSR of every settled
-                     # node read once + the distance row written once
+                     # node read once (in the format the kernel reads) + the distance
+                     # row written once
                      "algorithmic_bytes_per_sssp": per_sssp,
                      "algorithmic_achieved": round(achieved, 1) if achieved else None,
                      "algorithmic_frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,

@@ -115,3 +115,35 @@ def summaries_from_rows(rows32, masks, words, nbrs, mix_rows=()):
                 mix = mix + splitmix64_np(key).sum(dtype=np.uint64)
         out[q, 3] = mix
     return out
+
+
+def dist_summaries_torch(rows):
+    """(reached, sum_dist, 0, mix) of distance-only rows, computed where the
+    rows live: `rows` is an int32 torch tensor [Q, V] (-1 = unreached, the
+    uint32 rows reinterpreted), on any device — the checker side of the
+    100,000-row WAN golden (tests/golden/wan100k_allsources.npz) without
+    copying 40 GB to the host.  uint64 arithmetic is done in int64 (two's
+    complement: sums and products wrap mod 2^64 alike, right shifts are
+    masked to be logical).  Returns uint64 [Q, 4] numpy."""
+    import torch
+
+    def lsr(x, k):
+        return (x >> k) & ((1 << (64 - k)) - 1)
+
+    def s64(c):
+        return c - (1 << 64) if c >= 1 << 63 else c
+
+    Q, V = rows.shape
+    reach = rows != -1
+    d = rows.to(torch.int64) & 0xFFFFFFFF
+    x = (d << 24) ^ torch.arange(V, device=rows.device, dtype=torch.int64)
+    x = x + s64(0x9E3779B97F4A7C15)
+    x = (x ^ lsr(x, 30)) * s64(0xBF58476D1CE4E5B9)
+    x = (x ^ lsr(x, 27)) * s64(0x94D049BB133111EB)
+    x = x ^ lsr(x, 31)
+    zero = torch.zeros((), dtype=torch.int64, device=rows.device)
+    out = torch.stack([reach.sum(dim=1, dtype=torch.int64),
+                       torch.where(reach, d, zero).sum(dim=1),
+                       torch.zeros(Q, dtype=torch.int64, device=rows.device),
+                       torch.where(reach, x, zero).sum(dim=1)], dim=1)
+    return out.cpu().numpy().view(np.uint64)

@@ -228,7 +228,7 @@ def test_msdstep_vs_dstep_and_replay(gpu_ready, seed, monkeypatch):
     drained = [int(v) for v in np.flatnonzero(ov)[:3]]
     srcs = [rng.randrange(V) for _ in range(150)] + drained + [5, 5, 77]
     ref = g.query(srcs, 0).run()
-    assert ref.kernel == "dstep"
+    assert ref.kernel == "dstep-ldsrow"  # distance rows in LDS (metrics <= 300)
     monkeypatch.setenv("OPENR_SPF_MSD", "1")
     want = [ref.dist(i) for i in range(len(srcs))]
     for shift, cluster in (("0", "1"), ("4", "0"), (None, "1"), ("30", "1")):
@@ -271,7 +271,7 @@ def test_msdstep_wan_anchor(gpu_ready):
     assert int(d0.sum()) == a["sum_dist"]
     rows = list(range(0, 256, 16))
     r = g.query(srcs[rows], 0).run()  # 16 sources: per-source kernel
-    assert r.kernel == "dstep"
+    assert r.kernel == "dstep-ldsrow"
     for k, i in enumerate(rows):
         assert (q.dist(i) == r.dist(k)).all(), i
 

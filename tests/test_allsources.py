@@ -141,7 +141,7 @@ def test_sharded_all_sources_engine(gpu_ready):
     srcs = np.asarray(rng.sample(range(V), 300), dtype=np.uint32)
     torch.cuda.set_device(0)
     sas = AS.ShardedAllSources(csr, sources=srcs, gather=False)
-    assert sas.kernel == "dstep"
+    assert sas.kernel == "dstep-ldsrow"  # distances fit the 12-bit LDS rows
     run = sas.run()
     assert run.count == 300 and run.spf_ms > 0
     g = abi.Graph(csr)

@@ -9,8 +9,9 @@ DijkstraQ replay) and against size-independent properties.
             for EVERY source, the reference-form digest of the 8
             fabric_sampled.json sources.
   config 3  the 100k-node / 1M-link WAN, all 100,000 sources through
-            ShardedAllSources (world 1, push-only delta-stepping): the
-            reference's own checksum of row n0, 32 sampled rows by sha256, and
+            ShardedAllSources (world 1, LDS-resident delta-stepping): the
+            reference's own checksum of row n0, EVERY row's (reached, sum,
+            mix) against the 100,000-source golden, 32 sampled rows by sha256, and
             for those rows the Bellman conditions (no edge relaxes, every
             reached node has a tight in-edge) plus D[s][t] == D[t][s].
   config 5  8,192 single-link-failure SPFs from the border node 2-0-0 over two
@@ -105,10 +106,22 @@ def test_config3_wan100k_all_sources_sharded(gpu_ready):
     csr = topo.csr()
     V = csr.num_nodes
     sas = AS.ShardedAllSources(csr, device=0, gather=False)
-    assert sas.kernel == "dstep"  # push-only delta-stepping, the config-3 plan
+    # LDS-resident delta-stepping (12-bit rows), the config-3 plan
+    assert sas.kernel == "dstep-ldsrow"
     sas.run()
     # the reference's runSpf checksum of source n0
     assert int(sas.row(0).astype(np.int64).sum()) == anchor["sum_dist"]
+    # EVERY row against the 100,000-source golden (oracle/csr_spf.h,
+    # tests/golden/make_wan_allsources.py): (reached, sum, mix) per source,
+    # summarised on the device in 2,048-row slices
+    from tests.golden.summary import dist_summaries_torch
+
+    want = np.load(os.path.join(GOLD, "wan100k_allsources.npz"))["summary"]
+    bad = []
+    for lo in range(0, V, 2048):
+        got = dist_summaries_torch(sas.table[lo:min(V, lo + 2048)])
+        bad += (lo + np.flatnonzero((got != want[lo:lo + len(got)]).any(axis=1))).tolist()
+    assert not bad, f"{len(bad)} of {V} WAN rows differ from the golden, first {bad[:5]}"
     row = csr.row_ptr.astype(np.int64)
     src_of_edge = np.repeat(np.arange(V, dtype=np.int64), np.diff(row))
     col = csr.col.astype(np.int64)
@@ -149,7 +162,7 @@ def test_config3_wan100k_all_sources_spf_table(gpu_ready):
     c = abi.Cluster([0])
     cg = abi.ClusterGraph(c, csr)
     t = cg.table(np.arange(csr.num_nodes, dtype=np.uint32), 0, gather=abi.SPF_T_GATHER_ROWS).run()
-    assert t.kernel(0) == "dstep"
+    assert t.kernel(0) == "dstep-ldsrow"
     assert int(t.fetch_rows(0, 1)[0].astype(np.int64).sum()) == anchor["sum_dist"]
     for r in gold:
         row = t.fetch_rows(r["src"], 1)[0]

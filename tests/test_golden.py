@@ -81,6 +81,43 @@ def test_oracle_matches_reference_wan_checksum(oracle):
     assert total == a["sum_dist"]
 
 
+def test_wan100k_allsources_golden_pins(oracle):
+    """tests/golden/wan100k_allsources.npz (every one of the 100,000 WAN
+    sources, oracle/csr_spf.h) agrees with the reference's own checksum of
+    row n0 and with 3 of the committed sha256 rows recomputed here; the
+    torch summariser the GPU test uses equals the oracle's rows_summary."""
+    import hashlib
+
+    import torch
+
+    from openr_amd import topologies as TP
+    from tests.golden.summary import dist_summaries_torch
+
+    S = np.load(os.path.join(GOLD, "wan100k_allsources.npz"))["summary"]
+    assert S.shape == (100000, 4) and S.dtype == np.uint64
+    assert (S[:, 0] == 100000).all() and (S[:, 2] == 0).all()  # connected, distances only
+    anchor = [a for a in _gold("wan_anchors.json")["anchors"] if a["V"] == 100000 and a["S"] == 1][0]
+    assert int(S[0, 1]) == anchor["sum_dist"]
+    gold = _gold("wan100k_rows.json")["rows"][:3]
+    csr = TP.wan(100000, 1000000).csr()
+    srcs = np.asarray([r["src"] for r in gold], dtype=np.uint32)
+    rows = oracle.csr_spf_rows(csr.row_ptr, csr.col, csr.metric.astype(np.uint64), csr.link_id,
+                               csr.overloaded, srcs, True, 4)
+    r32 = np.where(rows == np.uint64(2**64 - 1), np.uint64(0xFFFFFFFF), rows).astype(np.uint32)
+    for r, row in zip(gold, r32):
+        assert hashlib.sha256(row.tobytes()).hexdigest() == r["sha256"]
+    got = dist_summaries_torch(torch.from_numpy(r32.view(np.int32)))
+    assert (got == S[srcs]).all()
+    # unreached entries and the oracle's own rows summary
+    r32[1, ::7] = 0xFFFFFFFF
+    V = r32.shape[1]
+    z = np.zeros(len(r32) + 1, dtype=np.uint64)
+    want = oracle.rows_summary(r32, np.zeros(1, dtype=np.uint64), z, z.astype(np.uint32),
+                               np.zeros(1, dtype=np.uint32), 2)
+    assert (dist_summaries_torch(torch.from_numpy(r32.view(np.int32))) == want).all()
+    assert V == 100000
+
+
 def test_oracle_grid10_golden(oracle):
     from openr_amd import thrift as T
     from openr_amd import topologies as TP

@@ -359,7 +359,7 @@ def _full_table(csr, srcs):
 @pytest.mark.parametrize("mode", ["repair", "recompute"])
 @pytest.mark.parametrize(
     "V,L,wmax,nsrc,expect_kernel",
-    [(3000, 12000, 50, 3000, None), (40000, 160000, 1000, 400, "dstep"), (2500, 9000, 1, 2500, None)],
+    [(3000, 12000, 50, 3000, None), (40000, 160000, 1000, 400, "dstep-ldsrow"), (2500, 9000, 1, 2500, None)],
 )
 def test_repair_equals_full_recompute(gpu_ready, V, L, wmax, nsrc, expect_kernel, mode, monkeypatch):
     import torch

@@ -833,12 +833,13 @@ struct DeviceTraces {
   bool unsupported = false; // 64-bit rows in some block: use runBatchAuto
 };
 
-// opt-in (OPENR_KSP2_DEVICE_TRACE=1): on the fabric the device traces cost
-// more than the host pool's (profiles/r03d: 59 ms of device DFS, 632 of
-// 9,975 traces overflowing to the host, KSP2 loop 219 ms vs 174-189 ms)
+// default (OPENR_KSP2_DEVICE_TRACE=0 traces on the host pool instead): the
+// cursor DFS (spf_trace_cursor_kernel) keeps one pathLinks cursor per node in
+// device scratch; the round-3 kernel re-scanned a node's in-edges per step
+// and overflowed 632 of the fabric's 9,975 traces to the host (profiles/r03d)
 bool deviceTraceEnabled() {
   const char* e = std::getenv("OPENR_KSP2_DEVICE_TRACE");
-  return e && std::atoi(e) != 0;
+  return !e || std::atoi(e) != 0;
 }
 
 DeviceTraces traceSecondPasses(

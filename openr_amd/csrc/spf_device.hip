@@ -4510,7 +4510,7 @@ constexpr uint32_t kTraceHash = 1024;    // visited-link slots per wave (<= 1/2 
 constexpr uint32_t kTraceDead = 512;     // failed-node slots per wave
 constexpr uint32_t kTraceDepth = 128;    // recursion frames per wave
 constexpr uint32_t kTraceOverflow = 0xFFFFFFFFu;
-constexpr uint32_t kTraceCap = 1024;     // links (and paths) per query
+constexpr uint32_t kTraceCap = 4096;     // links (and paths) per query
 constexpr uint32_t kTraceEmpty = 0xFFFFFFFFu;
 
 struct TraceArgs {
@@ -4756,6 +4756,212 @@ __global__ __launch_bounds__(64 * kTraceWaves) void spf_trace_paths_kernel(Trace
   }
 }
 
+// Cursor DFS (spf_trace_cursor_kernel, the default).  traceOnePath's visited
+// set only ever grows, and a link u -> v is examined only by the loop over
+// pathLinks(v) (on the 32-bit plans every metric is >= 1, so a link is a
+// pathLink of at most one of its ends), in pathLinks order, from the start,
+// inserting every link it examines (LinkState.cpp:407-416).  The examined
+// links of v are therefore always a PREFIX of pathLinks(v), and the whole
+// visited set is one cursor per node: a step is "take pathLinks(v)[cursor(v)++]",
+// a node whose cursor reached the end fails at once (the host trace's dead
+// memo), and a later traceOnePath of the same loop resumes every node where
+// the last one left it.  pathLinks(v) is built once per (query, node) when
+// the search first enters v: v's in-edges are filtered (usable, tight, tail
+// the source or transit, link not ignored), ranked by (d[u], u, u's row
+// position) and written to a per-wave arena in global scratch; node states
+// {query tag, arena offset, length, cursor} live in a per-wave node array.
+// Only the recursion stack is in LDS, so nothing but a path longer than
+// kTcDepth links, a node with more than kTcSort pathLinks or a full arena
+// overflows to the host.
+constexpr uint32_t kTcWaves = 4;    // waves (queries in flight) per block
+constexpr uint32_t kTcDepth = 256;  // recursion frames per wave
+constexpr uint32_t kTcSort = 256;   // pathLinks of one node ranked in LDS
+constexpr uint32_t kTcIgn = 256;    // ignore-list entries staged in LDS per query
+
+struct TraceCursorArgs {
+  TraceArgs t;
+  uint4* nstate;   // [waves][V] {tag, arena offset, length, cursor}
+  uint32_t* arena; // [waves][arena_cap] in-edges e (v's row) in pathLinks order
+  uint32_t arena_cap;
+  uint32_t V;
+};
+
+__device__ __forceinline__ void tc_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint4 tc_load4(const uint4* p) {
+  // the state may have been written by another lane of this wave (or by
+  // this wave for an earlier query): read it from L2, not the vector L1
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+  return make_uint4(ld_coh(w), ld_coh(w + 1), ld_coh(w + 2), ld_coh(w + 3));
+}
+
+__global__ __launch_bounds__(64 * kTcWaves) void spf_trace_cursor_kernel(TraceCursorArgs A) {
+  const TraceArgs& a = A.t;
+  __shared__ uint32_t stk_s[kTcWaves][kTcDepth]; // node of each frame
+  __shared__ uint32_t lnk_s[kTcWaves][kTcDepth]; // link taken at each frame
+  __shared__ uint64_t key_s[kTcWaves][kTcSort];  // (d[u] << 32 | u)
+  __shared__ uint32_t sub_s[kTcWaves][kTcSort];  // u's row position (tie-break)
+  __shared__ uint32_t edg_s[kTcWaves][kTcSort];  // in-edge e of v's row
+  __shared__ uint32_t ign_s[kTcWaves][kTcIgn];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t gw = blockIdx.x * kTcWaves + wv, nwaves = gridDim.x * kTcWaves;
+  uint4* ns = A.nstate + (size_t)gw * A.V;
+  uint32_t* arena = A.arena + (size_t)gw * A.arena_cap;
+  uint32_t* stk = stk_s[wv];
+  uint32_t* lnk = lnk_s[wv];
+  uint64_t* keys = key_s[wv];
+  uint32_t* subs = sub_s[wv];
+  uint32_t* edgs = edg_s[wv];
+  uint32_t* ignl = ign_s[wv];
+  const uint64_t lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (uint32_t q = gw; q < a.nq; q += nwaves) { // wave-uniform loop
+    const uint32_t tag = q + 1;
+    const uint32_t s = a.src[q], d = a.dst[q];
+    const uint32_t* dist = a.dist + (size_t)q * a.Vp;
+    const uint32_t ilo = a.ign_off ? a.ign_off[q] : 0u;
+    const uint32_t nign = a.ign_off ? a.ign_off[q + 1] - ilo : 0u;
+    const uint32_t* ignp = a.ign + ilo;
+    if (nign <= kTcIgn) {
+      for (uint32_t i = lane; i < nign; i += 64) {
+        ignl[i] = ignp[i];
+      }
+      ignp = ignl;
+    }
+    tc_sync();
+    uint32_t* out_links = a.out_links + (size_t)q * a.cap;
+    uint32_t* out_ends = a.out_ends + (size_t)q * a.cap;
+    uint32_t npaths = 0, nl = 0, atop = 0;
+    bool overflow = false;
+    if (s != d && dist[d] != kInf32) {
+      for (;;) { // one traceOnePath per iteration
+        uint32_t depth = 0;
+        if (lane == 0) {
+          stk[0] = d;
+        }
+        tc_sync();
+        bool found = false;
+        for (;;) {
+          const uint32_t v = stk[depth];
+          uint4 st = tc_load4(ns + v);
+          if (st.x != tag) {
+            // pathLinks(v): candidates compacted into LDS, then ranked
+            const uint64_t dv = dist[v];
+            const uint32_t e0 = a.row[v], e1 = a.row[v + 1];
+            uint32_t n = 0;
+            for (uint32_t base = e0; base < e1; base += 64) {
+              const uint32_t e = base + lane;
+              bool ok = false;
+              uint32_t u = 0, du = 0, eu = 0;
+              if (e < e1) {
+                u = a.col[e];
+                du = dist[u];
+                ok = du != kInf32 && (u == s || ((a.trbits[u >> 5] >> (u & 31)) & 1u));
+                if (ok) {
+                  eu = a.rev[e];
+                  const uint64_t w = a.unit ? 1ull : (uint64_t)a.wout[eu];
+                  ok = (uint64_t)du + w == dv;
+                }
+                if (ok && nign) {
+                  ok = !in_sorted(ignp, nign, a.link[e]);
+                }
+              }
+              const uint64_t m = __ballot(ok);
+              const uint32_t pos = n + (uint32_t)__popcll(m & lt_mask);
+              if (ok && pos < kTcSort) {
+                keys[pos] = ((uint64_t)du << 32) | u;
+                subs[pos] = eu;
+                edgs[pos] = e;
+              }
+              n += (uint32_t)__popcll(m);
+            }
+            tc_sync();
+            if (n > kTcSort || atop + n > A.arena_cap) {
+              overflow = true;
+              break;
+            }
+            for (uint32_t i = lane; i < n; i += 64) {
+              const uint64_t k = keys[i];
+              const uint32_t su = subs[i];
+              uint32_t r = 0;
+              for (uint32_t j = 0; j < n; ++j) {
+                const uint64_t kj = keys[j];
+                r += kj < k || (kj == k && subs[j] < su);
+              }
+              arena[atop + r] = edgs[i];
+            }
+            st = make_uint4(tag, atop, n, 0);
+            atop += n;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            tc_sync();
+          }
+          if (st.w < st.z) {
+            const uint32_t e = ld_coh(arena + st.y + st.w);
+            st.w += 1;
+            // every lane stores the same state: a lane's later read of it
+            // follows its own store
+            ns[v] = st;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint32_t u = a.col[e];
+            if (lane == 0) {
+              lnk[depth] = a.link[e];
+            }
+            if (u == s) {
+              found = true;
+              break;
+            }
+            if (depth + 1 >= kTcDepth) {
+              overflow = true;
+              break;
+            }
+            ++depth;
+            if (lane == 0) {
+              stk[depth] = u;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            tc_sync();
+            continue;
+          }
+          // v exhausted: the search through it fails
+          ns[v] = st;
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (depth == 0) {
+            break;
+          }
+          --depth;
+        }
+        if (overflow || !found) {
+          break;
+        }
+        tc_sync();
+        const uint32_t len = depth + 1;
+        if (nl + len > a.cap || npaths + 1 > a.cap) {
+          overflow = true;
+          break;
+        }
+        // frames deepest first: the path runs src -> dst
+        for (uint32_t i = lane; i < len; i += 64) {
+          out_links[nl + i] = lnk[depth - i];
+        }
+        nl += len;
+        if (lane == 0) {
+          out_ends[npaths] = nl;
+        }
+        ++npaths;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        tc_sync();
+      }
+    }
+    if (lane == 0) {
+      a.out_n[q] = overflow ? kTraceOverflow : npaths;
+      a.out_len[q] = overflow ? 0u : nl;
+    }
+    tc_sync(); // the next query restages the ignore list
+  }
+}
+
 struct TracePackArgs {
   const uint32_t* out_n;
   const uint32_t* out_len;
@@ -4953,6 +5159,8 @@ struct spf_query {
   // trace's per-query path / link counts
   uint32_t* d_trace = nullptr;
   size_t trace_words = 0;
+  char* d_tcs = nullptr; // spf_trace_cursor_kernel node states + arenas
+  size_t tcs_bytes = 0;
   uint32_t trace_n = 0, trace_cap = 0;
   uint64_t trace_links = 0, trace_paths = 0;
   std::vector<uint32_t> trace_pc, trace_lc;
@@ -5147,7 +5355,7 @@ void free_query(spf_query* q) {
         (void*)q->d_slab, (void*)q->d_msd, (void*)q->d_base_of,
         (void*)q->d_skip, (void*)q->d_key, (void*)q->d_qctr, (void*)q->d_scatter,
         (void*)q->d_trace, (void*)q->d_big, (void*)q->d_zl, (void*)q->d_zvar,
-        (void*)q->d_ovf, q->narrow ? (void*)q->d_nhb : nullptr}) {
+        (void*)q->d_ovf, q->narrow ? (void*)q->d_nhb : nullptr, (void*)q->d_tcs}) {
     pool_free(p);
   }
   if (q->base) {
@@ -7900,7 +8108,7 @@ int spf_query_trace_paths(
   HIP_TRY(hipSetDevice(g->device));
   // scratch: dests | out_n | out_len | links [count][cap] | ends [count][cap]
   // (OPENR_SPF_TRACE_CAP lowers the per-query capacity: overflow tests)
-  const uint32_t cap = std::max<uint32_t>(1, std::min(kTraceCap, env_flag("OPENR_SPF_TRACE_CAP", kTraceCap)));
+  const uint32_t cap = std::max<uint32_t>(1, std::min(kTraceCap, env_u32("OPENR_SPF_TRACE_CAP", kTraceCap)));
   q->trace_cap = cap;
   const size_t cells = (size_t)count * cap;
   const size_t words = 3 * (size_t)count + 2 * cells;
@@ -7935,8 +8143,35 @@ int spf_query_trace_paths(
   a.nq = count;
   a.cap = cap;
   a.unit = (q->flags & SPF_F_UNIT_METRIC) ? 1u : 0u;
-  hipLaunchKernelGGL(spf_trace_paths_kernel, dim3((count + kTraceWaves - 1) / kTraceWaves),
-                     dim3(64 * kTraceWaves), 0, g->stream, a);
+  if (env_flag("OPENR_SPF_TRACE_CURSOR", 1)) {
+    // cursor DFS: per-wave node states + pathLinks arena (zeroed per launch:
+    // a state's tag is its query index + 1)
+    const uint32_t maxw = g->V > 50000 ? 512u : 1024u;
+    const uint32_t nw = std::min<uint32_t>((count + kTcWaves - 1) / kTcWaves * kTcWaves, maxw);
+    const uint32_t acap = std::max<uint32_t>(1024, std::min<uint32_t>(g->E, 1u << 16));
+    const size_t need = (size_t)nw * g->V * sizeof(uint4) + (size_t)nw * acap * 4;
+    if (q->d_tcs && q->tcs_bytes < need) {
+      HIP_TRY(hipStreamSynchronize(g->stream));
+      pool_free(q->d_tcs);
+      q->d_tcs = nullptr;
+    }
+    if (!q->d_tcs) {
+      HIP_TRY(pool_malloc((void**)&q->d_tcs, need));
+      q->tcs_bytes = need;
+    }
+    TraceCursorArgs ta{};
+    ta.t = a;
+    ta.nstate = reinterpret_cast<uint4*>(q->d_tcs);
+    ta.arena = reinterpret_cast<uint32_t*>(q->d_tcs + (size_t)nw * g->V * sizeof(uint4));
+    ta.arena_cap = acap;
+    ta.V = g->V;
+    HIP_TRY(hipMemsetAsync(q->d_tcs, 0, (size_t)nw * g->V * sizeof(uint4), g->stream));
+    hipLaunchKernelGGL(spf_trace_cursor_kernel, dim3(nw / kTcWaves), dim3(64 * kTcWaves), 0,
+                       g->stream, ta);
+  } else {
+    hipLaunchKernelGGL(spf_trace_paths_kernel, dim3((count + kTraceWaves - 1) / kTraceWaves),
+                       dim3(64 * kTraceWaves), 0, g->stream, a);
+  }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(path_count, a.out_n, (size_t)count * 4, hipMemcpyDeviceToHost,
                          g->stream));

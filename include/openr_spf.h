@@ -119,11 +119,12 @@ int spf_graph_patch_metrics(
  * metrics, in place: link removal / re-addition (LinkState.cpp:421-434
  * removeLink / addLink; the reference drops its whole memo, :712-715) without
  * a new device graph.  A down half-edge stays at its CSR position as a
- * self-loop of its tail (never relaxed, never tight).  Distance queries
- * only: a graph changed this way refuses SPF_F_NEXTHOPS / SPF_F_ORDER
- * (SPF_E_UNSUPPORTED; its distinct-neighbour lists still hold the old
- * heads) — rebuild it for those.  SPF_E_UNSUPPORTED too for 64-bit graphs,
- * metric 0, or metrics the packed edge words cannot hold. */
+ * self-loop of its tail (never relaxed, never tight); the distinct-neighbour
+ * lists (spf_graph_nbrs, the next-hop mask bits) are rebuilt over the up
+ * half-edges, so next-hop queries stay exact.  A graph changed this way
+ * refuses SPF_F_ORDER (SPF_E_UNSUPPORTED) — rebuild it for settle orders.
+ * SPF_E_UNSUPPORTED too for 64-bit graphs, metric 0, or metrics the packed
+ * edge words cannot hold. */
 int spf_graph_set_edges(
     spf_graph* g, uint32_t n, const uint32_t* edge_idx, const uint8_t* up,
     const uint64_t* metric);

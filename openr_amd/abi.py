@@ -392,9 +392,16 @@ class Graph:
         _check(lib.spf_graph_create(C.byref(d), C.byref(h)), "spf_graph_create")
         self.h = h
         self.V = csr.num_nodes
+        import weakref
+
+        self._queries = weakref.WeakSet()  # live queries: destroyed before the graph
 
     def close(self):
         if self.h:
+            # a query reads its graph when it is destroyed (device, stream):
+            # close the ones still alive first
+            for q in list(self._queries):
+                q.close()
             load().spf_graph_destroy(self.h)
             self.h = None
 
@@ -554,6 +561,7 @@ class Query:
         self._keep = keep
         self.n = len(src)
         self.flags = flags
+        graph._queries.add(self)
 
     def close(self):
         if self.h:

@@ -482,7 +482,7 @@ class ShardedAllSources:
             bool(self._lay_up.all()) and len(self._lay_col) == len(old.col)
             and np.array_equal(self._lay_row, old.row_ptr) and np.array_equal(self._lay_col, old.col))
         inplace = None
-        if (not (same_links and layout_is_old) and not self.nexthops
+        if (not (same_links and layout_is_old)
                 and os.environ.get("OPENR_SPF_LINKS_INPLACE", "1") != "0"):
             inplace = self._links_in_place(deltas)
         if same_links and layout_is_old:
@@ -558,9 +558,11 @@ class ShardedAllSources:
         if self.nexthops:
             # next hops of the repaired sources (a source the screen passed
             # keeps them: they are defined by its tight edges alone); a link
-            # set change can add / drop a source's neighbours, which moves
-            # its mask bits, so then every source is recomputed
-            if out.graph_patched:
+            # set change -- rebuilt, or set in place (spf_graph_set_edges
+            # rebuilds the distinct-neighbour lists) -- can add / drop a
+            # source's neighbours, which moves its mask bits, so then every
+            # source is recomputed
+            if out.graph_patched and inplace is None:
                 self._refresh_masks(hit)
             else:
                 self._mask_layout()

@@ -56,7 +56,11 @@ AllSourcesTable::Csr AllSourcesTable::snapshot(const LinkState& ls) const {
   return c;
 }
 
-AllSourcesTable::AllSourcesTable(const LinkState& ls, std::vector<int> devices) {
+AllSourcesTable::AllSourcesTable(const LinkState& ls, std::vector<int> devices)
+    : AllSourcesTable(ls, std::move(devices), false) {}
+
+AllSourcesTable::AllSourcesTable(const LinkState& ls, std::vector<int> devices, bool withNextHops)
+    : withNh_(withNextHops) {
   LinkState::Engine& eng = ls.engine();
   if (eng.exact) {
     throw std::invalid_argument(
@@ -73,6 +77,10 @@ AllSourcesTable::AllSourcesTable(const LinkState& ls, std::vector<int> devices) 
   }
   const uint32_t V = (uint32_t)names_.size();
   const uint32_t n = (uint32_t)devices.size();
+  if (withNh_ && n != 1) {
+    throw std::invalid_argument(
+        "AllSourcesTable: next hops need every neighbour's row beside the source's (one device)");
+  }
   // contiguous source blocks (spf_table_layout's split: n / world each, the
   // first n % world one more)
   uint32_t first = 0;
@@ -96,6 +104,13 @@ AllSourcesTable::AllSourcesTable(const LinkState& ls, std::vector<int> devices) 
     }
     buildGraphs(cur_);
     recompute();
+    if (withNh_) {
+      rowOf_.resize(V);
+      for (uint32_t i = 0; i < V; ++i) {
+        rowOf_[i] = (int32_t)i; // one block: source i's row is row i
+      }
+      refreshMasks({});
+    }
   } catch (...) {
     for (auto& b : blocks_) {
       if (b.graph) {
@@ -103,11 +118,64 @@ AllSourcesTable::AllSourcesTable(const LinkState& ls, std::vector<int> devices) 
       }
       spf_device_free(b.device, b.rows);
     }
+    if (masks_) {
+      spf_device_free(blocks_.front().device, masks_);
+    }
     throw;
   }
 }
 
+void AllSourcesTable::refreshMasks(const std::vector<uint32_t>& idx) {
+  Block& b = blocks_.front();
+  const uint32_t V = (uint32_t)names_.size();
+  if (idx.empty()) {
+    // layout from the graph's current distinct-neighbour lists
+    maskWords_.assign(V, 1);
+    maskOff_.assign(V + 1, 0);
+    for (uint32_t i = 0; i < V; ++i) {
+      const int nb = spf_graph_num_nbrs(b.graph, i);
+      check(nb < 0 ? nb : SPF_OK, "spf_graph_num_nbrs");
+      maskWords_[i] = std::max<uint32_t>(1, ((uint32_t)nb + 63) / 64);
+      maskOff_[i + 1] = maskOff_[i] + (uint64_t)V * maskWords_[i];
+    }
+    const size_t bytes = std::max<size_t>(maskOff_[V], 1) * 8;
+    if (bytes > maskBytes_) {
+      if (masks_) {
+        spf_device_free(b.device, masks_);
+        masks_ = nullptr;
+      }
+      void* p = nullptr;
+      check(spf_device_alloc(b.device, bytes, &p), "spf_device_alloc");
+      masks_ = static_cast<uint64_t*>(p);
+      maskBytes_ = bytes;
+    }
+    if (!V) {
+      return;
+    }
+    std::vector<uint32_t> all(V);
+    for (uint32_t i = 0; i < V; ++i) {
+      all[i] = i;
+    }
+    check(spf_table_nexthops(b.graph, b.rows, V, rowOf_.data(), V, all.data(), masks_,
+                             maskOff_.data()),
+          "spf_table_nexthops");
+    return;
+  }
+  std::vector<uint32_t> srcs(idx.size());
+  std::vector<uint64_t> off(idx.size());
+  for (size_t k = 0; k < idx.size(); ++k) {
+    srcs[k] = b.sources[idx[k]];
+    off[k] = maskOff_[srcs[k]];
+  }
+  check(spf_table_nexthops(b.graph, b.rows, V, rowOf_.data(), (uint32_t)srcs.size(), srcs.data(),
+                           masks_, off.data()),
+        "spf_table_nexthops");
+}
+
 AllSourcesTable::~AllSourcesTable() {
+  if (masks_ && !blocks_.empty()) {
+    spf_device_free(blocks_.front().device, masks_);
+  }
   for (auto& b : blocks_) {
     if (b.graph) {
       spf_graph_destroy(b.graph);
@@ -270,6 +338,9 @@ AllSourcesTable::UpdateStats AllSourcesTable::update(const LinkState& ls) {
       throw std::invalid_argument("AllSourcesTable::update: the new topology needs 64-bit rows");
     }
     recompute();
+    if (withNh_) {
+      refreshMasks({});
+    }
     stale_ = false;
     st.affected = (uint32_t)names_.size();
     st.spfMs = lastSpfMs_;
@@ -301,7 +372,9 @@ AllSourcesTable::UpdateStats AllSourcesTable::update(const LinkState& ls) {
   std::vector<uint32_t> edges;
   std::vector<uint8_t> up;
   std::vector<uint64_t> w;
+  bool linkSetChanged = true; // next hops: neighbour lists (mask bits) may move
   if (sameLinks && layoutIsCur) {
+    linkSetChanged = false;
     std::vector<uint32_t> ch;
     std::vector<uint64_t> cm;
     for (uint32_t e = 0; e < nc.metric.size(); ++e) {
@@ -345,6 +418,7 @@ AllSourcesTable::UpdateStats AllSourcesTable::update(const LinkState& ls) {
   // screen, then repair (or recompute) the affected rows of each block
   lastSpfMs_ = 0;
   bool anyRelaxed = false, anyRecomputed = false;
+  std::vector<uint32_t> hitRows; // block-local rows repaired (one block with next hops)
   for (auto& b : blocks_) {
     if (!b.count || deltas.empty()) {
       continue;
@@ -363,6 +437,9 @@ AllSourcesTable::UpdateStats AllSourcesTable::update(const LinkState& ls) {
       }
     }
     st.affected += (uint32_t)idx.size();
+    if (withNh_) {
+      hitRows = idx;
+    }
     if (idx.empty()) {
       continue;
     }
@@ -380,8 +457,57 @@ AllSourcesTable::UpdateStats AllSourcesTable::update(const LinkState& ls) {
     st.spfMs += msSince(tr);
   }
   st.relaxed = anyRelaxed && !anyRecomputed;
+  if (withNh_ && !deltas.empty()) {
+    // a source the screen passed keeps its masks (defined by its tight edges
+    // alone) unless its neighbour list moved; a link-set change may move any
+    const auto tn = Clock::now();
+    if (linkSetChanged) {
+      refreshMasks({});
+    } else if (!hitRows.empty()) {
+      refreshMasks(hitRows);
+    }
+    st.nextHopsMs = msSince(tn);
+  }
   st.wallMs = msSince(t0);
   return st;
+}
+
+std::vector<std::string> AllSourcesTable::nextHops(const std::string& src,
+                                                   const std::string& dst) const {
+  if (!withNh_) {
+    throw std::logic_error("AllSourcesTable::nextHops: table built without next hops");
+  }
+  if (stale_) {
+    throw std::logic_error("AllSourcesTable::nextHops: the last update() failed, the rows are stale");
+  }
+  const auto s = ids_.find(src), d = ids_.find(dst);
+  if (s == ids_.end() || d == ids_.end()) {
+    throw std::out_of_range("AllSourcesTable::nextHops: unknown node");
+  }
+  const Block& b = blocks_.front();
+  const uint32_t V = (uint32_t)names_.size(), W = maskWords_[s->second];
+  std::vector<uint64_t> m(W);
+  check(spf_device_memcpy(b.device, m.data(), masks_ + maskOff_[s->second] + (size_t)d->second * W,
+                          (size_t)W * 8, SPF_COPY_D2H),
+        "spf_device_memcpy");
+  const int nn = spf_graph_num_nbrs(b.graph, s->second);
+  check(nn < 0 ? nn : SPF_OK, "spf_graph_num_nbrs");
+  std::vector<uint32_t> nb(std::max(nn, 0));
+  if (nn > 0) {
+    check(spf_graph_nbrs(b.graph, s->second, nb.data()), "spf_graph_nbrs");
+  }
+  std::vector<std::string> out;
+  for (uint32_t w = 0; w < W; ++w) {
+    for (uint64_t x = m[w]; x; x &= x - 1) {
+      const uint32_t bit = w * 64 + (uint32_t)__builtin_ctzll(x);
+      if (bit < nb.size()) {
+        out.push_back(names_[nb[bit]]);
+      }
+    }
+  }
+  (void)V;
+  std::sort(out.begin(), out.end());
+  return out;
 }
 
 std::vector<uint32_t> AllSourcesTable::row(const std::string& src) const {

@@ -47,7 +47,7 @@ class AllSourcesTable {
     uint32_t affected{0};    // rows recomputed or repaired, over all blocks
     bool graphPatched{false}; // device graphs patched in place (no rebuild)
     bool relaxed{false};      // rows repaired in place (spf_table_repair)
-    double diffMs{0}, graphMs{0}, screenMs{0}, spfMs{0}, wallMs{0};
+    double diffMs{0}, graphMs{0}, screenMs{0}, spfMs{0}, nextHopsMs{0}, wallMs{0};
   };
 
   // Every node of `ls`'s area as a source, link metrics (getSpfResult(node,
@@ -55,6 +55,12 @@ class AllSourcesTable {
   // Throws std::invalid_argument for graphs that need 64-bit rows (metric 0,
   // sums that may pass 32 bits) and std::runtime_error on engine failures.
   explicit AllSourcesTable(const LinkState& ls, std::vector<int> devices = {});
+  // withNextHops: also every source's ECMP next-hop masks (getSpfResult's
+  // nextHops per node), kept current under churn from the table rows
+  // (spf_table_nexthops, the all-sources rule).  One device only: a source's
+  // neighbours' rows must sit beside its own (std::invalid_argument with
+  // several devices).
+  AllSourcesTable(const LinkState& ls, std::vector<int> devices, bool withNextHops);
   ~AllSourcesTable();
   AllSourcesTable(const AllSourcesTable&) = delete;
   AllSourcesTable& operator=(const AllSourcesTable&) = delete;
@@ -75,6 +81,10 @@ class AllSourcesTable {
   std::vector<uint32_t> row(const std::string& src) const;
   // getMetricFromAToB of the memoized SpfResult (nullopt if unreachable)
   std::optional<uint64_t> distance(const std::string& src, const std::string& dst) const;
+  // next-hop node names from `src` towards `dst` (sorted by name; empty if
+  // unreachable or src == dst); std::logic_error without withNextHops
+  std::vector<std::string> nextHops(const std::string& src, const std::string& dst) const;
+  bool hasNextHops() const { return withNh_; }
   double lastSpfMs() const { return lastSpfMs_; }
 
  private:
@@ -97,6 +107,9 @@ class AllSourcesTable {
   void computeBlock(Block& b, const std::vector<uint32_t>& idx, bool scatter);
   bool linksInPlace(const std::vector<spf_edge_delta>& deltas, std::vector<uint32_t>& edges,
                     std::vector<uint8_t>& up, std::vector<uint64_t>& w);
+  // (re)compute the masks of block-local rows idx (empty: every row; the
+  // layout is re-derived from the graph's current neighbour lists)
+  void refreshMasks(const std::vector<uint32_t>& idx);
 
   std::vector<std::string> names_;
   std::unordered_map<std::string, uint32_t> ids_;
@@ -112,6 +125,13 @@ class AllSourcesTable {
   // needs 64-bit rows) left rows of the old topology: the next update()
   // rebuilds and recomputes, row() refuses until then
   bool stale_{false};
+  // next-hop masks (single block): device words, per-source word offsets
+  bool withNh_{false};
+  uint64_t* masks_{nullptr};
+  size_t maskBytes_{0};
+  std::vector<uint64_t> maskOff_;
+  std::vector<uint32_t> maskWords_;
+  std::vector<int32_t> rowOf_;
 };
 
 } // namespace openr

@@ -356,10 +356,12 @@ PYBIND11_MODULE(_openr_spf, m) {
       .def("is_border", &AllAreasRouteTable::isBorder);
 
   py::class_<AllSourcesTable>(m, "AllSourcesTable")
-      .def(py::init([](const AreaMapHolder& areas, const std::string& area, std::vector<int> devices) {
-             return std::make_unique<AllSourcesTable>(areas.map.at(area), devices);
+      .def(py::init([](const AreaMapHolder& areas, const std::string& area, std::vector<int> devices,
+                       bool nexthops) {
+             return std::make_unique<AllSourcesTable>(areas.map.at(area), devices, nexthops);
            }),
-           py::arg("areas"), py::arg("area"), py::arg("devices") = std::vector<int>{})
+           py::arg("areas"), py::arg("area"), py::arg("devices") = std::vector<int>{},
+           py::arg("nexthops") = false)
       .def_property_readonly("num_nodes", &AllSourcesTable::numNodes)
       .def_property_readonly("num_devices", &AllSourcesTable::numDevices)
       .def_property_readonly("node_names", &AllSourcesTable::nodeNames)
@@ -376,11 +378,14 @@ PYBIND11_MODULE(_openr_spf, m) {
         d["graph_ms"] = st.graphMs;
         d["screen_ms"] = st.screenMs;
         d["spf_ms"] = st.spfMs;
+        d["nexthops_ms"] = st.nextHopsMs;
         d["wall_ms"] = st.wallMs;
         return d;
       })
       .def("row", &AllSourcesTable::row)
-      .def("distance", &AllSourcesTable::distance);
+      .def("distance", &AllSourcesTable::distance)
+      .def("next_hops", &AllSourcesTable::nextHops)
+      .def_property_readonly("has_next_hops", &AllSourcesTable::hasNextHops);
 
   py::class_<AllNodesRouteTable>(m, "AllNodesRouteTable")
       .def(py::init([](const AreaMapHolder& areas, const std::string& area, const PrefixState& ps,

@@ -5068,6 +5068,7 @@ struct spf_graph {
   std::vector<uint32_t> col_orig;
   std::vector<uint8_t> edge_up;
   bool links_patched = false;
+  size_t nbr_cap = 0; // entries of d_nbrs / d_nbr_w (set_edges re-sizes them)
   // spf_table_repair's delta block + per-workgroup queues, kept between
   // calls (a 100k-node graph needs 200 MB: allocating it per churn event
   // cost more than the screen)
@@ -5381,6 +5382,52 @@ void free_query(spf_query* q) {
     }
   }
   delete q;
+}
+
+// Distinct neighbours per node over its UP half-edges (ascending id = name
+// order) and each half-edge's slot among them (sorted unique neighbours of u
+// staged in scratch[row[u] ..], counted, then packed; node blocks on the host
+// pool).  A half-edge taken down in place (spf_graph_set_edges) is no
+// neighbour; its slot is 0 (it is never tight, so never read).
+void build_nbr_lists(spf_graph* g) {
+  const uint32_t V = g->V, E = g->E;
+  const bool patched = !g->edge_up.empty();
+  g->nbr_off.assign(V + 1, 0);
+  g->slot.assign(E, 0);
+  std::vector<uint32_t> scratch(E);
+  std::vector<uint32_t> cnt(V, 0);
+  const uint32_t nblk = (V + kHostBlock - 1) / kHostBlock;
+  const unsigned nth = openr::hostThreads(E, 1u << 16);
+  openr::parallelFor(nblk, nth, [&](size_t b, unsigned) {
+    const uint32_t u1 = std::min<uint32_t>(V, (uint32_t)(b + 1) * kHostBlock);
+    for (uint32_t u = (uint32_t)b * kHostBlock; u < u1; ++u) {
+      uint32_t* lo = scratch.data() + g->row[u];
+      uint32_t* hi = lo;
+      for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
+        if (!patched || g->edge_up[e]) {
+          *hi++ = g->col[e];
+        }
+      }
+      std::sort(lo, hi);
+      hi = std::unique(lo, hi);
+      cnt[u] = (uint32_t)(hi - lo);
+      for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
+        if (!patched || g->edge_up[e]) {
+          g->slot[e] = (uint32_t)(std::lower_bound(lo, hi, g->col[e]) - lo);
+        }
+      }
+    }
+  }, 1);
+  for (uint32_t u = 0; u < V; ++u) {
+    g->nbr_off[u + 1] = g->nbr_off[u] + cnt[u];
+  }
+  g->nbrs.resize(g->nbr_off[V]);
+  openr::parallelFor(nblk, nth, [&](size_t b, unsigned) {
+    const uint32_t u1 = std::min<uint32_t>(V, (uint32_t)(b + 1) * kHostBlock);
+    for (uint32_t u = (uint32_t)b * kHostBlock; u < u1; ++u) {
+      std::copy_n(scratch.data() + g->row[u], cnt[u], g->nbrs.data() + g->nbr_off[u]);
+    }
+  }, 1);
 }
 
 // Upper bound on the hop count of some valid path from any node to any node
@@ -6089,39 +6136,7 @@ int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
     }
   }
   // distinct neighbours per node (ascending id = name order) and edge slots
-  // (sorted unique neighbours of u staged in scratch[row[u] ..], counted,
-  // then packed; node blocks on the host pool)
-  g->nbr_off.assign(V + 1, 0);
-  g->slot.assign(E, 0);
-  {
-    std::vector<uint32_t> scratch(g->col);
-    const uint32_t nblk = (V + kHostBlock - 1) / kHostBlock;
-    const unsigned nth = openr::hostThreads(E, 1u << 16);
-    openr::parallelFor(nblk, nth, [&](size_t b, unsigned) {
-      const uint32_t u1 = std::min<uint32_t>(V, (uint32_t)(b + 1) * kHostBlock);
-      for (uint32_t u = (uint32_t)b * kHostBlock; u < u1; ++u) {
-        uint32_t* lo = scratch.data() + g->row[u];
-        uint32_t* hi = scratch.data() + g->row[u + 1];
-        std::sort(lo, hi);
-        hi = std::unique(lo, hi);
-        g->nbr_off[u + 1] = (uint32_t)(hi - lo);
-        for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
-          g->slot[e] = (uint32_t)(std::lower_bound(lo, hi, g->col[e]) - lo);
-        }
-      }
-    }, 1);
-    for (uint32_t u = 0; u < V; ++u) {
-      g->nbr_off[u + 1] += g->nbr_off[u];
-    }
-    g->nbrs.resize(g->nbr_off[V]);
-    openr::parallelFor(nblk, nth, [&](size_t b, unsigned) {
-      const uint32_t u1 = std::min<uint32_t>(V, (uint32_t)(b + 1) * kHostBlock);
-      for (uint32_t u = (uint32_t)b * kHostBlock; u < u1; ++u) {
-        std::copy_n(scratch.data() + g->row[u], g->nbr_off[u + 1] - g->nbr_off[u],
-                    g->nbrs.data() + g->nbr_off[u]);
-      }
-    }, 1);
-  }
+  build_nbr_lists(g);
   // lanes per node: the median degree, rounded to a power of two in [4, 64]
   {
     std::vector<uint32_t> deg(V);
@@ -6169,6 +6184,7 @@ int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
       (s = upload_weights(g))) {
     return bail(s);
   }
+  g->nbr_cap = g->nbrs.size();
   {
     std::vector<uint32_t> half(2 * (size_t)g->L, kInf32);
     for (uint32_t e = 0; e < E; ++e) {
@@ -6338,8 +6354,41 @@ int spf_graph_set_edges(
   rescan_scalars(g);
   g->ecc_est = 0;
   g->links_patched = true;
+  // distinct-neighbour lists over the up half-edges (a neighbour whose every
+  // link went down leaves its source's list; one coming back re-enters it),
+  // edge slots and cheapest metric per neighbour, so next-hop queries stay
+  // exact on the patched graph; re-uploaded whole (O(E), no graph rebuild)
+  build_nbr_lists(g);
+  g->nbr_w.assign(g->nbrs.size(), 0xFFFFFFFFu);
+  for (uint32_t u = 0; u < g->V; ++u) {
+    for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
+      if (g->edge_up[e]) {
+        uint32_t& w = g->nbr_w[g->nbr_off[u] + g->slot[e]];
+        w = std::min<uint32_t>(w, (uint32_t)std::min<uint64_t>(g->w64[e], 0xFFFFFFFFull));
+      }
+    }
+  }
+  {
+    const size_t nn = g->nbrs.size();
+    if (nn != g->nbr_cap) {
+      (void)hipFree(g->d_nbrs);
+      (void)hipFree(g->d_nbr_w);
+      g->d_nbrs = nullptr;
+      g->d_nbr_w = nullptr;
+      HIP_TRY(hipMalloc((void**)&g->d_nbrs, std::max<size_t>(nn, 1) * 4));
+      HIP_TRY(hipMalloc((void**)&g->d_nbr_w, std::max<size_t>(nn, 1) * 4));
+      g->nbr_cap = nn;
+    }
+    HIP_TRY(hipMemcpy(g->d_slot, g->slot.data(), (size_t)g->E * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(g->d_nbr_off, g->nbr_off.data(), ((size_t)g->V + 1) * 4,
+                      hipMemcpyHostToDevice));
+    if (nn) {
+      HIP_TRY(hipMemcpy(g->d_nbrs, g->nbrs.data(), nn * 4, hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(g->d_nbr_w, g->nbr_w.data(), nn * 4, hipMemcpyHostToDevice));
+    }
+  }
   PatchArgs a{};
-  uint32_t* arrays[kPatch32] = {g->d_wout, g->d_win, g->d_nbr_w, g->d_cw, g->d_col,
+  uint32_t* arrays[kPatch32] = {g->d_wout, g->d_win, nullptr, g->d_cw, g->d_col,
                                 reinterpret_cast<uint32_t*>(g->d_sell)};
   std::vector<uint32_t> pk;
   for (int k = 0; k < kPatch32; ++k) {
@@ -6511,9 +6560,9 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
   const bool unit = desc->flags & SPF_F_UNIT_METRIC;
   const bool want_nh = desc->flags & SPF_F_NEXTHOPS;
   const bool want_order = desc->flags & SPF_F_ORDER;
-  if ((want_nh || want_order) && g->links_patched) {
+  if (want_order && g->links_patched) {
     return bail(fail(SPF_E_UNSUPPORTED,
-                     "next hops / settle order on a graph whose links were set in place "
+                     "settle order on a graph whose links were set in place "
                      "(spf_graph_set_edges): rebuild the graph"));
   }
 
@@ -6702,8 +6751,11 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       if (q->dlds) {
         q->dlds_lds = dl_lds;
         q->dlds_grid = std::min<uint32_t>(std::max<uint32_t>(nq, 1), (uint32_t)g->num_cus);
-        // bucket width: the delta-stepping Delta (mean metric / mean degree)
-        q->dlds_shift = dstep_bucket_shift(g, true);
+        // bucket width: 8x the delta-stepping Delta (mean metric / mean
+        // degree): with the row in LDS a bucket scan is cheap, and wider
+        // buckets mean fewer phases (100k WAN, profiles/r04c: 2^4 9.5,
+        // 2^5 7.7, 2^7 6.7 us/SPF)
+        q->dlds_shift = std::min<uint32_t>(dstep_bucket_shift(g, false) + 1, 11);
         if (const char* env = getenv("OPENR_SPF_DSTEP_LSHIFT")) {
           q->dlds_shift = (uint32_t)std::min(11, std::max(0, atoi(env)));
         }
@@ -8516,11 +8568,6 @@ int spf_table_nexthops(
   }
   if (g->exact) {
     return fail(SPF_E_UNSUPPORTED, "64-bit rows");
-  }
-  if (g->links_patched) {
-    // the distinct-neighbour lists / cheapest metrics still describe the
-    // links before spf_graph_set_edges (as spf_query_create refuses)
-    return fail(SPF_E_UNSUPPORTED, "next hops on a graph whose links were set in place");
   }
   if (pitch < g->V || pitch > 0xFFFFFFFFull) {
     return fail(SPF_E_INVALID, "pitch");

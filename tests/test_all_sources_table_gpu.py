@@ -160,3 +160,55 @@ def test_all_sources_table_parallel_link_flaps(mods):
     assert patched >= 3
     t.recompute()
     _check_rows(E, O, t, ea, oa)
+
+
+def _check_next_hops(t, oa):
+    names = list(t.node_names)
+    for src in names:
+        ref = oa["0"].getSpfResult(src, True)
+        for dst in names:
+            want = sorted(ref[dst][1]) if dst in ref and dst != src else []
+            assert t.next_hops(src, dst) == want, (src, dst)
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_all_sources_table_next_hops_under_churn(mods, seed):
+    """AllSourcesTable(nexthops=True): every source's ECMP next hops
+    (getSpfResult's nextHops, LinkState.cpp:842-871) kept current under
+    drains, metric changes and link flaps -- the flaps set in place
+    (spf_graph_set_edges rebuilds the distinct-neighbour lists, so next-hop
+    queries stay exact on the patched graph) -- against the oracle at every
+    step."""
+    E, O = mods
+    names, adj_dbs, prefix_dbs = RZ.random_network(
+        4100 + seed, n_nodes=40, n_links=100, overload_prob=0.05, link_overload_prob=0.0)
+    have = {d.thisNodeName for d in adj_dbs["0"]}
+    for n in names:
+        if n not in have:
+            adj_dbs["0"].append(T.createAdjDb(n, [], 0, False, "0"))
+    ea, _ = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    oa, _ = RZ.load(O, adj_dbs, prefix_dbs, seed)
+    t = E.AllSourcesTable(ea, "0", [0], True)
+    assert t.has_next_hops
+    _check_rows(E, O, t, ea, oa)
+    _check_next_hops(t, oa)
+    rng = random.Random(seed)
+    dbs = {d.thisNodeName: copy.deepcopy(d) for d in adj_dbs["0"]}
+    patched = 0
+    for step in range(12):
+        db = rng.choice([d for d in dbs.values() if d.adjacencies])
+        r = rng.random()
+        if r < 0.25:
+            db.isOverloaded = not db.isOverloaded
+        elif r < 0.5:
+            rng.choice(db.adjacencies).metric = rng.randint(1, 20)
+        else:
+            adj = rng.choice(db.adjacencies)  # link down / back up (flap)
+            adj.isOverloaded = not adj.isOverloaded
+        ea["0"].updateAdjacencyDatabase(db)
+        oa["0"].updateAdjacencyDatabase(db)
+        st = t.update(ea, "0")
+        patched += st["graph_patched"]
+        _check_rows(E, O, t, ea, oa)
+        _check_next_hops(t, oa)
+    assert patched > 0

@@ -77,6 +77,7 @@ def test_ldsrow_vs_oracle_and_hbm_rows(gpu_ready, seed, wmax, monkeypatch):
     ref = g.query(srcs, 0).run()
     assert ref.kernel == "dstep"
     assert (_rows(ref, len(srcs), V) == want).all()
+    ref.close()
     monkeypatch.delenv("OPENR_SPF_DSTEP_LDSROW")
     for shift in (None, "0", "3", "7", "11"):
         if shift is None:

@@ -1514,11 +1514,16 @@ __global__ __launch_bounds__(BS) void spf_dlds_kernel(DldsArgs a) {
                 const uint32_t w = v[j] / 5, sh = 12 * (v[j] % 5);
                 uint64_t o = old[j];
                 uint32_t cur = (uint32_t)(o >> sh) & 0xFFFu;
-                if (c[j] >= cur) {
+                if (c[j] > kDlMaxDist) {
+                  // an unreached node whose first value does not fit 12 bits:
+                  // the source's row goes to the HBM-row pass (a reached node
+                  // holds a smaller value, so c is no improvement there)
+                  if (cur == kDlUnreached) {
+                    ctl[3] = 1;
+                  }
                   continue;
                 }
-                if (c[j] > kDlMaxDist) {
-                  ctl[3] = 1; // cur is kDlUnreached: the value does not fit
+                if (c[j] >= cur) {
                   continue;
                 }
                 bool done = false;

@@ -1364,7 +1364,7 @@ __device__ __forceinline__ uint32_t dl_field(uint64_t x, uint32_t k) {
   return (uint32_t)(x >> (12 * k)) & 0xFFFu;
 }
 
-template <uint32_t BS, uint32_t G>
+template <uint32_t BS, uint32_t G, bool PF>
 __global__ __launch_bounds__(BS) void spf_dlds_kernel(DldsArgs a) {
   extern __shared__ __align__(16) uint64_t fld[];
   const uint32_t V = a.V, nw = (V + 4) / 5;
@@ -1457,10 +1457,88 @@ __global__ __launch_bounds__(BS) void spf_dlds_kernel(DldsArgs a) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
       }
-      // EXPAND qc[0, len): a group's next node id and its row range are
-      // loaded while the current node's edges are in flight
+      // EXPAND qc[0, len).  PF: a group keeps two nodes ahead in flight —
+      // the next node's edge chunks and the one after's row range are loaded
+      // before the current node's relaxations (LDS work) run, so a group
+      // waits for at most one HBM round trip per node instead of two
+      // (header, then chunks); without PF only the next header is early.
       uint32_t* cnt = ctl + ph;
       {
+        // relax the (up to) 8 edges of a lane's two chunks of node u
+        auto relax_chunks = [&](const uint4 (&x)[2], uint32_t kc, uint32_t beg, uint32_t end,
+                                uint32_t du) {
+          uint32_t v[8], c[8];
+#pragma unroll
+          for (uint32_t h = 0; h < 2; ++h) {
+            const uint32_t kk = kc + h * G;
+            const uint32_t xs[4] = {x[h].x, x[h].y, x[h].z, x[h].w};
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+              const uint32_t e = 4 * kk + j;
+              const bool ok = e >= beg && e < end;
+              v[4 * h + j] = ok ? (xs[j] & mask) : kInf32;
+              c[4 * h + j] = du + (xs[j] >> a.cwbits);
+            }
+          }
+          uint64_t old[8];
+#pragma unroll
+          for (uint32_t j = 0; j < 8; ++j) {
+            old[j] = v[j] != kInf32 ? ld(v[j] / 5) : 0ull;
+          }
+#pragma unroll
+          for (uint32_t j = 0; j < 8; ++j) {
+            if (v[j] == kInf32) {
+              continue;
+            }
+            const uint32_t w = v[j] / 5, sh = 12 * (v[j] % 5);
+            uint64_t o = old[j];
+            uint32_t cur = (uint32_t)(o >> sh) & 0xFFFu;
+            if (c[j] > kDlMaxDist) {
+              // an unreached node whose first value does not fit 12 bits:
+              // the source's row goes to the HBM-row pass (a reached node
+              // holds a smaller value, so c is no improvement there)
+              if (cur == kDlUnreached) {
+                ctl[3] = 1;
+              }
+              continue;
+            }
+            if (c[j] >= cur) {
+              continue;
+            }
+            bool done = false;
+            while (!done && c[j] < cur) {
+              const uint64_t nv = (o & ~(0xFFFull << sh)) | ((uint64_t)c[j] << sh);
+              const uint64_t p = atomicCAS((unsigned long long*)(fld + w),
+                                           (unsigned long long)o, (unsigned long long)nv);
+              done = p == o;
+              o = p;
+              cur = (uint32_t)(o >> sh) & 0xFFFu;
+            }
+            st[4] += stats;
+            if (done) {
+              st[5] += stats;
+              if (c[j] <= hi) {
+                // lowered into the bucket: expanded again next phase (a
+                // full queue drops the id; the bucket is rescanned then)
+                const uint32_t slot = atomicAdd(cnt, 1u);
+                if (slot < V) {
+                  qn[slot] = v[j];
+                }
+              }
+            }
+          }
+        };
+        auto load_chunks = [&](uint32_t kc, uint32_t end, uint4 (&x)[2]) {
+#pragma unroll
+          for (uint32_t h = 0; h < 2; ++h) {
+            const uint32_t kk = kc + h * G;
+            x[h] = 4 * kk < end ? reinterpret_cast<const uint4*>(a.cw)[kk] : make_uint4(0, 0, 0, 0);
+          }
+        };
+        // the source, or a transit node (overloaded: recorded, never transited)
+        auto expands = [&](uint32_t u, uint32_t trb) {
+          return u == src || ((trb >> (u & 31)) & 1u);
+        };
         uint32_t i = grp;
         uint32_t u = i < len ? qc[i] : kInf32;
         uint32_t nu = i + ngrp < len ? qc[i + ngrp] : kInf32;
@@ -1470,92 +1548,70 @@ __global__ __launch_bounds__(BS) void spf_dlds_kernel(DldsArgs a) {
           end = a.row[u + 1];
           trb = a.trbits[u >> 5];
         }
-        while (u != kInf32) {
-          const uint32_t nnu = i + 2 * ngrp < len ? qc[i + 2 * ngrp] : kInf32;
-          uint32_t nbeg = 0, nend = 0, ntrb = 0;
+        uint4 xc[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+        uint32_t nbeg = 0, nend = 0, ntrb = 0;
+        if constexpr (PF) {
+          if (u != kInf32 && expands(u, trb)) {
+            load_chunks((beg >> 2) + lg, end, xc);
+          }
           if (nu != kInf32) {
             nbeg = a.row[nu];
             nend = a.row[nu + 1];
             ntrb = a.trbits[nu >> 5];
           }
-          // the source, or a transit node (overloaded: recorded, never transited)
-          if (u == src || ((trb >> (u & 31)) & 1u)) {
+        }
+        while (u != kInf32) {
+          const uint32_t nnu = i + 2 * ngrp < len ? qc[i + 2 * ngrp] : kInf32;
+          uint4 xn[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+          uint32_t bb = 0, ee = 0, tt = 0; // the node after next (PF), else the next
+          if constexpr (PF) {
+            if (nu != kInf32 && expands(nu, ntrb)) {
+              load_chunks((nbeg >> 2) + lg, nend, xn);
+            }
+            if (nnu != kInf32) {
+              bb = a.row[nnu];
+              ee = a.row[nnu + 1];
+              tt = a.trbits[nnu >> 5];
+            }
+          } else if (nu != kInf32) {
+            bb = a.row[nu];
+            ee = a.row[nu + 1];
+            tt = a.trbits[nu >> 5];
+          }
+          if (expands(u, trb)) {
             const uint32_t du = dl_field(ld(u / 5), u % 5);
             if (stats && lg == 0) {
               st[0] += 1;
               st[1] += end - beg;
             }
-            for (uint32_t kc = (beg >> 2) + lg; 4 * kc < end; kc += 2 * G) {
-              uint32_t v[8], c[8];
-#pragma unroll
-              for (uint32_t h = 0; h < 2; ++h) {
-                const uint32_t kk = kc + h * G;
-                const uint4 x = 4 * kk < end ? reinterpret_cast<const uint4*>(a.cw)[kk]
-                                             : make_uint4(0, 0, 0, 0);
-                const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-                for (uint32_t j = 0; j < 4; ++j) {
-                  const uint32_t e = 4 * kk + j;
-                  const bool ok = e >= beg && e < end;
-                  v[4 * h + j] = ok ? (xs[j] & mask) : kInf32;
-                  c[4 * h + j] = du + (xs[j] >> a.cwbits);
-                }
-              }
-              uint64_t old[8];
-#pragma unroll
-              for (uint32_t j = 0; j < 8; ++j) {
-                old[j] = v[j] != kInf32 ? ld(v[j] / 5) : 0ull;
-              }
-#pragma unroll
-              for (uint32_t j = 0; j < 8; ++j) {
-                if (v[j] == kInf32) {
-                  continue;
-                }
-                const uint32_t w = v[j] / 5, sh = 12 * (v[j] % 5);
-                uint64_t o = old[j];
-                uint32_t cur = (uint32_t)(o >> sh) & 0xFFFu;
-                if (c[j] > kDlMaxDist) {
-                  // an unreached node whose first value does not fit 12 bits:
-                  // the source's row goes to the HBM-row pass (a reached node
-                  // holds a smaller value, so c is no improvement there)
-                  if (cur == kDlUnreached) {
-                    ctl[3] = 1;
-                  }
-                  continue;
-                }
-                if (c[j] >= cur) {
-                  continue;
-                }
-                bool done = false;
-                while (!done && c[j] < cur) {
-                  const uint64_t nv = (o & ~(0xFFFull << sh)) | ((uint64_t)c[j] << sh);
-                  const uint64_t p = atomicCAS((unsigned long long*)(fld + w),
-                                               (unsigned long long)o, (unsigned long long)nv);
-                  done = p == o;
-                  o = p;
-                  cur = (uint32_t)(o >> sh) & 0xFFFu;
-                }
-                st[4] += stats;
-                if (done) {
-                  st[5] += stats;
-                  if (c[j] <= hi) {
-                    // lowered into the bucket: expanded again next phase (a
-                    // full queue drops the id; the bucket is rescanned then)
-                    const uint32_t slot = atomicAdd(cnt, 1u);
-                    if (slot < V) {
-                      qn[slot] = v[j];
-                    }
-                  }
-                }
-              }
+            uint32_t kc = (beg >> 2) + lg;
+            if constexpr (PF) {
+              relax_chunks(xc, kc, beg, end, du);
+              kc += 2 * G;
+            }
+            for (; 4 * kc < end; kc += 2 * G) {
+              uint4 x[2];
+              load_chunks(kc, end, x);
+              relax_chunks(x, kc, beg, end, du);
             }
           }
           i += ngrp;
           u = nu;
           nu = nnu;
-          beg = nbeg;
-          end = nend;
-          trb = ntrb;
+          if constexpr (PF) {
+            beg = nbeg;
+            end = nend;
+            trb = ntrb;
+            nbeg = bb;
+            nend = ee;
+            ntrb = tt;
+            xc[0] = xn[0];
+            xc[1] = xn[1];
+          } else {
+            beg = bb;
+            end = ee;
+            trb = tt;
+          }
         }
       }
       // the next phase's counter was last read two phases ago (before the
@@ -7249,16 +7305,19 @@ int launch_dlds(spf_query* q) {
     HIP_TRY(hipMalloc((void**)&a.stats, 8 * sizeof(unsigned long long)));
     HIP_TRY(hipMemsetAsync(a.stats, 0, 8 * sizeof(unsigned long long), g->stream));
   }
-  auto kern = spf_dlds_kernel<1024, 4>;
+  // lanes per node (OPENR_SPF_DSTEP_LG 1/2/4/8) and the two-node prefetch
+  // (OPENR_SPF_DSTEP_LPF=0 disables)
+  const bool pf = env_flag("OPENR_SPF_DSTEP_LPF", 1);
+  auto kern = pf ? spf_dlds_kernel<1024, 4, true> : spf_dlds_kernel<1024, 4, false>;
   switch (env_u32("OPENR_SPF_DSTEP_LG", 4)) {
   case 1:
-    kern = spf_dlds_kernel<1024, 1>;
+    kern = pf ? spf_dlds_kernel<1024, 1, true> : spf_dlds_kernel<1024, 1, false>;
     break;
   case 2:
-    kern = spf_dlds_kernel<1024, 2>;
+    kern = pf ? spf_dlds_kernel<1024, 2, true> : spf_dlds_kernel<1024, 2, false>;
     break;
   case 8:
-    kern = spf_dlds_kernel<1024, 8>;
+    kern = pf ? spf_dlds_kernel<1024, 8, true> : spf_dlds_kernel<1024, 8, false>;
     break;
   default:
     break;

@@ -24,7 +24,8 @@ sys.path.insert(0, ROOT)
 KNOBS = ("OPENR_SPF_DSTEP_FINE", "OPENR_SPF_DSTEP_NORET", "OPENR_SPF_DSTEP_SHIFT",
          "OPENR_SPF_DSTEP_G", "OPENR_SPF_DSTEP_PACK", "OPENR_SPF_DSTEP_STATS",
          "OPENR_SPF_DSTEP_HASH", "OPENR_SPF_DSTEP_HCAP", "OPENR_SPF_DSTEP_HCHUNK",
-         "OPENR_SPF_DSTEP_LDSROW", "OPENR_SPF_DSTEP_LSHIFT")
+         "OPENR_SPF_DSTEP_LDSROW", "OPENR_SPF_DSTEP_LSHIFT", "OPENR_SPF_DSTEP_LG",
+         "OPENR_SPF_DSTEP_LPF")
 
 
 def main():

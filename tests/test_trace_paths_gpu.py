@@ -119,12 +119,16 @@ def test_trace_paths_overflow_and_range(gpu_ready, monkeypatch):
     assert sub == full[1:]
 
 
-def test_trace_paths_visited_set_overflow(gpu_ready):
+@pytest.mark.parametrize("cursor", ["1", "0"])
+def test_trace_paths_visited_set_overflow(gpu_ready, cursor, monkeypatch):
     """Two full bipartite middle layers: the traces take more links than the
-    per-wave visited set holds, so the device reports overflow (None) and
-    never a wrong path; smaller layers trace exactly."""
+    round-3 kernel's per-wave visited set holds (OPENR_SPF_TRACE_CURSOR=0), so
+    it reports overflow (None) and never a wrong path; the cursor DFS keeps no
+    visited set (one pathLinks cursor per node in device scratch) and traces
+    both sizes exactly."""
+    monkeypatch.setenv("OPENR_SPF_TRACE_CURSOR", cursor)
     sys.setrecursionlimit(10000)
-    for m, expect_overflow in ((8, False), (40, True)):
+    for m, expect_overflow in ((8, False), (40, cursor == "0")):
         V = 2 + 2 * m
         src, dst = 0, V - 1
         links = [(src, 1 + i, 1, 1) for i in range(m)]

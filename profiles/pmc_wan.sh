@@ -20,5 +20,5 @@ for P in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
     python3 $R/profiles/quick_wan.py $N $VAR > $OUT/p$i.log 2>&1
 done
 cd $R
-python3 profiles/pmc_summary.py $OUT spf_dstep_kernel > $OUT/summary.json
+python3 profiles/pmc_summary.py $OUT ${4:-spf_dstep_kernel} > $OUT/summary.json
 cat $OUT/summary.json

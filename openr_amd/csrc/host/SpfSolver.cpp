@@ -13,6 +13,7 @@
 #include "SpfSolver.h"
 
 #include <atomic>
+#include <cstdlib>
 #include <chrono>
 #include <memory>
 #include <string_view>
@@ -233,6 +234,11 @@ struct EcmpClock {
   }
 };
 thread_local EcmpClock tEcmpClock;
+// A/B switch: `name`=0 in the environment turns a fast path off
+bool getenv_flag_off(const char* name) {
+  const char* v = std::getenv(name);
+  return v && std::atoi(v) == 0;
+}
 inline int64_t nowNs() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(
              std::chrono::steady_clock::now().time_since_epoch())
@@ -419,6 +425,26 @@ class SpfSolver::SpfSolverImpl {
     return SpfRead(ls, myNodeName, *v);
   }
 
+  // SP_ECMP fast path (one area, LFA off): myNode's shortest-path links per
+  // next-hop mask bit of its own SPF row, with next-hop templates (metric
+  // set per prefix), built once per RouteDb build before the worker pool
+  struct FastEcmp {
+    bool ok{false};
+    const LinkState* ls{nullptr};
+    const std::string* area{nullptr};
+    const SpfView* view{nullptr};
+    std::vector<std::vector<uint32_t>> bitLinks; // mask bit -> template index
+    std::vector<thrift::NextHopThrift> tmpl4, tmpl6;
+  };
+  FastEcmp fast_;
+  void buildFastEcmp(const std::string& myNodeName, AreaLinkStates const& areaLinkStates);
+  bool fastEcmpOpenr(
+      std::unordered_map<thrift::IpPrefix, RibUnicastEntry>& unicastEntries,
+      const std::string& myNodeName,
+      const thrift::IpPrefix& prefix,
+      const thrift::PrefixEntries& prefixEntries,
+      bool isV4);
+
   thrift::StaticRoutes staticRoutes_;
   std::vector<thrift::RouteDatabaseDelta> staticRoutesUpdates_;
   const std::string myNodeName_;
@@ -584,6 +610,7 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
   for (const auto& [area, ls] : areaLinkStates) {
     myLinks(myNodeName, area, ls); // fill the per-build cache before the workers read it
   }
+  buildFastEcmp(myNodeName, areaLinkStates);
   std::vector<std::unordered_map<thrift::IpPrefix, RibUnicastEntry>> parts(shards);
   const auto tpar = std::chrono::steady_clock::now();
   parallelShards(shards, [&](unsigned s) {
@@ -600,7 +627,7 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
         selectKsp2(
             parts[s], *x.prefix, myNodeName, nodes, *x.entries, x.hasBGP, areaLinkStates,
             prefixState, x.algo);
-      } else {
+      } else if (!fastEcmpOpenr(parts[s], myNodeName, *x.prefix, *x.entries, x.isV4)) {
         selectEcmpOpenr(parts[s], myNodeName, *x.prefix, *x.entries, x.isV4, areaLinkStates);
       }
     }
@@ -922,6 +949,169 @@ std::optional<int64_t> SpfSolver::SpfSolverImpl::getMinNextHopThreshold(
     }
   }
   return threshold;
+}
+
+// The SP_ECMP route of a prefix in the common case -- one area, LFA off, IP
+// forwarding -- read straight from myNode's flat SPF row with the reference's
+// exact rules (getBestAnnouncingNodes :544-630 with maybeFilterDrainedNodes
+// :651-666, getNextHopsWithMetric :1093-1179, getNextHopsThrift :1181-1271):
+// announcers resolved by node id, the next-hop neighbours read as mask bits,
+// and a neighbour's links taken iff metric(link) + (min - d(nbr)) == min,
+// i.e. metric(link) == d(nbr) -- a per-build property of the bit, so each
+// bit's next hops are templates whose metric is set to the prefix's min.
+// No std::set<std::string> of announcers, no name-keyed next-hop map.
+void SpfSolver::SpfSolverImpl::buildFastEcmp(
+    const std::string& myNodeName, AreaLinkStates const& areaLinkStates) {
+  fast_ = FastEcmp{};
+  if (areaLinkStates.size() != 1 || computeLfaPaths_ || getenv_flag_off("OPENR_ECMP_FAST")) {
+    return;
+  }
+  const auto& [area, ls] = *areaLinkStates.begin();
+  const MyLinks* mls = cachedLinks(myNodeName, area);
+  if (!mls) {
+    return;
+  }
+  const SpfView& view = ls.spfView(myNodeName, true);
+  if (view.src == ~0u || view.exact || !view.useLinkMetric) {
+    return;
+  }
+  fast_.ls = &ls;
+  fast_.area = &area;
+  fast_.view = &view;
+  fast_.bitLinks.assign(view.nbrs.size(), {});
+  std::unordered_map<uint32_t, uint32_t> bitOf;
+  for (uint32_t j = 0; j < view.nbrs.size(); ++j) {
+    bitOf[view.nbrs[j]] = j;
+  }
+  for (uint32_t li = 0; li < mls->links.size(); ++li) {
+    const MyLink& ml = mls->links[li];
+    if (!ml.up) {
+      continue;
+    }
+    const auto id = ls.nodeId(*ml.nbr);
+    if (!id) {
+      continue;
+    }
+    auto b = bitOf.find(*id);
+    if (b == bitOf.end() || !view.reached(*id) || ml.metric != view.dist[*id]) {
+      continue; // never a shortest-path link (distOverLink != minMetric)
+    }
+    fast_.bitLinks[b->second].push_back((uint32_t)fast_.tmpl4.size());
+    fast_.tmpl4.push_back(createNextHop(*ml.nhV4, *ml.iface, 0, std::nullopt, false,
+                                        ml.link->getArea()));
+    fast_.tmpl6.push_back(createNextHop(*ml.nhV6, *ml.iface, 0, std::nullopt, false,
+                                        ml.link->getArea()));
+  }
+  fast_.ok = true;
+}
+
+bool SpfSolver::SpfSolverImpl::fastEcmpOpenr(
+    std::unordered_map<thrift::IpPrefix, RibUnicastEntry>& unicastEntries,
+    const std::string& myNodeName,
+    const thrift::IpPrefix& prefix,
+    const thrift::PrefixEntries& prefixEntries,
+    bool isV4) {
+  if (!fast_.ok) {
+    return false;
+  }
+  auto& clk = tEcmpClock;
+  int64_t t = nowNs();
+  auto lap = [&](int i) {
+    const int64_t n = nowNs();
+    clk.ns[i] += n - t;
+    t = n;
+  };
+  const LinkState& ls = *fast_.ls;
+  const SpfView& view = *fast_.view;
+  // reachable announcers in name order (the first is the best node)
+  struct Ann {
+    const std::string* node;
+    const std::string* area;
+    uint32_t id;
+    bool drained;
+  };
+  Ann anns[16];
+  std::vector<Ann> more;
+  size_t n = 0;
+  for (const auto& [node, byArea] : prefixEntries) {
+    if (node == myNodeName) {
+      return false; // (the caller filters these) general path
+    }
+    for (const auto& [area, entry] : byArea) {
+      if (area != *fast_.area) {
+        return false; // an area this build does not hold: general path
+      }
+      const auto id = ls.nodeId(node);
+      if (!id || !view.reached(*id)) {
+        continue;
+      }
+      const Ann a{&node, &area, *id, ls.isNodeOverloaded(node)};
+      if (n < 16) {
+        anns[n] = a;
+      } else {
+        more.push_back(a);
+      }
+      ++n;
+    }
+  }
+  auto ann = [&](size_t i) -> const Ann& { return i < 16 ? anns[i] : more[i - 16]; };
+  lap(0);
+  if (n == 0) {
+    Counters::add("decision.no_route_to_prefix", 1);
+    return true;
+  }
+  // drained announcers count only when every reachable one is drained
+  bool anyUndrained = false;
+  for (size_t i = 0; i < n; ++i) {
+    anyUndrained |= !ann(i).drained;
+  }
+  Metric shortest = std::numeric_limits<Metric>::max();
+  for (size_t i = 0; i < n; ++i) {
+    if (!anyUndrained || !ann(i).drained) {
+      shortest = std::min<Metric>(shortest, view.dist[ann(i).id]);
+    }
+  }
+  const uint32_t W = view.words;
+  uint64_t m[4] = {0, 0, 0, 0};
+  std::vector<uint64_t> mw(W > 4 ? W : 0, 0);
+  uint64_t* mask = W > 4 ? mw.data() : m;
+  for (size_t i = 0; i < n; ++i) {
+    const Ann& a = ann(i);
+    if ((!anyUndrained || !a.drained) && view.dist[a.id] == shortest) {
+      const uint64_t* row = view.nh.data() + (size_t)a.id * W;
+      for (uint32_t w = 0; w < W; ++w) {
+        mask[w] |= row[w];
+      }
+    }
+  }
+  bool any = false;
+  for (uint32_t w = 0; w < W; ++w) {
+    any |= mask[w] != 0;
+  }
+  lap(1);
+  if (!any) {
+    Counters::add("decision.no_route_to_prefix", 1);
+    return true;
+  }
+  std::unordered_set<thrift::NextHopThrift> nextHops;
+  const auto& tmpl = isV4 ? fast_.tmpl4 : fast_.tmpl6;
+  for (uint32_t w = 0; w < W; ++w) {
+    for (uint64_t b = mask[w]; b; b &= b - 1) {
+      const uint32_t bit = w * 64 + (uint32_t)__builtin_ctzll(b);
+      for (const uint32_t k : fast_.bitLinks[bit]) {
+        thrift::NextHopThrift nh = tmpl[k];
+        nh.metric = (int32_t)shortest;
+        nextHops.insert(std::move(nh));
+      }
+    }
+  }
+  const Ann& best = ann(0);
+  RibUnicastEntry entry(prefix, std::move(nextHops), prefixEntries.at(*best.node).at(*best.area),
+                        *best.area);
+  lap(2);
+  unicastEntries.emplace(prefix, std::move(entry));
+  lap(3);
+  return true;
 }
 
 void SpfSolver::SpfSolverImpl::selectEcmpOpenr(

@@ -1,6 +1,8 @@
 set -o pipefail
-# round 4: full bench at HEAD (fabric byte masks, LDS-row WAN pass, cursor KSP2 traces)
+# round 4: RouteDb parity with the SP_ECMP fast path, then the full bench at HEAD
 D=gpurun_out/r04g; mkdir -p $D
+timeout -k 10 600 python -u -m pytest tests/test_routedb_golden_gpu.py tests/test_engine_parity_gpu.py -x -q --timeout 300 --timeout-method thread -m gpu > $D/gpu_tests.log 2>&1 || { tail -5 $D/gpu_tests.log; exit 4; }
+tail -2 $D/gpu_tests.log
 timeout -k 10 900 python bench.py > $D/bench_full.json 2> $D/bench_full.err || exit 5
 python - <<'PY'
 import json

@@ -435,9 +435,15 @@ class SpfSolver::SpfSolverImpl {
     const SpfView* view{nullptr};
     std::vector<std::vector<uint32_t>> bitLinks; // mask bit -> template index
     std::vector<thrift::NextHopThrift> tmpl4, tmpl6;
+    std::vector<uint32_t> tmplNbr; // node id of each template's neighbour
   };
   FastEcmp fast_;
   void buildFastEcmp(const std::string& myNodeName, AreaLinkStates const& areaLinkStates);
+  // node label `label` held by `owner` (a single holder, not myNode):
+  // getNextHopsWithMetric + getNextHopsThrift with the swap label, from the
+  // fast path's bit templates (false: take the general path)
+  bool fastLabelRoute(int32_t label, const std::string& owner, const std::string& area,
+                      std::unordered_map<int32_t, RibMplsEntry>& out);
   bool fastEcmpOpenr(
       std::unordered_map<thrift::IpPrefix, RibUnicastEntry>& unicastEntries,
       const std::string& myNodeName,
@@ -703,6 +709,9 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
   parallelShards(labelShards, [&](unsigned s) {
     for (const uint32_t i : labelShardJobs[s]) {
       const auto& db = *labelItems[i].db;
+      if (fastLabelRoute(db.nodeLabel, db.thisNodeName, *labelItems[i].area, labelParts[s])) {
+        continue;
+      }
       const auto metricNhs =
           getNextHopsWithMetric(myNodeName, {db.thisNodeName}, false, areaLinkStates);
       if (metricNhs.second.empty()) {
@@ -997,12 +1006,64 @@ void SpfSolver::SpfSolverImpl::buildFastEcmp(
       continue; // never a shortest-path link (distOverLink != minMetric)
     }
     fast_.bitLinks[b->second].push_back((uint32_t)fast_.tmpl4.size());
+    fast_.tmplNbr.push_back(*id);
     fast_.tmpl4.push_back(createNextHop(*ml.nhV4, *ml.iface, 0, std::nullopt, false,
                                         ml.link->getArea()));
     fast_.tmpl6.push_back(createNextHop(*ml.nhV6, *ml.iface, 0, std::nullopt, false,
                                         ml.link->getArea()));
   }
   fast_.ok = true;
+}
+
+bool SpfSolver::SpfSolverImpl::fastLabelRoute(
+    int32_t label, const std::string& owner, const std::string& area,
+    std::unordered_map<int32_t, RibMplsEntry>& out) {
+  if (!fast_.ok || area != *fast_.area) {
+    return false;
+  }
+  const SpfView& view = *fast_.view;
+  const auto id = fast_.ls->nodeId(owner);
+  if (!id || !view.reached(*id)) {
+    // getNextHopsWithMetric finds no next hop (Decision.cpp:449-452)
+    Counters::add("decision.no_route_to_label", 1);
+    return true;
+  }
+  const uint32_t W = view.words;
+  const uint64_t* row = view.nh.data() + (size_t)*id * W;
+  const Metric shortest = view.dist[*id];
+  size_t cnt = 0;
+  for (uint32_t w = 0; w < W; ++w) {
+    for (uint64_t b = row[w]; b; b &= b - 1) {
+      cnt += fast_.bitLinks[w * 64 + (uint32_t)__builtin_ctzll(b)].size();
+    }
+  }
+  if (cnt == 0) {
+    bool any = false;
+    for (uint32_t w = 0; w < W; ++w) {
+      any |= row[w] != 0;
+    }
+    if (!any) {
+      Counters::add("decision.no_route_to_label", 1);
+      return true;
+    }
+  }
+  std::unordered_set<thrift::NextHopThrift> nextHops;
+  nextHops.reserve(cnt);
+  for (uint32_t w = 0; w < W; ++w) {
+    for (uint64_t b = row[w]; b; b &= b - 1) {
+      for (const uint32_t k : fast_.bitLinks[w * 64 + (uint32_t)__builtin_ctzll(b)]) {
+        thrift::NextHopThrift nh = fast_.tmpl6[k];
+        nh.metric = (int32_t)shortest;
+        // PHP into the label's owner, else SWAP (getNextHopsThrift :1211-1217)
+        nh.mplsAction = fast_.tmplNbr[k] == *id
+            ? createMplsAction(thrift::MplsActionCode::PHP)
+            : createMplsAction(thrift::MplsActionCode::SWAP, label);
+        nextHops.insert(std::move(nh));
+      }
+    }
+  }
+  out.emplace(label, RibMplsEntry(label, std::move(nextHops)));
+  return true;
 }
 
 bool SpfSolver::SpfSolverImpl::fastEcmpOpenr(
@@ -1094,6 +1155,15 @@ bool SpfSolver::SpfSolverImpl::fastEcmpOpenr(
     return true;
   }
   std::unordered_set<thrift::NextHopThrift> nextHops;
+  {
+    size_t cnt = 0;
+    for (uint32_t w = 0; w < W; ++w) {
+      for (uint64_t b = mask[w]; b; b &= b - 1) {
+        cnt += fast_.bitLinks[w * 64 + (uint32_t)__builtin_ctzll(b)].size();
+      }
+    }
+    nextHops.reserve(cnt);
+  }
   const auto& tmpl = isV4 ? fast_.tmpl4 : fast_.tmpl6;
   for (uint32_t w = 0; w < W; ++w) {
     for (uint64_t b = mask[w]; b; b &= b - 1) {

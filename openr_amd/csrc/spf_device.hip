@@ -4834,7 +4834,7 @@ __global__ __launch_bounds__(64 * kTraceWaves) void spf_trace_paths_kernel(Trace
 // Only the recursion stack is in LDS, so nothing but a path longer than
 // kTcDepth links, a node with more than kTcSort pathLinks or a full arena
 // overflows to the host.
-constexpr uint32_t kTcWaves = 4;    // waves (queries in flight) per block
+constexpr uint32_t kTcWaves = 4;    // waves (queries in flight) per block (16 per CU)
 constexpr uint32_t kTcDepth = 256;  // recursion frames per wave
 constexpr uint32_t kTcSort = 256;   // pathLinks of one node ranked in LDS
 constexpr uint32_t kTcIgn = 256;    // ignore-list entries staged in LDS per query
@@ -4842,7 +4842,7 @@ constexpr uint32_t kTcIgn = 256;    // ignore-list entries staged in LDS per que
 struct TraceCursorArgs {
   TraceArgs t;
   uint4* nstate;   // [waves][V] {tag, arena offset, length, cursor}
-  uint32_t* arena; // [waves][arena_cap] in-edges e (v's row) in pathLinks order
+  uint2* arena;    // [waves][arena_cap] {tail, link} of pathLinks(v), in order
   uint32_t arena_cap;
   uint32_t V;
 };
@@ -4850,6 +4850,12 @@ struct TraceCursorArgs {
 __device__ __forceinline__ void tc_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint2 ld_coh2(const uint2* p) {
+  const uint64_t x = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  return make_uint2((uint32_t)x, (uint32_t)(x >> 32));
 }
 
 __device__ __forceinline__ uint4 tc_load4(const uint4* p) {
@@ -4861,18 +4867,20 @@ __device__ __forceinline__ uint4 tc_load4(const uint4* p) {
 
 __global__ __launch_bounds__(64 * kTcWaves) void spf_trace_cursor_kernel(TraceCursorArgs A) {
   const TraceArgs& a = A.t;
-  __shared__ uint32_t stk_s[kTcWaves][kTcDepth]; // node of each frame
-  __shared__ uint32_t lnk_s[kTcWaves][kTcDepth]; // link taken at each frame
-  __shared__ uint64_t key_s[kTcWaves][kTcSort];  // (d[u] << 32 | u)
-  __shared__ uint32_t sub_s[kTcWaves][kTcSort];  // u's row position (tie-break)
-  __shared__ uint32_t edg_s[kTcWaves][kTcSort];  // in-edge e of v's row
+  __shared__ uint32_t stk_s[kTcWaves][kTcDepth];  // node of each frame
+  __shared__ uint32_t lnk_s[kTcWaves][kTcDepth];  // link taken at each frame
+  __shared__ uint4 fst_s[kTcWaves][kTcDepth];     // the frame node's state (cursor in LDS)
+  __shared__ uint64_t key_s[kTcWaves][kTcSort];   // (d[u] << 32 | u)
+  __shared__ uint32_t sub_s[kTcWaves][kTcSort];   // u's row position (tie-break)
+  __shared__ uint32_t edg_s[kTcWaves][kTcSort];   // in-edge e of v's row
   __shared__ uint32_t ign_s[kTcWaves][kTcIgn];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t gw = blockIdx.x * kTcWaves + wv, nwaves = gridDim.x * kTcWaves;
   uint4* ns = A.nstate + (size_t)gw * A.V;
-  uint32_t* arena = A.arena + (size_t)gw * A.arena_cap;
+  uint2* arena = A.arena + (size_t)gw * A.arena_cap;
   uint32_t* stk = stk_s[wv];
   uint32_t* lnk = lnk_s[wv];
+  uint4* fst = fst_s[wv];
   uint64_t* keys = key_s[wv];
   uint32_t* subs = sub_s[wv];
   uint32_t* edgs = edg_s[wv];
@@ -4896,79 +4904,98 @@ __global__ __launch_bounds__(64 * kTcWaves) void spf_trace_cursor_kernel(TraceCu
     uint32_t* out_ends = a.out_ends + (size_t)q * a.cap;
     uint32_t npaths = 0, nl = 0, atop = 0;
     bool overflow = false;
+    // the state of node v for this query: {tag, arena offset, length,
+    // cursor}; pathLinks(v) built into the arena on first use
+    auto enter = [&](uint32_t v) -> uint4 {
+      uint4 st = tc_load4(ns + v);
+      if (st.x == tag) {
+        return st;
+      }
+      const uint64_t dv = dist[v];
+      const uint32_t e0 = a.row[v], e1 = a.row[v + 1];
+      uint32_t n = 0;
+      for (uint32_t base = e0; base < e1; base += 64) {
+        const uint32_t e = base + lane;
+        bool ok = false;
+        uint32_t u = 0, du = 0, eu = 0;
+        if (e < e1) {
+          u = a.col[e];
+          du = dist[u];
+          ok = du != kInf32 && (u == s || ((a.trbits[u >> 5] >> (u & 31)) & 1u));
+          if (ok) {
+            eu = a.rev[e];
+            const uint64_t w = a.unit ? 1ull : (uint64_t)a.wout[eu];
+            ok = (uint64_t)du + w == dv;
+          }
+          if (ok && nign) {
+            ok = !in_sorted(ignp, nign, a.link[e]);
+          }
+        }
+        const uint64_t m = __ballot(ok);
+        const uint32_t pos = n + (uint32_t)__popcll(m & lt_mask);
+        if (ok && pos < kTcSort) {
+          keys[pos] = ((uint64_t)du << 32) | u;
+          subs[pos] = eu;
+          edgs[pos] = e;
+        }
+        n += (uint32_t)__popcll(m);
+      }
+      tc_sync();
+      if (n > kTcSort || atop + n > A.arena_cap) {
+        return make_uint4(0, 0, 0, kInf32); // overflow marker
+      }
+      for (uint32_t i = lane; i < n; i += 64) {
+        const uint64_t k = keys[i];
+        const uint32_t su = subs[i];
+        uint32_t r = 0;
+        for (uint32_t j = 0; j < n; ++j) {
+          const uint64_t kj = keys[j];
+          r += kj < k || (kj == k && subs[j] < su);
+        }
+        // the tail and the link: a step reads one 8-byte entry
+        arena[atop + r] = make_uint2((uint32_t)k, a.link[edgs[i]]);
+      }
+      st = make_uint4(tag, atop, n, 0);
+      atop += n;
+      if (n == 0) {
+        ns[v] = st; // no pathLink: every later visit fails at once
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      tc_sync();
+      return st;
+    };
+    // cursors of the frames' nodes back to their global states
+    auto save = [&](uint32_t lo, uint32_t hi) {
+      for (uint32_t f = lo + lane; f <= hi; f += 64) {
+        ns[stk[f]] = fst[f];
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      tc_sync();
+    };
     if (s != d && dist[d] != kInf32) {
       for (;;) { // one traceOnePath per iteration
         uint32_t depth = 0;
+        uint4 st = enter(d);
+        if (st.w == kInf32) {
+          overflow = true;
+          break;
+        }
         if (lane == 0) {
           stk[0] = d;
+          fst[0] = st;
         }
         tc_sync();
         bool found = false;
         for (;;) {
-          const uint32_t v = stk[depth];
-          uint4 st = tc_load4(ns + v);
-          if (st.x != tag) {
-            // pathLinks(v): candidates compacted into LDS, then ranked
-            const uint64_t dv = dist[v];
-            const uint32_t e0 = a.row[v], e1 = a.row[v + 1];
-            uint32_t n = 0;
-            for (uint32_t base = e0; base < e1; base += 64) {
-              const uint32_t e = base + lane;
-              bool ok = false;
-              uint32_t u = 0, du = 0, eu = 0;
-              if (e < e1) {
-                u = a.col[e];
-                du = dist[u];
-                ok = du != kInf32 && (u == s || ((a.trbits[u >> 5] >> (u & 31)) & 1u));
-                if (ok) {
-                  eu = a.rev[e];
-                  const uint64_t w = a.unit ? 1ull : (uint64_t)a.wout[eu];
-                  ok = (uint64_t)du + w == dv;
-                }
-                if (ok && nign) {
-                  ok = !in_sorted(ignp, nign, a.link[e]);
-                }
-              }
-              const uint64_t m = __ballot(ok);
-              const uint32_t pos = n + (uint32_t)__popcll(m & lt_mask);
-              if (ok && pos < kTcSort) {
-                keys[pos] = ((uint64_t)du << 32) | u;
-                subs[pos] = eu;
-                edgs[pos] = e;
-              }
-              n += (uint32_t)__popcll(m);
-            }
-            tc_sync();
-            if (n > kTcSort || atop + n > A.arena_cap) {
-              overflow = true;
-              break;
-            }
-            for (uint32_t i = lane; i < n; i += 64) {
-              const uint64_t k = keys[i];
-              const uint32_t su = subs[i];
-              uint32_t r = 0;
-              for (uint32_t j = 0; j < n; ++j) {
-                const uint64_t kj = keys[j];
-                r += kj < k || (kj == k && subs[j] < su);
-              }
-              arena[atop + r] = edgs[i];
-            }
-            st = make_uint4(tag, atop, n, 0);
-            atop += n;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            tc_sync();
-          }
+          st = fst[depth];
           if (st.w < st.z) {
-            const uint32_t e = ld_coh(arena + st.y + st.w);
+            const uint2 ent = ld_coh2(arena + st.y + st.w);
             st.w += 1;
-            // every lane stores the same state: a lane's later read of it
-            // follows its own store
-            ns[v] = st;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const uint32_t u = a.col[e];
             if (lane == 0) {
-              lnk[depth] = a.link[e];
+              fst[depth] = st;
+              lnk[depth] = ent.y;
             }
+            const uint32_t u = ent.x;
             if (u == s) {
               found = true;
               break;
@@ -4977,17 +5004,28 @@ __global__ __launch_bounds__(64 * kTcWaves) void spf_trace_cursor_kernel(TraceCu
               overflow = true;
               break;
             }
+            const uint4 su = enter(u);
+            if (su.w == kInf32) {
+              overflow = true;
+              break;
+            }
+            if (su.w >= su.z) {
+              // u's search fails at once (the host trace's dead memo): next
+              // pathLink of v
+              tc_sync();
+              continue;
+            }
             ++depth;
             if (lane == 0) {
               stk[depth] = u;
+              fst[depth] = su;
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             tc_sync();
             continue;
           }
-          // v exhausted: the search through it fails
-          ns[v] = st;
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          // v exhausted: the search through it fails; its state goes back
+          tc_sync();
+          save(depth, depth);
           if (depth == 0) {
             break;
           }
@@ -4997,6 +5035,7 @@ __global__ __launch_bounds__(64 * kTcWaves) void spf_trace_cursor_kernel(TraceCu
           break;
         }
         tc_sync();
+        save(0, depth); // every frame's cursor moved on
         const uint32_t len = depth + 1;
         if (nl + len > a.cap || npaths + 1 > a.cap) {
           overflow = true;
@@ -8262,10 +8301,12 @@ int spf_query_trace_paths(
   if (env_flag("OPENR_SPF_TRACE_CURSOR", 1)) {
     // cursor DFS: per-wave node states + pathLinks arena (zeroed per launch:
     // a state's tag is its query index + 1)
-    const uint32_t maxw = g->V > 50000 ? 512u : 1024u;
+    // 16 waves per CU (a wave's DFS is a chain of L2 round trips: the more
+    // queries in flight, the better); scratch bounded for large graphs
+    const uint32_t maxw = g->V > 50000 ? 1024u : (uint32_t)g->num_cus * 16u;
     const uint32_t nw = std::min<uint32_t>((count + kTcWaves - 1) / kTcWaves * kTcWaves, maxw);
-    const uint32_t acap = std::max<uint32_t>(1024, std::min<uint32_t>(g->E, 1u << 16));
-    const size_t need = (size_t)nw * g->V * sizeof(uint4) + (size_t)nw * acap * 4;
+    const uint32_t acap = std::max<uint32_t>(1024, std::min<uint32_t>(g->E, 1u << 15));
+    const size_t need = (size_t)nw * g->V * sizeof(uint4) + (size_t)nw * acap * sizeof(uint2);
     if (q->d_tcs && q->tcs_bytes < need) {
       HIP_TRY(hipStreamSynchronize(g->stream));
       pool_free(q->d_tcs);
@@ -8278,7 +8319,7 @@ int spf_query_trace_paths(
     TraceCursorArgs ta{};
     ta.t = a;
     ta.nstate = reinterpret_cast<uint4*>(q->d_tcs);
-    ta.arena = reinterpret_cast<uint32_t*>(q->d_tcs + (size_t)nw * g->V * sizeof(uint4));
+    ta.arena = reinterpret_cast<uint2*>(q->d_tcs + (size_t)nw * g->V * sizeof(uint4));
     ta.arena_cap = acap;
     ta.V = g->V;
     HIP_TRY(hipMemsetAsync(q->d_tcs, 0, (size_t)nw * g->V * sizeof(uint4), g->stream));

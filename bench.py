@@ -164,6 +164,29 @@ def pmc_traffic_largest(kernel_name):
     return None, None
 
 
+WHATIF_PMC_KERNELS = ("spf_sssp_kernel", "spf_whatif_screen_kernel", "spf_nh_narrow_kernel")
+
+
+def pmc_traffic_sum(kernel_names, fname):
+    """HBM bytes of one batch of a multi-kernel plan: the sum over its
+    kernels of (all dispatches' bytes / batches) from the newest committed
+    profiles/*/<fname> (a probe that ran only that plan, e.g.
+    profiles/whatif_probe.py)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", fname)))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        ks = d.get("kernels", {})
+        runs = d.get("batches")
+        if not runs or not all(k in ks for k in kernel_names):
+            continue
+        tot = sum(ks[k]["hbm_bytes_per_launch"] * ks[k]["dispatches"] for k in kernel_names)
+        return int(tot / runs), os.path.relpath(f, ROOT)
+    return None, None
+
+
 def pmc_traffic_smallest(kernel_name):
     """HBM bytes of the smallest dispatch of `kernel_name` in the committed
     PMC passes (a kernel launched in two modes: the plain one)."""
@@ -432,11 +455,14 @@ def cpu_baseline(topo, sample):
     }
 
 
-def _rebuild_loop(M, topo, iters, timed, fwd=(0, 0), after_cold=None, check=None):
+def _rebuild_loop(M, topo, iters, timed, fwd=(0, 0), after_cold=None, check=None, mode="overload"):
     """DecisionBenchmark BM_DecisionFabric loop (DecisionBenchmark.cpp:
     600-626): toggle an RSW's overload bit, rebuild the RouteDb of "2-0-0".
     fwd = (PrefixForwardingType, PrefixForwardingAlgorithm) of every prefix;
-    after_cold() runs once the cold build is done (counter reset)."""
+    after_cold() runs once the cold build is done (counter reset).
+    mode="link": flap one link instead -- the RSW withdraws its first
+    adjacency (the link to that FSW goes down), then announces it again
+    (tests/golden/make_linkflap_golden.py holds the down states)."""
     areas = M.AreaLinkStates()
     ls = areas.add("0")
     dbs = topo.adj_dbs()
@@ -454,8 +480,12 @@ def _rebuild_loop(M, topo, iters, timed, fwd=(0, 0), after_cold=None, check=None
     routes = 0
     for it in range(iters):
         db = dbs[rsw[(it * 7919) % len(rsw)]]
-        for overloaded in (True, False):
-            db.isOverloaded = overloaded
+        full = db.adjacencies
+        for down in (True, False):
+            if mode == "link":
+                db.adjacencies = full[1:] if down else full
+            else:
+                db.isOverloaded = down
             t0 = time.perf_counter()
             ls.updateAdjacencyDatabase(db)
             t1 = time.perf_counter()
@@ -530,6 +560,53 @@ def publication_ingest(topo, reps=3):
         "cpu_oracle_note": "oracle/ref_decision.cpp updateAdjacencyDatabase of the same adjacency "
                            "databases as objects (no decode, no prefixes), 1 thread",
     }
+
+
+def route_db_link_flap(topo, device, iters=4):
+    """Link flap + buildRouteDb: an RSW withdraws its adjacency to one FSW
+    (the link goes down; LinkState.cpp updateAdjacencyDatabase), the
+    RouteDb of "2-0-0" is rebuilt, then the adjacency comes back and the
+    RouteDb is rebuilt again (SP_ECMP, LFA off).  Parity: the down state of
+    the first flap against the oracle's RouteDb
+    (tests/golden/fabric_linkflap.json.gz)."""
+    import openr_amd._openr_spf as E
+    from tests.golden import routes as R
+
+    E.set_spf_device(device)
+
+    def timed(solver, areas, ps):
+        nu, nm, us, free_us = solver.buildRouteDbTimed("2-0-0", areas, ps)
+        return nu + nm, us, free_us
+
+    counters = {}
+
+    def check(ls, solver, areas, ps, dbs):
+        counters.update(E.get_counters())
+        gold = R.load(os.path.join(ROOT, "tests", "golden", "fabric_linkflap.json.gz"))
+        base = _routedb_golden()[1]["sp_ecmp"]["base"]["hashes"]
+        rsw = [i for i, n in enumerate(topo.names) if n.startswith("3-")][0]
+        st = gold["states"].get(f"linkdown:{topo.names[rsw]}")
+        if st is None:
+            return f"golden lacks linkdown:{topo.names[rsw]}"
+        full = dbs[rsw].adjacencies
+        dbs[rsw].adjacencies = full[1:]
+        ls.updateAdjacencyDatabase(dbs[rsw])
+        e = _check_routedb(R, solver.buildRouteDb("2-0-0", areas, ps), R.apply_delta(base, st["delta_vs_base"]),
+                           f"linkdown:{topo.names[rsw]}")
+        dbs[rsw].adjacencies = full
+        ls.updateAdjacencyDatabase(dbs[rsw])
+        return f"ok (oracle golden: linkdown:{topo.names[rsw]} - {st['peer']})" if e is None else e
+
+    out = _rebuild_loop(E, topo, iters, timed, after_cold=E.reset_counters, check=check, mode="link")
+    c = counters or E.get_counters()
+    n = max(1, c.get("decision.route_build_runs", 1))
+    out["per_build_us"] = {k.split(".", 1)[1]: round(c.get(k, 0) / n, 1)
+                           for k in ("decision.graph_build_us", "decision.graph_upload_us",
+                                     "decision.spf_batch_us", "decision.spf_device_us",
+                                     "decision.route_prefetch_us", "decision.route_prefix_pool_us")}
+    out["node"] = "2-0-0"
+    out["what"] = "link flap (RSW withdraws / restores its adjacency to one FSW) + buildRouteDb, LFA off"
+    return out
 
 
 def route_db_rebuild_ms(topo, device, iters=5):
@@ -649,13 +726,15 @@ def all_nodes_route_table(topo, device, reps=3):
     # algorithmic bytes of spf_route_table_kernel per launch: per (node,
     # prefix) cell the metric + best words written, the link mask written
     # (8 B x link words of the node), the announcer's distance read and its
-    # next-hop mask word(s) read (8 B x mask words of the node)
+    # next-hop mask read (SPF_NH_BYTES of the node: the byte-strided rows)
+    from openr_amd import abi as _abi
+
     csr = topo.csr()
     deg = np.diff(csr.row_ptr.astype(np.int64))
     lw = (deg + 63) // 64
-    nbr = np.array([len(set(csr.col[csr.row_ptr[u]:csr.row_ptr[u + 1]].tolist())) for u in range(V)])
-    nw = np.maximum(1, (nbr + 63) // 64)
-    alg = int((P + NL) * (12 * V + 8 * int(lw.sum()) + 8 * int(nw.sum())))
+    nbr = [len(set(csr.col[csr.row_ptr[u]:csr.row_ptr[u + 1]].tolist())) for u in range(V)]
+    nb = np.array([_abi.nh_bytes_for(k) for k in nbr], dtype=np.int64)
+    alg = int((P + NL) * (12 * V + 8 * int(lw.sum()) + int(nb.sum())))
     med = lambda x: sorted(x)[len(x) // 2]  # noqa: E731
     k_ms = med(rt)
     # the plain (non-LFA) launches are the smallest of the profiled ones
@@ -840,6 +919,26 @@ def whatif_batch(world, rank, local, dist, steps=3, cpu_lines=True):
                         bad += d[v] != np.uint64(abi.SPF_UNREACHABLE)
         check = "ok" if bad == 0 else f"{bad} mismatches"
     kernels = sorted({q.kernel for q in queries})
+    # algorithmic bytes of the batch (both areas): every query's u32
+    # distance row and byte-strided mask row written once (SPF_NH_BYTES of
+    # the source), plus the baseline SSSP of each area (its CSR read once:
+    # row pointers + 8 B per edge, head and metric).  Screened queries copy
+    # the baseline rows and repaired ones touch only the edges of their K
+    # (DESIGN.md §3), so no per-query CSR term.  Priced against the plan's
+    # device time (HIP events around base + screen + repair + narrow)
+    alg, screened = 0, 0
+    for (a, _, ign), q in zip(graphs, queries):
+        csr = areas[a][0]
+        V, E = csr.num_nodes, len(csr.col)
+        nq = len(ign)
+        screened += q.screened() or 0
+        B = q.nh_bytes(0)
+        alg += nq * (4 * V + V * B) + (4 * (V + 1) + 8 * E)
+    gbs = alg / (dev_ms / 1e3) / 1e9 if dev_ms > 0 else 0.0
+    wi_traffic = None
+    wi_src = None
+    if world == 1:
+        wi_traffic, wi_src = pmc_traffic_sum(WHATIF_PMC_KERNELS, "pmc_whatif.json")
     for q in queries:
         q.close()
     for _, g, _ in graphs:
@@ -873,6 +972,14 @@ def whatif_batch(world, rank, local, dist, steps=3, cpu_lines=True):
         "ms": round(ms, 3), "device_ms": round(dev_ms, 3),
         "value": round(len(allq) / (ms / 1e3), 1), "unit": "SPF/s",
         "parity_check": check,
+        "screened_queries": screened,
+        "roofline": {"bound": "hbm", "kernel": "what-if plan (base SSSP + spf_whatif_screen_kernel + "
+                     "spf_sssp_kernel repair + spf_nh_narrow_kernel)",
+                     "note": "latency-bound: the per-area baseline SSSP runs on one workgroup before "
+                             "the batch can start", "algorithmic_bytes": int(alg),
+                     "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": wi_traffic,
+                     "traffic_source": wi_src},
         **({"cpu_baseline_optimised_all_cores": cpu} if cpu else {}),
     }
 
@@ -1662,6 +1769,10 @@ def main():
             out["route_db_rebuild"] = route_db_rebuild_ms(topo, local)
         except Exception as e:  # reported, never silently replaced
             out["route_db_rebuild"] = {"error": repr(e)}
+        try:
+            out["route_db_link_flap"] = route_db_link_flap(topo, local)
+        except Exception as e:
+            out["route_db_link_flap"] = {"error": repr(e)}
         try:
             out["all_nodes_route_table"] = all_nodes_route_table(topo, local)
         except Exception as e:

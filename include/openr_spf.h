@@ -159,6 +159,11 @@ int spf_query_stage_ms(spf_query* q, float* dist_ms, float* nh_ms);
  * (lets a caller time a loop of asynchronous runs per kernel). */
 int spf_query_stage_history(
     spf_query* q, uint32_t n, float* dist_ms, float* nh_ms, uint32_t* got);
+/* What-if screen of the last run (batches with ignore lists): *screened =
+ * queries whose ignored links were all off the baseline's shortest-path DAG
+ * (rows copied from the baseline, no SSSP), *has_screen = 0 when the query
+ * has no screen (every query ran its own SSSP).  Synchronises the query. */
+int spf_query_screened(spf_query* q, uint32_t* screened, uint32_t* has_screen);
 /* Name of the plan the last run used ("lds", "dstep", "msbfs+levels", "wide",
  * "exact", ...). */
 const char* spf_query_kernel_name(const spf_query* q);

@@ -51,6 +51,7 @@ EXPORTED_SYMBOLS = (
     "spf_query_elapsed_ms",
     "spf_query_stage_ms",
     "spf_query_stage_history",
+    "spf_query_screened",
     "spf_query_kernel_name",
     "spf_query_dist",
     "spf_query_nh_words",
@@ -246,6 +247,7 @@ def load():
         "spf_query_run": (C.c_int, [vp]),
         "spf_query_sync": (C.c_int, [vp]),
         "spf_query_elapsed_ms": (C.c_int, [vp, C.POINTER(C.c_float)]),
+        "spf_query_screened": (C.c_int, [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
         "spf_query_stage_ms": (
             C.c_int,
             [vp, C.POINTER(C.c_float), C.POINTER(C.c_float)],
@@ -602,6 +604,13 @@ class Query:
         got = C.c_uint32()
         _check(load().spf_query_stage_history(self.h, n, d, h, C.byref(got)), "stage_history")
         return [(float(d[i]), float(h[i])) for i in range(got.value)]
+
+    def screened(self):
+        """Queries of the last run the what-if screen resolved by copying the
+        baseline rows (None: the query has no screen)."""
+        n, has = C.c_uint32(), C.c_uint32()
+        _check(load().spf_query_screened(self.h, C.byref(n), C.byref(has)), "screened")
+        return int(n.value) if has.value else None
 
     @property
     def kernel(self) -> str:

@@ -3,15 +3,23 @@
 #include "RouteTable.h"
 
 #include <algorithm>
+#include <chrono>
 #include <set>
 #include <stdexcept>
 
 #include "Engine.h"
+#include "Parallel.h"
 #include "Util.h"
 
 namespace openr {
 
 namespace {
+int64_t usSince(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration_cast<std::chrono::microseconds>(
+             std::chrono::steady_clock::now() - t0)
+      .count();
+}
+
 [[noreturn]] void tableFailure(const char* what, int status) {
   throw std::runtime_error(
       std::string("openr_spf: ") + what + ": " + spf_error_string(status) + " (" +
@@ -23,7 +31,10 @@ AllNodesRouteTable::AllNodesRouteTable(
     const LinkState& ls, const PrefixState& ps, bool enableV4, bool computeLfa,
     const std::unordered_set<std::string>* borderNodes)
     : area_(ls.getArea()), enableV4_(enableV4), lfa_(computeLfa) {
+  auto tp = std::chrono::steady_clock::now();
   LinkState::Engine& eng = ls.engine();
+  Counters::add("decision.route_table_engine_us", usSince(tp));
+  tp = std::chrono::steady_clock::now();
   if (eng.exact) {
     throw std::invalid_argument(
         "AllNodesRouteTable: metric 0 / 64-bit sums need the exact kernel");
@@ -98,6 +109,7 @@ AllNodesRouteTable::AllNodesRouteTable(
       annOff.push_back((uint32_t)ann.size());
     }
   }
+  Counters::add("decision.route_table_prefixes_us", usSince(tp));
   // node-label columns (Decision.cpp:415-481): one pseudo-prefix per (valid
   // label, owner in the graph), owners of a label by name; the cell of node
   // s is getNextHopsWithMetric(s, {owner}) with LFA off
@@ -120,9 +132,11 @@ AllNodesRouteTable::AllNodesRouteTable(
       }
     }
   }
+  Counters::add("decision.route_table_labels_us", usSince(tp));
   // adjacency labels of every node (Decision.cpp:511-534), values copied
+  // (independent per node: read-only LinkState lookups on the host pool)
   adjLabels_.resize(names_.size());
-  for (uint32_t i = 0; i < names_.size(); ++i) {
+  parallelFor(names_.size(), hostThreads(names_.size(), 256), [&](size_t i, unsigned) {
     for (const auto& link : ls.linksFromNode(names_[i])) {
       const int32_t label = link->getAdjLabelFromNode(names_[i]);
       if (label == 0 || !isMplsLabelValid(label)) {
@@ -132,7 +146,9 @@ AllNodesRouteTable::AllNodesRouteTable(
           label, link->getNhV6FromNode(names_[i]), link->getIfaceFromNode(names_[i]),
           (int32_t)link->getMetricFromNode(names_[i]), link->getArea()});
     }
-  }
+  }, 64);
+  Counters::add("decision.route_table_host_us", usSince(tp));
+  tp = std::chrono::steady_clock::now();
   // own snapshot of the device graph: the table outlives LinkState changes
   spf_graph_desc d{};
   d.num_nodes = (uint32_t)eng.names.size();
@@ -148,6 +164,8 @@ AllNodesRouteTable::AllNodesRouteTable(
   if (int s = spf_graph_create(&d, &graph_); s != SPF_OK) {
     tableFailure("spf_graph_create", s);
   }
+  Counters::add("decision.route_table_graph_us", usSince(tp));
+  tp = std::chrono::steady_clock::now();
   std::vector<uint32_t> src(d.num_nodes);
   for (uint32_t i = 0; i < d.num_nodes; ++i) {
     src[i] = i;
@@ -173,11 +191,15 @@ AllNodesRouteTable::AllNodesRouteTable(
   if ((s = spf_query_run(query_)) != SPF_OK) {
     cleanup("spf_query_run", s);
   }
+  Counters::add("decision.route_table_query_us", usSince(tp));
+  tp = std::chrono::steady_clock::now();
   if ((s = spf_route_table_create_ex(
            query_, (uint32_t)(prefixes_.size() + owners_.size()), annOff.data(),
            ann.empty() ? nullptr : ann.data(), lfa_ ? SPF_RT_LFA : 0u, &table_)) != SPF_OK) {
     cleanup("spf_route_table_create", s);
   }
+  Counters::add("decision.route_table_create_us", usSince(tp));
+  tp = std::chrono::steady_clock::now();
   if ((s = spf_route_table_run(table_)) != SPF_OK) {
     cleanup("spf_route_table_run", s);
   }
@@ -185,13 +207,16 @@ AllNodesRouteTable::AllNodesRouteTable(
       (s = spf_route_table_elapsed_ms(table_, &routeMs_)) != SPF_OK) {
     cleanup("elapsed", s);
   }
+  Counters::add("decision.route_table_run_us", usSince(tp));
   Counters::add("decision.route_table_builds", 1);
 }
 
 AllNodesRouteTable::~AllNodesRouteTable() {
+  const auto tp = std::chrono::steady_clock::now();
   spf_route_table_destroy(table_);
   spf_query_destroy(query_);
   spf_graph_destroy(graph_);
+  Counters::add("decision.route_table_destroy_us", usSince(tp));
 }
 
 uint64_t AllNodesRouteTable::countRoutes() const {

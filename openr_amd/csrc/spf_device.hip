@@ -302,7 +302,201 @@ struct SsspArgs {
   // what-if screen: queries whose rows were copied from the baseline run
   // (skip[q] != 0) are not recomputed; nullptr = none
   const uint32_t* skip;
+  // what-if repair (IGN batches behind the screen; base_dist = nullptr: off):
+  // a query the screen could not resolve starts from its baseline rows and
+  // recomputes only the nodes downstream of its tight ignored links
+  // (whatif_repair_init); base rows in the word layout of the query's own
+  const uint32_t* base_dist = nullptr; // [nb][Vp]
+  const uint64_t* base_nh = nullptr;
+  const uint64_t* base_nh_off = nullptr;
+  const uint32_t* base_of = nullptr;
+  const uint32_t* link_half = nullptr; // [2 * L] half-edges of each link
+  uint32_t L = 0;
+  // queries beyond the first gridDim.x are claimed from this counter (zeroed
+  // per launch); nullptr: static stride
+  uint32_t* qctr = nullptr;
+  // OPENR_SPF_WHATIF_STATS: repaired / from-scratch queries, |K| total, PULL
+  // rounds, and wall-clock ticks (100 MHz) of copy / init / rounds / output
+  unsigned long long* stats = nullptr;
 };
+
+__device__ __forceinline__ bool bit_test(const uint32_t* b, uint32_t v) {
+  return (b[v >> 5] >> (v & 31)) & 1u;
+}
+// set bit v; true if this call set it
+__device__ __forceinline__ bool bit_claim(uint32_t* b, uint32_t v) {
+  const uint32_t m = 1u << (v & 31);
+  return !(atomicOr(&b[v >> 5], m) & m);
+}
+
+// n elements src -> dst by a workgroup of BS threads, U loads in flight per
+// thread (a plain strided loop waits out one load latency per element)
+template <typename T, uint32_t BS, int U = 8>
+__device__ __forceinline__ void block_copy(T* __restrict__ dst, const T* __restrict__ src, size_t n) {
+  size_t i = threadIdx.x;
+  for (; i + (size_t)(U - 1) * BS < n; i += (size_t)U * BS) {
+    T t[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      t[k] = src[i + (size_t)k * BS];
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      dst[i + (size_t)k * BS] = t[k];
+    }
+  }
+  for (; i < n; i += BS) {
+    dst[i] = src[i];
+  }
+}
+
+// What-if repair prologue (spf_sssp_kernel, IGN with baseline rows): the
+// query's rows start as the baseline run's from the same source, then
+//  K  = heads of the ignored links' halves that are tight usable edges of the
+//       baseline (d[u] + w == d[v], u the source or transit) and every node
+//       reachable from them over tight usable non-ignored edges: no node
+//       outside K had a shortest path through an ignored link, so its
+//       distance and next-hop set are unchanged (and no path through K can
+//       tie it later: a K node's distance only grows, and an edge K -> w
+//       that was not tight stays strictly longer);
+//  ok = nodes of K reachable over tight usable non-ignored edges from outside
+//       K: their distance is still achieved (exact), only their next hops
+//       may shrink;
+// K \ ok is reset to unreached, and all of K is queued for the PULL step
+// (distance + next-hop union from every in-edge), so the rounds that follow
+// reach the same fixpoint as a run from scratch.  kb / okb:
+// zeroed LDS bitmaps; act / chg: clear on entry and exit.  Returns |K|, with
+// K's ids in `queue`, or kInf32 (bitmaps clear) when K passes V / 4 nodes and
+// the query should run from scratch instead.
+template <typename QT, bool UNIT>
+__device__ uint32_t whatif_repair_init(
+    const SsspArgs& a, uint32_t src, uint32_t* dist, uint32_t* kb, uint32_t* okb,
+    uint32_t* act, const uint32_t* tr, QT* queue, uint32_t* ctl, const uint32_t* ignp,
+    uint32_t nign) {
+  const uint32_t tid = threadIdx.x, G = a.G, V = a.V, nbw = a.nbw;
+  const uint32_t lg = tid & (G - 1), grp = tid / G, ngrp = kBlock / G;
+  auto usable = [&](uint32_t u) { return u == src || ((tr[u >> 5] >> (u & 31)) & 1u); };
+  auto ignored = [&](uint32_t e) { return nign && in_sorted(ignp, nign, a.link[e]); };
+  auto mark = [&](uint32_t* bm, uint32_t v) {
+    const uint32_t m = 1u << (v & 31);
+    if (!(atomicOr(&bm[v >> 5], m) & m)) {
+      atomicOr(&act[v >> 5], m);
+    }
+  };
+  // seeds: heads of tight ignored halves
+  for (uint32_t i = tid; i < 2 * nign; i += kBlock) {
+    const uint32_t l = ignp[i >> 1];
+    const uint32_t e = l < a.L ? a.link_half[2 * (size_t)l + (i & 1)] : kInf32;
+    if (e == kInf32) {
+      continue;
+    }
+    const uint32_t u = a.col[a.rev[e]], v = a.col[e];
+    const uint32_t du = dist[u];
+    if (du != kInf32 && usable(u) && du + (UNIT ? 1u : a.wout[e]) == dist[v]) {
+      mark(kb, v);
+    }
+  }
+  __syncthreads();
+  // K: closure over tight usable non-ignored edges
+  uint32_t ksize = 0;
+  for (;;) {
+    const uint32_t n = compact_bits<QT>(act, nbw, queue, ctl + 1);
+    __syncthreads();
+    ksize += n;
+    if (!n) {
+      break;
+    }
+    if (ksize * 4 > V) {
+      // K spans most of the graph (a failure next to the source): the
+      // caller's run from scratch is cheaper than repairing it
+      for (uint32_t w = tid; w < nbw; w += kBlock) {
+        kb[w] = 0;
+        act[w] = 0;
+      }
+      __syncthreads();
+      return kInf32;
+    }
+    for (uint32_t i = grp; i < n; i += ngrp) {
+      const uint32_t u = queue[i];
+      if (!usable(u)) {
+        continue;
+      }
+      const uint32_t du = dist[u];
+      for (uint32_t e = a.row[u] + lg; e < a.row[u + 1]; e += G) {
+        const uint32_t v = a.col[e];
+        if (du + (UNIT ? 1u : a.wout[e]) == dist[v] && !bit_test(kb, v) && !ignored(e)) {
+          mark(kb, v);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // ok seeds: K nodes with a tight usable non-ignored in-edge from outside K
+  // (K listed into the queue first: |K| is usually a handful of nodes)
+  for (uint32_t w = tid; w < nbw; w += kBlock) {
+    act[w] = kb[w];
+  }
+  __syncthreads();
+  const uint32_t nk = compact_bits<QT>(act, nbw, queue, ctl + 1);
+  __syncthreads();
+  for (uint32_t i = grp; i < nk; i += ngrp) {
+    const uint32_t v = queue[i];
+    const uint32_t dv = dist[v];
+    bool found = false;
+    for (uint32_t e = a.row[v] + lg; e < a.row[v + 1] && !found; e += G) {
+      const uint32_t u = a.col[e];
+      if (bit_test(kb, u) || !usable(u)) {
+        continue;
+      }
+      const uint32_t du = dist[u];
+      found = du != kInf32 && du + (UNIT ? 1u : a.win[e]) == dv && !ignored(e);
+    }
+    found = grp_min(found ? 0u : 1u, (int)G) == 0;
+    if (found && lg == 0) {
+      mark(okb, v);
+    }
+  }
+  __syncthreads();
+  // ok: closure inside K over tight usable non-ignored edges
+  for (;;) {
+    const uint32_t n = compact_bits<QT>(act, nbw, queue, ctl + 1);
+    __syncthreads();
+    if (!n) {
+      break;
+    }
+    for (uint32_t i = grp; i < n; i += ngrp) {
+      const uint32_t u = queue[i];
+      if (!usable(u)) {
+        continue;
+      }
+      const uint32_t du = dist[u];
+      for (uint32_t e = a.row[u] + lg; e < a.row[u + 1]; e += G) {
+        const uint32_t v = a.col[e];
+        if (bit_test(kb, v) && !bit_test(okb, v) && du + (UNIT ? 1u : a.wout[e]) == dist[v] &&
+            !ignored(e)) {
+          mark(okb, v);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // K \ ok reset; all of K queued for the PULL step
+  for (uint32_t w = tid; w < nbw; w += kBlock) {
+    uint32_t bad = kb[w] & ~okb[w];
+    act[w] = kb[w];
+    kb[w] = 0;
+    okb[w] = 0;
+    while (bad) {
+      const uint32_t k = __ffs(bad) - 1;
+      bad &= bad - 1;
+      dist[w * 32 + k] = kInf32;
+    }
+  }
+  __syncthreads();
+  const uint32_t n = compact_bits<QT>(act, nbw, queue, ctl + 1);
+  __syncthreads();
+  return n;
+}
 
 // WMAX: max next-hop words (0 = distances only).  UNIT: every hop costs 1.
 // IGN: per-query ignored links.  GMEM: distances / queue in global memory.
@@ -321,13 +515,17 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
   uint32_t* tr = chg + nbw;
   uint32_t* ctl = tr + nbw;
   uint32_t* ignl = ctl + kCtlWords;
+  // what-if repair bitmaps (K, ok) behind the ignore list
+  const bool rep = IGN && a.base_dist != nullptr;
+  uint32_t* kb = ignl + a.ign_cap;
+  uint32_t* okb = kb + (rep ? nbw : 0);
   QT* queue;
   uint32_t* dist;
   if constexpr (GMEM) {
     queue = a.gscratch + (size_t)blockIdx.x * V;
     dist = nullptr;
   } else {
-    queue = reinterpret_cast<QT*>(ignl + a.ign_cap);
+    queue = reinterpret_cast<QT*>(okb + (rep ? nbw : 0));
     dist = reinterpret_cast<uint32_t*>(queue + ((V + 1) & ~1u));
   }
 
@@ -335,10 +533,32 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
     act[i] = 0;
     chg[i] = 0;
     tr[i] = a.trbits[i];
+    if (rep) {
+      kb[i] = 0;
+      okb[i] = 0;
+    }
   }
+  __syncthreads();
 
-  for (uint32_t q = blockIdx.x; q < a.nq; q += gridDim.x) {
-    if (a.skip && a.skip[q]) {
+  auto next_query = [&](uint32_t q) -> uint32_t {
+    if (!a.qctr) {
+      return q + gridDim.x;
+    }
+    __syncthreads(); // every lane has read ctl[kCtlWords - 1] of this query
+    if (tid == 0) {
+      ctl[kCtlWords - 1] = gridDim.x + atomicAdd(a.qctr, 1u);
+    }
+    __syncthreads();
+    return ctl[kCtlWords - 1];
+  };
+  // repair batches claim in two passes: first the queries whose failed link
+  // leaves the source (skip == 2, the screen's mark: their K is most of the
+  // graph and they run from scratch), then the rest (skip == 0)
+  const bool two_pass = rep && a.qctr;
+  const uint32_t nclaim = two_pass ? 2 * a.nq : a.nq;
+  for (uint32_t c = blockIdx.x; c < nclaim; c = next_query(c)) {
+    const uint32_t q = c < a.nq ? c : c - a.nq;
+    if (two_pass ? a.skip[q] != (c < a.nq ? 2u : 0u) : (a.skip && a.skip[q])) {
       continue; // uniform per block
     }
     const uint32_t src = a.src[q];
@@ -364,24 +584,61 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
       Wm = a.nh_w[q];
       nhrow = a.nh_out + a.nh_off[q];
     }
-    for (uint32_t v = tid; v < V; v += kBlock) {
-      dist[v] = kInf32;
+    uint32_t qlen;
+    bool pull_first = false;
+    unsigned long long tk0 = 0, tk1 = 0, tk2 = 0;
+    uint32_t rounds = 0;
+    if (a.stats && tid == 0) {
+      tk0 = wall_clock64();
     }
-    __syncthreads();
-    if (tid == 0) {
-      dist[src] = 0;
-      queue[0] = (QT)src;
-      ctl[0] = 1;
-    }
-    if constexpr (WMAX > 0) {
-      if (tid < Wm) {
-        nhrow[(size_t)src * Wm + tid] = 0; // the source has no next hop
+    if (rep) {
+      // baseline rows, then only K is recomputed (whatif_repair_init)
+      const uint32_t b = a.base_of[q];
+      block_copy<uint32_t, kBlock>(dist, a.base_dist + (size_t)b * a.Vp, V);
+      if constexpr (WMAX > 0) {
+        block_copy<uint64_t, kBlock>(nhrow, a.base_nh + a.base_nh_off[b], (size_t)V * Wm);
+      }
+      __syncthreads();
+      if (a.stats && tid == 0) {
+        tk1 = wall_clock64();
+      }
+      qlen = whatif_repair_init<QT, UNIT>(a, src, dist, kb, okb, act, tr, queue, ctl, ignp, nign);
+      pull_first = qlen != kInf32;
+      if (a.stats && tid == 0) {
+        atomicAdd(&a.stats[pull_first ? 0 : 1], 1ull);
+        atomicAdd(&a.stats[2], pull_first ? (unsigned long long)qlen : 0ull);
+        tk2 = wall_clock64();
+        atomicAdd(&a.stats[4], tk1 - tk0);
+        atomicAdd(&a.stats[5], tk2 - tk1);
       }
     }
-    __syncthreads();
-    uint32_t qlen = ctl[0];
+    if (!pull_first) {
+      for (uint32_t v = tid; v < V; v += kBlock) {
+        dist[v] = kInf32;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        dist[src] = 0;
+        queue[0] = (QT)src;
+        ctl[0] = 1;
+      }
+      if constexpr (WMAX > 0) {
+        if (tid < Wm) {
+          nhrow[(size_t)src * Wm + tid] = 0; // the source has no next hop
+        }
+      }
+      __syncthreads();
+      qlen = ctl[0];
+    }
 
+    if (a.stats && tid == 0 && !tk2) {
+      tk2 = wall_clock64();
+    }
     while (qlen) {
+      ++rounds;
+      if (pull_first) {
+        pull_first = false; // the queue holds K: straight to the PULL step
+      } else {
       // ---- PUSH: changed nodes mark the neighbours they can improve or tie
       for (uint32_t i = grp; i < qlen; i += ngrp) {
         const uint32_t u = queue[i];
@@ -409,6 +666,7 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
       __syncthreads();
       qlen = compact_bits<QT>(act, nbw, queue, ctl + 1);
       __syncthreads();
+      }
 
       // ---- PULL: marked nodes recompute (dist, next hops) from all in-edges
       for (uint32_t i = grp; i < qlen; i += ngrp) {
@@ -507,6 +765,12 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
       __syncthreads();
     }
 
+    unsigned long long tk3 = 0;
+    if (a.stats && tid == 0) {
+      tk3 = wall_clock64();
+      atomicAdd(&a.stats[3], (unsigned long long)rounds);
+      atomicAdd(&a.stats[6], tk3 - tk2);
+    }
     if constexpr (!GMEM) {
       uint32_t* out = a.dist_out + (size_t)q * a.Vp;
       for (uint32_t v = tid; v < V; v += kBlock) {
@@ -525,6 +789,9 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
       }
     }
     __syncthreads();
+    if (a.stats && tid == 0) {
+      atomicAdd(&a.stats[7], wall_clock64() - tk3);
+    }
   }
 }
 
@@ -666,14 +933,6 @@ __device__ __forceinline__ uint32_t min_pending_bucket(
   return r;
 }
 
-__device__ __forceinline__ bool bit_test(const uint32_t* b, uint32_t v) {
-  return (b[v >> 5] >> (v & 31)) & 1u;
-}
-// set bit v; true if this call set it
-__device__ __forceinline__ bool bit_claim(uint32_t* b, uint32_t v) {
-  const uint32_t m = 1u << (v & 31);
-  return !(atomicOr(&b[v >> 5], m) & m);
-}
 
 // Repair prologue of the seeded delta-stepping run (spf_table_repair) for
 // one table row `dist` of source `src`, after edges were REMOVED (link down,
@@ -4172,6 +4431,10 @@ struct WhatifArgs {
   uint32_t Vp;
   uint32_t L; // link ids >= L match no edge (ignored)
   uint32_t want_nh;
+  uint32_t unit; // SPF_F_UNIT_METRIC: every hop costs 1
+  // repair batches: a tight ignored link of the source itself is flagged
+  // skip = 2 (spf_sssp_kernel claims those first)
+  uint32_t mark_heavy;
 };
 
 __global__ __launch_bounds__(256) void spf_whatif_screen_kernel(WhatifArgs a) {
@@ -4179,7 +4442,7 @@ __global__ __launch_bounds__(256) void spf_whatif_screen_kernel(WhatifArgs a) {
   const uint32_t s = a.src[q], b = a.base_of[q];
   const uint32_t* bd = a.base_dist + (size_t)b * a.Vp;
   const uint32_t lo = a.ign_off[q], n = a.ign_off[q + 1] - lo;
-  int tight = 0;
+  int tight = 0, heavy = 0;
   for (uint32_t i = threadIdx.x; i < 2 * n; i += blockDim.x) {
     const uint32_t l = a.ign[lo + (i >> 1)];
     const uint32_t e = l < a.L ? a.link_half[2 * (size_t)l + (i & 1)] : kInf32;
@@ -4191,26 +4454,22 @@ __global__ __launch_bounds__(256) void spf_whatif_screen_kernel(WhatifArgs a) {
     if (du == kInf32 || (u != s && !((a.trbits[u >> 5] >> (u & 31)) & 1u))) {
       continue;
     }
-    tight |= du + a.wout[e] == bd[v];
+    const bool t = du + (a.unit ? 1u : a.wout[e]) == bd[v];
+    tight |= t;
+    heavy |= t && u == s;
   }
   tight = __syncthreads_or(tight);
+  heavy = __syncthreads_or(heavy);
   if (threadIdx.x == 0) {
-    a.skip[q] = tight ? 0u : 1u;
+    a.skip[q] = tight ? (heavy && a.mark_heavy ? 2u : 0u) : 1u;
   }
   if (tight) {
     return;
   }
-  uint32_t* dst = a.dist_out + (size_t)q * a.Vp;
-  for (uint32_t v = threadIdx.x; v < a.V; v += blockDim.x) {
-    dst[v] = bd[v];
-  }
+  block_copy<uint32_t, 256>(a.dist_out + (size_t)q * a.Vp, bd, a.V);
   if (a.want_nh) {
-    const size_t n64 = (size_t)a.V * a.nh_w[q];
-    const uint64_t* from = a.base_nh + a.base_nh_off[b];
-    uint64_t* to = a.nh_out + a.nh_off[q];
-    for (size_t i = threadIdx.x; i < n64; i += blockDim.x) {
-      to[i] = from[i];
-    }
+    block_copy<uint64_t, 256>(a.nh_out + a.nh_off[q], a.base_nh + a.base_nh_off[b],
+                              (size_t)a.V * a.nh_w[q]);
   }
 }
 
@@ -5197,6 +5456,9 @@ struct spf_query {
   // LDS-resident rows (spf_dlds_kernel) first, the HBM-row pass only for the
   // sources whose values left the 12-bit range
   bool dlds = false;
+  // what-if batch behind the screen whose tight queries start from the
+  // baseline rows (spf_sssp_kernel repair mode, OPENR_SPF_WHATIF_REPAIR)
+  bool repair = false;
   uint32_t dlds_shift = 4, dlds_grid = 0;
   size_t dlds_lds = 0;
   uint32_t* d_ovf = nullptr; // [0] overflow count, [1] claim counter, [2..] list
@@ -6792,7 +7054,13 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     const size_t dstep_lds =
         (2 * (size_t)g->nbw + kCtlWords + (has_ign ? std::min(max_ign, kIgnLdsMax) : 0)) * 4 +
         (q->dstep_lbk ? (((size_t)V + 15) & ~(size_t)15) : 0);
-    const bool dstep = big && !uniform && dstep_lds <= kLdsLimit && maxw <= 16 &&
+    // a few sources of a weighted graph that fits LDS (a what-if baseline, a
+    // RouteDb build's SPFs): one workgroup per source either way, and bucket
+    // order relaxes most nodes once where the frontier rounds of
+    // spf_sssp_kernel re-relax them (OPENR_SPF_FEW_DSTEP=0 disables)
+    const bool few = !big && !has_ign && V >= 4096 && (size_t)nq * 16 <= (size_t)g->num_cus &&
+                     env_flag("OPENR_SPF_FEW_DSTEP", 1);
+    const bool dstep = (big || few) && !uniform && dstep_lds <= kLdsLimit && maxw <= 16 &&
                        getenv("OPENR_SPF_DSTEP") == nullptr;
     // many distance-only rows of such a graph: 32 sources per workgroup over
     // a node-major slab.  Measured slower than per-source delta-stepping on
@@ -6819,7 +7087,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       msd_perm = msd_batches(g, desc->sources, nq, !(cl && atoi(cl) == 0));
       q->msd_nbatch = (uint32_t)(msd_perm.size() / kMsdK);
       q->grid = std::min<uint32_t>(q->msd_nbatch, (uint32_t)g->num_cus);
-    } else if (V <= 65535 && lds <= kLdsLimit) {
+    } else if (V <= 65535 && lds <= kLdsLimit && !(few && dstep)) {
       q->dist = bfs ? DistPlan::BfsLds : DistPlan::SsspLds;
       q->lds_bytes = lds;
       const uint32_t per_cu =
@@ -7137,6 +7405,22 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       if (pool_malloc((void**)&q->d_skip, (size_t)nq * 4) != hipSuccess) {
         return bail(fail(SPF_E_NOMEM, "what-if screen flags"));
       }
+      // repair mode: the K / ok bitmaps join the workgroup's LDS image
+      // (positive metrics only: the K rule needs a DAG of tight edges)
+      const size_t extra = 2 * (size_t)g->nbw * 4;
+      if ((q->dist == DistPlan::SsspLds || q->dist == DistPlan::SsspGmem) && !g->n_zero &&
+          q->lds_bytes + extra <= kLdsLimit && env_flag("OPENR_SPF_WHATIF_REPAIR", 1)) {
+        q->repair = true;
+        q->lds_bytes += extra;
+        if (q->dist == DistPlan::SsspLds) {
+          const uint32_t per_cu =
+              std::max<uint32_t>(1, std::min<uint32_t>(4, kLdsLimit / q->lds_bytes));
+          q->grid = std::min<uint32_t>(std::max<uint32_t>(nq, 1), (uint32_t)g->num_cus * per_cu);
+        }
+        if (!q->d_qctr && pool_malloc((void**)&q->d_qctr, 4) != hipSuccess) {
+          return bail(fail(SPF_E_NOMEM, "what-if claim counter"));
+        }
+      }
     }
   }
   if (ev_get(&q->ev0) != hipSuccess || ev_get(&q->ev1) != hipSuccess ||
@@ -7184,6 +7468,24 @@ int launch_sssp(spf_query* q) {
   a.G = g->G;
   a.ign_cap = q->ign_cap;
   a.skip = q->d_skip;
+  if (q->repair) {
+    const spf_query* b = q->base;
+    if (b->Vp != q->Vp || b->nq == 0) {
+      return fail(SPF_E_INVALID, "baseline row layout differs");
+    }
+    a.base_dist = (const uint32_t*)b->d_dist;
+    a.base_nh = b->d_nh;
+    a.base_nh_off = b->d_nh_off;
+    a.base_of = q->d_base_of;
+    a.link_half = g->d_link_half;
+    a.L = g->L;
+    a.qctr = q->d_qctr;
+    HIP_TRY(hipMemsetAsync(q->d_qctr, 0, 4, g->stream));
+    if (env_flag("OPENR_SPF_WHATIF_STATS", 0)) {
+      HIP_TRY(hipMalloc((void**)&a.stats, 8 * sizeof(unsigned long long)));
+      HIP_TRY(hipMemsetAsync(a.stats, 0, 8 * sizeof(unsigned long long), g->stream));
+    }
+  }
   auto kern = spf_sssp_kernel<WMAX, UNIT, IGN, GMEM>;
   HIP_TRY(hipFuncSetAttribute(
       (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -7191,6 +7493,16 @@ int launch_sssp(spf_query* q) {
   hipLaunchKernelGGL(
       kern, dim3(q->grid), dim3(kBlock), q->lds_bytes, g->stream, a);
   HIP_TRY(hipGetLastError());
+  if (a.stats) {
+    unsigned long long h[8];
+    HIP_TRY(hipStreamSynchronize(g->stream));
+    HIP_TRY(hipMemcpy(h, a.stats, sizeof(h), hipMemcpyDeviceToHost));
+    HIP_TRY(hipFree(a.stats));
+    fprintf(stderr,
+            "[whatif stats] nq=%u grid=%u repaired=%llu scratch=%llu K=%llu rounds=%llu "
+            "ticks(100MHz, summed over queries) copy=%llu init=%llu rounds=%llu output=%llu\n",
+            q->nq, q->grid, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
+  }
   return SPF_OK;
 }
 
@@ -7826,6 +8138,8 @@ int run_screen(spf_query* q) {
   a.Vp = q->Vp;
   a.L = g->L;
   a.want_nh = (q->flags & SPF_F_NEXTHOPS) ? 1u : 0u;
+  a.unit = (q->flags & SPF_F_UNIT_METRIC) ? 1u : 0u;
+  a.mark_heavy = q->repair ? 1u : 0u;
   if (b->Vp != q->Vp) {
     return fail(SPF_E_INVALID, "baseline row stride differs");
   }
@@ -7981,6 +8295,24 @@ int spf_query_elapsed_ms(spf_query* q, float* ms) {
   }
   HIP_TRY(hipEventSynchronize(q->ev1));
   HIP_TRY(hipEventElapsedTime(ms, q->ev0, q->ev1));
+  return SPF_OK;
+}
+
+int spf_query_screened(spf_query* q, uint32_t* screened, uint32_t* has_screen) {
+  if (!q || !screened || !has_screen || !q->ran) {
+    return fail(SPF_E_INVALID, "query has not run");
+  }
+  *screened = 0;
+  *has_screen = q->d_skip ? 1u : 0u;
+  if (!q->d_skip) {
+    return SPF_OK;
+  }
+  HIP_TRY(hipEventSynchronize(q->ev1));
+  std::vector<uint32_t> skip(q->nq);
+  HIP_TRY(hipMemcpy(skip.data(), q->d_skip, (size_t)q->nq * 4, hipMemcpyDeviceToHost));
+  for (uint32_t v : skip) {
+    *screened += v == 1; // 2 = a heavy repair (not screened)
+  }
   return SPF_OK;
 }
 

@@ -27,7 +27,12 @@ struct LinkState::Engine {
   std::vector<uint64_t> metric;
   std::vector<uint8_t> overloaded;
   std::vector<std::shared_ptr<Link>> links; // link id -> Link
-  std::unordered_map<const Link*, uint32_t> linkIndex;
+  // Link -> link id of this build: the tag buildGraph left on the Link
+  // (Link::engineEpoch / engineId), ~0u for links that are not up links of it
+  uint64_t epoch{0};
+  uint32_t linkIdOf(const Link* l) const {
+    return l->engineEpoch == epoch ? l->engineId : ~0u;
+  }
   std::vector<std::array<uint32_t, 2>> halves; // link id -> half-edge from first/second node
   spf_graph* graph{nullptr};
   // the same graph on every device of the multi-GPU fan-out (setSpfDevices),

@@ -12,6 +12,7 @@
 #include "FollyHash.h"
 #include "Engine.h"
 
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -443,36 +444,107 @@ void buildGraph(
   eng.linkId.clear();
   eng.metric.clear();
   eng.links.clear();
-  eng.linkIndex.clear();
   eng.overloaded.assign(V, 0);
   // half-edge slots per link: [0] = from firstNodeName, [1] = from second
   auto& halves = eng.halves;
   halves.clear();
-  for (uint32_t u = 0; u < V; ++u) {
+  // Link ids without hashing, on the host pool.  Ids are name ranks, so a
+  // link's side-0 half (from firstNodeName, the smaller name) is the one met
+  // first in row order: link ids number the side-0 halves in CSR order (the
+  // order a serial walk would give).  Pass A counts each row's up links and
+  // side-0 halves, pass B fills the rows and tags each link with its id
+  // (Link::engineEpoch / engineId, per build), pass C completes the side-1
+  // halves from the tags: each half's other endpoint is the node holding the
+  // other half, so no name -> id lookup per half-edge.
+  static std::atomic<uint64_t> epochs{0};
+  const uint64_t epoch = eng.epoch = ++epochs;
+  const unsigned nt = hostThreads(V, 256);
+  std::vector<const LinkState::LinkSet*> sets(V, nullptr);
+  std::vector<uint32_t> firstBase(V + 1, 0);
+  parallelFor(V, nt, [&](size_t u, unsigned) {
     const std::string& name = eng.names[u];
     eng.overloaded[u] = ls.isNodeOverloaded(name) ? 1 : 0;
     auto it = linkMap.find(name);
-    if (it != linkMap.end()) {
-      for (const auto& link : it->second) {
-        if (!link->isUp()) {
-          continue;
-        }
-        auto [pos, inserted] =
-            eng.linkIndex.emplace(link.get(), (uint32_t)eng.links.size());
-        if (inserted) {
-          eng.links.push_back(link);
-          halves.push_back({~0u, ~0u});
-        }
-        const uint32_t lid = pos->second;
-        const std::string& other = link->getOtherNodeName(name);
-        const uint32_t e = (uint32_t)eng.col.size();
-        eng.col.push_back(eng.ids.at(other));
-        eng.linkId.push_back(lid);
-        eng.metric.push_back(link->getMetricFromNode(name));
-        halves[lid][name == link->firstNodeName() ? 0 : 1] = e;
+    if (it == linkMap.end()) {
+      return;
+    }
+    sets[u] = &it->second;
+    uint32_t d = 0, f = 0;
+    for (const auto& link : it->second) {
+      if (link->isUp()) {
+        ++d;
+        f += name == link->firstNodeName() ? 1u : 0u;
       }
     }
-    eng.row[u + 1] = (uint32_t)eng.col.size();
+    eng.row[u + 1] = d;
+    firstBase[u + 1] = f;
+  }, 64);
+  for (uint32_t u = 0; u < V; ++u) {
+    eng.row[u + 1] += eng.row[u];
+    firstBase[u + 1] += firstBase[u];
+  }
+  const uint32_t E0 = eng.row[V], L0 = firstBase[V];
+  eng.col.assign(E0, ~0u);
+  eng.linkId.assign(E0, ~0u);
+  eng.metric.assign(E0, 0);
+  eng.links.assign(L0, nullptr);
+  halves.assign(L0, {~0u, ~0u});
+  std::vector<uint32_t> firstNode(L0);
+  std::vector<const std::shared_ptr<Link>*> halfLink(E0); // the row's set element
+  parallelFor(V, nt, [&](size_t u, unsigned) {
+    if (!sets[u]) {
+      return;
+    }
+    const std::string& name = eng.names[u];
+    uint32_t e = eng.row[u], lid = firstBase[u];
+    for (const auto& link : *sets[u]) {
+      if (!link->isUp()) {
+        continue;
+      }
+      eng.metric[e] = link->getMetricFromNode(name);
+      halfLink[e] = &link;
+      if (name == link->firstNodeName()) {
+        link->engineEpoch = epoch;
+        link->engineId = lid;
+        eng.links[lid] = link;
+        halves[lid][0] = e;
+        firstNode[lid] = (uint32_t)u;
+        eng.linkId[e] = lid++;
+      }
+      ++e;
+    }
+  }, 64);
+  parallelFor(V, nt, [&](size_t u, unsigned) {
+    for (uint32_t e = eng.row[u]; e < eng.row[u + 1]; ++e) {
+      const Link* link = halfLink[e]->get();
+      if (eng.linkId[e] != ~0u || link->engineEpoch != epoch) {
+        continue; // side 0, or a link its side-0 endpoint does not list
+      }
+      const uint32_t lid = link->engineId;
+      eng.linkId[e] = lid;
+      eng.col[e] = firstNode[lid];
+      halves[lid][1] = e;
+      eng.col[halves[lid][0]] = (uint32_t)u;
+    }
+  }, 64);
+  // halves the passes could not pair (not expected: linkMap lists every
+  // link under both endpoints) resolve by name
+  for (uint32_t u = 0; u < V; ++u) {
+    for (uint32_t e = eng.row[u]; e < eng.row[u + 1]; ++e) {
+      const std::shared_ptr<Link>& link = *halfLink[e];
+      if (eng.linkId[e] == ~0u) {
+        const uint32_t lid = (uint32_t)eng.links.size();
+        link->engineEpoch = epoch;
+        link->engineId = lid;
+        eng.links.push_back(link);
+        halves.push_back({~0u, ~0u});
+        halves[lid][eng.names[u] == link->firstNodeName() ? 0 : 1] = e;
+        eng.linkId[e] = lid;
+      }
+      if (eng.col[e] == ~0u) {
+        eng.col[e] = eng.ids.at(link->getOtherNodeName(eng.names[u]));
+      }
+    }
   }
   const uint32_t E = (uint32_t)eng.col.size();
   eng.rev.assign(E, 0);
@@ -1252,12 +1324,12 @@ void LinkState::patchMemo(
   std::vector<uint32_t> edges;
   std::vector<uint64_t> metrics;
   for (const auto& [link, from] : metricPatches) {
-    auto li = eng.linkIndex.find(link.get());
-    if (li == eng.linkIndex.end()) {
+    const uint32_t li = eng.linkIdOf(link.get());
+    if (li == ~0u) {
       clearMemo(); // not an up link of the device graph: rebuild
       return;
     }
-    const auto& h = eng.halves[li->second];
+    const auto& h = eng.halves[li];
     const uint32_t e = from == link->firstNodeName() ? h[0] : h[1];
     if (e == ~0u) {
       clearMemo();
@@ -1793,16 +1865,16 @@ std::unique_ptr<LinkState::SpfBatch> LinkState::runSpfBatch(
   std::vector<std::vector<uint32_t>> lists(nq);
   for (size_t i = 0; i < nq; ++i) {
     for (const auto& link : linksToIgnore[i]) {
-      auto li = eng.linkIndex.find(link.get());
-      if (li == eng.linkIndex.end()) {
+      uint32_t li = eng.linkIdOf(link.get());
+      if (li == ~0u) {
         // an equal Link object of this LinkState (the caller may hold a copy)
         auto own = allLinks_.find(link);
         if (own != allLinks_.end()) {
-          li = eng.linkIndex.find(own->get());
+          li = eng.linkIdOf(own->get());
         }
       }
-      if (li != eng.linkIndex.end()) {
-        lists[i].push_back(li->second);
+      if (li != ~0u) {
+        lists[i].push_back(li);
       }
     }
     std::sort(lists[i].begin(), lists[i].end());

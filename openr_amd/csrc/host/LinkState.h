@@ -87,6 +87,10 @@ class Link {
 
  public:
   const size_t hash{0};
+  // the engine build that last numbered this link (LinkState.cpp buildGraph)
+  // and the id it gave; bookkeeping of the device CSR, not link state
+  mutable uint64_t engineEpoch{0};
+  mutable uint32_t engineId{0};
 
   void setHoldUpTtl(LinkStateMetric ttl);
   bool isUp() const;

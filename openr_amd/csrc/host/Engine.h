@@ -34,6 +34,9 @@ struct LinkState::Engine {
     return l->engineEpoch == epoch ? l->engineId : ~0u;
   }
   std::vector<std::array<uint32_t, 2>> halves; // link id -> half-edge from first/second node
+  // link ids freed by in-place link removals (LinkState::patchStructure):
+  // links[id] == nullptr, reused by the next link that comes up
+  std::vector<uint32_t> freeIds;
   spf_graph* graph{nullptr};
   // the same graph on every device of the multi-GPU fan-out (setSpfDevices),
   // created on the first fanned-out batch and patched with the same churn as

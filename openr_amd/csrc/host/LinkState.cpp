@@ -1445,6 +1445,272 @@ void LinkState::patchMemo(
           .count());
 }
 
+// Link flaps in place (SURVEY §8(f) row 2 for the product LinkState): the
+// links whose up-ness flipped change the rows of their endpoints only, so
+// those rows are rebuilt from linkMap_ and every other row is copied (node
+// ids are name ranks and the node set is unchanged).  Link ids of links that
+// stay are kept (a removed link's id is freed, a new link takes a free id or
+// the next one), so the Link tags stay valid; half-edge indices of the kept
+// rows shift by their row's offset change.  The device graph is recreated
+// from the spliced arrays; SPF memos survive where no edge delta can touch
+// them (the same screen as patchMemo).  Returns false (nothing changed) when
+// a link's endpoint is not a node of the graph, or the engine is not built.
+bool LinkState::patchStructure(
+    const std::vector<std::shared_ptr<Link>>& down,
+    const std::vector<std::shared_ptr<Link>>& up,
+    const std::vector<std::string>& transitNodes,
+    const std::vector<std::pair<std::shared_ptr<Link>, std::string>>& metricPatches) const {
+  static const bool enabled = [] {
+    const char* e = std::getenv("OPENR_LS_INPLACE_LINKS");
+    return !(e && std::atoi(e) == 0);
+  }();
+  if (!enabled || !engine_ || !engine_->built || !engine_->graph) {
+    return false;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  auto& eng = *engine_;
+  const uint32_t V = (uint32_t)eng.names.size();
+  std::vector<uint8_t> aff(V, 0);
+  auto nodeOf = [&](const std::string& n) -> uint32_t {
+    auto it = eng.ids.find(n);
+    return it == eng.ids.end() ? ~0u : it->second;
+  };
+  for (const auto& l : down) {
+    const uint32_t a = nodeOf(l->firstNodeName()), b = nodeOf(l->secondNodeName());
+    if (a == ~0u || b == ~0u || eng.linkIdOf(l.get()) == ~0u) {
+      return false;
+    }
+    aff[a] = aff[b] = 1;
+  }
+  for (const auto& l : up) {
+    const uint32_t a = nodeOf(l->firstNodeName()), b = nodeOf(l->secondNodeName());
+    if (a == ~0u || b == ~0u || eng.linkIdOf(l.get()) != ~0u || !l->isUp()) {
+      return false;
+    }
+    aff[a] = aff[b] = 1;
+  }
+  // new rows of the affected nodes, in linksFromNode order (up links only)
+  std::vector<uint32_t> affNodes;
+  for (uint32_t u = 0; u < V; ++u) {
+    if (aff[u]) {
+      affNodes.push_back(u);
+    }
+  }
+  std::vector<std::vector<const std::shared_ptr<Link>*>> affRows(affNodes.size());
+  std::vector<uint32_t> newRow(V + 1, 0);
+  {
+    size_t k = 0;
+    for (uint32_t u = 0; u < V; ++u) {
+      uint32_t d = eng.row[u + 1] - eng.row[u];
+      if (aff[u]) {
+        for (const auto& link : linksFromNode(eng.names[u])) {
+          if (link->isUp()) {
+            affRows[k].push_back(&link);
+          }
+        }
+        d = (uint32_t)affRows[k++].size();
+      }
+      newRow[u + 1] = newRow[u] + d;
+    }
+  }
+  const uint32_t E = newRow[V];
+  // link ids: freed for the links going down, taken for the ones coming up
+  std::vector<std::shared_ptr<Link>> links = eng.links;
+  std::vector<std::array<uint32_t, 2>> halves = eng.halves;
+  std::vector<uint32_t> freeIds = eng.freeIds;
+  std::vector<spf_edge_delta> dMetric, dHops;
+  for (const auto& l : down) {
+    const uint32_t lid = eng.linkIdOf(l.get());
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t e = eng.halves[lid][s];
+      if (e != ~0u) {
+        const uint32_t u = eng.col[eng.rev[e]], v = eng.col[e];
+        dMetric.push_back({u, v, eng.metric[e], SPF_DELTA_REMOVED, SPF_SCOPE_ALL});
+        dHops.push_back({u, v, 1, SPF_DELTA_REMOVED, SPF_SCOPE_ALL});
+      }
+    }
+    links[lid] = nullptr;
+    halves[lid] = {~0u, ~0u};
+    freeIds.push_back(lid);
+  }
+  std::sort(freeIds.begin(), freeIds.end(), std::greater<uint32_t>());
+  std::unordered_map<const Link*, uint32_t> upIds;
+  for (const auto& l : up) {
+    uint32_t lid;
+    if (!freeIds.empty()) {
+      lid = freeIds.back();
+      freeIds.pop_back();
+    } else {
+      lid = (uint32_t)links.size();
+      links.emplace_back();
+      halves.push_back({~0u, ~0u});
+    }
+    links[lid] = l;
+    upIds.emplace(l.get(), lid);
+  }
+  auto idOf = [&](const Link* l) {
+    auto it = upIds.find(l);
+    return it != upIds.end() ? it->second : eng.linkIdOf(l);
+  };
+  // kept halves shift with their row; halves in affected rows are re-set below
+  for (uint32_t lid = 0; lid < halves.size(); ++lid) {
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t e = halves[lid][s];
+      if (e == ~0u || lid >= eng.halves.size()) {
+        continue;
+      }
+      const uint32_t tail = eng.col[eng.rev[e]];
+      halves[lid][s] = aff[tail] ? ~0u : e - eng.row[tail] + newRow[tail];
+    }
+  }
+  std::vector<uint32_t> col(E), linkId(E);
+  std::vector<uint64_t> metric(E);
+  {
+    size_t k = 0;
+    for (uint32_t u = 0; u < V; ++u) {
+      if (!aff[u]) {
+        const uint32_t a = eng.row[u], b = eng.row[u + 1], o = newRow[u];
+        std::copy(eng.col.begin() + a, eng.col.begin() + b, col.begin() + o);
+        std::copy(eng.linkId.begin() + a, eng.linkId.begin() + b, linkId.begin() + o);
+        std::copy(eng.metric.begin() + a, eng.metric.begin() + b, metric.begin() + o);
+        continue;
+      }
+      const std::string& name = eng.names[u];
+      uint32_t e = newRow[u];
+      for (const auto* lp : affRows[k++]) {
+        const Link* link = lp->get();
+        const uint32_t lid = idOf(link);
+        const uint32_t v = nodeOf(link->getOtherNodeName(name));
+        if (lid == ~0u || v == ~0u) {
+          return false; // an up link the graph does not know: rebuild
+        }
+        col[e] = v;
+        linkId[e] = lid;
+        metric[e] = link->getMetricFromNode(name);
+        halves[lid][name == link->firstNodeName() ? 0 : 1] = e;
+        ++e;
+      }
+    }
+  }
+  std::vector<uint32_t> rev(E, ~0u);
+  for (uint32_t lid = 0; lid < halves.size(); ++lid) {
+    const auto& h = halves[lid];
+    if (!links[lid]) {
+      continue;
+    }
+    if (h[0] == ~0u || h[1] == ~0u) {
+      return false; // a link with one half: rebuild
+    }
+    rev[h[0]] = h[1];
+    rev[h[1]] = h[0];
+  }
+  for (const auto& l : up) {
+    const auto& h = halves[upIds.at(l.get())];
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t e = h[s];
+      dMetric.push_back({col[rev[e]], col[e], metric[e], SPF_DELTA_ADDED, SPF_SCOPE_ALL});
+      dHops.push_back({col[rev[e]], col[e], 1, SPF_DELTA_ADDED, SPF_SCOPE_ALL});
+    }
+  }
+  // metric patches of the same update (kept links)
+  for (const auto& [link, from] : metricPatches) {
+    const uint32_t lid = idOf(link.get());
+    if (lid == ~0u) {
+      return false;
+    }
+    const uint32_t e = halves[lid][from == link->firstNodeName() ? 0 : 1];
+    if (e == ~0u) {
+      return false;
+    }
+    const uint64_t w = link->getMetricFromNode(from);
+    dMetric.push_back({col[rev[e]], col[e], metric[e], SPF_DELTA_REMOVED, SPF_SCOPE_ALL});
+    dMetric.push_back({col[rev[e]], col[e], w, SPF_DELTA_ADDED, SPF_SCOPE_ALL});
+    metric[e] = w;
+  }
+  std::vector<uint8_t> overloaded = eng.overloaded;
+  for (const auto& n : transitNodes) {
+    const uint32_t x = nodeOf(n);
+    if (x == ~0u) {
+      continue;
+    }
+    const uint8_t ov = isNodeOverloaded(n) ? 1 : 0;
+    if (overloaded[x] != ov) {
+      const uint32_t kind = ov ? SPF_DELTA_REMOVED : SPF_DELTA_ADDED;
+      for (uint32_t e = newRow[x]; e < newRow[x + 1]; ++e) {
+        dMetric.push_back({x, col[e], metric[e], kind, SPF_SCOPE_NOT_TAIL});
+        dHops.push_back({x, col[e], 1, kind, SPF_SCOPE_NOT_TAIL});
+      }
+    }
+    overloaded[x] = ov;
+  }
+  // the new device graph first: on failure nothing of the engine changed
+  spf_graph_desc d{};
+  d.num_nodes = V;
+  d.num_edges = E;
+  d.row_ptr = newRow.data();
+  d.col = col.data();
+  d.metric = metric.data();
+  d.link_id = linkId.data();
+  d.rev = rev.data();
+  d.node_overloaded = overloaded.data();
+  d.num_links = (uint32_t)links.size();
+  d.device = getSpfDevice();
+  spf_graph* g = nullptr;
+  if (spf_graph_create(&d, &g) != SPF_OK) {
+    return false;
+  }
+  // commit
+  ++topoGen_;
+  spfResultsMetric_.clear();
+  spfResultsHops_.clear();
+  clearKthMemo();
+  for (const auto& l : down) {
+    l->engineEpoch = 0;
+  }
+  for (const auto& [l, lid] : upIds) {
+    l->engineEpoch = eng.epoch;
+    l->engineId = lid;
+  }
+  spf_graph_destroy(eng.graph);
+  eng.graph = g;
+  if (eng.cgraph) {
+    spf_cgraph_destroy(eng.cgraph);
+    eng.cgraph = nullptr;
+    eng.cgraphGen = 0;
+  }
+  eng.row = std::move(newRow);
+  eng.col = std::move(col);
+  eng.linkId = std::move(linkId);
+  eng.metric = std::move(metric);
+  eng.rev = std::move(rev);
+  eng.overloaded = std::move(overloaded);
+  eng.links = std::move(links);
+  eng.halves = std::move(halves);
+  eng.freeIds = std::move(freeIds);
+  eng.exact = spf_graph_needs_exact(eng.graph) != 0;
+  if (memoScreenEnabled() && !eng.exact) {
+    for (int k = 0; k < 2; ++k) {
+      std::remove_reference_t<decltype(eng.memo[0])> keep;
+      screenMemo(eng.memo[k], keep, k ? dMetric : dHops);
+      eng.memo[k] = std::move(keep);
+    }
+  } else {
+    eng.memo[0].clear();
+    eng.memo[1].clear();
+  }
+  for (auto& m : eng.prefetched) {
+    m.clear();
+  }
+  eng.kthPrefetch.clear();
+  eng.isolated.clear();
+  Counters::add("decision.graph_inplace_link_patches", 1);
+  Counters::add("decision.graph_patch_us",
+                std::chrono::duration_cast<std::chrono::microseconds>(
+                    std::chrono::steady_clock::now() - t0)
+                    .count());
+  return true;
+}
+
 void LinkState::addLink(std::shared_ptr<Link> link) {
   if (!linkMap_[link->firstNodeName()].insert(link).second ||
       !linkMap_[link->secondNodeName()].insert(link).second ||
@@ -1597,6 +1863,7 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
   // else in-place transit / metric patches
   bool structural = false;
   std::vector<std::pair<std::shared_ptr<Link>, std::string>> metricPatches;
+  std::vector<std::shared_ptr<Link>> downLinks, upLinks; // up-ness flips
 
   size_t ni = 0, oi = 0;
   while (ni < newLinks.size() || oi < oldLinks.size()) {
@@ -1606,6 +1873,9 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
       newLinks[ni]->setHoldUpTtl(holdUpTtl);
       change.topologyChanged |= newLinks[ni]->isUp();
       structural |= newLinks[ni]->isUp();
+      if (newLinks[ni]->isUp()) {
+        upLinks.push_back(newLinks[ni]);
+      }
       addLink(newLinks[ni]);
       ++ni;
       continue;
@@ -1614,6 +1884,9 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
       // link disappears (a held or overloaded link was not carrying traffic)
       change.topologyChanged |= oldLinks[oi]->isUp();
       structural |= oldLinks[oi]->isUp();
+      if (oldLinks[oi]->isUp()) {
+        downLinks.push_back(oldLinks[oi]);
+      }
       removeLink(oldLinks[oi]);
       ++oi;
       continue;
@@ -1633,6 +1906,7 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
     }
     if (cur.isUp() != wasUp) {
       structural = true;
+      (wasUp ? downLinks : upLinks).push_back(oldLinks[oi]);
     } else if (wasUp && cur.getMetricFromNode(nodeName) != oldMetric) {
       metricPatches.emplace_back(oldLinks[oi], nodeName);
     }
@@ -1653,7 +1927,12 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
   }
   if (change.topologyChanged) {
     if (structural) {
-      clearMemo();
+      if (!patchStructure(
+              downLinks, upLinks,
+              transitChanged ? std::vector<std::string>{nodeName} : std::vector<std::string>{},
+              metricPatches)) {
+        clearMemo();
+      }
     } else {
       patchMemo(
           transitChanged ? std::vector<std::string>{nodeName} : std::vector<std::string>{},

@@ -404,6 +404,14 @@ class LinkState {
   void patchMemo(
       const std::vector<std::string>& transitNodes,
       const std::vector<std::pair<std::shared_ptr<Link>, std::string>>& metricPatches) const;
+  // links going down / coming up with the node set unchanged (link flaps):
+  // the affected rows of the flat CSR are spliced in place and the memo is
+  // screened with the edge deltas; false = not applicable (full rebuild)
+  bool patchStructure(
+      const std::vector<std::shared_ptr<Link>>& down,
+      const std::vector<std::shared_ptr<Link>>& up,
+      const std::vector<std::string>& transitNodes,
+      const std::vector<std::pair<std::shared_ptr<Link>, std::string>>& metricPatches) const;
   Engine& engine() const;
   struct TraceMemo; // per getKthPaths call (LinkState.cpp)
   bool traceOnePath(

@@ -200,6 +200,56 @@ def test_incremental_updates(mods, seed):
 
 
 @pytest.mark.parametrize("seed", range(4))
+def test_link_flaps_in_place(mods, seed):
+    """Link flaps in the product LinkState (LinkState::patchStructure): an
+    adjacency withdrawn (the link goes down), restored, or a link overload
+    toggled splices the affected CSR rows in place (link ids of the other
+    links kept, freed ids reused) instead of flattening the LinkState again.
+    After every flap every node's metric and hop-count SpfResult (distances,
+    next hops, pathLinks order), k = 2 paths and a RouteDb equal the
+    oracle's; the in-place path ran and no full rebuild happened."""
+    import random
+
+    E, O = mods
+    names, adj_dbs, prefix_dbs = RZ.random_network(3100 + seed, n_nodes=32, n_links=90)
+    ea, ep = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    oa, op = RZ.load(O, adj_dbs, prefix_dbs, seed)
+    es = E.SpfSolver(names[0], True, False)
+    os_ = O.SpfSolver(names[0], True, False)
+    rng = random.Random(seed)
+    dbs = [copy.deepcopy(d) for d in adj_dbs["0"]]
+    withdrawn = {}  # node index -> withdrawn adjacencies
+    es.buildRouteDb(names[0], ea, ep)  # builds the engine
+    E.reset_counters()
+    for step in range(24):
+        i = rng.randrange(len(dbs))
+        db = dbs[i]
+        kind = rng.random()
+        if withdrawn.get(i) and kind < 0.4:
+            db.adjacencies = db.adjacencies + [withdrawn[i].pop()]
+        elif db.adjacencies and kind < 0.8:
+            k = rng.randrange(len(db.adjacencies))
+            withdrawn.setdefault(i, []).append(db.adjacencies[k])
+            db.adjacencies = db.adjacencies[:k] + db.adjacencies[k + 1:]
+        elif db.adjacencies:
+            adj = rng.choice(db.adjacencies)
+            adj.isOverloaded = not adj.isOverloaded
+        assert ea["0"].updateAdjacencyDatabase(db) == oa["0"].updateAdjacencyDatabase(db)
+        for node in names[step % 4::4]:
+            if ea["0"].hasNode(node):
+                _spf_equal(ea["0"], oa["0"], node, True)
+                _spf_equal(ea["0"], oa["0"], node, False)
+        a, b = names[step % len(names)], names[(7 * step + 3) % len(names)]
+        if a != b and ea["0"].hasNode(a) and ea["0"].hasNode(b):
+            assert _paths(ea["0"], a, b, 2) == _paths(oa["0"], a, b, 2), (step, a, b)
+        me = names[step % len(names)]
+        assert es.buildRouteDb(me, ea, ep) == os_.buildRouteDb(me, oa, op), (step, me)
+    c = E.get_counters()
+    assert c.get("decision.graph_inplace_link_patches", 0) > 0
+    assert c.get("decision.graph_build_us", 0) == 0  # never flattened again
+
+
+@pytest.mark.parametrize("seed", range(4))
 def test_selective_memo_invalidation(mods, seed):
     """SURVEY §8(f) row 2 in LinkState: a topology change keeps the memoized
     SPF views whose shortest-path DAG no edge delta touches (the table screen

@@ -14,7 +14,11 @@
 #pragma once
 
 #include <cstdint>
+#include <cstring>
 #include <functional>
+#include <new>
+#include <ostream>
+#include <string_view>
 #include <map>
 #include <optional>
 #include <set>
@@ -26,6 +30,150 @@
 #include <vector>
 
 namespace openr {
+
+// String value with the bytes inline up to 30 characters (heap beyond): the
+// IPv6 next-hop addresses (16 bytes) and interface names ("if_3-172-45_2-
+// 172-0", 19) of every NextHopThrift would each be one heap block in a
+// std::string (15-byte SSO), and a fabric RouteDb holds ~1.6M of them, built
+// per build and freed per release.  Same bytes, comparisons and std::hash
+// value as the std::string it replaces; converts to std::string implicitly.
+class SmallString {
+ public:
+  static constexpr size_t kInline = 30;
+  SmallString() noexcept { buf_[0] = 0; n_ = 0; }
+  SmallString(const char* p, size_t n) { init(p, n); }
+  SmallString(const char* p) : SmallString(p, std::strlen(p)) {} // NOLINT
+  SmallString(const std::string& s) : SmallString(s.data(), s.size()) {} // NOLINT
+  SmallString(std::string_view s) : SmallString(s.data(), s.size()) {} // NOLINT
+  SmallString(size_t n, char c) {
+    init(nullptr, n);
+    std::memset(mut(), c, n);
+  }
+  SmallString(const SmallString& o) {
+    if (o.n_ != kHeap) {
+      std::memcpy(this, &o, sizeof(SmallString));
+    } else {
+      init(o.data(), o.size());
+    }
+  }
+  SmallString(SmallString&& o) noexcept {
+    std::memcpy(this, &o, sizeof(SmallString));
+    o.buf_[0] = 0;
+    o.n_ = 0;
+  }
+  SmallString& operator=(const SmallString& o) {
+    if (this != &o) {
+      release();
+      new (this) SmallString(o);
+    }
+    return *this;
+  }
+  SmallString& operator=(SmallString&& o) noexcept {
+    if (this != &o) {
+      release();
+      new (this) SmallString(std::move(o));
+    }
+    return *this;
+  }
+  SmallString& operator=(const std::string& s) {
+    release();
+    init(s.data(), s.size());
+    return *this;
+  }
+  SmallString& operator=(const char* p) {
+    release();
+    init(p, std::strlen(p));
+    return *this;
+  }
+  ~SmallString() { release(); }
+
+  size_t size() const noexcept { return n_ == kHeap ? heapLen() : n_; }
+  size_t length() const noexcept { return size(); }
+  bool empty() const noexcept { return size() == 0; }
+  const char* data() const noexcept { return n_ == kHeap ? heapPtr() : buf_; }
+  const char* c_str() const noexcept { return data(); }
+  const char* begin() const noexcept { return data(); }
+  const char* end() const noexcept { return data() + size(); }
+  char operator[](size_t i) const { return data()[i]; }
+  char& operator[](size_t i) { return mut()[i]; }
+  std::string_view view() const noexcept { return {data(), size()}; }
+  std::string str() const { return std::string(data(), size()); }
+  operator std::string() const { return str(); } // NOLINT
+  int compare(const SmallString& o) const noexcept { return view().compare(o.view()); }
+  SmallString& assign(const char* p, size_t n) {
+    SmallString t(p, n);
+    return *this = std::move(t);
+  }
+
+  friend bool operator==(const SmallString& a, const SmallString& b) noexcept {
+    return a.view() == b.view();
+  }
+  friend bool operator!=(const SmallString& a, const SmallString& b) noexcept { return !(a == b); }
+  friend bool operator<(const SmallString& a, const SmallString& b) noexcept {
+    return a.view() < b.view();
+  }
+  friend bool operator==(const SmallString& a, const std::string& b) noexcept {
+    return a.view() == std::string_view(b);
+  }
+  friend bool operator==(const std::string& a, const SmallString& b) noexcept { return b == a; }
+  friend bool operator!=(const SmallString& a, const std::string& b) noexcept { return !(a == b); }
+  friend bool operator!=(const std::string& a, const SmallString& b) noexcept { return !(b == a); }
+  friend bool operator==(const SmallString& a, const char* b) noexcept {
+    return a.view() == std::string_view(b);
+  }
+  friend bool operator!=(const SmallString& a, const char* b) noexcept { return !(a == b); }
+  friend std::string operator+(const std::string& a, const SmallString& b) {
+    return a + b.str();
+  }
+  friend std::string operator+(const SmallString& a, const std::string& b) {
+    return a.str() + b;
+  }
+  friend std::string operator+(const char* a, const SmallString& b) { return a + b.str(); }
+  friend std::string operator+(const SmallString& a, const char* b) { return a.str() + b; }
+
+ private:
+  static constexpr uint8_t kHeap = 255;
+  char buf_[31]; // inline bytes + NUL, or {char* ptr; size_t len} when n_ == kHeap
+  uint8_t n_;
+  const char* heapPtr() const noexcept {
+    const char* p;
+    std::memcpy(&p, buf_, sizeof p);
+    return p;
+  }
+  size_t heapLen() const noexcept {
+    size_t n;
+    std::memcpy(&n, buf_ + sizeof(char*), sizeof n);
+    return n;
+  }
+  char* mut() noexcept { return n_ == kHeap ? const_cast<char*>(heapPtr()) : buf_; }
+  void init(const char* p, size_t n) {
+    if (n <= kInline) {
+      if (p) {
+        std::memcpy(buf_, p, n);
+      }
+      buf_[n] = 0;
+      n_ = (uint8_t)n;
+      return;
+    }
+    char* h = new char[n + 1];
+    if (p) {
+      std::memcpy(h, p, n);
+    }
+    h[n] = 0;
+    std::memcpy(buf_, &h, sizeof h);
+    std::memcpy(buf_ + sizeof(char*), &n, sizeof n);
+    n_ = kHeap;
+  }
+  void release() noexcept {
+    if (n_ == kHeap) {
+      delete[] heapPtr();
+      n_ = 0;
+      buf_[0] = 0;
+    }
+  }
+};
+
+inline std::ostream& operator<<(std::ostream& os, const SmallString& s) { return os << s.view(); }
 
 // A reference CHECK on the path failed (glog CHECK aborts the daemon there,
 // e.g. LinkState.cpp:423-433; thrown here and never swallowed as a
@@ -66,8 +214,8 @@ enum class CompareType : int32_t {
 };
 
 struct BinaryAddress {
-  std::string addr;
-  std::optional<std::string> ifName;
+  SmallString addr; // 4 / 16 raw bytes
+  std::optional<SmallString> ifName;
   auto tie() const { return std::tie(addr, ifName); }
   bool operator==(const BinaryAddress& o) const { return tie() == o.tie(); }
   bool operator!=(const BinaryAddress& o) const { return !(*this == o); }
@@ -241,11 +389,17 @@ mix(size_t seed, size_t v) {
 
 namespace std {
 template <>
+struct hash<openr::SmallString> {
+  size_t operator()(const openr::SmallString& s) const noexcept {
+    return std::hash<std::string_view>()(s.view()); // == std::hash<std::string>
+  }
+};
+template <>
 struct hash<openr::thrift::BinaryAddress> {
   size_t operator()(const openr::thrift::BinaryAddress& a) const {
-    size_t h = std::hash<std::string>()(a.addr);
+    size_t h = std::hash<openr::SmallString>()(a.addr);
     if (a.ifName) {
-      h = openr::detail::mix(h, std::hash<std::string>()(*a.ifName));
+      h = openr::detail::mix(h, std::hash<openr::SmallString>()(*a.ifName));
     }
     return h;
   }

@@ -6978,6 +6978,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
   const bool exact = ((g->exact && !unit) || want_order) && !zcand;
   const bool uniform = unit || g->uniform != 0 || zcand;
   bool rows_ok = false;
+  bool few_rows = false; // weighted few-source batch with helper rows (below)
   if (want_nh && !exact && !has_ign) {
     // next hops from distance rows need every neighbour's row in the batch
     row_of.assign(V, -1);
@@ -7000,7 +7001,10 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     // batch's own rows and serve only the next-hop pass — instead of the
     // batch dropping to per-source SSSP (fabric block of 1,247 sources:
     // 1.93 ms on the lds plan, profiles/r03j)
-    const bool msbfs_candidate = !rows_ok && uniform && !literal && nq >= 32 &&
+    // (a batch below 32 sources qualifies when its helpers bring it there:
+    // one source and its neighbours' rows in one MS-BFS pass beat the
+    // single-workgroup SSSP of that source, e.g. a what-if baseline)
+    const bool msbfs_candidate = !rows_ok && uniform && !literal &&
                                  V <= kMsThreads * kMsMaxK &&
                                  2 * (size_t)V * 4 <= kLdsLimit &&
                                  !(getenv("OPENR_SPF_MSBFS") && atoi(getenv("OPENR_SPF_MSBFS")) == 0) &&
@@ -7020,8 +7024,42 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
           }
         }
       }
-      rows_ok = true;
-      helpers = std::move(extra);
+      if (nq >= 32 || (nq + extra.size() >= 32 && env_flag("OPENR_SPF_MSBFS_FEW", 1))) {
+        rows_ok = true;
+        helpers = std::move(extra);
+      }
+    }
+    // a few sources of a weighted graph (a what-if baseline, a RouteDb
+    // build's prefetch): their neighbours ride along as helper sources of a
+    // distances-only delta-stepping pass (one workgroup per row, all in
+    // parallel), and the next hops come from the rows (spf_nh_rows_kernel)
+    // instead of the PULL rounds of one workgroup per source
+    // (OPENR_SPF_FEW_ROWS=0 disables)
+    // (exactly the batches the planner below sends to the few-source
+    // delta-stepping plan: weighted, V in [4096, 65535], the LDS-plan image
+    // fits, at most one source per 16 CUs, <= 16 mask words; and LDS-row
+    // eligible: 12-bit metrics, packed edges)
+    if (!rows_ok && !uniform && !literal && V >= 4096 && V <= 65535 &&
+        lds_ctl_bytes(g, 0) + lds_state_bytes(V) <= kLdsLimit && maxw <= 16 &&
+        (size_t)nq * 16 <= (size_t)g->num_cus && g->cw_bits && g->maxw <= kDlMaxDist &&
+        env_flag("OPENR_SPF_FEW_DSTEP", 1) && getenv("OPENR_SPF_DSTEP") == nullptr &&
+        env_flag("OPENR_SPF_DSTEP_LDSROW", 1) && env_flag("OPENR_SPF_FEW_ROWS", 1)) {
+      std::vector<uint32_t> extra;
+      for (uint32_t i = 0; i < nq; ++i) {
+        const uint32_t s = desc->sources[i];
+        for (uint32_t k = g->nbr_off[s]; k < g->nbr_off[s + 1]; ++k) {
+          const uint32_t f = g->nbrs[k];
+          if (row_of[f] < 0) {
+            row_of[f] = (int32_t)(nq + extra.size());
+            extra.push_back(f);
+          }
+        }
+      }
+      if (nq + extra.size() <= (size_t)g->num_cus) {
+        rows_ok = true;
+        helpers = std::move(extra);
+        few_rows = true;
+      }
     }
     if (!rows_ok) {
       row_of.clear();
@@ -7069,7 +7107,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     const char* msd_env = getenv("OPENR_SPF_MSD");
     const bool msd = big && !uniform && !want_nh && !has_ign && nq >= 2 * kMsdK &&
                      msd_lds_bytes(g) <= kLdsLimit && msd_env && atoi(msd_env) == 1;
-    if (dstep && q->nh == NhPlan::Rows) {
+    if (dstep && q->nh == NhPlan::Rows && !few_rows) {
       q->nh = NhPlan::Inline;
     }
     const bool bfs = uniform && !has_ign && q->nh != NhPlan::Inline;
@@ -7087,7 +7125,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       msd_perm = msd_batches(g, desc->sources, nq, !(cl && atoi(cl) == 0));
       q->msd_nbatch = (uint32_t)(msd_perm.size() / kMsdK);
       q->grid = std::min<uint32_t>(q->msd_nbatch, (uint32_t)g->num_cus);
-    } else if (V <= 65535 && lds <= kLdsLimit && !(few && dstep)) {
+    } else if (V <= 65535 && lds <= kLdsLimit && !(few && dstep) && !few_rows) {
       q->dist = bfs ? DistPlan::BfsLds : DistPlan::SsspLds;
       q->lds_bytes = lds;
       const uint32_t per_cu =
@@ -7109,16 +7147,17 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       if (const char* pc = getenv("OPENR_SPF_DSTEP_PERCU")) {
         per_cu = std::max<uint32_t>(1, std::min<uint32_t>(per_cu, (uint32_t)atoi(pc)));
       }
-      q->grid = std::min<uint32_t>(std::max<uint32_t>(nq, 1), (uint32_t)g->num_cus * per_cu);
+      const uint32_t nr = nq + (uint32_t)helpers.size();
+      q->grid = std::min<uint32_t>(std::max<uint32_t>(nr, 1), (uint32_t)g->num_cus * per_cu);
       // distance rows whose every value fits 12 bits (metrics <= 4,094; the
       // kernel flags a source whose values do not, and the pass above redoes
       // only those): the row lives in LDS (OPENR_SPF_DSTEP_LDSROW=0 disables)
       const size_t dl_lds = (size_t)((V + 4) / 5) * 8 + kDlCtl * 4;
-      q->dlds = !want_nh && !has_ign && g->cw_bits && g->maxw <= kDlMaxDist &&
+      q->dlds = q->nh != NhPlan::Inline && !has_ign && g->cw_bits && g->maxw <= kDlMaxDist &&
                 dl_lds <= kLdsLimit && env_flag("OPENR_SPF_DSTEP_LDSROW", 1);
       if (q->dlds) {
         q->dlds_lds = dl_lds;
-        q->dlds_grid = std::min<uint32_t>(std::max<uint32_t>(nq, 1), (uint32_t)g->num_cus);
+        q->dlds_grid = std::min<uint32_t>(std::max<uint32_t>(nr, 1), (uint32_t)g->num_cus);
         // bucket width: 8x the delta-stepping Delta (mean metric / mean
         // degree): with the row in LDS a bucket scan is cheap, and wider
         // buckets mean fewer phases (100k WAN, profiles/r04c: 2^4 9.5,
@@ -7141,7 +7180,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
   // many sources on a uniform metric: bit-parallel multi-source BFS
   // (OPENR_SPF_MSBFS=0 disables, =32 / =64 picks the batch width)
   if ((q->dist == DistPlan::BfsLds || q->dist == DistPlan::BfsGmem) &&
-      V <= kMsThreads * kMsMaxK && nq >= 32) {
+      V <= kMsThreads * kMsMaxK && nq + helpers.size() >= 32) {
     const char* env = getenv("OPENR_SPF_MSBFS");
     int width = env ? atoi(env) : 64;
     if (width == 64 && 2 * (size_t)V * 8 > kLdsLimit) {
@@ -7161,7 +7200,8 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
       }
     }
   }
-  if (!helpers.empty() && !(q->dist == DistPlan::MsBfs && q->nh == NhPlan::Levels)) {
+  if (!helpers.empty() && !(q->dist == DistPlan::MsBfs && q->nh == NhPlan::Levels) &&
+      !(few_rows && q->dist == DistPlan::Dstep && q->nh == NhPlan::Rows && q->dlds)) {
     return bail(fail(SPF_E_INVALID, "internal: helper sources outside the MS-BFS plan"));
   }
   if (zcand && !(q->dist == DistPlan::MsBfs && (!want_nh || q->nh == NhPlan::Levels))) {
@@ -7350,7 +7390,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
                       4) != hipSuccess) {
     return bail(fail(SPF_E_NOMEM, "queue scratch"));
   }
-  if (q->dlds && pool_malloc((void**)&q->d_ovf, ((size_t)nq + 2) * 4) != hipSuccess) {
+  if (q->dlds && pool_malloc((void**)&q->d_ovf, ((size_t)q->nrows + 2) * 4) != hipSuccess) {
     return bail(fail(SPF_E_NOMEM, "overflow list"));
   }
   if (q->dist == DistPlan::MsDstep) {
@@ -7548,7 +7588,7 @@ int launch_dstep_t(spf_query* q) {
   a.V = g->V;
   a.Vp = q->Vp;
   a.nbw = g->nbw;
-  a.nq = q->nq;
+  a.nq = q->nrows; // the batch + its helper sources (few-source rows plan)
   a.G = g->G;
   a.ign_cap = q->ign_cap;
   a.skip = q->d_skip;
@@ -7577,7 +7617,7 @@ int launch_dstep_t(spf_query* q) {
   if constexpr (WMAX == 0) {
     if (q->dstep_lbk && d.cwvec && (d.noret & 3u) == 3u) {
       kern = spf_dstep_kernel<WMAX, IGN, BS, true, false, true>;
-      if (q->nq > q->grid) {
+      if (q->nrows > q->grid) {
         if (!q->d_qctr) {
           HIP_TRY(pool_malloc((void**)&q->d_qctr, 4));
         }
@@ -7644,7 +7684,7 @@ int launch_dlds(spf_query* q) {
   a.ovf_list = q->d_ovf + 2;
   a.V = g->V;
   a.Vp = q->Vp;
-  a.nq = q->nq;
+  a.nq = q->nrows; // the batch + its helper sources (few-source rows plan)
   a.cwbits = g->cw_bits;
   a.wshift = q->dlds_shift;
   if (!g->d_cw || !g->cw_bits) {
@@ -8191,7 +8231,15 @@ int run_plan_kernels(spf_query* q) {
     return launch_wide(q);
   case DistPlan::Dstep: {
     int s = q->dlds ? launch_dlds(q) : SPF_OK;
-    return s == SPF_OK ? launch_dstep(q) : s;
+    s = s == SPF_OK ? launch_dstep(q) : s;
+    if (s == SPF_OK && q->nh == NhPlan::Rows) {
+      // few-source rows plan: next hops from the batch's + helpers' rows
+      s = mark_stage(q);
+      if (s == SPF_OK) {
+        s = launch_nh_rows(q, unit);
+      }
+    }
+    return s;
   }
   case DistPlan::MsDstep:
     return launch_msdstep(q);

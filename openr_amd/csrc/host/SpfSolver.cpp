@@ -17,6 +17,7 @@
 #include <chrono>
 #include <memory>
 #include <string_view>
+#include <thread>
 #include <list>
 
 #include "Parallel.h"
@@ -640,23 +641,40 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
     tEcmpClock.flush();
   });
   const auto tmerge = std::chrono::steady_clock::now();
-  // move the workers' map nodes themselves (no re-allocation on this thread)
+  Counters::add("decision.route_prefix_pool_us",
+                std::chrono::duration_cast<std::chrono::microseconds>(tmerge - tpar).count());
+  // move the workers' map nodes themselves (no re-allocation): one thread
+  // merges them into the RouteDb's map while the label phase below runs on
+  // the pool (the two touch disjoint maps and only read the SPF views)
   size_t built = routeDb.unicastEntries.size();
   for (const auto& part : parts) {
     built += part.size();
   }
   routeDb.unicastEntries.reserve(built);
-  for (auto& part : parts) {
-    while (!part.empty()) {
-      routeDb.unicastEntries.insert(part.extract(part.begin()));
+  auto mergeUnicast = [&routeDb, &parts, tmerge] {
+    for (auto& part : parts) {
+      while (!part.empty()) {
+        routeDb.unicastEntries.insert(part.extract(part.begin()));
+      }
     }
+    Counters::add("decision.route_merge_us",
+                  std::chrono::duration_cast<std::chrono::microseconds>(
+                      std::chrono::steady_clock::now() - tmerge)
+                      .count());
+  };
+  struct Merger {
+    std::thread t;
+    ~Merger() {
+      if (t.joinable()) {
+        t.join(); // every exit path (a throwing label route included)
+      }
+    }
+  } merger;
+  if (skipMpls_ || std::getenv("OPENR_ROUTE_MERGE_INLINE")) {
+    mergeUnicast();
+  } else {
+    merger.t = std::thread(mergeUnicast);
   }
-  Counters::add("decision.route_prefix_pool_us",
-                std::chrono::duration_cast<std::chrono::microseconds>(tmerge - tpar).count());
-  Counters::add("decision.route_merge_us",
-                std::chrono::duration_cast<std::chrono::microseconds>(
-                    std::chrono::steady_clock::now() - tmerge)
-                    .count());
 
   // node-label MPLS routes: on a label collision the smaller node name wins.
   // Labels held by a single (other) node cannot collide: they are expanded
@@ -807,6 +825,9 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
                 std::chrono::duration_cast<std::chrono::microseconds>(
                     std::chrono::steady_clock::now() - tlabel)
                     .count());
+  if (merger.t.joinable()) {
+    merger.t.join();
+  }
   const auto elapsed = std::chrono::steady_clock::now() - t0;
   Counters::add(
       "decision.route_build_us",

@@ -144,6 +144,49 @@ __device__ __forceinline__ bool in_sorted(
   return false;
 }
 
+// A query's ignored links: the sorted list (in_sorted), or, for lists of 8+
+// links, an open-addressing hash set in the same LDS words (2^hbits slots,
+// load factor <= 1/2, kInf32 = empty): one or two probes per edge instead of
+// a binary search (KSP2 second passes ignore every link of the k = 1 paths,
+// hundreds per query, and test every relaxed edge)
+struct IgnSet {
+  const uint32_t* p = nullptr;
+  uint32_t n = 0;
+  uint32_t hbits = 0;
+  __device__ __forceinline__ bool has(uint32_t l) const {
+    if (!n) {
+      return false;
+    }
+    if (hbits) {
+      const uint32_t mask = (1u << hbits) - 1;
+      uint32_t h = (l * 0x9E3779B1u) >> (32 - hbits);
+      for (;;) {
+        const uint32_t x = p[h];
+        if (x == l) {
+          return true;
+        }
+        if (x == kInf32) {
+          return false;
+        }
+        h = (h + 1) & mask;
+      }
+    }
+    return in_sorted(p, n, l);
+  }
+};
+
+// slots of the hash form for n links (0: keep the sorted list)
+__host__ __device__ inline uint32_t ign_hash_slots(uint32_t n) {
+  if (n < 8) {
+    return 0;
+  }
+  uint32_t t = 16;
+  while (t < 2 * n) {
+    t <<= 1;
+  }
+  return t;
+}
+
 // ---- next-hop mask rows (byte-strided layout of spf_query results)
 // A query's row holds B bytes per node: B = 1, 2, 4 for sources with at most
 // 8, 16, 32 distinct neighbours (bit j of the byte / short / word = the j-th
@@ -371,12 +414,12 @@ __device__ __forceinline__ void block_copy(T* __restrict__ dst, const T* __restr
 template <typename QT, bool UNIT>
 __device__ uint32_t whatif_repair_init(
     const SsspArgs& a, uint32_t src, uint32_t* dist, uint32_t* kb, uint32_t* okb,
-    uint32_t* act, const uint32_t* tr, QT* queue, uint32_t* ctl, const uint32_t* ignp,
-    uint32_t nign) {
+    uint32_t* act, const uint32_t* tr, QT* queue, uint32_t* ctl, const uint32_t* ilist,
+    uint32_t nign, const IgnSet& ig) {
   const uint32_t tid = threadIdx.x, G = a.G, V = a.V, nbw = a.nbw;
   const uint32_t lg = tid & (G - 1), grp = tid / G, ngrp = kBlock / G;
   auto usable = [&](uint32_t u) { return u == src || ((tr[u >> 5] >> (u & 31)) & 1u); };
-  auto ignored = [&](uint32_t e) { return nign && in_sorted(ignp, nign, a.link[e]); };
+  auto ignored = [&](uint32_t e) { return ig.has(a.link[e]); };
   auto mark = [&](uint32_t* bm, uint32_t v) {
     const uint32_t m = 1u << (v & 31);
     if (!(atomicOr(&bm[v >> 5], m) & m)) {
@@ -385,7 +428,7 @@ __device__ uint32_t whatif_repair_init(
   };
   // seeds: heads of tight ignored halves
   for (uint32_t i = tid; i < 2 * nign; i += kBlock) {
-    const uint32_t l = ignp[i >> 1];
+    const uint32_t l = ilist[i >> 1]; // the query's list (the LDS copy may be a hash set)
     const uint32_t e = l < a.L ? a.link_half[2 * (size_t)l + (i & 1)] : kInf32;
     if (e == kInf32) {
       continue;
@@ -567,16 +610,38 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
     }
     uint32_t nign = 0;
     const uint32_t* ignp = ignl;
+    IgnSet ig;
     if constexpr (IGN) {
       const uint32_t lo = a.ign_off[q];
       nign = a.ign_off[q + 1] - lo;
-      if (nign <= a.ign_cap) {
+      const uint32_t slots = ign_hash_slots(nign);
+      if (slots && slots <= a.ign_cap) {
+        for (uint32_t i = tid; i < slots; i += kBlock) {
+          ignl[i] = kInf32;
+        }
+        __syncthreads();
+        const uint32_t hb = __builtin_ctz(slots);
+        for (uint32_t i = tid; i < nign; i += kBlock) {
+          const uint32_t l = a.ign[lo + i];
+          uint32_t h = (l * 0x9E3779B1u) >> (32 - hb);
+          for (;;) {
+            const uint32_t prev = atomicCAS(&ignl[h], kInf32, l);
+            if (prev == kInf32 || prev == l) {
+              break;
+            }
+            h = (h + 1) & (slots - 1);
+          }
+        }
+        ig.hbits = hb;
+      } else if (nign <= a.ign_cap) {
         for (uint32_t i = tid; i < nign; i += kBlock) {
           ignl[i] = a.ign[lo + i];
         }
       } else {
         ignp = a.ign + lo;
       }
+      ig.p = ignp;
+      ig.n = nign;
     }
     uint32_t Wm = 0;
     uint64_t* nhrow = nullptr;
@@ -602,7 +667,8 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
       if (a.stats && tid == 0) {
         tk1 = wall_clock64();
       }
-      qlen = whatif_repair_init<QT, UNIT>(a, src, dist, kb, okb, act, tr, queue, ctl, ignp, nign);
+      qlen = whatif_repair_init<QT, UNIT>(a, src, dist, kb, okb, act, tr, queue, ctl,
+                                          a.ign + a.ign_off[q], nign, ig);
       pull_first = qlen != kInf32;
       if (a.stats && tid == 0) {
         atomicAdd(&a.stats[pull_first ? 0 : 1], 1ull);
@@ -649,7 +715,7 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
         const uint32_t beg = a.row[u], end = a.row[u + 1];
         for (uint32_t e = beg + lg; e < end; e += G) {
           if constexpr (IGN) {
-            if (nign && in_sorted(ignp, nign, a.link[e])) {
+            if (ig.has(a.link[e])) {
               continue;
             }
           }
@@ -680,7 +746,7 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
         }
         for (uint32_t e = beg + lg; e < end; e += G) {
           if constexpr (IGN) {
-            if (nign && in_sorted(ignp, nign, a.link[e])) {
+            if (ig.has(a.link[e])) {
               continue;
             }
           }
@@ -2835,6 +2901,11 @@ struct NhLevelsArgs {
   // level 255 (lvl * scale) into dist_w and reads neighbour distances from
   // the level byte when it is below 255
   uint32_t* dist_w;
+  // held kernel work order (OPENR_NL_ORDER=1): hardware block b runs item
+  // held_order[b] = q * held_nch + chunk (kInf32: none); nullptr = the
+  // chunk-major default
+  const uint32_t* held_order = nullptr;
+  uint32_t held_nch = 0;
 };
 
 constexpr uint32_t kNlThreads = 256;
@@ -3632,8 +3703,16 @@ __global__ __launch_bounds__(T) void spf_nh_levels_held_kernel(
   // OPENR_NL_XCD=1 consecutive logical blocks also share an XCD
   const uint32_t bid = a.xcd_swizzle ? xcd_logical_block(blockIdx.x, gridDim.x) : blockIdx.x;
   const uint32_t nsrc = H <= 3 ? a.nq : nmid;
-  const uint32_t c = bid / nsrc;
-  const uint32_t q = H <= 3 ? bid - c * nsrc : big[bid - c * nsrc];
+  uint32_t c = bid / nsrc;
+  uint32_t q = H <= 3 ? bid - c * nsrc : big[bid - c * nsrc];
+  if (H <= 3 && a.held_order) {
+    const uint32_t it = a.held_order[blockIdx.x];
+    if (it == kInf32) {
+      return;
+    }
+    q = it / a.held_nch;
+    c = it - q * a.held_nch;
+  }
   const uint32_t Wm = a.nh_w[q];
   if (a.flags[0] != 0 || Wm > H || (H > 3 && Wm <= 3)) {
     return;
@@ -5463,6 +5542,7 @@ struct spf_query {
   size_t dlds_lds = 0;
   uint32_t* d_ovf = nullptr; // [0] overflow count, [1] claim counter, [2..] list
   uint32_t ign_cap = 0, grid = 0, Vp = 0, Vp8 = 0;
+  uint32_t dstep_ign_cap = 0; // the delta-stepping kernels' ignore-list words
   uint8_t* d_lvl = nullptr;
   uint32_t* d_flags = nullptr;
   size_t lds_bytes = 0;
@@ -5505,6 +5585,8 @@ struct spf_query {
   uint64_t* d_key = nullptr; // wide plan settle keys (SPF_F_ORDER)
   uint32_t* d_qctr = nullptr; // dstep source-claim counter
   uint32_t* d_big = nullptr;  // nh_levels: queries with more than kNsHeldMax mask words
+  uint32_t* d_held_order = nullptr; // OPENR_NL_ORDER=1: XCD-contiguous held-kernel work order
+  uint32_t held_blocks = 0, held_nch = 0, held_t = 0;
   uint32_t nbig = 0;
   uint32_t nmid = 0;          // the first nmid of them have at most kNsHeldWide words
   // zero-metric plan (spf_zvar_kernel): variant tables, their closure pairs
@@ -5717,7 +5799,8 @@ void free_query(spf_query* q) {
         (void*)q->d_lvl, (void*)q->d_flags, (void*)q->d_perm,
         (void*)q->d_slab, (void*)q->d_msd, (void*)q->d_base_of,
         (void*)q->d_skip, (void*)q->d_key, (void*)q->d_qctr, (void*)q->d_scatter,
-        (void*)q->d_trace, (void*)q->d_big, (void*)q->d_zl, (void*)q->d_zvar,
+        (void*)q->d_trace, (void*)q->d_big, (void*)q->d_held_order, (void*)q->d_zl,
+        (void*)q->d_zvar,
         (void*)q->d_ovf, q->narrow ? (void*)q->d_nhb : nullptr, (void*)q->d_tcs}) {
     pool_free(p);
   }
@@ -7089,8 +7172,9 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     // nodes cost more than the extra waves hide)
     const char* lbk_env = getenv("OPENR_SPF_DSTEP_LDSBKT");
     q->dstep_lbk = !(lbk_env && atoi(lbk_env) == 0);
+    q->dstep_ign_cap = has_ign ? std::min(max_ign, kIgnLdsMax) : 0; // sorted list only
     const size_t dstep_lds =
-        (2 * (size_t)g->nbw + kCtlWords + (has_ign ? std::min(max_ign, kIgnLdsMax) : 0)) * 4 +
+        (2 * (size_t)g->nbw + kCtlWords + q->dstep_ign_cap) * 4 +
         (q->dstep_lbk ? (((size_t)V + 15) & ~(size_t)15) : 0);
     // a few sources of a weighted graph that fits LDS (a what-if baseline, a
     // RouteDb build's SPFs): one workgroup per source either way, and bucket
@@ -7112,7 +7196,9 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     }
     const bool bfs = uniform && !has_ign && q->nh != NhPlan::Inline;
     q->wmax = q->nh != NhPlan::Inline ? 0 : (maxw <= 1 ? 1 : (maxw <= 4 ? 4 : 16));
-    q->ign_cap = has_ign ? std::min(max_ign, kIgnLdsMax) : 0;
+    // LDS words for a query's ignore list: the sorted list, or its hash form
+    // (ign_hash_slots) when that fits
+    q->ign_cap = has_ign ? std::min(std::max(max_ign, ign_hash_slots(max_ign)), kIgnLdsMax) : 0;
     const size_t ctl = lds_ctl_bytes(g, q->ign_cap);
     const size_t lds = ctl + lds_state_bytes(V);
     if (msd) {
@@ -7353,6 +7439,55 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     if (!big.empty() && dev_upload_q(&q->d_big, big.data(), big.size()) != SPF_OK) {
       return bail(fail(SPF_E_NOMEM, "next-hop source list"));
     }
+    // OPENR_NL_ORDER=1: the held kernel's (source, chunk) items cut into 8
+    // contiguous source ranges of equal cost (8 + neighbours per item), one
+    // per XCD (hardware block b runs on XCD b % 8), source-major inside a
+    // range: the rows an XCD's resident blocks read (a pod's RSW / FSW rows)
+    // stay in its L2 instead of every XCD fetching nearly every row
+    if (env_u32("OPENR_NL_ORDER", 0) == 1) {
+      const uint32_t ht = env_u32("OPENR_NL_HT", 256);
+      const uint32_t T = ht == 1024 ? 1024u : (ht == 512 ? 512u : 256u);
+      const uint32_t nch = (V + 4 * T - 1) / (4 * T);
+      double total = 0;
+      for (uint32_t i = 0; i < nq; ++i) {
+        if (q->nh_w[i] <= kNsHeldMax) {
+          const uint32_t s = desc->sources[i];
+          total += (double)nch * (8.0 + (g->nbr_off[s + 1] - g->nbr_off[s]));
+        }
+      }
+      std::vector<std::vector<uint32_t>> lists(8);
+      double acc = 0;
+      for (uint32_t i = 0; i < nq; ++i) {
+        if (q->nh_w[i] > kNsHeldMax) {
+          continue;
+        }
+        const uint32_t s = desc->sources[i];
+        const double cst = (double)nch * (8.0 + (g->nbr_off[s + 1] - g->nbr_off[s]));
+        const uint32_t x = std::min<uint32_t>(7, (uint32_t)(8.0 * (acc + 0.5 * cst) / total));
+        acc += cst;
+        for (uint32_t c = 0; c < nch; ++c) {
+          lists[x].push_back(i * nch + c);
+        }
+      }
+      size_t maxlen = 0;
+      for (const auto& l : lists) {
+        maxlen = std::max(maxlen, l.size());
+      }
+      std::vector<uint32_t> order(8 * maxlen, kInf32);
+      for (uint32_t x = 0; x < 8; ++x) {
+        for (size_t i = 0; i < lists[x].size(); ++i) {
+          order[i * 8 + x] = lists[x][i];
+        }
+      }
+      if (!order.empty() && nq * (uint64_t)nch < 0xFFFFFFFFull) {
+        if (dev_upload_q(&q->d_held_order, order.data(), order.size()) != SPF_OK) {
+          return bail(fail(SPF_E_NOMEM, "next-hop work order"));
+        }
+        q->held_blocks = (uint32_t)order.size();
+        q->held_nch = nch;
+        q->held_t = T;
+      }
+    }
   }
   const size_t ntab = std::max<uint32_t>(1, q->zvars); // MS-BFS tables (zero-metric variants)
   if (q->dist == DistPlan::MsBfs) {
@@ -7590,7 +7725,7 @@ int launch_dstep_t(spf_query* q) {
   a.nbw = g->nbw;
   a.nq = q->nrows; // the batch + its helper sources (few-source rows plan)
   a.G = g->G;
-  a.ign_cap = q->ign_cap;
+  a.ign_cap = q->dstep_ign_cap;
   a.skip = q->d_skip;
   // lanes per node: fewer than the median degree, so more nodes (and more
   // independent HBM gathers) are in flight per CU (4: measured on the 100k
@@ -7968,7 +8103,12 @@ int launch_nh_levels(spf_query* q, bool unit) {
     // threads per block (OPENR_NL_HT = 256 / 512 / 1024; chunk = 4 nodes per thread)
     const uint32_t ht = env_u32("OPENR_NL_HT", 256);
     const uint32_t T = ht == 1024 ? 1024u : (ht == 512 ? 512u : 256u);
-    const uint64_t hblocks = (uint64_t)q->nq * ((g->V + 4 * T - 1) / (4 * T));
+    uint64_t hblocks = (uint64_t)q->nq * ((g->V + 4 * T - 1) / (4 * T));
+    if (q->d_held_order && q->held_t == T) {
+      a.held_order = q->d_held_order;
+      a.held_nch = q->held_nch;
+      hblocks = q->held_blocks;
+    }
     if (hblocks > 0x7FFFFFFFull) {
       return fail(SPF_E_UNSUPPORTED, "batch too large for the next-hop pass");
     }

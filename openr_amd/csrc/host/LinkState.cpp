@@ -20,6 +20,7 @@
 #include <mutex>
 #include <shared_mutex>
 #include <stdexcept>
+#include <thread>
 
 #include "Parallel.h"
 
@@ -1245,7 +1246,11 @@ LinkState::Engine& LinkState::engine() const {
 // ---------------------------------------------------------------- LinkState
 
 LinkState::LinkState(const std::string& area) : area_(area) {}
-LinkState::~LinkState() = default;
+LinkState::~LinkState() {
+  if (kthReaper_.joinable()) {
+    kthReaper_.join();
+  }
+}
 LinkState::LinkState(LinkState&& o) noexcept
     : area_(o.area_),
       linkMap_(std::move(o.linkMap_)),
@@ -1255,6 +1260,7 @@ LinkState::LinkState(LinkState&& o) noexcept
       spfResultsMetric_(std::move(o.spfResultsMetric_)),
       spfResultsHops_(std::move(o.spfResultsHops_)),
       kth_(std::move(o.kth_)),
+      kthReaper_(std::move(o.kthReaper_)),
       kthFill_(std::move(o.kthFill_)),
       engine_(std::move(o.engine_)),
       retired_(std::move(o.retired_)),
@@ -1274,15 +1280,30 @@ bool LinkState::LinkPtrEqual::operator()(
 
 void LinkState::clearKthMemo() const {
   // the stripes hold one entry per (src, dst, k) a KSP2 build filled (20k on
-  // the fabric): freed on the worker pool, one stripe per task
+  // the fabric, two vectors each, allocated by the build's worker threads):
+  // the filled memo is swapped for an empty one at once and freed by a
+  // reaper thread, off the update path (freeing it here took 24 ms of every
+  // KSP2 topology update, most of it in malloc arena locks).  Nothing reads
+  // the old memo any more (updates and builds do not overlap); the next
+  // clear and the destructor join the reaper first.
   size_t n = 0;
   for (auto& stripe : *kth_) {
     n += stripe.ids.size() + stripe.paths.size();
   }
-  openr::parallelFor(kKthStripes, openr::hostThreads(n, 2048), [&](size_t i, unsigned) {
-    (*kth_)[i].ids.clear();
-    (*kth_)[i].paths.clear();
-  }, 1);
+  if (n == 0) {
+    return;
+  }
+  auto old = std::move(kth_);
+  kth_ = std::make_unique<std::array<KthStripe, kKthStripes>>();
+  if (kthReaper_.joinable()) {
+    kthReaper_.join();
+  }
+  static const bool inlineFree = std::getenv("OPENR_KTH_FREE_INLINE") != nullptr;
+  if (inlineFree) {
+    old.reset();
+    return;
+  }
+  kthReaper_ = std::thread([o = std::move(old)]() mutable { o.reset(); });
 }
 
 void LinkState::clearMemo() const {
@@ -1971,6 +1992,30 @@ bool LinkState::pathAInPathB(Path const& a, Path const& b) {
 }
 
 // ---------------------------------------------------------- SPF accessors
+
+bool LinkState::linkHop(
+    uint32_t linkId, uint32_t from, uint32_t& to, LinkStateMetric& metric) const {
+  const auto& eng = engine();
+  if (linkId >= eng.halves.size()) {
+    return false;
+  }
+  const auto& h = eng.halves[linkId];
+  if (h[0] == ~0u || h[1] == ~0u) {
+    return false;
+  }
+  const uint32_t first = eng.col[h[1]], second = eng.col[h[0]];
+  if (from == first) {
+    to = second;
+    metric = eng.metric[h[0]];
+    return true;
+  }
+  if (from == second) {
+    to = first;
+    metric = eng.metric[h[1]];
+    return true;
+  }
+  return false;
+}
 
 std::optional<uint32_t> LinkState::nodeId(const std::string& name) const {
   auto& eng = engine();

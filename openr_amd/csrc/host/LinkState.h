@@ -26,6 +26,7 @@
 #include <mutex>
 #include <shared_mutex>
 #include <string>
+#include <thread>
 #include <array>
 #include <atomic>
 #include <unordered_map>
@@ -358,6 +359,11 @@ class LinkState {
   // id -> name of the device graph (valid until the next topology change)
   const std::vector<std::string>& nodeNames() const;
   uint32_t numGraphNodes() const;
+  // one hop of a path of device link ids (kthPathIds): from node id `from`
+  // over link `linkId` to `to`, at the link's metric from `from`'s side;
+  // false when the link is not an up link of the graph or `from` is not one
+  // of its ends (the engine must be built: a RouteDb build's prefetch did)
+  bool linkHop(uint32_t linkId, uint32_t from, uint32_t& to, LinkStateMetric& metric) const;
   // What-if link-failure SPFs (BASELINE config 5, LFA / failure
   // precomputation): runSpf(src, useLinkMetric, linksToIgnore[i])
   // (LinkState.cpp:806-880 -- the reference's own ignore-set semantics, which
@@ -467,6 +473,8 @@ class LinkState {
     return (*kth_)[KthKeyHash{}(key) % kKthStripes];
   }
   void clearKthMemo() const;
+  // frees a cleared k-th path memo off the update path (clearKthMemo)
+  mutable std::thread kthReaper_;
   // once-only fills of kthIds_ (the reference memo runs each
   // (src, dst, k) once, and decision.spf_runs counts it once): a fill holds
   // the stripe of its key; stripes are per k (k = 1, 2; one lock for k >= 3).

@@ -439,6 +439,15 @@ class SpfSolver::SpfSolverImpl {
     std::vector<uint32_t> tmplNbr; // node id of each template's neighbour
   };
   FastEcmp fast_;
+  // per build, one area: node labels by device node id (selectKsp2)
+  struct Ksp2Fast {
+    bool ok{false};
+    const LinkState* ls{nullptr};
+    const std::string* area{nullptr};
+    uint32_t me{0};
+    std::vector<int32_t> labels;
+  };
+  Ksp2Fast ksp2Fast_;
   void buildFastEcmp(const std::string& myNodeName, AreaLinkStates const& areaLinkStates);
   // node label `label` held by `owner` (a single holder, not myNode):
   // getNextHopsWithMetric + getNextHopsThrift with the swap label, from the
@@ -993,6 +1002,26 @@ std::optional<int64_t> SpfSolver::SpfSolverImpl::getMinNextHopThreshold(
 void SpfSolver::SpfSolverImpl::buildFastEcmp(
     const std::string& myNodeName, AreaLinkStates const& areaLinkStates) {
   fast_ = FastEcmp{};
+  ksp2Fast_ = Ksp2Fast{};
+  if (areaLinkStates.size() == 1 && !getenv_flag_off("OPENR_KSP2_FAST")) {
+    // node labels by device node id for selectKsp2's label stacks
+    const auto& [area, ls] = *areaLinkStates.begin();
+    if (const auto me = ls.nodeId(myNodeName)) {
+      const auto& names = ls.nodeNames();
+      const auto& adj = ls.getAdjacencyDatabases();
+      ksp2Fast_.labels.assign(names.size(), 0);
+      bool ok = true;
+      for (uint32_t i = 0; i < names.size() && ok; ++i) {
+        auto it = adj.find(names[i]);
+        ok = it != adj.end();
+        ksp2Fast_.labels[i] = ok ? it->second.nodeLabel : 0;
+      }
+      ksp2Fast_.ok = ok;
+      ksp2Fast_.ls = &ls;
+      ksp2Fast_.area = &area;
+      ksp2Fast_.me = *me;
+    }
+  }
   if (areaLinkStates.size() != 1 || computeLfaPaths_ || getenv_flag_off("OPENR_ECMP_FAST")) {
     return;
   }
@@ -1370,11 +1399,62 @@ void SpfSolver::SpfSolverImpl::selectKsp2(
   // the destination's prepend label (Decision.cpp:1000-1047)
   const bool isV4Prefix = prefix.prefixAddress.addr.size() == 4;
   std::vector<int32_t> hopLabels;
+  // one area (the fabric): walk the paths by node id -- labels from the
+  // per-build array, hop metrics from the device CSR -- instead of a name
+  // lookup in the adjacency databases per hop (same values: the engine's
+  // metrics are the links' metrics, ksp2Labels_ the databases' labels)
+  const bool byId = ksp2Fast_.ok && areaLinkStates.size() == 1;
+  std::vector<std::pair<uint32_t, const thrift::PrefixEntry*>> destCache;
   for (const auto& path : paths) {
     if (path.size() == 0) {
       throw std::logic_error("selectKsp2: empty path");
     }
     const Link& firstLink = path.ls->linkOfId(path.first[0]);
+    if (byId && path.ls == ksp2Fast_.ls) {
+      const auto& area = *ksp2Fast_.area;
+      Metric cost = 0;
+      uint32_t at = ksp2Fast_.me;
+      hopLabels.clear();
+      bool ok = true;
+      for (const uint32_t* l = path.first; l != path.last && ok; ++l) {
+        uint32_t to = 0;
+        LinkStateMetric w = 0;
+        ok = path.ls->linkHop(*l, at, to, w);
+        cost += w;
+        at = to;
+        hopLabels.push_back(ok ? ksp2Fast_.labels[at] : 0);
+      }
+      if (ok) {
+        const thrift::PrefixEntry* destEntry = nullptr;
+        for (const auto& [id, e] : destCache) {
+          if (id == at) {
+            destEntry = e;
+          }
+        }
+        if (!destEntry) {
+          destEntry = &prefixEntries.at(path.ls->nodeNameOf(at)).at(area);
+          destCache.emplace_back(at, destEntry);
+        }
+        std::vector<int32_t> labels;
+        labels.reserve(hopLabels.size());
+        if (destEntry->prependLabel) {
+          labels.push_back(*destEntry->prependLabel); // bottom of stack
+        }
+        for (size_t h = hopLabels.size(); h-- > 1;) {
+          labels.push_back(hopLabels[h]);
+        }
+        std::optional<thrift::MplsAction> action;
+        if (!labels.empty()) {
+          action = createMplsAction(thrift::MplsActionCode::PUSH, std::nullopt, std::move(labels));
+        }
+        entry.nexthops.insert(createNextHop(
+            isV4Prefix ? firstLink.getNhV4FromNode(myNodeName)
+                       : firstLink.getNhV6FromNode(myNodeName),
+            firstLink.getIfaceFromNode(myNodeName), (int32_t)cost, action, true,
+            firstLink.getArea()));
+        continue;
+      }
+    }
     for (const auto& [area, ls] : areaLinkStates) {
       const auto& adjDbs = ls.getAdjacencyDatabases();
       Metric cost = 0;

@@ -2605,7 +2605,42 @@ struct MsBfsArgs {
   // writes them from the level rows as coalesced 16-byte stores
   // (OPENR_MS_LVL_ONLY); levels >= 255 and unreached pairs still go here
   uint32_t lvl_only;
+  // per-query ignore lists (KSP2 second passes): ign_mask[b * E + e] = the
+  // batch-b queries whose list holds link(e) (bit q - B b), ign_flag[b * nfw
+  // + v / 32] bit v: a half-edge of node v's row is ignored by one of them.
+  // Flagged nodes pull over the plain CSR with the masks applied, the others
+  // over the sliced copy as before; nullptr = no ignore lists
+  const uint64_t* ign_mask = nullptr;
+  const uint32_t* ign_flag = nullptr;
+  uint32_t E = 0;
+  uint32_t nfw = 0;
 };
+
+// Masks and flags of spf_msbfs_kernel's ignore mode: one block per query,
+// both halves of every ignored link (a half-edge h sits in the row of its
+// tail, which is where the pull reads it)
+__global__ __launch_bounds__(256) void spf_ms_ign_kernel(
+    const uint32_t* ign_off, const uint32_t* ign, const uint32_t* link_half,
+    const uint32_t* col, const uint32_t* rev, uint32_t L, uint32_t B, uint32_t E,
+    uint32_t nfw, uint64_t* mask, uint32_t* flag) {
+  const uint32_t q = blockIdx.x, b = q / B, j = q - b * B;
+  const uint32_t lo = ign_off[q], hi = ign_off[q + 1];
+  for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const uint32_t l = ign[i];
+    if (l >= L) {
+      continue;
+    }
+    for (uint32_t side = 0; side < 2; ++side) {
+      const uint32_t h = link_half[2 * (size_t)l + side];
+      if (h == kInf32) {
+        continue;
+      }
+      const uint32_t t = col[rev[h]];
+      atomicOr(reinterpret_cast<unsigned long long*>(mask + (size_t)b * E + h), 1ull << j);
+      atomicOr(flag + (size_t)b * nfw + (t >> 5), 1u << (t & 31));
+    }
+  }
+}
 
 // Write each (source, node) distance the moment its bit appears (one store
 // per bit).  These stores overlap the latency-bound row scans of the later
@@ -2761,7 +2796,19 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
         }
         const bool valid = v < V;
         MT nw = 0;
-        if (SELL && valid && vis[k] != full) {
+        const bool ignv = a.ign_flag && valid && vis[k] != full &&
+                          ((a.ign_flag[(size_t)b * a.nfw + (v >> 5)] >> (v & 31)) & 1u);
+        if (ignv) {
+          // a row with ignored half-edges: the plain CSR, each edge's bits
+          // masked by the queries that ignore its link
+          const uint64_t* m = a.ign_mask + (size_t)b * a.E;
+          MT acc = 0;
+          for (uint32_t e = a.row[v]; e < a.row[v + 1]; ++e) {
+            acc |= cur[a.col[e]] & ~(MT)m[e];
+          }
+          nw = acc & ~vis[k];
+          vis[k] |= nw;
+        } else if (SELL && valid && vis[k] != full) {
           // a wave reads 1 KB of its slice per load instead of one line per lane
           const uint32_t c = __builtin_amdgcn_readfirstlane(v >> 6);
           const uint32_t g0 = __builtin_amdgcn_readfirstlane(a.sell_off[c]);
@@ -5526,6 +5573,12 @@ struct spf_query {
   NhPlan nh = NhPlan::None;
   int wmax = 0;
   int ms_bits = 64; // MS-BFS batch width (32 or 64 sources per workgroup)
+  // MS-BFS over queries with ignore lists (KSP2 second passes): per-batch
+  // masks of ignored half-edges and flags of the rows holding one
+  bool ms_ign = false;
+  uint64_t* d_ms_mask = nullptr;
+  uint32_t* d_ms_flag = nullptr;
+  uint32_t ms_nfw = 0, ms_nbatch = 0;
   uint32_t dstep_shift = 5; // delta-stepping bucket width 2^shift
   bool dstep_lbk = false;    // bucket bytes in LDS (else from the dist row)
   uint32_t dstep_bs = 1024;  // delta-stepping workgroup size
@@ -5800,7 +5853,7 @@ void free_query(spf_query* q) {
         (void*)q->d_slab, (void*)q->d_msd, (void*)q->d_base_of,
         (void*)q->d_skip, (void*)q->d_key, (void*)q->d_qctr, (void*)q->d_scatter,
         (void*)q->d_trace, (void*)q->d_big, (void*)q->d_held_order, (void*)q->d_zl,
-        (void*)q->d_zvar,
+        (void*)q->d_zvar, (void*)q->d_ms_mask, (void*)q->d_ms_flag,
         (void*)q->d_ovf, q->narrow ? (void*)q->d_nhb : nullptr, (void*)q->d_tcs}) {
     pool_free(p);
   }
@@ -7263,6 +7316,22 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     }
   }
 
+  DistPlan ms_ign_prev = q->dist;
+  // distance-only batches with ignore lists on a uniform metric (KSP2 second
+  // passes: 9,975 per fabric build, each ignoring the links of its k = 1
+  // paths): the bit-parallel BFS with per-batch masks of the ignored
+  // half-edges instead of one SSSP workgroup per query (OPENR_SPF_MSBFS_IGN=0
+  // disables).  Mask memory: 8 B per (batch, half-edge), at most 1 GiB.
+  if (has_ign && uniform && !want_nh && !want_order && !literal && !exact && nq >= 32 &&
+      V <= kMsThreads * kMsMaxK && helpers.empty() &&
+      (q->dist == DistPlan::SsspLds || q->dist == DistPlan::SsspGmem) &&
+      env_flag("OPENR_SPF_MSBFS_IGN", 1) &&
+      !(getenv("OPENR_SPF_MSBFS") && atoi(getenv("OPENR_SPF_MSBFS")) == 0) &&
+      (uint64_t)((nq + 63) / 64) * g->E * 8 <= (1ull << 30)) {
+    ms_ign_prev = q->dist;
+    q->dist = DistPlan::BfsLds; // becomes MS-BFS just below
+    q->ms_ign = true;
+  }
   // many sources on a uniform metric: bit-parallel multi-source BFS
   // (OPENR_SPF_MSBFS=0 disables, =32 / =64 picks the batch width)
   if ((q->dist == DistPlan::BfsLds || q->dist == DistPlan::BfsGmem) &&
@@ -7285,6 +7354,10 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
         q->nh = NhPlan::Levels;
       }
     }
+  }
+  if (q->ms_ign && q->dist != DistPlan::MsBfs) {
+    q->dist = ms_ign_prev; // the MS-BFS plan did not apply: back to per-query SSSP
+    q->ms_ign = false;
   }
   if (!helpers.empty() && !(q->dist == DistPlan::MsBfs && q->nh == NhPlan::Levels) &&
       !(few_rows && q->dist == DistPlan::Dstep && q->nh == NhPlan::Rows && q->dlds)) {
@@ -7494,6 +7567,15 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     if (pool_malloc((void**)&q->d_lvl, ntab * q->nrows * q->Vp8) != hipSuccess ||
         pool_malloc((void**)&q->d_flags, 16) != hipSuccess) {
       return bail(fail(SPF_E_NOMEM, "level rows"));
+    }
+    if (q->ms_ign) {
+      q->ms_nbatch = (q->nrows + q->ms_bits - 1) / q->ms_bits;
+      q->ms_nfw = (V + 31) / 32;
+      if (pool_malloc((void**)&q->d_ms_mask, (size_t)q->ms_nbatch * g->E * 8) != hipSuccess ||
+          pool_malloc((void**)&q->d_ms_flag, (size_t)q->ms_nbatch * q->ms_nfw * 4) !=
+              hipSuccess) {
+        return bail(fail(SPF_E_NOMEM, "ignored half-edge masks"));
+      }
     }
   }
   if (want_nh) {
@@ -7993,6 +8075,20 @@ int launch_msbfs(spf_query* q, bool unit) {
   a.nz = 0;
   a.lvl_only = lvl_only(q) ? 1u : 0u;
   HIP_TRY(hipMemsetAsync(q->d_flags, 0, 16, g->stream));
+  if (q->ms_ign) {
+    HIP_TRY(hipMemsetAsync(q->d_ms_mask, 0, (size_t)q->ms_nbatch * g->E * 8, g->stream));
+    HIP_TRY(hipMemsetAsync(q->d_ms_flag, 0, (size_t)q->ms_nbatch * q->ms_nfw * 4, g->stream));
+    if (q->nq) {
+      hipLaunchKernelGGL(spf_ms_ign_kernel, dim3(q->nq), dim3(256), 0, g->stream, q->d_ign_off,
+                         q->d_ign, g->d_link_half, g->d_col, g->d_rev, g->L,
+                         (uint32_t)q->ms_bits, g->E, q->ms_nfw, q->d_ms_mask, q->d_ms_flag);
+      HIP_TRY(hipGetLastError());
+    }
+    a.ign_mask = q->d_ms_mask;
+    a.ign_flag = q->d_ms_flag;
+    a.E = g->E;
+    a.nfw = q->ms_nfw;
+  }
   const uint32_t K = (g->V + kMsThreads - 1) / kMsThreads;
   const void* kern = nullptr;
 #define MS_PICK(MT, KM)                                                            \

@@ -665,3 +665,37 @@ def test_msbfs_20k_nodes_32bit_batches(gpu_ready):
     q = g.query(srcs, abi.SPF_F_NEXTHOPS | abi.SPF_F_UNIT_METRIC).run()
     assert q.kernel == "msbfs+levels"
     check_query(csr, q, [int(s) for s in srcs], False, rows={0, 50, 95})
+
+
+@pytest.mark.parametrize("seed", [71, 72])
+def test_msbfs_ignore_lists(gpu_ready, seed, monkeypatch):
+    """Distance-only batches with ignore lists on a uniform metric run the
+    bit-parallel BFS with per-batch masks of the ignored half-edges (KSP2
+    second passes): rows equal the per-query SSSP (OPENR_SPF_MSBFS_IGN=0)
+    and the literal replay, with drained nodes, parallel links (one of two
+    parallel links ignored keeps the other), repeated and distinct sources,
+    lists from empty to hundreds of links, ids beyond the graph, and a batch
+    that is not a multiple of 64."""
+    rng = random.Random(seed)
+    V = 1500
+    links = random_links(rng, V, 5000, wmin=3, wmax=3, parallel=0.05, asym=False)
+    ov = np.zeros(V, dtype=np.uint8)
+    ov[rng.sample(range(V), 30)] = 1
+    csr = abi.Csr.from_links(V, links, overloaded=ov)
+    g = abi.Graph(csr)
+    srcs = [rng.randrange(V) for _ in range(60)] + [7] * 70
+    ign = []
+    for i in range(len(srcs)):
+        k = rng.choice([0, 1, 3, 20, 200])
+        ign.append(rng.sample(range(len(links)), k) + ([len(links) + 5] if i % 9 == 0 else []))
+    q = g.query(srcs, 0, ignore=ign).run()
+    assert q.kernel == "msbfs"
+    monkeypatch.setenv("OPENR_SPF_MSBFS_IGN", "0")
+    r = g.query(srcs, 0, ignore=ign).run()
+    assert r.kernel != "msbfs"
+    for i in range(len(srcs)):
+        assert (q.dist(i) == r.dist(i)).all(), i
+    check_query(csr, q, srcs, True, ignore=ign, rows={0, 5, 63, 64, 100, 129})
+    q.close()
+    r.close()
+    g.close()

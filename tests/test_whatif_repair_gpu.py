@@ -75,6 +75,10 @@ def _batch(g, csr, rng, srcs, per_src, flags, nlinks):
 
 
 def _compare(g, csr, qs, ign, flags, monkeypatch, rows):
+    # distance-only batches on a uniform metric take the bit-parallel BFS
+    # with ignore masks (no screen, test_msbfs_ignore_lists); keep them on
+    # the repair path here
+    monkeypatch.setenv("OPENR_SPF_MSBFS_IGN", "0")
     q = g.query(qs, flags, ignore=ign).run()
     nscr = q.screened()
     assert nscr is not None and nscr < len(qs)  # the repair ran on the rest

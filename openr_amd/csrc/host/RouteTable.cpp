@@ -48,37 +48,54 @@ AllNodesRouteTable::AllNodesRouteTable(
   }
   // eligible prefixes (Decision.cpp:313-412 restricted to selectEcmpOpenr)
   std::vector<uint32_t> annOff{0}, ann;
-  for (const auto& [prefix, entries] : ps.prefixes()) {
-    bool otherArea = false, bgp = false, inArea = false, borderAnn = false;
-    for (const auto& [node, byArea] : entries) {
-      for (const auto& [area, entry] : byArea) {
-        otherArea |= area != area_;
-        inArea |= area == area_;
-        borderAnn |= area == area_ && borderNodes && borderNodes->count(node);
-        bgp |= entry.type == thrift::PrefixType::BGP;
+  {
+    // eligibility and announcers per prefix on the host pool (read-only
+    // PrefixState lookups), kept in the map's iteration order
+    std::vector<std::pair<const thrift::IpPrefix*, const thrift::PrefixEntries*>> items;
+    items.reserve(ps.prefixes().size());
+    for (const auto& [prefix, entries] : ps.prefixes()) {
+      items.emplace_back(&prefix, &entries);
+    }
+    std::vector<uint8_t> keep(items.size(), 0);
+    std::vector<std::vector<Announcer>> anns(items.size());
+    parallelFor(items.size(), hostThreads(items.size(), 256), [&](size_t i, unsigned) {
+      const auto& prefix = *items[i].first;
+      const auto& entries = *items[i].second;
+      bool otherArea = false, bgp = false, inArea = false, borderAnn = false;
+      for (const auto& [node, byArea] : entries) {
+        for (const auto& [area, entry] : byArea) {
+          otherArea |= area != area_;
+          inArea |= area == area_;
+          borderAnn |= area == area_ && borderNodes && borderNodes->count(node);
+          bgp |= entry.type == thrift::PrefixType::BGP;
+        }
+      }
+      if (bgp || entries.empty() || (otherArea && !borderNodes) || !inArea || borderAnn) {
+        return;
+      }
+      if (prefix.prefixAddress.addr.size() == 4 && !enableV4_) {
+        return;
+      }
+      if (getPrefixForwardingType(entries) != thrift::PrefixForwardingType::IP ||
+          getPrefixForwardingAlgorithm(entries) != thrift::PrefixForwardingAlgorithm::SP_ECMP) {
+        return;
+      }
+      for (const auto& [node, byArea] : entries) {
+        auto it = ids_.find(node);
+        auto ea = byArea.find(area_);
+        if (it == ids_.end() || ea == byArea.end()) {
+          continue; // not in the graph / announced in another area: never reachable
+        }
+        anns[i].push_back(Announcer{it->second, ea->second});
+      }
+      keep[i] = 1;
+    }, 64);
+    for (size_t i = 0; i < items.size(); ++i) {
+      if (keep[i]) {
+        prefixes_.push_back(*items[i].first);
+        announcers_.push_back(std::move(anns[i]));
       }
     }
-    if (bgp || entries.empty() || (otherArea && !borderNodes) || !inArea || borderAnn) {
-      continue;
-    }
-    if (prefix.prefixAddress.addr.size() == 4 && !enableV4_) {
-      continue;
-    }
-    if (getPrefixForwardingType(entries) != thrift::PrefixForwardingType::IP ||
-        getPrefixForwardingAlgorithm(entries) != thrift::PrefixForwardingAlgorithm::SP_ECMP) {
-      continue;
-    }
-    std::vector<Announcer> as;
-    for (const auto& [node, byArea] : entries) {
-      auto it = ids_.find(node);
-      auto ea = byArea.find(area_);
-      if (it == ids_.end() || ea == byArea.end()) {
-        continue; // not in the graph / announced in another area: never reachable
-      }
-      as.push_back(Announcer{it->second, ea->second});
-    }
-    prefixes_.push_back(prefix);
-    announcers_.push_back(std::move(as));
   }
   // prefix order: by first announcer id, so neighbouring lanes of the
   // kernel read neighbouring distance / next-hop mask words of a row

@@ -8919,7 +8919,8 @@ int spf_query_trace_paths(
     // a state's tag is its query index + 1)
     // 16 waves per CU (a wave's DFS is a chain of L2 round trips: the more
     // queries in flight, the better); scratch bounded for large graphs
-    const uint32_t maxw = g->V > 50000 ? 1024u : (uint32_t)g->num_cus * 16u;
+    const uint32_t wpc = std::max<uint32_t>(1, std::min<uint32_t>(16, env_u32("OPENR_SPF_TRACE_WPC", 16)));
+    const uint32_t maxw = g->V > 50000 ? 1024u : (uint32_t)g->num_cus * wpc;
     const uint32_t nw = std::min<uint32_t>((count + kTcWaves - 1) / kTcWaves * kTcWaves, maxw);
     const uint32_t acap = std::max<uint32_t>(1024, std::min<uint32_t>(g->E, 1u << 15));
     const size_t need = (size_t)nw * g->V * sizeof(uint4) + (size_t)nw * acap * sizeof(uint2);

@@ -2628,7 +2628,13 @@ void LinkState::prefetchKthPaths(
     if (!traced) {
       tr.count.clear();
     }
-    const std::string* dstName = nullptr;
+    // the (src, dst, 2) entries: offsets serially, then one host-pool task
+    // per memo stripe (9,975 fills on the fabric; serially they were ~15 ms)
+    struct Fill {
+      const std::string* dst;
+      size_t i, lo, po;
+    };
+    std::vector<std::vector<Fill>> byStripe(kKthStripes);
     size_t j = 0, lo = 0, po = 0;
     uint64_t overflowed = 0;
     for (size_t i = 0; i < tr.count.size(); ++i) {
@@ -2639,24 +2645,32 @@ void LinkState::prefetchKthPaths(
       while (todo[j].second != dstIds[i]) {
         ++j; // todo and dstIds are in the same order (dstIds skips entries)
       }
-      dstName = todo[j].first;
-      KthPathIds paths;
-      const uint32_t* L = tr.links.data() + lo;
-      const uint32_t* E = tr.ends.data() + po;
-      paths.links.assign(L, L + tr.linkCount[i]);
-      paths.off.reserve(tr.count[i] + 1);
-      for (uint32_t p = 0; p < tr.count[i]; ++p) {
-        paths.off.push_back(E[p]);
-      }
+      const std::string* dstName = todo[j].first;
+      const size_t st = KthKeyHash{}(KthKey{src, *dstName, 2}) % kKthStripes;
+      byStripe[st].push_back({dstName, i, lo, po});
       lo += tr.linkCount[i];
       po += tr.count[i];
-      KthKey key{src, *dstName, 2};
-      KthStripe& stripe = kthStripe(key);
-      std::unique_lock<std::shared_mutex> wr(stripe.mu);
-      if (stripe.ids.emplace(std::move(key), std::move(paths)).second) {
-        Counters::add("decision.spf_runs", 1);
-      }
     }
+    std::atomic<int64_t> filled{0};
+    parallelFor(kKthStripes, hostThreads(tr.count.size(), 256), [&](size_t st, unsigned) {
+      KthStripe& stripe = (*kth_)[st];
+      int64_t n = 0;
+      std::unique_lock<std::shared_mutex> wr(stripe.mu);
+      for (const Fill& f : byStripe[st]) {
+        KthPathIds paths;
+        const uint32_t* L = tr.links.data() + f.lo;
+        const uint32_t* E = tr.ends.data() + f.po;
+        paths.links.assign(L, L + tr.linkCount[f.i]);
+        paths.off.reserve(tr.count[f.i] + 1);
+        for (uint32_t p = 0; p < tr.count[f.i]; ++p) {
+          paths.off.push_back(E[p]);
+        }
+        n += stripe.ids.emplace(KthKey{src, *f.dst, 2}, std::move(paths)).second ? 1 : 0;
+      }
+      filled += n;
+    }, 1);
+    // one COUNT sample per SPF, as the per-entry add(1) of the fill
+    Counters::addSamples("decision.spf_runs", filled.load(), filled.load());
     if (traced) {
       views = std::move(tr.rows);
       Counters::add("decision.kth2_device_traces", (int64_t)(tr.count.size() - overflowed));

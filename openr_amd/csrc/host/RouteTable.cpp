@@ -131,22 +131,31 @@ AllNodesRouteTable::AllNodesRouteTable(
   // label, owner in the graph), owners of a label by name; the cell of node
   // s is getNextHopsWithMetric(s, {owner}) with LFA off
   {
-    std::map<int32_t, std::vector<std::string>> byLabel;
+    // (label, owner id) sorted: labels ascending, owners by name (ids are
+    // name ranks) -- the order of a label -> sorted names map, without one
+    std::vector<std::pair<int32_t, uint32_t>> lab;
+    lab.reserve(names_.size());
     for (const auto& [node, db] : ls.getAdjacencyDatabases()) {
-      if (db.nodeLabel == 0 || !isMplsLabelValid(db.nodeLabel) || !ids_.count(node)) {
+      if (db.nodeLabel == 0 || !isMplsLabelValid(db.nodeLabel)) {
         continue;
       }
-      byLabel[db.nodeLabel].push_back(node);
+      auto it = ids_.find(node);
+      if (it != ids_.end()) {
+        lab.emplace_back(db.nodeLabel, it->second);
+      }
     }
-    for (auto& [label, owners] : byLabel) {
-      std::sort(owners.begin(), owners.end());
-      auto& cols = labelCols_[label];
-      for (const auto& n : owners) {
+    std::sort(lab.begin(), lab.end());
+    for (size_t i = 0; i < lab.size();) {
+      auto& cols = labelCols_.emplace_hint(labelCols_.end(), lab[i].first, std::vector<uint32_t>{})
+                       ->second;
+      size_t j = i;
+      for (; j < lab.size() && lab[j].first == lab[i].first; ++j) {
         cols.push_back((uint32_t)(prefixes_.size() + owners_.size()));
-        owners_.push_back(LabelOwner{label, ids_.at(n)});
-        ann.push_back(ids_.at(n));
+        owners_.push_back(LabelOwner{lab[j].first, lab[j].second});
+        ann.push_back(lab[j].second);
         annOff.push_back((uint32_t)ann.size());
       }
+      i = j;
     }
   }
   Counters::add("decision.route_table_labels_us", usSince(tp));

@@ -5216,13 +5216,20 @@ __global__ __launch_bounds__(64 * kTraceWaves) void spf_trace_paths_kernel(Trace
 // the source or transit, link not ignored), ranked by (d[u], u, u's row
 // position) and written to a per-wave arena in global scratch; node states
 // {query tag, arena offset, length, cursor} live in a per-wave node array.
+// The whole search is one wave's chain of dependent L2 round trips (the
+// fabric's slowest query, 24,859 steps over 5,301 lists, was the entire
+// 23.7 ms launch: profiles/r04ab), so a step is a BATCH: the 64 next
+// pathLinks of v and their tails' states {state, d, row bounds} in two round
+// trips, every entry whose tail already failed taken at once, the first live
+// one entered with its build inputs already in registers, and a just-built
+// list scanned from its LDS ranking instead of the arena.
 // Only the recursion stack is in LDS, so nothing but a path longer than
 // kTcDepth links, a node with more than kTcSort pathLinks or a full arena
 // overflows to the host.
 constexpr uint32_t kTcWaves = 4;    // waves (queries in flight) per block (16 per CU)
 constexpr uint32_t kTcDepth = 256;  // recursion frames per wave
 constexpr uint32_t kTcSort = 256;   // pathLinks of one node ranked in LDS
-constexpr uint32_t kTcIgn = 256;    // ignore-list entries staged in LDS per query
+constexpr uint32_t kTcIgn = 512;    // ignore-list LDS words per query (hash slots or the sorted list)
 
 struct TraceCursorArgs {
   TraceArgs t;
@@ -5230,7 +5237,11 @@ struct TraceCursorArgs {
   uint2* arena;    // [waves][arena_cap] {tail, link} of pathLinks(v), in order
   uint32_t arena_cap;
   uint32_t V;
+  // OPENR_SPF_TRACE_STATS=1: per query {wall ticks (100 MHz), DFS steps,
+  // pathLinks lists built, their filter ticks, rank ticks, entries}; nullptr = off
+  unsigned long long* qstat = nullptr;
 };
+constexpr uint32_t kTcStat = 6;
 
 __device__ __forceinline__ void tc_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -5250,14 +5261,17 @@ __device__ __forceinline__ uint4 tc_load4(const uint4* p) {
   return make_uint4(ld_coh(w), ld_coh(w + 1), ld_coh(w + 2), ld_coh(w + 3));
 }
 
+// STATS: the OPENR_SPF_TRACE_STATS build of the kernel (per-query clocks and
+// counts); the default build carries no instrumentation
+template <bool STATS>
 __global__ __launch_bounds__(64 * kTcWaves) void spf_trace_cursor_kernel(TraceCursorArgs A) {
   const TraceArgs& a = A.t;
   __shared__ uint32_t stk_s[kTcWaves][kTcDepth];  // node of each frame
   __shared__ uint32_t lnk_s[kTcWaves][kTcDepth];  // link taken at each frame
   __shared__ uint4 fst_s[kTcWaves][kTcDepth];     // the frame node's state (cursor in LDS)
-  __shared__ uint64_t key_s[kTcWaves][kTcSort];   // (d[u] << 32 | u)
+  __shared__ uint64_t key_s[kTcWaves][kTcSort];   // (d[u] << 32 | u), then the ranked list
   __shared__ uint32_t sub_s[kTcWaves][kTcSort];   // u's row position (tie-break)
-  __shared__ uint32_t edg_s[kTcWaves][kTcSort];   // in-edge e of v's row
+  __shared__ uint32_t edg_s[kTcWaves][kTcSort];   // link of the in-edge
   __shared__ uint32_t ign_s[kTcWaves][kTcIgn];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t gw = blockIdx.x * kTcWaves + wv, nwaves = gridDim.x * kTcWaves;
@@ -5267,53 +5281,91 @@ __global__ __launch_bounds__(64 * kTcWaves) void spf_trace_cursor_kernel(TraceCu
   uint32_t* lnk = lnk_s[wv];
   uint4* fst = fst_s[wv];
   uint64_t* keys = key_s[wv];
+  uint2* srt = reinterpret_cast<uint2*>(key_s[wv]); // the last built list, ranked
   uint32_t* subs = sub_s[wv];
-  uint32_t* edgs = edg_s[wv];
+  uint32_t* lnks = edg_s[wv];
   uint32_t* ignl = ign_s[wv];
   const uint64_t lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
+  // a wave's own node-state / arena stores are waited for before its next
+  // coherent read of that array (one s_waitcnt, not one per store; the
+  // arena's after a build, so a fresh list's scan does not wait on them).
+  // A macro on plain locals: flags captured by a lambda around the asm's
+  // memory clobber were kept in scratch, a vector memory round trip per test.
+  bool pend_a = false, pend_n = false;
+#define TC_DRAIN(p)                                     \
+  do {                                                  \
+    if (p) {                                            \
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+      pend_a = pend_n = false;                          \
+    }                                                   \
+  } while (0)
   for (uint32_t q = gw; q < a.nq; q += nwaves) { // wave-uniform loop
     const uint32_t tag = q + 1;
     const uint32_t s = a.src[q], d = a.dst[q];
     const uint32_t* dist = a.dist + (size_t)q * a.Vp;
     const uint32_t ilo = a.ign_off ? a.ign_off[q] : 0u;
     const uint32_t nign = a.ign_off ? a.ign_off[q + 1] - ilo : 0u;
-    const uint32_t* ignp = a.ign + ilo;
-    if (nign <= kTcIgn) {
-      for (uint32_t i = lane; i < nign; i += 64) {
-        ignl[i] = ignp[i];
+    // the ignore list (the k = 1 paths' links, hundreds on the fabric) as an
+    // LDS hash set: one or two probes per filtered in-edge, not a binary search
+    IgnSet ig;
+    ig.p = a.ign + ilo;
+    ig.n = nign;
+    const uint32_t slots = ign_hash_slots(nign);
+    if (slots && slots <= kTcIgn) {
+      for (uint32_t i = lane; i < slots; i += 64) {
+        ignl[i] = kInf32;
       }
-      ignp = ignl;
+      tc_sync();
+      const uint32_t hb = __builtin_ctz(slots);
+      for (uint32_t i = lane; i < nign; i += 64) {
+        const uint32_t l = a.ign[ilo + i];
+        uint32_t h = (l * 0x9E3779B1u) >> (32 - hb);
+        for (;;) {
+          const uint32_t prev = atomicCAS(&ignl[h], kInf32, l);
+          if (prev == kInf32 || prev == l) {
+            break;
+          }
+          h = (h + 1) & (slots - 1);
+        }
+      }
+      ig.p = ignl;
+      ig.hbits = hb;
+    } else if (nign <= kTcIgn) {
+      for (uint32_t i = lane; i < nign; i += 64) {
+        ignl[i] = a.ign[ilo + i];
+      }
+      ig.p = ignl;
     }
     tc_sync();
     uint32_t* out_links = a.out_links + (size_t)q * a.cap;
     uint32_t* out_ends = a.out_ends + (size_t)q * a.cap;
     uint32_t npaths = 0, nl = 0, atop = 0;
     bool overflow = false;
-    // the state of node v for this query: {tag, arena offset, length,
-    // cursor}; pathLinks(v) built into the arena on first use
-    auto enter = [&](uint32_t v) -> uint4 {
-      uint4 st = tc_load4(ns + v);
-      if (st.x == tag) {
-        return st;
-      }
-      const uint64_t dv = dist[v];
-      const uint32_t e0 = a.row[v], e1 = a.row[v + 1];
+    unsigned long long tq0 = STATS ? wall_clock64() : 0ull, nsteps = 0, nbuilt = 0;
+    unsigned long long tbuild = 0, trank = 0, nlen = 0; // stats: filter / rank ticks, list entries
+    // pathLinks(v) into the arena (and ranked into srt): v's in-edges e0..e1
+    // filtered (usable, tight against dv, tail the source or transit, link
+    // not ignored) and ranked by (d[u], u, u's row position).  Returns v's
+    // new state {tag, offset, length, 0}, or cursor kInf32 on overflow.
+    auto build = [&](uint32_t v, uint32_t dv, uint32_t e0, uint32_t e1) -> uint4 {
+      ++nbuilt;
+      const unsigned long long tb0 = STATS ? wall_clock64() : 0ull;
       uint32_t n = 0;
       for (uint32_t base = e0; base < e1; base += 64) {
         const uint32_t e = base + lane;
         bool ok = false;
-        uint32_t u = 0, du = 0, eu = 0;
+        uint32_t u = 0, du = 0, eu = 0, l = 0;
         if (e < e1) {
+          // two dependent round trips: the edge's words, then its tail's
           u = a.col[e];
+          eu = a.rev[e];
+          l = a.link[e];
           du = dist[u];
-          ok = du != kInf32 && (u == s || ((a.trbits[u >> 5] >> (u & 31)) & 1u));
-          if (ok) {
-            eu = a.rev[e];
-            const uint64_t w = a.unit ? 1ull : (uint64_t)a.wout[eu];
-            ok = (uint64_t)du + w == dv;
-          }
+          const uint32_t tb = a.trbits[u >> 5];
+          const uint64_t w = a.unit ? 1ull : (uint64_t)a.wout[eu];
+          ok = du != kInf32 && (u == s || ((tb >> (u & 31)) & 1u)) && (uint64_t)du + w == dv;
           if (ok && nign) {
-            ok = !in_sorted(ignp, nign, a.link[e]);
+            ok = !ig.has(l);
           }
         }
         const uint64_t m = __ballot(ok);
@@ -5321,7 +5373,7 @@ __global__ __launch_bounds__(64 * kTcWaves) void spf_trace_cursor_kernel(TraceCu
         if (ok && pos < kTcSort) {
           keys[pos] = ((uint64_t)du << 32) | u;
           subs[pos] = eu;
-          edgs[pos] = e;
+          lnks[pos] = l;
         }
         n += (uint32_t)__popcll(m);
       }
@@ -5329,41 +5381,81 @@ __global__ __launch_bounds__(64 * kTcWaves) void spf_trace_cursor_kernel(TraceCu
       if (n > kTcSort || atop + n > A.arena_cap) {
         return make_uint4(0, 0, 0, kInf32); // overflow marker
       }
-      for (uint32_t i = lane; i < n; i += 64) {
-        const uint64_t k = keys[i];
-        const uint32_t su = subs[i];
+      const unsigned long long tb1 = STATS ? wall_clock64() : 0ull;
+      uint32_t rr[kTcSort / 64], tl[kTcSort / 64], lk[kTcSort / 64];
+      if (n <= 64) {
+        // one entry per lane: rank against the others' keys read across
+        // lanes (no LDS round trip per comparison)
+        const bool in = lane < n;
+        const uint64_t key = in ? keys[lane] : ~0ull;
+        const uint32_t su = in ? subs[lane] : ~0u;
+        const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
         uint32_t r = 0;
         for (uint32_t j = 0; j < n; ++j) {
-          const uint64_t kj = keys[j];
-          r += kj < k || (kj == k && subs[j] < su);
+          const uint32_t jlo = (uint32_t)__builtin_amdgcn_readlane((int)klo, (int)j);
+          const uint32_t jhi = (uint32_t)__builtin_amdgcn_readlane((int)khi, (int)j);
+          const uint32_t js = (uint32_t)__builtin_amdgcn_readlane((int)su, (int)j);
+          const uint64_t kj = ((uint64_t)jhi << 32) | jlo;
+          r += (uint32_t)(kj < key) | ((uint32_t)(kj == key) & (uint32_t)(js < su));
         }
-        // the tail and the link: a step reads one 8-byte entry
-        arena[atop + r] = make_uint2((uint32_t)k, a.link[edgs[i]]);
+        rr[0] = r;
+        tl[0] = klo;
+        lk[0] = in ? lnks[lane] : 0u;
+      } else {
+#pragma unroll
+        for (uint32_t k = 0; k < kTcSort / 64; ++k) {
+          const uint32_t i = lane + 64 * k;
+          if (i < n) {
+            const uint64_t key = keys[i];
+            const uint32_t su = subs[i];
+            uint32_t r = 0;
+            for (uint32_t j = 0; j < n; ++j) {
+              const uint64_t kj = keys[j];
+              r += (uint32_t)(kj < key) | ((uint32_t)(kj == key) & (uint32_t)(subs[j] < su));
+            }
+            rr[k] = r;
+            tl[k] = (uint32_t)key;
+            lk[k] = lnks[i];
+          }
+        }
       }
-      st = make_uint4(tag, atop, n, 0);
+      tc_sync(); // every rank read the keys: srt reuses their words
+#pragma unroll
+      for (uint32_t k = 0; k < kTcSort / 64; ++k) {
+        if (lane + 64 * k < n) {
+          // the tail and the link: a scan reads one 8-byte entry per lane
+          const uint2 ent = make_uint2(tl[k], lk[k]);
+          srt[rr[k]] = ent;
+          arena[atop + rr[k]] = ent;
+        }
+      }
+      const uint4 st = make_uint4(tag, atop, n, 0);
       atop += n;
-      if (n == 0) {
+      if (n == 0 && lane == 0) {
         ns[v] = st; // no pathLink: every later visit fails at once
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       tc_sync();
-      return st;
-    };
-    // cursors of the frames' nodes back to their global states
-    auto save = [&](uint32_t lo, uint32_t hi) {
-      for (uint32_t f = lo + lane; f <= hi; f += 64) {
-        ns[stk[f]] = fst[f];
+      if (STATS) {
+        const unsigned long long tb2 = wall_clock64();
+        tbuild += tb1 - tb0;
+        trank += tb2 - tb1;
+        nlen += n;
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      tc_sync();
+      return st;
     };
     if (s != d && dist[d] != kInf32) {
       for (;;) { // one traceOnePath per iteration
-        uint32_t depth = 0;
-        uint4 st = enter(d);
-        if (st.w == kInf32) {
-          overflow = true;
-          break;
+        uint32_t depth = 0, fresh = kTcDepth; // fresh: the frame whose list is in srt
+        TC_DRAIN(pend_n);
+        uint4 st = tc_load4(ns + d);
+        if (st.x != tag) {
+          st = build(d, dist[d], a.row[d], a.row[d + 1]);
+          (st.z ? pend_a : pend_n) = true;
+          fresh = 0;
+          if (st.w == kInf32) {
+            overflow = true;
+            break;
+          }
         }
         if (lane == 0) {
           stk[0] = d;
@@ -5372,55 +5464,107 @@ __global__ __launch_bounds__(64 * kTcWaves) void spf_trace_cursor_kernel(TraceCu
         tc_sync();
         bool found = false;
         for (;;) {
+          ++nsteps;
           st = fst[depth];
-          if (st.w < st.z) {
-            const uint2 ent = ld_coh2(arena + st.y + st.w);
-            st.w += 1;
+          if (st.w >= st.z) {
+            // v exhausted: the search through it fails; its state goes back
+            if (lane == 0) {
+              ns[stk[depth]] = st;
+            }
+            pend_n = true;
+            if (depth == 0) {
+              break;
+            }
+            --depth;
+            continue;
+          }
+          // a batch of v's next pathLinks and the states of their tails in
+          // two round trips: entries whose tail already failed are taken
+          // (their link becomes visited) and skipped without a step each
+          const uint32_t cnt = min(64u, st.z - st.w);
+          const bool have = lane < cnt;
+          uint2 ent = make_uint2(kInf32, 0);
+          if (have) {
+            if (depth == fresh) {
+              ent = srt[st.w + lane];
+            } else {
+              TC_DRAIN(pend_a);
+              ent = ld_coh2(arena + st.y + st.w + lane);
+            }
+          }
+          const uint32_t u = ent.x;
+          uint4 su = make_uint4(0, 0, 0, 0);
+          uint32_t du = 0, r0 = 0, r1 = 0;
+          TC_DRAIN(pend_n);
+          if (have && u != s) {
+            su = tc_load4(ns + u);
+            du = dist[u];
+            r0 = a.row[u];
+            r1 = a.row[u + 1];
+          }
+          const bool live = have && (u == s || su.x != tag || su.w < su.z);
+          const uint64_t lm = __ballot(live);
+          if (lm == 0) {
+            st.w += cnt;
             if (lane == 0) {
               fst[depth] = st;
-              lnk[depth] = ent.y;
-            }
-            const uint32_t u = ent.x;
-            if (u == s) {
-              found = true;
-              break;
-            }
-            if (depth + 1 >= kTcDepth) {
-              overflow = true;
-              break;
-            }
-            const uint4 su = enter(u);
-            if (su.w == kInf32) {
-              overflow = true;
-              break;
-            }
-            if (su.w >= su.z) {
-              // u's search fails at once (the host trace's dead memo): next
-              // pathLink of v
-              tc_sync();
-              continue;
-            }
-            ++depth;
-            if (lane == 0) {
-              stk[depth] = u;
-              fst[depth] = su;
             }
             tc_sync();
             continue;
           }
-          // v exhausted: the search through it fails; its state goes back
-          tc_sync();
-          save(depth, depth);
-          if (depth == 0) {
+          const int f = (int)__builtin_ctzll(lm);
+          const uint32_t fu = (uint32_t)__builtin_amdgcn_readlane((int)u, f);
+          st.w += (uint32_t)f + 1;
+          if (lane == 0) {
+            fst[depth] = st;
+            lnk[depth] = (uint32_t)__builtin_amdgcn_readlane((int)ent.y, f);
+          }
+          if (fu == s) {
+            found = true;
             break;
           }
-          --depth;
+          if (depth + 1 >= kTcDepth) {
+            overflow = true;
+            break;
+          }
+          uint4 sf = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)su.x, f),
+                                (uint32_t)__builtin_amdgcn_readlane((int)su.y, f),
+                                (uint32_t)__builtin_amdgcn_readlane((int)su.z, f),
+                                (uint32_t)__builtin_amdgcn_readlane((int)su.w, f));
+          bool built = false;
+          if (sf.x != tag) {
+            sf = build(fu, (uint32_t)__builtin_amdgcn_readlane((int)du, f),
+                       (uint32_t)__builtin_amdgcn_readlane((int)r0, f),
+                       (uint32_t)__builtin_amdgcn_readlane((int)r1, f));
+            if (sf.w == kInf32) {
+              overflow = true;
+              break;
+            }
+            (sf.z ? pend_a : pend_n) = true;
+            built = true;
+            if (sf.z == 0) {
+              fresh = kTcDepth;
+              tc_sync();
+              continue; // u's search fails at once: next pathLink of v
+            }
+          }
+          ++depth;
+          fresh = built ? depth : kTcDepth;
+          if (lane == 0) {
+            stk[depth] = fu;
+            fst[depth] = sf;
+          }
+          tc_sync();
         }
         if (overflow || !found) {
           break;
         }
         tc_sync();
-        save(0, depth); // every frame's cursor moved on
+        // every frame's cursor moved on: the states go back
+        for (uint32_t f = lane; f <= depth; f += 64) {
+          ns[stk[f]] = fst[f];
+        }
+        pend_n = true;
         const uint32_t len = depth + 1;
         if (nl + len > a.cap || npaths + 1 > a.cap) {
           overflow = true;
@@ -5435,16 +5579,26 @@ __global__ __launch_bounds__(64 * kTcWaves) void spf_trace_cursor_kernel(TraceCu
           out_ends[npaths] = nl;
         }
         ++npaths;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         tc_sync();
       }
     }
     if (lane == 0) {
       a.out_n[q] = overflow ? kTraceOverflow : npaths;
       a.out_len[q] = overflow ? 0u : nl;
+      if (STATS) {
+        unsigned long long* o = A.qstat + kTcStat * (size_t)q;
+        o[0] = wall_clock64() - tq0;
+        o[1] = nsteps;
+        o[2] = nbuilt;
+        o[3] = tbuild;
+        o[4] = trank;
+        o[5] = nlen;
+      }
     }
+    TC_DRAIN(pend_a || pend_n); // the next query's tag check reads node states
     tc_sync(); // the next query restages the ignore list
   }
+#undef TC_DRAIN
 }
 
 struct TracePackArgs {
@@ -8940,8 +9094,47 @@ int spf_query_trace_paths(
     ta.arena_cap = acap;
     ta.V = g->V;
     HIP_TRY(hipMemsetAsync(q->d_tcs, 0, (size_t)nw * g->V * sizeof(uint4), g->stream));
-    hipLaunchKernelGGL(spf_trace_cursor_kernel, dim3(nw / kTcWaves), dim3(64 * kTcWaves), 0,
-                       g->stream, ta);
+    if (env_flag("OPENR_SPF_TRACE_STATS", 0)) {
+      HIP_TRY(hipMalloc((void**)&ta.qstat, (size_t)count * kTcStat * 8));
+      HIP_TRY(hipMemsetAsync(ta.qstat, 0, (size_t)count * kTcStat * 8, g->stream));
+    }
+    if (ta.qstat) {
+      hipLaunchKernelGGL(spf_trace_cursor_kernel<true>, dim3(nw / kTcWaves), dim3(64 * kTcWaves),
+                         0, g->stream, ta);
+    } else {
+      hipLaunchKernelGGL(spf_trace_cursor_kernel<false>, dim3(nw / kTcWaves), dim3(64 * kTcWaves),
+                         0, g->stream, ta);
+    }
+    if (ta.qstat) {
+      // per-query cost and the per-wave sums (wave w ran queries w, w + nw, ...)
+      std::vector<unsigned long long> h((size_t)count * kTcStat);
+      HIP_TRY(hipStreamSynchronize(g->stream));
+      HIP_TRY(hipMemcpy(h.data(), ta.qstat, h.size() * 8, hipMemcpyDeviceToHost));
+      HIP_TRY(hipFree(ta.qstat));
+      unsigned long long sum = 0, mx = 0, msteps = 0, ssteps = 0, sbuilt = 0;
+      uint32_t imax = 0;
+      std::vector<unsigned long long> wave(nw, 0);
+      for (uint32_t i = 0; i < count; ++i) {
+        const unsigned long long* r = h.data() + (size_t)kTcStat * i;
+        sum += r[0];
+        ssteps += r[1];
+        sbuilt += r[2];
+        msteps = std::max(msteps, r[1]);
+        if (r[0] > mx) {
+          mx = r[0];
+          imax = i;
+        }
+        wave[i % nw] += r[0];
+      }
+      const unsigned long long wmax = *std::max_element(wave.begin(), wave.end());
+      const unsigned long long* r = h.data() + (size_t)kTcStat * imax;
+      fprintf(stderr,
+              "[trace stats] queries=%u waves=%u ticks(100MHz): sum=%llu mean=%.1f max=%llu "
+              "(query %u: %llu steps, %llu lists of %llu entries, filter %llu rank %llu ticks) "
+              "wave-max=%llu; steps mean=%.1f max=%llu; lists mean=%.1f\n",
+              count, nw, sum, (double)sum / count, mx, imax, r[1], r[2], r[5], r[3], r[4], wmax,
+              (double)ssteps / count, msteps, (double)sbuilt / count);
+    }
   } else {
     hipLaunchKernelGGL(spf_trace_paths_kernel, dim3((count + kTraceWaves - 1) / kTraceWaves),
                        dim3(64 * kTraceWaves), 0, g->stream, a);

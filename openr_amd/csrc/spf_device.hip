@@ -2732,7 +2732,12 @@ __device__ __forceinline__ void ms_zero_close(
   }
 }
 
-template <typename MT, uint32_t KMAX, bool SELL>
+// GEN = false: the plain batch (no ignore masks, no wave-recorded levels, no
+// zero-metric closure) with those paths compiled out of the KMAX unrolled
+// node copies.  The general form spilled 79 VGPRs and 164 SGPRs per thread
+// (320 B of scratch, ~60 reloads per BFS level on the fabric's KMAX = 12);
+// the plain one 24 / 47 (100 B).
+template <typename MT, uint32_t KMAX, bool SELL, bool GEN>
 __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
   extern __shared__ __align__(16) unsigned char ms_smem[];
   constexpr uint32_t B = sizeof(MT) * 8;
@@ -2769,7 +2774,7 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
         trm |= ((a.trbits[v >> 5] >> (v & 31)) & 1u) << k;
       }
       vis[k] = (k < K && v < V) ? cur[v] : (MT)0;
-      if (a.wrec) {
+      if (GEN && a.wrec) {
         if (k < K) {
           ms_record_wave<MT>(a, q0, v, vis[k], 0); // level 0 = the sources
         }
@@ -2777,7 +2782,7 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
         ms_record<MT>(a, q0, v, vis[k], 0);
       }
     }
-    if (a.nz) {
+    if (GEN && a.nz) {
       ms_zero_close<MT, KMAX>(a, q0, cur, vis, trm, 0);
       __syncthreads();
     }
@@ -2796,7 +2801,7 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
         }
         const bool valid = v < V;
         MT nw = 0;
-        const bool ignv = a.ign_flag && valid && vis[k] != full &&
+        const bool ignv = GEN && a.ign_flag && valid && vis[k] != full &&
                           ((a.ign_flag[(size_t)b * a.nfw + (v >> 5)] >> (v & 31)) & 1u);
         if (ignv) {
           // a row with ignored half-edges: the plain CSR, each edge's bits
@@ -2855,7 +2860,7 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
         if (valid) {
           nxt[v] = transit ? nw : (MT)0;
         }
-        if (a.wrec) {
+        if (GEN && a.wrec) {
           ms_record_wave<MT>(a, q0, v, nw, L);
         } else if (nw) {
           ms_record<MT>(a, q0, v, nw, L);
@@ -2865,7 +2870,7 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
       if (!more) {
         break;
       }
-      if (a.nz) {
+      if (GEN && a.nz) {
         ms_zero_close<MT, KMAX>(a, q0, nxt, vis, trm, L);
         __syncthreads();
       }
@@ -2878,7 +2883,7 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
 #pragma unroll
     for (uint32_t k = 0; k < KMAX; ++k) {
       const uint32_t v = tid + k * kMsThreads;
-      if (a.wrec) {
+      if (GEN && a.wrec) {
         if (k < K) {
           // unreached pairs as one more "level" whose value is the sentinel
           const MT miss = v < V ? (full & ~vis[k]) : (MT)0;
@@ -8245,9 +8250,13 @@ int launch_msbfs(spf_query* q, bool unit) {
   }
   const uint32_t K = (g->V + kMsThreads - 1) / kMsThreads;
   const void* kern = nullptr;
-#define MS_PICK(MT, KM)                                                            \
-  kern = sell ? (const void*)spf_msbfs_kernel<MT, KM, true>                        \
-              : (const void*)spf_msbfs_kernel<MT, KM, false>
+  // OPENR_MS_GEN=1: the general instance for every batch (A/B of the plain one)
+  const bool gen = q->ms_ign || a.wrec || q->zvars || env_flag("OPENR_MS_GEN", 0);
+#define MS_PICK(MT, KM)                                                                      \
+  kern = gen ? (sell ? (const void*)spf_msbfs_kernel<MT, KM, true, true>                     \
+                     : (const void*)spf_msbfs_kernel<MT, KM, false, true>)                   \
+             : (sell ? (const void*)spf_msbfs_kernel<MT, KM, true, false>                    \
+                     : (const void*)spf_msbfs_kernel<MT, KM, false, false>)
   if (q->ms_bits == 64) {
     if (K <= 4) {
       MS_PICK(uint64_t, 4);

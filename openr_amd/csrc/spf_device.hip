@@ -8262,6 +8262,9 @@ int launch_msbfs(spf_query* q, bool unit) {
       MS_PICK(uint64_t, 4);
     } else if (K <= 8) {
       MS_PICK(uint64_t, 8);
+    } else if (K <= 10 && env_flag("OPENR_MS_K10", 1)) {
+      // the 10k fabric (K = 10): the plain instance spills 2 VGPRs, not 24
+      MS_PICK(uint64_t, 10);
     } else if (K <= 12) {
       MS_PICK(uint64_t, 12);
     } else {

@@ -36,6 +36,7 @@ import argparse
 import glob
 import json
 import os
+import re
 import sys
 import time
 
@@ -121,10 +122,20 @@ def msbfs_bytes(csr, nsrc, levels_per_batch, dist_rows=True):
     return int((5 if dist_rows else 1) * V * nsrc + sum(levels_per_batch) * (4 * E + 4 * (V + 1)))
 
 
+def _profile_files(fname):
+    """profiles/<round>/<fname>, oldest first in round order: r04z < r04aa
+    (a plain sort puts r04al before r04z)."""
+    def key(f):
+        d = os.path.basename(os.path.dirname(f))
+        m = re.match(r"r(\d+)([a-z]*)$", d)
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, d)
+    return sorted(glob.glob(os.path.join(ROOT, "profiles", "*", fname)), key=key)
+
+
 def pmc_traffic(kernel_name):
     """Per-launch HBM bytes of `kernel_name` from the committed PMC passes
     (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, MI355X_MICROARCH.md)."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")))
+    files = _profile_files("pmc_traffic.json")
     for f in reversed(files):
         try:
             d = json.load(open(f))
@@ -152,7 +163,7 @@ def wan_sssp_bytes(plan, V, E):
 def pmc_traffic_largest(kernel_name):
     """HBM bytes of the largest dispatch of `kernel_name` in the committed
     PMC passes (the measured launch, not a warm-up batch)."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")))
+    files = _profile_files("pmc_traffic.json")
     for f in reversed(files):
         try:
             d = json.load(open(f))
@@ -172,7 +183,7 @@ def pmc_traffic_sum(kernel_names, fname):
     kernels of (all dispatches' bytes / batches) from the newest committed
     profiles/*/<fname> (a probe that ran only that plan, e.g.
     profiles/whatif_probe.py)."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", fname)))
+    files = _profile_files(fname)
     for f in reversed(files):
         try:
             d = json.load(open(f))
@@ -190,7 +201,7 @@ def pmc_traffic_sum(kernel_names, fname):
 def pmc_traffic_smallest(kernel_name):
     """HBM bytes of the smallest dispatch of `kernel_name` in the committed
     PMC passes (a kernel launched in two modes: the plain one)."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")))
+    files = _profile_files("pmc_traffic.json")
     for f in reversed(files):
         try:
             d = json.load(open(f))

@@ -2591,6 +2591,10 @@ struct MsBfsArgs {
   uint32_t* dist_out; // [nq][Vp]
   uint8_t* lvl_out;   // [nq][Vp8]
   uint32_t* flags;    // [0] |= 1 when a level >= 255 occurred
+  // the other launch's flag word, zeroed by block 0 (flags alternate between
+  // two words per launch, so no per-run memset: stream order guarantees the
+  // last readers of this word, the previous run's next-hop pass, are done)
+  uint32_t* flags_clear = nullptr;
   uint32_t V;
   uint32_t Vp;
   uint32_t Vp8;
@@ -2744,6 +2748,9 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
   const uint32_t V = a.V, tid = threadIdx.x;
   const uint32_t K = (V + kMsThreads - 1) / kMsThreads; // <= KMAX
   const uint32_t nbatch = (a.nq + B - 1) / B;
+  if (a.flags_clear && blockIdx.x == 0 && tid == 0) {
+    *a.flags_clear = 0;
+  }
 
   for (uint32_t b = blockIdx.x; b < nbatch; b += gridDim.x) {
     // frontier double buffer: cur is read during a level, nxt written
@@ -5757,6 +5764,7 @@ struct spf_query {
   uint32_t dstep_ign_cap = 0; // the delta-stepping kernels' ignore-list words
   uint8_t* d_lvl = nullptr;
   uint32_t* d_flags = nullptr;
+  uint32_t ms_par = 0; // the flag word (0 / 1) of the last MS-BFS launch
   size_t lds_bytes = 0;
   bool has_ign = false;
   // next-hop masks.  Working layout (u64 words, nh_w[i] per node, query i at
@@ -7727,6 +7735,9 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
         pool_malloc((void**)&q->d_flags, 16) != hipSuccess) {
       return bail(fail(SPF_E_NOMEM, "level rows"));
     }
+    if (hipMemsetAsync(q->d_flags, 0, 16, g->stream) != hipSuccess) { // once: launches alternate words
+      return bail(fail(SPF_E_DEVICE, "level flags"));
+    }
     if (q->ms_ign) {
       q->ms_nbatch = (q->nrows + q->ms_bits - 1) / q->ms_bits;
       q->ms_nfw = (V + 31) / 32;
@@ -8233,7 +8244,9 @@ int launch_msbfs(spf_query* q, bool unit) {
   a.zlist = nullptr;
   a.nz = 0;
   a.lvl_only = lvl_only(q) ? 1u : 0u;
-  HIP_TRY(hipMemsetAsync(q->d_flags, 0, 16, g->stream));
+  q->ms_par ^= 1u;
+  a.flags = q->d_flags + q->ms_par;
+  a.flags_clear = q->d_flags + (q->ms_par ^ 1u);
   if (q->ms_ign) {
     HIP_TRY(hipMemsetAsync(q->d_ms_mask, 0, (size_t)q->ms_nbatch * g->E * 8, g->stream));
     HIP_TRY(hipMemsetAsync(q->d_ms_flag, 0, (size_t)q->ms_nbatch * q->ms_nfw * 4, g->stream));
@@ -8335,7 +8348,7 @@ int launch_nh_levels(spf_query* q, bool unit) {
   a.row_of = q->d_row_of;
   a.lvl = q->d_lvl;
   a.dist = (const uint32_t*)q->d_dist;
-  a.flags = q->d_flags;
+  a.flags = q->d_flags ? q->d_flags + q->ms_par : nullptr;
   a.nh_off = q->d_nh_off;
   a.nh_w = q->d_nh_w;
   a.nh_out = q->d_nh;

@@ -1,0 +1,12 @@
+set -o pipefail
+# round 4: MS-BFS flag words alternate per launch (no per-run 16-byte memset)
+D=gpurun_out/r04am; mkdir -p $D
+B="bench.py --no-cpu-baseline --no-route-db --no-whatif --no-wan --steps 20 --warmup 3"
+for i in 1 2; do
+timeout -k 10 300 python3 $B > $D/fabric.$i.json 2> $D/fabric.$i.err || { tail -5 $D/fabric.$i.err; exit 2; }
+python3 -c "import json,sys; d=json.load(open('$D/fabric.$i.json')); print(d['value'], d['ms_per_step'], {k: v['avg_ms'] for k, v in d['kernels'].items()})"
+done
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $D/gpu_tests.log 2>&1 || { tail -15 $D/gpu_tests.log; exit 3; }
+tail -1 $D/gpu_tests.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $D/smoke.log 2>&1 || { tail -5 $D/smoke.log; exit 4; }
+tail -1 $D/smoke.log

@@ -359,6 +359,11 @@ def test_deep_graph_many_levels(gpu_ready, msbfs):
     q = g.query(sources, abi.SPF_F_NEXTHOPS).run()
     assert q.kernel == _bfs_kernel(msbfs)
     check_query(csr, q, sources, True, rows=set(range(0, V, 37)) | {V - 1})
+    # reruns: the MS-BFS "level >= 255" flag alternates between two words
+    # per launch (each launch clears the other), so both words are exercised
+    for _ in range(2):
+        q.run()
+        check_query(csr, q, sources, True, rows={0, 150, V - 1})
 
 
 def test_fabric_all_sources_sampled(gpu_ready, msbfs):

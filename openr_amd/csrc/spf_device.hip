@@ -225,22 +225,44 @@ __device__ __forceinline__ void nh_store(uint8_t* row, uint32_t B, uint32_t W, u
   }
 }
 
+typedef uint32_t nt_u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t nt_u32x4 __attribute__((ext_vector_type(4)));
+
+// a streaming (write-once, never re-read by this pass) store: NT = true marks
+// it non-temporal so the output rows do not evict the level rows the other
+// blocks of the pass re-read from L2
+template <typename T>
+__device__ __forceinline__ void st_stream(T* p, T v, bool nt) {
+  if (nt) {
+    __builtin_nontemporal_store(v, p);
+  } else {
+    *p = v;
+  }
+}
+
 // single-word masks of nodes v0..v0+3 (v0 % 4 == 0) of a narrow row (B < 8):
 // one 4 / 8 / 16-byte store when all four nodes exist
 __device__ __forceinline__ void nh_store4_narrow(uint8_t* row, uint32_t B, uint32_t v0,
-                                                 uint32_t V, const uint64_t (&x)[4]) {
+                                                 uint32_t V, const uint64_t (&x)[4],
+                                                 bool nt = false) {
   if (v0 + 4 <= V) {
     if (B == 1) {
-      *reinterpret_cast<uint32_t*>(row + v0) =
-          (uint32_t)(x[0] & 0xFFu) | (uint32_t)(x[1] & 0xFFu) << 8 |
-          (uint32_t)(x[2] & 0xFFu) << 16 | (uint32_t)(x[3] & 0xFFu) << 24;
+      st_stream(reinterpret_cast<uint32_t*>(row + v0),
+                (uint32_t)(x[0] & 0xFFu) | (uint32_t)(x[1] & 0xFFu) << 8 |
+                    (uint32_t)(x[2] & 0xFFu) << 16 | (uint32_t)(x[3] & 0xFFu) << 24,
+                nt);
     } else if (B == 2) {
-      *reinterpret_cast<uint2*>(row + 2 * (size_t)v0) =
-          make_uint2((uint32_t)(x[0] & 0xFFFFu) | (uint32_t)(x[1] & 0xFFFFu) << 16,
-                     (uint32_t)(x[2] & 0xFFFFu) | (uint32_t)(x[3] & 0xFFFFu) << 16);
+      nt_u32x2 w;
+      w.x = (uint32_t)(x[0] & 0xFFFFu) | (uint32_t)(x[1] & 0xFFFFu) << 16;
+      w.y = (uint32_t)(x[2] & 0xFFFFu) | (uint32_t)(x[3] & 0xFFFFu) << 16;
+      st_stream(reinterpret_cast<nt_u32x2*>(row + 2 * (size_t)v0), w, nt);
     } else {
-      *reinterpret_cast<uint4*>(row + 4 * (size_t)v0) =
-          make_uint4((uint32_t)x[0], (uint32_t)x[1], (uint32_t)x[2], (uint32_t)x[3]);
+      nt_u32x4 w;
+      w.x = (uint32_t)x[0];
+      w.y = (uint32_t)x[1];
+      w.z = (uint32_t)x[2];
+      w.w = (uint32_t)x[3];
+      st_stream(reinterpret_cast<nt_u32x4*>(row + 4 * (size_t)v0), w, nt);
     }
     return;
   }
@@ -2965,6 +2987,9 @@ struct NhLevelsArgs {
   // chunk-major default
   const uint32_t* held_order = nullptr;
   uint32_t held_nch = 0;
+  // OPENR_NL_NT=1: the byte-SIMD pass's mask and distance rows as
+  // non-temporal stores
+  uint32_t nt_store = 0;
 };
 
 constexpr uint32_t kNlThreads = 256;
@@ -3408,8 +3433,12 @@ __device__ __forceinline__ void nl_dist_from_levels(
   uint32_t* dw = a.dist_w + (size_t)q * a.Vp + v0;
   const uint32_t b[4] = {ls & 0xFFu, (ls >> 8) & 0xFFu, (ls >> 16) & 0xFFu, ls >> 24};
   if (v0 + 4 <= a.V && b[0] < 255 && b[1] < 255 && b[2] < 255 && b[3] < 255) {
-    *reinterpret_cast<uint4*>(dw) =
-        make_uint4(b[0] * a.scale, b[1] * a.scale, b[2] * a.scale, b[3] * a.scale);
+    nt_u32x4 w;
+    w.x = b[0] * a.scale;
+    w.y = b[1] * a.scale;
+    w.z = b[2] * a.scale;
+    w.w = b[3] * a.scale;
+    st_stream(reinterpret_cast<nt_u32x4*>(dw), w, a.nt_store != 0);
     return;
   }
 #pragma unroll
@@ -3559,7 +3588,7 @@ __device__ __forceinline__ void nl_swar_held(
       // node-major: node v0 + i, word w at (v0 + i) * Wm + w; narrow rows
       // (B < 8 bytes per node, one word) as one 4 / 8 / 16-byte run
       if (H <= 3 && B < 8) {
-        nh_store4_narrow(nhrow_b, B, v0, a.V, held[0]);
+        nh_store4_narrow(nhrow_b, B, v0, a.V, held[0], a.nt_store != 0);
       } else if (H <= 3 && v0 + 4 <= a.V) {
         ulonglong2* o = reinterpret_cast<ulonglong2*>(nhrow + (size_t)v0 * Wm);
         if (Wm == 1) {
@@ -8349,6 +8378,7 @@ int launch_nh_levels(spf_query* q, bool unit) {
   a.lvl = q->d_lvl;
   a.dist = (const uint32_t*)q->d_dist;
   a.flags = q->d_flags ? q->d_flags + q->ms_par : nullptr;
+  a.nt_store = env_flag("OPENR_NL_NT", 0) ? 1u : 0u;
   a.nh_off = q->d_nh_off;
   a.nh_w = q->d_nh_w;
   a.nh_out = q->d_nh;

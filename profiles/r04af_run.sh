@@ -1,5 +1,6 @@
 set -o pipefail
-# round 4: trace store waits split vs joined, same box (A/B/A/B)
+# round 4: trace store waits split vs joined, same box (A/B/A/B); the
+# OPENR_SPF_TRACE_JOIN knob was removed after this run (no difference)
 D=gpurun_out/r04af; mkdir -p $D
 for i in 1 2; do
 for j in 0 1; do

@@ -28,6 +28,15 @@
  *   - Ownership: every device buffer is owned by the handle that allocated it.
  *     Host buffers passed in are read during the call only; host output
  *     buffers are caller-allocated and filled synchronously.
+ *   - Lifetime: a handle must outlive every handle created over it — queries
+ *     over a graph, route tables over a query, cluster graphs and tables over
+ *     a cluster, tables over a cluster graph.  Destroying a handle while
+ *     dependants are alive is refused: spf_graph_destroy, spf_query_destroy,
+ *     spf_cgraph_destroy and spf_cluster_destroy then return SPF_E_INVALID
+ *     and free nothing (the handle stays valid; destroy the dependants, then
+ *     call again).  This mirrors the reference's contract that SpfResult
+ *     references stay valid until the next topology change
+ *     (openr/decision/LinkState.h:269-275).  Destroying NULL is a no-op.
  *   - Threading: a graph and its queries are used from one host thread.  All
  *     work of a graph is enqueued on one HIP stream (spf_graph_set_stream).
  *   - Node ids are 0..V-1 and MUST equal the lexicographic rank of the node

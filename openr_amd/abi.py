@@ -19,6 +19,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("OPENR_SPF_LIB") or os.path.join(_HERE, "libopenr_spf.so")
 
 SPF_OK = 0
+SPF_E_INVALID = -1
+SPF_E_NOMEM = -2
+SPF_E_DEVICE = -3
 SPF_E_UNSUPPORTED = -4
 SPF_UNREACHABLE = (1 << 64) - 1
 SPF_TRACE_OVERFLOW = 0xFFFFFFFF
@@ -404,7 +407,9 @@ class Graph:
             # close the ones still alive first
             for q in list(self._queries):
                 q.close()
-            load().spf_graph_destroy(self.h)
+            # refused (and nothing freed) while a query is alive: the C ABI's
+            # lifetime rule, include/openr_spf.h
+            _check(load().spf_graph_destroy(self.h), "spf_graph_destroy")
             self.h = None
 
     def __del__(self):

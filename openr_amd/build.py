@@ -79,7 +79,8 @@ def _run(cmd):
 
 def build_device(force=False):
     cmd = recipe()["engine"]
-    srcs = _recipe_sources(cmd) + [os.path.join(INC, "openr_spf.h")]
+    srcs = _recipe_sources(cmd) + [os.path.join(INC, "openr_spf.h"),
+                                   os.path.join(CSRC, "host", "Parallel.h")]
     if force or _newer(LIB, srcs):
         _run(cmd)
     return LIB

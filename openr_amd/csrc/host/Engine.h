@@ -30,8 +30,14 @@ struct LinkState::Engine {
   // Link -> link id of this build: the tag buildGraph left on the Link
   // (Link::engineEpoch / engineId), ~0u for links that are not up links of it
   uint64_t epoch{0};
+  // (a copy of a Link carries the tag too, and freed ids are reused by
+  // patchStructure: the id only counts if it still names this very Link)
   uint32_t linkIdOf(const Link* l) const {
-    return l->engineEpoch == epoch ? l->engineId : ~0u;
+    if (l->engineEpoch != epoch) {
+      return ~0u;
+    }
+    const uint32_t id = l->engineId;
+    return id < links.size() && links[id].get() == l ? id : ~0u;
   }
   std::vector<std::array<uint32_t, 2>> halves; // link id -> half-edge from first/second node
   // link ids freed by in-place link removals (LinkState::patchStructure):

@@ -1633,19 +1633,36 @@ bool LinkState::patchStructure(
       dHops.push_back({col[rev[e]], col[e], 1, SPF_DELTA_ADDED, SPF_SCOPE_ALL});
     }
   }
-  // metric patches of the same update (kept links)
+  // metric patches of the same update.  The REMOVED delta must carry the
+  // metric the memoized rows were computed with: an affected row was rebuilt
+  // from linkMap_ above, where Link::setMetricFromNode has already run, so
+  // metric[e] may hold the new value; the old one is in the retired arrays
+  // (eng.metric at the link's old half-edge).
   for (const auto& [link, from] : metricPatches) {
-    const uint32_t lid = idOf(link.get());
-    if (lid == ~0u) {
-      return false;
-    }
-    const uint32_t e = halves[lid][from == link->firstNodeName() ? 0 : 1];
-    if (e == ~0u) {
-      return false;
-    }
+    const int side = from == link->firstNodeName() ? 0 : 1;
     const uint64_t w = link->getMetricFromNode(from);
-    dMetric.push_back({col[rev[e]], col[e], metric[e], SPF_DELTA_REMOVED, SPF_SCOPE_ALL});
-    dMetric.push_back({col[rev[e]], col[e], w, SPF_DELTA_ADDED, SPF_SCOPE_ALL});
+    if (const auto it = upIds.find(link.get()); it != upIds.end()) {
+      // came up in this update: its ADDED delta above has the new metric
+      const uint32_t e = halves[it->second][side];
+      if (e == ~0u) {
+        return false;
+      }
+      metric[e] = w;
+      continue;
+    }
+    const uint32_t lid = eng.linkIdOf(link.get());
+    if (lid == ~0u || lid >= eng.halves.size()) {
+      return false;
+    }
+    const uint32_t eOld = eng.halves[lid][side], e = halves[lid][side];
+    if (eOld == ~0u || e == ~0u) {
+      return false;
+    }
+    const uint64_t wOld = eng.metric[eOld];
+    if (wOld != w) {
+      dMetric.push_back({col[rev[e]], col[e], wOld, SPF_DELTA_REMOVED, SPF_SCOPE_ALL});
+      dMetric.push_back({col[rev[e]], col[e], w, SPF_DELTA_ADDED, SPF_SCOPE_ALL});
+    }
     metric[e] = w;
   }
   std::vector<uint8_t> overloaded = eng.overloaded;

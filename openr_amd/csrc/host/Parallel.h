@@ -20,10 +20,12 @@ namespace openr {
 // Worker threads for `n` independent items: OPENR_SPF_HOST_THREADS, else
 // min(hardware threads, 16); 1 (run inline) for small batches.
 inline unsigned hostThreads(size_t n, size_t minPerThread = 64) {
-  unsigned t = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  if (const char* env = std::getenv("OPENR_SPF_HOST_THREADS")) {
-    t = (unsigned)std::max(1, std::atoi(env));
-  }
+  static const unsigned t = [] { // read once: called several times per build
+    if (const char* env = std::getenv("OPENR_SPF_HOST_THREADS")) {
+      return (unsigned)std::max(1, std::atoi(env));
+    }
+    return std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  }();
   const size_t cap = std::max<size_t>(1, n / std::max<size_t>(1, minPerThread));
   return (unsigned)std::min<size_t>(t, cap);
 }

@@ -679,7 +679,12 @@ std::optional<DecisionRouteDb> SpfSolver::SpfSolverImpl::buildRouteDb(
       }
     }
   } merger;
-  if (skipMpls_ || std::getenv("OPENR_ROUTE_MERGE_INLINE")) {
+  // a thread per build costs more than merging a small RouteDb (the 10x10
+  // grid: ~100 routes, DecisionBenchmark.cpp:360-431): overlap only big ones.
+  // OPENR_ROUTE_MERGE_INLINE=1 always merges inline (read once).
+  static const bool mergeInlineEnv = std::getenv("OPENR_ROUTE_MERGE_INLINE") != nullptr;
+  constexpr size_t kMergeThreadMinRoutes = 2048;
+  if (skipMpls_ || mergeInlineEnv || built - routeDb.unicastEntries.size() < kMergeThreadMinRoutes) {
     mergeUnicast();
   } else {
     merger.t = std::thread(mergeUnicast);

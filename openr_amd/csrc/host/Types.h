@@ -81,9 +81,9 @@ class SmallString {
     return *this;
   }
   SmallString& operator=(const char* p) {
-    release();
-    init(p, std::strlen(p));
-    return *this;
+    // p may point into this string's own buffer (s = s.c_str()): copy first
+    SmallString tmp(p, std::strlen(p));
+    return *this = std::move(tmp);
   }
   ~SmallString() { release(); }
 

@@ -23,6 +23,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <memory>
@@ -79,21 +80,30 @@ uint64_t roundup32(uint64_t x) { return (x + 31) & ~31ull; }
 
 } // namespace
 
+// spf_device.hip (same library, not exported)
+extern "C" uint32_t spf_graph_live_queries_(const spf_graph* g);
+
 struct spf_cluster {
   uint32_t world = 1;
   uint32_t first_rank = 0; // global rank of local device 0
   std::vector<int> devices;
   std::vector<ncclComm_t> comms;
+  // live spf_cgraph / spf_table handles over this cluster: they use its
+  // devices and communicators, so spf_cluster_destroy refuses while any lives
+  std::atomic<uint32_t> users{0};
 };
 
 struct spf_cgraph {
   spf_cluster* c = nullptr;
   uint32_t V = 0;
   std::vector<spf_graph*> g; // one per local device, c->devices order
+  // live spf_table handles borrowing these graphs (spf_cgraph_destroy refuses)
+  std::atomic<uint32_t> tables{0};
 };
 
 struct spf_table {
   spf_cluster* c = nullptr;
+  spf_cgraph* cg = nullptr; // the borrowed graphs' owner (spf_table_create_q)
   bool borrowed = false; // graphs belong to an spf_cgraph (not destroyed here)
   uint32_t V = 0, n = 0, flags = 0, cap = 0;
   std::vector<uint32_t> sources;
@@ -214,6 +224,10 @@ int spf_cluster_destroy(spf_cluster* c) {
   if (!c) {
     return SPF_OK;
   }
+  if (const uint32_t n = c->users.load(std::memory_order_relaxed)) {
+    return cfail(SPF_E_INVALID, "spf_cluster_destroy: " + std::to_string(n) +
+                                    " live tables / cluster graphs (destroy them first)");
+  }
   for (auto comm : c->comms) {
     if (comm) {
       (void)ncclCommDestroy(comm);
@@ -241,6 +255,12 @@ int spf_cluster_info(
 }
 
 static void free_table(spf_table* t) {
+  if (t->c) {
+    t->c->users.fetch_sub(1, std::memory_order_relaxed);
+  }
+  if (t->cg) {
+    t->cg->tables.fetch_sub(1, std::memory_order_relaxed);
+  }
   for (auto& L : t->local) {
     (void)hipSetDevice(L.device);
     if (L.q) {
@@ -280,6 +300,7 @@ int spf_cgraph_create(spf_cluster* c, const spf_graph_desc* desc, spf_cgraph** o
   }
   auto cg = std::make_unique<spf_cgraph>();
   cg->c = c;
+  c->users.fetch_add(1, std::memory_order_relaxed); // spf_cgraph_destroy gives it back
   cg->V = desc->num_nodes;
   for (int dev : c->devices) {
     spf_graph_desc gd = *desc;
@@ -300,8 +321,21 @@ int spf_cgraph_destroy(spf_cgraph* cg) {
   if (!cg) {
     return SPF_OK;
   }
+  if (const uint32_t n = cg->tables.load(std::memory_order_relaxed)) {
+    return cfail(SPF_E_INVALID, "spf_cgraph_destroy: " + std::to_string(n) +
+                                    " live tables over this graph (destroy them first)");
+  }
+  for (spf_graph* g : cg->g) {
+    if (const uint32_t n = spf_graph_live_queries_(g)) {
+      return cfail(SPF_E_INVALID, "spf_cgraph_destroy: " + std::to_string(n) +
+                                      " live queries on a device graph (destroy them first)");
+    }
+  }
   for (spf_graph* g : cg->g) {
     spf_graph_destroy(g);
+  }
+  if (cg->c) {
+    cg->c->users.fetch_sub(1, std::memory_order_relaxed);
   }
   delete cg;
   return SPF_OK;
@@ -360,6 +394,7 @@ static int table_init(
     return cfail(SPF_E_INVALID, "spf_table_create: ignore_offsets[0] != 0");
   }
   t->c = c;
+  c->users.fetch_add(1, std::memory_order_relaxed); // free_table gives it back
   t->V = V;
   t->n = num_sources;
   t->flags = flags;
@@ -476,6 +511,8 @@ int spf_table_create_q(spf_cgraph* cg, const spf_query_desc* qd, uint32_t flags,
   }
   std::unique_ptr<spf_table, void (*)(spf_table*)> t(new spf_table, free_table);
   t->borrowed = true;
+  t->cg = cg;
+  cg->tables.fetch_add(1, std::memory_order_relaxed); // free_table gives it back
   CL_TRY(table_init(t.get(), cg->c, cg->g, cg->V, qd,
                     flags | (qd->flags & (SPF_F_UNIT_METRIC | SPF_F_NEXTHOPS))));
   *out = t.release();

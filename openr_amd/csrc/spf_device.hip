@@ -42,6 +42,7 @@
 #include <functional>
 #include <queue>
 #include <string>
+#include <map>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -3812,6 +3813,339 @@ __global__ __launch_bounds__(T) void spf_nh_levels_held_kernel(
                      lvl + (size_t)q * a.Vp8, st_row, st_node, st_nt);
 }
 
+// ---- held next-hop pass v2 (round 5): short dependency chains, shared rows
+//
+// The held kernel above is latency-bound, not bandwidth-bound: a block does
+// ~5 KB of output behind a chain of dependent round trips (src[q] ->
+// nbr_off[s] -> nbrs[] -> row_of[f] / trbits -> LDS + barrier -> the level
+// rows), and 83 % of the fabric's blocks are RSW sources with 8 neighbours.
+// Here the chain is cut to three trips and the RSW blocks are shared:
+//  * the host lists, per source, its neighbours' level-row indices and node
+//    ids once per query (NlEnt); lane j of each wave loads entry j and the
+//    rows reach the loads as readlane scalars — no LDS, no barrier;
+//  * sources whose distinct-neighbour lists are identical and short (<= GN
+//    neighbours, one mask word: the 48 RSWs of a fabric pod share their 8
+//    FSWs) form groups; a block serves GS of them on one chunk, holding the
+//    neighbours' level words in registers and reading only each source's own
+//    level row besides;
+//  * block descriptors are indexed straight by blockIdx (one scalar trip).
+// Same compare, masks and distance rows as nl_swar_held (byte for byte).
+struct NlEnt {
+  uint32_t row; // the neighbour's level-row index in the query (row_of)
+  uint32_t node;
+};
+struct NlSolo {
+  uint32_t q, n, lo, B; // query, neighbours, first NlEnt, mask bytes per node
+  uint64_t nhb_off;     // byte offset of the query's mask row
+  uint32_t Wm, pad;
+};
+struct NlSub { // GS (or fewer) sources with one neighbour list
+  uint32_t m0, cnt, n, lo, B, pad;
+};
+struct NlMem {
+  uint32_t q, pad;
+  uint64_t nhb_off;
+};
+struct NlV2Args {
+  const NlSolo* solo;
+  const NlSub* subs;
+  const NlMem* mem;
+  const NlEnt* ent;
+  uint32_t nsolo, nsub;
+  // measurement only (OPENR_NL_V2_DBG): bit 0 skips the solo items, bit 1 the
+  // groups, bit 2 computes without storing (the results stay live)
+  uint32_t dbg;
+};
+constexpr uint32_t kNlGS = 8;  // sources per group block
+constexpr uint32_t kNlGN = 16; // neighbours of a group source (one mask word, B <= 2)
+
+__device__ __forceinline__ bool nl_transit(const uint32_t* trbits, uint32_t f) {
+  return (trbits[f >> 5] >> (f & 31)) & 1u;
+}
+
+// the eight level words of group g (neighbours 8g .. 8g+7 of the word whose
+// entries lane j holds in `er`); missing neighbours read as 0xFF bytes, which
+// match no live node
+__device__ __forceinline__ void nl_v2_ld8(const uint8_t* lvl, uint32_t Vp8, uint32_t v0,
+                                          bool active, uint32_t er, uint32_t g, uint32_t cnt,
+                                          uint32_t (&lf)[8]) {
+#pragma unroll
+  for (uint32_t kk = 0; kk < 8; ++kk) {
+    lf[kk] = 0xFFFFFFFFu;
+    const uint32_t j = 8 * g + kk;
+    if (j < cnt) {
+      const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)er, (int)j);
+      if (active) {
+        lf[kk] = *reinterpret_cast<const uint32_t*>(lvl + (size_t)r * Vp8 + v0);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void nl_v2_cmp8(const uint32_t (&lf)[8], uint32_t tgt, uint32_t live,
+                                           uint32_t ntg, uint32_t er_node, uint32_t g,
+                                           uint32_t v0, uint32_t& P) {
+#pragma unroll
+  for (uint32_t kk = 0; kk < 8; ++kk) {
+    uint32_t m = live & swar_zero_bytes(lf[kk] ^ tgt);
+    if ((ntg >> kk) & 1u) {
+      // a drained neighbour is a next hop only to itself
+      const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)er_node, (int)(8 * g + kk));
+      const uint32_t r = f - v0;
+      m &= r < 4u ? (0x80u << (8u * r)) : 0u;
+    }
+    P |= m >> (7u - kk);
+  }
+}
+
+template <uint32_t T>
+__device__ __forceinline__ void nl_v2_solo(const NhLevelsArgs& a, const NlV2Args& v,
+                                           uint32_t k, uint32_t c) {
+  const NlSolo d = v.solo[k];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t vbase = c * (4 * T) + wv * 256;
+  if (vbase >= a.V) {
+    return; // wave-uniform
+  }
+  const uint32_t v0 = vbase + 4 * lane;
+  const bool active = v0 < a.V;
+  // every lane takes part in the entry loads (readlane reads lanes, not EXEC)
+  NlEnt e[kNsHeldMax];
+#pragma unroll
+  for (uint32_t w = 0; w < kNsHeldMax; ++w) {
+    e[w] = NlEnt{0u, 0u};
+    if (w < d.Wm && 64 * w + lane < d.n) {
+      e[w] = v.ent[d.lo + 64 * w + lane];
+    }
+  }
+  const uint32_t ls =
+      active ? *reinterpret_cast<const uint32_t*>(a.lvl + (size_t)d.q * a.Vp8 + v0) : 0xFFFFFFFFu;
+  const uint32_t tgt = ((ls | 0x80808080u) - 0x01010101u) ^ (~ls & 0x80808080u);
+  const uint32_t live = 0x80808080u & ~(swar_zero_bytes(ls) | swar_zero_bytes(~ls));
+  uint64_t held[kNsHeldMax][4];
+#pragma unroll
+  for (uint32_t w = 0; w < kNsHeldMax; ++w) {
+    if (w < d.Wm) {
+      const uint32_t cnt = min(64u, d.n - min(d.n, 64 * w));
+      uint32_t P[8];
+      uint32_t A[8], Bq[8];
+      nl_v2_ld8(a.lvl, a.Vp8, v0, active, e[w].row, 0, cnt, A);
+      const uint64_t ntmask = __ballot(64 * w + lane < d.n && !nl_transit(a.trbits, e[w].node));
+#pragma unroll
+      for (uint32_t g = 0; g < 8; ++g) {
+        P[g] = 0;
+        if (8 * g < cnt) {
+          // the next group's loads go out before this group's compares
+          if (g + 1 < 8 && 8 * (g + 1) < cnt) {
+            if (g & 1u) {
+              nl_v2_ld8(a.lvl, a.Vp8, v0, active, e[w].row, g + 1, cnt, A);
+            } else {
+              nl_v2_ld8(a.lvl, a.Vp8, v0, active, e[w].row, g + 1, cnt, Bq);
+            }
+          }
+          const uint32_t ntg = (uint32_t)(ntmask >> (8 * g)) & 0xFFu;
+          nl_v2_cmp8((g & 1u) ? Bq : A, tgt, live, ntg, e[w].node, g, v0, P[g]);
+        }
+      }
+      uint32_t lo[4], hi[4];
+      swar_transpose4(P[0], P[1], P[2], P[3], lo);
+      swar_transpose4(P[4], P[5], P[6], P[7], hi);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        held[w][i] = ((uint64_t)hi[i] << 32) | lo[i];
+      }
+    }
+  }
+  if (!active) {
+    return;
+  }
+  if (v.dbg & 4u) {
+    uint64_t x = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kNsHeldMax; ++w) {
+      x ^= held[w][0] ^ held[w][1] ^ held[w][2] ^ held[w][3];
+    }
+    if (x != 0x5A5A5A5A12345678ull) {
+      return; // measurement: no stores
+    }
+  }
+  if (a.dist_w) {
+    nl_dist_from_levels(a, d.q, v0, ls);
+  }
+  uint8_t* nhrow_b = a.nhb + d.nhb_off;
+  uint64_t* nhrow = reinterpret_cast<uint64_t*>(nhrow_b);
+  const uint32_t Wm = d.Wm;
+  if (d.B < 8) {
+    nh_store4_narrow(nhrow_b, d.B, v0, a.V, held[0], a.nt_store != 0);
+  } else if (v0 + 4 <= a.V) {
+    ulonglong2* o = reinterpret_cast<ulonglong2*>(nhrow + (size_t)v0 * Wm);
+    if (Wm == 1) {
+      o[0] = make_ulonglong2(held[0][0], held[0][1]);
+      o[1] = make_ulonglong2(held[0][2], held[0][3]);
+    } else if (Wm == 2) {
+      o[0] = make_ulonglong2(held[0][0], held[1][0]);
+      o[1] = make_ulonglong2(held[0][1], held[1][1]);
+      o[2] = make_ulonglong2(held[0][2], held[1][2]);
+      o[3] = make_ulonglong2(held[0][3], held[1][3]);
+    } else {
+      o[0] = make_ulonglong2(held[0][0], held[1][0]);
+      o[1] = make_ulonglong2(held[2][0], held[0][1]);
+      o[2] = make_ulonglong2(held[1][1], held[2][1]);
+      o[3] = make_ulonglong2(held[0][2], held[1][2]);
+      o[4] = make_ulonglong2(held[2][2], held[0][3]);
+      o[5] = make_ulonglong2(held[1][3], held[2][3]);
+    }
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+      if (v0 + i < a.V) {
+#pragma unroll
+        for (uint32_t w = 0; w < kNsHeldMax; ++w) {
+          if (w < Wm) {
+            nhrow[(size_t)(v0 + i) * Wm + w] = held[w][i];
+          }
+        }
+      }
+    }
+  }
+}
+
+template <uint32_t T>
+__device__ __forceinline__ void nl_v2_group(const NhLevelsArgs& a, const NlV2Args& v,
+                                            uint32_t k, uint32_t c) {
+  const NlSub d = v.subs[k];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t vbase = c * (4 * T) + wv * 256;
+  if (vbase >= a.V) {
+    return; // wave-uniform
+  }
+  const uint32_t v0 = vbase + 4 * lane;
+  const bool active = v0 < a.V;
+  NlEnt e{0u, 0u};
+  if (lane < d.n) {
+    e = v.ent[d.lo + lane];
+  }
+  uint32_t qs[kNlGS];
+  uint64_t offs[kNlGS];
+  uint32_t ls[kNlGS];
+#pragma unroll
+  for (uint32_t i = 0; i < kNlGS; ++i) {
+    qs[i] = 0;
+    offs[i] = 0;
+    if (i < d.cnt) {
+      const NlMem m = v.mem[d.m0 + i];
+      qs[i] = m.q;
+      offs[i] = m.nhb_off;
+    }
+  }
+  // the neighbours' level words: loaded once, held for every source
+  uint32_t lf[kNlGN];
+#pragma unroll
+  for (uint32_t j = 0; j < kNlGN; ++j) {
+    lf[j] = 0xFFFFFFFFu;
+    if (j < d.n) {
+      const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)e.row, (int)j);
+      if (active) {
+        lf[j] = *reinterpret_cast<const uint32_t*>(a.lvl + (size_t)r * a.Vp8 + v0);
+      }
+    }
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kNlGS; ++i) {
+    ls[i] = 0xFFFFFFFFu;
+    if (i < d.cnt && active) {
+      ls[i] = *reinterpret_cast<const uint32_t*>(a.lvl + (size_t)qs[i] * a.Vp8 + v0);
+    }
+  }
+  const uint64_t ntmask = __ballot(lane < d.n && !nl_transit(a.trbits, e.node));
+  // per neighbour: the byte lanes a match may set (a drained neighbour only
+  // its own node), the same for every source of the group
+  uint32_t allow[kNlGN];
+#pragma unroll
+  for (uint32_t j = 0; j < kNlGN; ++j) {
+    allow[j] = 0xFFFFFFFFu;
+    if ((ntmask >> j) & 1u) {
+      const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)e.node, (int)j);
+      const uint32_t r = f - v0;
+      allow[j] = r < 4u ? (0x80u << (8u * r)) : 0u;
+    }
+  }
+  if (!active) {
+    return;
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kNlGS; ++i) {
+    if (i < d.cnt) {
+      const uint32_t x = ls[i];
+      const uint32_t tgt = ((x | 0x80808080u) - 0x01010101u) ^ (~x & 0x80808080u);
+      const uint32_t live = 0x80808080u & ~(swar_zero_bytes(x) | swar_zero_bytes(~x));
+      uint32_t P0 = 0, P1 = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < kNlGN; ++j) {
+        if (j < d.n) {
+          const uint32_t m = live & allow[j] & swar_zero_bytes(lf[j] ^ tgt);
+          if (j < 8) {
+            P0 |= m >> (7u - j);
+          } else {
+            P1 |= m >> (15u - j);
+          }
+        }
+      }
+      uint8_t* row = a.nhb + offs[i];
+      if ((v.dbg & 4u) && (P0 ^ P1) != 0x5A5A5A5Au) {
+        continue; // measurement: no stores
+      }
+      if (v0 + 4 <= a.V) {
+        if (d.B == 1) {
+          st_stream(reinterpret_cast<uint32_t*>(row + v0), P0, a.nt_store != 0);
+        } else {
+          nt_u32x2 w2;
+          w2.x = __builtin_amdgcn_perm(P1, P0, 0x05010400u); // nodes 0, 1 (16 bits each)
+          w2.y = __builtin_amdgcn_perm(P1, P0, 0x07030602u); // nodes 2, 3
+          st_stream(reinterpret_cast<nt_u32x2*>(row + 2 * (size_t)v0), w2, a.nt_store != 0);
+        }
+      } else {
+#pragma unroll
+        for (uint32_t b = 0; b < 4; ++b) {
+          if (v0 + b < a.V) {
+            const uint32_t lo8 = (P0 >> (8 * b)) & 0xFFu, hi8 = (P1 >> (8 * b)) & 0xFFu;
+            nh_store(row, d.B, 1, v0 + b, 0, lo8 | (hi8 << 8));
+          }
+        }
+      }
+      if (a.dist_w) {
+        nl_dist_from_levels(a, qs[i], v0, x);
+      }
+    }
+  }
+}
+
+// blocks [0, nsolo * nch): solo (source, chunk) items, chunk-major (the
+// heavy SSW / FSW sources of the fabric first); then the groups' (sub-group,
+// chunk) items.  A BFS deeper than 254 levels leaves everything to
+// spf_nh_levels_swar_kernel.
+template <uint32_t T>
+__global__ __launch_bounds__(T) void spf_nh_levels_v2_kernel(NhLevelsArgs a, NlV2Args v) {
+  if (a.flags[0] != 0) {
+    return;
+  }
+  const uint32_t bid = blockIdx.x;
+  const uint32_t ns = v.nsolo * ((a.V + 4 * T - 1) / (4 * T));
+  if (bid < ns) {
+    if (v.dbg & 1u) {
+      return;
+    }
+    const uint32_t c = bid / v.nsolo;
+    nl_v2_solo<T>(a, v, bid - c * v.nsolo, c);
+  } else {
+    if (v.dbg & 2u) {
+      return;
+    }
+    const uint32_t b2 = bid - ns, c = b2 / v.nsub;
+    nl_v2_group<T>(a, v, b2 - c * v.nsub, c);
+  }
+}
+
 // Working word rows -> byte-strided output rows, after a plan whose kernels
 // wrote the word layout (spf_query::narrow): one block per (query, 1,024
 // nodes), four nodes per thread; narrow rows (B < 8) keep the low 8 * B bits
@@ -5754,6 +6088,14 @@ struct spf_graph {
   // cost more than the screen)
   char* d_repair = nullptr;
   size_t repair_bytes = 0;
+  // live spf_query handles over this graph (their own base / zfix sub-queries
+  // included): spf_graph_destroy refuses while any is alive, since a query
+  // reads g->device / g->stream / the device CSR until it is destroyed
+  std::atomic<uint32_t> live_queries{0};
+  // bumped whenever the distinct-neighbour lists are rebuilt (creation,
+  // spf_graph_set_edges): per-query tables built from them (the v2 next-hop
+  // pass) are stale after a change
+  uint64_t nbr_gen = 0;
 };
 
 // How a batch is computed.
@@ -5835,6 +6177,13 @@ struct spf_query {
   uint32_t* d_qctr = nullptr; // dstep source-claim counter
   uint32_t* d_big = nullptr;  // nh_levels: queries with more than kNsHeldMax mask words
   uint32_t* d_held_order = nullptr; // OPENR_NL_ORDER=1: XCD-contiguous held-kernel work order
+  // the v2 next-hop pass (spf_nh_levels_v2_kernel, OPENR_NL_V2): solo / group
+  // descriptors, members and neighbour entries in one pooled block, valid
+  // while the graph's neighbour lists are those of nbr_gen
+  void* d_v2 = nullptr;
+  NlV2Args v2{};
+  bool has_v2 = false;
+  uint64_t v2_gen = 0;
   uint32_t held_blocks = 0, held_nch = 0, held_t = 0;
   uint32_t nbig = 0;
   uint32_t nmid = 0;          // the first nmid of them have at most kNsHeldWide words
@@ -5863,6 +6212,9 @@ struct spf_query {
   hipEvent_t evm = nullptr; // after the distance stage, before next hops
   bool ran = false;
   bool two_stage = false; // evm recorded between two kernels
+  // live spf_route_table handles reading this query's rows (spf_query_destroy
+  // refuses while any is alive)
+  std::atomic<uint32_t> live_tables{0};
   // per-run event triples (start, after distance stage, end) of the last
   // kHist runs, for per-kernel averages over a timed loop without syncs
   static constexpr uint32_t kHist = 64;
@@ -6013,6 +6365,118 @@ int dev_upload(T** dst, const T* src, size_t n) {
   return SPF_OK;
 }
 
+// The v2 next-hop pass's tables (spf_nh_levels_v2_kernel): every source with
+// at most kNsHeldMax mask words is a solo item or a member of a group of
+// sources with the same short distinct-neighbour list (<= kNlGN neighbours,
+// one word); entries list each solo source's / group's neighbours as
+// (level-row index, node).
+int build_nl_v2(spf_query* q, const uint32_t* sources, const std::vector<int32_t>& row_of) {
+  const spf_graph* g = q->g;
+  std::vector<NlSolo> solo;
+  std::vector<NlSub> subs;
+  std::vector<NlMem> mem;
+  std::vector<NlEnt> ent;
+  std::map<std::vector<uint32_t>, std::vector<uint32_t>> groups;
+  std::vector<const std::vector<uint32_t>*> order; // groups in first-member order
+  auto addEnt = [&](uint32_t s) -> uint32_t {
+    const uint32_t lo = (uint32_t)ent.size();
+    for (uint32_t k = g->nbr_off[s]; k < g->nbr_off[s + 1]; ++k) {
+      const uint32_t f = g->nbrs[k];
+      ent.push_back(NlEnt{(uint32_t)row_of[f], f});
+    }
+    return lo;
+  };
+  std::vector<uint32_t> soloQ;
+  for (uint32_t i = 0; i < q->nq; ++i) {
+    if (q->nh_w[i] > kNsHeldMax) {
+      continue;
+    }
+    const uint32_t s = sources[i], n = g->nbr_off[s + 1] - g->nbr_off[s];
+    for (uint32_t k = g->nbr_off[s]; k < g->nbr_off[s + 1]; ++k) {
+      if (row_of.empty() || row_of[g->nbrs[k]] < 0) {
+        return SPF_OK; // a neighbour without a row: keep the held kernel
+      }
+    }
+    if (n >= 1 && n <= kNlGN && q->nh_w[i] == 1) {
+      std::vector<uint32_t> key(g->nbrs.begin() + g->nbr_off[s], g->nbrs.begin() + g->nbr_off[s + 1]);
+      auto [it, fresh] = groups.try_emplace(std::move(key));
+      if (fresh) {
+        order.push_back(&it->first);
+      }
+      it->second.push_back(i);
+    } else {
+      soloQ.push_back(i);
+    }
+  }
+  for (const auto* key : order) {
+    const auto& members = groups[*key];
+    if (members.size() == 1) {
+      soloQ.push_back(members[0]);
+      continue;
+    }
+    const uint32_t s = sources[members[0]];
+    const uint32_t lo = addEnt(s), n = (uint32_t)key->size();
+    for (size_t m = 0; m < members.size(); m += kNlGS) {
+      NlSub sb{};
+      sb.m0 = (uint32_t)mem.size();
+      sb.cnt = (uint32_t)std::min<size_t>(kNlGS, members.size() - m);
+      sb.n = n;
+      sb.lo = lo;
+      sb.B = q->nh_b[members[0]];
+      for (uint32_t x = 0; x < sb.cnt; ++x) {
+        const uint32_t i = members[m + x];
+        mem.push_back(NlMem{i, 0u, q->nhb_off[i]});
+      }
+      subs.push_back(sb);
+    }
+  }
+  // heavy solo sources first: their blocks are the longest
+  std::stable_sort(soloQ.begin(), soloQ.end(), [&](uint32_t x, uint32_t y) {
+    const uint32_t sx = sources[x], sy = sources[y];
+    return g->nbr_off[sx + 1] - g->nbr_off[sx] > g->nbr_off[sy + 1] - g->nbr_off[sy];
+  });
+  for (const uint32_t i : soloQ) {
+    const uint32_t s = sources[i];
+    NlSolo so{};
+    so.q = i;
+    so.n = g->nbr_off[s + 1] - g->nbr_off[s];
+    so.lo = addEnt(s);
+    so.B = q->nh_b[i];
+    so.nhb_off = q->nhb_off[i];
+    so.Wm = q->nh_w[i];
+    solo.push_back(so);
+  }
+  const uint32_t nch = (g->V + 1023) / 1024;
+  if ((uint64_t)(solo.size() + subs.size()) * nch > 0x7FFFFFFFull) {
+    return SPF_OK; // the held kernel's own limit check reports it
+  }
+  auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  const size_t o_solo = 0, o_sub = al(o_solo + solo.size() * sizeof(NlSolo)),
+               o_mem = al(o_sub + subs.size() * sizeof(NlSub)),
+               o_ent = al(o_mem + mem.size() * sizeof(NlMem)),
+               total = al(o_ent + std::max<size_t>(1, ent.size()) * sizeof(NlEnt));
+  std::vector<uint8_t> host(total, 0);
+  std::memcpy(host.data() + o_solo, solo.data(), solo.size() * sizeof(NlSolo));
+  std::memcpy(host.data() + o_sub, subs.data(), subs.size() * sizeof(NlSub));
+  std::memcpy(host.data() + o_mem, mem.data(), mem.size() * sizeof(NlMem));
+  std::memcpy(host.data() + o_ent, ent.data(), ent.size() * sizeof(NlEnt));
+  if (pool_malloc(&q->d_v2, total) != hipSuccess ||
+      hipMemcpy(q->d_v2, host.data(), total, hipMemcpyHostToDevice) != hipSuccess) {
+    return fail(SPF_E_NOMEM, "v2 next-hop tables");
+  }
+  uint8_t* b = static_cast<uint8_t*>(q->d_v2);
+  q->v2.solo = reinterpret_cast<const NlSolo*>(b + o_solo);
+  q->v2.subs = reinterpret_cast<const NlSub*>(b + o_sub);
+  q->v2.mem = reinterpret_cast<const NlMem*>(b + o_mem);
+  q->v2.ent = reinterpret_cast<const NlEnt*>(b + o_ent);
+  q->v2.nsolo = (uint32_t)solo.size();
+  q->v2.nsub = (uint32_t)subs.size();
+  q->v2.dbg = env_u32("OPENR_NL_V2_DBG", 0);
+  q->has_v2 = true;
+  q->v2_gen = g->nbr_gen;
+  return SPF_OK;
+}
+
 void free_graph(spf_graph* g) {
   if (!g) {
     return;
@@ -6050,7 +6514,7 @@ void free_query(spf_query* q) {
         (void*)q->d_skip, (void*)q->d_key, (void*)q->d_qctr, (void*)q->d_scatter,
         (void*)q->d_trace, (void*)q->d_big, (void*)q->d_held_order, (void*)q->d_zl,
         (void*)q->d_zvar, (void*)q->d_ms_mask, (void*)q->d_ms_flag,
-        (void*)q->d_ovf, q->narrow ? (void*)q->d_nhb : nullptr, (void*)q->d_tcs}) {
+        (void*)q->d_ovf, q->narrow ? (void*)q->d_nhb : nullptr, (void*)q->d_tcs, q->d_v2}) {
     pool_free(p);
   }
   if (q->base) {
@@ -6075,6 +6539,7 @@ void free_query(spf_query* q) {
       }
     }
   }
+  q->g->live_queries.fetch_sub(1, std::memory_order_relaxed);
   delete q;
 }
 
@@ -6084,6 +6549,7 @@ void free_query(spf_query* q) {
 // pool).  A half-edge taken down in place (spf_graph_set_edges) is no
 // neighbour; its slot is 0 (it is never tight, so never read).
 void build_nbr_lists(spf_graph* g) {
+  ++g->nbr_gen;
   const uint32_t V = g->V, E = g->E;
   const bool patched = !g->edge_up.empty();
   g->nbr_off.assign(V + 1, 0);
@@ -6937,8 +7403,22 @@ int spf_device_memcpy(int device, void* dst, const void* src, size_t bytes, int 
   return SPF_OK;
 }
 
+// live queries of a graph (not exported: spf_cgraph_destroy checks every
+// device graph before it frees any)
+__attribute__((visibility("hidden"))) uint32_t spf_graph_live_queries_(const spf_graph* g) {
+  return g ? g->live_queries.load(std::memory_order_relaxed) : 0u;
+}
+
 int spf_graph_destroy(spf_graph* g) {
   SPF_ABI_RANGE("spf_graph_destroy");
+  if (g) {
+    if (const uint32_t n = g->live_queries.load(std::memory_order_relaxed)) {
+      // destroying it would leave those queries reading freed memory (their
+      // destroy sets g->device and syncs g->stream): refuse, free nothing
+      return fail(SPF_E_INVALID, "spf_graph_destroy: " + std::to_string(n) +
+                                     " live queries on this graph (destroy them first)");
+    }
+  }
   free_graph(g);
   return SPF_OK;
 }
@@ -7242,6 +7722,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
 
   spf_query* q = new spf_query();
   q->g = g;
+  g->live_queries.fetch_add(1, std::memory_order_relaxed); // free_query gives it back
   q->nq = nq;
   q->flags = desc->flags;
   q->has_ign = has_ign;
@@ -7708,6 +8189,11 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
     if (!big.empty() && dev_upload_q(&q->d_big, big.data(), big.size()) != SPF_OK) {
       return bail(fail(SPF_E_NOMEM, "next-hop source list"));
     }
+    if (q->zvars == 0 && env_flag("OPENR_NL_V2", 1) && env_u32("OPENR_NL_ORDER", 0) != 1) {
+      if (const int s = build_nl_v2(q, desc->sources, row_of); s != SPF_OK) {
+        return bail(s);
+      }
+    }
     // OPENR_NL_ORDER=1: the held kernel's (source, chunk) items cut into 8
     // contiguous source ranges of equal cost (8 + neighbours per item), one
     // per XCD (hardware block b runs on XCD b % 8), source-major inside a
@@ -7889,6 +8375,12 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
 
 int spf_query_destroy(spf_query* q) {
   SPF_ABI_RANGE("spf_query_destroy");
+  if (q) {
+    if (const uint32_t n = q->live_tables.load(std::memory_order_relaxed)) {
+      return fail(SPF_E_INVALID, "spf_query_destroy: " + std::to_string(n) +
+                                     " live route tables over this query (destroy them first)");
+    }
+  }
   free_query(q);
   return SPF_OK;
 }
@@ -8418,7 +8910,14 @@ int launch_nh_levels(spf_query* q, bool unit) {
       return fail(SPF_E_UNSUPPORTED, "batch too large for the next-hop pass");
     }
     const uint32_t* nolist = nullptr;
-    if (T == 1024) {
+    if (q->has_v2 && q->v2_gen == g->nbr_gen && T == 256 && !a.held_order) {
+      // v2: solo items and shared-neighbour groups (spf_nh_levels_v2_kernel)
+      const uint64_t vblocks = (uint64_t)(q->v2.nsolo + q->v2.nsub) * ((g->V + 1023) / 1024);
+      if (vblocks) {
+        hipLaunchKernelGGL((spf_nh_levels_v2_kernel<256>), dim3((uint32_t)vblocks), dim3(256), 0,
+                           g->stream, a, q->v2);
+      }
+    } else if (T == 1024) {
       hipLaunchKernelGGL((spf_nh_levels_held_kernel<1024, kNsHeldMax>), dim3((uint32_t)hblocks),
                          dim3(1024), 0, g->stream, a, nolist, 0u);
     } else if (T == 512) {
@@ -9779,6 +10278,7 @@ void free_route_table(spf_route_table* t) {
     return;
   }
   (void)hipSetDevice(t->q->g->device);
+  t->q->live_tables.fetch_sub(1, std::memory_order_relaxed);
   for (void* p : {(void*)t->d_ann_off, (void*)t->d_ann, (void*)t->d_metric, (void*)t->d_best,
                   (void*)t->d_lk_off, (void*)t->d_links, (void*)t->d_diff, (void*)t->d_count,
                   (void*)t->d_lm_off, (void*)t->d_lmet, (void*)t->d_row_of}) {
@@ -9863,6 +10363,7 @@ int spf_route_table_create_ex(
   }
   auto* t = new spf_route_table();
   t->q = q;
+  q->live_tables.fetch_add(1, std::memory_order_relaxed); // free_route_table gives it back
   t->P = num_prefixes;
   t->lfa = lfa;
   t->lk_off.assign(q->nq + 1, 0);
@@ -9914,6 +10415,7 @@ int spf_route_table_create_ex(
 }
 
 int spf_route_table_destroy(spf_route_table* t) {
+  SPF_ABI_RANGE("spf_route_table_destroy");
   free_route_table(t);
   return SPF_OK;
 }

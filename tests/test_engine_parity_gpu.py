@@ -250,6 +250,59 @@ def test_link_flaps_in_place(mods, seed):
 
 
 @pytest.mark.parametrize("seed", range(4))
+def test_link_flap_with_metric_raise_in_one_update(mods, seed):
+    """one adjacency update that withdraws an adjacency AND
+    raises the metric of another (tight) link of the same node.  The node's
+    CSR row is rebuilt from linkMap_ after Link::setMetricFromNode ran, so the
+    memo screen must take the REMOVED delta's metric from the retired arrays;
+    with the new metric it kept memoized views whose shortest paths used the
+    old, cheaper link.  Every node's metric SpfResult is memoized before each
+    update and must equal the oracle's after it (no full rebuild)."""
+    import random
+
+    E, O = mods
+    names, adj_dbs, prefix_dbs = RZ.random_network(4100 + seed, n_nodes=30, n_links=80)
+    ea, ep = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    oa, op = RZ.load(O, adj_dbs, prefix_dbs, seed)
+    es = E.SpfSolver(names[0], True, False)
+    os_ = O.SpfSolver(names[0], True, False)
+    rng = random.Random(seed)
+    dbs = [copy.deepcopy(d) for d in adj_dbs["0"]]
+    es.buildRouteDb(names[0], ea, ep)
+    E.reset_counters()
+    steps = 0
+    for _ in range(40):
+        if steps == 8:
+            break
+        i = rng.randrange(len(dbs))
+        db = dbs[i]
+        if len(db.adjacencies) < 3:
+            continue
+        for node in names:  # warm the whole memo
+            if ea["0"].hasNode(node):
+                ea["0"].getSpfResult(node, True)
+        k = rng.randrange(len(db.adjacencies))
+        rest = db.adjacencies[:k] + db.adjacencies[k + 1:]
+        # raise one kept link (or every one) of the same node in the same update
+        bump = rest if steps % 2 else [rng.choice(rest)]
+        for adj in bump:
+            adj.metric = adj.metric + rng.randint(1, 6)
+        db.adjacencies = rest
+        assert ea["0"].updateAdjacencyDatabase(db) == oa["0"].updateAdjacencyDatabase(db)
+        for node in names:
+            if ea["0"].hasNode(node):
+                _spf_equal(ea["0"], oa["0"], node, True)
+        me = names[steps % len(names)]
+        assert es.buildRouteDb(me, ea, ep) == os_.buildRouteDb(me, oa, op), (steps, me)
+        steps += 1
+    assert steps == 8
+    c = E.get_counters()
+    assert c.get("decision.graph_inplace_link_patches", 0) > 0
+    assert c.get("decision.graph_build_us", 0) == 0
+    assert c.get("decision.spf_memo_dropped", 0) > 0
+
+
+@pytest.mark.parametrize("seed", range(4))
 def test_selective_memo_invalidation(mods, seed):
     """SURVEY §8(f) row 2 in LinkState: a topology change keeps the memoized
     SPF views whose shortest-path DAG no edge delta touches (the table screen

@@ -113,13 +113,22 @@ def nh_levels_bytes(csr, nbrs, nh_bytes, level_bytes=1, dist_rows=False):
 
 
 def msbfs_bytes(csr, nsrc, levels_per_batch, dist_rows=True):
-    """Compulsory bytes of one spf_msbfs_kernel launch: u8 level rows (and
-    u32 distance rows unless the next-hop pass writes them) written once,
-    the CSR read once per 64-source batch and level (each level is one pull
-    scan of the CSR for the whole batch)."""
+    """Compulsory HBM bytes of one spf_msbfs_kernel launch: u8 level rows (and
+    u32 distance rows unless the next-hop pass writes them) written once and
+    the CSR read once.  The per-level pull scans (one per 64-source batch and
+    level, bit-shared by the batch's sources) re-read the CSR from L2; they are
+    reported apart (msbfs_scan_bytes), never priced against HBM."""
     V = csr.num_nodes
     E = len(csr.col)
-    return int((5 if dist_rows else 1) * V * nsrc + sum(levels_per_batch) * (4 * E + 4 * (V + 1)))
+    return int((5 if dist_rows else 1) * V * nsrc + 4 * E + 4 * (V + 1))
+
+
+def msbfs_scan_bytes(csr, levels_per_batch):
+    """CSR bytes the bit-parallel pull scans read (L2-served): one scan per
+    64-source batch and BFS level."""
+    V = csr.num_nodes
+    E = len(csr.col)
+    return int(sum(levels_per_batch) * (4 * E + 4 * (V + 1)))
 
 
 def _profile_files(fname):
@@ -175,27 +184,30 @@ def pmc_traffic_largest(kernel_name):
     return None, None
 
 
-WHATIF_PMC_KERNELS = ("spf_sssp_kernel", "spf_whatif_screen_kernel", "spf_nh_narrow_kernel")
-
-
-def pmc_traffic_sum(kernel_names, fname):
-    """HBM bytes of one batch of a multi-kernel plan: the sum over its
-    kernels of (all dispatches' bytes / batches) from the newest committed
-    profiles/*/<fname> (a probe that ran only that plan, e.g.
-    profiles/whatif_probe.py)."""
-    files = _profile_files(fname)
-    for f in reversed(files):
+def pmc_plan_traffic(launched, fname):
+    """HBM bytes of one batch of a multi-kernel plan from the newest
+    committed profiles/*/<fname> whose kernel set (runtime copies / fills
+    aside) is EXACTLY `launched`, the kernels the plan that ran here launched
+    (spf_query_kernels): a profile of another plan is refused, not summed.
+    Returns (bytes per batch, file, note)."""
+    want = set(launched)
+    skipped = []
+    for f in reversed(_profile_files(fname)):
         try:
             d = json.load(open(f))
         except Exception:
             continue
         ks = d.get("kernels", {})
         runs = d.get("batches")
-        if not runs or not all(k in ks for k in kernel_names):
+        have = {k for k in ks if not k.startswith("__amd_rocclr")}
+        if not runs or have != want:
+            skipped.append(os.path.relpath(f, ROOT))
             continue
-        tot = sum(ks[k]["hbm_bytes_per_launch"] * ks[k]["dispatches"] for k in kernel_names)
-        return int(tot / runs), os.path.relpath(f, ROOT)
-    return None, None
+        tot = sum(ks[k]["hbm_bytes_per_launch"] * ks[k]["dispatches"] for k in want)
+        return int(tot / runs), os.path.relpath(f, ROOT), None
+    note = ("no committed PMC profile of this plan's kernel set "
+            f"{sorted(want)}" + (f" (refused: {', '.join(skipped)})" if skipped else ""))
+    return None, None, note
 
 
 def pmc_traffic_smallest(kernel_name):
@@ -613,6 +625,7 @@ def route_db_link_flap(topo, device, iters=4):
     n = max(1, c.get("decision.route_build_runs", 1))
     out["per_build_us"] = {k.split(".", 1)[1]: round(c.get(k, 0) / n, 1)
                            for k in ("decision.graph_build_us", "decision.graph_upload_us",
+                                     "decision.graph_patch_us", "decision.graph_update_us", "decision.graph_splice_us", "decision.graph_memo_screen_us",
                                      "decision.spf_batch_us", "decision.spf_device_us",
                                      "decision.route_prefetch_us", "decision.route_prefix_pool_us")}
     out["node"] = "2-0-0"
@@ -930,6 +943,7 @@ def whatif_batch(world, rank, local, dist, steps=3, cpu_lines=True):
                         bad += d[v] != np.uint64(abi.SPF_UNREACHABLE)
         check = "ok" if bad == 0 else f"{bad} mismatches"
     kernels = sorted({q.kernel for q in queries})
+    launched = sorted(set().union(*(set(q.kernels()) for q in queries)))
     # algorithmic bytes of the batch (both areas): every query's u32
     # distance row and byte-strided mask row written once (SPF_NH_BYTES of
     # the source), plus the baseline SSSP of each area (its CSR read once:
@@ -948,8 +962,9 @@ def whatif_batch(world, rank, local, dist, steps=3, cpu_lines=True):
     gbs = alg / (dev_ms / 1e3) / 1e9 if dev_ms > 0 else 0.0
     wi_traffic = None
     wi_src = None
+    wi_note = None
     if world == 1:
-        wi_traffic, wi_src = pmc_traffic_sum(WHATIF_PMC_KERNELS, "pmc_whatif.json")
+        wi_traffic, wi_src, wi_note = pmc_plan_traffic(launched, "pmc_whatif.json")
     for q in queries:
         q.close()
     for _, g, _ in graphs:
@@ -984,13 +999,15 @@ def whatif_batch(world, rank, local, dist, steps=3, cpu_lines=True):
         "value": round(len(allq) / (ms / 1e3), 1), "unit": "SPF/s",
         "parity_check": check,
         "screened_queries": screened,
-        "roofline": {"bound": "hbm", "kernel": "what-if plan (base SSSP + spf_whatif_screen_kernel + "
-                     "spf_sssp_kernel repair + spf_nh_narrow_kernel)",
+        "kernels_launched": launched,
+        "roofline": {"bound": "hbm", "kernel": "what-if plan: " + " + ".join(launched),
                      "note": "latency-bound: the per-area baseline SSSP runs on one workgroup before "
                              "the batch can start", "algorithmic_bytes": int(alg),
                      "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": wi_traffic,
-                     "traffic_source": wi_src},
+                     "traffic_source": wi_src,
+                     "traffic_over_algorithmic": round(wi_traffic / alg, 3) if wi_traffic and alg else None,
+                     **({"traffic_note": wi_note} if wi_note else {})},
         **({"cpu_baseline_optimised_all_cores": cpu} if cpu else {}),
     }
 
@@ -1128,8 +1145,8 @@ def wan_all_sources_table(args, world, rank, local, dist, cluster):
         "gather_algbw_gbs": round(V * V * 4 / (gather_ms / 1e3) / 1e9, 1) if world > 1 and gather_ms else None,
         "roofline": {"bound": "hbm", "kernel": kdesc,
                      "algorithmic_bytes_per_sssp": per_sssp,
-                     "algorithmic_achieved": round(V * per_sssp / (comp_ms / 1e3) / 1e9 / world, 1),
-                     "algorithmic_frac": round(V * per_sssp / (comp_ms / 1e3) / 1e9 / world / HBM_PEAK_GBS, 4),
+                     "achieved": round(V * per_sssp / (comp_ms / 1e3) / 1e9 / world, 1),
+                     "frac": round(V * per_sssp / (comp_ms / 1e3) / 1e9 / world / HBM_PEAK_GBS, 4),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "note": "per GPU"},
         "parity_check": check,
         "generate_s": round(gen_s, 1),
@@ -1255,17 +1272,20 @@ def wan_all_sources(args, world, rank, local, dist):
                      # SURVEY §8(d) per-SSSP figure without masks: CSR of every settled
                      # node read once (in the format the kernel reads) + the distance
                      # row written once
+                     # same keys as the headline: achieved / frac = ALGORITHMIC bytes
+                     # per live kernel time; traffic_* = PMC bytes (2*FETCH_SIZE +
+                     # WRITE_SIZE of the one-GPU 100k-source launch)
                      "algorithmic_bytes_per_sssp": per_sssp,
-                     "algorithmic_achieved": round(achieved, 1) if achieved else None,
-                     "algorithmic_frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                     "achieved": round(achieved, 1) if achieved else None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     # PMC bytes of the one-GPU 100k-source launch (2*FETCH_SIZE + WRITE_SIZE)
                      "traffic_per_sssp": (traffic // 100000) if traffic else None,
-                     "achieved": round(traffic / 100000 * sas.count / kernel_s / 1e9, 1)
+                     "traffic_achieved": round(traffic / 100000 * sas.count / kernel_s / 1e9, 1)
                      if traffic and kernel_s else None,
-                     "frac": round(traffic / 100000 * sas.count / kernel_s / 1e9 / HBM_PEAK_GBS, 4)
+                     "traffic_frac": round(traffic / 100000 * sas.count / kernel_s / 1e9 / HBM_PEAK_GBS, 4)
                      if traffic and kernel_s else None,
-                     "basis": "PMC HBM bytes per SSSP x SSSPs / live kernel time",
+                     "traffic_over_algorithmic": round(traffic / 100000 / per_sssp, 3)
+                     if traffic and per_sssp else None,
                      "traffic_source": traffic_src},
         "parity_check": check,
         "generate_s": round(gen_s, 1),
@@ -1650,6 +1670,12 @@ def fabric_single(args, topo, world, rank, local, dist):
         "avg_ms": round(d_ms, 4),
         "algorithmic_bytes": msbfs_bytes(csr, nsrc, levels, dist_rows=not lo) if levels else None,
     }
+    if levels:
+        # the bit-shared pull scans: one CSR scan per batch and level serves
+        # 64 sources, served from L2 (not HBM traffic)
+        sb = msbfs_scan_bytes(csr, levels)
+        stages[dist_k]["csr_scan_bytes_l2"] = sb
+        stages[dist_k]["csr_scan_gbs_l2"] = round(sb / (d_ms / 1e3) / 1e9, 1) if d_ms else None
     dom = max(stages, key=lambda k: stages[k]["avg_ms"])
     dom_bytes = stages[dom]["algorithmic_bytes"]
     dom_ms = stages[dom]["avg_ms"]
@@ -1704,6 +1730,9 @@ def fabric_single(args, topo, world, rank, local, dist):
             "parallelism": f"source-batch per GPU, drain scenario per rank (x{world})",
         },
         "gteps": round(world * nsrc * E / (step_ms / 1000.0) / 1e9, 2),
+        "gteps_note": "per-source-equivalent: sources x directed edges per step time (each SSSP "
+                      "traverses every edge once); the bit-parallel BFS scans an edge once per "
+                      "level for 64 sources, so this counts shared scans, not memory traffic",
         "kernel_ms": round(kernel_ms, 4),
         "kernels": stages,
         "parity_spot_check": check,

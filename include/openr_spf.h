@@ -137,6 +137,13 @@ int spf_graph_patch_metrics(
 int spf_graph_set_edges(
     spf_graph* g, uint32_t n, const uint32_t* edge_idx, const uint8_t* up,
     const uint64_t* metric);
+/* Rebuild the graph in place from a new CSR of the same node set (a link
+ * added or removed: LinkState::updateAdjacencyDatabase's structural changes,
+ * LinkState.cpp:421-434 / :564-717) without a new handle: same device and
+ * stream, device buffers reused where they fit.  SPF_E_INVALID while a query
+ * of the graph is alive or when num_nodes differs.  On any other failure the
+ * graph is left unusable: destroy it. */
+int spf_graph_update(spf_graph* g, const spf_graph_desc* desc);
 /* Work of this graph is enqueued on `stream` (a hipStream_t, NULL = the
  * graph's own stream). */
 int spf_graph_set_stream(spf_graph* g, void* stream);
@@ -176,6 +183,12 @@ int spf_query_screened(spf_query* q, uint32_t* screened, uint32_t* has_screen);
 /* Name of the plan the last run used ("lds", "dstep", "msbfs+levels", "wide",
  * "exact", ...). */
 const char* spf_query_kernel_name(const spf_query* q);
+/* The HIP kernels the last run launched (its sub-queries' included), sorted
+ * and comma-separated, as rocprofv3 names them without template arguments;
+ * writes at most cap - 1 bytes and a NUL into buf (may be NULL) and returns
+ * the full length, or a negative status.  Lets a measurement check that a
+ * profile was taken of the same plan. */
+int spf_query_kernels(const spf_query* q, char* buf, size_t cap);
 
 /* Distances of query i, one per node; SPF_UNREACHABLE = not reached. */
 int spf_query_dist(spf_query* q, uint32_t i, uint64_t* out /*[V]*/);

@@ -39,6 +39,7 @@ EXPORTED_SYMBOLS = (
     "spf_device_memcpy",
     "spf_graph_create",
     "spf_graph_destroy",
+    "spf_graph_update",
     "spf_graph_set_transit",
     "spf_graph_patch_metrics",
     "spf_graph_set_edges",
@@ -56,6 +57,7 @@ EXPORTED_SYMBOLS = (
     "spf_query_stage_history",
     "spf_query_screened",
     "spf_query_kernel_name",
+    "spf_query_kernels",
     "spf_query_dist",
     "spf_query_nh_words",
     "spf_query_nh_bytes",
@@ -237,6 +239,7 @@ def load():
         "spf_device_free": (C.c_int, [C.c_int, vp]),
         "spf_device_memcpy": (C.c_int, [C.c_int, vp, vp, C.c_size_t, C.c_int]),
         "spf_graph_destroy": (C.c_int, [vp]),
+        "spf_graph_update": (C.c_int, [vp, C.POINTER(_GraphDesc)]),
         "spf_graph_set_transit": (C.c_int, [vp, C.POINTER(C.c_uint8)]),
         "spf_graph_patch_metrics": (C.c_int, [vp, u32, pu32, pu64]),
         "spf_graph_set_edges": (C.c_int, [vp, u32, pu32, C.POINTER(C.c_uint8), pu64]),
@@ -260,6 +263,7 @@ def load():
             [vp, u32, C.POINTER(C.c_float), C.POINTER(C.c_float), pu32],
         ),
         "spf_query_kernel_name": (C.c_char_p, [vp]),
+        "spf_query_kernels": (C.c_int, [vp, C.c_char_p, C.c_size_t]),
         "spf_query_dist": (C.c_int, [vp, u32, pu64]),
         "spf_query_nh_words": (C.c_int, [vp, u32]),
         "spf_query_nh_bytes": (C.c_int, [vp, u32]),
@@ -458,6 +462,14 @@ class Graph:
         _check(load().spf_graph_patch_metrics(self.h, len(e), _p(e, C.c_uint32), _p(m, C.c_uint64)),
                "patch_metrics")
 
+    def update(self, csr: "Csr"):
+        """Rebuild in place from a new CSR of the same node set
+        (spf_graph_update); no query of this graph may be alive."""
+        d, keep = _graph_desc(csr, 0)
+        _check(load().spf_graph_update(self.h, C.byref(d)), "spf_graph_update")
+        self.csr = csr
+        self._keep = keep
+
     def set_stream(self, stream_ptr: int | None):
         _check(load().spf_graph_set_stream(self.h, stream_ptr), "set_stream")
 
@@ -620,6 +632,15 @@ class Query:
     @property
     def kernel(self) -> str:
         return load().spf_query_kernel_name(self.h).decode()
+
+    def kernels(self) -> list:
+        """The HIP kernels the last run launched (spf_query_kernels)."""
+        lib = load()
+        n = lib.spf_query_kernels(self.h, None, 0)
+        _check(min(n, 0), "spf_query_kernels")
+        buf = C.create_string_buffer(n + 1)
+        lib.spf_query_kernels(self.h, buf, n + 1)
+        return [k for k in buf.value.decode().split(",") if k]
 
     def dist(self, i: int) -> np.ndarray:
         out = np.zeros(self.graph.V, dtype=np.uint64)

@@ -90,7 +90,9 @@ def build_decision(force=False):
     """libopenr_decision.so (host layer) and the standalone consumer."""
     r = recipe()
     hdrs = sorted(glob.glob(os.path.join(CSRC, "host", "*.h"))) + [os.path.join(INC, "openr_spf.h")]
-    if force or _newer(DECISION, _recipe_sources(r["host"]) + hdrs + [LIB]):
+    # linked dynamically against the engine: a rebuilt libopenr_spf.so with the
+    # same header needs no relink
+    if force or _newer(DECISION, _recipe_sources(r["host"]) + hdrs):
         _run(r["host"])
     if force or _newer(CONSUMER, _recipe_sources(r["consumer"]) + hdrs + [DECISION]):
         _run(r["consumer"])
@@ -102,7 +104,7 @@ def build_host(force=False):
 
     hdrs = sorted(glob.glob(os.path.join(CSRC, "host", "*.h")))
     bind = os.path.join(CSRC, "py", "bindings.cpp")
-    if force or _newer(EXT, hdrs + [bind, LIB, DECISION, os.path.join(INC, "openr_spf.h")]):
+    if force or _newer(EXT, hdrs + [bind, os.path.join(INC, "openr_spf.h")]):
         _run(
             [
                 os.environ.get("CXX", "g++"),

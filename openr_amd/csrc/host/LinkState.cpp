@@ -1472,8 +1472,8 @@ void LinkState::patchMemo(
 // ids are name ranks and the node set is unchanged).  Link ids of links that
 // stay are kept (a removed link's id is freed, a new link takes a free id or
 // the next one), so the Link tags stay valid; half-edge indices of the kept
-// rows shift by their row's offset change.  The device graph is recreated
-// from the spliced arrays; SPF memos survive where no edge delta can touch
+// rows shift by their row's offset change.  The device graph is rebuilt in
+// place from the spliced arrays (spf_graph_update); SPF memos survive where no edge delta can touch
 // them (the same screen as patchMemo).  Returns false (nothing changed) when
 // a link's endpoint is not a node of the graph, or the engine is not built.
 bool LinkState::patchStructure(
@@ -1693,10 +1693,22 @@ bool LinkState::patchStructure(
   d.node_overloaded = overloaded.data();
   d.num_links = (uint32_t)links.size();
   d.device = getSpfDevice();
-  spf_graph* g = nullptr;
-  if (spf_graph_create(&d, &g) != SPF_OK) {
+  // the device graph is rebuilt in place (same handle, stream and buffers:
+  // spf_graph_update).  A failed update leaves it unusable: it is dropped,
+  // and the caller's clearMemo() retires the engine, whose next build
+  // creates a fresh graph
+  const auto tu = std::chrono::steady_clock::now();
+  Counters::add("decision.graph_splice_us",
+                std::chrono::duration_cast<std::chrono::microseconds>(tu - t0).count());
+  if (spf_graph_update(eng.graph, &d) != SPF_OK) {
+    spf_graph_destroy(eng.graph);
+    eng.graph = nullptr;
     return false;
   }
+  Counters::add("decision.graph_update_us",
+                std::chrono::duration_cast<std::chrono::microseconds>(
+                    std::chrono::steady_clock::now() - tu)
+                    .count());
   // commit
   ++topoGen_;
   spfResultsMetric_.clear();
@@ -1709,8 +1721,6 @@ bool LinkState::patchStructure(
     l->engineEpoch = eng.epoch;
     l->engineId = lid;
   }
-  spf_graph_destroy(eng.graph);
-  eng.graph = g;
   if (eng.cgraph) {
     spf_cgraph_destroy(eng.cgraph);
     eng.cgraph = nullptr;
@@ -1727,11 +1737,16 @@ bool LinkState::patchStructure(
   eng.freeIds = std::move(freeIds);
   eng.exact = spf_graph_needs_exact(eng.graph) != 0;
   if (memoScreenEnabled() && !eng.exact) {
+    const auto ts = std::chrono::steady_clock::now();
     for (int k = 0; k < 2; ++k) {
       std::remove_reference_t<decltype(eng.memo[0])> keep;
       screenMemo(eng.memo[k], keep, k ? dMetric : dHops);
       eng.memo[k] = std::move(keep);
     }
+    Counters::add("decision.graph_memo_screen_us",
+                  std::chrono::duration_cast<std::chrono::microseconds>(
+                      std::chrono::steady_clock::now() - ts)
+                      .count());
   } else {
     eng.memo[0].clear();
     eng.memo[1].clear();

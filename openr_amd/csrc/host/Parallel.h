@@ -8,10 +8,16 @@
 // fixed order; nothing observable depends on which thread ran which item.
 #pragma once
 
+#include <pthread.h>
+
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <cstdint>
 #include <cstdlib>
 #include <exception>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -29,6 +35,99 @@ inline unsigned hostThreads(size_t n, size_t minPerThread = 64) {
   const size_t cap = std::max<size_t>(1, n / std::max<size_t>(1, minPerThread));
   return (unsigned)std::min<size_t>(t, cap);
 }
+
+// Persistent workers: a parallel section used to start and join fresh
+// std::threads (~30-50 us each), which on a RouteDb build (three sections of
+// up to 16 threads) and a graph rebuild (five) cost more than the work.  One
+// section runs at a time; a section started while another runs (from another
+// host thread) or from inside a worker falls back to fresh threads.  The pool
+// is never destroyed (its detached workers park on a condition variable); a
+// forked child starts a new, empty one.  OPENR_HOST_POOL=0: fresh threads.
+class HostPool {
+ public:
+  static HostPool& get() {
+    static const bool init = [] {
+      pthread_atfork(nullptr, nullptr, [] { instance() = new HostPool(); });
+      instance() = new HostPool();
+      return true;
+    }();
+    (void)init;
+    return *instance();
+  }
+
+  // body(w) for w in [0, threads): w = 0 on the calling thread.  false: the
+  // pool is busy (or this is a worker): the caller runs the section itself.
+  bool run(unsigned threads, const std::function<void(unsigned)>& body) {
+    static const bool enabled = [] {
+      const char* e = std::getenv("OPENR_HOST_POOL");
+      return !(e && std::atoi(e) == 0);
+    }();
+    if (!enabled || inWorker() || threads <= 1) {
+      return false; // (inWorker: also the calling thread of a running section)
+    }
+    std::unique_lock<std::mutex> job(jobMu_, std::try_to_lock);
+    if (!job.owns_lock()) {
+      return false;
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      while (nworkers_ + 1 < threads) {
+        const unsigned id = ++nworkers_;
+        std::thread([this, id] { loop(id); }).detach();
+      }
+      body_ = &body;
+      want_ = threads - 1;
+      pending_ = threads - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    inWorker() = true; // a nested section on this thread starts fresh threads
+    body(0);
+    inWorker() = false;
+    std::unique_lock<std::mutex> l(mu_);
+    done_.wait(l, [this] { return pending_ == 0; });
+    body_ = nullptr;
+    return true;
+  }
+
+ private:
+  static HostPool*& instance() {
+    static HostPool* p = nullptr;
+    return p;
+  }
+  static bool& inWorker() {
+    static thread_local bool w = false;
+    return w;
+  }
+  void loop(unsigned id) {
+    inWorker() = true;
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(unsigned)>* body;
+      {
+        std::unique_lock<std::mutex> l(mu_);
+        cv_.wait(l, [&] { return gen_ != seen && id <= want_; });
+        seen = gen_;
+        body = body_;
+      }
+      (*body)(id);
+      {
+        std::lock_guard<std::mutex> l(mu_);
+        if (--pending_ == 0) {
+          done_.notify_one();
+        }
+      }
+    }
+  }
+
+  std::mutex jobMu_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  unsigned nworkers_ = 0;
+  const std::function<void(unsigned)>* body_ = nullptr;
+  unsigned want_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+};
 
 // fn(item, worker) for item in [0, n), chunks handed out dynamically.  The
 // first exception (by worker index) is rethrown after every worker joined.
@@ -59,14 +158,17 @@ void parallelFor(size_t n, unsigned threads, Fn&& fn, size_t chunk = 16) {
       next.store(n); // stop handing out work
     }
   };
-  std::vector<std::thread> pool;
-  pool.reserve(threads - 1);
-  for (unsigned w = 1; w < threads; ++w) {
-    pool.emplace_back(body, w);
-  }
-  body(0);
-  for (auto& t : pool) {
-    t.join();
+  const std::function<void(unsigned)> job(body);
+  if (!HostPool::get().run(threads, job)) {
+    std::vector<std::thread> pool;
+    pool.reserve(threads - 1);
+    for (unsigned w = 1; w < threads; ++w) {
+      pool.emplace_back(body, w);
+    }
+    body(0);
+    for (auto& t : pool) {
+      t.join();
+    }
   }
   for (auto& e : errors) {
     if (e) {

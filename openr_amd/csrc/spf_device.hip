@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cstdint>
 #include <cstdio>
@@ -64,13 +65,33 @@ struct AbiRange {
 } // namespace
 #define SPF_ABI_RANGE(name) AbiRange spf_abi_range_(name)
 
+// The kernels the running query launched (spf_query_kernels): every launch
+// site goes through SPF_LAUNCH, which notes the kernel expression while a
+// spf_query_run is active on this thread (sub-queries of a plan — a what-if
+// baseline, the zero-metric fix-up — land in the outermost query's list).
+namespace {
+thread_local std::vector<const char*>* tl_launched = nullptr;
+inline void spf_note_launch(const char* expr) {
+  if (tl_launched && std::find(tl_launched->begin(), tl_launched->end(), expr) == tl_launched->end()) {
+    tl_launched->push_back(expr);
+  }
+}
+} // namespace
+#define SPF_LAUNCH(kern, ...)           \
+  do {                                  \
+    spf_note_launch(#kern);             \
+    hipLaunchKernelGGL(kern, __VA_ARGS__); \
+  } while (0)
+
 namespace {
 
 constexpr uint32_t kBlock = 512;           // threads per workgroup (8 waves)
 constexpr uint32_t kWaves = kBlock / 64;
 constexpr uint32_t kInf32 = 0xFFFFFFFFu;
 // nodes per host-pool work item of the graph preparation loops
-constexpr uint32_t kHostBlock = 2048;
+constexpr uint32_t kHostBlock = 512;
+// host passes over the CSR go parallel from this many edges per thread
+constexpr size_t kHostMinEdges = 1u << 14;
 constexpr uint32_t kCtlWords = 32;         // qlen + scan scratch (<= 16 waves + 1)
 constexpr size_t kLdsLimit = 160 * 1024;   // gfx950 LDS per CU
 constexpr uint32_t kIgnLdsMax = 2048;      // ignore-list entries staged in LDS
@@ -3852,9 +3873,20 @@ struct NlV2Args {
   const NlMem* mem;
   const NlEnt* ent;
   uint32_t nsolo, nsub;
+  // bytes of the level table (< 2^31: the kernel's buffer descriptor)
+  uint32_t lvl_bytes;
   // measurement only (OPENR_NL_V2_DBG): bit 0 skips the solo items, bit 1 the
   // groups, bit 2 computes without storing (the results stay live)
   uint32_t dbg;
+  // block order (OPENR_NL_V2_ORDER): 0 = all solo items chunk-major, then
+  // all groups; 1 = chunk-major over both kinds (chunk c: its solo items,
+  // then its groups); 2 = order 1 with XCD-contiguous logical ranges, so an
+  // XCD sweeps ~1/8 of the chunks and the level-row slices its blocks read
+  // stay in its L2 (round-robin dealing makes every XCD fetch every row);
+  // 3 = chunk-major with the chunk's solo and group items interleaved in
+  // proportion, so VALU-heavy solo blocks and store-heavy group blocks are
+  // resident together
+  uint32_t order;
 };
 constexpr uint32_t kNlGS = 8;  // sources per group block
 constexpr uint32_t kNlGN = 16; // neighbours of a group source (one mask word, B <= 2)
@@ -3863,44 +3895,96 @@ __device__ __forceinline__ bool nl_transit(const uint32_t* trbits, uint32_t f) {
   return (trbits[f >> 5] >> (f & 31)) & 1u;
 }
 
-// the eight level words of group g (neighbours 8g .. 8g+7 of the word whose
-// entries lane j holds in `er`); missing neighbours read as 0xFF bytes, which
-// match no live node
-__device__ __forceinline__ void nl_v2_ld8(const uint8_t* lvl, uint32_t Vp8, uint32_t v0,
-                                          bool active, uint32_t er, uint32_t g, uint32_t cnt,
-                                          uint32_t (&lf)[8]) {
+// Level words of neighbours base .. base+7 of a source (entries e[base ..]):
+// the entries are wave-uniform, so they arrive by scalar loads (the list is
+// padded by 64 entries, so reading past its end is safe) and the row offsets
+// are scalar products; missing neighbours read as 0xFF bytes, which match no
+// live node.
+// A level word through the level table's buffer descriptor: the row offset
+// is a scalar (SGPR soffset) and the lane's node offset a 32-bit voffset, so
+// a load costs no vector address arithmetic (the 64-bit per-lane address of
+// a global load was ~20 % of the pass's VALU instructions, profiles/r05k);
+// reads past the table return 0 (hardware bounds check).
+__device__ __forceinline__ uint32_t nl_lvl_word(__amdgpu_buffer_rsrc_t rs, uint32_t v0,
+                                                uint32_t rowoff) {
+  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)v0, (int)rowoff, 0);
+}
+
+__device__ __forceinline__ void nl_v3_ld8(__amdgpu_buffer_rsrc_t rs, uint32_t v0, uint32_t Vp8,
+                                          const NlEnt* e, uint32_t rem, uint32_t (&lf)[8]) {
+  uint32_t r[8];
+#pragma unroll
+  for (uint32_t kk = 0; kk < 8; ++kk) {
+    r[kk] = __builtin_amdgcn_readfirstlane(e[kk].row);
+  }
 #pragma unroll
   for (uint32_t kk = 0; kk < 8; ++kk) {
     lf[kk] = 0xFFFFFFFFu;
-    const uint32_t j = 8 * g + kk;
-    if (j < cnt) {
-      const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)er, (int)j);
-      if (active) {
-        lf[kk] = *reinterpret_cast<const uint32_t*>(lvl + (size_t)r * Vp8 + v0);
-      }
+    if (kk < rem) {
+      lf[kk] = nl_lvl_word(rs, v0, r[kk] * Vp8);
     }
   }
 }
 
-__device__ __forceinline__ void nl_v2_cmp8(const uint32_t (&lf)[8], uint32_t tgt, uint32_t live,
-                                           uint32_t ntg, uint32_t er_node, uint32_t g,
-                                           uint32_t v0, uint32_t& P) {
+// SWAR compares of eight neighbours' level words against the source's
+// (tgt = level - 1 bytewise, live = not the source, not unreached): the 0x80
+// of a matching byte lands in bit kk of that byte of P.  Drained neighbours
+// (bit kk of ntg) match only their own node.
+__device__ __forceinline__ uint32_t nl_v3_cmp8(const uint32_t (&lf)[8], uint32_t tgt,
+                                               uint32_t live, uint32_t ntg, const NlEnt* e,
+                                               uint32_t v0) {
+  uint32_t P = 0;
 #pragma unroll
   for (uint32_t kk = 0; kk < 8; ++kk) {
     uint32_t m = live & swar_zero_bytes(lf[kk] ^ tgt);
     if ((ntg >> kk) & 1u) {
-      // a drained neighbour is a next hop only to itself
-      const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)er_node, (int)(8 * g + kk));
-      const uint32_t r = f - v0;
+      const uint32_t r = __builtin_amdgcn_readfirstlane(e[kk].node) - v0;
       m &= r < 4u ? (0x80u << (8u * r)) : 0u;
     }
-    P |= m >> (7u - kk);
+    P = (P >> 1) | m; // neighbour kk's flag ends at bit kk after the eight steps
+  }
+  return P;
+}
+
+// Mask rows of B = 8 * Wm bytes per node, one wave's 256 nodes: a lane holds
+// 4 consecutive nodes (32 * Wm contiguous bytes), so storing from registers
+// puts 16-byte pieces 32 * Wm bytes apart in every wave instruction (partial
+// cache lines; measured 1.9 TB/s against 4 TB/s for the coalesced distance
+// rows, profiles/r05j).  The wave's tile goes through its LDS slice instead
+// and leaves as 16 bytes per lane, 1 KB contiguous per instruction.  Every
+// lane of the wave calls it.
+__device__ __forceinline__ void nl_store_wide(uint8_t* row, uint32_t vbase, uint32_t V,
+                                              uint32_t Wm, const uint64_t (&held)[kNsHeldMax][4],
+                                              uint64_t* tile, uint32_t lane) {
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i) {
+#pragma unroll
+    for (uint32_t w = 0; w < kNsHeldMax; ++w) {
+      if (w < Wm) {
+        tile[(4 * lane + i) * Wm + w] = held[w][i];
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint32_t bytes = min(256u, V - vbase) * 8 * Wm;
+  uint8_t* dst = row + (size_t)vbase * 8 * Wm;
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(tile);
+  for (uint32_t j = 0; j < 2 * Wm; ++j) {
+    const uint32_t off = j * 1024 + 16 * lane;
+    if (off + 16 <= bytes) {
+      *reinterpret_cast<uint4*>(dst + off) = *reinterpret_cast<const uint4*>(src + off);
+    } else if (off < bytes) { // bytes is a multiple of 8
+      *reinterpret_cast<uint2*>(dst + off) = *reinterpret_cast<const uint2*>(src + off);
+    }
   }
 }
 
 template <uint32_t T>
 __device__ __forceinline__ void nl_v2_solo(const NhLevelsArgs& a, const NlV2Args& v,
-                                           uint32_t k, uint32_t c) {
+                                           uint32_t k, uint32_t c, uint64_t* tile,
+                                           __amdgpu_buffer_rsrc_t rs) {
   const NlSolo d = v.solo[k];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t vbase = c * (4 * T) + wv * 256;
@@ -3909,55 +3993,96 @@ __device__ __forceinline__ void nl_v2_solo(const NhLevelsArgs& a, const NlV2Args
   }
   const uint32_t v0 = vbase + 4 * lane;
   const bool active = v0 < a.V;
-  // every lane takes part in the entry loads (readlane reads lanes, not EXEC)
-  NlEnt e[kNsHeldMax];
+  const uint8_t* lvl_v0 = a.lvl + v0;
+  const NlEnt* ent = v.ent + d.lo;
+  if (v.dbg & 8u) {
+    // measurement: the pass's stores alone (same addresses, no loads)
+    if (!active) {
+      return;
+    }
+    uint64_t x4[4] = {v0, v0 + 1, v0 + 2, v0 + 3};
+    if (a.dist_w && !(v.dbg & 16u)) {
+      nl_dist_from_levels(a, d.q, v0, 0x01010101u * (v0 & 7u));
+    }
+    uint8_t* nb = a.nhb + d.nhb_off;
+    if (v.dbg & 32u) {
+    } else if (d.B < 8) {
+      nh_store4_narrow(nb, d.B, v0, a.V, x4);
+    } else if (v.dbg & 64u) { // the register-layout stores (before LDS staging)
+      uint64_t* nr = reinterpret_cast<uint64_t*>(nb);
+      for (uint32_t w = 0; w < d.Wm; ++w) {
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {
+          if (v0 + i < a.V) {
+            nr[(size_t)(v0 + i) * d.Wm + w] = x4[i];
+          }
+        }
+      }
+    }
+    return;
+  }
+  if ((v.dbg & 8u) && !(v.dbg & 32u) && d.B >= 8 && !(v.dbg & 64u)) {
+    uint64_t hx[kNsHeldMax][4];
+#pragma unroll
+    for (uint32_t w = 0; w < kNsHeldMax; ++w) {
+#pragma unroll
+      for (uint32_t i = 0; i < 4; ++i) {
+        hx[w][i] = v0 + i + w;
+      }
+    }
+    nl_store_wide(a.nhb + d.nhb_off, vbase, a.V, d.Wm, hx, tile, lane);
+    return;
+  }
+  // drained neighbours: lane j tests entry 64w + j (every lane takes part)
+  uint64_t ntm[kNsHeldMax];
 #pragma unroll
   for (uint32_t w = 0; w < kNsHeldMax; ++w) {
-    e[w] = NlEnt{0u, 0u};
+    bool nt = false;
     if (w < d.Wm && 64 * w + lane < d.n) {
-      e[w] = v.ent[d.lo + 64 * w + lane];
+      nt = !nl_transit(a.trbits, ent[64 * w + lane].node);
     }
+    ntm[w] = __ballot(nt);
   }
-  const uint32_t ls =
-      active ? *reinterpret_cast<const uint32_t*>(a.lvl + (size_t)d.q * a.Vp8 + v0) : 0xFFFFFFFFu;
+  const uint32_t ls = active ? nl_lvl_word(rs, v0, d.q * a.Vp8) : 0xFFFFFFFFu;
   const uint32_t tgt = ((ls | 0x80808080u) - 0x01010101u) ^ (~ls & 0x80808080u);
   const uint32_t live = 0x80808080u & ~(swar_zero_bytes(ls) | swar_zero_bytes(~ls));
   uint64_t held[kNsHeldMax][4];
+#pragma unroll 1
+  for (uint32_t w = 0; w < d.Wm; ++w) {
+    const uint32_t cnt = min(64u, d.n - min(d.n, 64 * w));
+    const uint64_t ntmask = w == 0 ? ntm[0] : (w == 1 ? ntm[1] : ntm[2]);
+    const NlEnt* ew = ent + 64 * w;
+    uint32_t P[8];
+    uint32_t A[8], Bq[8];
+    nl_v3_ld8(rs, v0, a.Vp8, ew, cnt, A);
 #pragma unroll
-  for (uint32_t w = 0; w < kNsHeldMax; ++w) {
-    if (w < d.Wm) {
-      const uint32_t cnt = min(64u, d.n - min(d.n, 64 * w));
-      uint32_t P[8];
-      uint32_t A[8], Bq[8];
-      nl_v2_ld8(a.lvl, a.Vp8, v0, active, e[w].row, 0, cnt, A);
-      const uint64_t ntmask = __ballot(64 * w + lane < d.n && !nl_transit(a.trbits, e[w].node));
-#pragma unroll
-      for (uint32_t g = 0; g < 8; ++g) {
-        P[g] = 0;
-        if (8 * g < cnt) {
-          // the next group's loads go out before this group's compares
-          if (g + 1 < 8 && 8 * (g + 1) < cnt) {
-            if (g & 1u) {
-              nl_v2_ld8(a.lvl, a.Vp8, v0, active, e[w].row, g + 1, cnt, A);
-            } else {
-              nl_v2_ld8(a.lvl, a.Vp8, v0, active, e[w].row, g + 1, cnt, Bq);
-            }
+    for (uint32_t g = 0; g < 8; ++g) {
+      P[g] = 0;
+      if (8 * g < cnt) {
+        // the next group's loads go out before this group's compares
+        if (g + 1 < 8 && 8 * (g + 1) < cnt) {
+          if (g & 1u) {
+            nl_v3_ld8(rs, v0, a.Vp8, ew + 8 * (g + 1), cnt - 8 * (g + 1), A);
+          } else {
+            nl_v3_ld8(rs, v0, a.Vp8, ew + 8 * (g + 1), cnt - 8 * (g + 1), Bq);
           }
-          const uint32_t ntg = (uint32_t)(ntmask >> (8 * g)) & 0xFFu;
-          nl_v2_cmp8((g & 1u) ? Bq : A, tgt, live, ntg, e[w].node, g, v0, P[g]);
         }
-      }
-      uint32_t lo[4], hi[4];
-      swar_transpose4(P[0], P[1], P[2], P[3], lo);
-      swar_transpose4(P[4], P[5], P[6], P[7], hi);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        held[w][i] = ((uint64_t)hi[i] << 32) | lo[i];
+        const uint32_t ntg = (uint32_t)(ntmask >> (8 * g)) & 0xFFu;
+        P[g] = nl_v3_cmp8((g & 1u) ? Bq : A, tgt, live, ntg, ew + 8 * g, v0);
       }
     }
-  }
-  if (!active) {
-    return;
+    uint32_t lo[4], hi[4];
+    swar_transpose4(P[0], P[1], P[2], P[3], lo);
+    swar_transpose4(P[4], P[5], P[6], P[7], hi);
+#pragma unroll
+    for (uint32_t ww = 0; ww < kNsHeldMax; ++ww) {
+      if (ww == w) { // static register indices
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          held[ww][i] = ((uint64_t)hi[i] << 32) | lo[i];
+        }
+      }
+    }
   }
   if (v.dbg & 4u) {
     uint64_t x = 0;
@@ -3969,10 +4094,20 @@ __device__ __forceinline__ void nl_v2_solo(const NhLevelsArgs& a, const NlV2Args
       return; // measurement: no stores
     }
   }
+  uint8_t* nhrow_b = a.nhb + d.nhb_off;
+  if (d.B >= 8 && !(v.dbg & 64u)) {
+    nl_store_wide(nhrow_b, vbase, a.V, d.Wm, held, tile, lane); // every lane
+    if (active && a.dist_w) {
+      nl_dist_from_levels(a, d.q, v0, ls);
+    }
+    return;
+  }
+  if (!active) {
+    return;
+  }
   if (a.dist_w) {
     nl_dist_from_levels(a, d.q, v0, ls);
   }
-  uint8_t* nhrow_b = a.nhb + d.nhb_off;
   uint64_t* nhrow = reinterpret_cast<uint64_t*>(nhrow_b);
   const uint32_t Wm = d.Wm;
   if (d.B < 8) {
@@ -4012,7 +4147,8 @@ __device__ __forceinline__ void nl_v2_solo(const NhLevelsArgs& a, const NlV2Args
 
 template <uint32_t T>
 __device__ __forceinline__ void nl_v2_group(const NhLevelsArgs& a, const NlV2Args& v,
-                                            uint32_t k, uint32_t c) {
+                                            uint32_t k, uint32_t c,
+                                            __amdgpu_buffer_rsrc_t rs) {
   const NlSub d = v.subs[k];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t vbase = c * (4 * T) + wv * 256;
@@ -4021,43 +4157,64 @@ __device__ __forceinline__ void nl_v2_group(const NhLevelsArgs& a, const NlV2Arg
   }
   const uint32_t v0 = vbase + 4 * lane;
   const bool active = v0 < a.V;
-  NlEnt e{0u, 0u};
+  const uint8_t* lvl_v0 = a.lvl + v0;
+  const NlEnt* ent = v.ent + d.lo;
+  const NlMem* mem = v.mem + d.m0;
+  if (v.dbg & 8u) {
+    // measurement: the group's stores alone (same addresses, no loads)
+    if (!active) {
+      return;
+    }
+    for (uint32_t i = 0; i < d.cnt; ++i) {
+      const NlMem m = mem[i];
+      uint8_t* row = a.nhb + m.nhb_off;
+      if (v0 + 4 <= a.V && !(v.dbg & 32u)) {
+        if (d.B == 1) {
+          *reinterpret_cast<uint32_t*>(row + v0) = v0;
+        } else {
+          *reinterpret_cast<nt_u32x2*>(row + 2 * (size_t)v0) = nt_u32x2{v0, v0};
+        }
+      }
+      if (a.dist_w && !(v.dbg & 16u)) {
+        nl_dist_from_levels(a, m.q, v0, 0x01010101u * (v0 & 7u));
+      }
+    }
+    return;
+  }
+  bool nt = false;
   if (lane < d.n) {
-    e = v.ent[d.lo + lane];
+    nt = !nl_transit(a.trbits, ent[lane].node);
+  }
+  const uint64_t ntmask = __ballot(nt);
+  // the neighbours' level words: loaded once, held for every source
+  uint32_t lf[kNlGN];
+  {
+    uint32_t r[kNlGN];
+#pragma unroll
+    for (uint32_t j = 0; j < kNlGN; ++j) {
+      r[j] = __builtin_amdgcn_readfirstlane(ent[j].row);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kNlGN; ++j) {
+      lf[j] = 0xFFFFFFFFu;
+      if (j < d.n) {
+        lf[j] = nl_lvl_word(rs, v0, r[j] * a.Vp8);
+      }
+    }
   }
   uint32_t qs[kNlGS];
-  uint64_t offs[kNlGS];
   uint32_t ls[kNlGS];
 #pragma unroll
   for (uint32_t i = 0; i < kNlGS; ++i) {
-    qs[i] = 0;
-    offs[i] = 0;
-    if (i < d.cnt) {
-      const NlMem m = v.mem[d.m0 + i];
-      qs[i] = m.q;
-      offs[i] = m.nhb_off;
-    }
-  }
-  // the neighbours' level words: loaded once, held for every source
-  uint32_t lf[kNlGN];
-#pragma unroll
-  for (uint32_t j = 0; j < kNlGN; ++j) {
-    lf[j] = 0xFFFFFFFFu;
-    if (j < d.n) {
-      const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)e.row, (int)j);
-      if (active) {
-        lf[j] = *reinterpret_cast<const uint32_t*>(a.lvl + (size_t)r * a.Vp8 + v0);
-      }
-    }
+    qs[i] = __builtin_amdgcn_readfirstlane(mem[i].q); // past cnt: padding, unused
   }
 #pragma unroll
   for (uint32_t i = 0; i < kNlGS; ++i) {
     ls[i] = 0xFFFFFFFFu;
-    if (i < d.cnt && active) {
-      ls[i] = *reinterpret_cast<const uint32_t*>(a.lvl + (size_t)qs[i] * a.Vp8 + v0);
+    if (i < d.cnt) {
+      ls[i] = nl_lvl_word(rs, v0, qs[i] * a.Vp8);
     }
   }
-  const uint64_t ntmask = __ballot(lane < d.n && !nl_transit(a.trbits, e.node));
   // per neighbour: the byte lanes a match may set (a drained neighbour only
   // its own node), the same for every source of the group
   uint32_t allow[kNlGN];
@@ -4065,8 +4222,7 @@ __device__ __forceinline__ void nl_v2_group(const NhLevelsArgs& a, const NlV2Arg
   for (uint32_t j = 0; j < kNlGN; ++j) {
     allow[j] = 0xFFFFFFFFu;
     if ((ntmask >> j) & 1u) {
-      const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)e.node, (int)j);
-      const uint32_t r = f - v0;
+      const uint32_t r = __builtin_amdgcn_readfirstlane(ent[j].node) - v0;
       allow[j] = r < 4u ? (0x80u << (8u * r)) : 0u;
     }
   }
@@ -4091,7 +4247,8 @@ __device__ __forceinline__ void nl_v2_group(const NhLevelsArgs& a, const NlV2Arg
           }
         }
       }
-      uint8_t* row = a.nhb + offs[i];
+      uint8_t* row = a.nhb + __builtin_amdgcn_readfirstlane((uint32_t)mem[i].nhb_off) +
+                     ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(mem[i].nhb_off >> 32)) << 32);
       if ((v.dbg & 4u) && (P0 ^ P1) != 0x5A5A5A5Au) {
         continue; // measurement: no stores
       }
@@ -4126,7 +4283,36 @@ __device__ __forceinline__ void nl_v2_group(const NhLevelsArgs& a, const NlV2Arg
 // spf_nh_levels_swar_kernel.
 template <uint32_t T>
 __global__ __launch_bounds__(T) void spf_nh_levels_v2_kernel(NhLevelsArgs a, NlV2Args v) {
+  // per wave: the 256-node mask tile of a wide solo source (nl_store_wide)
+  __shared__ uint64_t tiles[T / 64][256 * kNsHeldMax];
+  uint64_t* tile = tiles[threadIdx.x >> 6];
   if (a.flags[0] != 0) {
+    return;
+  }
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.lvl, (short)0, (int)v.lvl_bytes, 0x00020000);
+  if (v.order != 0) {
+    const uint32_t bid = v.order == 2 ? xcd_logical_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t per = v.nsolo + v.nsub;
+    uint32_t c = bid / per, k = bid - c * per;
+    if (v.order == 4) { // item-major: an item's chunks back to back
+      const uint32_t nch = (a.V + 4 * T - 1) / (4 * T);
+      k = bid / nch;
+      c = bid - k * nch;
+    }
+    if (v.order >= 3) {
+      // Bresenham spread of the nsub group items over the chunk's items
+      const uint32_t gi = (uint32_t)((uint64_t)k * v.nsub / per);
+      const bool grp = (uint32_t)((uint64_t)(k + 1) * v.nsub / per) > gi;
+      k = grp ? v.nsolo + gi : k - gi;
+    }
+    if (k < v.nsolo) {
+      if (!(v.dbg & 1u)) {
+        nl_v2_solo<T>(a, v, k, c, tile, rs);
+      }
+    } else if (!(v.dbg & 2u)) {
+      nl_v2_group<T>(a, v, k - v.nsolo, c, rs);
+    }
     return;
   }
   const uint32_t bid = blockIdx.x;
@@ -4136,13 +4322,13 @@ __global__ __launch_bounds__(T) void spf_nh_levels_v2_kernel(NhLevelsArgs a, NlV
       return;
     }
     const uint32_t c = bid / v.nsolo;
-    nl_v2_solo<T>(a, v, bid - c * v.nsolo, c);
+    nl_v2_solo<T>(a, v, bid - c * v.nsolo, c, tile, rs);
   } else {
     if (v.dbg & 2u) {
       return;
     }
     const uint32_t b2 = bid - ns, c = b2 / v.nsub;
-    nl_v2_group<T>(a, v, b2 - c * v.nsub, c);
+    nl_v2_group<T>(a, v, b2 - c * v.nsub, c, rs);
   }
 }
 
@@ -6083,6 +6269,10 @@ struct spf_graph {
   std::vector<uint8_t> edge_up;
   bool links_patched = false;
   size_t nbr_cap = 0; // entries of d_nbrs / d_nbr_w (set_edges re-sizes them)
+  // allocated entries of the edge-sized device arrays (d_col, d_link, d_rev,
+  // d_slot; d_wout, d_win, d_w64; d_cw) and of d_link_half: spf_graph_update
+  // rebuilds in place and reallocates only what outgrew its buffer
+  size_t cap_e = 0, cap_w = 0, cap_cw = 0, cap_half = 0;
   // spf_table_repair's delta block + per-workgroup queues, kept between
   // calls (a 100k-node graph needs 200 MB: allocating it per churn event
   // cost more than the screen)
@@ -6215,6 +6405,8 @@ struct spf_query {
   // live spf_route_table handles reading this query's rows (spf_query_destroy
   // refuses while any is alive)
   std::atomic<uint32_t> live_tables{0};
+  // SPF_LAUNCH expressions of the last run (spf_query_kernels)
+  std::vector<const char*> launched;
   // per-run event triples (start, after distance stage, end) of the last
   // kHist runs, for per-kernel averages over a timed loop without syncs
   static constexpr uint32_t kHist = 64;
@@ -6450,11 +6642,19 @@ int build_nl_v2(spf_query* q, const uint32_t* sources, const std::vector<int32_t
   if ((uint64_t)(solo.size() + subs.size()) * nch > 0x7FFFFFFFull) {
     return SPF_OK; // the held kernel's own limit check reports it
   }
+  const uint64_t lvl_bytes = (uint64_t)q->nrows * q->Vp8;
+  if (lvl_bytes >= 0x80000000ull) {
+    return SPF_OK; // beyond one buffer descriptor: the held kernel
+  }
+  // the kernel reads entries and members by whole groups of 8 / 16 / GS with
+  // scalar loads: zero padding past the ends
+  ent.resize(ent.size() + 64, NlEnt{0u, 0u});
+  mem.resize(mem.size() + kNlGS, NlMem{0u, 0u, 0ull});
   auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
   const size_t o_solo = 0, o_sub = al(o_solo + solo.size() * sizeof(NlSolo)),
                o_mem = al(o_sub + subs.size() * sizeof(NlSub)),
                o_ent = al(o_mem + mem.size() * sizeof(NlMem)),
-               total = al(o_ent + std::max<size_t>(1, ent.size()) * sizeof(NlEnt));
+               total = al(o_ent + ent.size() * sizeof(NlEnt));
   std::vector<uint8_t> host(total, 0);
   std::memcpy(host.data() + o_solo, solo.data(), solo.size() * sizeof(NlSolo));
   std::memcpy(host.data() + o_sub, subs.data(), subs.size() * sizeof(NlSub));
@@ -6471,9 +6671,82 @@ int build_nl_v2(spf_query* q, const uint32_t* sources, const std::vector<int32_t
   q->v2.ent = reinterpret_cast<const NlEnt*>(b + o_ent);
   q->v2.nsolo = (uint32_t)solo.size();
   q->v2.nsub = (uint32_t)subs.size();
+  q->v2.lvl_bytes = (uint32_t)lvl_bytes;
   q->v2.dbg = env_u32("OPENR_NL_V2_DBG", 0);
+  // item-major (4): measured fastest with the LDS-staged wide tiles
+  // (profiles/r05k: 0.364 ms against 0.385-0.389 for the chunk-major orders)
+  q->v2.order = std::min<uint32_t>(4, env_u32("OPENR_NL_V2_ORDER", 4));
   q->has_v2 = true;
   q->v2_gen = g->nbr_gen;
+  return SPF_OK;
+}
+
+// OPENR_SPF_CREATE_TIMING=1: phase times of spf_graph_create / _update on
+// stderr (measurement); mark("phase") closes the phase that ends there
+struct PhaseTimer {
+  const char* who;
+  bool on;
+  std::vector<std::pair<const char*, std::chrono::steady_clock::time_point>> m;
+  explicit PhaseTimer(const char* w) : who(w), on(env_flag("OPENR_SPF_CREATE_TIMING", 0)) {
+    (*this)("start");
+  }
+  void operator()(const char* what) {
+    if (on) {
+      m.emplace_back(what, std::chrono::steady_clock::now());
+    }
+  }
+  ~PhaseTimer() {
+    for (size_t i = 1; i < m.size(); ++i) {
+      std::fprintf(stderr, "[%s] %-12s %8.3f ms\n", who, m[i].first,
+                   std::chrono::duration<double, std::milli>(m[i].second - m[i - 1].second).count());
+    }
+  }
+};
+
+// spf_graph_create / spf_graph_update: the CSR arrays are present and every
+// half-edge has a consistent reverse (node blocks on the host pool; the lowest
+// bad edge is reported)
+int validate_graph_desc(const spf_graph_desc* desc) {
+  const uint32_t V = desc->num_nodes, E = desc->num_edges;
+  if (!desc->row_ptr || (E && (!desc->col || !desc->metric ||
+                               !desc->link_id || !desc->rev)) ||
+      (V && !desc->node_overloaded)) {
+    return fail(SPF_E_INVALID, "missing graph array");
+  }
+  if (desc->row_ptr[0] != 0 || desc->row_ptr[V] != E) {
+    return fail(SPF_E_INVALID, "row_ptr does not span [0, E]");
+  }
+  for (uint32_t u = 0; u < V; ++u) {
+    if (desc->row_ptr[u + 1] < desc->row_ptr[u]) {
+      return fail(SPF_E_INVALID, "row_ptr not monotone");
+    }
+  }
+  {
+    // half-edge consistency, node blocks on the host pool; the lowest bad
+    // edge is reported (same message as a sequential scan)
+    std::atomic<uint32_t> bad{kInf32};
+    const uint32_t nblk = (V + kHostBlock - 1) / kHostBlock;
+    openr::parallelFor(nblk, openr::hostThreads(E, kHostMinEdges), [&](size_t b, unsigned) {
+      const uint32_t u1 = std::min<uint32_t>(V, (uint32_t)(b + 1) * kHostBlock);
+      for (uint32_t u = (uint32_t)b * kHostBlock; u < u1; ++u) {
+        for (uint32_t e = desc->row_ptr[u]; e < desc->row_ptr[u + 1]; ++e) {
+          const uint32_t v = desc->col[e], r = desc->rev[e];
+          if (v >= V || v == u || r >= E || desc->rev[r] != e ||
+              desc->col[r] != u || desc->link_id[e] >= desc->num_links ||
+              desc->link_id[r] != desc->link_id[e]) {
+            uint32_t cur = bad.load();
+            while (e < cur && !bad.compare_exchange_weak(cur, e)) {
+            }
+            return;
+          }
+        }
+      }
+    }, 1);
+    if (bad.load() != kInf32) {
+      return fail(SPF_E_INVALID, "inconsistent half-edge at " +
+                                     std::to_string(bad.load()));
+    }
+  }
   return SPF_OK;
 }
 
@@ -6557,7 +6830,7 @@ void build_nbr_lists(spf_graph* g) {
   std::vector<uint32_t> scratch(E);
   std::vector<uint32_t> cnt(V, 0);
   const uint32_t nblk = (V + kHostBlock - 1) / kHostBlock;
-  const unsigned nth = openr::hostThreads(E, 1u << 16);
+  const unsigned nth = openr::hostThreads(E, kHostMinEdges);
   openr::parallelFor(nblk, nth, [&](size_t b, unsigned) {
     const uint32_t u1 = std::min<uint32_t>(V, (uint32_t)(b + 1) * kHostBlock);
     for (uint32_t u = (uint32_t)b * kHostBlock; u < u1; ++u) {
@@ -6666,7 +6939,7 @@ void refresh_exact(spf_graph* g) {
 // fast-path weights, exactness, uniformity and per-neighbour cheapest metric
 int upload_weights(spf_graph* g) {
   const uint32_t E = g->E, V = g->V;
-  const unsigned nth = openr::hostThreads(E, 1u << 16);
+  const unsigned nth = openr::hostThreads(E, kHostMinEdges);
   const uint32_t nblk = (V + kHostBlock - 1) / kHostBlock;
   auto blocks = [&](auto&& fn) {
     openr::parallelFor(nblk, nth, [&](size_t b, unsigned w) {
@@ -6743,11 +7016,21 @@ int upload_weights(spf_graph* g) {
     }
   });
   if (E) {
-    if (!g->d_wout) {
-      HIP_TRY(hipMalloc((void**)&g->d_wout, E * 4));
-      HIP_TRY(hipMalloc((void**)&g->d_win, E * 4));
-      HIP_TRY(hipMalloc((void**)&g->d_w64, E * 8));
-      HIP_TRY(hipMalloc((void**)&g->d_nbr_w, g->nbr_w.size() * 4));
+    if (!g->d_wout || E > g->cap_w) {
+      for (void* p : {(void*)g->d_wout, (void*)g->d_win, (void*)g->d_w64}) {
+        if (p) {
+          (void)hipFree(p);
+        }
+      }
+      const size_t c = (size_t)E + E / 8; // headroom for in-place rebuilds
+      HIP_TRY(hipMalloc((void**)&g->d_wout, c * 4));
+      HIP_TRY(hipMalloc((void**)&g->d_win, c * 4));
+      HIP_TRY(hipMalloc((void**)&g->d_w64, c * 8));
+      g->cap_w = c;
+    }
+    if (!g->d_nbr_w || g->nbr_w.size() > g->nbr_cap) {
+      // d_nbrs / d_nbr_w share nbr_cap (the caller sizes d_nbrs first)
+      return fail(SPF_E_INVALID, "neighbour-weight buffer smaller than the neighbour lists");
     }
     HIP_TRY(hipMemcpy(g->d_wout, wout.data(), E * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(g->d_win, win.data(), E * 4, hipMemcpyHostToDevice));
@@ -6776,8 +7059,13 @@ int upload_weights(spf_graph* g) {
     });
     // padded to whole 16-byte chunks (the vector reads of the last one)
     cw.resize(((size_t)E + 3) & ~(size_t)3, 0u);
-    if (!g->d_cw) {
-      HIP_TRY(hipMalloc((void**)&g->d_cw, cw.size() * 4));
+    if (!g->d_cw || cw.size() > g->cap_cw) {
+      if (g->d_cw) {
+        (void)hipFree(g->d_cw);
+      }
+      const size_t c = (cw.size() + cw.size() / 8 + 3) & ~(size_t)3;
+      HIP_TRY(hipMalloc((void**)&g->d_cw, c * 4));
+      g->cap_cw = c;
     }
     HIP_TRY(hipMemcpy(g->d_cw, cw.data(), cw.size() * 4, hipMemcpyHostToDevice));
     g->cw_bits = bits;
@@ -6836,7 +7124,7 @@ int upload_sell(spf_graph* g) {
 // scan of the host metrics
 void rescan_scalars(spf_graph* g) {
   const uint32_t E = g->E;
-  const unsigned nth = openr::hostThreads(E, 1u << 16);
+  const unsigned nth = openr::hostThreads(E, kHostMinEdges);
   const size_t chunk = (E + nth - 1) / std::max(1u, nth);
   std::vector<uint64_t> wmax(nth, 0), wsum(nth, 0);
   std::vector<uint8_t> same(nth, 1);
@@ -6945,7 +7233,7 @@ int patch_weights_sparse(spf_graph* g, uint32_t n, const uint32_t* edge_idx, con
   HIP_TRY(pool_malloc((void**)&d, pk.size() * 4));
   HIP_TRY(hipMemcpyAsync(d, pk.data(), pk.size() * 4, hipMemcpyHostToDevice, g->stream));
   a.pk = d;
-  hipLaunchKernelGGL(spf_patch_words_kernel, dim3(1), dim3(256), 0, g->stream, a);
+  SPF_LAUNCH(spf_patch_words_kernel, dim3(1), dim3(256), 0, g->stream, a);
   const hipError_t le = hipGetLastError();
   const hipError_t se = hipStreamSynchronize(g->stream); // pk is host memory too
   pool_free(d);
@@ -7229,47 +7517,13 @@ int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
   if (!desc || !out) {
     return fail(SPF_E_INVALID, "null argument");
   }
+  PhaseTimer mark("spf_graph_create");
   *out = nullptr;
   const uint32_t V = desc->num_nodes, E = desc->num_edges;
-  if (!desc->row_ptr || (E && (!desc->col || !desc->metric ||
-                               !desc->link_id || !desc->rev)) ||
-      (V && !desc->node_overloaded)) {
-    return fail(SPF_E_INVALID, "missing graph array");
+  if (const int vs = validate_graph_desc(desc)) {
+    return vs;
   }
-  if (desc->row_ptr[0] != 0 || desc->row_ptr[V] != E) {
-    return fail(SPF_E_INVALID, "row_ptr does not span [0, E]");
-  }
-  for (uint32_t u = 0; u < V; ++u) {
-    if (desc->row_ptr[u + 1] < desc->row_ptr[u]) {
-      return fail(SPF_E_INVALID, "row_ptr not monotone");
-    }
-  }
-  {
-    // half-edge consistency, node blocks on the host pool; the lowest bad
-    // edge is reported (same message as a sequential scan)
-    std::atomic<uint32_t> bad{kInf32};
-    const uint32_t nblk = (V + kHostBlock - 1) / kHostBlock;
-    openr::parallelFor(nblk, openr::hostThreads(E, 1u << 16), [&](size_t b, unsigned) {
-      const uint32_t u1 = std::min<uint32_t>(V, (uint32_t)(b + 1) * kHostBlock);
-      for (uint32_t u = (uint32_t)b * kHostBlock; u < u1; ++u) {
-        for (uint32_t e = desc->row_ptr[u]; e < desc->row_ptr[u + 1]; ++e) {
-          const uint32_t v = desc->col[e], r = desc->rev[e];
-          if (v >= V || v == u || r >= E || desc->rev[r] != e ||
-              desc->col[r] != u || desc->link_id[e] >= desc->num_links ||
-              desc->link_id[r] != desc->link_id[e]) {
-            uint32_t cur = bad.load();
-            while (e < cur && !bad.compare_exchange_weak(cur, e)) {
-            }
-            return;
-          }
-        }
-      }
-    }, 1);
-    if (bad.load() != kInf32) {
-      return fail(SPF_E_INVALID, "inconsistent half-edge at " +
-                                     std::to_string(bad.load()));
-    }
-  }
+  mark("validate");
   const int ndev = spf_device_count();
   if (ndev <= 0) {
     return fail(SPF_E_DEVICE, "no HIP device visible");
@@ -7295,8 +7549,10 @@ int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
       g->trbits[v >> 5] |= 1u << (v & 31);
     }
   }
+  mark("host copy");
   // distinct neighbours per node (ascending id = name order) and edge slots
   build_nbr_lists(g);
+  mark("nbr lists");
   // lanes per node: the median degree, rounded to a power of two in [4, 64]
   {
     std::vector<uint32_t> deg(V);
@@ -7332,6 +7588,7 @@ int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
     return bail(fail(SPF_E_DEVICE, "hipStreamCreate failed"));
   }
   g->stream = g->own_stream;
+  mark("dev/stream");
   int s = SPF_OK;
   if ((s = dev_upload(&g->d_row, g->row.data(), V + 1)) ||
       (s = dev_upload(&g->d_col, g->col.data(), E)) ||
@@ -7340,11 +7597,19 @@ int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
       (s = dev_upload(&g->d_slot, g->slot.data(), E)) ||
       (s = dev_upload(&g->d_tr, g->trbits.data(), g->trbits.size())) ||
       (s = dev_upload(&g->d_nbr_off, g->nbr_off.data(), V + 1)) ||
-      (s = dev_upload(&g->d_nbrs, g->nbrs.data(), g->nbrs.size())) ||
-      (s = upload_weights(g))) {
+      (s = dev_upload(&g->d_nbrs, g->nbrs.data(), g->nbrs.size()))) {
     return bail(s);
   }
   g->nbr_cap = g->nbrs.size();
+  g->cap_e = E;
+  if (hipMalloc((void**)&g->d_nbr_w, std::max<size_t>(g->nbr_cap, 1) * 4) != hipSuccess) {
+    return bail(fail(SPF_E_NOMEM, "neighbour weights"));
+  }
+  mark("csr upload");
+  if ((s = upload_weights(g))) {
+    return bail(s);
+  }
+  mark("weights");
   {
     std::vector<uint32_t> half(2 * (size_t)g->L, kInf32);
     for (uint32_t e = 0; e < E; ++e) {
@@ -7353,11 +7618,141 @@ int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
     if ((s = dev_upload(&g->d_link_half, half.data(), half.size()))) {
       return bail(s);
     }
+    g->cap_half = half.size();
   }
+  mark("link halves");
   if (V && V <= kMsThreads * kMsMaxK && (s = upload_sell(g))) {
     return bail(s);
   }
+  mark("sliced ELL");
   *out = g;
+  return SPF_OK;
+}
+
+// In-place rebuild (LinkState::patchStructure's link flaps): same device,
+// stream and node set; every host array and derived structure is recomputed
+// from `desc`, and the device buffers are rewritten where they are large
+// enough (reallocated with headroom otherwise), so a flap costs the host
+// passes and the uploads, not an allocation / free of every array, a stream
+// and the device-property query.
+int spf_graph_update(spf_graph* g, const spf_graph_desc* desc) {
+  SPF_ABI_RANGE("spf_graph_update");
+  if (!g || !desc) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  if (const uint32_t n = g->live_queries.load(std::memory_order_relaxed)) {
+    return fail(SPF_E_INVALID, "spf_graph_update: " + std::to_string(n) +
+                                   " live queries read this graph (destroy them first)");
+  }
+  if (desc->num_nodes != g->V) {
+    return fail(SPF_E_INVALID, "spf_graph_update: the node set changed (create a new graph)");
+  }
+  PhaseTimer mark("spf_graph_update");
+  if (const int vs = validate_graph_desc(desc)) {
+    return vs;
+  }
+  mark("validate");
+  const uint32_t V = desc->num_nodes, E = desc->num_edges;
+  HIP_TRY(hipSetDevice(g->device));
+  HIP_TRY(hipStreamSynchronize(g->stream)); // queued work reads the old arrays
+  mark("sync");
+  g->E = E;
+  g->L = desc->num_links;
+  g->row.assign(desc->row_ptr, desc->row_ptr + V + 1);
+  g->col.assign(desc->col, desc->col + E);
+  g->link.assign(desc->link_id, desc->link_id + E);
+  g->rev.assign(desc->rev, desc->rev + E);
+  g->w64.assign(desc->metric, desc->metric + E);
+  std::fill(g->trbits.begin(), g->trbits.end(), 0u);
+  for (uint32_t v = 0; v < V; ++v) {
+    if (!desc->node_overloaded[v]) {
+      g->trbits[v >> 5] |= 1u << (v & 31);
+    }
+  }
+  // a fresh CSR: no half-edge is down in place any more
+  g->col_orig.clear();
+  g->edge_up.clear();
+  g->links_patched = false;
+  mark("host copy");
+  build_nbr_lists(g);
+  mark("nbr lists");
+  // edge-sized arrays: rewritten in place, or reallocated with headroom
+  auto store32 = [&](uint32_t** d, const std::vector<uint32_t>& h, size_t& cap) -> int {
+    if (!*d || h.size() > cap) {
+      if (*d) {
+        (void)hipFree(*d);
+        *d = nullptr;
+      }
+      const size_t c = std::max<size_t>(1, h.size() + h.size() / 8);
+      HIP_TRY(hipMalloc((void**)d, c * 4));
+      cap = c;
+    }
+    if (!h.empty()) {
+      HIP_TRY(hipMemcpy(*d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    }
+    return SPF_OK;
+  };
+  int s = SPF_OK;
+  size_t cap_e = g->cap_e, cap_nbr = g->nbr_cap, cap_v = (size_t)V + 1;
+  // col / link / rev / slot share cap_e: grow them together
+  if (E > g->cap_e) {
+    for (uint32_t** d : {&g->d_col, &g->d_link, &g->d_rev, &g->d_slot}) {
+      if (*d) {
+        (void)hipFree(*d);
+        *d = nullptr;
+      }
+    }
+  }
+  size_t c1 = cap_e, c2 = cap_e, c3 = cap_e, c4 = cap_e;
+  if ((s = store32(&g->d_col, g->col, c1)) || (s = store32(&g->d_link, g->link, c2)) ||
+      (s = store32(&g->d_rev, g->rev, c3)) || (s = store32(&g->d_slot, g->slot, c4)) ||
+      (s = store32(&g->d_row, g->row, cap_v)) || (s = store32(&g->d_nbr_off, g->nbr_off, cap_v))) {
+    return s;
+  }
+  g->cap_e = std::max(c1, (size_t)E);
+  HIP_TRY(hipMemcpy(g->d_tr, g->trbits.data(), g->trbits.size() * 4, hipMemcpyHostToDevice));
+  if (g->nbrs.size() > cap_nbr || !g->d_nbrs) {
+    for (uint32_t** d : {&g->d_nbrs, &g->d_nbr_w}) {
+      if (*d) {
+        (void)hipFree(*d);
+        *d = nullptr;
+      }
+    }
+    const size_t c = std::max<size_t>(1, g->nbrs.size() + g->nbrs.size() / 8);
+    HIP_TRY(hipMalloc((void**)&g->d_nbrs, c * 4));
+    HIP_TRY(hipMalloc((void**)&g->d_nbr_w, c * 4));
+    g->nbr_cap = c;
+  }
+  if (!g->nbrs.empty()) {
+    HIP_TRY(hipMemcpy(g->d_nbrs, g->nbrs.data(), g->nbrs.size() * 4, hipMemcpyHostToDevice));
+  }
+  mark("csr upload");
+  if ((s = upload_weights(g))) {
+    return s;
+  }
+  mark("weights");
+  {
+    std::vector<uint32_t> half(2 * (size_t)g->L, kInf32);
+    for (uint32_t e = 0; e < E; ++e) {
+      half[2 * (size_t)g->link[e] + (e < g->rev[e] ? 0 : 1)] = e;
+    }
+    if ((s = store32(&g->d_link_half, half, g->cap_half))) {
+      return s;
+    }
+  }
+  if (g->d_sell) {
+    (void)hipFree(g->d_sell);
+    g->d_sell = nullptr;
+  }
+  if (g->d_sell_off) {
+    (void)hipFree(g->d_sell_off);
+    g->d_sell_off = nullptr;
+  }
+  mark("link halves");
+  if (V && V <= kMsThreads * kMsMaxK && (s = upload_sell(g))) {
+    return s;
+  }
+  mark("sliced ELL");
   return SPF_OK;
 }
 
@@ -7582,7 +7977,7 @@ int spf_graph_set_edges(
   HIP_TRY(pool_malloc((void**)&d, pk.size() * 4));
   HIP_TRY(hipMemcpyAsync(d, pk.data(), pk.size() * 4, hipMemcpyHostToDevice, g->stream));
   a.pk = d;
-  hipLaunchKernelGGL(spf_patch_words_kernel, dim3(1), dim3(256), 0, g->stream, a);
+  SPF_LAUNCH(spf_patch_words_kernel, dim3(1), dim3(256), 0, g->stream, a);
   const hipError_t le = hipGetLastError();
   const hipError_t se = hipStreamSynchronize(g->stream);
   pool_free(d);
@@ -8438,7 +8833,7 @@ int launch_sssp(spf_query* q) {
   HIP_TRY(hipFuncSetAttribute(
       (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
       (int)q->lds_bytes));
-  hipLaunchKernelGGL(
+  SPF_LAUNCH(
       kern, dim3(q->grid), dim3(kBlock), q->lds_bytes, g->stream, a);
   HIP_TRY(hipGetLastError());
   if (a.stats) {
@@ -8548,7 +8943,7 @@ int launch_dstep_t(spf_query* q) {
     HIP_TRY(hipMalloc((void**)&d.stats, 8 * sizeof(unsigned long long)));
     HIP_TRY(hipMemsetAsync(d.stats, 0, 8 * sizeof(unsigned long long), g->stream));
   }
-  hipLaunchKernelGGL(kern, dim3(q->grid), dim3(BS), lds, g->stream, d);
+  SPF_LAUNCH(kern, dim3(q->grid), dim3(BS), lds, g->stream, d);
   HIP_TRY(hipGetLastError());
   if (d.stats) {
     unsigned long long h[8];
@@ -8623,7 +9018,7 @@ int launch_dlds(spf_query* q) {
   }
   HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)q->dlds_lds));
-  hipLaunchKernelGGL(kern, dim3(q->dlds_grid), dim3(1024), q->dlds_lds, g->stream, a);
+  SPF_LAUNCH(kern, dim3(q->dlds_grid), dim3(1024), q->dlds_lds, g->stream, a);
   HIP_TRY(hipGetLastError());
   if (a.stats) {
     unsigned long long h[8];
@@ -8671,7 +9066,7 @@ int launch_msdstep(spf_query* q) {
   HIP_TRY(hipFuncSetAttribute(
       (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
       (int)q->lds_bytes));
-  hipLaunchKernelGGL(kern, dim3(q->grid), dim3(1024), q->lds_bytes, g->stream, a);
+  SPF_LAUNCH(kern, dim3(q->grid), dim3(1024), q->lds_bytes, g->stream, a);
   HIP_TRY(hipGetLastError());
   return SPF_OK;
 }
@@ -8697,7 +9092,7 @@ int launch_bfs(spf_query* q, bool unit) {
   HIP_TRY(hipFuncSetAttribute(
       (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
       (int)q->lds_bytes));
-  hipLaunchKernelGGL(
+  SPF_LAUNCH(
       kern, dim3(q->grid), dim3(kBlock), q->lds_bytes, g->stream, a);
   HIP_TRY(hipGetLastError());
   return SPF_OK;
@@ -8725,7 +9120,7 @@ int launch_nh_rows(spf_query* q, bool unit) {
   if (blocks > 0x7FFFFFFFull) {
     return fail(SPF_E_UNSUPPORTED, "batch too large for the next-hop pass");
   }
-  hipLaunchKernelGGL(
+  SPF_LAUNCH(
       spf_nh_rows_kernel, dim3((uint32_t)blocks), dim3(kNhThreads), 0,
       g->stream, a);
   HIP_TRY(hipGetLastError());
@@ -8772,7 +9167,7 @@ int launch_msbfs(spf_query* q, bool unit) {
     HIP_TRY(hipMemsetAsync(q->d_ms_mask, 0, (size_t)q->ms_nbatch * g->E * 8, g->stream));
     HIP_TRY(hipMemsetAsync(q->d_ms_flag, 0, (size_t)q->ms_nbatch * q->ms_nfw * 4, g->stream));
     if (q->nq) {
-      hipLaunchKernelGGL(spf_ms_ign_kernel, dim3(q->nq), dim3(256), 0, g->stream, q->d_ign_off,
+      SPF_LAUNCH(spf_ms_ign_kernel, dim3(q->nq), dim3(256), 0, g->stream, q->d_ign_off,
                          q->d_ign, g->d_link_half, g->d_col, g->d_rev, g->L,
                          (uint32_t)q->ms_bits, g->E, q->ms_nfw, q->d_ms_mask, q->d_ms_flag);
       HIP_TRY(hipGetLastError());
@@ -8848,7 +9243,7 @@ int launch_msbfs(spf_query* q, bool unit) {
     z.nq = q->nq;
     z.nvar = q->zvars;
     z.nlinks = q->znlinks;
-    hipLaunchKernelGGL(spf_zvar_kernel, dim3((q->nq + 255) / 256), dim3(256), 0, g->stream, z);
+    SPF_LAUNCH(spf_zvar_kernel, dim3((q->nq + 255) / 256), dim3(256), 0, g->stream, z);
     HIP_TRY(hipGetLastError());
   }
   return SPF_OK;
@@ -8914,35 +9309,35 @@ int launch_nh_levels(spf_query* q, bool unit) {
       // v2: solo items and shared-neighbour groups (spf_nh_levels_v2_kernel)
       const uint64_t vblocks = (uint64_t)(q->v2.nsolo + q->v2.nsub) * ((g->V + 1023) / 1024);
       if (vblocks) {
-        hipLaunchKernelGGL((spf_nh_levels_v2_kernel<256>), dim3((uint32_t)vblocks), dim3(256), 0,
+        SPF_LAUNCH((spf_nh_levels_v2_kernel<256>), dim3((uint32_t)vblocks), dim3(256), 0,
                            g->stream, a, q->v2);
       }
     } else if (T == 1024) {
-      hipLaunchKernelGGL((spf_nh_levels_held_kernel<1024, kNsHeldMax>), dim3((uint32_t)hblocks),
+      SPF_LAUNCH((spf_nh_levels_held_kernel<1024, kNsHeldMax>), dim3((uint32_t)hblocks),
                          dim3(1024), 0, g->stream, a, nolist, 0u);
     } else if (T == 512) {
-      hipLaunchKernelGGL((spf_nh_levels_held_kernel<512, kNsHeldMax>), dim3((uint32_t)hblocks),
+      SPF_LAUNCH((spf_nh_levels_held_kernel<512, kNsHeldMax>), dim3((uint32_t)hblocks),
                          dim3(512), 0, g->stream, a, nolist, 0u);
     } else {
-      hipLaunchKernelGGL((spf_nh_levels_held_kernel<256, kNsHeldMax>), dim3((uint32_t)hblocks),
+      SPF_LAUNCH((spf_nh_levels_held_kernel<256, kNsHeldMax>), dim3((uint32_t)hblocks),
                          dim3(256), 0, g->stream, a, nolist, 0u);
     }
     HIP_TRY(hipGetLastError());
     if (q->nmid && env_flag("OPENR_NL_WIDE", 1)) {
       // sources with 4-8 words: the same per-(source, chunk) pass
       const uint64_t mblocks = (uint64_t)q->nmid * ((g->V + 1023) / 1024);
-      hipLaunchKernelGGL((spf_nh_levels_held_kernel<256, kNsHeldWide>), dim3((uint32_t)mblocks),
+      SPF_LAUNCH((spf_nh_levels_held_kernel<256, kNsHeldWide>), dim3((uint32_t)mblocks),
                          dim3(256), 0, g->stream, a, (const uint32_t*)q->d_big, q->nmid);
       HIP_TRY(hipGetLastError());
     }
     const uint32_t skip = env_flag("OPENR_NL_WIDE", 1) ? q->nmid : 0;
     const uint32_t grid = std::max<uint32_t>(q->nbig - skip, std::min<uint32_t>(q->nq, 1024));
-    hipLaunchKernelGGL(spf_nh_levels_swar_kernel, dim3(grid), dim3(kNsThreads), 0, g->stream,
+    SPF_LAUNCH(spf_nh_levels_swar_kernel, dim3(grid), dim3(kNsThreads), 0, g->stream,
                        a, (const uint32_t*)q->d_big + skip, q->nbig - skip);
     HIP_TRY(hipGetLastError());
     return SPF_OK;
   }
-  hipLaunchKernelGGL(spf_nh_levels_kernel, dim3((uint32_t)blocks),
+  SPF_LAUNCH(spf_nh_levels_kernel, dim3((uint32_t)blocks),
                      dim3(kNlThreads), 0, g->stream, a);
   HIP_TRY(hipGetLastError());
   return SPF_OK;
@@ -8974,7 +9369,7 @@ int launch_exact(spf_query* q) {
     HIP_TRY(hipMemsetAsync(q->d_nh, 0, q->nh_total * 8, g->stream));
   }
   const uint32_t threads = 64;
-  hipLaunchKernelGGL(
+  SPF_LAUNCH(
       spf_exact_kernel, dim3((q->nq + threads - 1) / threads), dim3(threads),
       0, g->stream, a);
   HIP_TRY(hipGetLastError());
@@ -9022,7 +9417,7 @@ int launch_wide(spf_query* q) {
   if (q->d_nh && q->nh_total) {
     HIP_TRY(hipMemsetAsync(q->d_nh, 0, q->nh_total * 8, g->stream));
   }
-  hipLaunchKernelGGL(spf_wide_kernel, dim3(q->grid), dim3(kWideBlock), q->lds_bytes,
+  SPF_LAUNCH(spf_wide_kernel, dim3(q->grid), dim3(kWideBlock), q->lds_bytes,
                      g->stream, a);
   HIP_TRY(hipGetLastError());
   return SPF_OK;
@@ -9050,7 +9445,7 @@ int finish_zero_plan(spf_query* q) {
   if (!q->d_zvar) {
     return SPF_OK; // distances alone: one table, already in place
   }
-  hipLaunchKernelGGL(spf_zrows_kernel, dim3(q->nq), dim3(256), 0, g->stream, (uint32_t*)q->d_dist,
+  SPF_LAUNCH(spf_zrows_kernel, dim3(q->nq), dim3(256), 0, g->stream, (uint32_t*)q->d_dist,
                      (const uint8_t*)q->d_zvar, (uint64_t)q->nrows * q->Vp, q->Vp);
   HIP_TRY(hipGetLastError());
   if (!q->zfix) {
@@ -9081,11 +9476,11 @@ int finish_zero_plan(spf_query* q) {
       na.nw1 = q->nh_w[i];
       na.V = V;
       na.nq = 1;
-      hipLaunchKernelGGL(spf_nh_narrow_kernel, dim3((V + 1023) / 1024), dim3(256), 0, g->stream,
+      SPF_LAUNCH(spf_nh_narrow_kernel, dim3((V + 1023) / 1024), dim3(256), 0, g->stream,
                          na);
       HIP_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL(spf_rows64to32_kernel, dim3((V + 255) / 256), dim3(256), 0, g->stream,
+    SPF_LAUNCH(spf_rows64to32_kernel, dim3((V + 255) / 256), dim3(256), 0, g->stream,
                        (const uint64_t*)f->d_dist + (size_t)j * V,
                        (uint32_t*)q->d_dist + (size_t)i * q->Vp, V);
     HIP_TRY(hipGetLastError());
@@ -9127,7 +9522,7 @@ int run_screen(spf_query* q) {
   if (b->Vp != q->Vp) {
     return fail(SPF_E_INVALID, "baseline row stride differs");
   }
-  hipLaunchKernelGGL(spf_whatif_screen_kernel, dim3(q->nq), dim3(256), 0, g->stream, a);
+  SPF_LAUNCH(spf_whatif_screen_kernel, dim3(q->nq), dim3(256), 0, g->stream, a);
   HIP_TRY(hipGetLastError());
   return SPF_OK;
 }
@@ -9154,7 +9549,7 @@ int run_plan(spf_query* q) {
   if (blocks > 0x7FFFFFFFull) {
     return fail(SPF_E_UNSUPPORTED, "batch too large for the mask narrowing pass");
   }
-  hipLaunchKernelGGL(spf_nh_narrow_kernel, dim3((uint32_t)blocks), dim3(256), 0, q->g->stream,
+  SPF_LAUNCH(spf_nh_narrow_kernel, dim3((uint32_t)blocks), dim3(256), 0, q->g->stream,
                      na);
   HIP_TRY(hipGetLastError());
   return SPF_OK;
@@ -9259,6 +9654,21 @@ int spf_query_run(spf_query* q) {
   HIP_TRY(hipEventRecord(q->ev0, g->stream));
   HIP_TRY(hipEventRecord(q->hist[h][0], g->stream));
   q->two_stage = false;
+  struct LaunchLog {
+    bool own = false;
+    explicit LaunchLog(spf_query* x) {
+      if (!tl_launched) {
+        x->launched.clear();
+        tl_launched = &x->launched;
+        own = true;
+      }
+    }
+    ~LaunchLog() {
+      if (own) {
+        tl_launched = nullptr;
+      }
+    }
+  } launch_log(q);
   int s = SPF_OK;
   if (q->nq && g->V) {
     s = run_plan(q);
@@ -9269,6 +9679,36 @@ int spf_query_run(spf_query* q) {
   ++q->runs;
   q->ran = true;
   return s;
+}
+
+int spf_query_kernels(const spf_query* q, char* buf, size_t cap) {
+  if (!q) {
+    return fail(SPF_E_INVALID, "null query");
+  }
+  std::vector<std::string> names;
+  for (const char* e : q->launched) {
+    std::string n(e);
+    const size_t b = n.find_first_not_of("( ");
+    if (b == std::string::npos) {
+      continue;
+    }
+    const size_t x = n.find_first_of("<), ", b);
+    n = n.substr(b, x == std::string::npos ? std::string::npos : x - b);
+    if (std::find(names.begin(), names.end(), n) == names.end()) {
+      names.push_back(n);
+    }
+  }
+  std::sort(names.begin(), names.end());
+  std::string out;
+  for (const auto& n : names) {
+    out += (out.empty() ? "" : ",") + n;
+  }
+  if (buf && cap) {
+    const size_t k = std::min(cap - 1, out.size());
+    std::memcpy(buf, out.data(), k);
+    buf[k] = '\0';
+  }
+  return (int)out.size();
 }
 
 int spf_query_sync(spf_query* q) {
@@ -9653,10 +10093,10 @@ int spf_query_trace_paths(
       HIP_TRY(hipMemsetAsync(ta.qstat, 0, (size_t)count * kTcStat * 8, g->stream));
     }
     if (ta.qstat) {
-      hipLaunchKernelGGL(spf_trace_cursor_kernel<true>, dim3(nw / kTcWaves), dim3(64 * kTcWaves),
+      SPF_LAUNCH(spf_trace_cursor_kernel<true>, dim3(nw / kTcWaves), dim3(64 * kTcWaves),
                          0, g->stream, ta);
     } else {
-      hipLaunchKernelGGL(spf_trace_cursor_kernel<false>, dim3(nw / kTcWaves), dim3(64 * kTcWaves),
+      SPF_LAUNCH(spf_trace_cursor_kernel<false>, dim3(nw / kTcWaves), dim3(64 * kTcWaves),
                          0, g->stream, ta);
     }
     if (ta.qstat) {
@@ -9690,7 +10130,7 @@ int spf_query_trace_paths(
               (double)ssteps / count, msteps, (double)sbuilt / count);
     }
   } else {
-    hipLaunchKernelGGL(spf_trace_paths_kernel, dim3((count + kTraceWaves - 1) / kTraceWaves),
+    SPF_LAUNCH(spf_trace_paths_kernel, dim3((count + kTraceWaves - 1) / kTraceWaves),
                        dim3(64 * kTraceWaves), 0, g->stream, a);
   }
   HIP_TRY(hipGetLastError());
@@ -9757,7 +10197,7 @@ int spf_query_trace_fetch(spf_query* q, uint32_t* links, uint32_t* ends) {
   a.dst_ends = pk + 2 * (size_t)count + lo;
   a.cap = q->trace_cap;
   a.nq = count;
-  hipLaunchKernelGGL(spf_trace_pack_kernel, dim3(count), dim3(64), 0, g->stream, a);
+  SPF_LAUNCH(spf_trace_pack_kernel, dim3(count), dim3(64), 0, g->stream, a);
   HIP_TRY(hipGetLastError());
   if (lo) {
     HIP_TRY(hipMemcpyAsync(links, a.dst_links, lo * 4, hipMemcpyDeviceToHost, g->stream));
@@ -9840,7 +10280,7 @@ int spf_graph_diff(
   const uint32_t nblk = (V + kHostBlock - 1) / kHostBlock;
   std::vector<std::vector<spf_edge_delta>> found(nblk);
   const unsigned nth =
-      openr::hostThreads((size_t)before->num_edges + after->num_edges, 1u << 16);
+      openr::hostThreads((size_t)before->num_edges + after->num_edges, kHostMinEdges);
   openr::parallelFor(nblk, nth, [&](size_t blk, unsigned) {
   std::vector<spf_edge_delta>& lst = found[blk];
   auto emit = [&](uint32_t u, uint32_t v, uint64_t w, uint32_t kind, uint32_t scope) {
@@ -9974,7 +10414,7 @@ int spf_table_screen(
     a.nrows = num_rows;
     a.ndelta = n_deltas;
     a.affected = (uint8_t*)(d + moff + nd * 8);
-    hipLaunchKernelGGL(spf_table_screen_kernel, dim3((num_rows + 255) / 256), dim3(256), 0,
+    SPF_LAUNCH(spf_table_screen_kernel, dim3((num_rows + 255) / 256), dim3(256), 0,
                        g->stream, a);
     if (hipGetLastError() != hipSuccess ||
         hipMemcpyAsync(affected, a.affected, num_rows, hipMemcpyDeviceToHost, g->stream) != hipSuccess ||
@@ -10014,7 +10454,7 @@ int spf_query_scatter_rows(
   HIP_TRY(hipStreamSynchronize(q->g->stream));
   HIP_TRY(hipMemcpy(q->d_scatter, dst_rows, (size_t)q->nq * 4, hipMemcpyHostToDevice));
   const uint32_t chunk = 256 * 16;
-  hipLaunchKernelGGL(spf_scatter_rows_kernel, dim3(q->nq, (V + chunk - 1) / chunk), dim3(256), 0,
+  SPF_LAUNCH(spf_scatter_rows_kernel, dim3(q->nq, (V + chunk - 1) / chunk), dim3(256), 0,
                      q->g->stream, (const uint32_t*)q->d_dist, q->Vp, q->d_scatter,
                      (char*)table, pitch, V);
   HIP_TRY(hipGetLastError());
@@ -10098,7 +10538,7 @@ int spf_table_nexthops(
     release();
     return fail(SPF_E_UNSUPPORTED, "too many rows for one next-hop pass");
   }
-  hipLaunchKernelGGL(spf_nh_rows_kernel, dim3((uint32_t)blocks), dim3(kNhThreads), 0, g->stream, a);
+  SPF_LAUNCH(spf_nh_rows_kernel, dim3((uint32_t)blocks), dim3(kNhThreads), 0, g->stream, a);
   const hipError_t le = hipGetLastError();
   release(); // waits for the pass: the index buffers go back to the pool
   if (le != hipSuccess) {
@@ -10239,7 +10679,7 @@ int spf_table_repair(
                             (int)lds) != hipSuccess) {
       st = fail(SPF_E_DEVICE, "LDS attribute");
     } else {
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), lds, g->stream, da);
+      SPF_LAUNCH(kern, dim3(grid), dim3(1024), lds, g->stream, da);
       if (hipGetLastError() != hipSuccess || hipStreamSynchronize(g->stream) != hipSuccess) {
         st = fail(SPF_E_DEVICE, "repair kernel failed");
       }
@@ -10459,7 +10899,7 @@ int spf_route_table_run(spf_route_table* t) {
     a.P = t->P;
     a.nq = q->nq;
     const uint32_t grid = std::min<uint32_t>(q->nq, (uint32_t)g->num_cus * 8);
-    hipLaunchKernelGGL(spf_route_table_kernel, dim3(grid), dim3(256), 0, g->stream, a);
+    SPF_LAUNCH(spf_route_table_kernel, dim3(grid), dim3(256), 0, g->stream, a);
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipEventRecord(t->ev1, g->stream));
@@ -10572,7 +11012,7 @@ int spf_route_table_diff(spf_route_table* older, spf_route_table* newer, uint32_
   HIP_TRY(hipMemsetAsync(newer->d_count, 0, (size_t)nq * 4, gb->stream));
   if (P) {
     const uint32_t grid = std::min<uint32_t>(nq, (uint32_t)gb->num_cus * 8);
-    hipLaunchKernelGGL(spf_route_table_diff_kernel, dim3(grid), dim3(256), 0, gb->stream,
+    SPF_LAUNCH(spf_route_table_diff_kernel, dim3(grid), dim3(256), 0, gb->stream,
                        older->d_metric, older->d_best, older->d_links, newer->d_metric,
                        newer->d_best, newer->d_links, newer->d_lk_off, P, nq, pw,
                        newer->d_diff, newer->d_count, older->d_lmet, newer->d_lmet,

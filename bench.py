@@ -15,15 +15,14 @@ step time, gather included.
 
 Roofline: the dominant kernel of the step (the one with the larger average
 device time over the timed launches, HIP events on the engine's stream) is
-priced by its ALGORITHMIC bytes per launch (DESIGN.md §4):
-  spf_nh_levels_held_kernel (or spf_nh_levels_kernel)
-                        sum_q [ V*(1 + nbrs(q)) * b + 8*V*W_q ]
-                         (own level row + one row per distinct neighbour of
-                          the source, b = 1 byte per 8-bit level, 4 if the
-                          32-bit rows are used; next-hop mask row written)
-  spf_msbfs_kernel      sum_q 5*V + levels * (4*E + 4*(V+1)) per 64-source
-                         batch (dist u32 + level u8 rows written; CSR scanned
-                         once per BFS level)
+priced by its ALGORITHMIC bytes per launch (DESIGN.md §3):
+  spf_nh_levels_v2_kernel (held / per-node kernels with OPENR_NL_V2=0 /
+  OPENR_NL_SWAR=0)      sum_q [ V + V*B_q + 4*V ]
+                         (every level row read once, the byte-strided mask
+                          row and the u32 distance row written once)
+  spf_msbfs_kernel      sum_q V + 4*E + 4*(V+1) (u8 level rows written, CSR
+                         read once; the per-level pull scans are L2-served
+                         and reported apart as csr_scan_bytes_l2)
 `traffic` comes from the rocprofv3 PMC passes committed under profiles/
 (profiles/<round>/pmc_traffic.json, written by profiles/collect_pmc.py).
 
@@ -1651,6 +1650,12 @@ def fabric_single(args, topo, world, rank, local, dist):
     value = world * nsrc / (step_ms / 1000.0)
     kname = q.kernel
     dist_k, nh_k = KERNELS.get(kname, (kname, None))
+    # the kernels the run actually launched (spf_query_kernels): the MS-BFS
+    # plan's next-hop stage is the v2 pass unless OPENR_NL_V2=0 / a plan
+    # outside it selects the held kernel
+    launched = q.kernels()
+    if nh_k == "spf_nh_levels_held_kernel" and "spf_nh_levels_v2_kernel" in launched:
+        nh_k = "spf_nh_levels_v2_kernel"
     nbrs = distinct_nbrs(csr)
     # BFS levels per 64-source batch, from the distance rows (unit metric)
     levels = []
@@ -1735,6 +1740,7 @@ def fabric_single(args, topo, world, rank, local, dist):
                       "level for 64 sources, so this counts shared scans, not memory traffic",
         "kernel_ms": round(kernel_ms, 4),
         "kernels": stages,
+        "kernels_launched": launched,
         "parity_spot_check": check,
         "roofline": _roofline(dom, dom_ms, dom_bytes, traffic, traffic_src),
         "step_output_floor": {

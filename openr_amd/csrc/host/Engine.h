@@ -40,6 +40,10 @@ struct LinkState::Engine {
     return id < links.size() && links[id].get() == l ? id : ~0u;
   }
   std::vector<std::array<uint32_t, 2>> halves; // link id -> half-edge from first/second node
+  // the arrays the last in-place link splice retired (patchStructure reuses
+  // their capacity: no fresh pages per flap)
+  std::vector<uint32_t> spareRow, spareCol, spareLinkId, spareRev;
+  std::vector<uint64_t> spareMetric;
   // link ids freed by in-place link removals (LinkState::patchStructure):
   // links[id] == nullptr, reused by the next link that comes up
   std::vector<uint32_t> freeIds;

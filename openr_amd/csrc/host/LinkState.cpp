@@ -1518,7 +1518,9 @@ bool LinkState::patchStructure(
     }
   }
   std::vector<std::vector<const std::shared_ptr<Link>*>> affRows(affNodes.size());
-  std::vector<uint32_t> newRow(V + 1, 0);
+  // the retired arrays of the last splice are reused (no fresh pages)
+  std::vector<uint32_t> newRow = std::move(eng.spareRow);
+  newRow.assign(V + 1, 0);
   {
     size_t k = 0;
     for (uint32_t u = 0; u < V; ++u) {
@@ -1535,8 +1537,15 @@ bool LinkState::patchStructure(
     }
   }
   const uint32_t E = newRow[V];
-  // link ids: freed for the links going down, taken for the ones coming up
-  std::vector<std::shared_ptr<Link>> links = eng.links;
+  // link ids: freed for the links going down, taken for the ones coming up.
+  // eng.links is not copied (a copy of ~100k shared_ptrs is two atomic
+  // refcount updates per link, ~2 ms on the fabric): which ids are alive is a
+  // byte per id, and the id -> Link changes are applied at the commit
+  std::vector<uint8_t> alive(eng.links.size());
+  for (size_t i = 0; i < eng.links.size(); ++i) {
+    alive[i] = eng.links[i] != nullptr;
+  }
+  std::vector<std::pair<uint32_t, std::shared_ptr<Link>>> linkSets; // applied at the commit
   std::vector<std::array<uint32_t, 2>> halves = eng.halves;
   std::vector<uint32_t> freeIds = eng.freeIds;
   std::vector<spf_edge_delta> dMetric, dHops;
@@ -1550,7 +1559,8 @@ bool LinkState::patchStructure(
         dHops.push_back({u, v, 1, SPF_DELTA_REMOVED, SPF_SCOPE_ALL});
       }
     }
-    links[lid] = nullptr;
+    alive[lid] = 0;
+    linkSets.emplace_back(lid, nullptr);
     halves[lid] = {~0u, ~0u};
     freeIds.push_back(lid);
   }
@@ -1562,11 +1572,12 @@ bool LinkState::patchStructure(
       lid = freeIds.back();
       freeIds.pop_back();
     } else {
-      lid = (uint32_t)links.size();
-      links.emplace_back();
+      lid = (uint32_t)alive.size();
+      alive.push_back(0);
       halves.push_back({~0u, ~0u});
     }
-    links[lid] = l;
+    alive[lid] = 1;
+    linkSets.emplace_back(lid, l);
     upIds.emplace(l.get(), lid);
   }
   auto idOf = [&](const Link* l) {
@@ -1584,8 +1595,11 @@ bool LinkState::patchStructure(
       halves[lid][s] = aff[tail] ? ~0u : e - eng.row[tail] + newRow[tail];
     }
   }
-  std::vector<uint32_t> col(E), linkId(E);
-  std::vector<uint64_t> metric(E);
+  std::vector<uint32_t> col = std::move(eng.spareCol), linkId = std::move(eng.spareLinkId);
+  std::vector<uint64_t> metric = std::move(eng.spareMetric);
+  col.resize(E);
+  linkId.resize(E);
+  metric.resize(E);
   {
     size_t k = 0;
     for (uint32_t u = 0; u < V; ++u) {
@@ -1613,10 +1627,11 @@ bool LinkState::patchStructure(
       }
     }
   }
-  std::vector<uint32_t> rev(E, ~0u);
+  std::vector<uint32_t> rev = std::move(eng.spareRev);
+  rev.assign(E, ~0u);
   for (uint32_t lid = 0; lid < halves.size(); ++lid) {
     const auto& h = halves[lid];
-    if (!links[lid]) {
+    if (!alive[lid]) {
       continue;
     }
     if (h[0] == ~0u || h[1] == ~0u) {
@@ -1691,7 +1706,7 @@ bool LinkState::patchStructure(
   d.link_id = linkId.data();
   d.rev = rev.data();
   d.node_overloaded = overloaded.data();
-  d.num_links = (uint32_t)links.size();
+  d.num_links = (uint32_t)alive.size();
   d.device = getSpfDevice();
   // the device graph is rebuilt in place (same handle, stream and buffers:
   // spf_graph_update).  A failed update leaves it unusable: it is dropped,
@@ -1726,13 +1741,23 @@ bool LinkState::patchStructure(
     eng.cgraph = nullptr;
     eng.cgraphGen = 0;
   }
-  eng.row = std::move(newRow);
-  eng.col = std::move(col);
-  eng.linkId = std::move(linkId);
-  eng.metric = std::move(metric);
-  eng.rev = std::move(rev);
+  std::swap(eng.row, newRow);
+  std::swap(eng.col, col);
+  std::swap(eng.linkId, linkId);
+  std::swap(eng.metric, metric);
+  std::swap(eng.rev, rev);
+  eng.spareRow = std::move(newRow);
+  eng.spareCol = std::move(col);
+  eng.spareLinkId = std::move(linkId);
+  eng.spareMetric = std::move(metric);
+  eng.spareRev = std::move(rev);
   eng.overloaded = std::move(overloaded);
-  eng.links = std::move(links);
+  if (eng.links.size() < alive.size()) {
+    eng.links.resize(alive.size());
+  }
+  for (auto& [lid, l] : linkSets) {
+    eng.links[lid] = std::move(l); // in order: a freed id taken again ends up set
+  }
   eng.halves = std::move(halves);
   eng.freeIds = std::move(freeIds);
   eng.exact = spf_graph_needs_exact(eng.graph) != 0;

@@ -82,6 +82,12 @@ inline void spf_note_launch(const char* expr) {
     spf_note_launch(#kern);             \
     hipLaunchKernelGGL(kern, __VA_ARGS__); \
   } while (0)
+// a launch through a kernel variable: `name` is the kernel's own name
+#define SPF_LAUNCH_AS(name, kern, ...)  \
+  do {                                  \
+    spf_note_launch(name);              \
+    hipLaunchKernelGGL(kern, __VA_ARGS__); \
+  } while (0)
 
 namespace {
 
@@ -2662,6 +2668,8 @@ struct MsBfsArgs {
   const uint32_t* ign_flag = nullptr;
   uint32_t E = 0;
   uint32_t nfw = 0;
+  // measurement only (OPENR_MS_NOREC=1): the BFS without its row stores
+  uint32_t norec = 0;
 };
 
 // Masks and flags of spf_msbfs_kernel's ignore mode: one block per query,
@@ -2698,6 +2706,9 @@ __global__ __launch_bounds__(256) void spf_ms_ign_kernel(
 template <typename MT>
 __device__ __forceinline__ void ms_record(
     const MsBfsArgs& a, uint32_t q0, uint32_t v, MT bits, uint32_t level) {
+  if (a.norec) {
+    return;
+  }
   const uint32_t d = level * a.scale;
   const uint8_t l8 = level < 255 ? (uint8_t)level : (uint8_t)255;
   if (level >= 255 && bits) {
@@ -2963,6 +2974,171 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
       }
     }
     __syncthreads();
+  }
+}
+
+// ---- cooperative MS-BFS (a 64-source batch split over P workgroups) ----
+//
+// spf_msbfs_kernel runs a batch on ONE CU, and a level's pull over all V
+// nodes (~14 us on the fabric) is that CU's work: a rank's block of a sharded
+// table (20 batches at N = 8) leaves most of the chip idle and its MS-BFS stays
+// at the one-batch latency floor.  Here P workgroups share a batch:
+// part p owns nodes v = (k P + p) 1024 + tid, keeps its own LDS copy of the
+// whole frontier (V words, single-buffered), pulls only its nodes, and
+// publishes their next-frontier bits to a global exchange buffer (double-
+// buffered by level parity); the P parts meet at a counter barrier per level
+// (agent-scope release / acquire, MI355X cross-XCD hand-off recipe) and reload
+// the full frontier.  Launched cooperatively (every workgroup co-resident), P
+// sized from the occupancy query: the round-4 probe deadlocked because a grid
+// of two 1,024-thread workgroups per CU cannot be resident at 128 VGPRs.
+// Same rows as spf_msbfs_kernel (the plain instance: no ignore masks,
+// wave-recorded levels or zero-metric closure).
+struct MsCoopArgs {
+  MsBfsArgs a;
+  uint64_t* xbuf;  // [nbatch][2][V] published next-frontier bits
+  uint32_t* cnt;   // [nbatch] barrier arrivals (zeroed before the launch)
+  uint32_t* anyv;  // [nbatch][2][P] "some bit was new" per part and level parity
+  uint32_t* err;   // set when a barrier wait gave up (spf_query_sync reports it)
+  uint32_t P;
+};
+constexpr uint32_t kMsCoopSpin = 1u << 26; // polls before a barrier wait gives up
+
+template <uint32_t KMAX>
+__global__ __launch_bounds__(kMsThreads) void spf_msbfs_coop_kernel(MsCoopArgs c) {
+  extern __shared__ __align__(16) unsigned char ms_smem[];
+  const MsBfsArgs& a = c.a;
+  uint64_t* cur = reinterpret_cast<uint64_t*>(ms_smem); // this part's frontier copy
+  const uint32_t V = a.V, tid = threadIdx.x, P = c.P;
+  const uint32_t b = blockIdx.x / P, p = blockIdx.x - b * P;
+  const uint32_t nbatch = (a.nq + 63) / 64;
+  if (b >= nbatch) {
+    return; // whole workgroup (never: the grid is nbatch * P)
+  }
+  if (a.flags_clear && blockIdx.x == 0 && tid == 0) {
+    *a.flags_clear = 0;
+  }
+  const uint32_t q0 = b * 64, nb = min(64u, a.nq - q0);
+  const uint64_t full = nb == 64 ? ~0ull : ((1ull << nb) - 1);
+  const uint32_t span = P * kMsThreads;
+  const uint32_t Kp = (V + span - 1) / span; // <= KMAX
+  for (uint32_t v = tid; v < V; v += kMsThreads) {
+    cur[v] = 0;
+  }
+  __syncthreads();
+  if (tid < nb) {
+    atomicOr(reinterpret_cast<unsigned long long*>(&cur[a.src[q0 + tid]]), 1ull << tid);
+  }
+  __syncthreads();
+  uint64_t vis[KMAX];
+  uint32_t trm = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < KMAX; ++k) {
+    const uint32_t v = (k * P + p) * kMsThreads + tid;
+    vis[k] = 0;
+    if (k < Kp && v < V) {
+      trm |= ((a.trbits[v >> 5] >> (v & 31)) & 1u) << k;
+      vis[k] = cur[v];
+      if (vis[k]) {
+        ms_record<uint64_t>(a, q0, v, vis[k], 0);
+      }
+    }
+  }
+  uint64_t* xb = c.xbuf + (size_t)b * 2 * V;
+  uint32_t* anyb = c.anyv + (size_t)b * 2 * P;
+  bool aborted = false;
+  for (uint32_t L = 1;; ++L) {
+    uint64_t* xn = xb + (size_t)(L & 1u) * V;
+    bool any = false;
+#pragma unroll
+    for (uint32_t k = 0; k < KMAX; ++k) {
+      uint32_t v = (k * P + p) * kMsThreads + tid;
+      asm volatile("" : "+v"(v));
+      if (k >= Kp) {
+        continue; // uniform
+      }
+      uint64_t nw = 0;
+      if (v < V && vis[k] != full) {
+        const uint32_t cs = __builtin_amdgcn_readfirstlane(v >> 6);
+        const uint32_t g0 = __builtin_amdgcn_readfirstlane(a.sell_off[cs]);
+        const uint32_t g1 = __builtin_amdgcn_readfirstlane(a.sell_off[cs + 1]);
+        const uint4* pp = a.sell4 + (size_t)g0 * 64 + (tid & 63u);
+        uint64_t acc = 0;
+        uint32_t g = g0;
+        for (; g + 2 <= g1; g += 2, pp += 128) {
+          const uint4 c0 = pp[0], c1 = pp[64];
+          acc |= cur[c0.x] | cur[c0.y] | cur[c0.z] | cur[c0.w] | cur[c1.x] | cur[c1.y] |
+                 cur[c1.z] | cur[c1.w];
+        }
+        if (g < g1) {
+          const uint4 c0 = pp[0];
+          acc |= cur[c0.x] | cur[c0.y] | cur[c0.z] | cur[c0.w];
+        }
+        nw = acc & ~vis[k];
+        vis[k] |= nw;
+      }
+      any |= nw != 0;
+      if (v < V) {
+        // write-through (sc1) store: visible to the other parts' XCDs with
+        // no release fence (an agent-scope release writes back the L2, full
+        // of this launch's level rows)
+        __hip_atomic_store((__attribute__((address_space(1))) uint64_t*)(xn + v),
+                           ((trm >> k) & 1u) ? nw : 0ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (nw) {
+        ms_record<uint64_t>(a, q0, v, nw, L);
+      }
+    }
+    // publish: this part's bits and its "any" flag, then the barrier
+    const bool mine = __syncthreads_or(any);
+    if (tid == 0) {
+      __hip_atomic_store(anyb + (L & 1u) * P + p, mine ? 1u : 0u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // every storing wave drains
+    __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_fetch_add(c.cnt + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t target = L * P;
+      uint32_t spins = 0;
+      while (__hip_atomic_load(c.cnt + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > kMsCoopSpin) {
+          atomicOr(c.err, 1u);
+          aborted = true;
+          break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads(); // every wave reads the other parts' words after the acquire
+    uint32_t flag = 0;
+    if (tid < P) {
+      flag = __hip_atomic_load(anyb + (L & 1u) * P + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const bool more = __syncthreads_or(flag != 0);
+    if (__syncthreads_or(aborted) || !more) {
+      break;
+    }
+    for (uint32_t v = tid; v < V; v += kMsThreads) {
+      cur[v] = xn[v];
+    }
+    __syncthreads();
+  }
+  // unreached (source, node) pairs of this part's nodes
+#pragma unroll
+  for (uint32_t k = 0; k < KMAX; ++k) {
+    const uint32_t v = (k * P + p) * kMsThreads + tid;
+    if (k < Kp && v < V) {
+      uint64_t miss = full & ~vis[k];
+      while (miss) {
+        const uint32_t s = (uint32_t)__builtin_ctzll(miss);
+        miss &= miss - 1;
+        a.dist_out[(size_t)(q0 + s) * a.Vp + v] = kInf32;
+        a.lvl_out[(size_t)(q0 + s) * a.Vp8 + v] = 255;
+      }
+    }
   }
 }
 
@@ -3454,12 +3630,19 @@ __device__ __forceinline__ void nl_dist_from_levels(
     const NhLevelsArgs& a, uint32_t q, uint32_t v0, uint32_t ls) {
   uint32_t* dw = a.dist_w + (size_t)q * a.Vp + v0;
   const uint32_t b[4] = {ls & 0xFFu, (ls >> 8) & 0xFFu, (ls >> 16) & 0xFFu, ls >> 24};
-  if (v0 + 4 <= a.V && b[0] < 255 && b[1] < 255 && b[2] < 255 && b[3] < 255) {
+  if (v0 + 4 <= a.V && !swar_zero_bytes(~ls)) { // no byte is 255
     nt_u32x4 w;
-    w.x = b[0] * a.scale;
-    w.y = b[1] * a.scale;
-    w.z = b[2] * a.scale;
-    w.w = b[3] * a.scale;
+    if (a.scale == 1) { // hop count / metric 1: no multiplies (quarter-rate v_mul_lo)
+      w.x = b[0];
+      w.y = b[1];
+      w.z = b[2];
+      w.w = b[3];
+    } else {
+      w.x = b[0] * a.scale;
+      w.y = b[1] * a.scale;
+      w.z = b[2] * a.scale;
+      w.w = b[3] * a.scale;
+    }
     st_stream(reinterpret_cast<nt_u32x4*>(dw), w, a.nt_store != 0);
     return;
   }
@@ -3900,6 +4083,16 @@ __device__ __forceinline__ bool nl_transit(const uint32_t* trbits, uint32_t f) {
 // padded by 64 entries, so reading past its end is safe) and the row offsets
 // are scalar products; missing neighbours read as 0xFF bytes, which match no
 // live node.
+// The pass's per-query tables are read-only for the kernel's lifetime: seen
+// through the constant address space, wave-uniform reads of them become
+// scalar loads (no vector trip + v_readfirstlane before the row loads)
+template <typename T>
+using nl_cptr = const __attribute__((address_space(4))) T*;
+template <typename T>
+__device__ __forceinline__ nl_cptr<T> nl_const(const T* p) {
+  return (nl_cptr<T>)p;
+}
+
 // A level word through the level table's buffer descriptor: the row offset
 // is a scalar (SGPR soffset) and the lane's node offset a 32-bit voffset, so
 // a load costs no vector address arithmetic (the 64-bit per-lane address of
@@ -3911,7 +4104,7 @@ __device__ __forceinline__ uint32_t nl_lvl_word(__amdgpu_buffer_rsrc_t rs, uint3
 }
 
 __device__ __forceinline__ void nl_v3_ld8(__amdgpu_buffer_rsrc_t rs, uint32_t v0, uint32_t Vp8,
-                                          const NlEnt* e, uint32_t rem, uint32_t (&lf)[8]) {
+                                          nl_cptr<NlEnt> e, uint32_t rem, uint32_t (&lf)[8]) {
   uint32_t r[8];
 #pragma unroll
   for (uint32_t kk = 0; kk < 8; ++kk) {
@@ -3931,7 +4124,7 @@ __device__ __forceinline__ void nl_v3_ld8(__amdgpu_buffer_rsrc_t rs, uint32_t v0
 // of a matching byte lands in bit kk of that byte of P.  Drained neighbours
 // (bit kk of ntg) match only their own node.
 __device__ __forceinline__ uint32_t nl_v3_cmp8(const uint32_t (&lf)[8], uint32_t tgt,
-                                               uint32_t live, uint32_t ntg, const NlEnt* e,
+                                               uint32_t live, uint32_t ntg, nl_cptr<NlEnt> e,
                                                uint32_t v0) {
   uint32_t P = 0;
 #pragma unroll
@@ -3985,7 +4178,8 @@ template <uint32_t T>
 __device__ __forceinline__ void nl_v2_solo(const NhLevelsArgs& a, const NlV2Args& v,
                                            uint32_t k, uint32_t c, uint64_t* tile,
                                            __amdgpu_buffer_rsrc_t rs) {
-  const NlSolo d = v.solo[k];
+  const nl_cptr<NlSolo> dp = nl_const(v.solo) + k;
+  const NlSolo d{dp->q, dp->n, dp->lo, dp->B, dp->nhb_off, dp->Wm, 0u};
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t vbase = c * (4 * T) + wv * 256;
   if (vbase >= a.V) {
@@ -3994,7 +4188,7 @@ __device__ __forceinline__ void nl_v2_solo(const NhLevelsArgs& a, const NlV2Args
   const uint32_t v0 = vbase + 4 * lane;
   const bool active = v0 < a.V;
   const uint8_t* lvl_v0 = a.lvl + v0;
-  const NlEnt* ent = v.ent + d.lo;
+  const nl_cptr<NlEnt> ent = nl_const(v.ent + d.lo);
   if (v.dbg & 8u) {
     // measurement: the pass's stores alone (same addresses, no loads)
     if (!active) {
@@ -4051,7 +4245,7 @@ __device__ __forceinline__ void nl_v2_solo(const NhLevelsArgs& a, const NlV2Args
   for (uint32_t w = 0; w < d.Wm; ++w) {
     const uint32_t cnt = min(64u, d.n - min(d.n, 64 * w));
     const uint64_t ntmask = w == 0 ? ntm[0] : (w == 1 ? ntm[1] : ntm[2]);
-    const NlEnt* ew = ent + 64 * w;
+    const nl_cptr<NlEnt> ew = ent + 64 * w;
     uint32_t P[8];
     uint32_t A[8], Bq[8];
     nl_v3_ld8(rs, v0, a.Vp8, ew, cnt, A);
@@ -4149,7 +4343,8 @@ template <uint32_t T>
 __device__ __forceinline__ void nl_v2_group(const NhLevelsArgs& a, const NlV2Args& v,
                                             uint32_t k, uint32_t c,
                                             __amdgpu_buffer_rsrc_t rs) {
-  const NlSub d = v.subs[k];
+  const nl_cptr<NlSub> dp = nl_const(v.subs) + k;
+  const NlSub d{dp->m0, dp->cnt, dp->n, dp->lo, dp->B, 0u};
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t vbase = c * (4 * T) + wv * 256;
   if (vbase >= a.V) {
@@ -4158,15 +4353,15 @@ __device__ __forceinline__ void nl_v2_group(const NhLevelsArgs& a, const NlV2Arg
   const uint32_t v0 = vbase + 4 * lane;
   const bool active = v0 < a.V;
   const uint8_t* lvl_v0 = a.lvl + v0;
-  const NlEnt* ent = v.ent + d.lo;
-  const NlMem* mem = v.mem + d.m0;
+  const nl_cptr<NlEnt> ent = nl_const(v.ent + d.lo);
+  const nl_cptr<NlMem> mem = nl_const(v.mem + d.m0);
   if (v.dbg & 8u) {
     // measurement: the group's stores alone (same addresses, no loads)
     if (!active) {
       return;
     }
     for (uint32_t i = 0; i < d.cnt; ++i) {
-      const NlMem m = mem[i];
+      const NlMem m{mem[i].q, 0u, mem[i].nhb_off};
       uint8_t* row = a.nhb + m.nhb_off;
       if (v0 + 4 <= a.V && !(v.dbg & 32u)) {
         if (d.B == 1) {
@@ -5797,6 +5992,10 @@ struct TraceCursorArgs {
   uint4* nstate;   // [waves][V] {tag, arena offset, length, cursor}
   uint2* arena;    // [waves][arena_cap] {tail, link} of pathLinks(v), in order
   uint32_t arena_cap;
+  // DFS steps one query may take on the device (OPENR_SPF_TRACE_BUDGET,
+  // default unlimited): a query past it is reported as an overflow and traced
+  // on the host from its row.
+  uint32_t budget = 0xFFFFFFFFu;
   uint32_t V;
   // OPENR_SPF_TRACE_STATS=1: per query {wall ticks (100 MHz), DFS steps,
   // pathLinks lists built, their filter ticks, rank ticks, entries}; nullptr = off
@@ -6025,7 +6224,10 @@ __global__ __launch_bounds__(64 * kTcWaves) void spf_trace_cursor_kernel(TraceCu
         tc_sync();
         bool found = false;
         for (;;) {
-          ++nsteps;
+          if (++nsteps > A.budget) {
+            overflow = true;
+            break;
+          }
           st = fst[depth];
           if (st.w >= st.z) {
             // v exhausted: the search through it fails; its state goes back
@@ -6273,6 +6475,15 @@ struct spf_graph {
   // d_slot; d_wout, d_win, d_w64; d_cw) and of d_link_half: spf_graph_update
   // rebuilds in place and reallocates only what outgrew its buffer
   size_t cap_e = 0, cap_w = 0, cap_cw = 0, cap_half = 0;
+  // host scratch of the preparation passes, kept for in-place rebuilds
+  std::vector<uint32_t> scratch_e, scratch_v, scratch_slot;
+  std::vector<uint32_t> h_wout, h_win, h_cw;
+  // spf_graph_update: the CSR and neighbour lists it replaced (reused rows)
+  std::vector<uint32_t> old_row, old_col, old_nbr_off, old_nbrs, old_slot;
+  // pinned staging of the preparation uploads (g_stage): one DMA per array
+  // on the graph stream instead of a pageable synchronous hipMemcpy each
+  char* pin = nullptr;
+  size_t pin_cap = 0, pin_off = 0;
   // spf_table_repair's delta block + per-workgroup queues, kept between
   // calls (a 100k-node graph needs 200 MB: allocating it per churn event
   // cost more than the screen)
@@ -6326,6 +6537,11 @@ struct spf_query {
   uint8_t* d_lvl = nullptr;
   uint32_t* d_flags = nullptr;
   uint32_t ms_par = 0; // the flag word (0 / 1) of the last MS-BFS launch
+  // cooperative MS-BFS (spf_msbfs_coop_kernel): exchange buffer, barrier
+  // counters, per-part flags and the error word, in one pooled block
+  void* d_coop = nullptr;
+  size_t coop_bytes = 0;
+  uint32_t coop_p = 0; // parts per batch of the last launch (0: plain kernel)
   size_t lds_bytes = 0;
   bool has_ign = false;
   // next-hop masks.  Working layout (u64 words, nh_w[i] per node, query i at
@@ -6681,6 +6897,56 @@ int build_nl_v2(spf_query* q, const uint32_t* sources, const std::vector<int32_t
   return SPF_OK;
 }
 
+// Host -> device upload through the graph's pinned staging buffer: the bytes
+// are copied into it and one async DMA is queued on the graph stream
+// (pageable hipMemcpy measured ~1-2 GB/s in a link flap's rebuild,
+// profiles/r05p).  g_stage_flush waits for them.
+int g_stage(spf_graph* g, void* dst, const void* src, size_t bytes) {
+  if (!bytes) {
+    return SPF_OK;
+  }
+  const size_t need = (bytes + 255) & ~(size_t)255;
+  if (g->pin_off + need > g->pin_cap) {
+    HIP_TRY(hipStreamSynchronize(g->stream)); // queued copies read the buffer
+    g->pin_off = 0;
+    if (need > g->pin_cap) {
+      if (g->pin) {
+        (void)hipHostFree(g->pin);
+      }
+      g->pin = nullptr;
+      g->pin_cap = 0;
+      const size_t c = std::max<size_t>(need, (size_t)16 << 20);
+      if (hipHostMalloc((void**)&g->pin, c, hipHostMallocDefault) != hipSuccess) {
+        g->pin = nullptr;
+        (void)hipGetLastError();
+        HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice)); // unpinned fallback
+        return SPF_OK;
+      }
+      g->pin_cap = c;
+    }
+  }
+  std::memcpy(g->pin + g->pin_off, src, bytes);
+  HIP_TRY(hipMemcpyAsync(dst, g->pin + g->pin_off, bytes, hipMemcpyHostToDevice, g->stream));
+  g->pin_off += need;
+  return SPF_OK;
+}
+
+int g_stage_flush(spf_graph* g) {
+  HIP_TRY(hipStreamSynchronize(g->stream));
+  g->pin_off = 0;
+  return SPF_OK;
+}
+
+template <typename T>
+int dev_upload_g(spf_graph* g, T** dst, const T* src, size_t n) {
+  *dst = nullptr;
+  if (n == 0) {
+    return SPF_OK;
+  }
+  HIP_TRY(hipMalloc((void**)dst, n * sizeof(T)));
+  return g_stage(g, *dst, src, n * sizeof(T));
+}
+
 // OPENR_SPF_CREATE_TIMING=1: phase times of spf_graph_create / _update on
 // stderr (measurement); mark("phase") closes the phase that ends there
 struct PhaseTimer {
@@ -6702,6 +6968,9 @@ struct PhaseTimer {
     }
   }
 };
+
+// the running create / update's timer (upload_weights marks its sub-phases)
+thread_local PhaseTimer* tl_phase = nullptr;
 
 // spf_graph_create / spf_graph_update: the CSR arrays are present and every
 // half-edge has a consistent reverse (node blocks on the host pool; the lowest
@@ -6755,6 +7024,9 @@ void free_graph(spf_graph* g) {
     return;
   }
   (void)hipSetDevice(g->device);
+  if (g->stream) {
+    (void)hipStreamSynchronize(g->stream); // staged uploads may still be in flight
+  }
   for (void* p :
        {(void*)g->d_row, (void*)g->d_col, (void*)g->d_wout, (void*)g->d_win,
         (void*)g->d_link, (void*)g->d_rev, (void*)g->d_slot, (void*)g->d_tr,
@@ -6767,6 +7039,9 @@ void free_graph(spf_graph* g) {
   }
   if (g->own_stream) {
     (void)hipStreamDestroy(g->own_stream);
+  }
+  if (g->pin) {
+    (void)hipHostFree(g->pin);
   }
   delete g;
 }
@@ -6787,7 +7062,8 @@ void free_query(spf_query* q) {
         (void*)q->d_skip, (void*)q->d_key, (void*)q->d_qctr, (void*)q->d_scatter,
         (void*)q->d_trace, (void*)q->d_big, (void*)q->d_held_order, (void*)q->d_zl,
         (void*)q->d_zvar, (void*)q->d_ms_mask, (void*)q->d_ms_flag,
-        (void*)q->d_ovf, q->narrow ? (void*)q->d_nhb : nullptr, (void*)q->d_tcs, q->d_v2}) {
+        (void*)q->d_ovf, q->narrow ? (void*)q->d_nhb : nullptr, (void*)q->d_tcs, q->d_v2,
+        q->d_coop}) {
     pool_free(p);
   }
   if (q->base) {
@@ -6821,32 +7097,87 @@ void free_query(spf_query* q) {
 // staged in scratch[row[u] ..], counted, then packed; node blocks on the host
 // pool).  A half-edge taken down in place (spf_graph_set_edges) is no
 // neighbour; its slot is 0 (it is never tight, so never read).
-void build_nbr_lists(spf_graph* g) {
+// (reuse: the previous CSR's row / col / nbr_off / nbrs / slot, when the
+// graph is rebuilt in place: a row whose heads are unchanged keeps its
+// distinct-neighbour list and slots, shifted to the new offsets)
+struct NbrReuse {
+  const std::vector<uint32_t>* row = nullptr;
+  const std::vector<uint32_t>* col = nullptr;
+  const std::vector<uint32_t>* nbr_off = nullptr;
+  const std::vector<uint32_t>* nbrs = nullptr;
+  const std::vector<uint32_t>* slot = nullptr;
+};
+
+void build_nbr_lists(spf_graph* g, const NbrReuse* old = nullptr) {
   ++g->nbr_gen;
   const uint32_t V = g->V, E = g->E;
   const bool patched = !g->edge_up.empty();
-  g->nbr_off.assign(V + 1, 0);
-  g->slot.assign(E, 0);
-  std::vector<uint32_t> scratch(E);
-  std::vector<uint32_t> cnt(V, 0);
+  g->nbr_off.resize(V + 1);
+  g->nbr_off[0] = 0;
+  g->slot.resize(E); // every up half-edge's slot is written below
+  if (patched) {
+    std::fill(g->slot.begin(), g->slot.end(), 0u);
+  }
+  // kept between calls (a link flap rebuilds the lists; fresh vectors cost
+  // their page faults every time)
+  std::vector<uint32_t>& scratch = g->scratch_e;
+  std::vector<uint32_t>& cnt = g->scratch_v;
+  scratch.resize(E);
+  cnt.resize(V);
   const uint32_t nblk = (V + kHostBlock - 1) / kHostBlock;
   const unsigned nth = openr::hostThreads(E, kHostMinEdges);
-  openr::parallelFor(nblk, nth, [&](size_t b, unsigned) {
+  // per worker: neighbour -> slot of the row being processed (written before
+  // it is read, never cleared)
+  if (g->scratch_slot.size() < (size_t)nth * V) {
+    g->scratch_slot.resize((size_t)nth * V);
+  }
+  openr::parallelFor(nblk, nth, [&](size_t b, unsigned w) {
+    uint32_t* idx = g->scratch_slot.data() + (size_t)w * V;
     const uint32_t u1 = std::min<uint32_t>(V, (uint32_t)(b + 1) * kHostBlock);
     for (uint32_t u = (uint32_t)b * kHostBlock; u < u1; ++u) {
-      uint32_t* lo = scratch.data() + g->row[u];
-      uint32_t* hi = lo;
-      for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
-        if (!patched || g->edge_up[e]) {
-          *hi++ = g->col[e];
+      const uint32_t e0 = g->row[u], e1 = g->row[u + 1];
+      uint32_t* lo = scratch.data() + e0;
+      if (old && !patched) {
+        const uint32_t o0 = (*old->row)[u], o1 = (*old->row)[u + 1];
+        if (o1 - o0 == e1 - e0 &&
+            std::equal(g->col.begin() + e0, g->col.begin() + e1, old->col->begin() + o0)) {
+          const uint32_t n0 = (*old->nbr_off)[u], n1 = (*old->nbr_off)[u + 1];
+          std::copy(old->nbrs->begin() + n0, old->nbrs->begin() + n1, lo);
+          std::copy(old->slot->begin() + o0, old->slot->begin() + o1, g->slot.begin() + e0);
+          cnt[u] = n1 - n0;
+          continue;
         }
       }
-      std::sort(lo, hi);
-      hi = std::unique(lo, hi);
-      cnt[u] = (uint32_t)(hi - lo);
-      for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
+      uint32_t* hi = lo;
+      bool sorted = true;
+      uint32_t prev = 0;
+      for (uint32_t e = e0; e < e1; ++e) {
         if (!patched || g->edge_up[e]) {
-          g->slot[e] = (uint32_t)(std::lower_bound(lo, hi, g->col[e]) - lo);
+          const uint32_t c = g->col[e];
+          sorted = sorted && (hi == lo || c > prev);
+          prev = c;
+          *hi++ = c;
+        }
+      }
+      if (sorted && !patched) {
+        // the common row: distinct neighbours already ascending
+        cnt[u] = (uint32_t)(hi - lo);
+        for (uint32_t e = e0; e < e1; ++e) {
+          g->slot[e] = e - e0;
+        }
+        continue;
+      }
+      if (!sorted) {
+        std::sort(lo, hi);
+        hi = std::unique(lo, hi);
+      }
+      cnt[u] = (uint32_t)(hi - lo);
+      for (uint32_t* p = lo; p < hi; ++p) {
+        idx[*p] = (uint32_t)(p - lo);
+      }
+      for (uint32_t e = e0; e < e1; ++e) {
+        if (!patched || g->edge_up[e]) {
+          g->slot[e] = idx[g->col[e]];
         }
       }
     }
@@ -6950,22 +7281,34 @@ int upload_weights(spf_graph* g) {
     }, 1);
   };
   std::vector<uint64_t> wmax(nth, 0), wsum(nth, 0);
-  std::vector<uint8_t> wwrap(nth, 0);
+  std::vector<uint8_t> wwrap(nth, 0), wsame(nth, 1);
   std::vector<std::vector<uint32_t>> zeros(nth);
-  blocks([&](uint32_t u, unsigned w) {
-    for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
+  const uint64_t w0 = E ? g->w64[0] : 0;
+  // per-block locals, folded into the per-worker slots once per block (the
+  // slots of all workers share cache lines: updating them per edge made this
+  // scan ~6 ms of false sharing on the fabric, profiles/r05s)
+  openr::parallelFor(nblk, nth, [&](size_t b, unsigned w) {
+    const uint32_t u0 = (uint32_t)b * kHostBlock, u1 = std::min<uint32_t>(V, u0 + kHostBlock);
+    uint64_t mx = 0, sm = 0;
+    bool wrap = false, same = true;
+    for (uint32_t e = g->row[u0]; e < g->row[u1]; ++e) {
       const uint64_t m = g->w64[e];
       if (m > 0x7FFFFFFFull) {
-        wwrap[w] = 1;
+        wrap = true;
       } else {
-        wsum[w] += m;
+        sm += m;
       }
       if (m == 0) {
         zeros[w].push_back(e);
       }
-      wmax[w] = std::max(wmax[w], m);
+      mx = std::max(mx, m);
+      same = same && m == w0;
     }
-  });
+    wmax[w] = std::max(wmax[w], mx);
+    wsum[w] += sm;
+    wwrap[w] |= (uint8_t)wrap;
+    wsame[w] &= (uint8_t)same;
+  }, 1);
   uint64_t maxw = 0, sumw = 0;
   bool wrap = false;
   std::vector<uint32_t> zero_e;
@@ -6975,6 +7318,7 @@ int upload_weights(spf_graph* g) {
     wrap = wrap || wwrap[w];
     zero_e.insert(zero_e.end(), zeros[w].begin(), zeros[w].end());
   }
+  if (tl_phase) (*tl_phase)("w:scan");
   std::sort(zero_e.begin(), zero_e.end());
   g->wrap = wrap;
   g->n_zero = (uint32_t)zero_e.size();
@@ -6989,23 +7333,30 @@ int upload_weights(spf_graph* g) {
   }
   if (!zero_e.empty()) {
     HIP_TRY(hipMalloc((void**)&g->d_zero_e, zero_e.size() * 4));
-    HIP_TRY(hipMemcpy(g->d_zero_e, zero_e.data(), zero_e.size() * 4, hipMemcpyHostToDevice));
+    if (const int st = g_stage(g, g->d_zero_e, zero_e.data(), zero_e.size() * 4)) {
+      return st;
+    }
   }
   g->uniform = 0;
   if (!exact && E) {
-    const uint64_t c = g->w64[0];
     bool same = true;
-    for (uint32_t e = 1; e < E && same; ++e) {
-      same = g->w64[e] == c;
+    for (unsigned w = 0; w < nth; ++w) {
+      same = same && wsame[w];
     }
-    g->uniform = same ? (uint32_t)c : 0;
+    g->uniform = same ? (uint32_t)w0 : 0;
   }
-  std::vector<uint32_t> wout(E), win(E);
+  if (tl_phase) (*tl_phase)("w:exact+zero");
+  // host staging kept on the graph (in-place rebuilds: no page faults)
+  std::vector<uint32_t>& wout = g->h_wout;
+  std::vector<uint32_t>& win = g->h_win;
+  wout.resize(E);
+  win.resize(E);
   blocks([&](uint32_t u, unsigned) {
     for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
       wout[e] = (uint32_t)std::min<uint64_t>(g->w64[e], 0xFFFFFFFFull);
     }
   });
+  if (tl_phase) (*tl_phase)("w:wout");
   // cheapest usable link to each distinct neighbour (parallel links)
   g->nbr_w.assign(g->nbrs.size(), 0xFFFFFFFFu);
   blocks([&](uint32_t u, unsigned) {
@@ -7015,6 +7366,7 @@ int upload_weights(spf_graph* g) {
       w = std::min(w, wout[e]);
     }
   });
+  if (tl_phase) (*tl_phase)("w:nbr_w");
   if (E) {
     if (!g->d_wout || E > g->cap_w) {
       for (void* p : {(void*)g->d_wout, (void*)g->d_win, (void*)g->d_w64}) {
@@ -7032,12 +7384,15 @@ int upload_weights(spf_graph* g) {
       // d_nbrs / d_nbr_w share nbr_cap (the caller sizes d_nbrs first)
       return fail(SPF_E_INVALID, "neighbour-weight buffer smaller than the neighbour lists");
     }
-    HIP_TRY(hipMemcpy(g->d_wout, wout.data(), E * 4, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(g->d_win, win.data(), E * 4, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(g->d_w64, g->w64.data(), E * 8, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(g->d_nbr_w, g->nbr_w.data(), g->nbr_w.size() * 4,
-                      hipMemcpyHostToDevice));
+    int st = SPF_OK;
+    if ((st = g_stage(g, g->d_wout, wout.data(), (size_t)E * 4)) ||
+        (st = g_stage(g, g->d_win, win.data(), (size_t)E * 4)) ||
+        (st = g_stage(g, g->d_w64, g->w64.data(), (size_t)E * 8)) ||
+        (st = g_stage(g, g->d_nbr_w, g->nbr_w.data(), g->nbr_w.size() * 4))) {
+      return st;
+    }
   }
+  if (tl_phase) (*tl_phase)("w:stage");
   g->ecc_est = 0;
   // packed out-edges for the push-only delta-stepping pass
   uint32_t bits = 1;
@@ -7051,7 +7406,8 @@ int upload_weights(spf_graph* g) {
   }
   g->cw_bits = 0;
   if (pack) {
-    std::vector<uint32_t> cw(E);
+    std::vector<uint32_t>& cw = g->h_cw;
+    cw.resize(E);
     blocks([&](uint32_t u, unsigned) {
       for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
         cw[e] = g->col[e] | (wout[e] << bits);
@@ -7067,7 +7423,9 @@ int upload_weights(spf_graph* g) {
       HIP_TRY(hipMalloc((void**)&g->d_cw, c * 4));
       g->cap_cw = c;
     }
-    HIP_TRY(hipMemcpy(g->d_cw, cw.data(), cw.size() * 4, hipMemcpyHostToDevice));
+    if (const int st = g_stage(g, g->d_cw, cw.data(), cw.size() * 4)) {
+      return st;
+    }
     g->cw_bits = bits;
   }
   return SPF_OK;
@@ -7103,9 +7461,9 @@ int upload_sell(spf_graph* g) {
     }
   }
   g->sell_off = off;
-  int s = dev_upload(&g->d_sell_off, off.data(), off.size());
+  int s = dev_upload_g(g, &g->d_sell_off, off.data(), off.size());
   if (s == SPF_OK && !sell.empty()) {
-    s = dev_upload((uint32_t**)&g->d_sell, sell.data(), sell.size());
+    s = dev_upload_g(g, (uint32_t**)&g->d_sell, sell.data(), sell.size());
   }
   return s;
 }
@@ -7590,14 +7948,14 @@ int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
   g->stream = g->own_stream;
   mark("dev/stream");
   int s = SPF_OK;
-  if ((s = dev_upload(&g->d_row, g->row.data(), V + 1)) ||
-      (s = dev_upload(&g->d_col, g->col.data(), E)) ||
-      (s = dev_upload(&g->d_link, g->link.data(), E)) ||
-      (s = dev_upload(&g->d_rev, g->rev.data(), E)) ||
-      (s = dev_upload(&g->d_slot, g->slot.data(), E)) ||
-      (s = dev_upload(&g->d_tr, g->trbits.data(), g->trbits.size())) ||
-      (s = dev_upload(&g->d_nbr_off, g->nbr_off.data(), V + 1)) ||
-      (s = dev_upload(&g->d_nbrs, g->nbrs.data(), g->nbrs.size()))) {
+  if ((s = dev_upload_g(g, &g->d_row, g->row.data(), V + 1)) ||
+      (s = dev_upload_g(g, &g->d_col, g->col.data(), E)) ||
+      (s = dev_upload_g(g, &g->d_link, g->link.data(), E)) ||
+      (s = dev_upload_g(g, &g->d_rev, g->rev.data(), E)) ||
+      (s = dev_upload_g(g, &g->d_slot, g->slot.data(), E)) ||
+      (s = dev_upload_g(g, &g->d_tr, g->trbits.data(), g->trbits.size())) ||
+      (s = dev_upload_g(g, &g->d_nbr_off, g->nbr_off.data(), V + 1)) ||
+      (s = dev_upload_g(g, &g->d_nbrs, g->nbrs.data(), g->nbrs.size()))) {
     return bail(s);
   }
   g->nbr_cap = g->nbrs.size();
@@ -7615,13 +7973,16 @@ int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
     for (uint32_t e = 0; e < E; ++e) {
       half[2 * (size_t)g->link[e] + (e < g->rev[e] ? 0 : 1)] = e;
     }
-    if ((s = dev_upload(&g->d_link_half, half.data(), half.size()))) {
+    if ((s = dev_upload_g(g, &g->d_link_half, half.data(), half.size()))) {
       return bail(s);
     }
     g->cap_half = half.size();
   }
   mark("link halves");
   if (V && V <= kMsThreads * kMsMaxK && (s = upload_sell(g))) {
+    return bail(s);
+  }
+  if ((s = g_stage_flush(g))) {
     return bail(s);
   }
   mark("sliced ELL");
@@ -7648,6 +8009,10 @@ int spf_graph_update(spf_graph* g, const spf_graph_desc* desc) {
     return fail(SPF_E_INVALID, "spf_graph_update: the node set changed (create a new graph)");
   }
   PhaseTimer mark("spf_graph_update");
+  struct PhaseScope {
+    explicit PhaseScope(PhaseTimer* t) { tl_phase = t->on ? t : nullptr; }
+    ~PhaseScope() { tl_phase = nullptr; }
+  } phase_scope(&mark);
   if (const int vs = validate_graph_desc(desc)) {
     return vs;
   }
@@ -7656,6 +8021,14 @@ int spf_graph_update(spf_graph* g, const spf_graph_desc* desc) {
   HIP_TRY(hipSetDevice(g->device));
   HIP_TRY(hipStreamSynchronize(g->stream)); // queued work reads the old arrays
   mark("sync");
+  // the previous CSR and its neighbour lists: unchanged rows keep theirs
+  // (a flap changes the rows of its two endpoints only)
+  const bool reuse = !g->links_patched && g->edge_up.empty();
+  std::swap(g->row, g->old_row);
+  std::swap(g->col, g->old_col);
+  std::swap(g->nbr_off, g->old_nbr_off);
+  std::swap(g->nbrs, g->old_nbrs);
+  std::swap(g->slot, g->old_slot);
   g->E = E;
   g->L = desc->num_links;
   g->row.assign(desc->row_ptr, desc->row_ptr + V + 1);
@@ -7674,7 +8047,8 @@ int spf_graph_update(spf_graph* g, const spf_graph_desc* desc) {
   g->edge_up.clear();
   g->links_patched = false;
   mark("host copy");
-  build_nbr_lists(g);
+  NbrReuse nr{&g->old_row, &g->old_col, &g->old_nbr_off, &g->old_nbrs, &g->old_slot};
+  build_nbr_lists(g, reuse && g->old_row.size() == (size_t)V + 1 ? &nr : nullptr);
   mark("nbr lists");
   // edge-sized arrays: rewritten in place, or reallocated with headroom
   auto store32 = [&](uint32_t** d, const std::vector<uint32_t>& h, size_t& cap) -> int {
@@ -7687,10 +8061,7 @@ int spf_graph_update(spf_graph* g, const spf_graph_desc* desc) {
       HIP_TRY(hipMalloc((void**)d, c * 4));
       cap = c;
     }
-    if (!h.empty()) {
-      HIP_TRY(hipMemcpy(*d, h.data(), h.size() * 4, hipMemcpyHostToDevice));
-    }
-    return SPF_OK;
+    return g_stage(g, *d, h.data(), h.size() * 4);
   };
   int s = SPF_OK;
   size_t cap_e = g->cap_e, cap_nbr = g->nbr_cap, cap_v = (size_t)V + 1;
@@ -7710,7 +8081,9 @@ int spf_graph_update(spf_graph* g, const spf_graph_desc* desc) {
     return s;
   }
   g->cap_e = std::max(c1, (size_t)E);
-  HIP_TRY(hipMemcpy(g->d_tr, g->trbits.data(), g->trbits.size() * 4, hipMemcpyHostToDevice));
+  if ((s = g_stage(g, g->d_tr, g->trbits.data(), g->trbits.size() * 4))) {
+    return s;
+  }
   if (g->nbrs.size() > cap_nbr || !g->d_nbrs) {
     for (uint32_t** d : {&g->d_nbrs, &g->d_nbr_w}) {
       if (*d) {
@@ -7723,8 +8096,8 @@ int spf_graph_update(spf_graph* g, const spf_graph_desc* desc) {
     HIP_TRY(hipMalloc((void**)&g->d_nbr_w, c * 4));
     g->nbr_cap = c;
   }
-  if (!g->nbrs.empty()) {
-    HIP_TRY(hipMemcpy(g->d_nbrs, g->nbrs.data(), g->nbrs.size() * 4, hipMemcpyHostToDevice));
+  if ((s = g_stage(g, g->d_nbrs, g->nbrs.data(), g->nbrs.size() * 4))) {
+    return s;
   }
   mark("csr upload");
   if ((s = upload_weights(g))) {
@@ -7750,6 +8123,9 @@ int spf_graph_update(spf_graph* g, const spf_graph_desc* desc) {
   }
   mark("link halves");
   if (V && V <= kMsThreads * kMsMaxK && (s = upload_sell(g))) {
+    return s;
+  }
+  if ((s = g_stage_flush(g))) {
     return s;
   }
   mark("sliced ELL");
@@ -7864,7 +8240,10 @@ int spf_graph_patch_metrics(
     g->w64[edge_idx[i]] = m[i];
   }
   HIP_TRY(hipStreamSynchronize(g->stream));
-  return upload_weights(g);
+  if (const int st = upload_weights(g)) {
+    return st;
+  }
+  return g_stage_flush(g);
 }
 
 int spf_graph_set_edges(
@@ -8833,7 +9212,7 @@ int launch_sssp(spf_query* q) {
   HIP_TRY(hipFuncSetAttribute(
       (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
       (int)q->lds_bytes));
-  SPF_LAUNCH(
+  SPF_LAUNCH_AS("spf_sssp_kernel", 
       kern, dim3(q->grid), dim3(kBlock), q->lds_bytes, g->stream, a);
   HIP_TRY(hipGetLastError());
   if (a.stats) {
@@ -8943,7 +9322,7 @@ int launch_dstep_t(spf_query* q) {
     HIP_TRY(hipMalloc((void**)&d.stats, 8 * sizeof(unsigned long long)));
     HIP_TRY(hipMemsetAsync(d.stats, 0, 8 * sizeof(unsigned long long), g->stream));
   }
-  SPF_LAUNCH(kern, dim3(q->grid), dim3(BS), lds, g->stream, d);
+  SPF_LAUNCH_AS("spf_dstep_kernel", kern, dim3(q->grid), dim3(BS), lds, g->stream, d);
   HIP_TRY(hipGetLastError());
   if (d.stats) {
     unsigned long long h[8];
@@ -9018,7 +9397,7 @@ int launch_dlds(spf_query* q) {
   }
   HIP_TRY(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)q->dlds_lds));
-  SPF_LAUNCH(kern, dim3(q->dlds_grid), dim3(1024), q->dlds_lds, g->stream, a);
+  SPF_LAUNCH_AS("spf_dlds_kernel", kern, dim3(q->dlds_grid), dim3(1024), q->dlds_lds, g->stream, a);
   HIP_TRY(hipGetLastError());
   if (a.stats) {
     unsigned long long h[8];
@@ -9066,7 +9445,7 @@ int launch_msdstep(spf_query* q) {
   HIP_TRY(hipFuncSetAttribute(
       (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
       (int)q->lds_bytes));
-  SPF_LAUNCH(kern, dim3(q->grid), dim3(1024), q->lds_bytes, g->stream, a);
+  SPF_LAUNCH_AS("spf_msdstep_kernel", kern, dim3(q->grid), dim3(1024), q->lds_bytes, g->stream, a);
   HIP_TRY(hipGetLastError());
   return SPF_OK;
 }
@@ -9092,7 +9471,7 @@ int launch_bfs(spf_query* q, bool unit) {
   HIP_TRY(hipFuncSetAttribute(
       (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
       (int)q->lds_bytes));
-  SPF_LAUNCH(
+  SPF_LAUNCH_AS("spf_bfs_kernel", 
       kern, dim3(q->grid), dim3(kBlock), q->lds_bytes, g->stream, a);
   HIP_TRY(hipGetLastError());
   return SPF_OK;
@@ -9160,6 +9539,7 @@ int launch_msbfs(spf_query* q, bool unit) {
   a.zlist = nullptr;
   a.nz = 0;
   a.lvl_only = lvl_only(q) ? 1u : 0u;
+  a.norec = env_u32("OPENR_MS_NOREC", 0);
   q->ms_par ^= 1u;
   a.flags = q->d_flags + q->ms_par;
   a.flags_clear = q->d_flags + (q->ms_par ^ 1u);
@@ -9213,6 +9593,61 @@ int launch_msbfs(spf_query* q, bool unit) {
     }
   }
 #undef MS_PICK
+  // a block of a sharded table (few batches): split each batch over P
+  // workgroups when P >= 2 of them fit beside one another (OPENR_MS_COOP)
+  q->coop_p = 0;
+  // opt-in (OPENR_MS_COOP=1): measured slower than one workgroup per batch at
+  // every rank size (N = 8 block: 0.122 vs 0.117 ms; with the row stores off
+  // 0.122 vs 0.064 ms, profiles/r05u): a level's barrier, acquire and frontier
+  // reload cost ~7 us against ~8 us of pull work split P ways
+  if (!gen && q->ms_bits == 64 && sell && q->zvars == 0 && g->V <= 8u * kMsThreads * 2u &&
+      env_flag("OPENR_MS_COOP", 0)) {
+    const uint32_t nbatch = (q->nrows + 63) / 64;
+    const void* ck = (const void*)spf_msbfs_coop_kernel<8>;
+    const size_t clds = (size_t)g->V * 8;
+    int per_cu = 0;
+    if (nbatch && hipFuncSetAttribute(ck, hipFuncAttributeMaxDynamicSharedMemorySize, (int)clds) ==
+            hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ck, kMsThreads, clds) == hipSuccess &&
+        per_cu > 0) {
+      const uint32_t cap = (uint32_t)per_cu * (uint32_t)g->num_cus;
+      const uint32_t pmax = std::max<uint32_t>(1, std::min<uint32_t>(16, env_u32("OPENR_MS_COOP_P", 8)));
+      uint32_t P = std::min<uint32_t>(pmax, cap / nbatch);
+      // each part owns whole 1,024-node slots: no more parts than slots
+      P = std::min<uint32_t>(P, (g->V + kMsThreads - 1) / kMsThreads);
+      if (P >= 2) {
+        const size_t xb = (size_t)nbatch * 2 * g->V * 8;
+        const size_t need = xb + (size_t)nbatch * 4 + (size_t)nbatch * 2 * P * 4 + 16;
+        if (q->d_coop && q->coop_bytes < need) {
+          HIP_TRY(hipStreamSynchronize(g->stream));
+          pool_free(q->d_coop);
+          q->d_coop = nullptr;
+        }
+        if (!q->d_coop) {
+          HIP_TRY(pool_malloc(&q->d_coop, need));
+          q->coop_bytes = need;
+          HIP_TRY(hipMemsetAsync(q->d_coop, 0, need, g->stream));
+        }
+        MsCoopArgs c;
+        c.a = a;
+        c.xbuf = reinterpret_cast<uint64_t*>(q->d_coop);
+        c.cnt = reinterpret_cast<uint32_t*>(static_cast<char*>(q->d_coop) + xb);
+        c.anyv = c.cnt + nbatch;
+        c.err = c.anyv + (size_t)nbatch * 2 * P;
+        c.P = P;
+        HIP_TRY(hipMemsetAsync(c.cnt, 0, (size_t)nbatch * 4, g->stream));
+        void* cargs[] = {&c};
+        spf_note_launch("spf_msbfs_coop_kernel");
+        const hipError_t le = hipLaunchCooperativeKernel(ck, dim3(nbatch * P), dim3(kMsThreads),
+                                                         cargs, (unsigned)clds, g->stream);
+        if (le == hipSuccess) {
+          q->coop_p = P;
+          return SPF_OK;
+        }
+        (void)hipGetLastError(); // not co-resident: the plain kernel below
+      }
+    }
+  }
   HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)q->lds_bytes));
   const uint32_t ntab = std::max<uint32_t>(1, q->zvars);
@@ -9224,6 +9659,7 @@ int launch_msbfs(spf_query* q, bool unit) {
       a.nz = q->zoff[j + 1] - q->zoff[j];
     }
     void* args[] = {&a};
+    spf_note_launch("spf_msbfs_kernel");
     HIP_TRY(hipLaunchKernel(kern, dim3(q->grid), dim3(kMsThreads), args,
                             q->lds_bytes, g->stream));
     HIP_TRY(hipGetLastError());
@@ -9718,6 +10154,18 @@ int spf_query_sync(spf_query* q) {
   }
   HIP_TRY(hipSetDevice(q->g->device));
   HIP_TRY(hipStreamSynchronize(q->g->stream));
+  if (q->coop_p) {
+    // a cooperative MS-BFS barrier that gave up leaves its rows incomplete
+    const uint32_t nbatch = (q->nrows + 63) / 64;
+    const size_t off = (size_t)nbatch * 2 * q->g->V * 8 + (size_t)nbatch * 4 +
+                       (size_t)nbatch * 2 * q->coop_p * 4;
+    uint32_t err = 0;
+    HIP_TRY(hipMemcpy(&err, static_cast<char*>(q->d_coop) + off, 4, hipMemcpyDeviceToHost));
+    if (err) {
+      HIP_TRY(hipMemset(static_cast<char*>(q->d_coop) + off, 0, 4));
+      return fail(SPF_E_DEVICE, "cooperative MS-BFS: a level barrier timed out");
+    }
+  }
   return SPF_OK;
 }
 
@@ -10087,6 +10535,10 @@ int spf_query_trace_paths(
     ta.arena = reinterpret_cast<uint2*>(q->d_tcs + (size_t)nw * g->V * sizeof(uint4));
     ta.arena_cap = acap;
     ta.V = g->V;
+    // no budget by default: at 4,096 steps 252 fabric queries went to the host,
+    // whose traces cost more than the device's (KSP2 build 58 -> 74 ms,
+    // profiles/r05s); the knob stays for tests and measurements
+    ta.budget = env_u32("OPENR_SPF_TRACE_BUDGET", 0xFFFFFFFFu);
     HIP_TRY(hipMemsetAsync(q->d_tcs, 0, (size_t)nw * g->V * sizeof(uint4), g->stream));
     if (env_flag("OPENR_SPF_TRACE_STATS", 0)) {
       HIP_TRY(hipMalloc((void**)&ta.qstat, (size_t)count * kTcStat * 8));
@@ -10679,7 +11131,7 @@ int spf_table_repair(
                             (int)lds) != hipSuccess) {
       st = fail(SPF_E_DEVICE, "LDS attribute");
     } else {
-      SPF_LAUNCH(kern, dim3(grid), dim3(1024), lds, g->stream, da);
+      SPF_LAUNCH_AS("spf_dstep_kernel", kern, dim3(grid), dim3(1024), lds, g->stream, da);
       if (hipGetLastError() != hipSuccess || hipStreamSynchronize(g->stream) != hipSuccess) {
         st = fail(SPF_E_DEVICE, "repair kernel failed");
       }

@@ -1,0 +1,10 @@
+set -o pipefail
+# round 5: full GPU suite + smoke at HEAD (coop MS-BFS opt-in; unchanged rows
+# keep their neighbour lists on spf_graph_update) + link-flap probe + bench
+D=gpurun_out/r05v; mkdir -p $D
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $D/gpu_tests.log 2>&1 || { tail -30 $D/gpu_tests.log; exit 3; }
+tail -1 $D/gpu_tests.log
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $D/smoke.log 2>&1 || { tail -20 $D/smoke.log; exit 4; }
+tail -1 $D/smoke.log
+OPENR_SPF_CREATE_TIMING=1 timeout -k 10 300 python3 profiles/linkflap_probe.py > $D/linkflap.json 2> $D/linkflap.err || { tail -5 $D/linkflap.err; exit 5; }
+python3 -c "import json; d=json.load(open('$D/linkflap.json')); print({k: d.get(k) for k in ('ms_median','update_ms_median','build_ms_median','parity_check','per_build_us')})"

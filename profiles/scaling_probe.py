@@ -1,6 +1,7 @@
-"""What one rank of an N-GPU fabric table computes: the first ceil(9976/N)
-sources as one query on one GPU (msbfs+levels, and the per-source BFS plan
-for comparison), timed over 20 launches.  Emulates the per-rank device work
+"""What one rank of an N-GPU fabric table computes: a middle block of
+ceil(9976/N) sources as one query on one GPU (msbfs+levels with its helper
+rows), timed over 20 launches, with the cooperative MS-BFS split
+(OPENR_MS_COOP=1, default) and without it.  Emulates the per-rank device work
 of bench.py's fabric_sharded at N = 1, 2, 4, 8 on a one-GPU box."""
 import json
 import os
@@ -21,8 +22,8 @@ g = abi.Graph(csr)
 out = {}
 for N in (1, 2, 4, 8):
     n = (V + N - 1) // N
-    for plan in ("64", "0"):
-        os.environ["OPENR_SPF_MSBFS"] = plan
+    for coop in ("1", "0"):
+        os.environ["OPENR_MS_COOP"] = coop
         # a middle block (the first block holds the SSWs)
         first = (N // 2) * n if N > 1 else 0
         srcs = np.arange(first, min(V, first + n), dtype=np.uint32)
@@ -35,8 +36,8 @@ for N in (1, 2, 4, 8):
             q.run(sync=False)
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / 20 * 1e3
-        out[f"N{N}_{'msbfs' if plan == '64' else 'bfs'}"] = {
-            "sources": int(len(srcs)), "kernel": q.kernel, "ms": round(ms, 4),
-            "stage_ms": [round(x, 4) for x in q.stage_ms()] if hasattr(q, "stage_ms") else None}
+        out[f"N{N}_coop{coop}"] = {
+            "sources": int(len(srcs)), "plan": q.kernel, "kernels": q.kernels(), "ms": round(ms, 4),
+            "stage_ms": [round(x, 4) for x in q.stage_ms()]}
         q.close()
 print(json.dumps(out, indent=1))

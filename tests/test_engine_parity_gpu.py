@@ -420,3 +420,26 @@ def test_ksp2_route_db_device_traces(mods, seed, monkeypatch):
     for node in names[:6]:
         assert es.buildRouteDb(node, ea, ep) == os_.buildRouteDb(node, oa, op), node
     assert E.get_counters().get("decision.spf_runs") == O.get_counters().get("decision.spf_runs")
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_ksp2_route_db_trace_step_budget(mods, seed, monkeypatch):
+    """The device trace's per-query step budget (OPENR_SPF_TRACE_BUDGET):
+    a k = 2 trace longer than it is abandoned on the device and traced on the
+    host from its row.  With a budget of a few steps most traces take that
+    path; the KSP2 RouteDbs still equal the oracle's, spf_runs included."""
+    monkeypatch.setenv("OPENR_KSP2_DEVICE_TRACE", "1")
+    monkeypatch.setenv("OPENR_SPF_TRACE_BUDGET", "3")
+    E, O = mods
+    names, adj_dbs, prefix_dbs = RZ.random_network(720 + seed, n_nodes=30, n_links=80)
+    ea, ep = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    oa, op = RZ.load(O, adj_dbs, prefix_dbs, seed)
+    E.reset_counters()
+    O.reset_counters()
+    es = E.SpfSolver(names[0], True, False)
+    os_ = O.SpfSolver(names[0], True, False)
+    for node in names[:6]:
+        assert es.buildRouteDb(node, ea, ep) == os_.buildRouteDb(node, oa, op), node
+    c = E.get_counters()
+    assert c.get("decision.spf_runs") == O.get_counters().get("decision.spf_runs")
+    assert c.get("decision.kth2_device_overflows", 0) > 0

@@ -183,7 +183,8 @@ int spf_query_screened(spf_query* q, uint32_t* screened, uint32_t* has_screen);
 /* Name of the plan the last run used ("lds", "dstep", "msbfs+levels", "wide",
  * "exact", ...). */
 const char* spf_query_kernel_name(const spf_query* q);
-/* The HIP kernels the last run launched (its sub-queries' included), sorted
+/* The HIP kernels the last run launched (its sub-queries' included, and the
+ * trace calls' since that run: spf_query_trace_paths), sorted
  * and comma-separated, as rocprofv3 names them without template arguments;
  * writes at most cap - 1 bytes and a NUL into buf (may be NULL) and returns
  * the full length, or a negative status.  Lets a measurement check that a

@@ -1584,32 +1584,44 @@ bool LinkState::patchStructure(
     auto it = upIds.find(l);
     return it != upIds.end() ? it->second : eng.linkIdOf(l);
   };
+  // the copies and scatters below run in blocks on the host pool (one
+  // writer per element: a kept half / row / link id belongs to one block)
+  constexpr size_t kBlk = 4096;
+  const unsigned nth = hostThreads(eng.col.size(), 1u << 15);
   // kept halves shift with their row; halves in affected rows are re-set below
-  for (uint32_t lid = 0; lid < halves.size(); ++lid) {
-    for (int s = 0; s < 2; ++s) {
-      const uint32_t e = halves[lid][s];
-      if (e == ~0u || lid >= eng.halves.size()) {
-        continue;
+  const size_t nOld = std::min(halves.size(), eng.halves.size());
+  parallelFor((nOld + kBlk - 1) / kBlk, nth, [&](size_t b, unsigned) {
+    const size_t l1 = std::min(nOld, (b + 1) * kBlk);
+    for (size_t lid = b * kBlk; lid < l1; ++lid) {
+      for (int s = 0; s < 2; ++s) {
+        const uint32_t e = halves[lid][s];
+        if (e == ~0u) {
+          continue;
+        }
+        const uint32_t tail = eng.col[eng.rev[e]];
+        halves[lid][s] = aff[tail] ? ~0u : e - eng.row[tail] + newRow[tail];
       }
-      const uint32_t tail = eng.col[eng.rev[e]];
-      halves[lid][s] = aff[tail] ? ~0u : e - eng.row[tail] + newRow[tail];
     }
-  }
+  }, 1);
   std::vector<uint32_t> col = std::move(eng.spareCol), linkId = std::move(eng.spareLinkId);
   std::vector<uint64_t> metric = std::move(eng.spareMetric);
   col.resize(E);
   linkId.resize(E);
   metric.resize(E);
+  parallelFor((V + kBlk - 1) / kBlk, nth, [&](size_t b, unsigned) {
+    const uint32_t u1 = (uint32_t)std::min<size_t>(V, (b + 1) * kBlk);
+    for (uint32_t u = (uint32_t)(b * kBlk); u < u1; ++u) {
+      if (!aff[u]) {
+        const uint32_t a = eng.row[u], z = eng.row[u + 1], o = newRow[u];
+        std::copy(eng.col.begin() + a, eng.col.begin() + z, col.begin() + o);
+        std::copy(eng.linkId.begin() + a, eng.linkId.begin() + z, linkId.begin() + o);
+        std::copy(eng.metric.begin() + a, eng.metric.begin() + z, metric.begin() + o);
+      }
+    }
+  }, 1);
   {
     size_t k = 0;
-    for (uint32_t u = 0; u < V; ++u) {
-      if (!aff[u]) {
-        const uint32_t a = eng.row[u], b = eng.row[u + 1], o = newRow[u];
-        std::copy(eng.col.begin() + a, eng.col.begin() + b, col.begin() + o);
-        std::copy(eng.linkId.begin() + a, eng.linkId.begin() + b, linkId.begin() + o);
-        std::copy(eng.metric.begin() + a, eng.metric.begin() + b, metric.begin() + o);
-        continue;
-      }
+    for (uint32_t u : affNodes) {
       const std::string& name = eng.names[u];
       uint32_t e = newRow[u];
       for (const auto* lp : affRows[k++]) {
@@ -1629,16 +1641,25 @@ bool LinkState::patchStructure(
   }
   std::vector<uint32_t> rev = std::move(eng.spareRev);
   rev.assign(E, ~0u);
-  for (uint32_t lid = 0; lid < halves.size(); ++lid) {
-    const auto& h = halves[lid];
-    if (!alive[lid]) {
-      continue;
+  std::atomic<bool> oneHalf{false};
+  parallelFor((halves.size() + kBlk - 1) / kBlk, nth, [&](size_t b, unsigned) {
+    const size_t l1 = std::min(halves.size(), (b + 1) * kBlk);
+    for (size_t lid = b * kBlk; lid < l1; ++lid) {
+      const auto& h = halves[lid];
+      if (!alive[lid]) {
+        continue;
+      }
+      if (h[0] == ~0u || h[1] == ~0u) {
+        oneHalf.store(true, std::memory_order_relaxed);
+        return;
+      }
+      rev[h[0]] = h[1];
+      rev[h[1]] = h[0];
     }
-    if (h[0] == ~0u || h[1] == ~0u) {
-      return false; // a link with one half: rebuild
-    }
-    rev[h[0]] = h[1];
-    rev[h[1]] = h[0];
+  }, 1);
+  if (oneHalf.load()) {
+    eng.spareRev = std::move(rev);
+    return false; // a link with one half: rebuild
   }
   for (const auto& l : up) {
     const auto& h = halves[upIds.at(l.get())];

@@ -6364,6 +6364,235 @@ __global__ __launch_bounds__(64 * kTcWaves) void spf_trace_cursor_kernel(TraceCu
 #undef TC_DRAIN
 }
 
+// Heavy queries (the ones past the cursor kernel's step budget: on the fabric
+// ONE destination's trace was that whole 17 ms launch, 15,304 serial steps,
+// profiles/r04ab) get a launch of their own, in two kernels:
+//  * spf_trace_heavy_build_kernel, one wave per (query, node) over the whole
+//    grid: pathLinks(v) of every node of the query's row, filtered and ranked
+//    exactly as the cursor kernel's build, into an arena slotted by CSR row
+//    (pathLinks(v) <= in-degree(v) = row[v + 1] - row[v] entries at row[v]);
+//  * spf_trace_heavy_kernel, one wave per query: every node's {cursor,
+//    length} and arena base in LDS, so a DFS step is ONE global round trip
+//    (the 64 next entries of v's list) and the tails' states are LDS reads.
+// Same DFS, same output as spf_trace_cursor_kernel (the cursor argument
+// above); a list over kTcSort entries or a path over kTcDepth links is still
+// an overflow, traced on the host.
+constexpr uint32_t kHvMaxV = 16384; // LDS: 2 words per node
+// the cursor kernel's default step budget when the heavy launch is on
+constexpr uint32_t kTcHeavyBudget = 2048;
+constexpr uint32_t kHvWaves = 4;    // build waves per block
+
+struct TraceHeavyArgs {
+  TraceArgs t;
+  const uint32_t* hq; // [nh] query indices (into t's queries)
+  uint32_t nh;
+  uint32_t V, E;
+  uint2* arena;       // [nh][E] {tail, link}, pathLinks(v) at row[v]
+  uint32_t* len;      // [nh][V] pathLinks(v) length, or kInf32 (over kTcSort)
+  uint32_t budget;    // DFS steps per query (0xFFFFFFFF: none)
+};
+
+__global__ __launch_bounds__(64 * kHvWaves) void spf_trace_heavy_build_kernel(TraceHeavyArgs H) {
+  const TraceArgs& a = H.t;
+  __shared__ uint64_t key_s[kHvWaves][kTcSort];
+  __shared__ uint32_t sub_s[kHvWaves][kTcSort];
+  __shared__ uint32_t lnk_s[kHvWaves][kTcSort];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint64_t item = (uint64_t)blockIdx.x * kHvWaves + wv;
+  if (item >= (uint64_t)H.nh * H.V) {
+    return; // whole wave; no block barrier below
+  }
+  const uint32_t hi = (uint32_t)(item / H.V), v = (uint32_t)(item % H.V);
+  const uint32_t q = H.hq[hi];
+  const uint32_t s = a.src[q];
+  const uint32_t* dist = a.dist + (size_t)q * a.Vp;
+  const uint32_t ilo = a.ign_off ? a.ign_off[q] : 0u;
+  const uint32_t nign = a.ign_off ? a.ign_off[q + 1] - ilo : 0u;
+  const uint32_t dv = dist[v];
+  uint32_t* lenq = H.len + (size_t)hi * H.V;
+  if (dv == kInf32) {
+    if (lane == 0) {
+      lenq[v] = 0;
+    }
+    return;
+  }
+  uint64_t* keys = key_s[wv];
+  uint32_t* subs = sub_s[wv];
+  uint32_t* lnks = lnk_s[wv];
+  const uint64_t lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const uint32_t e0 = a.row[v], e1 = a.row[v + 1];
+  uint32_t n = 0;
+  for (uint32_t base = e0; base < e1; base += 64) {
+    const uint32_t e = base + lane;
+    bool ok = false;
+    uint32_t u = 0, du = 0, eu = 0, l = 0;
+    if (e < e1) {
+      u = a.col[e];
+      eu = a.rev[e];
+      l = a.link[e];
+      du = dist[u];
+      const uint32_t tb = a.trbits[u >> 5];
+      const uint64_t w = a.unit ? 1ull : (uint64_t)a.wout[eu];
+      ok = du != kInf32 && (u == s || ((tb >> (u & 31)) & 1u)) && (uint64_t)du + w == dv;
+      if (ok && nign) {
+        ok = !in_sorted(a.ign + ilo, nign, l);
+      }
+    }
+    const uint64_t m = __ballot(ok);
+    const uint32_t pos = n + (uint32_t)__popcll(m & lt_mask);
+    if (ok && pos < kTcSort) {
+      keys[pos] = ((uint64_t)du << 32) | u;
+      subs[pos] = eu;
+      lnks[pos] = l;
+    }
+    n += (uint32_t)__popcll(m);
+  }
+  tc_sync();
+  if (n > kTcSort) {
+    if (lane == 0) {
+      lenq[v] = kInf32;
+    }
+    return;
+  }
+  uint2* ar = H.arena + (size_t)hi * H.E + e0;
+  for (uint32_t i = lane; i < n; i += 64) {
+    const uint64_t key = keys[i];
+    const uint32_t su = subs[i];
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < n; ++j) {
+      const uint64_t kj = keys[j];
+      r += (uint32_t)(kj < key) | ((uint32_t)(kj == key) & (uint32_t)(subs[j] < su));
+    }
+    ar[r] = make_uint2((uint32_t)key, lnks[i]);
+  }
+  if (lane == 0) {
+    lenq[v] = n;
+  }
+}
+
+__global__ __launch_bounds__(64) void spf_trace_heavy_kernel(TraceHeavyArgs H) {
+  const TraceArgs& a = H.t;
+  __shared__ uint32_t st[kHvMaxV];   // cursor << 16 | length
+  __shared__ uint32_t rp[kHvMaxV];   // row[v]: v's arena base
+  __shared__ uint32_t stk[kTcDepth]; // node of each frame
+  __shared__ uint32_t lnk[kTcDepth]; // link taken at each frame
+  const uint32_t lane = threadIdx.x;
+  const uint32_t hi = blockIdx.x;
+  const uint32_t q = H.hq[hi];
+  const uint32_t s = a.src[q], d = a.dst[q];
+  const uint32_t* lenq = H.len + (size_t)hi * H.V;
+  const uint2* ar = H.arena + (size_t)hi * H.E;
+  bool bad = false;
+  for (uint32_t v = lane; v < H.V; v += 64) {
+    const uint32_t n = lenq[v];
+    bad = bad || n == kInf32;
+    st[v] = n == kInf32 ? 0u : n;
+    rp[v] = a.row[v];
+  }
+  bool overflow = __ballot(bad) != 0;
+  tc_sync();
+  uint32_t* out_links = a.out_links + (size_t)q * a.cap;
+  uint32_t* out_ends = a.out_ends + (size_t)q * a.cap;
+  uint32_t npaths = 0, nl = 0, nsteps = 0;
+  if (!overflow && s != d && a.dist[(size_t)q * a.Vp + d] != kInf32) {
+    for (;;) { // one traceOnePath per iteration
+      uint32_t depth = 0;
+      if (lane == 0) {
+        stk[0] = d;
+      }
+      tc_sync();
+      bool found = false;
+      for (;;) {
+        if (++nsteps > H.budget) {
+          overflow = true;
+          break;
+        }
+        const uint32_t v = stk[depth];
+        const uint32_t x = st[v];
+        const uint32_t c = x >> 16, n = x & 0xFFFFu;
+        if (c >= n) {
+          // v exhausted: the search through it fails
+          if (depth == 0) {
+            break;
+          }
+          --depth;
+          continue;
+        }
+        // v's next (up to) 64 pathLinks: one round trip; their tails' states
+        // from LDS.  Entries whose tail already failed are taken at once.
+        const uint32_t cnt = min(64u, n - c);
+        const bool have = lane < cnt;
+        uint2 ent = make_uint2(kInf32, 0);
+        if (have) {
+          ent = ar[rp[v] + c + lane];
+        }
+        const uint32_t u = ent.x;
+        bool live = false;
+        if (have) {
+          if (u == s) {
+            live = true;
+          } else {
+            const uint32_t su = st[u];
+            live = (su >> 16) < (su & 0xFFFFu);
+          }
+        }
+        const uint64_t lm = __ballot(live);
+        tc_sync(); // every lane read st[v] / st[u] before lane 0 moves v's cursor
+        if (lm == 0) {
+          if (lane == 0) {
+            st[v] = x + (cnt << 16);
+          }
+          tc_sync();
+          continue;
+        }
+        const int f = (int)__builtin_ctzll(lm);
+        const uint32_t fu = (uint32_t)__builtin_amdgcn_readlane((int)u, f);
+        const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)ent.y, f);
+        if (lane == 0) {
+          st[v] = x + (((uint32_t)f + 1) << 16);
+          lnk[depth] = fl;
+        }
+        if (fu == s) {
+          found = true;
+          break;
+        }
+        if (depth + 1 >= kTcDepth) {
+          overflow = true;
+          break;
+        }
+        ++depth;
+        if (lane == 0) {
+          stk[depth] = fu;
+        }
+        tc_sync();
+      }
+      if (overflow || !found) {
+        break;
+      }
+      tc_sync();
+      const uint32_t len = depth + 1;
+      if (nl + len > a.cap || npaths + 1 > a.cap) {
+        overflow = true;
+        break;
+      }
+      // frames deepest first: the path runs src -> dst
+      for (uint32_t i = lane; i < len; i += 64) {
+        out_links[nl + i] = lnk[depth - i];
+      }
+      nl += len;
+      if (lane == 0) {
+        out_ends[npaths] = nl;
+      }
+      ++npaths;
+      tc_sync();
+    }
+  }
+  if (lane == 0) {
+    a.out_n[q] = overflow ? kTraceOverflow : npaths;
+    a.out_len[q] = overflow ? 0u : nl;
+  }
+}
+
 struct TracePackArgs {
   const uint32_t* out_n;
   const uint32_t* out_len;
@@ -6480,6 +6709,8 @@ struct spf_graph {
   std::vector<uint32_t> h_wout, h_win, h_cw;
   // spf_graph_update: the CSR and neighbour lists it replaced (reused rows)
   std::vector<uint32_t> old_row, old_col, old_nbr_off, old_nbrs, old_slot;
+  std::vector<uint32_t> h_sell, h_half; // upload_sell / link-half staging
+  size_t cap_sell = 0, cap_sell_off = 0;
   // pinned staging of the preparation uploads (g_stage): one DMA per array
   // on the graph stream instead of a pageable synchronous hipMemcpy each
   char* pin = nullptr;
@@ -6609,6 +6840,7 @@ struct spf_query {
   uint32_t* d_trace = nullptr;
   size_t trace_words = 0;
   char* d_tcs = nullptr; // spf_trace_cursor_kernel node states + arenas
+  uint32_t trace_heavy = 0; // queries of the last trace call re-run by spf_trace_heavy_kernel
   size_t tcs_bytes = 0;
   uint32_t trace_n = 0, trace_cap = 0;
   uint64_t trace_links = 0, trace_paths = 0;
@@ -6897,6 +7129,29 @@ int build_nl_v2(spf_query* q, const uint32_t* sources, const std::vector<int32_t
   return SPF_OK;
 }
 
+// memcpy in 256 KB chunks on the host pool (a graph rebuild moves tens of MB
+// through host copies: single-threaded they cost ~25 GB/s)
+void par_copy(void* dst, const void* src, size_t bytes) {
+  constexpr size_t kChunk = (size_t)256 << 10;
+  const size_t n = (bytes + kChunk - 1) / kChunk;
+  const unsigned nth = openr::hostThreads(n, 2);
+  if (nth <= 1) {
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  openr::parallelFor(n, nth, [&](size_t i, unsigned) {
+    const size_t o = i * kChunk;
+    std::memcpy(static_cast<char*>(dst) + o, static_cast<const char*>(src) + o,
+                std::min(kChunk, bytes - o));
+  }, 1);
+}
+
+template <typename T>
+void par_assign(std::vector<T>& v, const T* src, size_t n) {
+  v.resize(n);
+  par_copy(v.data(), src, n * sizeof(T));
+}
+
 // Host -> device upload through the graph's pinned staging buffer: the bytes
 // are copied into it and one async DMA is queued on the graph stream
 // (pageable hipMemcpy measured ~1-2 GB/s in a link flap's rebuild,
@@ -6925,7 +7180,7 @@ int g_stage(spf_graph* g, void* dst, const void* src, size_t bytes) {
       g->pin_cap = c;
     }
   }
-  std::memcpy(g->pin + g->pin_off, src, bytes);
+  par_copy(g->pin + g->pin_off, src, bytes);
   HIP_TRY(hipMemcpyAsync(dst, g->pin + g->pin_off, bytes, hipMemcpyHostToDevice, g->stream));
   g->pin_off += need;
   return SPF_OK;
@@ -7351,19 +7606,18 @@ int upload_weights(spf_graph* g) {
   std::vector<uint32_t>& win = g->h_win;
   wout.resize(E);
   win.resize(E);
+  // one pass per row: fast-path out / in metrics and the cheapest usable
+  // link to each distinct neighbour (parallel links)
+  g->nbr_w.resize(g->nbrs.size());
   blocks([&](uint32_t u, unsigned) {
+    uint32_t* nw = g->nbr_w.data() + g->nbr_off[u];
+    std::fill(nw, g->nbr_w.data() + g->nbr_off[u + 1], 0xFFFFFFFFu);
     for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
-      wout[e] = (uint32_t)std::min<uint64_t>(g->w64[e], 0xFFFFFFFFull);
-    }
-  });
-  if (tl_phase) (*tl_phase)("w:wout");
-  // cheapest usable link to each distinct neighbour (parallel links)
-  g->nbr_w.assign(g->nbrs.size(), 0xFFFFFFFFu);
-  blocks([&](uint32_t u, unsigned) {
-    for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
+      const uint32_t wo = (uint32_t)std::min<uint64_t>(g->w64[e], 0xFFFFFFFFull);
+      wout[e] = wo;
       win[e] = (uint32_t)std::min<uint64_t>(g->w64[g->rev[e]], 0xFFFFFFFFull);
-      uint32_t& w = g->nbr_w[g->nbr_off[u] + g->slot[e]];
-      w = std::min(w, wout[e]);
+      uint32_t& w = nw[g->slot[e]];
+      w = std::min(w, wo);
     }
   });
   if (tl_phase) (*tl_phase)("w:nbr_w");
@@ -7448,22 +7702,46 @@ int upload_sell(spf_graph* g) {
     }
     off[c + 1] = off[c] + (w + 3) / 4;
   }
-  std::vector<uint32_t> sell((size_t)off[ns] * 256);
-  for (uint32_t c = 0; c < ns; ++c) {
+  // kept on the graph (in-place rebuilds: no page faults); slices on the
+  // host pool (each writes its own groups)
+  std::vector<uint32_t>& sell = g->h_sell;
+  sell.resize((size_t)off[ns] * 256);
+  openr::parallelFor(ns, openr::hostThreads(g->E, kHostMinEdges), [&](size_t c, unsigned) {
     const uint32_t groups = off[c + 1] - off[c];
     for (uint32_t L = 0; L < 64; ++L) {
-      const uint32_t v = 64 * c + L;
+      const uint32_t v = 64 * (uint32_t)c + L;
       const uint32_t deg = v < V ? g->row[v + 1] - g->row[v] : 0;
       for (uint32_t j = 0; j < groups * 4; ++j) {
         const uint32_t x = j < deg ? g->col[g->row[v] + j] : (v < V ? v : 0);
         sell[((size_t)(off[c] + j / 4) * 64 + L) * 4 + (j & 3)] = x;
       }
     }
-  }
+  }, 8);
   g->sell_off = off;
-  int s = dev_upload_g(g, &g->d_sell_off, off.data(), off.size());
+  // device buffers kept across in-place rebuilds while they fit
+  auto fit = [&](uint32_t** d, size_t n, size_t& cap) -> int {
+    if (*d && n <= cap) {
+      return SPF_OK;
+    }
+    if (*d) {
+      (void)hipFree(*d);
+      *d = nullptr;
+    }
+    cap = 0;
+    const size_t c = std::max<size_t>(1, n + n / 8);
+    HIP_TRY(hipMalloc((void**)d, c * 4));
+    cap = c;
+    return SPF_OK;
+  };
+  int s = fit(&g->d_sell_off, off.size(), g->cap_sell_off);
+  if (s == SPF_OK) {
+    s = g_stage(g, g->d_sell_off, off.data(), off.size() * 4);
+  }
   if (s == SPF_OK && !sell.empty()) {
-    s = dev_upload_g(g, (uint32_t**)&g->d_sell, sell.data(), sell.size());
+    s = fit((uint32_t**)&g->d_sell, sell.size(), g->cap_sell);
+    if (s == SPF_OK) {
+      s = g_stage(g, g->d_sell, sell.data(), sell.size() * 4);
+    }
   }
   return s;
 }
@@ -8031,11 +8309,11 @@ int spf_graph_update(spf_graph* g, const spf_graph_desc* desc) {
   std::swap(g->slot, g->old_slot);
   g->E = E;
   g->L = desc->num_links;
-  g->row.assign(desc->row_ptr, desc->row_ptr + V + 1);
-  g->col.assign(desc->col, desc->col + E);
-  g->link.assign(desc->link_id, desc->link_id + E);
-  g->rev.assign(desc->rev, desc->rev + E);
-  g->w64.assign(desc->metric, desc->metric + E);
+  par_assign(g->row, desc->row_ptr, (size_t)V + 1);
+  par_assign(g->col, desc->col, E);
+  par_assign(g->link, desc->link_id, E);
+  par_assign(g->rev, desc->rev, E);
+  par_assign(g->w64, desc->metric, E);
   std::fill(g->trbits.begin(), g->trbits.end(), 0u);
   for (uint32_t v = 0; v < V; ++v) {
     if (!desc->node_overloaded[v]) {
@@ -8105,21 +8383,20 @@ int spf_graph_update(spf_graph* g, const spf_graph_desc* desc) {
   }
   mark("weights");
   {
-    std::vector<uint32_t> half(2 * (size_t)g->L, kInf32);
-    for (uint32_t e = 0; e < E; ++e) {
-      half[2 * (size_t)g->link[e] + (e < g->rev[e] ? 0 : 1)] = e;
-    }
+    // one writer per slot (a link's two halves), edge blocks on the pool
+    std::vector<uint32_t>& half = g->h_half;
+    half.assign(2 * (size_t)g->L, kInf32);
+    constexpr uint32_t kBlk = 1u << 14;
+    openr::parallelFor((E + kBlk - 1) / kBlk, openr::hostThreads(E, kHostMinEdges),
+                       [&](size_t b, unsigned) {
+      const uint32_t e1 = std::min<uint32_t>(E, (uint32_t)(b + 1) * kBlk);
+      for (uint32_t e = (uint32_t)b * kBlk; e < e1; ++e) {
+        half[2 * (size_t)g->link[e] + (e < g->rev[e] ? 0 : 1)] = e;
+      }
+    }, 1);
     if ((s = store32(&g->d_link_half, half, g->cap_half))) {
       return s;
     }
-  }
-  if (g->d_sell) {
-    (void)hipFree(g->d_sell);
-    g->d_sell = nullptr;
-  }
-  if (g->d_sell_off) {
-    (void)hipFree(g->d_sell_off);
-    g->d_sell_off = nullptr;
   }
   mark("link halves");
   if (V && V <= kMsThreads * kMsMaxK && (s = upload_sell(g))) {
@@ -10473,6 +10750,21 @@ int spf_query_trace_paths(
     return SPF_OK;
   }
   HIP_TRY(hipSetDevice(g->device));
+  // the trace kernels join the run's launch list (spf_query_kernels)
+  struct TraceLog {
+    bool own = false;
+    explicit TraceLog(spf_query* x) {
+      if (!tl_launched) {
+        tl_launched = &x->launched;
+        own = true;
+      }
+    }
+    ~TraceLog() {
+      if (own) {
+        tl_launched = nullptr;
+      }
+    }
+  } trace_log(q);
   // scratch: dests | out_n | out_len | links [count][cap] | ends [count][cap]
   // (OPENR_SPF_TRACE_CAP lowers the per-query capacity: overflow tests)
   const uint32_t cap = std::max<uint32_t>(1, std::min(kTraceCap, env_u32("OPENR_SPF_TRACE_CAP", kTraceCap)));
@@ -10510,7 +10802,11 @@ int spf_query_trace_paths(
   a.nq = count;
   a.cap = cap;
   a.unit = (q->flags & SPF_F_UNIT_METRIC) ? 1u : 0u;
-  if (env_flag("OPENR_SPF_TRACE_CURSOR", 1)) {
+  const bool cursor = env_flag("OPENR_SPF_TRACE_CURSOR", 1);
+  // queries past the cursor kernel's step budget go to the heavy launch
+  // (spf_trace_heavy_kernel; its node states live in LDS: V <= kHvMaxV)
+  const bool heavy = cursor && g->V <= kHvMaxV && env_flag("OPENR_SPF_TRACE_HEAVY", 1);
+  if (cursor) {
     // cursor DFS: per-wave node states + pathLinks arena (zeroed per launch:
     // a state's tag is its query index + 1)
     // 16 waves per CU (a wave's DFS is a chain of L2 round trips: the more
@@ -10535,10 +10831,10 @@ int spf_query_trace_paths(
     ta.arena = reinterpret_cast<uint2*>(q->d_tcs + (size_t)nw * g->V * sizeof(uint4));
     ta.arena_cap = acap;
     ta.V = g->V;
-    // no budget by default: at 4,096 steps 252 fabric queries went to the host,
-    // whose traces cost more than the device's (KSP2 build 58 -> 74 ms,
-    // profiles/r05s); the knob stays for tests and measurements
-    ta.budget = env_u32("OPENR_SPF_TRACE_BUDGET", 0xFFFFFFFFu);
+    // without the heavy launch no budget by default: at 4,096 steps 252
+    // fabric queries went to the host, whose traces cost more than the
+    // device's (KSP2 build 58 -> 74 ms, profiles/r05s)
+    ta.budget = env_u32("OPENR_SPF_TRACE_BUDGET", heavy ? kTcHeavyBudget : 0xFFFFFFFFu);
     HIP_TRY(hipMemsetAsync(q->d_tcs, 0, (size_t)nw * g->V * sizeof(uint4), g->stream));
     if (env_flag("OPENR_SPF_TRACE_STATS", 0)) {
       HIP_TRY(hipMalloc((void**)&ta.qstat, (size_t)count * kTcStat * 8));
@@ -10591,6 +10887,55 @@ int spf_query_trace_paths(
   HIP_TRY(hipMemcpyAsync(link_count, a.out_len, (size_t)count * 4, hipMemcpyDeviceToHost,
                          g->stream));
   HIP_TRY(hipStreamSynchronize(g->stream));
+  if (heavy) {
+    std::vector<uint32_t> hq;
+    for (uint32_t i = 0; i < count; ++i) {
+      if (path_count[i] == SPF_TRACE_OVERFLOW) {
+        hq.push_back(i);
+      }
+    }
+    // chunks: arena + lengths bounded to ~1 GiB per launch
+    const size_t per = (size_t)g->E * sizeof(uint2) + (size_t)g->V * 4;
+    const size_t chunk = std::max<size_t>(1, std::min<size_t>(1024, ((size_t)1 << 30) / per));
+    for (size_t c0 = 0; c0 < hq.size(); c0 += chunk) {
+      const uint32_t nh = (uint32_t)std::min(chunk, hq.size() - c0);
+      char* hb = nullptr; // hq [nh] | len [nh][V] | arena [nh][E]
+      const size_t o_len = ((size_t)nh * 4 + 255) & ~(size_t)255;
+      const size_t o_ar = (o_len + (size_t)nh * g->V * 4 + 255) & ~(size_t)255;
+      HIP_TRY(pool_malloc((void**)&hb, o_ar + (size_t)nh * g->E * sizeof(uint2)));
+      struct Free {
+        char* p;
+        hipStream_t st;
+        ~Free() {
+          (void)hipStreamSynchronize(st);
+          pool_free(p);
+        }
+      } guard{hb, g->stream};
+      HIP_TRY(hipMemcpyAsync(hb, hq.data() + c0, (size_t)nh * 4, hipMemcpyHostToDevice, g->stream));
+      TraceHeavyArgs h{};
+      h.t = a;
+      h.hq = reinterpret_cast<const uint32_t*>(hb);
+      h.nh = nh;
+      h.V = g->V;
+      h.E = g->E;
+      h.len = reinterpret_cast<uint32_t*>(hb + o_len);
+      h.arena = reinterpret_cast<uint2*>(hb + o_ar);
+      h.budget = env_u32("OPENR_SPF_TRACE_HEAVY_BUDGET", 0xFFFFFFFFu);
+      const uint64_t items = (uint64_t)nh * g->V;
+      SPF_LAUNCH(spf_trace_heavy_build_kernel, dim3((uint32_t)((items + kHvWaves - 1) / kHvWaves)),
+                 dim3(64 * kHvWaves), 0, g->stream, h);
+      SPF_LAUNCH(spf_trace_heavy_kernel, dim3(nh), dim3(64), 0, g->stream, h);
+      HIP_TRY(hipGetLastError());
+    }
+    if (!hq.empty()) {
+      HIP_TRY(hipMemcpyAsync(path_count, a.out_n, (size_t)count * 4, hipMemcpyDeviceToHost,
+                             g->stream));
+      HIP_TRY(hipMemcpyAsync(link_count, a.out_len, (size_t)count * 4, hipMemcpyDeviceToHost,
+                             g->stream));
+      HIP_TRY(hipStreamSynchronize(g->stream));
+    }
+    q->trace_heavy = (uint32_t)hq.size();
+  }
   q->trace_n = count;
   q->trace_pc.assign(path_count, path_count + count);
   q->trace_lc.assign(link_count, link_count + count);

@@ -422,14 +422,18 @@ def test_ksp2_route_db_device_traces(mods, seed, monkeypatch):
     assert E.get_counters().get("decision.spf_runs") == O.get_counters().get("decision.spf_runs")
 
 
-@pytest.mark.parametrize("seed", range(3))
-def test_ksp2_route_db_trace_step_budget(mods, seed, monkeypatch):
-    """The device trace's per-query step budget (OPENR_SPF_TRACE_BUDGET):
-    a k = 2 trace longer than it is abandoned on the device and traced on the
-    host from its row.  With a budget of a few steps most traces take that
-    path; the KSP2 RouteDbs still equal the oracle's, spf_runs included."""
+@pytest.mark.parametrize("seed,heavy", [(0, "0"), (1, "0"), (2, "1"), (3, "1")])
+def test_ksp2_route_db_trace_step_budget(mods, seed, heavy, monkeypatch):
+    """The device trace's per-query step budgets: a k = 2 trace longer than
+    the cursor kernel's (OPENR_SPF_TRACE_BUDGET) goes to the heavy launch, and
+    one longer than that launch's (OPENR_SPF_TRACE_HEAVY_BUDGET; any, with the
+    heavy launch off) is traced on the host from its row.  With budgets of a
+    few steps most traces take those paths; the KSP2 RouteDbs still equal the
+    oracle's, spf_runs included."""
     monkeypatch.setenv("OPENR_KSP2_DEVICE_TRACE", "1")
     monkeypatch.setenv("OPENR_SPF_TRACE_BUDGET", "3")
+    monkeypatch.setenv("OPENR_SPF_TRACE_HEAVY", heavy)
+    monkeypatch.setenv("OPENR_SPF_TRACE_HEAVY_BUDGET", "3")
     E, O = mods
     names, adj_dbs, prefix_dbs = RZ.random_network(720 + seed, n_nodes=30, n_links=80)
     ea, ep = RZ.load(E, adj_dbs, prefix_dbs, seed)

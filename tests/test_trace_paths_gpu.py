@@ -142,3 +142,72 @@ def test_trace_paths_visited_set_overflow(gpu_ready, cursor, monkeypatch):
             assert got is None
         else:
             assert got == trace_all(csr, spf_py.run_spf(csr, src, False), src, dst)
+
+
+@pytest.mark.parametrize("seed,unit", [(5, False), (6, True)])
+def test_trace_paths_heavy_launch(gpu_ready, seed, unit, monkeypatch):
+    """Queries past the cursor kernel's step budget are re-traced by the heavy
+    launch (spf_trace_heavy_build_kernel + spf_trace_heavy_kernel: every
+    node's pathLinks pre-built, the cursors in LDS).  With a budget of one
+    step every query takes that path; the traces must equal the recursion's,
+    for the k = 1 rows and the KSP2 ignore-list rows.  A heavy budget too
+    small reports overflow (None), never a wrong path."""
+    sys.setrecursionlimit(10000)
+    monkeypatch.setenv("OPENR_SPF_TRACE_BUDGET", "1")
+    rng = random.Random(seed)
+    V = 150
+    links = random_links(rng, V, 520, wmax=1 if unit else 5)
+    ov = np.zeros(V, dtype=np.uint8)
+    ov[rng.sample(range(V), 5)] = 1
+    csr = abi.Csr.from_links(V, links, overloaded=ov)
+    g = abi.Graph(csr)
+    src = rng.randrange(V)
+    dsts = [d for d in range(V) if d != src]
+    flags = abi.SPF_F_UNIT_METRIC if unit else 0
+    q1 = g.query([src] * len(dsts), flags).run()
+    got1 = q1.trace_paths(dsts)
+    assert "spf_trace_heavy_kernel" in q1.kernels()
+    ref = spf_py.run_spf(csr, src, not unit)
+    first = []
+    for d, got in zip(dsts, got1):
+        want = trace_all(csr, ref, src, d)
+        assert got == want, (d, got, want)
+        first.append(sorted({l for p in want for l in p}))
+    keep = [i for i, f in enumerate(first) if f]
+    ign = [first[i] for i in keep]
+    q2 = g.query([src] * len(keep), flags, ignore=ign).run()
+    got2 = q2.trace_paths([dsts[i] for i in keep])
+    for j, i in enumerate(keep):
+        r2 = spf_py.run_spf(csr, src, not unit, frozenset(ign[j]))
+        assert got2[j] == trace_all(csr, r2, src, dsts[i]), dsts[i]
+    # the heavy kernel's own budget: a multi-step trace overflows, the rest
+    # stay exact
+    monkeypatch.setenv("OPENR_SPF_TRACE_HEAVY_BUDGET", "3")
+    small = q1.trace_paths(dsts)
+    n_over = 0
+    for d, got in zip(dsts, small):
+        if got is None:
+            n_over += 1
+        else:
+            assert got == trace_all(csr, ref, src, d), d
+    assert n_over > 0
+
+
+def test_trace_paths_heavy_bipartite(gpu_ready, monkeypatch):
+    """The two-layer bipartite case (1,600 middle links) through the heavy
+    launch only."""
+    monkeypatch.setenv("OPENR_SPF_TRACE_BUDGET", "1")
+    sys.setrecursionlimit(10000)
+    m = 40
+    V = 2 + 2 * m
+    src, dst = 0, V - 1
+    links = [(src, 1 + i, 1, 1) for i in range(m)]
+    links += [(1 + i, 1 + m + j, 1, 1) for i in range(m) for j in range(m)]
+    links += [(1 + m + j, dst, 1, 1) for j in range(m)]
+    csr = abi.Csr.from_links(V, links)
+    g = abi.Graph(csr)
+    q = g.query([src, src], abi.SPF_F_UNIT_METRIC).run()
+    got = q.trace_paths([dst, 1 + m])
+    ref = spf_py.run_spf(csr, src, False)
+    assert got == [trace_all(csr, ref, src, dst), trace_all(csr, ref, src, 1 + m)]
+    assert "spf_trace_heavy_kernel" in q.kernels()

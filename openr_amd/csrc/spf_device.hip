@@ -6379,7 +6379,7 @@ __global__ __launch_bounds__(64 * kTcWaves) void spf_trace_cursor_kernel(TraceCu
 // an overflow, traced on the host.
 constexpr uint32_t kHvMaxV = 16384; // LDS: 2 words per node
 // the cursor kernel's default step budget when the heavy launch is on
-constexpr uint32_t kTcHeavyBudget = 2048;
+constexpr uint32_t kTcHeavyBudget = 1024;
 constexpr uint32_t kHvWaves = 4;    // build waves per block
 
 struct TraceHeavyArgs {
@@ -6390,31 +6390,158 @@ struct TraceHeavyArgs {
   uint2* arena;       // [nh][E] {tail, link}, pathLinks(v) at row[v]
   uint32_t* len;      // [nh][V] pathLinks(v) length, or kInf32 (over kTcSort)
   uint32_t budget;    // DFS steps per query (0xFFFFFFFF: none)
+  // OPENR_SPF_TRACE_STATS=1: per heavy query {wall ticks (100 MHz), steps,
+  // pushes, global batch loads}; nullptr = off
+  unsigned long long* hstat;
+  // blocks of query hi built on XCD hi % 8, the XCD its DFS block runs on
+  // (blocks go round-robin over the 8 XCDs): its arena is read from that
+  // XCD's L2 instead of across the fabric.  0: plain item order.
+  uint32_t xcd;
+  uint32_t L;         // link ids (the removed-link bitset of the reach kernel)
+  uint32_t* fq;       // [nh][2][V] the reach kernel's BFS frontiers
+  const uint32_t* nodes; // [V] build order: in-degree <= 16 first (nsmall), then the rest
+  uint32_t nsmall;
 };
+
+// Blocks of the build per heavy query: nodes of in-degree <= 16 four to a
+// wave (16 lanes each: the fabric's RSWs, 83% of its nodes, have 8), the
+// others one per wave.
+// work units of one query (a unit = one block's pass); a block takes
+// kHvRounds of them (4 measured slower than 1: 1.24 vs 1.08 ms, profiles/r05af)
+constexpr uint32_t kHvRounds = 1;
+__host__ __device__ inline uint32_t hv_units(uint32_t nsmall, uint32_t nbig) {
+  return (nsmall + 4 * kHvWaves - 1) / (4 * kHvWaves) + (nbig + kHvWaves - 1) / kHvWaves;
+}
+__host__ __device__ inline uint32_t hv_blocks(uint32_t nsmall, uint32_t nbig) {
+  return (hv_units(nsmall, nbig) + kHvRounds - 1) / kHvRounds;
+}
 
 __global__ __launch_bounds__(64 * kHvWaves) void spf_trace_heavy_build_kernel(TraceHeavyArgs H) {
   const TraceArgs& a = H.t;
   __shared__ uint64_t key_s[kHvWaves][kTcSort];
   __shared__ uint32_t sub_s[kHvWaves][kTcSort];
   __shared__ uint32_t lnk_s[kHvWaves][kTcSort];
+  __shared__ uint32_t ign_s[kTcIgn];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint64_t item = (uint64_t)blockIdx.x * kHvWaves + wv;
-  if (item >= (uint64_t)H.nh * H.V) {
-    return; // whole wave; no block barrier below
+  const uint32_t nbig = H.V - H.nsmall;
+  const uint32_t bs = (H.nsmall + 4 * kHvWaves - 1) / (4 * kHvWaves);
+  const uint32_t bq = hv_blocks(H.nsmall, nbig);
+  uint32_t hi, k;
+  if (H.xcd) {
+    const uint32_t ka = blockIdx.x >> 3;
+    hi = (ka / bq) * 8u + (blockIdx.x & 7u);
+    k = ka % bq;
+  } else {
+    hi = blockIdx.x / bq;
+    k = blockIdx.x % bq;
   }
-  const uint32_t hi = (uint32_t)(item / H.V), v = (uint32_t)(item % H.V);
+  if (hi >= H.nh) {
+    return; // whole block
+  }
   const uint32_t q = H.hq[hi];
   const uint32_t s = a.src[q];
   const uint32_t* dist = a.dist + (size_t)q * a.Vp;
   const uint32_t ilo = a.ign_off ? a.ign_off[q] : 0u;
   const uint32_t nign = a.ign_off ? a.ign_off[q + 1] - ilo : 0u;
-  const uint32_t dv = dist[v];
+  // the query's ignore list as an LDS hash set (one block = one query)
+  IgnSet ig;
+  ig.p = a.ign + ilo;
+  ig.n = nign;
+  const uint32_t slots = ign_hash_slots(nign);
+  if (slots && slots <= kTcIgn) {
+    for (uint32_t i = threadIdx.x; i < slots; i += 64 * kHvWaves) {
+      ign_s[i] = kInf32;
+    }
+    __syncthreads();
+    const uint32_t hb = __builtin_ctz(slots);
+    for (uint32_t i = threadIdx.x; i < nign; i += 64 * kHvWaves) {
+      const uint32_t l = a.ign[ilo + i];
+      uint32_t h = (l * 0x9E3779B1u) >> (32 - hb);
+      for (;;) {
+        const uint32_t prev = atomicCAS(&ign_s[h], kInf32, l);
+        if (prev == kInf32 || prev == l) {
+          break;
+        }
+        h = (h + 1) & (slots - 1);
+      }
+    }
+    __syncthreads();
+    ig.p = ign_s;
+    ig.hbits = hb;
+  }
   uint32_t* lenq = H.len + (size_t)hi * H.V;
+  uint2* arq = H.arena + (size_t)hi * H.E;
+  // in-edge e of v (tail u = col[e]) as a pathLink: usable, tight, tail the
+  // source or transit, link not ignored (the cursor kernel's filter)
+  auto tight = [&](uint32_t e, uint32_t dv, uint32_t& u, uint32_t& du, uint32_t& eu,
+                   uint32_t& l) -> bool {
+    u = a.col[e];
+    eu = a.rev[e];
+    l = a.link[e];
+    du = dist[u];
+    const uint32_t tb = a.trbits[u >> 5];
+    const uint64_t w = a.unit ? 1ull : (uint64_t)a.wout[eu];
+    bool ok = du != kInf32 && (u == s || ((tb >> (u & 31)) & 1u)) && (uint64_t)du + w == dv;
+    if (ok && nign) {
+      ok = !ig.has(l);
+    }
+    return ok;
+  };
+  const uint32_t nunits = hv_units(H.nsmall, nbig);
+  for (uint32_t rd = 0; rd < kHvRounds; ++rd) {
+  const uint32_t un = k * kHvRounds + rd; // block-uniform
+  if (un >= nunits) {
+    break;
+  }
+  if (un < bs) {
+    // four small nodes per wave, 16 lanes each: filter in one pass, rank
+    // the group's keys across its lanes
+    const uint32_t g = lane >> 4, gl = lane & 15u;
+    const uint32_t slot = (un * kHvWaves + wv) * 4 + g;
+    const bool act = slot < H.nsmall;
+    const uint32_t v = act ? H.nodes[slot] : 0u;
+    const uint32_t dv = act ? dist[v] : kInf32;
+    uint32_t e0 = 0, e1 = 0;
+    if (dv != kInf32) {
+      e0 = a.row[v];
+      e1 = a.row[v + 1];
+    }
+    bool ok = false;
+    uint32_t u = 0, du = 0, eu = 0, l = 0;
+    if (e0 + gl < e1) {
+      ok = tight(e0 + gl, dv, u, du, eu, l);
+    }
+    const uint32_t gm = (uint32_t)(__ballot(ok) >> (16 * g)) & 0xFFFFu;
+    const uint64_t key = ((uint64_t)du << 32) | u;
+    uint32_t r = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+      const uint32_t src = 16 * g + j;
+      const uint32_t jlo = (uint32_t)__shfl((int)u, (int)src, 64);
+      const uint32_t jhi = (uint32_t)__shfl((int)du, (int)src, 64);
+      const uint32_t js = (uint32_t)__shfl((int)eu, (int)src, 64);
+      const uint64_t kj = ((uint64_t)jhi << 32) | jlo;
+      r += ((gm >> j) & 1u) & ((uint32_t)(kj < key) | ((uint32_t)(kj == key) & (uint32_t)(js < eu)));
+    }
+    if (ok) {
+      arq[e0 + r] = make_uint2(u, l);
+    }
+    if (act && gl == 0) {
+      lenq[v] = (uint32_t)__popc(gm);
+    }
+    continue;
+  }
+  const uint32_t bi = (un - bs) * kHvWaves + wv;
+  if (bi >= nbig) {
+    continue; // whole wave; no block barrier below
+  }
+  const uint32_t v = H.nodes[H.nsmall + bi];
+  const uint32_t dv = dist[v];
   if (dv == kInf32) {
     if (lane == 0) {
       lenq[v] = 0;
     }
-    return;
+    continue;
   }
   uint64_t* keys = key_s[wv];
   uint32_t* subs = sub_s[wv];
@@ -6427,16 +6554,7 @@ __global__ __launch_bounds__(64 * kHvWaves) void spf_trace_heavy_build_kernel(Tr
     bool ok = false;
     uint32_t u = 0, du = 0, eu = 0, l = 0;
     if (e < e1) {
-      u = a.col[e];
-      eu = a.rev[e];
-      l = a.link[e];
-      du = dist[u];
-      const uint32_t tb = a.trbits[u >> 5];
-      const uint64_t w = a.unit ? 1ull : (uint64_t)a.wout[eu];
-      ok = du != kInf32 && (u == s || ((tb >> (u & 31)) & 1u)) && (uint64_t)du + w == dv;
-      if (ok && nign) {
-        ok = !in_sorted(a.ign + ilo, nign, l);
-      }
+      ok = tight(e, dv, u, du, eu, l);
     }
     const uint64_t m = __ballot(ok);
     const uint32_t pos = n + (uint32_t)__popcll(m & lt_mask);
@@ -6452,9 +6570,9 @@ __global__ __launch_bounds__(64 * kHvWaves) void spf_trace_heavy_build_kernel(Tr
     if (lane == 0) {
       lenq[v] = kInf32;
     }
-    return;
+    continue;
   }
-  uint2* ar = H.arena + (size_t)hi * H.E + e0;
+  uint2* ar = arq + e0;
   for (uint32_t i = lane; i < n; i += 64) {
     const uint64_t key = keys[i];
     const uint32_t su = subs[i];
@@ -6468,7 +6586,17 @@ __global__ __launch_bounds__(64 * kHvWaves) void spf_trace_heavy_build_kernel(Tr
   if (lane == 0) {
     lenq[v] = n;
   }
+  tc_sync(); // the wave's next pass reuses its LDS key buffer
+  }
 }
+
+// The DFS of one heavy query.  The current frame (node, cursor, length,
+// arena base, the batch of its next 64 entries: one per lane) lives in
+// registers; a push saves the frame's batch to LDS (frames < kHvCache), so a
+// pop resumes without a global round trip.  A step is then one LDS gather of
+// the tails' states when it resumes a frame, plus one global load when it
+// enters a new node (or runs past a 64-entry batch).
+constexpr uint32_t kHvCache = 16;
 
 __global__ __launch_bounds__(64) void spf_trace_heavy_kernel(TraceHeavyArgs H) {
   const TraceArgs& a = H.t;
@@ -6476,6 +6604,8 @@ __global__ __launch_bounds__(64) void spf_trace_heavy_kernel(TraceHeavyArgs H) {
   __shared__ uint32_t rp[kHvMaxV];   // row[v]: v's arena base
   __shared__ uint32_t stk[kTcDepth]; // node of each frame
   __shared__ uint32_t lnk[kTcDepth]; // link taken at each frame
+  __shared__ uint32_t fbs[kHvCache]; // first entry of each cached batch
+  __shared__ uint2 cache[kHvCache][64];
   const uint32_t lane = threadIdx.x;
   const uint32_t hi = blockIdx.x;
   const uint32_t q = H.hq[hi];
@@ -6493,42 +6623,60 @@ __global__ __launch_bounds__(64) void spf_trace_heavy_kernel(TraceHeavyArgs H) {
   tc_sync();
   uint32_t* out_links = a.out_links + (size_t)q * a.cap;
   uint32_t* out_ends = a.out_ends + (size_t)q * a.cap;
-  uint32_t npaths = 0, nl = 0, nsteps = 0;
+  uint32_t npaths = 0, nl = 0, nsteps = 0, npush = 0, nload = 0;
+  const unsigned long long t0 = H.hstat ? wall_clock64() : 0ull;
+  // entries [bs, bs + 64) of the frame's list, one per lane
+  auto load = [&](uint32_t base, uint32_t bs, uint32_t n) -> uint2 {
+    ++nload;
+    return bs + lane < n ? ar[base + bs + lane] : make_uint2(kInf32, 0u);
+  };
   if (!overflow && s != d && a.dist[(size_t)q * a.Vp + d] != kInf32) {
     for (;;) { // one traceOnePath per iteration
-      uint32_t depth = 0;
+      uint32_t depth = 0, v = d;
+      uint32_t x = st[v];
+      uint32_t c = x >> 16, n = x & 0xFFFFu, base = rp[v], bs = c;
+      uint2 ent = load(base, bs, n);
       if (lane == 0) {
         stk[0] = d;
       }
-      tc_sync();
       bool found = false;
       for (;;) {
         if (++nsteps > H.budget) {
           overflow = true;
           break;
         }
-        const uint32_t v = stk[depth];
-        const uint32_t x = st[v];
-        const uint32_t c = x >> 16, n = x & 0xFFFFu;
         if (c >= n) {
-          // v exhausted: the search through it fails
+          // v exhausted: the search through it fails; back to its parent
+          if (lane == 0) {
+            st[v] = (n << 16) | n;
+          }
           if (depth == 0) {
             break;
           }
           --depth;
+          tc_sync();
+          v = stk[depth];
+          x = st[v];
+          c = x >> 16;
+          n = x & 0xFFFFu;
+          base = rp[v];
+          if (depth < kHvCache && c - fbs[depth] < 64u) {
+            bs = fbs[depth];
+            ent = cache[depth][lane];
+          } else {
+            bs = c;
+            ent = load(base, bs, n);
+          }
           continue;
         }
-        // v's next (up to) 64 pathLinks: one round trip; their tails' states
-        // from LDS.  Entries whose tail already failed are taken at once.
-        const uint32_t cnt = min(64u, n - c);
-        const bool have = lane < cnt;
-        uint2 ent = make_uint2(kInf32, 0);
-        if (have) {
-          ent = ar[rp[v] + c + lane];
+        if (c - bs >= 64u) {
+          bs = c;
+          ent = load(base, bs, n);
         }
+        const uint32_t idx = bs + lane;
         const uint32_t u = ent.x;
         bool live = false;
-        if (have) {
+        if (idx >= c && idx < n) {
           if (u == s) {
             live = true;
           } else {
@@ -6537,19 +6685,16 @@ __global__ __launch_bounds__(64) void spf_trace_heavy_kernel(TraceHeavyArgs H) {
           }
         }
         const uint64_t lm = __ballot(live);
-        tc_sync(); // every lane read st[v] / st[u] before lane 0 moves v's cursor
         if (lm == 0) {
-          if (lane == 0) {
-            st[v] = x + (cnt << 16);
-          }
-          tc_sync();
+          // every remaining entry of the batch has a failed tail: taken
+          c = min(n, bs + 64u);
           continue;
         }
-        const int f = (int)__builtin_ctzll(lm);
-        const uint32_t fu = (uint32_t)__builtin_amdgcn_readlane((int)u, f);
-        const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)ent.y, f);
+        const uint32_t f = (uint32_t)__builtin_ctzll(lm);
+        const uint32_t fu = (uint32_t)__builtin_amdgcn_readlane((int)u, (int)f);
+        const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)ent.y, (int)f);
+        c = bs + f + 1;
         if (lane == 0) {
-          st[v] = x + (((uint32_t)f + 1) << 16);
           lnk[depth] = fl;
         }
         if (fu == s) {
@@ -6560,16 +6705,41 @@ __global__ __launch_bounds__(64) void spf_trace_heavy_kernel(TraceHeavyArgs H) {
           overflow = true;
           break;
         }
+        // push: v's cursor and batch saved, fu entered
+        ++npush;
+        if (lane == 0) {
+          st[v] = (c << 16) | n;
+        }
+        if (depth < kHvCache) {
+          cache[depth][lane] = ent;
+          if (lane == 0) {
+            fbs[depth] = bs;
+          }
+        }
         ++depth;
         if (lane == 0) {
           stk[depth] = fu;
         }
         tc_sync();
+        v = fu;
+        x = st[v];
+        c = x >> 16;
+        n = x & 0xFFFFu;
+        base = rp[v];
+        bs = c;
+        ent = load(base, bs, n);
       }
-      if (overflow || !found) {
+      if (overflow) {
         break;
       }
+      // the frame the search ended in keeps its cursor
+      if (lane == 0) {
+        st[v] = (c << 16) | n;
+      }
       tc_sync();
+      if (!found) {
+        break;
+      }
       const uint32_t len = depth + 1;
       if (nl + len > a.cap || npaths + 1 > a.cap) {
         overflow = true;
@@ -6590,6 +6760,282 @@ __global__ __launch_bounds__(64) void spf_trace_heavy_kernel(TraceHeavyArgs H) {
   if (lane == 0) {
     a.out_n[q] = overflow ? kTraceOverflow : npaths;
     a.out_len[q] = overflow ? 0u : nl;
+    if (H.hstat) {
+      unsigned long long* o = H.hstat + 4 * (size_t)hi;
+      o[0] = wall_clock64() - t0;
+      o[1] = nsteps;
+      o[2] = npush;
+      o[3] = nload;
+    }
+  }
+}
+
+// The same traces without the DFS (spf_trace_reach_kernel, the default heavy
+// kernel).  traceOnePath from v succeeds iff the source reaches v over links
+// not yet visited (DFS completeness on the pathLinks DAG: a failed branch only
+// visits links whose tail the source cannot reach, so it never cuts a path
+// another branch needs).  The DFS therefore returns the GREEDY walk from the
+// destination: at each node the first pathLink whose link is unvisited and
+// whose tail is the source or reachable; and the links a failed branch
+// visits never matter again (reachability only shrinks).  So the kernel keeps
+//   cnt[v] = # pathLinks of v with a live link and a reachable tail
+// (reachable = cnt > 0; initially every node of the row: cnt = length),
+// walks one path per iteration (one wave, a global load per node), removes
+// the path's links and propagates the nodes whose count drops to 0 along
+// their out-edges (all waves, level by level).  Output identical to the DFS
+// (tests/test_trace_paths_gpu.py: the literal recursion); a 16-deep DAG
+// walk replaces ~15k dependent DFS steps on the fabric's slowest query.
+// LDS words of the reach kernel's per-node and per-link arrays (dynamic
+// LDS, sized per launch): st, dist, row [V + 1], transit and ancestor
+// bitsets, removed-link bitset
+__host__ __device__ inline size_t reach_lds_words(uint32_t V, uint32_t L) {
+  return 3 * (size_t)V + 1 + 2 * (((size_t)V + 31) / 32) + ((size_t)L + 31) / 32;
+}
+constexpr size_t kRqMaxLds = 150u << 10;
+constexpr uint32_t kRqThreads = 1024;
+
+// st[v] fields: live-pathLink count (cnt), list length, next candidate index
+__device__ __forceinline__ uint32_t rq_cnt(uint32_t x) { return x & 0xFFFu; }
+__device__ __forceinline__ uint32_t rq_len(uint32_t x) { return (x >> 12) & 0x3FFu; }
+__device__ __forceinline__ uint32_t rq_pos(uint32_t x) { return x >> 22; }
+
+__global__ __launch_bounds__(kRqThreads) void spf_trace_reach_kernel(TraceHeavyArgs H) {
+  const TraceArgs& a = H.t;
+  extern __shared__ __align__(16) uint32_t rq_smem[];
+  const uint32_t V = H.V;
+  uint32_t* st = rq_smem;            // [V] pos << 22 | len << 12 | cnt
+  uint32_t* dl = st + V;             // [V] the row's distances
+  uint32_t* rp = dl + V;             // [V + 1] CSR row offsets = arena bases
+  uint32_t* tr = rp + V + 1;         // [V / 32] transit bits
+  uint32_t* inc = tr + (V + 31) / 32; // [V / 32] the destination's ancestors
+  uint32_t* rm = inc + (V + 31) / 32; // [L / 32] removed (ignored or found) links
+  __shared__ uint32_t lnk[kTcDepth];   // the walk's links, destination first
+  __shared__ uint32_t wnode[kTcDepth]; // the walk's nodes (heads of lnk)
+  __shared__ uint32_t sh_len, sh_flag, sh_fn[2];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  constexpr uint32_t nw = kRqThreads / 64;
+  const uint32_t hi = blockIdx.x;
+  const uint32_t q = H.hq[hi];
+  const uint32_t s = a.src[q], d = a.dst[q];
+  const uint32_t* dist = a.dist + (size_t)q * a.Vp;
+  const uint32_t* lenq = H.len + (size_t)hi * V;
+  const uint2* ar = H.arena + (size_t)hi * H.E;
+  const uint32_t ilo = a.ign_off ? a.ign_off[q] : 0u;
+  const uint32_t nign = a.ign_off ? a.ign_off[q + 1] - ilo : 0u;
+  // frontiers in global scratch: a node enters each BFS at most once, so V
+  // slots per level never overflow (a fabric level of RSWs can be thousands)
+  uint32_t* fq[2] = {H.fq + (size_t)hi * 2 * V, H.fq + (size_t)hi * 2 * V + V};
+  const uint64_t t0 = H.hstat ? wall_clock64() : 0ull;
+  uint32_t nwalk = 0, ncas = 0;
+  if (tid == 0) {
+    sh_flag = 0;
+  }
+  bool bad = false;
+  for (uint32_t v = tid; v < V; v += kRqThreads) {
+    const uint32_t n = lenq[v];
+    bad = bad || n == kInf32;
+    st[v] = n == kInf32 ? 0u : (n << 12) | n;
+    dl[v] = dist[v];
+    rp[v] = a.row[v];
+  }
+  if (tid == 0) {
+    rp[V] = a.row[V];
+  }
+  for (uint32_t i = tid; i < (V + 31) / 32; i += kRqThreads) {
+    tr[i] = a.trbits[i];
+    inc[i] = 0u;
+  }
+  for (uint32_t i = tid; i < (H.L + 31) / 32; i += kRqThreads) {
+    rm[i] = 0u;
+  }
+  __syncthreads();
+  if (bad) {
+    sh_flag = 1; // a list over kTcSort entries: traced on the host
+  }
+  // ignored links never tighten a pathLink: removed from the start (the
+  // cascade's edge test then needs no ignore-list lookup)
+  for (uint32_t i = tid; i < nign; i += kRqThreads) {
+    const uint32_t l = a.ign[ilo + i];
+    if (l < H.L) {
+      atomicOr(&rm[l >> 5], 1u << (l & 31));
+    }
+  }
+  // the walk only visits ancestors of d in the pathLinks DAG, and a node
+  // outside that set never feeds one inside (its out-neighbours are outside
+  // too): counts are kept, and cascades followed, on the ancestors only
+  if (tid == 0) {
+    inc[d >> 5] |= 1u << (d & 31);
+    fq[0][0] = d;
+    sh_fn[0] = 1;
+  }
+  __syncthreads();
+  const uint32_t sub = lane >> 4, sl = lane & 15u; // 4 nodes per wave, 16 lanes each
+  if (sh_flag == 0 && s != d && dl[d] != kInf32) {
+    uint32_t cur = 0;
+    for (;;) {
+      const uint32_t fn = sh_fn[cur];
+      if (fn == 0) {
+        break;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        sh_fn[cur ^ 1] = 0;
+      }
+      __syncthreads();
+      for (uint32_t i = wv * 4 + sub; i < fn; i += nw * 4) {
+        const uint32_t v = fq[cur][i];
+        const uint32_t n = rq_len(st[v]), base = rp[v];
+        for (uint32_t j = sl; j < n; j += 16) {
+          const uint32_t u = ar[base + j].x;
+          if (u != s && !(atomicOr(&inc[u >> 5], 1u << (u & 31)) & (1u << (u & 31)))) {
+            fq[cur ^ 1][atomicAdd(&sh_fn[cur ^ 1], 1u)] = u;
+          }
+        }
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+  __syncthreads();
+  bool overflow = sh_flag != 0;
+  uint32_t* out_links = a.out_links + (size_t)q * a.cap;
+  uint32_t* out_ends = a.out_ends + (size_t)q * a.cap;
+  uint32_t npaths = 0, nl = 0;
+  auto removed = [&](uint32_t l) { return (rm[l >> 5] >> (l & 31)) & 1u; };
+  if (!overflow && s != d && dl[d] != kInf32) {
+    for (;;) { // one traceOnePath per iteration
+      if (rq_cnt(st[d]) == 0) {
+        break; // the destination is no longer reachable: the trace fails
+      }
+      // the walk (wave 0): the first live pathLink with a reachable tail
+      if (wv == 0) {
+        uint32_t v = d, h = 0;
+        bool ovf = false;
+        for (;;) {
+          if (++nwalk > H.budget) {
+            ovf = true;
+            break;
+          }
+          const uint32_t x = st[v];
+          const uint32_t n = rq_len(x), base = rp[v];
+          uint32_t p = rq_pos(x);
+          uint32_t f = kInf32;
+          uint2 ent = make_uint2(kInf32, 0u);
+          for (; p < n; p += 64) {
+            const uint32_t idx = p + lane;
+            ent = idx < n ? ar[base + idx] : make_uint2(kInf32, 0u);
+            bool ok = false;
+            if (idx < n && !removed(ent.y)) {
+              ok = ent.x == s || rq_cnt(st[ent.x]) != 0;
+            }
+            const uint64_t m = __ballot(ok);
+            if (m) {
+              f = (uint32_t)__builtin_ctzll(m);
+              break;
+            }
+          }
+          if (f == kInf32 || h >= kTcDepth) {
+            ovf = true; // no live entry cannot happen while cnt[v] > 0
+            break;
+          }
+          const uint32_t u = (uint32_t)__builtin_amdgcn_readlane((int)ent.x, (int)f);
+          const uint32_t l = (uint32_t)__builtin_amdgcn_readlane((int)ent.y, (int)f);
+          if (lane == 0) {
+            // earlier entries are dead for good
+            st[v] = ((p + f) << 22) | (x & 0x3FFFFFu);
+            lnk[h] = l;
+            wnode[h] = v;
+          }
+          ++h;
+          if (u == s) {
+            break;
+          }
+          v = u;
+        }
+        if (lane == 0) {
+          sh_len = h;
+          if (ovf) {
+            sh_flag = 1;
+          }
+        }
+      }
+      __syncthreads();
+      if (sh_flag) {
+        overflow = true;
+        break;
+      }
+      const uint32_t len = sh_len;
+      if (nl + len > a.cap || npaths + 1 > a.cap) {
+        overflow = true;
+        break;
+      }
+      // the path out (source first), then its links removed: each head
+      // loses one reachable pathLink; heads left with none start the cascade
+      for (uint32_t i = tid; i < len; i += kRqThreads) {
+        out_links[nl + i] = lnk[len - 1 - i];
+      }
+      nl += len;
+      if (tid == 0) {
+        out_ends[npaths] = nl;
+        sh_fn[0] = 0;
+      }
+      ++npaths;
+      __syncthreads();
+      for (uint32_t i = tid; i < len; i += kRqThreads) {
+        const uint32_t l = lnk[i], v = wnode[i];
+        atomicOr(&rm[l >> 5], 1u << (l & 31));
+        if (rq_cnt(atomicSub(&st[v], 1u)) == 1u) {
+          fq[0][atomicAdd(&sh_fn[0], 1u)] = v;
+        }
+      }
+      __syncthreads();
+      // cascade, level by level: a node that lost its last reachable
+      // pathLink takes the support it gave its out-neighbours' lists
+      uint32_t cur = 0;
+      for (;;) {
+        const uint32_t fn = sh_fn[cur];
+        if (fn == 0) {
+          break;
+        }
+        __syncthreads();
+        if (tid == 0) {
+          sh_fn[cur ^ 1] = 0;
+        }
+        __syncthreads();
+        for (uint32_t i = wv * 4 + sub; i < fn; i += nw * 4) {
+          ++ncas;
+          const uint32_t v = fq[cur][i];
+          if (v != s && !((tr[v >> 5] >> (v & 31)) & 1u)) {
+            continue; // not transit: the tail of no pathLink
+          }
+          const uint32_t dv = dl[v];
+          const uint32_t e1 = rp[v + 1];
+          for (uint32_t e = rp[v] + sl; e < e1; e += 16) {
+            const uint32_t w = a.col[e], l = a.link[e];
+            const uint64_t wt = a.unit ? 1ull : (uint64_t)a.wout[e];
+            if (((inc[w >> 5] >> (w & 31)) & 1u) && (uint64_t)dv + wt == dl[w] && !removed(l)) {
+              if (rq_cnt(atomicSub(&st[w], 1u)) == 1u) {
+                fq[cur ^ 1][atomicAdd(&sh_fn[cur ^ 1], 1u)] = w;
+              }
+            }
+          }
+        }
+        __syncthreads();
+        cur ^= 1;
+      }
+      __syncthreads();
+    }
+  }
+  if (tid == 0) {
+    a.out_n[q] = overflow ? kTraceOverflow : npaths;
+    a.out_len[q] = overflow ? 0u : nl;
+    if (H.hstat) {
+      unsigned long long* o = H.hstat + 4 * (size_t)hi;
+      o[0] = wall_clock64() - t0;
+      o[1] = nwalk;
+      o[2] = npaths;
+      o[3] = ncas;
+    }
   }
 }
 
@@ -10806,6 +11252,10 @@ int spf_query_trace_paths(
   // queries past the cursor kernel's step budget go to the heavy launch
   // (spf_trace_heavy_kernel; its node states live in LDS: V <= kHvMaxV)
   const bool heavy = cursor && g->V <= kHvMaxV && env_flag("OPENR_SPF_TRACE_HEAVY", 1);
+  // the heavy queries' kernel: the reachability walk (its arrays fit LDS), or
+  // the DFS with LDS cursors (OPENR_SPF_TRACE_REACH=0)
+  const bool reach =
+      reach_lds_words(g->V, g->L) * 4 <= kRqMaxLds && env_flag("OPENR_SPF_TRACE_REACH", 1);
   if (cursor) {
     // cursor DFS: per-wave node states + pathLinks arena (zeroed per launch:
     // a state's tag is its query index + 1)
@@ -10894,14 +11344,33 @@ int spf_query_trace_paths(
         hq.push_back(i);
       }
     }
+    // build order: nodes of in-degree <= 16 first (four per wave)
+    std::vector<uint32_t> hv_nodes;
+    uint32_t hv_nsmall = 0;
+    if (!hq.empty()) {
+      hv_nodes.reserve(g->V);
+      for (uint32_t v = 0; v < g->V; ++v) {
+        if (g->row[v + 1] - g->row[v] <= 16) {
+          hv_nodes.push_back(v);
+        }
+      }
+      hv_nsmall = (uint32_t)hv_nodes.size();
+      for (uint32_t v = 0; v < g->V; ++v) {
+        if (g->row[v + 1] - g->row[v] > 16) {
+          hv_nodes.push_back(v);
+        }
+      }
+    }
     // chunks: arena + lengths bounded to ~1 GiB per launch
-    const size_t per = (size_t)g->E * sizeof(uint2) + (size_t)g->V * 4;
+    const size_t per = (size_t)g->E * sizeof(uint2) + (size_t)g->V * 12;
     const size_t chunk = std::max<size_t>(1, std::min<size_t>(1024, ((size_t)1 << 30) / per));
     for (size_t c0 = 0; c0 < hq.size(); c0 += chunk) {
       const uint32_t nh = (uint32_t)std::min(chunk, hq.size() - c0);
-      char* hb = nullptr; // hq [nh] | len [nh][V] | arena [nh][E]
-      const size_t o_len = ((size_t)nh * 4 + 255) & ~(size_t)255;
-      const size_t o_ar = (o_len + (size_t)nh * g->V * 4 + 255) & ~(size_t)255;
+      char* hb = nullptr; // nodes [V] | hq [nh] | len [nh][V] | frontiers [nh][2][V] | arena [nh][E]
+      const size_t o_hq = ((size_t)g->V * 4 + 255) & ~(size_t)255;
+      const size_t o_len = (o_hq + (size_t)nh * 4 + 255) & ~(size_t)255;
+      const size_t o_fq = (o_len + (size_t)nh * g->V * 4 + 255) & ~(size_t)255;
+      const size_t o_ar = (o_fq + (size_t)nh * g->V * 8 + 255) & ~(size_t)255;
       HIP_TRY(pool_malloc((void**)&hb, o_ar + (size_t)nh * g->E * sizeof(uint2)));
       struct Free {
         char* p;
@@ -10911,21 +11380,55 @@ int spf_query_trace_paths(
           pool_free(p);
         }
       } guard{hb, g->stream};
-      HIP_TRY(hipMemcpyAsync(hb, hq.data() + c0, (size_t)nh * 4, hipMemcpyHostToDevice, g->stream));
+      HIP_TRY(hipMemcpyAsync(hb, hv_nodes.data(), (size_t)g->V * 4, hipMemcpyHostToDevice,
+                             g->stream));
+      HIP_TRY(hipMemcpyAsync(hb + o_hq, hq.data() + c0, (size_t)nh * 4, hipMemcpyHostToDevice,
+                             g->stream));
       TraceHeavyArgs h{};
       h.t = a;
-      h.hq = reinterpret_cast<const uint32_t*>(hb);
+      h.hq = reinterpret_cast<const uint32_t*>(hb + o_hq);
+      h.nodes = reinterpret_cast<const uint32_t*>(hb);
+      h.nsmall = hv_nsmall;
       h.nh = nh;
       h.V = g->V;
       h.E = g->E;
       h.len = reinterpret_cast<uint32_t*>(hb + o_len);
+      h.fq = reinterpret_cast<uint32_t*>(hb + o_fq);
       h.arena = reinterpret_cast<uint2*>(hb + o_ar);
       h.budget = env_u32("OPENR_SPF_TRACE_HEAVY_BUDGET", 0xFFFFFFFFu);
-      const uint64_t items = (uint64_t)nh * g->V;
-      SPF_LAUNCH(spf_trace_heavy_build_kernel, dim3((uint32_t)((items + kHvWaves - 1) / kHvWaves)),
-                 dim3(64 * kHvWaves), 0, g->stream, h);
-      SPF_LAUNCH(spf_trace_heavy_kernel, dim3(nh), dim3(64), 0, g->stream, h);
+      const bool stats = env_flag("OPENR_SPF_TRACE_STATS", 0);
+      if (stats) {
+        HIP_TRY(hipMalloc((void**)&h.hstat, (size_t)nh * 32));
+      }
+      h.xcd = env_flag("OPENR_SPF_TRACE_HEAVY_XCD", 1) ? 1u : 0u;
+      const uint64_t bq = hv_blocks(hv_nsmall, g->V - hv_nsmall);
+      const uint64_t nblk = h.xcd ? 8 * ((nh + 7) / 8) * bq : (uint64_t)nh * bq;
+      SPF_LAUNCH(spf_trace_heavy_build_kernel, dim3((uint32_t)nblk), dim3(64 * kHvWaves), 0,
+                 g->stream, h);
+      h.L = g->L;
+      if (reach) {
+        const size_t lds = reach_lds_words(g->V, g->L) * 4;
+        HIP_TRY(hipFuncSetAttribute((const void*)spf_trace_reach_kernel,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        SPF_LAUNCH(spf_trace_reach_kernel, dim3(nh), dim3(kRqThreads), lds, g->stream, h);
+      } else {
+        SPF_LAUNCH(spf_trace_heavy_kernel, dim3(nh), dim3(64), 0, g->stream, h);
+      }
       HIP_TRY(hipGetLastError());
+      if (stats) {
+        std::vector<unsigned long long> hs((size_t)nh * 4);
+        HIP_TRY(hipStreamSynchronize(g->stream));
+        HIP_TRY(hipMemcpy(hs.data(), h.hstat, hs.size() * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipFree(h.hstat));
+        size_t im = 0;
+        for (size_t i = 1; i < nh; ++i) {
+          if (hs[4 * i] > hs[4 * im]) {
+            im = i;
+          }
+        }
+        fprintf(stderr, "[trace heavy stats] nh=%u slowest: ticks=%llu steps=%llu pushes=%llu loads=%llu\n",
+                nh, hs[4 * im], hs[4 * im + 1], hs[4 * im + 2], hs[4 * im + 3]);
+      }
     }
     if (!hq.empty()) {
       HIP_TRY(hipMemcpyAsync(path_count, a.out_n, (size_t)count * 4, hipMemcpyDeviceToHost,
@@ -10935,6 +11438,14 @@ int spf_query_trace_paths(
       HIP_TRY(hipStreamSynchronize(g->stream));
     }
     q->trace_heavy = (uint32_t)hq.size();
+    if (!hq.empty() && env_flag("OPENR_SPF_TRACE_STATS", 0)) {
+      uint32_t still = 0;
+      for (uint32_t i : hq) {
+        still += path_count[i] == SPF_TRACE_OVERFLOW;
+      }
+      fprintf(stderr, "[trace heavy] queries=%u re-traced=%zu still-overflow=%u\n", count,
+              hq.size(), still);
+    }
   }
   q->trace_n = count;
   q->trace_pc.assign(path_count, path_count + count);

@@ -144,16 +144,20 @@ def test_trace_paths_visited_set_overflow(gpu_ready, cursor, monkeypatch):
             assert got == trace_all(csr, spf_py.run_spf(csr, src, False), src, dst)
 
 
-@pytest.mark.parametrize("seed,unit", [(5, False), (6, True)])
-def test_trace_paths_heavy_launch(gpu_ready, seed, unit, monkeypatch):
+@pytest.mark.parametrize("reach", ["1", "0"])
+@pytest.mark.parametrize("seed,unit", [(5, False), (6, True), (7, False)])
+def test_trace_paths_heavy_launch(gpu_ready, seed, unit, reach, monkeypatch):
     """Queries past the cursor kernel's step budget are re-traced by the heavy
-    launch (spf_trace_heavy_build_kernel + spf_trace_heavy_kernel: every
-    node's pathLinks pre-built, the cursors in LDS).  With a budget of one
-    step every query takes that path; the traces must equal the recursion's,
-    for the k = 1 rows and the KSP2 ignore-list rows.  A heavy budget too
-    small reports overflow (None), never a wrong path."""
+    launch: spf_trace_heavy_build_kernel pre-builds every node's pathLinks,
+    then spf_trace_reach_kernel (reachability counts + greedy walk, the
+    default) or spf_trace_heavy_kernel (the DFS with LDS cursors,
+    OPENR_SPF_TRACE_REACH=0) traces.  With a budget of one step every query
+    takes that path; the traces must equal the recursion's, for the k = 1
+    rows and the KSP2 ignore-list rows.  A heavy budget too small reports
+    overflow (None), never a wrong path."""
     sys.setrecursionlimit(10000)
     monkeypatch.setenv("OPENR_SPF_TRACE_BUDGET", "1")
+    monkeypatch.setenv("OPENR_SPF_TRACE_REACH", reach)
     rng = random.Random(seed)
     V = 150
     links = random_links(rng, V, 520, wmax=1 if unit else 5)
@@ -166,7 +170,7 @@ def test_trace_paths_heavy_launch(gpu_ready, seed, unit, monkeypatch):
     flags = abi.SPF_F_UNIT_METRIC if unit else 0
     q1 = g.query([src] * len(dsts), flags).run()
     got1 = q1.trace_paths(dsts)
-    assert "spf_trace_heavy_kernel" in q1.kernels()
+    assert ("spf_trace_reach_kernel" if reach == "1" else "spf_trace_heavy_kernel") in q1.kernels()
     ref = spf_py.run_spf(csr, src, not unit)
     first = []
     for d, got in zip(dsts, got1):
@@ -193,10 +197,12 @@ def test_trace_paths_heavy_launch(gpu_ready, seed, unit, monkeypatch):
     assert n_over > 0
 
 
-def test_trace_paths_heavy_bipartite(gpu_ready, monkeypatch):
+@pytest.mark.parametrize("reach", ["1", "0"])
+def test_trace_paths_heavy_bipartite(gpu_ready, reach, monkeypatch):
     """The two-layer bipartite case (1,600 middle links) through the heavy
     launch only."""
     monkeypatch.setenv("OPENR_SPF_TRACE_BUDGET", "1")
+    monkeypatch.setenv("OPENR_SPF_TRACE_REACH", reach)
     sys.setrecursionlimit(10000)
     m = 40
     V = 2 + 2 * m
@@ -210,4 +216,4 @@ def test_trace_paths_heavy_bipartite(gpu_ready, monkeypatch):
     got = q.trace_paths([dst, 1 + m])
     ref = spf_py.run_spf(csr, src, False)
     assert got == [trace_all(csr, ref, src, dst), trace_all(csr, ref, src, 1 + m)]
-    assert "spf_trace_heavy_kernel" in q.kernels()
+    assert ("spf_trace_reach_kernel" if reach == "1" else "spf_trace_heavy_kernel") in q.kernels()

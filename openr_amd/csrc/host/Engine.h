@@ -44,6 +44,8 @@ struct LinkState::Engine {
   // their capacity: no fresh pages per flap)
   std::vector<uint32_t> spareRow, spareCol, spareLinkId, spareRev;
   std::vector<uint64_t> spareMetric;
+  std::vector<std::array<uint32_t, 2>> spareHalves; // the halves a splice replaced
+  std::vector<uint8_t> spareAlive;
   // link ids freed by in-place link removals (LinkState::patchStructure):
   // links[id] == nullptr, reused by the next link that comes up
   std::vector<uint32_t> freeIds;

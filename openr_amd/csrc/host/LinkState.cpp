@@ -15,6 +15,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -1489,6 +1490,20 @@ bool LinkState::patchStructure(
     return false;
   }
   const auto t0 = std::chrono::steady_clock::now();
+  // OPENR_LS_SPLICE_TIMING=1: phase times of the splice on stderr (diagnostics)
+  static const bool splTiming = [] {
+    const char* e = std::getenv("OPENR_LS_SPLICE_TIMING");
+    return e && std::atoi(e) != 0;
+  }();
+  auto tp = t0;
+  auto mark = [&](const char* what) {
+    if (splTiming) {
+      const auto t = std::chrono::steady_clock::now();
+      std::fprintf(stderr, "[patchStructure] %-10s %8.3f ms\n", what,
+                   std::chrono::duration<double, std::milli>(t - tp).count());
+      tp = t;
+    }
+  };
   auto& eng = *engine_;
   const uint32_t V = (uint32_t)eng.names.size();
   std::vector<uint8_t> aff(V, 0);
@@ -1537,16 +1552,58 @@ bool LinkState::patchStructure(
     }
   }
   const uint32_t E = newRow[V];
+  mark("rows");
   // link ids: freed for the links going down, taken for the ones coming up.
   // eng.links is not copied (a copy of ~100k shared_ptrs is two atomic
   // refcount updates per link, ~2 ms on the fabric): which ids are alive is a
-  // byte per id, and the id -> Link changes are applied at the commit
-  std::vector<uint8_t> alive(eng.links.size());
-  for (size_t i = 0; i < eng.links.size(); ++i) {
-    alive[i] = eng.links[i] != nullptr;
+  // byte per id, and the id -> Link changes are applied at the commit.  The
+  // byte and halves arrays of the last splice are reused (no fresh pages).
+  std::vector<uint8_t> alive = std::move(eng.spareAlive);
+  alive.resize(eng.links.size());
+  std::vector<std::array<uint32_t, 2>> halves = std::move(eng.spareHalves);
+  halves.resize(eng.halves.size());
+  {
+    // one parallel pass: the alive bytes, and the halves moved to the new
+    // CSR.  Only the affected rows change length, so a kept half-edge e moves
+    // by the summed length change of the affected rows before it (a few
+    // ranges: no per-edge lookup of its tail); a half in an affected row is
+    // re-set below.
+    std::vector<std::array<uint32_t, 3>> rng; // old [begin, end), shift after it
+    int64_t cum = 0;
+    for (uint32_t u : affNodes) {
+      cum += (int64_t)(newRow[u + 1] - newRow[u]) - (int64_t)(eng.row[u + 1] - eng.row[u]);
+      rng.push_back({eng.row[u], eng.row[u + 1], (uint32_t)cum});
+    }
+    auto moved = [&](uint32_t e) -> uint32_t {
+      uint32_t d = 0;
+      for (const auto& r : rng) {
+        if (e < r[0]) {
+          break;
+        }
+        if (e < r[1]) {
+          return ~0u;
+        }
+        d = r[2];
+      }
+      return e + d; // modular: a negative shift wraps back
+    };
+    constexpr size_t kLB = 16384;
+    const size_t nl = std::max(eng.links.size(), eng.halves.size());
+    parallelFor((nl + kLB - 1) / kLB, hostThreads(nl, 1u << 14), [&](size_t b, unsigned) {
+      const size_t i1 = std::min(nl, (b + 1) * kLB);
+      for (size_t i = b * kLB; i < i1; ++i) {
+        if (i < eng.links.size()) {
+          alive[i] = eng.links[i] != nullptr;
+        }
+        if (i < eng.halves.size()) {
+          const auto& h = eng.halves[i];
+          halves[i] = {h[0] == ~0u ? ~0u : moved(h[0]), h[1] == ~0u ? ~0u : moved(h[1])};
+        }
+      }
+    }, 1);
   }
   std::vector<std::pair<uint32_t, std::shared_ptr<Link>>> linkSets; // applied at the commit
-  std::vector<std::array<uint32_t, 2>> halves = eng.halves;
+  mark("ids");
   std::vector<uint32_t> freeIds = eng.freeIds;
   std::vector<spf_edge_delta> dMetric, dHops;
   for (const auto& l : down) {
@@ -1585,32 +1642,19 @@ bool LinkState::patchStructure(
     return it != upIds.end() ? it->second : eng.linkIdOf(l);
   };
   // the copies and scatters below run in blocks on the host pool (one
-  // writer per element: a kept half / row / link id belongs to one block)
-  constexpr size_t kBlk = 4096;
+  // writer per element: a kept half / row / link id belongs to one block);
+  // node blocks are small because a fabric's high-degree rows are adjacent
+  constexpr size_t kBlk = 4096, kNodeBlk = 256;
   const unsigned nth = hostThreads(eng.col.size(), 1u << 15);
-  // kept halves shift with their row; halves in affected rows are re-set below
-  const size_t nOld = std::min(halves.size(), eng.halves.size());
-  parallelFor((nOld + kBlk - 1) / kBlk, nth, [&](size_t b, unsigned) {
-    const size_t l1 = std::min(nOld, (b + 1) * kBlk);
-    for (size_t lid = b * kBlk; lid < l1; ++lid) {
-      for (int s = 0; s < 2; ++s) {
-        const uint32_t e = halves[lid][s];
-        if (e == ~0u) {
-          continue;
-        }
-        const uint32_t tail = eng.col[eng.rev[e]];
-        halves[lid][s] = aff[tail] ? ~0u : e - eng.row[tail] + newRow[tail];
-      }
-    }
-  }, 1);
+  mark("shift");
   std::vector<uint32_t> col = std::move(eng.spareCol), linkId = std::move(eng.spareLinkId);
   std::vector<uint64_t> metric = std::move(eng.spareMetric);
   col.resize(E);
   linkId.resize(E);
   metric.resize(E);
-  parallelFor((V + kBlk - 1) / kBlk, nth, [&](size_t b, unsigned) {
-    const uint32_t u1 = (uint32_t)std::min<size_t>(V, (b + 1) * kBlk);
-    for (uint32_t u = (uint32_t)(b * kBlk); u < u1; ++u) {
+  parallelFor((V + kNodeBlk - 1) / kNodeBlk, nth, [&](size_t b, unsigned) {
+    const uint32_t u1 = (uint32_t)std::min<size_t>(V, (b + 1) * kNodeBlk);
+    for (uint32_t u = (uint32_t)(b * kNodeBlk); u < u1; ++u) {
       if (!aff[u]) {
         const uint32_t a = eng.row[u], z = eng.row[u + 1], o = newRow[u];
         std::copy(eng.col.begin() + a, eng.col.begin() + z, col.begin() + o);
@@ -1639,6 +1683,7 @@ bool LinkState::patchStructure(
       }
     }
   }
+  mark("copy");
   std::vector<uint32_t> rev = std::move(eng.spareRev);
   rev.assign(E, ~0u);
   std::atomic<bool> oneHalf{false};
@@ -1733,6 +1778,7 @@ bool LinkState::patchStructure(
   // spf_graph_update).  A failed update leaves it unusable: it is dropped,
   // and the caller's clearMemo() retires the engine, whose next build
   // creates a fresh graph
+  mark("rev+rest");
   const auto tu = std::chrono::steady_clock::now();
   Counters::add("decision.graph_splice_us",
                 std::chrono::duration_cast<std::chrono::microseconds>(tu - t0).count());
@@ -1779,7 +1825,9 @@ bool LinkState::patchStructure(
   for (auto& [lid, l] : linkSets) {
     eng.links[lid] = std::move(l); // in order: a freed id taken again ends up set
   }
+  eng.spareHalves = std::move(eng.halves);
   eng.halves = std::move(halves);
+  eng.spareAlive = std::move(alive);
   eng.freeIds = std::move(freeIds);
   eng.exact = spf_graph_needs_exact(eng.graph) != 0;
   if (memoScreenEnabled() && !eng.exact) {

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
@@ -43,6 +44,9 @@ inline unsigned hostThreads(size_t n, size_t minPerThread = 64) {
 // host thread) or from inside a worker falls back to fresh threads.  The pool
 // is never destroyed (its detached workers park on a condition variable); a
 // forked child starts a new, empty one.  OPENR_HOST_POOL=0: fresh threads.
+// After a section the workers (and the caller, for the join) spin for up to
+// kSpin before blocking, so back-to-back sections (a graph rebuild runs ~10)
+// start without a futex wake-up each.
 class HostPool {
  public:
   static HostPool& get() {
@@ -79,11 +83,15 @@ class HostPool {
       want_ = threads - 1;
       pending_ = threads - 1;
       ++gen_;
+      awant_.store(want_, std::memory_order_relaxed);
+      apending_.store(pending_, std::memory_order_relaxed);
+      agen_.store(gen_, std::memory_order_release);
     }
     cv_.notify_all();
     inWorker() = true; // a nested section on this thread starts fresh threads
     body(0);
     inWorker() = false;
+    spinUntil([this] { return apending_.load(std::memory_order_acquire) == 0; });
     std::unique_lock<std::mutex> l(mu_);
     done_.wait(l, [this] { return pending_ == 0; });
     body_ = nullptr;
@@ -99,11 +107,28 @@ class HostPool {
     static thread_local bool w = false;
     return w;
   }
+  static constexpr auto kSpin = std::chrono::microseconds(200);
+  template <class Pred>
+  static void spinUntil(Pred&& done) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned i = 1; !done(); ++i) {
+      if ((i & 127) == 0 && std::chrono::steady_clock::now() - t0 > kSpin) {
+        return;
+      }
+#if defined(__x86_64__)
+      __builtin_ia32_pause();
+#endif
+    }
+  }
   void loop(unsigned id) {
     inWorker() = true;
     uint64_t seen = 0;
     for (;;) {
       const std::function<void(unsigned)>* body;
+      spinUntil([&] {
+        return agen_.load(std::memory_order_acquire) != seen &&
+            id <= awant_.load(std::memory_order_relaxed);
+      });
       {
         std::unique_lock<std::mutex> l(mu_);
         cv_.wait(l, [&] { return gen_ != seen && id <= want_; });
@@ -113,6 +138,7 @@ class HostPool {
       (*body)(id);
       {
         std::lock_guard<std::mutex> l(mu_);
+        apending_.fetch_sub(1, std::memory_order_release);
         if (--pending_ == 0) {
           done_.notify_one();
         }
@@ -127,6 +153,9 @@ class HostPool {
   const std::function<void(unsigned)>* body_ = nullptr;
   unsigned want_ = 0, pending_ = 0;
   uint64_t gen_ = 0;
+  // lock-free mirrors of gen_ / want_ / pending_ for the spins
+  std::atomic<uint64_t> agen_{0};
+  std::atomic<unsigned> awant_{0}, apending_{0};
 };
 
 // fn(item, worker) for item in [0, n), chunks handed out dynamically.  The

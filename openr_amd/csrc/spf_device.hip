@@ -94,10 +94,38 @@ namespace {
 constexpr uint32_t kBlock = 512;           // threads per workgroup (8 waves)
 constexpr uint32_t kWaves = kBlock / 64;
 constexpr uint32_t kInf32 = 0xFFFFFFFFu;
-// nodes per host-pool work item of the graph preparation loops
-constexpr uint32_t kHostBlock = 512;
 // host passes over the CSR go parallel from this many edges per thread
 constexpr size_t kHostMinEdges = 1u << 14;
+
+// Node blocks of about equal work (edges + nodes) for the host passes over a
+// CSR: name ranks put the fabric's 1,672 FSW / SSW nodes (71 % of its edges)
+// into 3-4 of twenty fixed 512-node blocks, so one worker did most of every
+// pass (profiles/r05ah).  Boundaries b[0] = 0 < ... < b.back() = V.
+std::vector<uint32_t> host_node_blocks(const uint32_t* row, uint32_t V, unsigned nth) {
+  std::vector<uint32_t> b{0};
+  if (!V) {
+    return b;
+  }
+  const uint64_t work = (uint64_t)row[V] - row[0] + V;
+  const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(V, 8 * std::max(1u, nth)));
+  const uint64_t target = std::max<uint64_t>(1, work / nb);
+  uint32_t u = 0;
+  while (u < V) {
+    // the first u' > u with (row[u'] - row[u]) + (u' - u) >= target
+    uint32_t lo = u + 1, hi = V;
+    while (lo < hi) {
+      const uint32_t mid = lo + (hi - lo) / 2;
+      if ((uint64_t)(row[mid] - row[u]) + (mid - u) >= target) {
+        hi = mid;
+      } else {
+        lo = mid + 1;
+      }
+    }
+    u = lo;
+    b.push_back(u);
+  }
+  return b;
+}
 constexpr uint32_t kCtlWords = 32;         // qlen + scan scratch (<= 16 waves + 1)
 constexpr size_t kLdsLimit = 160 * 1024;   // gfx950 LDS per CU
 constexpr uint32_t kIgnLdsMax = 2048;      // ignore-list entries staged in LDS
@@ -7152,10 +7180,8 @@ struct spf_graph {
   size_t cap_e = 0, cap_w = 0, cap_cw = 0, cap_half = 0;
   // host scratch of the preparation passes, kept for in-place rebuilds
   std::vector<uint32_t> scratch_e, scratch_v, scratch_slot;
-  std::vector<uint32_t> h_wout, h_win, h_cw;
   // spf_graph_update: the CSR and neighbour lists it replaced (reused rows)
   std::vector<uint32_t> old_row, old_col, old_nbr_off, old_nbrs, old_slot;
-  std::vector<uint32_t> h_sell, h_half; // upload_sell / link-half staging
   size_t cap_sell = 0, cap_sell_off = 0;
   // pinned staging of the preparation uploads (g_stage): one DMA per array
   // on the graph stream instead of a pageable synchronous hipMemcpy each
@@ -7575,6 +7601,80 @@ int build_nl_v2(spf_query* q, const uint32_t* sources, const std::vector<int32_t
   return SPF_OK;
 }
 
+// ---- graph preparation on the device (spf_graph_create / _update) ----
+// The raw CSR goes up once; the arrays derived from it per edge are built
+// here instead of on the host and uploaded (a link flap's rebuild spent
+// ~0.8 ms of host passes and 4 MB of staging on them, profiles/r05aj).
+struct DeriveArgs {
+  const uint32_t* col;
+  const uint32_t* rev;
+  const uint32_t* link;
+  const uint64_t* w64;
+  uint32_t* wout;      // min(w64[e], 2^32 - 1)
+  uint32_t* win;       // wout of the reverse half-edge
+  uint32_t* cw;        // col | wout << cw_bits (nullptr: not packed); [E4], zero tail
+  uint32_t* link_half; // [2L] half-edges of each link (pre-filled with ~0)
+  uint32_t E, E4, cw_bits;
+};
+
+__global__ __launch_bounds__(256) void spf_graph_derive_kernel(DeriveArgs a) {
+  const uint32_t e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= a.E4) {
+    return;
+  }
+  if (e >= a.E) {
+    if (a.cw) {
+      a.cw[e] = 0u; // padding of the last 16-byte chunk
+    }
+    return;
+  }
+  const uint32_t r = a.rev[e];
+  const uint32_t wo = (uint32_t)min(a.w64[e], (uint64_t)0xFFFFFFFFull);
+  a.wout[e] = wo;
+  a.win[e] = (uint32_t)min(a.w64[r], (uint64_t)0xFFFFFFFFull);
+  if (a.cw) {
+    a.cw[e] = a.col[e] | (wo << a.cw_bits);
+  }
+  a.link_half[2 * (size_t)a.link[e] + (e < r ? 0 : 1)] = e;
+}
+
+// The sliced-ELL copy (layout at upload_sell): one thread per word.
+struct SellArgs {
+  const uint32_t* row;
+  const uint32_t* col;
+  const uint32_t* sell_off; // [ns + 1] in 64-uint4 groups
+  uint32_t* sell;           // [sell_off[ns] * 256]
+  uint32_t V, ns, words;
+};
+
+__global__ __launch_bounds__(256) void spf_sell_kernel(SellArgs a) {
+  const uint32_t w = blockIdx.x * 256 + threadIdx.x;
+  if (w >= a.words) {
+    return;
+  }
+  const uint32_t grp = w >> 8, L = (w >> 2) & 63u;
+  // the slice holding this group (sell_off is ascending)
+  uint32_t lo = 0, hi = a.ns;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a.sell_off[mid] <= grp) {
+      lo = mid;
+    } else {
+      hi = mid;
+    }
+  }
+  const uint32_t c = lo, j = (grp - a.sell_off[c]) * 4 + (w & 3u);
+  const uint32_t v = 64 * c + L;
+  uint32_t x = v < a.V ? v : 0u; // short rows padded with the node itself
+  if (v < a.V) {
+    const uint32_t r0 = a.row[v];
+    if (j < a.row[v + 1] - r0) {
+      x = a.col[r0 + j];
+    }
+  }
+  a.sell[w] = x;
+}
+
 // memcpy in 256 KB chunks on the host pool (a graph rebuild moves tens of MB
 // through host copies: single-threaded they cost ~25 GB/s)
 void par_copy(void* dst, const void* src, size_t bytes) {
@@ -7596,6 +7696,32 @@ template <typename T>
 void par_assign(std::vector<T>& v, const T* src, size_t n) {
   v.resize(n);
   par_copy(v.data(), src, n * sizeof(T));
+}
+
+// several copies in ONE parallel section (256 KB chunks of all of them): a
+// section costs ~40-100 us of worker wake-ups, and a graph rebuild made ~30
+// of them one array at a time (profiles/r05w linkflap.err)
+struct CopyItem {
+  void* dst;
+  const void* src;
+  size_t bytes;
+};
+
+void par_copy_many(const CopyItem* it, size_t n) {
+  constexpr size_t kChunk = (size_t)256 << 10;
+  std::vector<std::pair<uint32_t, size_t>> chunks; // (item, offset)
+  for (size_t i = 0; i < n; ++i) {
+    for (size_t o = 0; o < it[i].bytes; o += kChunk) {
+      chunks.emplace_back((uint32_t)i, o);
+    }
+  }
+  openr::parallelFor(chunks.size(), openr::hostThreads(chunks.size(), 2),
+                     [&](size_t c, unsigned) {
+    const CopyItem& x = it[chunks[c].first];
+    const size_t o = chunks[c].second;
+    std::memcpy(static_cast<char*>(x.dst) + o, static_cast<const char*>(x.src) + o,
+                std::min(kChunk, x.bytes - o));
+  }, 1);
 }
 
 // Host -> device upload through the graph's pinned staging buffer: the bytes
@@ -7629,6 +7755,45 @@ int g_stage(spf_graph* g, void* dst, const void* src, size_t bytes) {
   par_copy(g->pin + g->pin_off, src, bytes);
   HIP_TRY(hipMemcpyAsync(dst, g->pin + g->pin_off, bytes, hipMemcpyHostToDevice, g->stream));
   g->pin_off += need;
+  return SPF_OK;
+}
+
+// g_stage of several arrays with one parallel staging copy (they must fit
+// the pinned buffer together, else one by one)
+int g_stage_many(spf_graph* g, std::initializer_list<CopyItem> items) {
+  size_t need = 0;
+  for (const CopyItem& x : items) {
+    need += (x.bytes + 255) & ~(size_t)255;
+  }
+  if (g->pin_off + need > g->pin_cap) {
+    HIP_TRY(hipStreamSynchronize(g->stream)); // queued copies read the buffer
+    g->pin_off = 0;
+  }
+  if (need > g->pin_cap) {
+    for (const CopyItem& x : items) {
+      if (const int s = g_stage(g, x.dst, x.src, x.bytes)) {
+        return s;
+      }
+    }
+    return SPF_OK;
+  }
+  std::vector<CopyItem> host;
+  std::vector<size_t> off;
+  for (const CopyItem& x : items) {
+    if (x.bytes) {
+      off.push_back(g->pin_off);
+      host.push_back({g->pin + g->pin_off, x.src, x.bytes});
+      g->pin_off += (x.bytes + 255) & ~(size_t)255;
+    }
+  }
+  par_copy_many(host.data(), host.size());
+  size_t i = 0;
+  for (const CopyItem& x : items) {
+    if (x.bytes) {
+      HIP_TRY(hipMemcpyAsync(x.dst, g->pin + off[i++], x.bytes, hipMemcpyHostToDevice,
+                             g->stream));
+    }
+  }
   return SPF_OK;
 }
 
@@ -7695,10 +7860,10 @@ int validate_graph_desc(const spf_graph_desc* desc) {
     // half-edge consistency, node blocks on the host pool; the lowest bad
     // edge is reported (same message as a sequential scan)
     std::atomic<uint32_t> bad{kInf32};
-    const uint32_t nblk = (V + kHostBlock - 1) / kHostBlock;
-    openr::parallelFor(nblk, openr::hostThreads(E, kHostMinEdges), [&](size_t b, unsigned) {
-      const uint32_t u1 = std::min<uint32_t>(V, (uint32_t)(b + 1) * kHostBlock);
-      for (uint32_t u = (uint32_t)b * kHostBlock; u < u1; ++u) {
+    const unsigned nth = openr::hostThreads(E, kHostMinEdges);
+    const std::vector<uint32_t> blk = host_node_blocks(desc->row_ptr, V, nth);
+    openr::parallelFor(blk.size() - 1, nth, [&](size_t b, unsigned) {
+      for (uint32_t u = blk[b]; u < blk[b + 1]; ++u) {
         for (uint32_t e = desc->row_ptr[u]; e < desc->row_ptr[u + 1]; ++e) {
           const uint32_t v = desc->col[e], r = desc->rev[e];
           if (v >= V || v == u || r >= E || desc->rev[r] != e ||
@@ -7825,17 +7990,16 @@ void build_nbr_lists(spf_graph* g, const NbrReuse* old = nullptr) {
   std::vector<uint32_t>& cnt = g->scratch_v;
   scratch.resize(E);
   cnt.resize(V);
-  const uint32_t nblk = (V + kHostBlock - 1) / kHostBlock;
   const unsigned nth = openr::hostThreads(E, kHostMinEdges);
+  const std::vector<uint32_t> blk = host_node_blocks(g->row.data(), V, nth);
   // per worker: neighbour -> slot of the row being processed (written before
   // it is read, never cleared)
   if (g->scratch_slot.size() < (size_t)nth * V) {
     g->scratch_slot.resize((size_t)nth * V);
   }
-  openr::parallelFor(nblk, nth, [&](size_t b, unsigned w) {
+  openr::parallelFor(blk.size() - 1, nth, [&](size_t b, unsigned w) {
     uint32_t* idx = g->scratch_slot.data() + (size_t)w * V;
-    const uint32_t u1 = std::min<uint32_t>(V, (uint32_t)(b + 1) * kHostBlock);
-    for (uint32_t u = (uint32_t)b * kHostBlock; u < u1; ++u) {
+    for (uint32_t u = blk[b]; u < blk[b + 1]; ++u) {
       const uint32_t e0 = g->row[u], e1 = g->row[u + 1];
       uint32_t* lo = scratch.data() + e0;
       if (old && !patched) {
@@ -7887,9 +8051,8 @@ void build_nbr_lists(spf_graph* g, const NbrReuse* old = nullptr) {
     g->nbr_off[u + 1] = g->nbr_off[u] + cnt[u];
   }
   g->nbrs.resize(g->nbr_off[V]);
-  openr::parallelFor(nblk, nth, [&](size_t b, unsigned) {
-    const uint32_t u1 = std::min<uint32_t>(V, (uint32_t)(b + 1) * kHostBlock);
-    for (uint32_t u = (uint32_t)b * kHostBlock; u < u1; ++u) {
+  openr::parallelFor(blk.size() - 1, nth, [&](size_t b, unsigned) {
+    for (uint32_t u = blk[b]; u < blk[b + 1]; ++u) {
       std::copy_n(scratch.data() + g->row[u], cnt[u], g->nbrs.data() + g->nbr_off[u]);
     }
   }, 1);
@@ -7972,38 +8135,49 @@ void refresh_exact(spf_graph* g) {
 int upload_weights(spf_graph* g) {
   const uint32_t E = g->E, V = g->V;
   const unsigned nth = openr::hostThreads(E, kHostMinEdges);
-  const uint32_t nblk = (V + kHostBlock - 1) / kHostBlock;
-  auto blocks = [&](auto&& fn) {
-    openr::parallelFor(nblk, nth, [&](size_t b, unsigned w) {
-      const uint32_t u1 = std::min<uint32_t>(V, (uint32_t)(b + 1) * kHostBlock);
-      for (uint32_t u = (uint32_t)b * kHostBlock; u < u1; ++u) {
-        fn(u, w);
-      }
-    }, 1);
-  };
+  const std::vector<uint32_t> blk = host_node_blocks(g->row.data(), V, nth);
   std::vector<uint64_t> wmax(nth, 0), wsum(nth, 0);
   std::vector<uint8_t> wwrap(nth, 0), wsame(nth, 1);
   std::vector<std::vector<uint32_t>> zeros(nth);
   const uint64_t w0 = E ? g->w64[0] : 0;
-  // per-block locals, folded into the per-worker slots once per block (the
-  // slots of all workers share cache lines: updating them per edge made this
-  // scan ~6 ms of false sharing on the fabric, profiles/r05s)
-  openr::parallelFor(nblk, nth, [&](size_t b, unsigned w) {
-    const uint32_t u0 = (uint32_t)b * kHostBlock, u1 = std::min<uint32_t>(V, u0 + kHostBlock);
+  // the packed out-edge words use ceil(log2 V) bits for the head
+  uint32_t bits = 1;
+  while (bits < 32 && (1ull << bits) < V) {
+    ++bits;
+  }
+  g->nbr_w.resize(g->nbrs.size());
+  const bool patched = !g->edge_up.empty();
+  // ONE pass over node blocks (a parallel section costs ~40-100 us of worker
+  // wake-ups): the metric scan (max, sum, wrap, uniformity, metric-0 edges)
+  // and the cheapest usable link to each distinct neighbour (parallel links;
+  // its host mirror serves the sparse metric patches).  The per-edge arrays
+  // (wout, win, packed edges, link halves) are derived on the device
+  // (spf_graph_derive_kernel).  Per-block locals, folded into the per-worker
+  // slots once per block (slots of all workers share cache lines: per-edge
+  // updates were ~6 ms of false sharing, profiles/r05s).
+  openr::parallelFor(blk.size() - 1, nth, [&](size_t b, unsigned w) {
     uint64_t mx = 0, sm = 0;
     bool wrap = false, same = true;
-    for (uint32_t e = g->row[u0]; e < g->row[u1]; ++e) {
-      const uint64_t m = g->w64[e];
-      if (m > 0x7FFFFFFFull) {
-        wrap = true;
-      } else {
-        sm += m;
+    for (uint32_t u = blk[b]; u < blk[b + 1]; ++u) {
+      uint32_t* nw = g->nbr_w.data() + g->nbr_off[u];
+      std::fill(nw, g->nbr_w.data() + g->nbr_off[u + 1], 0xFFFFFFFFu);
+      for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
+        const uint64_t m = g->w64[e];
+        if (m > 0x7FFFFFFFull) {
+          wrap = true;
+        } else {
+          sm += m;
+        }
+        if (m == 0) {
+          zeros[w].push_back(e);
+        }
+        mx = std::max(mx, m);
+        same = same && m == w0;
+        if (!patched || g->edge_up[e]) { // a down half-edge is no usable link
+          uint32_t& x = nw[g->slot[e]];
+          x = std::min(x, (uint32_t)std::min<uint64_t>(m, 0xFFFFFFFFull));
+        }
       }
-      if (m == 0) {
-        zeros[w].push_back(e);
-      }
-      mx = std::max(mx, m);
-      same = same && m == w0;
     }
     wmax[w] = std::max(wmax[w], mx);
     wsum[w] += sm;
@@ -8019,7 +8193,7 @@ int upload_weights(spf_graph* g) {
     wrap = wrap || wwrap[w];
     zero_e.insert(zero_e.end(), zeros[w].begin(), zeros[w].end());
   }
-  if (tl_phase) (*tl_phase)("w:scan");
+  if (tl_phase) (*tl_phase)("w:pass");
   std::sort(zero_e.begin(), zero_e.end());
   g->wrap = wrap;
   g->n_zero = (uint32_t)zero_e.size();
@@ -8046,27 +8220,27 @@ int upload_weights(spf_graph* g) {
     }
     g->uniform = same ? (uint32_t)w0 : 0;
   }
-  if (tl_phase) (*tl_phase)("w:exact+zero");
-  // host staging kept on the graph (in-place rebuilds: no page faults)
-  std::vector<uint32_t>& wout = g->h_wout;
-  std::vector<uint32_t>& win = g->h_win;
-  wout.resize(E);
-  win.resize(E);
-  // one pass per row: fast-path out / in metrics and the cheapest usable
-  // link to each distinct neighbour (parallel links)
-  g->nbr_w.resize(g->nbrs.size());
-  blocks([&](uint32_t u, unsigned) {
-    uint32_t* nw = g->nbr_w.data() + g->nbr_off[u];
-    std::fill(nw, g->nbr_w.data() + g->nbr_off[u + 1], 0xFFFFFFFFu);
-    for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
-      const uint32_t wo = (uint32_t)std::min<uint64_t>(g->w64[e], 0xFFFFFFFFull);
-      wout[e] = wo;
-      win[e] = (uint32_t)std::min<uint64_t>(g->w64[g->rev[e]], 0xFFFFFFFFull);
-      uint32_t& w = nw[g->slot[e]];
-      w = std::min(w, wo);
+  g->ecc_est = 0;
+  // packed out-edges for the push-only delta-stepping pass
+  const bool pack = E && bits < 32 && maxw < (1ull << (32 - bits));
+  if (g->d_cw && !pack) {
+    (void)hipFree(g->d_cw);
+    g->d_cw = nullptr;
+  }
+  g->cw_bits = 0;
+  // packed words padded to whole 16-byte chunks (the vector reads of the last one)
+  const size_t e4 = ((size_t)E + 3) & ~(size_t)3;
+  if (pack) {
+    if (!g->d_cw || e4 > g->cap_cw) {
+      if (g->d_cw) {
+        (void)hipFree(g->d_cw);
+      }
+      const size_t c = (e4 + e4 / 8 + 3) & ~(size_t)3;
+      HIP_TRY(hipMalloc((void**)&g->d_cw, c * 4));
+      g->cap_cw = c;
     }
-  });
-  if (tl_phase) (*tl_phase)("w:nbr_w");
+    g->cw_bits = bits;
+  }
   if (E) {
     if (!g->d_wout || E > g->cap_w) {
       for (void* p : {(void*)g->d_wout, (void*)g->d_win, (void*)g->d_w64}) {
@@ -8084,50 +8258,30 @@ int upload_weights(spf_graph* g) {
       // d_nbrs / d_nbr_w share nbr_cap (the caller sizes d_nbrs first)
       return fail(SPF_E_INVALID, "neighbour-weight buffer smaller than the neighbour lists");
     }
-    int st = SPF_OK;
-    if ((st = g_stage(g, g->d_wout, wout.data(), (size_t)E * 4)) ||
-        (st = g_stage(g, g->d_win, win.data(), (size_t)E * 4)) ||
-        (st = g_stage(g, g->d_w64, g->w64.data(), (size_t)E * 8)) ||
-        (st = g_stage(g, g->d_nbr_w, g->nbr_w.data(), g->nbr_w.size() * 4))) {
+    if (const int st = g_stage_many(g, {{g->d_w64, g->w64.data(), (size_t)E * 8},
+                                        {g->d_nbr_w, g->nbr_w.data(), g->nbr_w.size() * 4}})) {
       return st;
     }
+  }
+  // link halves: [2L], the derive kernel scatters them over a ~0 fill
+  if (!g->d_link_half || 2 * (size_t)g->L > g->cap_half) {
+    if (g->d_link_half) {
+      (void)hipFree(g->d_link_half);
+      g->d_link_half = nullptr;
+    }
+    const size_t c = std::max<size_t>(1, 2 * (size_t)g->L + g->L / 4);
+    HIP_TRY(hipMalloc((void**)&g->d_link_half, c * 4));
+    g->cap_half = c;
+  }
+  HIP_TRY(hipMemsetAsync(g->d_link_half, 0xFF, 2 * (size_t)g->L * 4, g->stream));
+  if (E) {
+    DeriveArgs da{g->d_col, g->d_rev, g->d_link, g->d_w64, g->d_wout, g->d_win,
+                  pack ? g->d_cw : nullptr, g->d_link_half, E, (uint32_t)e4, g->cw_bits};
+    SPF_LAUNCH(spf_graph_derive_kernel, dim3((uint32_t)((e4 + 255) / 256)), dim3(256), 0,
+               g->stream, da);
+    HIP_TRY(hipGetLastError());
   }
   if (tl_phase) (*tl_phase)("w:stage");
-  g->ecc_est = 0;
-  // packed out-edges for the push-only delta-stepping pass
-  uint32_t bits = 1;
-  while (bits < 32 && (1ull << bits) < V) {
-    ++bits;
-  }
-  const bool pack = E && bits < 32 && maxw < (1ull << (32 - bits));
-  if (g->d_cw && !pack) {
-    (void)hipFree(g->d_cw);
-    g->d_cw = nullptr;
-  }
-  g->cw_bits = 0;
-  if (pack) {
-    std::vector<uint32_t>& cw = g->h_cw;
-    cw.resize(E);
-    blocks([&](uint32_t u, unsigned) {
-      for (uint32_t e = g->row[u]; e < g->row[u + 1]; ++e) {
-        cw[e] = g->col[e] | (wout[e] << bits);
-      }
-    });
-    // padded to whole 16-byte chunks (the vector reads of the last one)
-    cw.resize(((size_t)E + 3) & ~(size_t)3, 0u);
-    if (!g->d_cw || cw.size() > g->cap_cw) {
-      if (g->d_cw) {
-        (void)hipFree(g->d_cw);
-      }
-      const size_t c = (cw.size() + cw.size() / 8 + 3) & ~(size_t)3;
-      HIP_TRY(hipMalloc((void**)&g->d_cw, c * 4));
-      g->cap_cw = c;
-    }
-    if (const int st = g_stage(g, g->d_cw, cw.data(), cw.size() * 4)) {
-      return st;
-    }
-    g->cw_bits = bits;
-  }
   return SPF_OK;
 }
 
@@ -8138,9 +8292,23 @@ int upload_weights(spf_graph* g) {
 // the node's own id (harmless in the pull, see MsBfsArgs).  Name ranks keep
 // nodes of one role (SSW / FSW / RSW) adjacent, so the padding is small
 // (fabric: 232,512 edges -> 233,472 slots).
+// The sliced-ELL copy for spf_msbfs_kernel (V <= 16 Ki): slice c = nodes
+// [64c, 64c + 64) (one wave's node slot), width = the slice's largest degree
+// rounded up to 4; lane L's edge j sits in word j % 4 of the uint4 at group
+// sell_off[c] + j / 4, so one wave load covers 1 KB.  Rows are padded with
+// the node's own id (harmless in the pull, see MsBfsArgs).  Name ranks keep
+// nodes of one role (SSW / FSW / RSW) adjacent, so the padding is small
+// (fabric: 232,512 edges -> 233,472 slots).  The widths are a host scan;
+// the words are written on the device (spf_sell_kernel) from the uploaded
+// CSR.
 int upload_sell(spf_graph* g) {
-  const uint32_t V = g->V, ns = (V + 63) / 64;
-  std::vector<uint32_t> off(ns + 1, 0);
+  const uint32_t V = g->V;
+  if (!V || V > kMsThreads * kMsMaxK) {
+    return SPF_OK;
+  }
+  const uint32_t ns = (V + 63) / 64;
+  std::vector<uint32_t>& off = g->sell_off;
+  off.assign(ns + 1, 0);
   for (uint32_t c = 0; c < ns; ++c) {
     uint32_t w = 0;
     for (uint32_t v = 64 * c; v < std::min(V, 64 * c + 64); ++v) {
@@ -8148,22 +8316,7 @@ int upload_sell(spf_graph* g) {
     }
     off[c + 1] = off[c] + (w + 3) / 4;
   }
-  // kept on the graph (in-place rebuilds: no page faults); slices on the
-  // host pool (each writes its own groups)
-  std::vector<uint32_t>& sell = g->h_sell;
-  sell.resize((size_t)off[ns] * 256);
-  openr::parallelFor(ns, openr::hostThreads(g->E, kHostMinEdges), [&](size_t c, unsigned) {
-    const uint32_t groups = off[c + 1] - off[c];
-    for (uint32_t L = 0; L < 64; ++L) {
-      const uint32_t v = 64 * (uint32_t)c + L;
-      const uint32_t deg = v < V ? g->row[v + 1] - g->row[v] : 0;
-      for (uint32_t j = 0; j < groups * 4; ++j) {
-        const uint32_t x = j < deg ? g->col[g->row[v] + j] : (v < V ? v : 0);
-        sell[((size_t)(off[c] + j / 4) * 64 + L) * 4 + (j & 3)] = x;
-      }
-    }
-  }, 8);
-  g->sell_off = off;
+  const size_t words = (size_t)off[ns] * 256;
   // device buffers kept across in-place rebuilds while they fit
   auto fit = [&](uint32_t** d, size_t n, size_t& cap) -> int {
     if (*d && n <= cap) {
@@ -8181,13 +8334,17 @@ int upload_sell(spf_graph* g) {
   };
   int s = fit(&g->d_sell_off, off.size(), g->cap_sell_off);
   if (s == SPF_OK) {
+    s = fit((uint32_t**)&g->d_sell, words, g->cap_sell);
+  }
+  if (s == SPF_OK) {
     s = g_stage(g, g->d_sell_off, off.data(), off.size() * 4);
   }
-  if (s == SPF_OK && !sell.empty()) {
-    s = fit((uint32_t**)&g->d_sell, sell.size(), g->cap_sell);
-    if (s == SPF_OK) {
-      s = g_stage(g, g->d_sell, sell.data(), sell.size() * 4);
-    }
+  if (s == SPF_OK && words) {
+    SellArgs sa{g->d_row, g->d_col, g->d_sell_off, reinterpret_cast<uint32_t*>(g->d_sell), V, ns,
+                (uint32_t)words};
+    SPF_LAUNCH(spf_sell_kernel, dim3((uint32_t)((words + 255) / 256)), dim3(256), 0, g->stream,
+               sa);
+    HIP_TRY(hipGetLastError());
   }
   return s;
 }
@@ -8692,18 +8849,7 @@ int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
     return bail(s);
   }
   mark("weights");
-  {
-    std::vector<uint32_t> half(2 * (size_t)g->L, kInf32);
-    for (uint32_t e = 0; e < E; ++e) {
-      half[2 * (size_t)g->link[e] + (e < g->rev[e] ? 0 : 1)] = e;
-    }
-    if ((s = dev_upload_g(g, &g->d_link_half, half.data(), half.size()))) {
-      return bail(s);
-    }
-    g->cap_half = half.size();
-  }
-  mark("link halves");
-  if (V && V <= kMsThreads * kMsMaxK && (s = upload_sell(g))) {
+  if ((s = upload_sell(g))) {
     return bail(s);
   }
   if ((s = g_stage_flush(g))) {
@@ -8755,11 +8901,19 @@ int spf_graph_update(spf_graph* g, const spf_graph_desc* desc) {
   std::swap(g->slot, g->old_slot);
   g->E = E;
   g->L = desc->num_links;
-  par_assign(g->row, desc->row_ptr, (size_t)V + 1);
-  par_assign(g->col, desc->col, E);
-  par_assign(g->link, desc->link_id, E);
-  par_assign(g->rev, desc->rev, E);
-  par_assign(g->w64, desc->metric, E);
+  g->row.resize((size_t)V + 1);
+  g->col.resize(E);
+  g->link.resize(E);
+  g->rev.resize(E);
+  g->w64.resize(E);
+  {
+    const CopyItem cp[] = {{g->row.data(), desc->row_ptr, ((size_t)V + 1) * 4},
+                           {g->col.data(), desc->col, (size_t)E * 4},
+                           {g->link.data(), desc->link_id, (size_t)E * 4},
+                           {g->rev.data(), desc->rev, (size_t)E * 4},
+                           {g->w64.data(), desc->metric, (size_t)E * 8}};
+    par_copy_many(cp, 5);
+  }
   std::fill(g->trbits.begin(), g->trbits.end(), 0u);
   for (uint32_t v = 0; v < V; ++v) {
     if (!desc->node_overloaded[v]) {
@@ -8775,17 +8929,17 @@ int spf_graph_update(spf_graph* g, const spf_graph_desc* desc) {
   build_nbr_lists(g, reuse && g->old_row.size() == (size_t)V + 1 ? &nr : nullptr);
   mark("nbr lists");
   // edge-sized arrays: rewritten in place, or reallocated with headroom
-  auto store32 = [&](uint32_t** d, const std::vector<uint32_t>& h, size_t& cap) -> int {
-    if (!*d || h.size() > cap) {
+  auto fit32 = [&](uint32_t** d, size_t n, size_t& cap) -> int {
+    if (!*d || n > cap) {
       if (*d) {
         (void)hipFree(*d);
         *d = nullptr;
       }
-      const size_t c = std::max<size_t>(1, h.size() + h.size() / 8);
+      const size_t c = std::max<size_t>(1, n + n / 8);
       HIP_TRY(hipMalloc((void**)d, c * 4));
       cap = c;
     }
-    return g_stage(g, *d, h.data(), h.size() * 4);
+    return SPF_OK;
   };
   int s = SPF_OK;
   size_t cap_e = g->cap_e, cap_nbr = g->nbr_cap, cap_v = (size_t)V + 1;
@@ -8799,15 +8953,13 @@ int spf_graph_update(spf_graph* g, const spf_graph_desc* desc) {
     }
   }
   size_t c1 = cap_e, c2 = cap_e, c3 = cap_e, c4 = cap_e;
-  if ((s = store32(&g->d_col, g->col, c1)) || (s = store32(&g->d_link, g->link, c2)) ||
-      (s = store32(&g->d_rev, g->rev, c3)) || (s = store32(&g->d_slot, g->slot, c4)) ||
-      (s = store32(&g->d_row, g->row, cap_v)) || (s = store32(&g->d_nbr_off, g->nbr_off, cap_v))) {
+  if ((s = fit32(&g->d_col, E, c1)) || (s = fit32(&g->d_link, E, c2)) ||
+      (s = fit32(&g->d_rev, E, c3)) || (s = fit32(&g->d_slot, E, c4)) ||
+      (s = fit32(&g->d_row, (size_t)V + 1, cap_v)) ||
+      (s = fit32(&g->d_nbr_off, (size_t)V + 1, cap_v))) {
     return s;
   }
   g->cap_e = std::max(c1, (size_t)E);
-  if ((s = g_stage(g, g->d_tr, g->trbits.data(), g->trbits.size() * 4))) {
-    return s;
-  }
   if (g->nbrs.size() > cap_nbr || !g->d_nbrs) {
     for (uint32_t** d : {&g->d_nbrs, &g->d_nbr_w}) {
       if (*d) {
@@ -8820,7 +8972,14 @@ int spf_graph_update(spf_graph* g, const spf_graph_desc* desc) {
     HIP_TRY(hipMalloc((void**)&g->d_nbr_w, c * 4));
     g->nbr_cap = c;
   }
-  if ((s = g_stage(g, g->d_nbrs, g->nbrs.data(), g->nbrs.size() * 4))) {
+  if ((s = g_stage_many(g, {{g->d_col, g->col.data(), (size_t)E * 4},
+                            {g->d_link, g->link.data(), (size_t)E * 4},
+                            {g->d_rev, g->rev.data(), (size_t)E * 4},
+                            {g->d_slot, g->slot.data(), (size_t)E * 4},
+                            {g->d_row, g->row.data(), ((size_t)V + 1) * 4},
+                            {g->d_nbr_off, g->nbr_off.data(), ((size_t)V + 1) * 4},
+                            {g->d_tr, g->trbits.data(), g->trbits.size() * 4},
+                            {g->d_nbrs, g->nbrs.data(), g->nbrs.size() * 4}}))) {
     return s;
   }
   mark("csr upload");
@@ -8828,24 +8987,7 @@ int spf_graph_update(spf_graph* g, const spf_graph_desc* desc) {
     return s;
   }
   mark("weights");
-  {
-    // one writer per slot (a link's two halves), edge blocks on the pool
-    std::vector<uint32_t>& half = g->h_half;
-    half.assign(2 * (size_t)g->L, kInf32);
-    constexpr uint32_t kBlk = 1u << 14;
-    openr::parallelFor((E + kBlk - 1) / kBlk, openr::hostThreads(E, kHostMinEdges),
-                       [&](size_t b, unsigned) {
-      const uint32_t e1 = std::min<uint32_t>(E, (uint32_t)(b + 1) * kBlk);
-      for (uint32_t e = (uint32_t)b * kBlk; e < e1; ++e) {
-        half[2 * (size_t)g->link[e] + (e < g->rev[e] ? 0 : 1)] = e;
-      }
-    }, 1);
-    if ((s = store32(&g->d_link_half, half, g->cap_half))) {
-      return s;
-    }
-  }
-  mark("link halves");
-  if (V && V <= kMsThreads * kMsMaxK && (s = upload_sell(g))) {
+  if ((s = upload_sell(g))) {
     return s;
   }
   if ((s = g_stage_flush(g))) {
@@ -11585,10 +11727,11 @@ int spf_graph_diff(
   }
   // node blocks in parallel, each into its own list; the lists are then
   // concatenated in node order (the serial scan's output order)
-  const uint32_t nblk = (V + kHostBlock - 1) / kHostBlock;
-  std::vector<std::vector<spf_edge_delta>> found(nblk);
   const unsigned nth =
       openr::hostThreads((size_t)before->num_edges + after->num_edges, kHostMinEdges);
+  const std::vector<uint32_t> bnd = host_node_blocks(after->row_ptr, V, nth);
+  const uint32_t nblk = (uint32_t)bnd.size() - 1;
+  std::vector<std::vector<spf_edge_delta>> found(nblk);
   openr::parallelFor(nblk, nth, [&](size_t blk, unsigned) {
   std::vector<spf_edge_delta>& lst = found[blk];
   auto emit = [&](uint32_t u, uint32_t v, uint64_t w, uint32_t kind, uint32_t scope) {
@@ -11596,8 +11739,7 @@ int spf_graph_diff(
   };
   using HE = std::pair<uint32_t, uint64_t>; // (head, metric)
   std::vector<HE> a, b;
-  const uint32_t u1 = std::min<uint32_t>(V, (uint32_t)(blk + 1) * kHostBlock);
-  for (uint32_t u = (uint32_t)blk * kHostBlock; u < u1; ++u) {
+  for (uint32_t u = bnd[blk]; u < bnd[blk + 1]; ++u) {
     const bool trA = !before->node_overloaded[u], trB = !after->node_overloaded[u];
     const uint32_t ra = before->row_ptr[u], na = before->row_ptr[u + 1] - ra;
     const uint32_t rb = after->row_ptr[u], nb = after->row_ptr[u + 1] - rb;

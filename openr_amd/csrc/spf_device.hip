@@ -5343,8 +5343,10 @@ struct WhatifArgs {
   uint32_t want_nh;
   uint32_t unit; // SPF_F_UNIT_METRIC: every hop costs 1
   // repair batches: a tight ignored link of the source itself is flagged
-  // skip = 2 (spf_sssp_kernel claims those first)
+  // skip = 2 (spf_sssp_kernel claims those first), or 3 when the query is
+  // one of spf_whatif_heavy_kernel's (wh_mark[q] != 0: it runs them)
   uint32_t mark_heavy;
+  const uint8_t* wh_mark = nullptr;
 };
 
 __global__ __launch_bounds__(256) void spf_whatif_screen_kernel(WhatifArgs a) {
@@ -5371,7 +5373,8 @@ __global__ __launch_bounds__(256) void spf_whatif_screen_kernel(WhatifArgs a) {
   tight = __syncthreads_or(tight);
   heavy = __syncthreads_or(heavy);
   if (threadIdx.x == 0) {
-    a.skip[q] = tight ? (heavy && a.mark_heavy ? 2u : 0u) : 1u;
+    a.skip[q] = tight ? (heavy && a.mark_heavy ? (a.wh_mark && a.wh_mark[q] ? 3u : 2u) : 0u)
+                      : 1u;
   }
   if (tight) {
     return;
@@ -5380,6 +5383,229 @@ __global__ __launch_bounds__(256) void spf_whatif_screen_kernel(WhatifArgs a) {
   if (a.want_nh) {
     block_copy<uint64_t, 256>(a.nh_out + a.nh_off[q], a.base_nh + a.base_nh_off[b],
                               (size_t)a.V * a.nh_w[q]);
+  }
+}
+
+// What-if queries whose failed link leaves the source (the screen's skip ==
+// 2) on a uniform-metric area: their repair set K is most of the graph, so
+// spf_sssp_kernel ran them from scratch on one 512-thread workgroup each, and
+// the fabric batch waited ~1.7 ms for the two of them (profiles/r05ah,
+// r05al).  Here one 1,024-thread workgroup per such query runs a
+// level-synchronous BFS (transit rule, ignored links skipped; the queue is in
+// BFS order, so levels are its segments), then the next-hop masks level by
+// level over the tight in-edges: nh(v) = OR over u -> v with lvl(u) + 1 =
+// lvl(v), u the source or transit, link not ignored, of (u == s ? the bit of
+// v's slot in s's neighbour list : nh(u)).  Distances = level x the uniform
+// metric.  The screen marks these queries skip = 3, which spf_sssp_kernel
+// never claims, and this kernel runs on its own stream beside it.
+struct WhatifHeavyArgs {
+  const uint32_t* row;
+  const uint32_t* col;
+  const uint32_t* link;
+  const uint32_t* rev;
+  const uint32_t* slot;
+  const uint32_t* trbits;
+  const uint32_t* src;
+  const uint32_t* ign_off;
+  const uint32_t* ign;
+  const uint32_t* cand; // candidate queries (an ignored link at their source)
+  uint32_t* skip;
+  uint32_t* dist_out;
+  uint64_t* nh_out;
+  const uint64_t* nh_off;
+  const uint32_t* nh_w;
+  uint32_t V, Vp, scale;
+  uint32_t want_nh; // distance-only batches have no mask rows
+  uint32_t* lstart; // [ncand][V + 1] level segments of each candidate's queue
+  // OPENR_SPF_WHATIF_STATS=1: per candidate {init, BFS, rows, masks ticks
+  // (100 MHz), levels, reached}; nullptr = off
+  unsigned long long* stats = nullptr;
+};
+constexpr uint32_t kWhThreads = 1024;
+constexpr uint32_t kWhIgn = 512; // ignore-list hash slots in LDS
+constexpr uint32_t kWhMaxW = 4; // mask words per node handled here
+
+__global__ __launch_bounds__(kWhThreads) void spf_whatif_heavy_kernel(WhatifHeavyArgs a) {
+  extern __shared__ __align__(16) uint32_t wh_smem[];
+  uint32_t* lvl = wh_smem;         // [V] BFS level, kInf32 = unreached
+  uint32_t* queue = lvl + a.V;     // [V] nodes in BFS order
+  uint32_t* rowl = queue + a.V;    // [V + 1] the CSR row offsets
+  uint32_t* trl = rowl + a.V + 1;  // [V / 32] transit bits
+  // level segments of the queue (global: up to V + 1 of them)
+  uint32_t* lstart = a.lstart + (size_t)blockIdx.x * (a.V + 1);
+  __shared__ uint32_t ign_s[kWhIgn];
+  __shared__ uint32_t sh_qb, sh_qe;
+  __shared__ uint32_t sh_tail;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t q = a.cand[blockIdx.x];
+  if (a.skip[q] != 3u) {
+    return; // screened (rows copied) or repairable: not this kernel's
+  }
+  unsigned long long tk[5] = {a.stats ? wall_clock64() : 0ull, 0, 0, 0, 0};
+  const uint32_t s = a.src[q], V = a.V;
+  const uint32_t ilo = a.ign_off[q], nign = a.ign_off[q + 1] - ilo;
+  IgnSet ig;
+  ig.p = a.ign + ilo;
+  ig.n = nign;
+  const uint32_t slots = ign_hash_slots(nign);
+  if (slots && slots <= kWhIgn) {
+    for (uint32_t i = tid; i < slots; i += kWhThreads) {
+      ign_s[i] = kInf32;
+    }
+    __syncthreads();
+    const uint32_t hb = __builtin_ctz(slots);
+    for (uint32_t i = tid; i < nign; i += kWhThreads) {
+      const uint32_t l = a.ign[ilo + i];
+      uint32_t h = (l * 0x9E3779B1u) >> (32 - hb);
+      for (;;) {
+        const uint32_t prev = atomicCAS(&ign_s[h], kInf32, l);
+        if (prev == kInf32 || prev == l) {
+          break;
+        }
+        h = (h + 1) & (slots - 1);
+      }
+    }
+    ig.p = ign_s;
+    ig.hbits = hb;
+  } else if (nign <= kWhIgn) {
+    // a short list stays sorted, in LDS (probing it in global memory cost a
+    // dependent round trip per edge: ~3 us per frontier node, r05an)
+    for (uint32_t i = tid; i < nign; i += kWhThreads) {
+      ign_s[i] = a.ign[ilo + i];
+    }
+    __syncthreads();
+    ig.p = ign_s;
+  }
+  for (uint32_t v = tid; v < V; v += kWhThreads) {
+    lvl[v] = v == s ? 0u : kInf32;
+    rowl[v] = a.row[v];
+  }
+  for (uint32_t i = tid; i < (V + 31) / 32; i += kWhThreads) {
+    trl[i] = a.trbits[i];
+  }
+  if (tid == 0) {
+    rowl[V] = a.row[V];
+    queue[0] = s;
+    sh_tail = 1;
+    lstart[0] = 0;
+    lstart[1] = 1;
+    sh_qb = 0;
+    sh_qe = 1;
+  }
+  __syncthreads();
+  if (a.stats) {
+    tk[1] = wall_clock64();
+  }
+  auto transit = [&](uint32_t u) { return u == s || ((trl[u >> 5] >> (u & 31)) & 1u); };
+  // BFS, level by level: frontier = queue[lstart[L], lstart[L + 1])
+  uint32_t L = 0;
+  for (;;) {
+    const uint32_t qb = sh_qb, qe = sh_qe;
+    if (qb == qe) {
+      break; // (at most V levels: lstart has V + 1 slots)
+    }
+    // 8 lanes per frontier node (128 nodes in flight), lanes over its out-edges
+    const uint32_t gl = tid & 7u, grp = tid >> 3;
+    for (uint32_t i = qb + grp; i < qe; i += kWhThreads / 8) {
+      const uint32_t u = queue[i];
+      if (!transit(u)) {
+        continue; // reached, not expanded (LinkState.cpp:829-836)
+      }
+      for (uint32_t e = rowl[u] + gl; e < rowl[u + 1]; e += 8) {
+        if (nign && ig.has(a.link[e])) {
+          continue;
+        }
+        const uint32_t v = a.col[e];
+        if (atomicCAS(&lvl[v], kInf32, L + 1) == kInf32) {
+          queue[atomicAdd(&sh_tail, 1u)] = v;
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      lstart[L + 2] = sh_tail;
+      sh_qb = qe;
+      sh_qe = sh_tail;
+    }
+    __syncthreads();
+    ++L;
+  }
+  __syncthreads();
+  if (a.stats) {
+    tk[2] = wall_clock64();
+  }
+  const uint32_t nlev = L; // levels 0 .. nlev - 1 hold nodes
+  uint32_t* dist = a.dist_out + (size_t)q * a.Vp;
+  const uint32_t W = a.want_nh ? a.nh_w[q] : 0u;
+  uint64_t* nh = a.want_nh ? a.nh_out + a.nh_off[q] : nullptr;
+  for (uint32_t v = tid; v < V; v += kWhThreads) {
+    const uint32_t l = lvl[v];
+    dist[v] = l == kInf32 ? kInf32 : l * a.scale;
+    if (l == kInf32 || v == s) {
+      for (uint32_t k = 0; k < W; ++k) {
+        nh[(size_t)v * W + k] = 0ull; // unreached (and the source): empty
+      }
+    }
+  }
+  __syncthreads();
+  if (a.stats) {
+    tk[3] = wall_clock64();
+  }
+  // next hops, level by level (level L reads level L - 1's masks: written
+  // by this workgroup before the barrier)
+  // 8 lanes per node, lanes over its in-edges, OR-reduced in the group
+  const uint32_t gl = tid & 7u, grp = tid >> 3;
+  for (uint32_t l = 1; W && l < nlev; ++l) {
+    const uint32_t i1 = lstart[l + 1];
+    for (uint32_t i0 = lstart[l]; i0 < i1; i0 += kWhThreads / 8) {
+      const uint32_t i = i0 + grp; // the loop is uniform: the shuffles below
+      const uint32_t v = i < i1 ? queue[i] : 0u;
+      uint64_t acc[kWhMaxW] = {0, 0, 0, 0};
+      if (i < i1) {
+        for (uint32_t e = rowl[v] + gl; e < rowl[v + 1]; e += 8) {
+          const uint32_t u = a.col[e]; // e = v -> u; its reverse u -> v is the in-edge
+          if (lvl[u] + 1 != l || !transit(u) || (nign && ig.has(a.link[e]))) {
+            continue;
+          }
+          if (u == s) {
+            const uint32_t b = a.slot[a.rev[e]]; // v's slot among s's neighbours
+            acc[b >> 6] |= 1ull << (b & 63);
+          } else {
+#pragma unroll
+            for (uint32_t k = 0; k < kWhMaxW; ++k) {
+              if (k < W) {
+                acc[k] |= nh[(size_t)u * W + k];
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < kWhMaxW; ++k) {
+#pragma unroll
+        for (int off = 4; off >= 1; off >>= 1) {
+          acc[k] |= (uint64_t)__shfl_xor((unsigned long long)acc[k], off, 8);
+        }
+      }
+      if (i < i1 && gl < W) {
+        uint64_t w = acc[0];
+#pragma unroll
+        for (uint32_t k = 1; k < kWhMaxW; ++k) {
+          w = gl == k ? acc[k] : w;
+        }
+        nh[(size_t)v * W + gl] = w;
+      }
+    }
+    __syncthreads();
+  }
+  if (a.stats && tid == 0) {
+    unsigned long long* o = a.stats + 6 * (size_t)blockIdx.x;
+    o[0] = tk[1] - tk[0];
+    o[1] = tk[2] - tk[1];
+    o[2] = tk[3] - tk[2];
+    o[3] = wall_clock64() - tk[3];
+    o[4] = nlev;
+    o[5] = sh_tail;
   }
 }
 
@@ -7232,6 +7458,15 @@ struct spf_query {
   // what-if batch behind the screen whose tight queries start from the
   // baseline rows (spf_sssp_kernel repair mode, OPENR_SPF_WHATIF_REPAIR)
   bool repair = false;
+  // what-if queries with an ignored link at their source, run by
+  // spf_whatif_heavy_kernel (uniform-metric areas; d_wh_cand: pool block)
+  std::vector<uint32_t> wh_cand;
+  uint32_t* d_wh_cand = nullptr;
+  uint8_t* d_wh_mark = nullptr;       // [nq] 1 = a candidate (the screen's skip = 3)
+  uint32_t* d_wh_lstart = nullptr;    // [ncand][V + 1] level segments
+  hipStream_t wh_stream = nullptr;    // the heavy kernel's stream (beside the SSSP)
+  hipEvent_t wh_ev0 = nullptr, wh_ev1 = nullptr;
+  bool wh_pending = false;            // the graph stream still has to join wh_ev1
   uint32_t dlds_shift = 4, dlds_grid = 0;
   size_t dlds_lds = 0;
   uint32_t* d_ovf = nullptr; // [0] overflow count, [1] claim counter, [2..] list
@@ -7929,7 +8164,7 @@ void free_query(spf_query* q) {
         (void*)q->d_trace, (void*)q->d_big, (void*)q->d_held_order, (void*)q->d_zl,
         (void*)q->d_zvar, (void*)q->d_ms_mask, (void*)q->d_ms_flag,
         (void*)q->d_ovf, q->narrow ? (void*)q->d_nhb : nullptr, (void*)q->d_tcs, q->d_v2,
-        q->d_coop}) {
+        q->d_coop, (void*)q->d_wh_cand, (void*)q->d_wh_mark, (void*)q->d_wh_lstart}) {
     pool_free(p);
   }
   if (q->base) {
@@ -7946,6 +8181,15 @@ void free_query(spf_query* q) {
   }
   if (q->evm) {
     ev_put(q->evm);
+  }
+  if (q->wh_ev0) {
+    ev_put(q->wh_ev0);
+  }
+  if (q->wh_ev1) {
+    ev_put(q->wh_ev1);
+  }
+  if (q->wh_stream) {
+    (void)hipStreamDestroy(q->wh_stream);
   }
   for (auto& h : q->hist) {
     for (hipEvent_t e : h) {
@@ -10001,6 +10245,53 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
         if (!q->d_qctr && pool_malloc((void**)&q->d_qctr, 4) != hipSuccess) {
           return bail(fail(SPF_E_NOMEM, "what-if claim counter"));
         }
+        // queries whose failed link leaves the source: their own BFS launch
+        // on a uniform-metric area (spf_whatif_heavy_kernel)
+        const bool uni = (desc->flags & SPF_F_UNIT_METRIC) || g->uniform;
+        const size_t wh_lds = (3 * (size_t)g->V + 1 + (g->V + 31) / 32) * 4;
+        if (uni && wh_lds <= kLdsLimit && desc->ignore_offsets &&
+            env_flag("OPENR_SPF_WHATIF_HEAVY", 1)) {
+          for (uint32_t i = 0; i < nq; ++i) {
+            const uint32_t s0 = desc->sources[i];
+            if (g->nbr_off[s0 + 1] - g->nbr_off[s0] > 64 * kWhMaxW) {
+              continue; // wider masks than the kernel keeps in registers
+            }
+            bool hit = false;
+            for (uint32_t j = desc->ignore_offsets[i]; j < desc->ignore_offsets[i + 1] && !hit; ++j) {
+              for (uint32_t e = g->row[s0]; e < g->row[s0 + 1]; ++e) {
+                if (g->link[e] == desc->ignore_links[j]) {
+                  hit = true;
+                  break;
+                }
+              }
+            }
+            if (hit) {
+              q->wh_cand.push_back(i);
+            }
+          }
+          if (!q->wh_cand.empty()) {
+            std::vector<uint8_t> mark(nq, 0);
+            for (uint32_t i : q->wh_cand) {
+              mark[i] = 1;
+            }
+            if ((s = dev_upload_q(&q->d_wh_cand, q->wh_cand.data(), q->wh_cand.size())) ||
+                (s = dev_upload_q(&q->d_wh_mark, mark.data(), mark.size()))) {
+              return bail(s);
+            }
+            if (pool_malloc((void**)&q->d_wh_lstart,
+                            q->wh_cand.size() * ((size_t)g->V + 1) * 4) != hipSuccess) {
+              return bail(fail(SPF_E_NOMEM, "what-if heavy level segments"));
+            }
+            // high priority: its two big-LDS workgroups must be placed before
+            // the SSSP's hundreds fill every CU (they waited ~0.6 ms, r05an)
+            int plo = 0, phi = 0;
+            (void)hipDeviceGetStreamPriorityRange(&plo, &phi);
+            if (hipStreamCreateWithPriority(&q->wh_stream, hipStreamNonBlocking, phi) != hipSuccess ||
+                ev_get(&q->wh_ev0) != hipSuccess || ev_get(&q->wh_ev1) != hipSuccess) {
+              return bail(fail(SPF_E_DEVICE, "what-if heavy stream"));
+            }
+          }
+        }
       }
     }
   }
@@ -10080,6 +10371,11 @@ int launch_sssp(spf_query* q) {
   SPF_LAUNCH_AS("spf_sssp_kernel", 
       kern, dim3(q->grid), dim3(kBlock), q->lds_bytes, g->stream, a);
   HIP_TRY(hipGetLastError());
+  if (q->wh_pending) {
+    // the heavy what-if queries ran beside it: later work waits for them
+    HIP_TRY(hipStreamWaitEvent(g->stream, q->wh_ev1, 0));
+    q->wh_pending = false;
+  }
   if (a.stats) {
     unsigned long long h[8];
     HIP_TRY(hipStreamSynchronize(g->stream));
@@ -10820,11 +11116,74 @@ int run_screen(spf_query* q) {
   a.want_nh = (q->flags & SPF_F_NEXTHOPS) ? 1u : 0u;
   a.unit = (q->flags & SPF_F_UNIT_METRIC) ? 1u : 0u;
   a.mark_heavy = q->repair ? 1u : 0u;
+  a.wh_mark = q->repair ? q->d_wh_mark : nullptr;
   if (b->Vp != q->Vp) {
     return fail(SPF_E_INVALID, "baseline row stride differs");
   }
   SPF_LAUNCH(spf_whatif_screen_kernel, dim3(q->nq), dim3(256), 0, g->stream, a);
   HIP_TRY(hipGetLastError());
+  if (q->repair && !q->wh_cand.empty()) {
+    WhatifHeavyArgs h{};
+    h.row = g->d_row;
+    h.col = g->d_col;
+    h.link = g->d_link;
+    h.rev = g->d_rev;
+    h.slot = g->d_slot;
+    h.trbits = g->d_tr;
+    h.src = q->d_src;
+    h.ign_off = q->d_ign_off;
+    h.ign = q->d_ign;
+    h.cand = q->d_wh_cand;
+    h.skip = q->d_skip;
+    h.dist_out = (uint32_t*)q->d_dist;
+    h.nh_out = q->d_nh;
+    h.nh_off = q->d_nh_off;
+    h.nh_w = q->d_nh_w;
+    h.V = g->V;
+    h.Vp = q->Vp;
+    h.scale = (q->flags & SPF_F_UNIT_METRIC) ? 1u : g->uniform;
+    h.want_nh = (q->flags & SPF_F_NEXTHOPS) ? 1u : 0u;
+    h.lstart = q->d_wh_lstart;
+    if (env_flag("OPENR_SPF_WHATIF_STATS", 0)) {
+      HIP_TRY(hipMalloc((void**)&h.stats, 6 * q->wh_cand.size() * 8));
+      HIP_TRY(hipMemset(h.stats, 0, 6 * q->wh_cand.size() * 8));
+    }
+    const size_t lds = (3 * (size_t)g->V + 1 + (g->V + 31) / 32) * 4;
+    HIP_TRY(hipFuncSetAttribute((const void*)spf_whatif_heavy_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    // on its own (high-priority) stream beside the SSSP of the rest, the
+    // graph stream joining it after that launch (launch_sssp): fabric batch
+    // 1.38 ms, against 1.54 ms in order on the graph stream
+    // (OPENR_SPF_WHATIF_HEAVY_STREAM=0; the kernel alone is 0.75 ms there,
+    // beside the SSSP its two 122 KB workgroups wait for free CUs)
+    const bool side = env_flag("OPENR_SPF_WHATIF_HEAVY_STREAM", 1);
+    hipStream_t hstream = side ? q->wh_stream : g->stream;
+    if (side) {
+      HIP_TRY(hipEventRecord(q->wh_ev0, g->stream));
+      HIP_TRY(hipStreamWaitEvent(q->wh_stream, q->wh_ev0, 0));
+    }
+    SPF_LAUNCH(spf_whatif_heavy_kernel, dim3((uint32_t)q->wh_cand.size()), dim3(kWhThreads), lds,
+               hstream, h);
+    HIP_TRY(hipGetLastError());
+    if (side) {
+      HIP_TRY(hipEventRecord(q->wh_ev1, q->wh_stream));
+      q->wh_pending = true;
+    }
+    if (h.stats) {
+      std::vector<unsigned long long> hs(6 * q->wh_cand.size());
+      HIP_TRY(hipStreamSynchronize(side ? q->wh_stream : g->stream));
+      HIP_TRY(hipMemcpy(hs.data(), h.stats, hs.size() * 8, hipMemcpyDeviceToHost));
+      HIP_TRY(hipFree(h.stats));
+      for (size_t i = 0; i < q->wh_cand.size(); ++i) {
+        const unsigned long long* o = hs.data() + 6 * i;
+        if (o[4]) {
+          fprintf(stderr, "[whatif heavy] query %u: init %llu bfs %llu rows %llu masks %llu ticks "
+                  "(100 MHz), %llu levels, %llu reached\n", q->wh_cand[i], o[0], o[1], o[2], o[3],
+                  o[4], o[5]);
+        }
+      }
+    }
+  }
   return SPF_OK;
 }
 

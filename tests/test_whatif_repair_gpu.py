@@ -148,3 +148,50 @@ def test_repair_fabric_clos(gpu_ready, monkeypatch):
     kern, nscr = _compare(g, csr, qs, ign, abi.SPF_F_NEXTHOPS, monkeypatch, rows={0, 3, 77, 150, 151, 299})
     assert kern.startswith("lds")
     g.close()
+
+
+@pytest.mark.parametrize("case", ["fabric", "uniform5"])
+def test_source_link_failures_heavy_kernel(gpu_ready, case, monkeypatch):
+    """What-ifs that fail a link of the source itself on a uniform-metric
+    area (K is most of the graph) run in spf_whatif_heavy_kernel: a BFS and
+    a level-by-level next-hop pass on one 1,024-thread workgroup per query.
+    Rows and masks equal the same batch with that kernel off
+    (OPENR_SPF_WHATIF_HEAVY=0: spf_sssp_kernel from scratch) and the
+    DijkstraQ replay; parallel links of the source keep its neighbour bit."""
+    monkeypatch.setenv("OPENR_SPF_MSBFS_IGN", "0")
+    rng = random.Random(306)
+    if case == "fabric":
+        topo = TP.fabric(1200)
+        csr = topo.csr()
+        r, _ = topo.rank()
+        s = int(r[topo.names.index("2-0-0")])
+    else:
+        V = 1500
+        links = random_links(rng, V, 5000, wmin=5, wmax=5, parallel=0.05, asym=False)
+        # a parallel link at the source
+        links.append((0, links[0][1] if links[0][0] == 0 else 1, 5, 5))
+        ov = np.zeros(V, dtype=np.uint8)
+        ov[rng.sample(range(1, V), 30)] = 1
+        csr = abi.Csr.from_links(V, links, overloaded=ov)
+        s = 0
+    g = abi.Graph(csr)
+    rp = csr.row_ptr
+    src_links = sorted({int(csr.link_id[e]) for e in range(int(rp[s]), int(rp[s + 1]))})
+    L = int(csr.link_id.max()) + 1
+    ign = [[l] for l in src_links] + [sorted(rng.sample(range(L), 2)) for _ in range(40)]
+    qs = [s] * len(ign)
+    flags = abi.SPF_F_NEXTHOPS
+    q = g.query(qs, flags, ignore=ign).run()
+    assert "spf_whatif_heavy_kernel" in q.kernels()
+    monkeypatch.setenv("OPENR_SPF_WHATIF_HEAVY", "0")
+    r = g.query(qs, flags, ignore=ign).run()
+    monkeypatch.delenv("OPENR_SPF_WHATIF_HEAVY")
+    assert "spf_whatif_heavy_kernel" not in r.kernels()
+    for i in range(len(qs)):
+        assert (q.dist(i) == r.dist(i)).all(), i
+        assert (q.nexthops(i) == r.nexthops(i)).all(), i
+    check_query(csr, q, qs, True, ignore=ign,
+                rows=set(range(0, len(src_links), max(1, len(src_links) // 6))) | {len(qs) - 1})
+    q.close()
+    r.close()
+    g.close()

@@ -183,6 +183,9 @@ def pmc_traffic_largest(kernel_name):
     return None, None
 
 
+GRAPH_PREP_KERNELS = {"spf_graph_derive_kernel", "spf_sell_kernel"}
+
+
 def pmc_plan_traffic(launched, fname):
     """HBM bytes of one batch of a multi-kernel plan from the newest
     committed profiles/*/<fname> whose kernel set (runtime copies / fills
@@ -198,7 +201,9 @@ def pmc_plan_traffic(launched, fname):
             continue
         ks = d.get("kernels", {})
         runs = d.get("batches")
-        have = {k for k in ks if not k.startswith("__amd_rocclr")}
+        # runtime copies / fills and the graph-preparation kernels (run once
+        # when the probe builds its graphs, not per batch) are not the plan's
+        have = {k for k in ks if not k.startswith("__amd_rocclr") and k not in GRAPH_PREP_KERNELS}
         if not runs or have != want:
             skipped.append(os.path.relpath(f, ROOT))
             continue

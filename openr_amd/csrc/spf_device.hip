@@ -5420,6 +5420,12 @@ struct WhatifHeavyArgs {
   // OPENR_SPF_WHATIF_STATS=1: per candidate {init, BFS, rows, masks ticks
   // (100 MHz), levels, reached}; nullptr = off
   unsigned long long* stats = nullptr;
+  // the pull form (spf_whatif_pull_kernel): the sliced-ELL copy and the
+  // links' half-edges
+  const uint4* sell4 = nullptr;
+  const uint32_t* sell_off = nullptr;
+  const uint32_t* link_half = nullptr;
+  uint32_t L = 0;
 };
 constexpr uint32_t kWhThreads = 1024;
 constexpr uint32_t kWhIgn = 512; // ignore-list hash slots in LDS
@@ -5606,6 +5612,181 @@ __global__ __launch_bounds__(kWhThreads) void spf_whatif_heavy_kernel(WhatifHeav
     o[3] = wall_clock64() - tk[3];
     o[4] = nlev;
     o[5] = sh_tail;
+  }
+}
+
+// The same queries in pull form (spf_whatif_pull_kernel, the default where
+// the graph has its sliced-ELL copy and a query ignores at most kWpIgnE / 2
+// links).  The queue form's levels cost ~50 us each: a group walks its
+// frontier nodes one after another, each a chain of dependent loads
+// (profiles/r05an).  Here thread t owns nodes t, t + 1,024, ... (a wave =
+// one 64-node slice of the sliced ELL, read 1 KB per load), and every level
+// each unreached node pulls over its row: reached at L + 1 iff some
+// neighbour u has lvl(u) = L, is the source or transit, and the half-edge's
+// link is not ignored (uniform metric: the row's out-neighbours are its
+// in-neighbours, each link has both halves).  The masks come the same way,
+// level by level.  The ignored links are their half-edge indices in LDS
+// (edge j of v's slice row is CSR edge row[v] + j).
+constexpr uint32_t kWpIgnE = 32;
+
+__global__ __launch_bounds__(kWhThreads) void spf_whatif_pull_kernel(WhatifHeavyArgs a) {
+  extern __shared__ __align__(16) uint32_t wp_smem[];
+  uint32_t* lvl = wp_smem;        // [V] BFS level, kInf32 = unreached
+  uint32_t* trl = lvl + a.V;      // [V / 32] transit bits
+  __shared__ uint32_t ige[kWpIgnE];
+  __shared__ uint32_t sh_nie;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t q = a.cand[blockIdx.x];
+  if (a.skip[q] != 3u) {
+    return; // screened (rows copied) or repairable: not this kernel's
+  }
+  unsigned long long tk[4] = {a.stats ? wall_clock64() : 0ull, 0, 0, 0};
+  const uint32_t s = a.src[q], V = a.V;
+  const uint32_t ilo = a.ign_off[q], nign = a.ign_off[q + 1] - ilo;
+  if (tid == 0) {
+    uint32_t n = 0;
+    for (uint32_t i = 0; i < nign; ++i) {
+      const uint32_t l = a.ign[ilo + i];
+      for (uint32_t side = 0; l < a.L && side < 2; ++side) {
+        const uint32_t e = a.link_half[2 * (size_t)l + side];
+        if (e != kInf32 && n < kWpIgnE) {
+          ige[n++] = e;
+        }
+      }
+    }
+    sh_nie = n;
+  }
+  for (uint32_t v = tid; v < V; v += kWhThreads) {
+    lvl[v] = v == s ? 0u : kInf32;
+  }
+  for (uint32_t i = tid; i < (V + 31) / 32; i += kWhThreads) {
+    trl[i] = a.trbits[i];
+  }
+  __syncthreads();
+  const uint32_t nie = sh_nie;
+  auto transit = [&](uint32_t u) { return u == s || ((trl[u >> 5] >> (u & 31)) & 1u); };
+  auto ignored = [&](uint32_t e) {
+    for (uint32_t i = 0; i < nie; ++i) {
+      if (ige[i] == e) {
+        return true;
+      }
+    }
+    return false;
+  };
+  const uint32_t K = (V + kWhThreads - 1) / kWhThreads;
+  // the BFS: level L + 1 = unreached nodes with a usable neighbour at L
+  uint32_t L = 0;
+  for (;; ++L) {
+    bool any = false;
+    for (uint32_t k = 0; k < K; ++k) {
+      const uint32_t v = tid + k * kWhThreads;
+      // a wave's 64 nodes are one slice: its bounds are wave-uniform
+      const uint32_t c = __builtin_amdgcn_readfirstlane(v >> 6);
+      if ((c << 6) >= V) {
+        continue; // uniform: the whole wave is past the last node
+      }
+      if (v >= V || lvl[v] != kInf32) {
+        continue;
+      }
+      const uint32_t g0 = a.sell_off[c], g1 = a.sell_off[c + 1];
+      const uint32_t r0 = a.row[v], deg = a.row[v + 1] - r0;
+      const uint4* p = a.sell4 + (size_t)g0 * 64 + lane;
+      bool found = false;
+      for (uint32_t gi = 0; gi < g1 - g0 && !found; ++gi) {
+        const uint4 w = p[(size_t)gi * 64];
+        const uint32_t us[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (uint32_t t = 0; t < 4; ++t) {
+          const uint32_t j = gi * 4 + t, u = us[t];
+          if (j < deg && lvl[u] == L && transit(u) && !ignored(r0 + j)) {
+            found = true;
+          }
+        }
+      }
+      if (found) {
+        lvl[v] = L + 1;
+        any = true;
+      }
+    }
+    if (!__syncthreads_or(any)) {
+      break;
+    }
+  }
+  const uint32_t nlev = L + 1; // levels 0 .. L hold nodes
+  if (a.stats) {
+    tk[1] = wall_clock64();
+  }
+  uint32_t* dist = a.dist_out + (size_t)q * a.Vp;
+  const uint32_t W = a.want_nh ? a.nh_w[q] : 0u;
+  uint64_t* nh = a.want_nh ? a.nh_out + a.nh_off[q] : nullptr;
+  for (uint32_t v = tid; v < V; v += kWhThreads) {
+    const uint32_t l = lvl[v];
+    dist[v] = l == kInf32 ? kInf32 : l * a.scale;
+    if (l == kInf32 || v == s) {
+      for (uint32_t w = 0; w < W; ++w) {
+        nh[(size_t)v * W + w] = 0ull; // unreached (and the source): empty
+      }
+    }
+  }
+  __syncthreads();
+  if (a.stats) {
+    tk[2] = wall_clock64();
+  }
+  // next hops, level by level (level l reads level l - 1's masks, written by
+  // this workgroup before the barrier)
+  for (uint32_t l = 1; W && l < nlev; ++l) {
+    for (uint32_t k = 0; k < K; ++k) {
+      const uint32_t v = tid + k * kWhThreads;
+      const uint32_t c = __builtin_amdgcn_readfirstlane(v >> 6);
+      if ((c << 6) >= V) {
+        continue;
+      }
+      if (v >= V || lvl[v] != l) {
+        continue;
+      }
+      const uint32_t g0 = a.sell_off[c], g1 = a.sell_off[c + 1];
+      const uint32_t r0 = a.row[v], deg = a.row[v + 1] - r0;
+      const uint4* p = a.sell4 + (size_t)g0 * 64 + lane;
+      uint64_t acc[kWhMaxW] = {0, 0, 0, 0};
+      for (uint32_t gi = 0; gi < g1 - g0; ++gi) {
+        const uint4 w = p[(size_t)gi * 64];
+        const uint32_t us[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (uint32_t t = 0; t < 4; ++t) {
+          const uint32_t j = gi * 4 + t, u = us[t];
+          if (j >= deg || lvl[u] + 1 != l || !transit(u) || ignored(r0 + j)) {
+            continue;
+          }
+          if (u == s) {
+            const uint32_t b = a.slot[a.rev[r0 + j]]; // v's slot among s's neighbours
+            acc[b >> 6] |= 1ull << (b & 63);
+          } else {
+#pragma unroll
+            for (uint32_t x = 0; x < kWhMaxW; ++x) {
+              if (x < W) {
+                acc[x] |= nh[(size_t)u * W + x];
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (uint32_t x = 0; x < kWhMaxW; ++x) {
+        if (x < W) {
+          nh[(size_t)v * W + x] = acc[x];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (a.stats && tid == 0) {
+    unsigned long long* o = a.stats + 6 * (size_t)blockIdx.x;
+    o[0] = 0;
+    o[1] = tk[1] - tk[0];
+    o[2] = tk[2] - tk[1];
+    o[3] = wall_clock64() - tk[2];
+    o[4] = nlev;
+    o[5] = 0;
   }
 }
 
@@ -7467,6 +7648,7 @@ struct spf_query {
   hipStream_t wh_stream = nullptr;    // the heavy kernel's stream (beside the SSSP)
   hipEvent_t wh_ev0 = nullptr, wh_ev1 = nullptr;
   bool wh_pending = false;            // the graph stream still has to join wh_ev1
+  bool wh_pull = false;               // spf_whatif_pull_kernel (sliced ELL, short lists)
   uint32_t dlds_shift = 4, dlds_grid = 0;
   size_t dlds_lds = 0;
   uint32_t* d_ovf = nullptr; // [0] overflow count, [1] claim counter, [2..] list
@@ -10269,6 +10451,12 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
               q->wh_cand.push_back(i);
             }
           }
+          q->wh_pull = g->d_sell != nullptr && env_flag("OPENR_SPF_WHATIF_PULL", 1);
+          for (uint32_t i : q->wh_cand) {
+            if (desc->ignore_offsets[i + 1] - desc->ignore_offsets[i] > kWpIgnE / 2) {
+              q->wh_pull = false;
+            }
+          }
           if (!q->wh_cand.empty()) {
             std::vector<uint8_t> mark(nq, 0);
             for (uint32_t i : q->wh_cand) {
@@ -11144,13 +11332,19 @@ int run_screen(spf_query* q) {
     h.scale = (q->flags & SPF_F_UNIT_METRIC) ? 1u : g->uniform;
     h.want_nh = (q->flags & SPF_F_NEXTHOPS) ? 1u : 0u;
     h.lstart = q->d_wh_lstart;
+    h.sell4 = g->d_sell;
+    h.sell_off = g->d_sell_off;
+    h.link_half = g->d_link_half;
+    h.L = g->L;
     if (env_flag("OPENR_SPF_WHATIF_STATS", 0)) {
       HIP_TRY(hipMalloc((void**)&h.stats, 6 * q->wh_cand.size() * 8));
       HIP_TRY(hipMemset(h.stats, 0, 6 * q->wh_cand.size() * 8));
     }
-    const size_t lds = (3 * (size_t)g->V + 1 + (g->V + 31) / 32) * 4;
-    HIP_TRY(hipFuncSetAttribute((const void*)spf_whatif_heavy_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const size_t lds = q->wh_pull ? ((size_t)g->V + (g->V + 31) / 32) * 4
+                                  : (3 * (size_t)g->V + 1 + (g->V + 31) / 32) * 4;
+    const void* hk = q->wh_pull ? (const void*)spf_whatif_pull_kernel
+                                : (const void*)spf_whatif_heavy_kernel;
+    HIP_TRY(hipFuncSetAttribute(hk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     // on its own (high-priority) stream beside the SSSP of the rest, the
     // graph stream joining it after that launch (launch_sssp): fabric batch
     // 1.38 ms, against 1.54 ms in order on the graph stream
@@ -11162,8 +11356,13 @@ int run_screen(spf_query* q) {
       HIP_TRY(hipEventRecord(q->wh_ev0, g->stream));
       HIP_TRY(hipStreamWaitEvent(q->wh_stream, q->wh_ev0, 0));
     }
-    SPF_LAUNCH(spf_whatif_heavy_kernel, dim3((uint32_t)q->wh_cand.size()), dim3(kWhThreads), lds,
-               hstream, h);
+    if (q->wh_pull) {
+      SPF_LAUNCH(spf_whatif_pull_kernel, dim3((uint32_t)q->wh_cand.size()), dim3(kWhThreads),
+                 lds, hstream, h);
+    } else {
+      SPF_LAUNCH(spf_whatif_heavy_kernel, dim3((uint32_t)q->wh_cand.size()), dim3(kWhThreads),
+                 lds, hstream, h);
+    }
     HIP_TRY(hipGetLastError());
     if (side) {
       HIP_TRY(hipEventRecord(q->wh_ev1, q->wh_stream));

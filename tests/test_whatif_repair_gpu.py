@@ -150,15 +150,20 @@ def test_repair_fabric_clos(gpu_ready, monkeypatch):
     g.close()
 
 
+@pytest.mark.parametrize("pull", ["1", "0"])
 @pytest.mark.parametrize("case", ["fabric", "uniform5"])
-def test_source_link_failures_heavy_kernel(gpu_ready, case, monkeypatch):
+def test_source_link_failures_heavy_kernel(gpu_ready, case, pull, monkeypatch):
     """What-ifs that fail a link of the source itself on a uniform-metric
-    area (K is most of the graph) run in spf_whatif_heavy_kernel: a BFS and
-    a level-by-level next-hop pass on one 1,024-thread workgroup per query.
-    Rows and masks equal the same batch with that kernel off
-    (OPENR_SPF_WHATIF_HEAVY=0: spf_sssp_kernel from scratch) and the
-    DijkstraQ replay; parallel links of the source keep its neighbour bit."""
+    area (K is most of the graph) run on one 1,024-thread workgroup per
+    query: a BFS and a level-by-level next-hop pass, in pull form over the
+    sliced ELL (spf_whatif_pull_kernel, default) or over a BFS queue
+    (spf_whatif_heavy_kernel, OPENR_SPF_WHATIF_PULL=0).  Rows and masks
+    equal the same batch with neither (OPENR_SPF_WHATIF_HEAVY=0:
+    spf_sssp_kernel from scratch) and the DijkstraQ replay; parallel links
+    of the source keep its neighbour bit."""
     monkeypatch.setenv("OPENR_SPF_MSBFS_IGN", "0")
+    monkeypatch.setenv("OPENR_SPF_WHATIF_PULL", pull)
+    kname = "spf_whatif_pull_kernel" if pull == "1" else "spf_whatif_heavy_kernel"
     rng = random.Random(306)
     if case == "fabric":
         topo = TP.fabric(1200)
@@ -182,11 +187,11 @@ def test_source_link_failures_heavy_kernel(gpu_ready, case, monkeypatch):
     qs = [s] * len(ign)
     flags = abi.SPF_F_NEXTHOPS
     q = g.query(qs, flags, ignore=ign).run()
-    assert "spf_whatif_heavy_kernel" in q.kernels()
+    assert kname in q.kernels()
     monkeypatch.setenv("OPENR_SPF_WHATIF_HEAVY", "0")
     r = g.query(qs, flags, ignore=ign).run()
     monkeypatch.delenv("OPENR_SPF_WHATIF_HEAVY")
-    assert "spf_whatif_heavy_kernel" not in r.kernels()
+    assert kname not in r.kernels()
     for i in range(len(qs)):
         assert (q.dist(i) == r.dist(i)).all(), i
         assert (q.nexthops(i) == r.nexthops(i)).all(), i

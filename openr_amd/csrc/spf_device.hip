@@ -6435,6 +6435,9 @@ struct TraceCursorArgs {
   // OPENR_SPF_TRACE_STATS=1: per query {wall ticks (100 MHz), DFS steps,
   // pathLinks lists built, their filter ticks, rank ticks, entries}; nullptr = off
   unsigned long long* qstat = nullptr;
+  // queries past the first nwaves are claimed from this counter (zeroed per
+  // launch) by the wave that frees up first; nullptr: static stride
+  uint32_t* qctr = nullptr;
 };
 constexpr uint32_t kTcStat = 6;
 
@@ -6494,7 +6497,20 @@ __global__ __launch_bounds__(64 * kTcWaves) void spf_trace_cursor_kernel(TraceCu
       pend_a = pend_n = false;                          \
     }                                                   \
   } while (0)
-  for (uint32_t q = gw; q < a.nq; q += nwaves) { // wave-uniform loop
+  // the next query of this wave: claimed dynamically (a wave that drew
+  // short traces takes more of them; with the static stride the slowest
+  // wave's share set the launch), or the static stride
+  auto next_query = [&](uint32_t q) -> uint32_t {
+    if (!A.qctr) {
+      return q + nwaves;
+    }
+    uint32_t c = 0;
+    if (lane == 0) {
+      c = atomicAdd(A.qctr, 1u);
+    }
+    return nwaves + (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+  };
+  for (uint32_t q = gw; q < a.nq; q = next_query(q)) { // wave-uniform loop
     const uint32_t tag = q + 1;
     const uint32_t s = a.src[q], d = a.dst[q];
     const uint32_t* dist = a.dist + (size_t)q * a.Vp;
@@ -11965,7 +11981,9 @@ int spf_query_trace_paths(
     const uint32_t maxw = g->V > 50000 ? 1024u : (uint32_t)g->num_cus * wpc;
     const uint32_t nw = std::min<uint32_t>((count + kTcWaves - 1) / kTcWaves * kTcWaves, maxw);
     const uint32_t acap = std::max<uint32_t>(1024, std::min<uint32_t>(g->E, 1u << 15));
-    const size_t need = (size_t)nw * g->V * sizeof(uint4) + (size_t)nw * acap * sizeof(uint2);
+    // node states | arenas | the query-claim counter
+    const size_t o_ctr = (size_t)nw * g->V * sizeof(uint4) + (size_t)nw * acap * sizeof(uint2);
+    const size_t need = o_ctr + 256;
     if (q->d_tcs && q->tcs_bytes < need) {
       HIP_TRY(hipStreamSynchronize(g->stream));
       pool_free(q->d_tcs);
@@ -11986,6 +12004,10 @@ int spf_query_trace_paths(
     // device's (KSP2 build 58 -> 74 ms, profiles/r05s)
     ta.budget = env_u32("OPENR_SPF_TRACE_BUDGET", heavy ? kTcHeavyBudget : 0xFFFFFFFFu);
     HIP_TRY(hipMemsetAsync(q->d_tcs, 0, (size_t)nw * g->V * sizeof(uint4), g->stream));
+    if (env_flag("OPENR_SPF_TRACE_DYN", 1) && count > nw) {
+      ta.qctr = reinterpret_cast<uint32_t*>(q->d_tcs + o_ctr);
+      HIP_TRY(hipMemsetAsync(ta.qctr, 0, 4, g->stream));
+    }
     if (env_flag("OPENR_SPF_TRACE_STATS", 0)) {
       HIP_TRY(hipMalloc((void**)&ta.qstat, (size_t)count * kTcStat * 8));
       HIP_TRY(hipMemsetAsync(ta.qstat, 0, (size_t)count * kTcStat * 8, g->stream));

@@ -4096,8 +4096,14 @@ struct NlV2Args {
   // stay in its L2 (round-robin dealing makes every XCD fetch every row);
   // 3 = chunk-major with the chunk's solo and group items interleaved in
   // proportion, so VALU-heavy solo blocks and store-heavy group blocks are
-  // resident together
+  // resident together; 4 = item-major; 5 = an explicit block map (xmap):
+  // items of one neighbour class (same largest neighbour: a pod's FSWs, a
+  // plane's SSWs, a pod's RSW groups) chunk by chunk, cut into 8 cost-
+  // balanced ranges, range x on the blocks b = 8 j + x that the dispatcher
+  // deals to XCD x, so a class's neighbour rows are fetched into one L2
   uint32_t order;
+  const uint32_t* xmap = nullptr; // [nmap] item << 12 | chunk, ~0 = empty
+  uint32_t nmap = 0;
 };
 constexpr uint32_t kNlGS = 8;  // sources per group block
 constexpr uint32_t kNlGN = 16; // neighbours of a group source (one mask word, B <= 2)
@@ -4514,6 +4520,19 @@ __global__ __launch_bounds__(T) void spf_nh_levels_v2_kernel(NhLevelsArgs a, NlV
   }
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.lvl, (short)0, (int)v.lvl_bytes, 0x00020000);
+  if (v.order == 5) {
+    const uint32_t e = v.xmap[blockIdx.x];
+    if (e == kInf32) {
+      return; // padding of a shorter XCD range
+    }
+    const uint32_t k = e >> 12, c = e & 0xFFFu;
+    if (k < v.nsolo) {
+      nl_v2_solo<T>(a, v, k, c, tile, rs);
+    } else {
+      nl_v2_group<T>(a, v, k - v.nsolo, c, rs);
+    }
+    return;
+  }
   if (v.order != 0) {
     const uint32_t bid = v.order == 2 ? xcd_logical_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint32_t per = v.nsolo + v.nsub;
@@ -7995,6 +8014,61 @@ int build_nl_v2(spf_query* q, const uint32_t* sources, const std::vector<int32_t
   if ((uint64_t)(solo.size() + subs.size()) * nch > 0x7FFFFFFFull) {
     return SPF_OK; // the held kernel's own limit check reports it
   }
+  const uint32_t vorder = std::min<uint32_t>(5, env_u32("OPENR_NL_V2_ORDER", 4));
+  std::vector<uint32_t> xmap;
+  if (vorder == 5 && solo.size() + subs.size() < (1u << 20) && nch <= 4096) {
+    // items by neighbour class (largest neighbour id), chunk by chunk within
+    // a class; cost ~ the neighbour rows a block reads plus its outputs
+    struct It {
+      uint32_t key, k, cost;
+    };
+    std::vector<It> items;
+    for (uint32_t k = 0; k < solo.size(); ++k) {
+      const uint32_t s = sources[solo[k].q];
+      items.push_back({g->nbrs[g->nbr_off[s + 1] - 1], k, 4 + solo[k].n + 2 * solo[k].B});
+    }
+    for (uint32_t j = 0; j < subs.size(); ++j) {
+      const NlSub& sb = subs[j];
+      items.push_back({ent[sb.lo + sb.n - 1].node, (uint32_t)solo.size() + j, 4 + sb.n + 2 * sb.cnt});
+    }
+    std::stable_sort(items.begin(), items.end(), [](const It& x, const It& y) { return x.key < y.key; });
+    std::vector<uint32_t> blocks;
+    std::vector<uint64_t> cost;
+    for (size_t i = 0; i < items.size();) {
+      size_t j = i;
+      while (j < items.size() && items[j].key == items[i].key) {
+        ++j;
+      }
+      for (uint32_t c = 0; c < nch; ++c) {
+        for (size_t x = i; x < j; ++x) {
+          blocks.push_back(items[x].k << 12 | c);
+          cost.push_back(items[x].cost);
+        }
+      }
+      i = j;
+    }
+    uint64_t total = 0;
+    for (uint64_t c : cost) {
+      total += c;
+    }
+    std::vector<std::vector<uint32_t>> rng(8);
+    uint64_t acc = 0;
+    for (size_t i = 0; i < blocks.size(); ++i) {
+      const uint32_t x = (uint32_t)std::min<uint64_t>(7, acc * 8 / std::max<uint64_t>(total, 1));
+      rng[x].push_back(blocks[i]);
+      acc += cost[i];
+    }
+    size_t mx = 0;
+    for (const auto& r : rng) {
+      mx = std::max(mx, r.size());
+    }
+    xmap.assign(8 * mx, kInf32);
+    for (uint32_t x = 0; x < 8; ++x) {
+      for (size_t j = 0; j < rng[x].size(); ++j) {
+        xmap[8 * j + x] = rng[x][j];
+      }
+    }
+  }
   const uint64_t lvl_bytes = (uint64_t)q->nrows * q->Vp8;
   if (lvl_bytes >= 0x80000000ull) {
     return SPF_OK; // beyond one buffer descriptor: the held kernel
@@ -8007,8 +8081,10 @@ int build_nl_v2(spf_query* q, const uint32_t* sources, const std::vector<int32_t
   const size_t o_solo = 0, o_sub = al(o_solo + solo.size() * sizeof(NlSolo)),
                o_mem = al(o_sub + subs.size() * sizeof(NlSub)),
                o_ent = al(o_mem + mem.size() * sizeof(NlMem)),
-               total = al(o_ent + ent.size() * sizeof(NlEnt));
+               o_map = al(o_ent + ent.size() * sizeof(NlEnt)),
+               total = al(o_map + xmap.size() * 4);
   std::vector<uint8_t> host(total, 0);
+  std::memcpy(host.data() + o_map, xmap.data(), xmap.size() * 4);
   std::memcpy(host.data() + o_solo, solo.data(), solo.size() * sizeof(NlSolo));
   std::memcpy(host.data() + o_sub, subs.data(), subs.size() * sizeof(NlSub));
   std::memcpy(host.data() + o_mem, mem.data(), mem.size() * sizeof(NlMem));
@@ -8028,7 +8104,9 @@ int build_nl_v2(spf_query* q, const uint32_t* sources, const std::vector<int32_t
   q->v2.dbg = env_u32("OPENR_NL_V2_DBG", 0);
   // item-major (4): measured fastest with the LDS-staged wide tiles
   // (profiles/r05k: 0.364 ms against 0.385-0.389 for the chunk-major orders)
-  q->v2.order = std::min<uint32_t>(4, env_u32("OPENR_NL_V2_ORDER", 4));
+  q->v2.order = vorder == 5 && xmap.empty() ? 4u : vorder;
+  q->v2.xmap = reinterpret_cast<const uint32_t*>(b + o_map);
+  q->v2.nmap = (uint32_t)xmap.size();
   q->has_v2 = true;
   q->v2_gen = g->nbr_gen;
   return SPF_OK;
@@ -11108,7 +11186,9 @@ int launch_nh_levels(spf_query* q, bool unit) {
     const uint32_t* nolist = nullptr;
     if (q->has_v2 && q->v2_gen == g->nbr_gen && T == 256 && !a.held_order) {
       // v2: solo items and shared-neighbour groups (spf_nh_levels_v2_kernel)
-      const uint64_t vblocks = (uint64_t)(q->v2.nsolo + q->v2.nsub) * ((g->V + 1023) / 1024);
+      const uint64_t vblocks = q->v2.order == 5 ? (uint64_t)q->v2.nmap
+                                                : (uint64_t)(q->v2.nsolo + q->v2.nsub) *
+                                                      ((g->V + 1023) / 1024);
       if (vblocks) {
         SPF_LAUNCH((spf_nh_levels_v2_kernel<256>), dim3((uint32_t)vblocks), dim3(256), 0,
                            g->stream, a, q->v2);

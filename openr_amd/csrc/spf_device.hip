@@ -4581,6 +4581,9 @@ __global__ __launch_bounds__(T) void spf_nh_levels_v2_kernel(NhLevelsArgs a, NlV
 // offsets / widths from device arrays, or (off == nullptr) the scalars of one
 // row.
 struct NhNarrowArgs {
+  // queries the what-if screen already wrote in the output layout
+  // (skip[q] == 1); nullptr: none
+  const uint32_t* skip = nullptr;
   const uint64_t* src;
   uint8_t* dst;
   const uint64_t* src_off; // words
@@ -4595,7 +4598,7 @@ struct NhNarrowArgs {
 __global__ __launch_bounds__(256) void spf_nh_narrow_kernel(NhNarrowArgs a) {
   const uint32_t nch = (a.V + 1023) / 1024;
   const uint32_t q = blockIdx.x / nch, c = blockIdx.x - q * nch;
-  if (q >= a.nq) {
+  if (q >= a.nq || (a.skip && a.skip[q] == 1u)) {
     return;
   }
   const bool list = a.src_off != nullptr;
@@ -5366,6 +5369,12 @@ struct WhatifArgs {
   // one of spf_whatif_heavy_kernel's (wh_mark[q] != 0: it runs them)
   uint32_t mark_heavy;
   const uint8_t* wh_mark = nullptr;
+  // narrow rows (spf_query::narrow): a screened query's masks go straight to
+  // the output layout (the baseline word row narrowed on the copy), and the
+  // narrowing pass skips it; nullptr: word rows, narrowed later
+  uint8_t* nhb = nullptr;
+  const uint64_t* nhb_off = nullptr;
+  const uint32_t* nh_b = nullptr;
 };
 
 __global__ __launch_bounds__(256) void spf_whatif_screen_kernel(WhatifArgs a) {
@@ -5400,8 +5409,27 @@ __global__ __launch_bounds__(256) void spf_whatif_screen_kernel(WhatifArgs a) {
   }
   block_copy<uint32_t, 256>(a.dist_out + (size_t)q * a.Vp, bd, a.V);
   if (a.want_nh) {
-    block_copy<uint64_t, 256>(a.nh_out + a.nh_off[q], a.base_nh + a.base_nh_off[b],
-                              (size_t)a.V * a.nh_w[q]);
+    const uint64_t* src = a.base_nh + a.base_nh_off[b];
+    const uint32_t W = a.nh_w[q];
+    if (!a.nhb) {
+      block_copy<uint64_t, 256>(a.nh_out + a.nh_off[q], src, (size_t)a.V * W);
+      return;
+    }
+    uint8_t* d = a.nhb + a.nhb_off[q];
+    const uint32_t B = a.nh_b[q];
+    if (B >= 8) {
+      // B = 8 W: the output layout is the word layout
+      block_copy<uint64_t, 256>(reinterpret_cast<uint64_t*>(d), src, (size_t)a.V * W);
+      return;
+    }
+    for (uint32_t v0 = 4 * threadIdx.x; v0 < a.V; v0 += 4 * blockDim.x) {
+      uint64_t x[4];
+#pragma unroll
+      for (uint32_t i = 0; i < 4; ++i) {
+        x[i] = v0 + i < a.V ? src[v0 + i] : 0ull; // B < 8: one word per node
+      }
+      nh_store4_narrow(d, B, v0, a.V, x);
+    }
   }
 }
 
@@ -7715,6 +7743,7 @@ struct spf_query {
   std::vector<uint32_t> nh_b;
   uint64_t nhb_total = 0;
   bool narrow = false, nh_direct = false;
+  bool screen_direct = false; // the last screen wrote its copies narrowed (run_screen)
   bool nl_swar = true; // the byte-SIMD next-hop kernels (OPENR_NL_SWAR, read at creation)
   uint8_t* d_nhb = nullptr;
   uint64_t* d_nhb_off = nullptr;
@@ -11401,6 +11430,15 @@ int run_screen(spf_query* q) {
   a.unit = (q->flags & SPF_F_UNIT_METRIC) ? 1u : 0u;
   a.mark_heavy = q->repair ? 1u : 0u;
   a.wh_mark = q->repair ? q->d_wh_mark : nullptr;
+  // screened rows straight into the output layout (the narrowing pass skips
+  // them: OPENR_SPF_SCREEN_DIRECT=0 keeps the word copy)
+  q->screen_direct = q->narrow && !q->nh_direct && a.want_nh && q->d_nhb && q->d_nhb_off &&
+                     env_flag("OPENR_SPF_SCREEN_DIRECT", 1);
+  if (q->screen_direct) {
+    a.nhb = q->d_nhb;
+    a.nhb_off = q->d_nhb_off;
+    a.nh_b = q->d_nh_b;
+  }
   if (b->Vp != q->Vp) {
     return fail(SPF_E_INVALID, "baseline row stride differs");
   }
@@ -11500,6 +11538,7 @@ int run_plan(spf_query* q) {
   na.nw = q->d_nh_w;
   na.V = q->g->V;
   na.nq = q->nq;
+  na.skip = q->base && q->screen_direct ? q->d_skip : nullptr;
   const uint64_t blocks = (uint64_t)q->nq * ((q->g->V + 1023) / 1024);
   if (blocks > 0x7FFFFFFFull) {
     return fail(SPF_E_UNSUPPORTED, "batch too large for the mask narrowing pass");

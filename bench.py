@@ -59,7 +59,9 @@ KERNELS = {
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="number of GPUs (= ranks, one process per GPU); without an outer "
+                        "torch.distributed.run this script starts the N rank processes itself")
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -1587,7 +1589,9 @@ def fabric_sharded(args, topo, world, rank, local, dist, cluster):
             "parallelism": f"contiguous source blocks over {world} GPUs inside the engine "
                            "(spf_table, RCCL cluster); rows stay on their owner GPU",
         },
-        "gteps": round(V * E / (step_ms / 1000.0) / 1e9, 2),
+        "gteps_equivalent": {"value": round(V * E / (step_ms / 1000.0) / 1e9, 2),
+                             "note": "per-source-equivalent (sources x directed edges / step), "
+                                     "not a measured rate"},
         "device_compute_ms": round(comp_ms, 4),
         "with_row_gather": {
             "what": "the same table with every GPU's uint32 distance rows all-gathered over xGMI "
@@ -1597,6 +1601,8 @@ def fabric_sharded(args, topo, world, rank, local, dist, cluster):
             "gathered_bytes": int(V * V * 4),
         },
         "parity_spot_check": check,
+        "communicator": {"world": int(cluster.world), "first_rank": int(cluster.first_rank),
+                         "local_devices": int(cluster.local_devices)},
     }
 
 
@@ -1726,7 +1732,7 @@ def fabric_single(args, topo, world, rank, local, dist):
         "warmup": args.warmup,
         "ms_per_step": round(step_ms, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic fabric (DecisionBenchmark createFabric, SSW bug fixed), metric 1",
@@ -1737,12 +1743,13 @@ def fabric_single(args, topo, world, rank, local, dist):
             "directed_edges": E,
             "sources_per_gpu": nsrc,
             "kernel": kname,
-            "parallelism": f"source-batch per GPU, drain scenario per rank (x{world})",
+            "parallelism": "one table of every source on one GPU (N > 1 runs fabric_sharded)",
         },
-        "gteps": round(world * nsrc * E / (step_ms / 1000.0) / 1e9, 2),
-        "gteps_note": "per-source-equivalent: sources x directed edges per step time (each SSSP "
-                      "traverses every edge once); the bit-parallel BFS scans an edge once per "
-                      "level for 64 sources, so this counts shared scans, not memory traffic",
+        "gteps_equivalent": {
+            "value": round(world * nsrc * E / (step_ms / 1000.0) / 1e9, 2),
+            "note": "per-source-equivalent, not a measured rate: sources x directed edges per step "
+                    "time (a textbook SSSP traverses every edge once); the bit-parallel BFS scans an "
+                    "edge once per level for 64 sources, so this counts shared scans, not traffic"},
         "kernel_ms": round(kernel_ms, 4),
         "kernels": stages,
         "kernels_launched": launched,
@@ -1761,8 +1768,102 @@ def fabric_single(args, topo, world, rank, local, dist):
     return out
 
 
+class RankLaunchError(RuntimeError):
+    """--gpus N cannot run as N ranks here (too few devices, or an outer
+    launcher with a different world size)."""
+
+
+def visible_devices() -> int:
+    """GPUs this process can see.  torch.cuda.device_count() does not
+    initialise the GPU on this image (it asks amdsmi), so the launching
+    parent stays GPU-free before it starts its rank processes."""
+    import torch
+
+    return int(torch.cuda.device_count())
+
+
+def check_world(gpus, env=None, devices=None) -> int:
+    """The world size this run must have, or RankLaunchError.  Under an outer
+    torch.distributed.run (WORLD_SIZE set) --gpus must agree with it; either
+    way at least N devices must be visible (one process per GPU, one node)."""
+    env = os.environ if env is None else env
+    outer = env.get("WORLD_SIZE")
+    n = gpus if gpus is not None else int(outer or 1)
+    if n < 1:
+        raise RankLaunchError(f"--gpus {n}: need at least one GPU")
+    if outer is not None and int(outer) != n:
+        raise RankLaunchError(f"--gpus {n} but the launcher started WORLD_SIZE={outer} ranks")
+    have = visible_devices() if devices is None else devices
+    if have < n:
+        raise RankLaunchError(f"--gpus {n} needs {n} visible GPUs on this node, found {have}")
+    return n
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv, script=None) -> int:
+    """--gpus N with no outer launcher: start the N rank processes (one per
+    GPU: RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1) as
+    children of this GPU-free parent, wait for all of them, and pass rank 0's
+    one JSON line through.  A rank that fails ends the others (their exact
+    PIDs), so no rank waits forever at a barrier; the exit code is non-zero
+    if any rank failed or the line does not report n_gpus == N."""
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv),
+                                      env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr))
+    rcs = [None] * n
+    failed = False
+    while any(rc is None for rc in rcs):
+        for r, p in enumerate(procs):
+            if rcs[r] is None:
+                rcs[r] = p.poll()
+                if rcs[r] not in (None, 0) and not failed:
+                    failed = True
+                    print(f"bench.py: rank {r} exited with {rcs[r]}; stopping the other ranks",
+                          file=sys.stderr)
+                    for q in procs:
+                        if q.poll() is None:
+                            q.terminate()
+        time.sleep(0.2)
+    line = procs[0].stdout.read().decode().strip()
+    if any(rcs):
+        print(f"bench.py: rank exit codes {rcs}", file=sys.stderr)
+        return max(abs(rc) for rc in rcs if rc) or 1
+    try:
+        rec = json.loads(line.splitlines()[-1])
+    except (ValueError, IndexError):
+        print(f"bench.py: rank 0 printed no JSON line ({line[-200:]!r})", file=sys.stderr)
+        return 1
+    if rec.get("n_gpus") != n:
+        print(f"bench.py: rank 0 reported n_gpus={rec.get('n_gpus')} for --gpus {n}", file=sys.stderr)
+        return 1
+    sys.stdout.write(json.dumps(rec) + "\n")
+    sys.stdout.flush()
+    return 0
+
+
 def main():
     args = parse()
+    try:
+        world_want = check_world(args.gpus)
+    except RankLaunchError as e:
+        print(f"bench.py: {e}", file=sys.stderr)
+        sys.exit(3)
+    if world_want > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(world_want, sys.argv[1:]))
     # everything but the final JSON line goes to stderr: RCCL's init banner
     # ("RCCL version : ...") and any library chatter write to fd 1 directly,
     # and the contract is ONE JSON line on rank 0's stdout
@@ -1793,6 +1894,20 @@ def main():
     else:
         cluster = None
         out = fabric_single(args, topo, world, rank, local, dist)
+        # the N > 1 code path at N = 1 (spf_table over a one-rank RCCL
+        # cluster), so the 1 -> N curve has a same-code N = 1 point beside
+        # the headline query
+        try:
+            c1 = cluster_for(1, 0, local, None)
+            tl = fabric_sharded(args, topo, 1, 0, local, None, c1)
+            c1.close()
+            out["table_path"] = {k: tl[k] for k in ("value", "unit", "ms_per_step", "device_compute_ms",
+                                                    "with_row_gather", "parity_spot_check",
+                                                    "communicator")}
+            out["table_path"]["what"] = ("the headline workload through spf_table over a one-rank "
+                                         "RCCL cluster: the code path of every N > 1 line")
+        except Exception as e:  # reported, never silently replaced
+            out["table_path"] = {"error": repr(e)}
     if not args.no_wan:
         try:
             if cluster is not None:
@@ -1861,6 +1976,11 @@ def main():
             except Exception as e:
                 out["cpu_baseline"]["ksp2_full"] = {"error": repr(e)}
         out["cpu_baseline"]["cpu_model"] = host_cpu_model()
+    if cluster is not None:
+        try:
+            cluster.close()
+        except Exception as e:
+            print(f"bench.py: cluster close: {e!r}", file=sys.stderr)
     sys.stdout.flush()
     if rank == 0:
         os.write(json_fd, (json.dumps(out) + "\n").encode())

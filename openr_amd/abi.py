@@ -808,7 +808,9 @@ class Cluster:
 
     def close(self):
         if self.h:
-            load().spf_cluster_destroy(self.h)
+            # refused (nothing freed, handle kept) while a table or cluster
+            # graph over it is alive: include/openr_spf.h "Lifetime"
+            _check_cl(load().spf_cluster_destroy(self.h), "spf_cluster_destroy")
             self.h = None
 
     def __del__(self):
@@ -833,7 +835,8 @@ class ClusterGraph:
 
     def close(self):
         if self.h:
-            load().spf_cgraph_destroy(self.h)
+            # refused (nothing freed, handle kept) while a table over it lives
+            _check_cl(load().spf_cgraph_destroy(self.h), "spf_cgraph_destroy")
             self.h = None
 
     def __del__(self):

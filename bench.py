@@ -484,7 +484,8 @@ def cpu_baseline(topo, sample):
     }
 
 
-def _rebuild_loop(M, topo, iters, timed, fwd=(0, 0), after_cold=None, check=None, mode="overload"):
+def _rebuild_loop(M, topo, iters, timed, fwd=(0, 0), after_cold=None, check=None, mode="overload",
+                  lfa=False):
     """DecisionBenchmark BM_DecisionFabric loop (DecisionBenchmark.cpp:
     600-626): toggle an RSW's overload bit, rebuild the RouteDb of "2-0-0".
     fwd = (PrefixForwardingType, PrefixForwardingAlgorithm) of every prefix;
@@ -500,7 +501,7 @@ def _rebuild_loop(M, topo, iters, timed, fwd=(0, 0), after_cold=None, check=None
     ps = M.PrefixState()
     for pdb in topo.prefix_dbs("0", fwd[0], fwd[1]):
         ps.updatePrefixDatabase(pdb)
-    solver = M.SpfSolver("2-0-0", False, False)
+    solver = M.SpfSolver("2-0-0", False, lfa)
     timed(solver, areas, ps)  # cold build (device graph for the engine)
     if after_cold:
         after_cold()
@@ -639,10 +640,14 @@ def route_db_link_flap(topo, device, iters=4):
     return out
 
 
-def route_db_rebuild_ms(topo, device, iters=5):
+def route_db_rebuild_ms(topo, device, iters=5, lfa=False):
     """Full RouteDb rebuild of the benchmark node "2-0-0" after an RSW
-    overload toggle: LinkState update + SPF on the engine (LFA off, as the
-    benchmark's Decision) + RouteDb."""
+    overload toggle: LinkState update + SPF on the engine + RouteDb.
+    lfa=True is the Decision DecisionBenchmark runs (computeLfaPaths = true,
+    DecisionBenchmark.cpp:74-79): the node's SPF plus its 84 neighbours'
+    (the RFC 5286 test of Decision.cpp:1146-1175) in one device batch, LFA
+    next hops on the SP_ECMP fast path; lfa=False is the lighter LFA-off
+    build, reported beside it."""
     import openr_amd._openr_spf as E
 
     E.set_spf_device(device)
@@ -655,9 +660,9 @@ def route_db_rebuild_ms(topo, device, iters=5):
 
     def check(ls, solver, areas, ps, dbs):
         counters.update(E.get_counters())  # the timed builds' counters, before the check's
-        return _routedb_parity("sp_ecmp", ls, solver, areas, ps, dbs, topo)
+        return _routedb_parity("sp_ecmp_lfa" if lfa else "sp_ecmp", ls, solver, areas, ps, dbs, topo)
 
-    out = _rebuild_loop(E, topo, iters, timed, after_cold=E.reset_counters, check=check)
+    out = _rebuild_loop(E, topo, iters, timed, after_cold=E.reset_counters, check=check, lfa=lfa)
     c = counters or E.get_counters()
     n = max(1, c.get("decision.route_build_runs", 1))
     # warm builds only (counters reset after the cold build)
@@ -674,7 +679,8 @@ def route_db_rebuild_ms(topo, device, iters=5):
     out["builds_counted"] = n
     out["releases_counted"] = c.get("decision.route_releases", 0)
     out["node"] = "2-0-0"
-    out["what"] = "adj-db update (RSW overload toggle) + buildRouteDb, LFA off"
+    out["what"] = ("adj-db update (RSW overload toggle) + buildRouteDb, "
+                   + ("LFA on (DecisionBenchmark's Decision)" if lfa else "LFA off"))
     return out
 
 
@@ -1075,6 +1081,37 @@ def route_db_rebuild_cpu(topo, iters=2):
     out["cores"] = 1
     out["kind"] = "port"
     return out
+
+
+def route_db_rebuild_lfa_cpu(topo):
+    """The LFA-on rebuild on the oracle (reference data structures), 1
+    thread: ONE build after the first RSW overload toggle of the loop (85
+    uncached runSpf + the LFA RouteDb, ~15-25 s, so a bounded sample)."""
+    from oracle import build as obuild
+
+    obuild.build()
+    from oracle import _oracle_ref as O
+
+    areas = O.AreaLinkStates()
+    ls = areas.add("0")
+    dbs = topo.adj_dbs()
+    for db in dbs:
+        ls.updateAdjacencyDatabase(db)
+    ps = O.PrefixState()
+    for pdb in topo.prefix_dbs("0", 0, 0):
+        ps.updatePrefixDatabase(pdb)
+    solver = O.SpfSolver("2-0-0", False, True)
+    rsw = [i for i, n in enumerate(topo.names) if n.startswith("3-")]
+    db = dbs[rsw[0]]
+    db.isOverloaded = True
+    t0 = time.perf_counter()
+    ls.updateAdjacencyDatabase(db)
+    nu, nm, _ = solver.buildRouteDbTimed("2-0-0", areas, ps)[:3]
+    ms = (time.perf_counter() - t0) * 1e3
+    db.isOverloaded = False
+    return {"ms": round(ms, 1), "routes": nu + nm, "cores": 1, "kind": "port",
+            "sample": f"one LFA-on rebuild of 2-0-0 after the {topo.names[rsw[0]]} overload toggle "
+                      "(oracle/ref_decision.cpp, reference data structures)"}
 
 
 def wan_all_sources_table(args, world, rank, local, dist, cluster):
@@ -1932,6 +1969,10 @@ def main():
         except Exception as e:
             out["ksp2_route_db"] = {"error": repr(e)}
         try:
+            out["route_db_rebuild_lfa"] = route_db_rebuild_ms(topo, local, lfa=True)
+        except Exception as e:  # reported, never silently replaced
+            out["route_db_rebuild_lfa"] = {"error": repr(e)}
+        try:
             out["route_db_rebuild"] = route_db_rebuild_ms(topo, local)
         except Exception as e:  # reported, never silently replaced
             out["route_db_rebuild"] = {"error": repr(e)}
@@ -1966,6 +2007,10 @@ def main():
             out["cpu_baseline"]["route_db_rebuild"] = route_db_rebuild_cpu(topo)
         except Exception as e:
             out["cpu_baseline"]["route_db_rebuild"] = {"error": repr(e)}
+        try:
+            out["cpu_baseline"]["route_db_rebuild_lfa"] = route_db_rebuild_lfa_cpu(topo)
+        except Exception as e:
+            out["cpu_baseline"]["route_db_rebuild_lfa"] = {"error": repr(e)}
         try:
             out["cpu_baseline"]["ksp2"] = ksp2_cpu_sample(topo)
         except Exception as e:

@@ -74,14 +74,35 @@ struct LinkState::Engine {
   // single-threaded per graph)
   std::shared_mutex viewMu;
   std::mutex devMu;
+  // graphs the engine let go of while the C ABI refused to free them (a
+  // query over them was still alive: include/openr_spf.h "Lifetime"); they
+  // are freed by the next retireGraph / reapRetired that the ABI accepts,
+  // never overwritten or leaked
+  std::vector<spf_graph*> retired;
+
+  // drop `graph`: freed now, or kept in `retired` if the ABI refuses
+  void retireGraph() {
+    if (graph && spf_graph_destroy(graph) != SPF_OK) {
+      retired.push_back(graph);
+    }
+    graph = nullptr;
+    reapRetired();
+  }
+  void reapRetired() {
+    std::vector<spf_graph*> keep;
+    for (spf_graph* g : retired) {
+      if (spf_graph_destroy(g) != SPF_OK) {
+        keep.push_back(g);
+      }
+    }
+    retired.swap(keep);
+  }
 
   ~Engine() {
     if (cgraph) {
       spf_cgraph_destroy(cgraph);
     }
-    if (graph) {
-      spf_graph_destroy(graph);
-    }
+    retireGraph();
   }
 };
 

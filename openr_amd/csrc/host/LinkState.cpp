@@ -565,10 +565,7 @@ void buildGraph(
   d.node_overloaded = eng.overloaded.data();
   d.num_links = (uint32_t)eng.links.size();
   d.device = getSpfDevice();
-  if (eng.graph) {
-    spf_graph_destroy(eng.graph);
-    eng.graph = nullptr;
-  }
+  eng.retireGraph(); // (refused while a query over it lives: kept, freed later)
   if (V > 0) {
     const auto tc = std::chrono::steady_clock::now();
     const int s = spf_graph_create(&d, &eng.graph);
@@ -1775,16 +1772,17 @@ bool LinkState::patchStructure(
   d.num_links = (uint32_t)alive.size();
   d.device = getSpfDevice();
   // the device graph is rebuilt in place (same handle, stream and buffers:
-  // spf_graph_update).  A failed update leaves it unusable: it is dropped,
-  // and the caller's clearMemo() retires the engine, whose next build
-  // creates a fresh graph
+  // spf_graph_update).  A failed update leaves it unusable: it is retired
+  // (Engine::retireGraph), and the caller's clearMemo() retires the engine,
+  // whose next build creates a fresh graph
   mark("rev+rest");
   const auto tu = std::chrono::steady_clock::now();
   Counters::add("decision.graph_splice_us",
                 std::chrono::duration_cast<std::chrono::microseconds>(tu - t0).count());
   if (spf_graph_update(eng.graph, &d) != SPF_OK) {
-    spf_graph_destroy(eng.graph);
-    eng.graph = nullptr;
+    // the handle is never nulled while the ABI still refuses to free it
+    // (live queries): retireGraph keeps it for a later destroy
+    eng.retireGraph();
     return false;
   }
   Counters::add("decision.graph_update_us",

@@ -196,6 +196,8 @@ class SpfRead {
   }
 
   // fn(name, metric to that next hop) — metric = getMetricFromAToB(src, nh)
+  const SpfView& view() const { return view_; }
+
   template <class Fn>
   void forEachNextHopWithMetric(const std::string& node, Fn&& fn) const {
     if (view_.src == ~0u) {
@@ -426,18 +428,38 @@ class SpfSolver::SpfSolverImpl {
     return SpfRead(ls, myNodeName, *v);
   }
 
-  // SP_ECMP fast path (one area, LFA off): myNode's shortest-path links per
-  // next-hop mask bit of its own SPF row, with next-hop templates (metric
-  // set per prefix), built once per RouteDb build before the worker pool
+  // SP_ECMP fast path (one area): myNode's links per next-hop mask bit of
+  // its own SPF row, with next-hop templates (metric set per prefix), built
+  // once per RouteDb build before the worker pool.  LFA off: only the
+  // shortest-path links of each bit (metric(link) == d(nbr)).  LFA on: every
+  // up link of each bit, plus the neighbours' own SPF views for the RFC 5286
+  // test (getNextHopsWithMetric Decision.cpp:1146-1175)
   struct FastEcmp {
     bool ok{false};
+    bool lfa{false};
     const LinkState* ls{nullptr};
     const std::string* area{nullptr};
     const SpfView* view{nullptr};
     std::vector<std::vector<uint32_t>> bitLinks; // mask bit -> template index
     std::vector<thrift::NextHopThrift> tmpl4, tmpl6;
     std::vector<uint32_t> tmplNbr; // node id of each template's neighbour
+    std::vector<Metric> tmplMetric; // the template link's metric from myNode
+    // LFA: one entry per distinct up neighbour (linksFromNode order of its
+    // first link): its mask bit, its SPF view, its distance back to myNode
+    struct LfaBit {
+      uint32_t bit;
+      const SpfView* view;
+      Metric toHere;
+    };
+    std::vector<LfaBit> lfaBits;
   };
+  // LFA fast path: the metric beyond each next-hop neighbour (bit) for the
+  // announcers `ids` at distance `shortest`, kNoValue where the neighbour is
+  // neither a shortest-path next hop (its bit in `mask`) nor a loop-free
+  // alternate; false if no neighbour has a value
+  static constexpr Metric kNoValue = std::numeric_limits<Metric>::max();
+  bool fastLfaValues(const uint32_t* ids, size_t nIds, Metric shortest, const uint64_t* mask,
+                     std::vector<Metric>& val) const;
   FastEcmp fast_;
   // per build, one area: node labels by device node id (selectKsp2)
   struct Ksp2Fast {
@@ -1027,7 +1049,7 @@ void SpfSolver::SpfSolverImpl::buildFastEcmp(
       ksp2Fast_.me = *me;
     }
   }
-  if (areaLinkStates.size() != 1 || computeLfaPaths_ || getenv_flag_off("OPENR_ECMP_FAST")) {
+  if (areaLinkStates.size() != 1 || getenv_flag_off("OPENR_ECMP_FAST")) {
     return;
   }
   const auto& [area, ls] = *areaLinkStates.begin();
@@ -1042,6 +1064,7 @@ void SpfSolver::SpfSolverImpl::buildFastEcmp(
   fast_.ls = &ls;
   fast_.area = &area;
   fast_.view = &view;
+  fast_.lfa = computeLfaPaths_;
   fast_.bitLinks.assign(view.nbrs.size(), {});
   std::unordered_map<uint32_t, uint32_t> bitOf;
   for (uint32_t j = 0; j < view.nbrs.size(); ++j) {
@@ -1054,20 +1077,83 @@ void SpfSolver::SpfSolverImpl::buildFastEcmp(
     }
     const auto id = ls.nodeId(*ml.nbr);
     if (!id) {
+      if (fast_.lfa) {
+        return; // an up link the device row has no bit for: general path
+      }
       continue;
     }
     auto b = bitOf.find(*id);
-    if (b == bitOf.end() || !view.reached(*id) || ml.metric != view.dist[*id]) {
+    if (fast_.lfa) {
+      if (b == bitOf.end()) {
+        return;
+      }
+    } else if (b == bitOf.end() || !view.reached(*id) || ml.metric != view.dist[*id]) {
       continue; // never a shortest-path link (distOverLink != minMetric)
     }
     fast_.bitLinks[b->second].push_back((uint32_t)fast_.tmpl4.size());
     fast_.tmplNbr.push_back(*id);
+    fast_.tmplMetric.push_back(ml.metric);
     fast_.tmpl4.push_back(createNextHop(*ml.nhV4, *ml.iface, 0, std::nullopt, false,
                                         ml.link->getArea()));
     fast_.tmpl6.push_back(createNextHop(*ml.nhV6, *ml.iface, 0, std::nullopt, false,
                                         ml.link->getArea()));
   }
+  if (fast_.lfa) {
+    // the LFA candidates: every up neighbour, once (the reference's loop over
+    // links revisits a neighbour of parallel links with the same values)
+    std::vector<uint8_t> seen(view.nbrs.size(), 0);
+    for (const LfaNbr& ln : mls->lfa) {
+      const SpfView& nv = ln.read.view();
+      const auto id = ls.nodeId(*ln.nbr);
+      if (!ln.toHere || nv.src == ~0u || nv.exact || !nv.useLinkMetric || !id) {
+        return; // the general path (which throws where the reference does)
+      }
+      auto b = bitOf.find(*id);
+      if (b == bitOf.end()) {
+        return;
+      }
+      if (!seen[b->second]) {
+        seen[b->second] = 1;
+        fast_.lfaBits.push_back({b->second, &nv, *ln.toHere});
+      }
+    }
+  }
   fast_.ok = true;
+}
+
+bool SpfSolver::SpfSolverImpl::fastLfaValues(
+    const uint32_t* ids, size_t nIds, Metric shortest, const uint64_t* mask,
+    std::vector<Metric>& val) const {
+  const SpfView& view = *fast_.view;
+  const uint32_t W = view.words;
+  val.assign(view.nbrs.size(), kNoValue);
+  bool any = false;
+  // shortest-path next hops: metric beyond = shortest - d(nbr)
+  for (uint32_t w = 0; w < W; ++w) {
+    for (uint64_t b = mask[w]; b; b &= b - 1) {
+      const uint32_t bit = w * 64 + (uint32_t)__builtin_ctzll(b);
+      val[bit] = shortest - view.dist[view.nbrs[bit]];
+      any = true;
+    }
+  }
+  // loop-free alternates: d(n, dst) < shortest + d(n, me), over every
+  // announcer; the smallest such d(n, dst) if below the value so far
+  for (const auto& lb : fast_.lfaBits) {
+    const SpfView& nv = *lb.view;
+    const Metric bound = shortest + lb.toHere;
+    Metric& v = val[lb.bit];
+    for (size_t i = 0; i < nIds; ++i) {
+      if (!nv.reached(ids[i])) {
+        continue;
+      }
+      const Metric d = nv.dist[ids[i]];
+      if (d < bound && d < v) {
+        v = d;
+        any = true;
+      }
+    }
+  }
+  return any;
 }
 
 bool SpfSolver::SpfSolverImpl::fastLabelRoute(
@@ -1086,6 +1172,32 @@ bool SpfSolver::SpfSolverImpl::fastLabelRoute(
   const uint32_t W = view.words;
   const uint64_t* row = view.nh.data() + (size_t)*id * W;
   const Metric shortest = view.dist[*id];
+  if (fast_.lfa) {
+    // getNextHopsWithMetric(me, {owner}) with LFAs, then every up link of a
+    // next-hop neighbour at link metric + value (no shortest filter)
+    thread_local std::vector<Metric> val;
+    const uint32_t owner = *id;
+    if (!fastLfaValues(&owner, 1, shortest, row, val)) {
+      Counters::add("decision.no_route_to_label", 1);
+      return true;
+    }
+    std::unordered_set<thrift::NextHopThrift> nextHops;
+    for (uint32_t bit = 0; bit < val.size(); ++bit) {
+      if (val[bit] == kNoValue) {
+        continue;
+      }
+      for (const uint32_t k : fast_.bitLinks[bit]) {
+        thrift::NextHopThrift nh = fast_.tmpl6[k];
+        nh.metric = (int32_t)(fast_.tmplMetric[k] + val[bit]);
+        nh.mplsAction = fast_.tmplNbr[k] == owner
+            ? createMplsAction(thrift::MplsActionCode::PHP)
+            : createMplsAction(thrift::MplsActionCode::SWAP, label);
+        nextHops.insert(std::move(nh));
+      }
+    }
+    out.emplace(label, RibMplsEntry(label, std::move(nextHops)));
+    return true;
+  }
   size_t cnt = 0;
   for (uint32_t w = 0; w < W; ++w) {
     for (uint64_t b = row[w]; b; b &= b - 1) {
@@ -1199,6 +1311,48 @@ bool SpfSolver::SpfSolverImpl::fastEcmpOpenr(
         mask[w] |= row[w];
       }
     }
+  }
+  if (fast_.lfa) {
+    // the announcers getNextHopsWithMetric sees (drain-filtered), their
+    // loop-free alternates, then every up link of a next-hop neighbour
+    thread_local std::vector<Metric> val;
+    thread_local std::vector<uint32_t> ids;
+    ids.clear();
+    for (size_t i = 0; i < n; ++i) {
+      if (!anyUndrained || !ann(i).drained) {
+        ids.push_back(ann(i).id);
+      }
+    }
+    const bool anyNh = fastLfaValues(ids.data(), ids.size(), shortest, mask, val);
+    lap(1);
+    if (!anyNh) {
+      Counters::add("decision.no_route_to_prefix", 1);
+      return true;
+    }
+    const auto& tmpl = isV4 ? fast_.tmpl4 : fast_.tmpl6;
+    std::unordered_set<thrift::NextHopThrift> nextHops;
+    size_t cnt = 0;
+    for (uint32_t bit = 0; bit < val.size(); ++bit) {
+      cnt += val[bit] == kNoValue ? 0 : fast_.bitLinks[bit].size();
+    }
+    nextHops.reserve(cnt);
+    for (uint32_t bit = 0; bit < val.size(); ++bit) {
+      if (val[bit] == kNoValue) {
+        continue;
+      }
+      for (const uint32_t k : fast_.bitLinks[bit]) {
+        thrift::NextHopThrift nh = tmpl[k];
+        nh.metric = (int32_t)(fast_.tmplMetric[k] + val[bit]);
+        nextHops.insert(std::move(nh));
+      }
+    }
+    const Ann& best = ann(0);
+    RibUnicastEntry entry(prefix, std::move(nextHops), prefixEntries.at(*best.node).at(*best.area),
+                          *best.area);
+    lap(2);
+    unicastEntries.emplace(prefix, std::move(entry));
+    lap(3);
+    return true;
   }
   bool any = false;
   for (uint32_t w = 0; w < W; ++w) {

@@ -4104,6 +4104,14 @@ struct NlV2Args {
   uint32_t order;
   const uint32_t* xmap = nullptr; // [nmap] item << 12 | chunk, ~0 = empty
   uint32_t nmap = 0;
+  // round 6: 2-bit level rows (spf_lvl_trit_kernel: level mod 3, 3 =
+  // unreached; row stride tstride = Vp8 / 4 bytes).  An item whose sources
+  // are all transit reads its NEIGHBOURS' rows in this form (a quarter of
+  // the bytes); nullptr = every item reads byte rows (OPENR_NL_TRIT=0, a
+  // graph whose half-edges are not all paired)
+  const uint8_t* trit = nullptr;
+  uint32_t trit_bytes = 0;
+  uint32_t tstride = 0;
 };
 constexpr uint32_t kNlGS = 8;  // sources per group block
 constexpr uint32_t kNlGN = 16; // neighbours of a group source (one mask word, B <= 2)
@@ -4173,6 +4181,107 @@ __device__ __forceinline__ uint32_t nl_v3_cmp8(const uint32_t (&lf)[8], uint32_t
   return P;
 }
 
+// ---- 2-bit neighbour rows (round 6)
+//
+// On a uniform metric with every half-edge paired, a transit source s and a
+// transit neighbour n have BFS levels one apart at most at every node v
+// (s -> n -> ... and n -> s -> ... are walks of one more link through a
+// transit node), so lvl(n, v) == lvl(s, v) - 1 is decided by the levels mod
+// 3.  Rows of 2 bits per node (level mod 3; 3 = unreached, which matches no
+// target) carry a neighbour's row in a quarter of the bytes; the source's
+// own byte row is still read for its distance row.  Lane layout as the byte
+// pass: four consecutive nodes, here one byte (node r in bits 2r, 2r+1).
+__device__ __forceinline__ uint32_t nl_trit_byte(__amdgpu_buffer_rsrc_t rt, uint32_t v0,
+                                                 uint32_t rowoff) {
+  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rt, (int)(v0 >> 2), (int)rowoff, 0);
+}
+
+// the source's targets (level - 1) mod 3 per field: 0 -> 2, 1 -> 0, 2 -> 1
+__device__ __forceinline__ uint32_t nl_trit_target(uint32_t y) {
+  const uint32_t lo = y & 0x55u, hi = (y >> 1) & 0x55u;
+  return (hi & ~lo) | ((~(lo | hi) & 0x55u) << 1);
+}
+
+// bit 2r: node v0 + r is reached from the source and is not the source
+__device__ __forceinline__ uint32_t nl_trit_live(uint32_t y, uint32_t s, uint32_t v0) {
+  const uint32_t r = s - v0;
+  return ~(y & (y >> 1)) & 0x55u & (r < 4u ? ~(1u << (2u * r)) : 0xFFu);
+}
+
+// byte r = 1 where neighbour byte nb's field r equals the target field
+// (z's bits 2r moved to bit 8r: z * (1 + 2^6 + 2^12 + 2^18), whose carries
+// land only on bits 7, 13 and 19, cleared by the mask)
+__device__ __forceinline__ uint32_t nl_trit_match(uint32_t nb, uint32_t t2, uint32_t live2) {
+  const uint32_t x = nb ^ t2;
+  const uint32_t z = live2 & ~(x | (x >> 1));
+  return __umul24(z, 0x41041u) & 0x01010101u;
+}
+
+__device__ __forceinline__ void nl_t_ld8(__amdgpu_buffer_rsrc_t rt, uint32_t v0, uint32_t tstride,
+                                         nl_cptr<NlEnt> e, uint32_t rem, uint32_t (&lf)[8]) {
+  uint32_t r[8];
+#pragma unroll
+  for (uint32_t kk = 0; kk < 8; ++kk) {
+    r[kk] = __builtin_amdgcn_readfirstlane(e[kk].row);
+  }
+#pragma unroll
+  for (uint32_t kk = 0; kk < 8; ++kk) {
+    lf[kk] = 0xFFu;
+    if (kk < rem) {
+      lf[kk] = nl_trit_byte(rt, v0, r[kk] * tstride);
+    }
+  }
+}
+
+// nl_v3_cmp8 over 2-bit rows: same P layout (bit kk of byte r)
+__device__ __forceinline__ uint32_t nl_t_cmp8(const uint32_t (&lf)[8], uint32_t t2, uint32_t live2,
+                                              uint32_t ntg, nl_cptr<NlEnt> e, uint32_t v0) {
+  uint32_t P = 0;
+#pragma unroll
+  for (uint32_t kk = 0; kk < 8; ++kk) {
+    uint32_t m = nl_trit_match(lf[kk], t2, live2);
+    if ((ntg >> kk) & 1u) {
+      const uint32_t r = __builtin_amdgcn_readfirstlane(e[kk].node) - v0;
+      m &= r < 4u ? (1u << (8u * r)) : 0u;
+    }
+    P |= m << kk;
+  }
+  return P;
+}
+
+// Level rows -> 2-bit rows: one thread per 16 nodes of a row (a 16-byte
+// load, a 4-byte store); rows [0, nrows), stride Vp8 bytes in, Vp8 / 4 out.
+// Skipped after a BFS deeper than 254 levels (flags[0]: the byte kernels
+// then run without the v2 pass)
+struct LvlTritArgs {
+  const uint8_t* lvl;
+  uint8_t* trit;
+  const uint32_t* flags;
+  uint32_t Vp8, nrows, per_row; // per_row = Vp8 / 16 threads
+};
+
+__global__ __launch_bounds__(256) void spf_lvl_trit_kernel(LvlTritArgs a) {
+  if (a.flags && a.flags[0] != 0) {
+    return;
+  }
+  const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint32_t r = (uint32_t)(t / a.per_row), c = (uint32_t)(t - (uint64_t)r * a.per_row);
+  if (r >= a.nrows) {
+    return;
+  }
+  const uint4 w = *reinterpret_cast<const uint4*>(a.lvl + (size_t)r * a.Vp8 + 16u * c);
+  const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+  uint32_t out = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 16; ++k) {
+    const uint32_t b = (ws[k >> 2] >> (8u * (k & 3u))) & 0xFFu;
+    // b mod 3 = b - 3 floor(b / 3), floor(b / 3) = (171 b) >> 9 for b < 256
+    const uint32_t m3 = b - 3u * (__umul24(b, 171u) >> 9);
+    out |= (b == 255u ? 3u : m3) << (2u * k);
+  }
+  *reinterpret_cast<uint32_t*>(a.trit + (size_t)r * (a.Vp8 / 4) + 4u * c) = out;
+}
+
 // Mask rows of B = 8 * Wm bytes per node, one wave's 256 nodes: a lane holds
 // 4 consecutive nodes (32 * Wm contiguous bytes), so storing from registers
 // puts 16-byte pieces 32 * Wm bytes apart in every wave instruction (partial
@@ -4208,10 +4317,10 @@ __device__ __forceinline__ void nl_store_wide(uint8_t* row, uint32_t vbase, uint
   }
 }
 
-template <uint32_t T>
+template <uint32_t T, bool TRIT>
 __device__ __forceinline__ void nl_v2_solo(const NhLevelsArgs& a, const NlV2Args& v,
                                            uint32_t k, uint32_t c, uint64_t* tile,
-                                           __amdgpu_buffer_rsrc_t rs) {
+                                           __amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rt) {
   const nl_cptr<NlSolo> dp = nl_const(v.solo) + k;
   const NlSolo d{dp->q, dp->n, dp->lo, dp->B, dp->nhb_off, dp->Wm, 0u};
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -4274,6 +4383,12 @@ __device__ __forceinline__ void nl_v2_solo(const NhLevelsArgs& a, const NlV2Args
   const uint32_t ls = active ? nl_lvl_word(rs, v0, d.q * a.Vp8) : 0xFFFFFFFFu;
   const uint32_t tgt = ((ls | 0x80808080u) - 0x01010101u) ^ (~ls & 0x80808080u);
   const uint32_t live = 0x80808080u & ~(swar_zero_bytes(ls) | swar_zero_bytes(~ls));
+  uint32_t t2 = 0, live2 = 0;
+  if constexpr (TRIT) {
+    const uint32_t ys = active ? nl_trit_byte(rt, v0, d.q * v.tstride) : 0xFFu;
+    t2 = nl_trit_target(ys);
+    live2 = nl_trit_live(ys, nl_const(a.src)[d.q], v0);
+  }
   uint64_t held[kNsHeldMax][4];
 #pragma unroll 1
   for (uint32_t w = 0; w < d.Wm; ++w) {
@@ -4282,7 +4397,14 @@ __device__ __forceinline__ void nl_v2_solo(const NhLevelsArgs& a, const NlV2Args
     const nl_cptr<NlEnt> ew = ent + 64 * w;
     uint32_t P[8];
     uint32_t A[8], Bq[8];
-    nl_v3_ld8(rs, v0, a.Vp8, ew, cnt, A);
+    auto ld8 = [&](nl_cptr<NlEnt> e8, uint32_t rem, uint32_t(&lf)[8]) {
+      if constexpr (TRIT) {
+        nl_t_ld8(rt, v0, v.tstride, e8, rem, lf);
+      } else {
+        nl_v3_ld8(rs, v0, a.Vp8, e8, rem, lf);
+      }
+    };
+    ld8(ew, cnt, A);
 #pragma unroll
     for (uint32_t g = 0; g < 8; ++g) {
       P[g] = 0;
@@ -4290,13 +4412,17 @@ __device__ __forceinline__ void nl_v2_solo(const NhLevelsArgs& a, const NlV2Args
         // the next group's loads go out before this group's compares
         if (g + 1 < 8 && 8 * (g + 1) < cnt) {
           if (g & 1u) {
-            nl_v3_ld8(rs, v0, a.Vp8, ew + 8 * (g + 1), cnt - 8 * (g + 1), A);
+            ld8(ew + 8 * (g + 1), cnt - 8 * (g + 1), A);
           } else {
-            nl_v3_ld8(rs, v0, a.Vp8, ew + 8 * (g + 1), cnt - 8 * (g + 1), Bq);
+            ld8(ew + 8 * (g + 1), cnt - 8 * (g + 1), Bq);
           }
         }
         const uint32_t ntg = (uint32_t)(ntmask >> (8 * g)) & 0xFFu;
-        P[g] = nl_v3_cmp8((g & 1u) ? Bq : A, tgt, live, ntg, ew + 8 * g, v0);
+        if constexpr (TRIT) {
+          P[g] = nl_t_cmp8((g & 1u) ? Bq : A, t2, live2, ntg, ew + 8 * g, v0);
+        } else {
+          P[g] = nl_v3_cmp8((g & 1u) ? Bq : A, tgt, live, ntg, ew + 8 * g, v0);
+        }
       }
     }
     uint32_t lo[4], hi[4];
@@ -4373,10 +4499,10 @@ __device__ __forceinline__ void nl_v2_solo(const NhLevelsArgs& a, const NlV2Args
   }
 }
 
-template <uint32_t T>
+template <uint32_t T, bool TRIT>
 __device__ __forceinline__ void nl_v2_group(const NhLevelsArgs& a, const NlV2Args& v,
                                             uint32_t k, uint32_t c,
-                                            __amdgpu_buffer_rsrc_t rs) {
+                                            __amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rt) {
   const nl_cptr<NlSub> dp = nl_const(v.subs) + k;
   const NlSub d{dp->m0, dp->cnt, dp->n, dp->lo, dp->B, 0u};
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -4425,14 +4551,19 @@ __device__ __forceinline__ void nl_v2_group(const NhLevelsArgs& a, const NlV2Arg
     }
 #pragma unroll
     for (uint32_t j = 0; j < kNlGN; ++j) {
-      lf[j] = 0xFFFFFFFFu;
+      lf[j] = TRIT ? 0xFFu : 0xFFFFFFFFu;
       if (j < d.n) {
-        lf[j] = nl_lvl_word(rs, v0, r[j] * a.Vp8);
+        if constexpr (TRIT) {
+          lf[j] = nl_trit_byte(rt, v0, r[j] * v.tstride);
+        } else {
+          lf[j] = nl_lvl_word(rs, v0, r[j] * a.Vp8);
+        }
       }
     }
   }
   uint32_t qs[kNlGS];
   uint32_t ls[kNlGS];
+  uint32_t ys[kNlGS]; // TRIT: the members' own 2-bit words
 #pragma unroll
   for (uint32_t i = 0; i < kNlGS; ++i) {
     qs[i] = __builtin_amdgcn_readfirstlane(mem[i].q); // past cnt: padding, unused
@@ -4440,8 +4571,12 @@ __device__ __forceinline__ void nl_v2_group(const NhLevelsArgs& a, const NlV2Arg
 #pragma unroll
   for (uint32_t i = 0; i < kNlGS; ++i) {
     ls[i] = 0xFFFFFFFFu;
+    ys[i] = 0xFFu;
     if (i < d.cnt) {
       ls[i] = nl_lvl_word(rs, v0, qs[i] * a.Vp8);
+      if constexpr (TRIT) {
+        ys[i] = nl_trit_byte(rt, v0, qs[i] * v.tstride);
+      }
     }
   }
   // per neighbour: the byte lanes a match may set (a drained neighbour only
@@ -4452,7 +4587,7 @@ __device__ __forceinline__ void nl_v2_group(const NhLevelsArgs& a, const NlV2Arg
     allow[j] = 0xFFFFFFFFu;
     if ((ntmask >> j) & 1u) {
       const uint32_t r = __builtin_amdgcn_readfirstlane(ent[j].node) - v0;
-      allow[j] = r < 4u ? (0x80u << (8u * r)) : 0u;
+      allow[j] = r < 4u ? ((TRIT ? 0x01u : 0x80u) << (8u * r)) : 0u;
     }
   }
   if (!active) {
@@ -4462,17 +4597,33 @@ __device__ __forceinline__ void nl_v2_group(const NhLevelsArgs& a, const NlV2Arg
   for (uint32_t i = 0; i < kNlGS; ++i) {
     if (i < d.cnt) {
       const uint32_t x = ls[i];
-      const uint32_t tgt = ((x | 0x80808080u) - 0x01010101u) ^ (~x & 0x80808080u);
-      const uint32_t live = 0x80808080u & ~(swar_zero_bytes(x) | swar_zero_bytes(~x));
       uint32_t P0 = 0, P1 = 0;
+      if constexpr (TRIT) {
+        const uint32_t t2 = nl_trit_target(ys[i]);
+        const uint32_t live2 = nl_trit_live(ys[i], nl_const(a.src)[qs[i]], v0);
 #pragma unroll
-      for (uint32_t j = 0; j < kNlGN; ++j) {
-        if (j < d.n) {
-          const uint32_t m = live & allow[j] & swar_zero_bytes(lf[j] ^ tgt);
-          if (j < 8) {
-            P0 |= m >> (7u - j);
-          } else {
-            P1 |= m >> (15u - j);
+        for (uint32_t j = 0; j < kNlGN; ++j) {
+          if (j < d.n) {
+            const uint32_t m = allow[j] & nl_trit_match(lf[j], t2, live2);
+            if (j < 8) {
+              P0 |= m << j;
+            } else {
+              P1 |= m << (j - 8u);
+            }
+          }
+        }
+      } else {
+        const uint32_t tgt = ((x | 0x80808080u) - 0x01010101u) ^ (~x & 0x80808080u);
+        const uint32_t live = 0x80808080u & ~(swar_zero_bytes(x) | swar_zero_bytes(~x));
+#pragma unroll
+        for (uint32_t j = 0; j < kNlGN; ++j) {
+          if (j < d.n) {
+            const uint32_t m = live & allow[j] & swar_zero_bytes(lf[j] ^ tgt);
+            if (j < 8) {
+              P0 |= m >> (7u - j);
+            } else {
+              P1 |= m >> (15u - j);
+            }
           }
         }
       }
@@ -4520,6 +4671,39 @@ __global__ __launch_bounds__(T) void spf_nh_levels_v2_kernel(NhLevelsArgs a, NlV
   }
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.lvl, (short)0, (int)v.lvl_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rt =
+      __builtin_amdgcn_make_buffer_rsrc((void*)v.trit, (short)0, (int)v.trit_bytes, 0x00020000);
+  // 2-bit neighbour rows for items whose sources are all transit (read at
+  // run time: spf_graph_set_transit patches the bits between runs)
+  const nl_cptr<uint32_t> tr = nl_const(a.trbits);
+  const nl_cptr<uint32_t> srcs = nl_const(a.src);
+  auto transit = [&](uint32_t q) {
+    const uint32_t f = srcs[q];
+    return ((tr[f >> 5] >> (f & 31u)) & 1u) != 0;
+  };
+  auto nl_v2_solo_t = [&](uint32_t k, uint32_t c) {
+    if (v.trit && transit(nl_const(v.solo)[k].q)) {
+      nl_v2_solo<T, true>(a, v, k, c, tile, rs, rt);
+    } else {
+      nl_v2_solo<T, false>(a, v, k, c, tile, rs, rt);
+    }
+  };
+  auto nl_v2_group_t = [&](uint32_t k, uint32_t c) {
+    bool all = v.trit != nullptr;
+    if (all) {
+      const nl_cptr<NlSub> dp = nl_const(v.subs) + k;
+      const uint32_t m0 = dp->m0, cnt = dp->cnt;
+      const nl_cptr<NlMem> mem = nl_const(v.mem) + m0;
+      for (uint32_t i = 0; i < cnt; ++i) {
+        all = all && transit(mem[i].q);
+      }
+    }
+    if (all) {
+      nl_v2_group<T, true>(a, v, k, c, rs, rt);
+    } else {
+      nl_v2_group<T, false>(a, v, k, c, rs, rt);
+    }
+  };
   if (v.order == 5) {
     const uint32_t e = v.xmap[blockIdx.x];
     if (e == kInf32) {
@@ -4527,9 +4711,9 @@ __global__ __launch_bounds__(T) void spf_nh_levels_v2_kernel(NhLevelsArgs a, NlV
     }
     const uint32_t k = e >> 12, c = e & 0xFFFu;
     if (k < v.nsolo) {
-      nl_v2_solo<T>(a, v, k, c, tile, rs);
+      nl_v2_solo_t(k, c);
     } else {
-      nl_v2_group<T>(a, v, k - v.nsolo, c, rs);
+      nl_v2_group_t(k - v.nsolo, c);
     }
     return;
   }
@@ -4550,10 +4734,10 @@ __global__ __launch_bounds__(T) void spf_nh_levels_v2_kernel(NhLevelsArgs a, NlV
     }
     if (k < v.nsolo) {
       if (!(v.dbg & 1u)) {
-        nl_v2_solo<T>(a, v, k, c, tile, rs);
+        nl_v2_solo_t(k, c);
       }
     } else if (!(v.dbg & 2u)) {
-      nl_v2_group<T>(a, v, k - v.nsolo, c, rs);
+      nl_v2_group_t(k - v.nsolo, c);
     }
     return;
   }
@@ -4564,13 +4748,13 @@ __global__ __launch_bounds__(T) void spf_nh_levels_v2_kernel(NhLevelsArgs a, NlV
       return;
     }
     const uint32_t c = bid / v.nsolo;
-    nl_v2_solo<T>(a, v, bid - c * v.nsolo, c, tile, rs);
+    nl_v2_solo_t(bid - c * v.nsolo, c);
   } else {
     if (v.dbg & 2u) {
       return;
     }
     const uint32_t b2 = bid - ns, c = b2 / v.nsub;
-    nl_v2_group<T>(a, v, b2 - c * v.nsub, c, rs);
+    nl_v2_group_t(b2 - c * v.nsub, c);
   }
 }
 
@@ -7643,6 +7827,11 @@ struct spf_graph {
   std::vector<uint32_t> col_orig;
   std::vector<uint8_t> edge_up;
   bool links_patched = false;
+  // every up half-edge's reverse is up (false only after spf_graph_set_edges
+  // took one half of a link down): kernels that read a node's out-edges as
+  // its in-edges (the what-if source-link kernels, the v2 pass's 2-bit rows)
+  // need it
+  bool paired = true;
   size_t nbr_cap = 0; // entries of d_nbrs / d_nbr_w (set_edges re-sizes them)
   // allocated entries of the edge-sized device arrays (d_col, d_link, d_rev,
   // d_slot; d_wout, d_win, d_w64; d_cw) and of d_link_half: spf_graph_update
@@ -7771,6 +7960,8 @@ struct spf_query {
   // descriptors, members and neighbour entries in one pooled block, valid
   // while the graph's neighbour lists are those of nbr_gen
   void* d_v2 = nullptr;
+  // 2-bit level rows of the v2 pass (spf_lvl_trit_kernel), nullptr = off
+  uint8_t* d_trit = nullptr;
   NlV2Args v2{};
   bool has_v2 = false;
   uint64_t v2_gen = 0;
@@ -8136,8 +8327,45 @@ int build_nl_v2(spf_query* q, const uint32_t* sources, const std::vector<int32_t
   q->v2.order = vorder == 5 && xmap.empty() ? 4u : vorder;
   q->v2.xmap = reinterpret_cast<const uint32_t*>(b + o_map);
   q->v2.nmap = (uint32_t)xmap.size();
+  // 2-bit neighbour rows (OPENR_NL_TRIT, default on): exact when every
+  // half-edge is paired with an up reverse (uniform metric is the plan's
+  // own condition), checked here since spf_graph_set_edges bumps nbr_gen and
+  // retires these tables; the per-item transit test runs in the kernel
+  const bool paired = g->paired;
+  const uint64_t trit_bytes = (uint64_t)q->nrows * (q->Vp8 / 4);
+  if (paired && env_flag("OPENR_NL_TRIT", 1) && trit_bytes < 0x80000000ull) {
+    if (pool_malloc((void**)&q->d_trit, trit_bytes) != hipSuccess) {
+      return fail(SPF_E_NOMEM, "2-bit level rows");
+    }
+    q->v2.trit = q->d_trit;
+    q->v2.trit_bytes = (uint32_t)trit_bytes;
+    q->v2.tstride = q->Vp8 / 4;
+  }
   q->has_v2 = true;
   q->v2_gen = g->nbr_gen;
+  return SPF_OK;
+}
+
+// the 2-bit rows of every level row, before the v2 pass reads them
+int launch_lvl_trits(spf_query* q) {
+  spf_graph* g = q->g;
+  if (!q->d_trit || !q->has_v2 || q->v2_gen != g->nbr_gen) {
+    return SPF_OK;
+  }
+  LvlTritArgs t{};
+  t.lvl = q->d_lvl;
+  t.trit = q->d_trit;
+  t.flags = q->d_flags ? q->d_flags + q->ms_par : nullptr;
+  t.Vp8 = q->Vp8;
+  t.nrows = q->nrows;
+  t.per_row = q->Vp8 / 16;
+  const uint64_t threads = (uint64_t)t.nrows * t.per_row;
+  const uint64_t blocks = (threads + 255) / 256;
+  if (blocks > 0x7FFFFFFFull) {
+    return fail(SPF_E_UNSUPPORTED, "batch too large for the 2-bit level rows");
+  }
+  SPF_LAUNCH(spf_lvl_trit_kernel, dim3((uint32_t)blocks), dim3(256), 0, g->stream, t);
+  HIP_TRY(hipGetLastError());
   return SPF_OK;
 }
 
@@ -8457,7 +8685,14 @@ void free_query(spf_query* q) {
     return;
   }
   (void)hipSetDevice(q->g->device);
-  // the buffers go back to the pool: nothing queued may still use them
+  // the buffers go back to the pool: nothing queued may still use them --
+  // including the what-if source-link kernel on the query's own stream,
+  // which the graph stream joins only once the rest of the plan launched
+  // (an error return after that kernel leaves wh_pending set)
+  if (q->wh_stream) {
+    (void)hipStreamSynchronize(q->wh_stream);
+    q->wh_pending = false;
+  }
   (void)hipStreamSynchronize(q->g->stream);
   // d_src, d_ign_off, d_ign, d_nh_off, d_nh_w, d_row_of live in d_pack
   for (void* p :
@@ -8469,6 +8704,7 @@ void free_query(spf_query* q) {
         (void*)q->d_trace, (void*)q->d_big, (void*)q->d_held_order, (void*)q->d_zl,
         (void*)q->d_zvar, (void*)q->d_ms_mask, (void*)q->d_ms_flag,
         (void*)q->d_ovf, q->narrow ? (void*)q->d_nhb : nullptr, (void*)q->d_tcs, q->d_v2,
+        (void*)q->d_trit,
         q->d_coop, (void*)q->d_wh_cand, (void*)q->d_wh_mark, (void*)q->d_wh_lstart}) {
     pool_free(p);
   }
@@ -8681,6 +8917,26 @@ void refresh_exact(spf_graph* g) {
 }
 
 // fast-path weights, exactness, uniformity and per-neighbour cheapest metric
+// lanes per node of the frontier kernels (a.G): the median degree, rounded
+// to a power of two in [4, 64]; spf_graph_create and spf_graph_update
+void set_lanes_per_node(spf_graph* g) {
+  const uint32_t V = g->V;
+  std::vector<uint32_t> deg(V);
+  for (uint32_t u = 0; u < V; ++u) {
+    deg[u] = g->row[u + 1] - g->row[u];
+  }
+  uint32_t med = 4;
+  if (V) {
+    std::nth_element(deg.begin(), deg.begin() + V / 2, deg.end());
+    med = deg[V / 2];
+  }
+  uint32_t G = 4;
+  while (G < med && G < 64) {
+    G <<= 1;
+  }
+  g->G = G;
+}
+
 int upload_weights(spf_graph* g) {
   const uint32_t E = g->E, V = g->V;
   const unsigned nth = openr::hostThreads(E, kHostMinEdges);
@@ -8783,6 +9039,8 @@ int upload_weights(spf_graph* g) {
     if (!g->d_cw || e4 > g->cap_cw) {
       if (g->d_cw) {
         (void)hipFree(g->d_cw);
+        g->d_cw = nullptr;
+        g->cap_cw = 0;
       }
       const size_t c = (e4 + e4 / 8 + 3) & ~(size_t)3;
       HIP_TRY(hipMalloc((void**)&g->d_cw, c * 4));
@@ -8792,11 +9050,20 @@ int upload_weights(spf_graph* g) {
   }
   if (E) {
     if (!g->d_wout || E > g->cap_w) {
-      for (void* p : {(void*)g->d_wout, (void*)g->d_win, (void*)g->d_w64}) {
-        if (p) {
-          (void)hipFree(p);
+      // freed pointers are cleared at once and the capacity is 0 until all
+      // three allocations succeed, so a failed allocation on a live graph
+      // (spf_graph_update) leaves nothing that free_graph would free twice
+      for (uint32_t** p : {&g->d_wout, &g->d_win}) {
+        if (*p) {
+          (void)hipFree(*p);
+          *p = nullptr;
         }
       }
+      if (g->d_w64) {
+        (void)hipFree(g->d_w64);
+        g->d_w64 = nullptr;
+      }
+      g->cap_w = 0;
       const size_t c = (size_t)E + E / 8; // headroom for in-place rebuilds
       HIP_TRY(hipMalloc((void**)&g->d_wout, c * 4));
       HIP_TRY(hipMalloc((void**)&g->d_win, c * 4));
@@ -9341,23 +9608,7 @@ int spf_graph_create(const spf_graph_desc* desc, spf_graph** out) {
   // distinct neighbours per node (ascending id = name order) and edge slots
   build_nbr_lists(g);
   mark("nbr lists");
-  // lanes per node: the median degree, rounded to a power of two in [4, 64]
-  {
-    std::vector<uint32_t> deg(V);
-    for (uint32_t u = 0; u < V; ++u) {
-      deg[u] = g->row[u + 1] - g->row[u];
-    }
-    uint32_t med = 4;
-    if (V) {
-      std::nth_element(deg.begin(), deg.begin() + V / 2, deg.end());
-      med = deg[V / 2];
-    }
-    uint32_t G = 4;
-    while (G < med && G < 64) {
-      G <<= 1;
-    }
-    g->G = G;
-  }
+  set_lanes_per_node(g);
 
   auto bail = [&](int s) {
     free_graph(g);
@@ -9473,9 +9724,11 @@ int spf_graph_update(spf_graph* g, const spf_graph_desc* desc) {
   g->col_orig.clear();
   g->edge_up.clear();
   g->links_patched = false;
+  g->paired = true;
   mark("host copy");
   NbrReuse nr{&g->old_row, &g->old_col, &g->old_nbr_off, &g->old_nbrs, &g->old_slot};
   build_nbr_lists(g, reuse && g->old_row.size() == (size_t)V + 1 ? &nr : nullptr);
+  set_lanes_per_node(g); // as spf_graph_create (it drifted after flaps)
   mark("nbr lists");
   // edge-sized arrays: rewritten in place, or reallocated with headroom
   auto fit32 = [&](uint32_t** d, size_t n, size_t& cap) -> int {
@@ -9716,6 +9969,10 @@ int spf_graph_set_edges(
   rescan_scalars(g);
   g->ecc_est = 0;
   g->links_patched = true;
+  g->paired = true;
+  for (uint32_t e = 0; e < g->E && g->paired; ++e) {
+    g->paired = g->edge_up[e] == g->edge_up[g->rev[e]];
+  }
   // distinct-neighbour lists over the up half-edges (a neighbour whose every
   // link went down leaves its source's list; one coming back re-enters it),
   // edge slots and cheapest metric per neighbour, so next-hop queries stay
@@ -10552,9 +10809,11 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
         }
         // queries whose failed link leaves the source: their own BFS launch
         // on a uniform-metric area (spf_whatif_heavy_kernel)
+        // (both kernels read v's out-edges as its in-edges: every half-edge
+        // paired with an up reverse)
         const bool uni = (desc->flags & SPF_F_UNIT_METRIC) || g->uniform;
         const size_t wh_lds = (3 * (size_t)g->V + 1 + (g->V + 31) / 32) * 4;
-        if (uni && wh_lds <= kLdsLimit && desc->ignore_offsets &&
+        if (uni && g->paired && wh_lds <= kLdsLimit && desc->ignore_offsets &&
             env_flag("OPENR_SPF_WHATIF_HEAVY", 1)) {
           for (uint32_t i = 0; i < nq; ++i) {
             const uint32_t s0 = desc->sources[i];
@@ -11401,6 +11660,12 @@ int finish_zero_plan(spf_query* q) {
 int run_screen(spf_query* q) {
   spf_query* b = q->base;
   spf_graph* g = q->g;
+  if (!q->wh_cand.empty() && !g->paired) {
+    // the source-link kernels were chosen for a graph whose half-edges were
+    // paired; spf_graph_set_edges has since taken one half of a link down
+    return fail(SPF_E_UNSUPPORTED,
+                "what-if query: a half-edge went down alone since creation (recreate the query)");
+  }
   int s = run_plan(b);
   if (s != SPF_OK) {
     return s;
@@ -11578,6 +11843,10 @@ int run_plan_kernels(spf_query* q) {
     return launch_msdstep(q);
   case DistPlan::MsBfs: {
     int s = launch_msbfs(q, unit);
+    if (s == SPF_OK && q->nh == NhPlan::Levels && q->d_trit) {
+      // part of the distance stage: the level rows' 2-bit copies
+      s = launch_lvl_trits(q);
+    }
     if (s == SPF_OK && q->nh == NhPlan::Levels) {
       s = mark_stage(q);
       if (s == SPF_OK) {

@@ -15,7 +15,12 @@ reference-style restatement of SpfSolverImpl::buildRouteDb, Decision.cpp:
                            (bench.py _rebuild_loop picks rsw[(it * 7919) %
                            n] for it = 0..7); digest + delta vs base
   sp_ecmp_lfa/base         LFA on (computeLfaPaths, Decision.cpp:1146-1175);
-                           full hashes
+                           full hashes -- the Decision DecisionBenchmark
+                           actually runs (DecisionBenchmark.cpp:74-79)
+  sp_ecmp_lfa/overload:<rsw>  LFA on after each of the bench's RSW overload
+                           toggles; digest + delta vs base (`--lfa-states`
+                           adds these to an existing file without rebuilding
+                           the other sections)
   nodes/<name>             SP_ECMP base RouteDb of the other nodes the bench's
                            all-nodes table checks; digest + route counts
   ksp2/base                every prefix SR_MPLS / KSP2_ED_ECMP: the k = 1 and
@@ -81,7 +86,35 @@ def _job(args):
     return args, h, time.time() - t0
 
 
+def lfa_states():
+    """Add sp_ecmp_lfa/overload:<rsw> for every toggle of the bench loop to
+    the committed file (the other sections are left as they are)."""
+    from oracle import build as OB
+
+    OB.build()
+    from openr_amd import topologies as TP
+    from tests.golden import routes as R
+
+    topo = TP.fabric(10000)
+    gold = R.load(OUT)
+    base = gold["sp_ecmp_lfa"]["base"]["hashes"]
+    toggles = sorted(set(rsw_sequence(topo)))
+    jobs = [("sp_ecmp_lfa", t, NODE, True, 0, 1) for t in toggles]
+    t0 = time.time()
+    with mp.get_context("spawn").Pool(min(8, os.cpu_count() or 1)) as pool:
+        for args, h, dt in pool.imap_unordered(_job, jobs):
+            ov = args[1]
+            gold["sp_ecmp_lfa"][f"overload:{topo.names[ov]}"] = {
+                "digest": R.digest(h), "num_unicast": len(h["unicast"]), "num_mpls": len(h["mpls"]),
+                "delta_vs_base": R.delta(h, base)}
+            print(f"[{time.time() - t0:7.1f}s] sp_ecmp_lfa overload={topo.names[ov]} {dt:.1f}s", flush=True)
+    R.save(OUT, gold)
+    print(f"wrote {OUT} ({os.path.getsize(OUT)} bytes) in {time.time() - t0:.0f}s")
+
+
 def main():
+    if "--lfa-states" in sys.argv:
+        return lfa_states()
     from oracle import build as OB
 
     OB.build()
@@ -95,6 +128,7 @@ def main():
     nk = 32  # KSP2 slices per state
     jobs = [("sp_ecmp", None, NODE, False, 0, 1), ("sp_ecmp_lfa", None, NODE, True, 0, 1)]
     jobs += [("sp_ecmp", t, NODE, False, 0, 1) for t in sorted(set(toggles))]
+    jobs += [("sp_ecmp_lfa", t, NODE, True, 0, 1) for t in sorted(set(toggles))]
     jobs += [("nodes", None, n, False, 0, 1) for n in other_nodes]
     jobs += [("ksp2", ov, NODE, False, c, nk) for ov in (None, toggles[0]) for c in range(nk)]
     t0 = time.time()

@@ -6,7 +6,8 @@ fabric_full(10000) equals, route by route, the CPU oracle's
   * every prefix IP / SP_ECMP, LFA off -- the base state and every RSW
     overload state of the bench's rebuild loop (DecisionBenchmark.cpp:
     600-626), reached by toggling on ONE LinkState the way the loop does;
-  * LFA on (Decision.cpp:1146-1175);
+  * LFA on (Decision.cpp:1146-1175), the base and every overload state of
+    the same loop (DecisionBenchmark's Decision computes LFAs);
   * every prefix SR_MPLS / KSP2_ED_ECMP: k = 1 and k = 2 edge-disjoint paths
     to all 9,975 destinations (LinkState.cpp:760-789, selectKsp2
     Decision.cpp:909-1066), base and first overload toggle;
@@ -89,10 +90,18 @@ def test_fabric_sp_ecmp_route_db_every_loop_state(gpu_ready, gold):
 
 
 @pytest.mark.gpu
-def test_fabric_sp_ecmp_lfa_route_db(gpu_ready, gold):
+@pytest.mark.parametrize("fast", ["1", "0"])
+def test_fabric_sp_ecmp_lfa_route_db_every_loop_state(gpu_ready, gold, monkeypatch, fast):
+    """LFA on, as DecisionBenchmark's Decision (DecisionBenchmark.cpp:74-79):
+    the base state and every RSW overload state of the bench's loop, with
+    the LFA fast path (FastEcmp, default) and with the general path
+    (OPENR_ECMP_FAST=0; read per build)."""
     import openr_amd._openr_spf as E
 
-    _walk_states(E, gold, "sp_ecmp_lfa", (0, 0), True, ["base"])
+    monkeypatch.setenv("OPENR_ECMP_FAST", fast)
+    names = ["base"] + [k for k in gold["sp_ecmp_lfa"] if k != "base"] + ["base"]
+    assert len(names) > 3, "golden lacks the LFA overload states (make_routedb_golden.py --lfa-states)"
+    _walk_states(E, gold, "sp_ecmp_lfa", (0, 0), True, names)
 
 
 @pytest.mark.gpu

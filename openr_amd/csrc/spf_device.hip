@@ -2651,6 +2651,7 @@ __global__ __launch_bounds__(kNhThreads) void spf_nh_rows_kernel(NhRowsArgs a) {
 #define OPENR_MS_UNROLL8 1
 #endif
 constexpr uint32_t kMsThreads = 1024;
+constexpr uint32_t kMsShallowLevel = 127;
 constexpr uint32_t kMsMaxK = 20; // nodes per thread -> V <= 20480 (32-bit batches above 10,240 nodes: the
                                  // double buffer is 2 * V * 4 B <= 160 KB of LDS)
 
@@ -2668,7 +2669,10 @@ struct MsBfsArgs {
   const uint32_t* src;
   uint32_t* dist_out; // [nq][Vp]
   uint8_t* lvl_out;   // [nq][Vp8]
-  uint32_t* flags;    // [0] |= 1 when a level >= 255 occurred
+  // [0] |= 1 when a level >= 255 occurred (32-bit rows: the byte passes
+  // step aside), |= 2 when a level >= kMsShallowLevel did (the v2 pass's
+  // one-add byte compare needs every level below it)
+  uint32_t* flags;
   // the other launch's flag word, zeroed by block 0 (flags alternate between
   // two words per launch, so no per-run memset: stream order guarantees the
   // last readers of this word, the previous run's next-hop pass, are done)
@@ -2739,8 +2743,8 @@ __device__ __forceinline__ void ms_record(
   }
   const uint32_t d = level * a.scale;
   const uint8_t l8 = level < 255 ? (uint8_t)level : (uint8_t)255;
-  if (level >= 255 && bits) {
-    atomicOr(a.flags, 1u);
+  if (level >= kMsShallowLevel && bits) {
+    atomicOr(a.flags, level >= 255 ? 3u : 2u);
   }
   const bool wd = !a.lvl_only || level >= 255;
   while (bits) {
@@ -2771,8 +2775,8 @@ __device__ __forceinline__ void ms_record_wave(
   }
   const uint32_t d = level * a.scale;
   const uint8_t l8 = level < 255 ? (uint8_t)level : (uint8_t)255;
-  if (level >= 255 && bits) {
-    atomicOr(a.flags, 1u);
+  if (level >= kMsShallowLevel && bits) {
+    atomicOr(a.flags, level >= 255 ? 3u : 2u);
   }
   while (w) {
     const uint32_t s = (uint32_t)__builtin_ctzll((unsigned long long)w);
@@ -3862,7 +3866,7 @@ void spf_nh_levels_swar_kernel(NhLevelsArgs a, const uint32_t* big, uint32_t nbi
   __shared__ uint32_t st_row[64];
   __shared__ uint32_t st_node[64];
   __shared__ uint32_t st_nt[2]; // non-transit neighbours of the staged word
-  const bool deep = a.flags[0] != 0; // uniform
+  const bool deep = (a.flags[0] & 1u) != 0; // uniform
   // sources with more than kNsHeldMax words (or every source of a deep BFS;
   // the held kernel takes the rest)
   for (uint32_t bi = blockIdx.x;; bi += gridDim.x) {
@@ -4035,7 +4039,7 @@ __global__ __launch_bounds__(T) void spf_nh_levels_held_kernel(
     c = it - q * a.held_nch;
   }
   const uint32_t Wm = a.nh_w[q];
-  if (a.flags[0] != 0 || Wm > H || (H > 3 && Wm <= 3)) {
+  if ((a.flags[0] & 1u) != 0 || Wm > H || (H > 3 && Wm <= 3)) {
     return;
   }
   const uint32_t s = a.src[q];
@@ -4107,11 +4111,14 @@ struct NlV2Args {
   // round 6: 2-bit level rows (spf_lvl_trit_kernel: level mod 3, 3 =
   // unreached; row stride tstride = Vp8 / 4 bytes).  An item whose sources
   // are all transit reads its NEIGHBOURS' rows in this form (a quarter of
-  // the bytes); nullptr = every item reads byte rows (OPENR_NL_TRIT=0, a
+  // the bytes); nullptr = every item reads byte rows (the default; opt-in with OPENR_NL_TRIT=1; a
   // graph whose half-edges are not all paired)
   const uint8_t* trit = nullptr;
   uint32_t trit_bytes = 0;
   uint32_t tstride = 0;
+  // round 6: 1 = the one-add compare when the BFS stayed below level 127
+  // (MsBfsArgs::flags bit 1 clear; OPENR_NL_SHALLOW=0 turns it off)
+  uint32_t shallow = 1;
 };
 constexpr uint32_t kNlGS = 8;  // sources per group block
 constexpr uint32_t kNlGN = 16; // neighbours of a group source (one mask word, B <= 2)
@@ -4179,6 +4186,43 @@ __device__ __forceinline__ uint32_t nl_v3_cmp8(const uint32_t (&lf)[8], uint32_t
     P = (P >> 1) | m; // neighbour kk's flag ends at bit kk after the eight steps
   }
   return P;
+}
+
+// Shallow compare (round 6): when every level of the batch is below
+// kMsShallowLevel, the levels and the targets are below 128 and unreached
+// is 255, so a byte of lf ^ tgt is zero iff its low seven bits are -- one
+// masked add per neighbour instead of the exact zero-byte test, and no
+// live / drained masks per neighbour: the NON-matches accumulate (bit kk of
+// byte r set: neighbour kk does not match node r) and the caller applies
+// the masks once per group.  A missing neighbour (0xFF bytes) never
+// matches: 0xFF ^ tgt keeps low bits for tgt < 127.
+__device__ __forceinline__ uint32_t nl_s_cmp8(const uint32_t (&lf)[8], uint32_t tgt) {
+  uint32_t Q = 0;
+#pragma unroll
+  for (uint32_t kk = 0; kk < 8; ++kk) {
+    const uint32_t t = ((lf[kk] ^ tgt) & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+    Q = (Q >> 1) | (t & 0x80808080u);
+  }
+  return Q;
+}
+
+// 0xFF in every byte whose 0x80 is set in `live`
+__device__ __forceinline__ uint32_t nl_live8(uint32_t live) {
+  const uint32_t x = live >> 7;
+  return (x << 8) - x;
+}
+
+// the bits drained neighbours may keep: neighbour kk (a bit of ntg) only at
+// its own node's byte (P layout: bit kk of byte r)
+__device__ __forceinline__ uint32_t nl_s_allow(uint32_t ntg, nl_cptr<NlEnt> e, uint32_t v0) {
+  uint32_t allow = 0xFFFFFFFFu;
+  for (uint32_t kk = 0; kk < 8; ++kk) {
+    if ((ntg >> kk) & 1u) {
+      const uint32_t r = __builtin_amdgcn_readfirstlane(e[kk].node) - v0;
+      allow &= ~(0x01010101u << kk) | (r < 4u ? 1u << (8u * r + kk) : 0u);
+    }
+  }
+  return allow;
 }
 
 // ---- 2-bit neighbour rows (round 6)
@@ -4261,7 +4305,7 @@ struct LvlTritArgs {
 };
 
 __global__ __launch_bounds__(256) void spf_lvl_trit_kernel(LvlTritArgs a) {
-  if (a.flags && a.flags[0] != 0) {
+  if (a.flags && (a.flags[0] & 1u) != 0) {
     return;
   }
   const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -4317,7 +4361,7 @@ __device__ __forceinline__ void nl_store_wide(uint8_t* row, uint32_t vbase, uint
   }
 }
 
-template <uint32_t T, bool TRIT>
+template <uint32_t T, bool TRIT, bool SH>
 __device__ __forceinline__ void nl_v2_solo(const NhLevelsArgs& a, const NlV2Args& v,
                                            uint32_t k, uint32_t c, uint64_t* tile,
                                            __amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rt) {
@@ -4334,6 +4378,22 @@ __device__ __forceinline__ void nl_v2_solo(const NhLevelsArgs& a, const NlV2Args
   const nl_cptr<NlEnt> ent = nl_const(v.ent + d.lo);
   if (v.dbg & 8u) {
     // measurement: the pass's stores alone (same addresses, no loads)
+    if (!(v.dbg & 32u) && d.B >= 8 && !(v.dbg & 64u)) {
+      // wide masks through the LDS tile, as the pass stores them (every lane)
+      uint64_t hx[kNsHeldMax][4];
+#pragma unroll
+      for (uint32_t w = 0; w < kNsHeldMax; ++w) {
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {
+          hx[w][i] = v0 + i + w;
+        }
+      }
+      nl_store_wide(a.nhb + d.nhb_off, vbase, a.V, d.Wm, hx, tile, lane);
+      if (active && a.dist_w && !(v.dbg & 16u)) {
+        nl_dist_from_levels(a, d.q, v0, 0x01010101u * (v0 & 7u));
+      }
+      return;
+    }
     if (!active) {
       return;
     }
@@ -4356,18 +4416,6 @@ __device__ __forceinline__ void nl_v2_solo(const NhLevelsArgs& a, const NlV2Args
         }
       }
     }
-    return;
-  }
-  if ((v.dbg & 8u) && !(v.dbg & 32u) && d.B >= 8 && !(v.dbg & 64u)) {
-    uint64_t hx[kNsHeldMax][4];
-#pragma unroll
-    for (uint32_t w = 0; w < kNsHeldMax; ++w) {
-#pragma unroll
-      for (uint32_t i = 0; i < 4; ++i) {
-        hx[w][i] = v0 + i + w;
-      }
-    }
-    nl_store_wide(a.nhb + d.nhb_off, vbase, a.V, d.Wm, hx, tile, lane);
     return;
   }
   // drained neighbours: lane j tests entry 64w + j (every lane takes part)
@@ -4420,6 +4468,9 @@ __device__ __forceinline__ void nl_v2_solo(const NhLevelsArgs& a, const NlV2Args
         const uint32_t ntg = (uint32_t)(ntmask >> (8 * g)) & 0xFFu;
         if constexpr (TRIT) {
           P[g] = nl_t_cmp8((g & 1u) ? Bq : A, t2, live2, ntg, ew + 8 * g, v0);
+        } else if constexpr (SH) {
+          const uint32_t Q = nl_s_cmp8((g & 1u) ? Bq : A, tgt);
+          P[g] = ~Q & nl_live8(live) & (ntg ? nl_s_allow(ntg, ew + 8 * g, v0) : 0xFFFFFFFFu);
         } else {
           P[g] = nl_v3_cmp8((g & 1u) ? Bq : A, tgt, live, ntg, ew + 8 * g, v0);
         }
@@ -4499,7 +4550,7 @@ __device__ __forceinline__ void nl_v2_solo(const NhLevelsArgs& a, const NlV2Args
   }
 }
 
-template <uint32_t T, bool TRIT>
+template <uint32_t T, bool TRIT, bool SH>
 __device__ __forceinline__ void nl_v2_group(const NhLevelsArgs& a, const NlV2Args& v,
                                             uint32_t k, uint32_t c,
                                             __amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rt) {
@@ -4590,6 +4641,14 @@ __device__ __forceinline__ void nl_v2_group(const NhLevelsArgs& a, const NlV2Arg
       allow[j] = r < 4u ? ((TRIT ? 0x01u : 0x80u) << (8u * r)) : 0u;
     }
   }
+  // SH: the drained neighbours' masks in the P layout, once for every member
+  uint32_t allow8[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+  if constexpr (SH) {
+    if (ntmask) {
+      allow8[0] = nl_s_allow((uint32_t)ntmask & 0xFFu, ent, v0);
+      allow8[1] = nl_s_allow((uint32_t)(ntmask >> 8) & 0xFFu, ent + 8, v0);
+    }
+  }
   if (!active) {
     return;
   }
@@ -4611,6 +4670,27 @@ __device__ __forceinline__ void nl_v2_group(const NhLevelsArgs& a, const NlV2Arg
               P1 |= m << (j - 8u);
             }
           }
+        }
+      } else if constexpr (SH) {
+        // one masked add per neighbour, masks once (nl_s_cmp8)
+        const uint32_t tgt = ((x | 0x80808080u) - 0x01010101u) ^ (~x & 0x80808080u);
+        const uint32_t live = 0x80808080u & ~(swar_zero_bytes(x) | swar_zero_bytes(~x));
+        const uint32_t l8 = nl_live8(live);
+        uint32_t Q0 = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+          const uint32_t t = ((lf[j] ^ tgt) & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+          Q0 = (Q0 >> 1) | (t & 0x80808080u);
+        }
+        P0 = ~Q0 & l8 & allow8[0];
+        if (d.n > 8) {
+          uint32_t Q1 = 0;
+#pragma unroll
+          for (uint32_t j = 8; j < kNlGN; ++j) {
+            const uint32_t t = ((lf[j] ^ tgt) & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+            Q1 = (Q1 >> 1) | (t & 0x80808080u);
+          }
+          P1 = ~Q1 & l8 & allow8[1];
         }
       } else {
         const uint32_t tgt = ((x | 0x80808080u) - 0x01010101u) ^ (~x & 0x80808080u);
@@ -4661,14 +4741,19 @@ __device__ __forceinline__ void nl_v2_group(const NhLevelsArgs& a, const NlV2Arg
 // heavy SSW / FSW sources of the fabric first); then the groups' (sub-group,
 // chunk) items.  A BFS deeper than 254 levels leaves everything to
 // spf_nh_levels_swar_kernel.
-template <uint32_t T>
+// TRITS: the instance with the 2-bit neighbour-row path compiled in
+// (OPENR_NL_TRIT=1); the default instance carries the byte path alone
+template <uint32_t T, bool TRITS>
 __global__ __launch_bounds__(T) void spf_nh_levels_v2_kernel(NhLevelsArgs a, NlV2Args v) {
   // per wave: the 256-node mask tile of a wide solo source (nl_store_wide)
   __shared__ uint64_t tiles[T / 64][256 * kNsHeldMax];
   uint64_t* tile = tiles[threadIdx.x >> 6];
-  if (a.flags[0] != 0) {
+  const uint32_t fl = a.flags[0];
+  if (fl & 1u) {
     return;
   }
+  // every level below kMsShallowLevel: the one-add compare (nl_s_cmp8)
+  const bool sh = v.shallow && !(fl & 2u);
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.lvl, (short)0, (int)v.lvl_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rt =
@@ -4677,19 +4762,27 @@ __global__ __launch_bounds__(T) void spf_nh_levels_v2_kernel(NhLevelsArgs a, NlV
   // run time: spf_graph_set_transit patches the bits between runs)
   const nl_cptr<uint32_t> tr = nl_const(a.trbits);
   const nl_cptr<uint32_t> srcs = nl_const(a.src);
-  auto transit = [&](uint32_t q) {
+  auto transit = [&](uint32_t q) __attribute__((always_inline)) {
     const uint32_t f = srcs[q];
     return ((tr[f >> 5] >> (f & 31u)) & 1u) != 0;
   };
-  auto nl_v2_solo_t = [&](uint32_t k, uint32_t c) {
-    if (v.trit && transit(nl_const(v.solo)[k].q)) {
-      nl_v2_solo<T, true>(a, v, k, c, tile, rs, rt);
+  // (always_inline: as out-of-line calls these took a 440-byte stack frame
+  // and 132 VGPRs in the TRITS instance)
+  auto nl_v2_solo_t = [&](uint32_t k, uint32_t c) __attribute__((always_inline)) {
+    if constexpr (TRITS) {
+      if (v.trit && transit(nl_const(v.solo)[k].q)) {
+        nl_v2_solo<T, true, false>(a, v, k, c, tile, rs, rt);
+        return;
+      }
+    }
+    if (sh) {
+      nl_v2_solo<T, false, true>(a, v, k, c, tile, rs, rt);
     } else {
-      nl_v2_solo<T, false>(a, v, k, c, tile, rs, rt);
+      nl_v2_solo<T, false, false>(a, v, k, c, tile, rs, rt);
     }
   };
-  auto nl_v2_group_t = [&](uint32_t k, uint32_t c) {
-    bool all = v.trit != nullptr;
+  auto nl_v2_group_t = [&](uint32_t k, uint32_t c) __attribute__((always_inline)) {
+    bool all = TRITS && v.trit != nullptr;
     if (all) {
       const nl_cptr<NlSub> dp = nl_const(v.subs) + k;
       const uint32_t m0 = dp->m0, cnt = dp->cnt;
@@ -4698,10 +4791,16 @@ __global__ __launch_bounds__(T) void spf_nh_levels_v2_kernel(NhLevelsArgs a, NlV
         all = all && transit(mem[i].q);
       }
     }
-    if (all) {
-      nl_v2_group<T, true>(a, v, k, c, rs, rt);
+    if constexpr (TRITS) {
+      if (all) {
+        nl_v2_group<T, true, false>(a, v, k, c, rs, rt);
+        return;
+      }
+    }
+    if (sh) {
+      nl_v2_group<T, false, true>(a, v, k, c, rs, rt);
     } else {
-      nl_v2_group<T, false>(a, v, k, c, rs, rt);
+      nl_v2_group<T, false, false>(a, v, k, c, rs, rt);
     }
   };
   if (v.order == 5) {
@@ -4926,7 +5025,7 @@ void spf_nh_levels_kernel(NhLevelsArgs a) {
   const uint32_t deg = a.nbr_off[s + 1] - a.nbr_off[s];
   const bool big = deg > kNlStage; // uniform per block
   const uint32_t wm = a.nh_w[q];
-  if (a.flags[0] != 0) {
+  if ((a.flags[0] & 1u) != 0) {
     if (big) {
       nl_body_multi_staged<true>(a, q, s, c0, c1, st_row, st_node);
     } else if (wm == 1) {
@@ -8322,18 +8421,22 @@ int build_nl_v2(spf_query* q, const uint32_t* sources, const std::vector<int32_t
   q->v2.nsub = (uint32_t)subs.size();
   q->v2.lvl_bytes = (uint32_t)lvl_bytes;
   q->v2.dbg = env_u32("OPENR_NL_V2_DBG", 0);
+  q->v2.shallow = env_flag("OPENR_NL_SHALLOW", 1) ? 1u : 0u;
   // item-major (4): measured fastest with the LDS-staged wide tiles
   // (profiles/r05k: 0.364 ms against 0.385-0.389 for the chunk-major orders)
   q->v2.order = vorder == 5 && xmap.empty() ? 4u : vorder;
   q->v2.xmap = reinterpret_cast<const uint32_t*>(b + o_map);
   q->v2.nmap = (uint32_t)xmap.size();
-  // 2-bit neighbour rows (OPENR_NL_TRIT, default on): exact when every
+  // 2-bit neighbour rows (OPENR_NL_TRIT=1, opt-in): exact when every
   // half-edge is paired with an up reverse (uniform metric is the plan's
   // own condition), checked here since spf_graph_set_edges bumps nbr_gen and
   // retires these tables; the per-item transit test runs in the kernel
   const bool paired = g->paired;
   const uint64_t trit_bytes = (uint64_t)q->nrows * (q->Vp8 / 4);
-  if (paired && env_flag("OPENR_NL_TRIT", 1) && trit_bytes < 0x80000000ull) {
+  // opt-in: same-process A/B on the fabric (profiles/r06c): v2 0.338 vs
+  // 0.322 ms per launch plus 0.028 ms for the pack kernel -- the pass is
+  // bound by its dependent load chains, not by the bytes the rows move
+  if (paired && env_flag("OPENR_NL_TRIT", 0) && trit_bytes < 0x80000000ull) {
     if (pool_malloc((void**)&q->d_trit, trit_bytes) != hipSuccess) {
       return fail(SPF_E_NOMEM, "2-bit level rows");
     }
@@ -11244,7 +11347,10 @@ int launch_nh_rows(spf_query* q, bool unit) {
 // writes them as 16-byte runs: fabric msbfs 0.228 -> 0.155 ms, next hops
 // 0.451 -> 0.499 ms, step 0.691 -> 0.666 ms (profiles/r03w)
 inline bool lvl_only(const spf_query* q) {
-  return q->nh == NhPlan::Levels && !q->zvars && env_flag("OPENR_NL_SWAR", 1) &&
+  // (the byte pass chosen when the query was created, q->nl_swar -- not the
+  // environment at run time, which could pair the BFS's skipped distance
+  // stores with a next-hop kernel that does not write them)
+  return q->nh == NhPlan::Levels && !q->zvars && q->nl_swar &&
          env_flag("OPENR_MS_LVL_ONLY", 1);
 }
 
@@ -11477,8 +11583,11 @@ int launch_nh_levels(spf_query* q, bool unit) {
       const uint64_t vblocks = q->v2.order == 5 ? (uint64_t)q->v2.nmap
                                                 : (uint64_t)(q->v2.nsolo + q->v2.nsub) *
                                                       ((g->V + 1023) / 1024);
-      if (vblocks) {
-        SPF_LAUNCH((spf_nh_levels_v2_kernel<256>), dim3((uint32_t)vblocks), dim3(256), 0,
+      if (vblocks && q->v2.trit) {
+        SPF_LAUNCH((spf_nh_levels_v2_kernel<256, true>), dim3((uint32_t)vblocks), dim3(256), 0,
+                           g->stream, a, q->v2);
+      } else if (vblocks) {
+        SPF_LAUNCH((spf_nh_levels_v2_kernel<256, false>), dim3((uint32_t)vblocks), dim3(256), 0,
                            g->stream, a, q->v2);
       }
     } else if (T == 1024) {

@@ -5,7 +5,7 @@ alternating timed blocks of each query; per-stage device times from the
 engine's HIP events (stage_history: msbfs stage incl. any pack kernel,
 next-hop stage = the v2 kernel).
 
-    python profiles/trit_ab.py [steps] [rounds] [ENV_NAME] > gpurun_out/ab.json
+    python profiles/nl_ab.py [steps] [rounds] [ENV_NAME] [MODE,MODE] > gpurun_out/ab.json
 """
 import json
 import os
@@ -23,6 +23,7 @@ from openr_amd import topologies as TP  # noqa: E402
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 env = sys.argv[3] if len(sys.argv) > 3 else "OPENR_NL_TRIT"
+modes = sys.argv[4].split(",") if len(sys.argv) > 4 else ["1", "0"]
 csr = TP.fabric(10000).csr()
 g = abi.Graph(csr, device=0)
 st = torch.cuda.Stream()
@@ -30,7 +31,7 @@ torch.cuda.set_stream(st)
 g.set_stream(st.cuda_stream)
 src = np.arange(csr.num_nodes, dtype=np.uint32)
 qs = {}
-for mode in ("1", "0"):
+for mode in modes:
     os.environ[env] = mode
     qs[mode] = g.query(src, abi.SPF_F_NEXTHOPS)
 out = {k: {"step_ms": [], "dist_ms": [], "nh_ms": []} for k in qs}
@@ -49,7 +50,7 @@ for r in range(rounds):
         h = q.stage_history(steps)
         out[mode]["dist_ms"].append(sum(x[0] for x in h) / len(h))
         out[mode]["nh_ms"].append(sum(x[1] for x in h) / len(h))
-a, b = qs["1"], qs["0"]
+a, b = qs[modes[0]], qs[modes[1]]
 same = bool((a.fetch_nexthops(0, csr.num_nodes) == b.fetch_nexthops(0, csr.num_nodes)).all())
 res = {"env": env}
 res.update({env + "=" + k: {kk: round(float(np.median(v)), 4) for kk, v in d.items()} for k, d in out.items()})

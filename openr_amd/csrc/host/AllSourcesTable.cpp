@@ -77,10 +77,6 @@ AllSourcesTable::AllSourcesTable(const LinkState& ls, std::vector<int> devices, 
   }
   const uint32_t V = (uint32_t)names_.size();
   const uint32_t n = (uint32_t)devices.size();
-  if (withNh_ && n != 1) {
-    throw std::invalid_argument(
-        "AllSourcesTable: next hops need every neighbour's row beside the source's (one device)");
-  }
   // contiguous source blocks (spf_table_layout's split: n / world each, the
   // first n % world one more)
   uint32_t first = 0;
@@ -95,21 +91,17 @@ AllSourcesTable::AllSourcesTable(const LinkState& ls, std::vector<int> devices, 
       for (uint32_t i = 0; i < b.count; ++i) {
         b.sources[i] = b.first + i;
       }
-      if (b.count) {
-        void* p = nullptr;
-        check(spf_device_alloc(b.device, (size_t)b.count * V * 4, &p), "spf_device_alloc");
-        b.rows = static_cast<uint32_t*>(p);
-      }
       blocks_.push_back(std::move(b));
     }
     buildGraphs(cur_);
+    for (auto& b : blocks_) {
+      setHalo(b); // (allocates the rows)
+    }
     recompute();
     if (withNh_) {
-      rowOf_.resize(V);
-      for (uint32_t i = 0; i < V; ++i) {
-        rowOf_[i] = (int32_t)i; // one block: source i's row is row i
+      for (auto& b : blocks_) {
+        refreshMasks(b, {});
       }
-      refreshMasks({});
     }
   } catch (...) {
     for (auto& b : blocks_) {
@@ -117,47 +109,87 @@ AllSourcesTable::AllSourcesTable(const LinkState& ls, std::vector<int> devices, 
         spf_graph_destroy(b.graph);
       }
       spf_device_free(b.device, b.rows);
-    }
-    if (masks_) {
-      spf_device_free(blocks_.front().device, masks_);
+      spf_device_free(b.device, b.masks);
     }
     throw;
   }
 }
 
-void AllSourcesTable::refreshMasks(const std::vector<uint32_t>& idx) {
-  Block& b = blocks_.front();
+bool AllSourcesTable::setHalo(Block& b) {
   const uint32_t V = (uint32_t)names_.size();
+  std::vector<uint32_t> srcs(b.sources.begin(), b.sources.begin() + b.count);
+  if (withNh_ && blocks_.size() > 1) {
+    std::vector<uint8_t> mark(V, 0);
+    for (uint32_t i = 0; i < b.count; ++i) {
+      const uint32_t u = b.first + i;
+      for (uint32_t e = layRow_[u]; e < layRow_[u + 1]; ++e) {
+        const uint32_t f = layCol_[e];
+        if (f < b.first || f >= b.first + b.count) {
+          mark[f] = 1;
+        }
+      }
+    }
+    for (uint32_t f = 0; f < V; ++f) {
+      if (mark[f]) {
+        srcs.push_back(f);
+      }
+    }
+  }
+  const bool changed = srcs != b.sources || !b.rows;
+  if (!changed) {
+    return false;
+  }
+  b.sources = std::move(srcs);
+  if (b.sources.size() > b.rowCap || !b.rows) {
+    spf_device_free(b.device, b.rows);
+    b.rows = nullptr;
+    b.rowCap = 0;
+    void* p = nullptr;
+    check(spf_device_alloc(b.device, std::max<size_t>(b.sources.size(), 1) * V * 4, &p),
+          "spf_device_alloc");
+    b.rows = static_cast<uint32_t*>(p);
+    b.rowCap = std::max<size_t>(b.sources.size(), 1);
+  }
+  if (withNh_) {
+    b.rowOf.assign(V, -1);
+    for (uint32_t r = 0; r < b.sources.size(); ++r) {
+      b.rowOf[b.sources[r]] = (int32_t)r;
+    }
+  }
+  return true;
+}
+
+void AllSourcesTable::refreshMasks(Block& b, const std::vector<uint32_t>& idx) {
+  const uint32_t V = (uint32_t)names_.size();
+  if (!b.count) {
+    return;
+  }
   if (idx.empty()) {
     // layout from the graph's current distinct-neighbour lists
-    maskWords_.assign(V, 1);
-    maskOff_.assign(V + 1, 0);
-    for (uint32_t i = 0; i < V; ++i) {
-      const int nb = spf_graph_num_nbrs(b.graph, i);
+    b.maskWords.assign(b.count, 1);
+    b.maskOff.assign(b.count + 1, 0);
+    for (uint32_t i = 0; i < b.count; ++i) {
+      const int nb = spf_graph_num_nbrs(b.graph, b.first + i);
       check(nb < 0 ? nb : SPF_OK, "spf_graph_num_nbrs");
-      maskWords_[i] = std::max<uint32_t>(1, ((uint32_t)nb + 63) / 64);
-      maskOff_[i + 1] = maskOff_[i] + (uint64_t)V * maskWords_[i];
+      b.maskWords[i] = std::max<uint32_t>(1, ((uint32_t)nb + 63) / 64);
+      b.maskOff[i + 1] = b.maskOff[i] + (uint64_t)V * b.maskWords[i];
     }
-    const size_t bytes = std::max<size_t>(maskOff_[V], 1) * 8;
-    if (bytes > maskBytes_) {
-      if (masks_) {
-        spf_device_free(b.device, masks_);
-        masks_ = nullptr;
-      }
+    const size_t bytes = std::max<size_t>(b.maskOff[b.count], 1) * 8;
+    if (bytes > b.maskBytes) {
+      spf_device_free(b.device, b.masks);
+      b.masks = nullptr;
+      b.maskBytes = 0;
       void* p = nullptr;
       check(spf_device_alloc(b.device, bytes, &p), "spf_device_alloc");
-      masks_ = static_cast<uint64_t*>(p);
-      maskBytes_ = bytes;
+      b.masks = static_cast<uint64_t*>(p);
+      b.maskBytes = bytes;
     }
-    if (!V) {
-      return;
+    std::vector<uint32_t> own(b.count);
+    for (uint32_t i = 0; i < b.count; ++i) {
+      own[i] = b.first + i;
     }
-    std::vector<uint32_t> all(V);
-    for (uint32_t i = 0; i < V; ++i) {
-      all[i] = i;
-    }
-    check(spf_table_nexthops(b.graph, b.rows, V, rowOf_.data(), V, all.data(), masks_,
-                             maskOff_.data()),
+    check(spf_table_nexthops(b.graph, b.rows, V, b.rowOf.data(), b.count, own.data(), b.masks,
+                             b.maskOff.data()),
           "spf_table_nexthops");
     return;
   }
@@ -165,22 +197,20 @@ void AllSourcesTable::refreshMasks(const std::vector<uint32_t>& idx) {
   std::vector<uint64_t> off(idx.size());
   for (size_t k = 0; k < idx.size(); ++k) {
     srcs[k] = b.sources[idx[k]];
-    off[k] = maskOff_[srcs[k]];
+    off[k] = b.maskOff[idx[k]];
   }
-  check(spf_table_nexthops(b.graph, b.rows, V, rowOf_.data(), (uint32_t)srcs.size(), srcs.data(),
-                           masks_, off.data()),
+  check(spf_table_nexthops(b.graph, b.rows, V, b.rowOf.data(), (uint32_t)srcs.size(), srcs.data(),
+                           b.masks, off.data()),
         "spf_table_nexthops");
 }
 
 AllSourcesTable::~AllSourcesTable() {
-  if (masks_ && !blocks_.empty()) {
-    spf_device_free(blocks_.front().device, masks_);
-  }
   for (auto& b : blocks_) {
     if (b.graph) {
       spf_graph_destroy(b.graph);
     }
     spf_device_free(b.device, b.rows);
+    spf_device_free(b.device, b.masks);
   }
 }
 
@@ -238,8 +268,8 @@ void AllSourcesTable::computeBlock(Block& b, const std::vector<uint32_t>& idx, b
 void AllSourcesTable::recompute() {
   lastSpfMs_ = 0;
   for (auto& b : blocks_) {
-    std::vector<uint32_t> all(b.count);
-    for (uint32_t i = 0; i < b.count; ++i) {
+    std::vector<uint32_t> all(b.sources.size());
+    for (uint32_t i = 0; i < all.size(); ++i) {
       all[i] = i;
     }
     computeBlock(b, all, false);
@@ -337,9 +367,14 @@ AllSourcesTable::UpdateStats AllSourcesTable::update(const LinkState& ls) {
     if (spf_graph_needs_exact(blocks_.front().graph)) {
       throw std::invalid_argument("AllSourcesTable::update: the new topology needs 64-bit rows");
     }
+    for (auto& b : blocks_) {
+      setHalo(b);
+    }
     recompute();
     if (withNh_) {
-      refreshMasks({});
+      for (auto& b : blocks_) {
+        refreshMasks(b, {});
+      }
     }
     stale_ = false;
     st.affected = (uint32_t)names_.size();
@@ -415,30 +450,48 @@ AllSourcesTable::UpdateStats AllSourcesTable::update(const LinkState& ls) {
     stale_ = true;
     throw std::invalid_argument("AllSourcesTable::update: the new topology needs 64-bit rows");
   }
-  // screen, then repair (or recompute) the affected rows of each block
+  // screen, then repair (or recompute) the affected rows of each block (its
+  // halo rows included); a block whose halo a rebuilt layout changed is
+  // recomputed whole
   lastSpfMs_ = 0;
   bool anyRelaxed = false, anyRecomputed = false;
-  std::vector<uint32_t> hitRows; // block-local rows repaired (one block with next hops)
-  for (auto& b : blocks_) {
-    if (!b.count || deltas.empty()) {
+  std::vector<std::vector<uint32_t>> hitRows(blocks_.size()); // own rows repaired, per block
+  std::vector<uint8_t> fresh(blocks_.size(), 0);
+  if (!st.graphPatched) {
+    for (size_t k = 0; k < blocks_.size(); ++k) {
+      if (setHalo(blocks_[k])) {
+        std::vector<uint32_t> all(blocks_[k].sources.size());
+        for (uint32_t i = 0; i < all.size(); ++i) {
+          all[i] = i;
+        }
+        computeBlock(blocks_[k], all, false);
+        fresh[k] = 1;
+        anyRecomputed = true;
+      }
+    }
+  }
+  for (size_t k = 0; k < blocks_.size(); ++k) {
+    Block& b = blocks_[k];
+    const uint32_t nr = (uint32_t)b.sources.size();
+    if (!nr || deltas.empty() || fresh[k]) {
       continue;
     }
     const auto ts = Clock::now();
-    std::vector<uint8_t> hit(b.count, 0);
-    check(spf_table_screen(b.graph, b.rows, V, b.count, b.sources.data(), deltas.data(),
+    std::vector<uint8_t> hit(nr, 0);
+    check(spf_table_screen(b.graph, b.rows, V, nr, b.sources.data(), deltas.data(),
                            (uint32_t)deltas.size(), hit.data()),
           "spf_table_screen");
     st.screenMs += msSince(ts);
     std::vector<uint32_t> idx, srcs;
-    for (uint32_t i = 0; i < b.count; ++i) {
+    for (uint32_t i = 0; i < nr; ++i) {
       if (hit[i]) {
         idx.push_back(i);
         srcs.push_back(b.sources[i]);
+        if (i < b.count) {
+          ++st.affected; // own rows (halo rows repeat another block's)
+          hitRows[k].push_back(i);
+        }
       }
-    }
-    st.affected += (uint32_t)idx.size();
-    if (withNh_) {
-      hitRows = idx;
     }
     if (idx.empty()) {
       continue;
@@ -460,11 +513,14 @@ AllSourcesTable::UpdateStats AllSourcesTable::update(const LinkState& ls) {
   if (withNh_ && !deltas.empty()) {
     // a source the screen passed keeps its masks (defined by its tight edges
     // alone) unless its neighbour list moved; a link-set change may move any
+    // (the neighbours' rows it reads are the block's halo, repaired above)
     const auto tn = Clock::now();
-    if (linkSetChanged) {
-      refreshMasks({});
-    } else if (!hitRows.empty()) {
-      refreshMasks(hitRows);
+    for (size_t k = 0; k < blocks_.size(); ++k) {
+      if (linkSetChanged || fresh[k]) {
+        refreshMasks(blocks_[k], {});
+      } else if (!hitRows[k].empty()) {
+        refreshMasks(blocks_[k], hitRows[k]);
+      }
     }
     st.nextHopsMs = msSince(tn);
   }
@@ -484,10 +540,20 @@ std::vector<std::string> AllSourcesTable::nextHops(const std::string& src,
   if (s == ids_.end() || d == ids_.end()) {
     throw std::out_of_range("AllSourcesTable::nextHops: unknown node");
   }
-  const Block& b = blocks_.front();
-  const uint32_t V = (uint32_t)names_.size(), W = maskWords_[s->second];
+  const Block* bp = nullptr;
+  for (const auto& x : blocks_) {
+    if (s->second >= x.first && s->second < x.first + x.count) {
+      bp = &x;
+    }
+  }
+  if (!bp) {
+    throw std::out_of_range("AllSourcesTable::nextHops: no block holds " + src);
+  }
+  const Block& b = *bp;
+  const uint32_t i = s->second - b.first;
+  const uint32_t V = (uint32_t)names_.size(), W = b.maskWords[i];
   std::vector<uint64_t> m(W);
-  check(spf_device_memcpy(b.device, m.data(), masks_ + maskOff_[s->second] + (size_t)d->second * W,
+  check(spf_device_memcpy(b.device, m.data(), b.masks + b.maskOff[i] + (size_t)d->second * W,
                           (size_t)W * 8, SPF_COPY_D2H),
         "spf_device_memcpy");
   const int nn = spf_graph_num_nbrs(b.graph, s->second);

@@ -57,9 +57,11 @@ class AllSourcesTable {
   explicit AllSourcesTable(const LinkState& ls, std::vector<int> devices = {});
   // withNextHops: also every source's ECMP next-hop masks (getSpfResult's
   // nextHops per node), kept current under churn from the table rows
-  // (spf_table_nexthops, the all-sources rule).  One device only: a source's
-  // neighbours' rows must sit beside its own (std::invalid_argument with
-  // several devices).
+  // (spf_table_nexthops, the all-sources rule).  A source's masks read its
+  // neighbours' rows: with several devices each block also keeps "halo"
+  // rows -- the neighbours of its sources that other blocks own, computed
+  // and repaired on the block's own device with its rows -- so every step
+  // still runs per device with no collective (round 6).
   AllSourcesTable(const LinkState& ls, std::vector<int> devices, bool withNextHops);
   ~AllSourcesTable();
   AllSourcesTable(const AllSourcesTable&) = delete;
@@ -99,17 +101,31 @@ class AllSourcesTable {
     int device{0};
     uint32_t first{0}, count{0};
     spf_graph* graph{nullptr};
-    uint32_t* rows{nullptr}; // device [count][V]
+    // device [sources.size()][V]: the block's own sources first (rows
+    // 0..count-1), then its halo (withNextHops: neighbours owned elsewhere)
+    uint32_t* rows{nullptr};
+    size_t rowCap{0}; // rows allocated
     std::vector<uint32_t> sources;
+    // next-hop masks of the own sources (withNextHops): device words,
+    // per-source word offsets and widths, node -> row index (-1: none)
+    uint64_t* masks{nullptr};
+    size_t maskBytes{0};
+    std::vector<uint64_t> maskOff;
+    std::vector<uint32_t> maskWords;
+    std::vector<int32_t> rowOf;
   };
   Csr snapshot(const LinkState& ls) const;
   void buildGraphs(const Csr& c);
   void computeBlock(Block& b, const std::vector<uint32_t>& idx, bool scatter);
+  // withNextHops: the block's halo from the resident layout's heads (a
+  // superset of every later neighbour list until the graphs are rebuilt);
+  // true when it changed (rows reallocated: recompute the block)
+  bool setHalo(Block& b);
   bool linksInPlace(const std::vector<spf_edge_delta>& deltas, std::vector<uint32_t>& edges,
                     std::vector<uint8_t>& up, std::vector<uint64_t>& w);
-  // (re)compute the masks of block-local rows idx (empty: every row; the
-  // layout is re-derived from the graph's current neighbour lists)
-  void refreshMasks(const std::vector<uint32_t>& idx);
+  // (re)compute the masks of block b's own rows idx (empty: every own row;
+  // the layout is re-derived from the graph's current neighbour lists)
+  void refreshMasks(Block& b, const std::vector<uint32_t>& idx);
 
   std::vector<std::string> names_;
   std::unordered_map<std::string, uint32_t> ids_;
@@ -125,13 +141,7 @@ class AllSourcesTable {
   // needs 64-bit rows) left rows of the old topology: the next update()
   // rebuilds and recomputes, row() refuses until then
   bool stale_{false};
-  // next-hop masks (single block): device words, per-source word offsets
   bool withNh_{false};
-  uint64_t* masks_{nullptr};
-  size_t maskBytes_{0};
-  std::vector<uint64_t> maskOff_;
-  std::vector<uint32_t> maskWords_;
-  std::vector<int32_t> rowOf_;
 };
 
 } // namespace openr

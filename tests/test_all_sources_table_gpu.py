@@ -37,8 +37,9 @@ def _check_rows(E, O, t, ea, oa):
             assert row[j] == want, (src, dst, row[j], want)
 
 
+@pytest.mark.parametrize("devices", [None, [0, 0]])
 @pytest.mark.parametrize("seed", range(3))
-def test_all_sources_table_under_churn(mods, seed):
+def test_all_sources_table_under_churn(mods, seed, devices):
     E, O = mods
     names, adj_dbs, prefix_dbs = RZ.random_network(
         3100 + seed, n_nodes=40, n_links=100, overload_prob=0.05, link_overload_prob=0.03)
@@ -49,7 +50,7 @@ def test_all_sources_table_under_churn(mods, seed):
             adj_dbs["0"].append(T.createAdjDb(n, [], 0, False, "0"))
     ea, _ = RZ.load(E, adj_dbs, prefix_dbs, seed)
     oa, _ = RZ.load(O, adj_dbs, prefix_dbs, seed)
-    t = E.AllSourcesTable(ea, "0")
+    t = E.AllSourcesTable(ea, "0") if devices is None else E.AllSourcesTable(ea, "0", devices)
     _check_rows(E, O, t, ea, oa)
     rng = random.Random(seed)
     dbs = {d.thisNodeName: copy.deepcopy(d) for d in adj_dbs["0"]}
@@ -171,14 +172,18 @@ def _check_next_hops(t, oa):
             assert t.next_hops(src, dst) == want, (src, dst)
 
 
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
 @pytest.mark.parametrize("seed", range(2))
-def test_all_sources_table_next_hops_under_churn(mods, seed):
+def test_all_sources_table_next_hops_under_churn(mods, seed, devices):
     """AllSourcesTable(nexthops=True): every source's ECMP next hops
     (getSpfResult's nextHops, LinkState.cpp:842-871) kept current under
-    drains, metric changes and link flaps -- the flaps set in place
+    drains, metric changes, link flaps -- the flaps set in place
     (spf_graph_set_edges rebuilds the distinct-neighbour lists, so next-hop
-    queries stay exact on the patched graph) -- against the oracle at every
-    step."""
+    queries stay exact on the patched graph) -- and brand-new links (a
+    rebuild), against the oracle at every step.  With several source blocks
+    (one per entry of `devices`; here all on device 0) each block keeps halo
+    rows for its sources' neighbours that other blocks own (round 6): a new
+    link can grow a halo, and the block is then recomputed."""
     E, O = mods
     names, adj_dbs, prefix_dbs = RZ.random_network(
         4100 + seed, n_nodes=40, n_links=100, overload_prob=0.05, link_overload_prob=0.0)
@@ -188,17 +193,28 @@ def test_all_sources_table_next_hops_under_churn(mods, seed):
             adj_dbs["0"].append(T.createAdjDb(n, [], 0, False, "0"))
     ea, _ = RZ.load(E, adj_dbs, prefix_dbs, seed)
     oa, _ = RZ.load(O, adj_dbs, prefix_dbs, seed)
-    t = E.AllSourcesTable(ea, "0", [0], True)
+    t = E.AllSourcesTable(ea, "0", devices, True)
     assert t.has_next_hops
     _check_rows(E, O, t, ea, oa)
     _check_next_hops(t, oa)
     rng = random.Random(seed)
     dbs = {d.thisNodeName: copy.deepcopy(d) for d in adj_dbs["0"]}
-    patched = 0
-    for step in range(12):
+    patched = rebuilt = 0
+    for step in range(14):
         db = rng.choice([d for d in dbs.values() if d.adjacencies])
         r = rng.random()
-        if r < 0.25:
+        if step in (5, 11):
+            # a brand-new link between two nodes (both sides advertise it)
+            a, b = rng.sample(sorted(dbs), 2)
+            k = 2000 + step
+            dbs[a].adjacencies.append(T.createAdjacency(
+                b, f"new_{a}_{k}", f"new_{b}_{k}", f"fe80::1:{k:x}", "10.9.9.1", rng.randint(1, 20), 0))
+            dbs[b].adjacencies.append(T.createAdjacency(
+                a, f"new_{b}_{k}", f"new_{a}_{k}", f"fe80::2:{k:x}", "10.9.9.2", rng.randint(1, 20), 0))
+            ea["0"].updateAdjacencyDatabase(dbs[a])
+            oa["0"].updateAdjacencyDatabase(dbs[a])
+            db = dbs[b]
+        elif r < 0.25:
             db.isOverloaded = not db.isOverloaded
         elif r < 0.5:
             rng.choice(db.adjacencies).metric = rng.randint(1, 20)
@@ -209,6 +225,10 @@ def test_all_sources_table_next_hops_under_churn(mods, seed):
         oa["0"].updateAdjacencyDatabase(db)
         st = t.update(ea, "0")
         patched += st["graph_patched"]
+        rebuilt += not st["graph_patched"]
         _check_rows(E, O, t, ea, oa)
         _check_next_hops(t, oa)
-    assert patched > 0
+    assert patched > 0 and rebuilt > 0
+    t.recompute()
+    _check_rows(E, O, t, ea, oa)
+    _check_next_hops(t, oa)

@@ -134,6 +134,9 @@ constexpr uint32_t kIgnLdsMax = 2048;      // ignore-list entries staged in LDS
 // whose rows another query copies into its working buffer (what-if
 // baselines, the zero-metric plan's wide-plan sources)
 constexpr uint32_t kQueryWideMasks = 0x80000000u;
+// internal query flag: no first-hop nested batch for this query's source-link
+// failures (the nested batch itself; spf_whatif_firsthop_kernel)
+constexpr uint32_t kQueryNoFirstHop = 0x40000000u;
 constexpr uint32_t kNotSeen = 0xFFFFFFFFu; // exact kernel heap states
 constexpr uint32_t kSettled = 0xFFFFFFFEu;
 
@@ -2702,6 +2705,10 @@ struct MsBfsArgs {
   uint32_t nfw = 0;
   // measurement only (OPENR_MS_NOREC=1): the BFS without its row stores
   uint32_t norec = 0;
+  // per batch: one node that stays non-transit in this batch (kInf32 none;
+  // nullptr: no such node) -- the what-if first-hop rows, BFS levels from a
+  // source's neighbours through every node but that source
+  const uint32_t* blocked = nullptr;
 };
 
 // Masks and flags of spf_msbfs_kernel's ignore mode: one block per query,
@@ -2861,10 +2868,11 @@ __global__ __launch_bounds__(kMsThreads) void spf_msbfs_kernel(MsBfsArgs a) {
     __syncthreads();
     MT vis[KMAX];
     uint32_t trm = 0; // bit k: this thread's k-th node may be transited
+    const uint32_t blk = a.blocked ? a.blocked[b] : kInf32;
 #pragma unroll
     for (uint32_t k = 0; k < KMAX; ++k) {
       const uint32_t v = tid + k * kMsThreads;
-      if (k < K && v < V) {
+      if (k < K && v < V && v != blk) {
         trm |= ((a.trbits[v >> 5] >> (v & 31)) & 1u) << k;
       }
       vis[k] = (k < K && v < V) ? cur[v] : (MT)0;
@@ -6120,6 +6128,158 @@ __global__ __launch_bounds__(kWhThreads) void spf_whatif_pull_kernel(WhatifHeavy
   }
 }
 
+// Source-link failures, first-hop form (round 6, spf_whatif_firsthop_kernel,
+// OPENR_SPF_WHATIF_FIRSTHOP=0 keeps the pull kernel for them).  On a uniform
+// metric a shortest path from s never returns to s, so for a query q that
+// ignores links of s alone, every node v != s has
+//   lvl_q(v) = 1 + min over usable first hops n of R_s[n][v],
+// where R_s[n] is the BFS level from n with every link of s ignored, and v's
+// next hops are the slots of the first hops reaching that minimum (a drained
+// first hop n reaches only itself: R = 0 at v = n, unreached elsewhere).  The
+// rows R_s of every such source's neighbours are ONE nested distance batch
+// (q->hop: the bit-parallel BFS with ignore masks, all neighbours of s at
+// once), computed per run; this kernel then combines them per (query, 256-node
+// chunk) instead of one 1,024-thread workgroup running a whole BFS and a
+// level-by-level mask pass per query (0.9 ms on the fabric, the what-if
+// batch's longest chain).  Usable first hops are read at run time: a half-edge
+// set down is a self-loop (spf_graph_set_edges), the transit bits are the
+// graph's current ones, slots are d_slot's.
+struct WhatifHopArgs {
+  const uint32_t* row;
+  const uint32_t* col;
+  const uint32_t* link;
+  const uint32_t* slot;
+  const uint32_t* trbits;
+  const uint32_t* src;
+  const uint32_t* ign_off;
+  const uint32_t* ign;
+  const uint32_t* skip;
+  const uint32_t* fh_q;      // [nfh] the queries
+  const uint32_t* fh_h;      // [nfh] their hop source
+  const uint32_t* hop_row0;  // [nhop] first row of the source's neighbours in the batch
+  const uint32_t* hop_cnt;   // [nhop] neighbours (sorted ids at hop_nodes + hop_off)
+  const uint32_t* hop_off;
+  const uint32_t* hop_nodes;
+  const uint32_t* rows;      // the nested batch's distance rows (levels)
+  uint32_t rows_pitch;
+  uint32_t* dist_out;
+  uint64_t* nh_out;
+  const uint64_t* nh_off;
+  const uint32_t* nh_w;
+  uint32_t V, Vp, scale, want_nh;
+};
+constexpr uint32_t kFhSlots = 64 * kWhMaxW; // the candidates' neighbour bound
+constexpr uint32_t kFhChunk = 256;          // nodes per workgroup
+constexpr uint32_t kFhGroup = 16;           // row loads in flight per thread
+
+__global__ __launch_bounds__(256) void spf_whatif_firsthop_kernel(WhatifHopArgs a) {
+  __shared__ int32_t sl_row[kFhSlots];  // -1 unusable, -2 drained (itself only)
+  __shared__ uint32_t sl_node[kFhSlots];
+  __shared__ uint32_t sh_nslot;
+  const uint32_t i = blockIdx.x, q = a.fh_q[i];
+  if (a.skip[q] != 3u) {
+    return; // screened (rows copied): not this kernel's
+  }
+  const uint32_t h = a.fh_h[i], s = a.src[q], tid = threadIdx.x;
+  for (uint32_t j = tid; j < kFhSlots; j += 256) {
+    sl_row[j] = -1;
+  }
+  if (tid == 0) {
+    sh_nslot = 0;
+  }
+  __syncthreads();
+  const uint32_t e0 = a.row[s], e1 = a.row[s + 1];
+  const uint32_t ilo = a.ign_off[q], nign = a.ign_off[q + 1] - ilo;
+  for (uint32_t e = e0 + tid; e < e1; e += 256) {
+    const uint32_t n = a.col[e];
+    if (n == s) {
+      continue; // a half-edge set down
+    }
+    const uint32_t l = a.link[e];
+    bool ig = false;
+    for (uint32_t k = 0; k < nign && !ig; ++k) {
+      ig = a.ign[ilo + k] == l;
+    }
+    const uint32_t j = a.slot[e];
+    if (!ig && j < kFhSlots) {
+      sl_row[j] = 0; // usable (parallel links: the same value)
+      sl_node[j] = n;
+      atomicMax(&sh_nslot, j + 1);
+    }
+  }
+  __syncthreads();
+  const uint32_t nslot = sh_nslot;
+  for (uint32_t j = tid; j < nslot; j += 256) {
+    if (sl_row[j] < 0) {
+      continue;
+    }
+    const uint32_t n = sl_node[j];
+    const uint32_t* nodes = a.hop_nodes + a.hop_off[h];
+    uint32_t lo = 0, hi = a.hop_cnt[h];
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (nodes[mid] < n) {
+        lo = mid + 1;
+      } else {
+        hi = mid;
+      }
+    }
+    const bool transit = (a.trbits[n >> 5] >> (n & 31)) & 1u;
+    // (every head of s's half-edges is in the batch: found by construction)
+    sl_row[j] = transit ? (int32_t)(a.hop_row0[h] + lo) : -2;
+  }
+  __syncthreads();
+  const uint32_t v = blockIdx.y * kFhChunk + tid;
+  if (v >= a.V) {
+    return;
+  }
+  uint32_t m = kInf32;
+  uint64_t acc[kWhMaxW] = {0, 0, 0, 0};
+  if (v != s) {
+    for (uint32_t j0 = 0; j0 < nslot; j0 += kFhGroup) {
+      uint32_t d[kFhGroup];
+#pragma unroll
+      for (uint32_t k = 0; k < kFhGroup; ++k) {
+        const uint32_t j = j0 + k;
+        const int32_t r = j < nslot ? sl_row[j] : -1;
+        d[k] = r >= 0 ? a.rows[(size_t)r * a.rows_pitch + v]
+                      : (r == -2 && sl_node[j] == v ? 0u : kInf32);
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < kFhGroup; ++k) {
+        const uint32_t j = j0 + k;
+        if (d[k] == kInf32) {
+          continue;
+        }
+        const uint64_t bit = 1ull << (j & 63u);
+        if (d[k] < m) {
+          m = d[k];
+#pragma unroll
+          for (uint32_t x = 0; x < kWhMaxW; ++x) {
+            acc[x] = x == (j >> 6) ? bit : 0ull;
+          }
+        } else if (d[k] == m) {
+#pragma unroll
+          for (uint32_t x = 0; x < kWhMaxW; ++x) {
+            acc[x] |= x == (j >> 6) ? bit : 0ull;
+          }
+        }
+      }
+    }
+  }
+  a.dist_out[(size_t)q * a.Vp + v] = v == s ? 0u : (m == kInf32 ? kInf32 : (m + 1) * a.scale);
+  if (a.want_nh) {
+    const uint32_t W = a.nh_w[q];
+    uint64_t* nh = a.nh_out + a.nh_off[q] + (size_t)v * W;
+#pragma unroll
+    for (uint32_t x = 0; x < kWhMaxW; ++x) {
+      if (x < W) {
+        nh[x] = acc[x];
+      }
+    }
+  }
+}
+
 // Table repair screen (spf_table_screen): one lane per source row, every
 // lane walks the same delta list (wave-uniform loads of the delta arrays).
 // Reads two uint32 of the lane's row per in-scope delta and stops at the
@@ -7998,8 +8158,21 @@ struct spf_query {
   uint32_t* d_wh_lstart = nullptr;    // [ncand][V + 1] level segments
   hipStream_t wh_stream = nullptr;    // the heavy kernel's stream (beside the SSSP)
   hipEvent_t wh_ev0 = nullptr, wh_ev1 = nullptr;
+  hipEvent_t wh_ev2 = nullptr;        // the side stream's fork before the baseline (hop rows)
+  // internal batches: launch_msbfs's stream instead of the graph's (the hop
+  // rows on the what-if side stream) and the per-batch blocked node
+  hipStream_t stream_override = nullptr;
+  uint32_t* d_ms_blocked = nullptr;
   bool wh_pending = false;            // the graph stream still has to join wh_ev1
   bool wh_pull = false;               // spf_whatif_pull_kernel (sliced ELL, short lists)
+  // the candidates the pull / heavy kernel runs (d_wh_cand); the others
+  // (every ignored link at the source) go to spf_whatif_firsthop_kernel over
+  // the nested batch `hop` (rows of the sources' neighbours, links of the
+  // source ignored); d_fh packs fh_q, fh_h and the hop tables
+  std::vector<uint32_t> wh_pull_cand;
+  spf_query* hop = nullptr;
+  uint32_t* d_fh = nullptr;
+  uint32_t nfh = 0, nhop = 0, nhop_nodes = 0;
   uint32_t dlds_shift = 4, dlds_grid = 0;
   size_t dlds_lds = 0;
   uint32_t* d_ovf = nullptr; // [0] overflow count, [1] claim counter, [2..] list
@@ -8808,11 +8981,15 @@ void free_query(spf_query* q) {
         (void*)q->d_zvar, (void*)q->d_ms_mask, (void*)q->d_ms_flag,
         (void*)q->d_ovf, q->narrow ? (void*)q->d_nhb : nullptr, (void*)q->d_tcs, q->d_v2,
         (void*)q->d_trit,
-        q->d_coop, (void*)q->d_wh_cand, (void*)q->d_wh_mark, (void*)q->d_wh_lstart}) {
+        q->d_coop, (void*)q->d_wh_cand, (void*)q->d_wh_mark, (void*)q->d_wh_lstart,
+        (void*)q->d_fh, (void*)q->d_ms_blocked}) {
     pool_free(p);
   }
   if (q->base) {
     free_query(q->base);
+  }
+  if (q->hop) {
+    free_query(q->hop);
   }
   if (q->zfix) {
     free_query(q->zfix);
@@ -8831,6 +9008,9 @@ void free_query(spf_query* q) {
   }
   if (q->wh_ev1) {
     ev_put(q->wh_ev1);
+  }
+  if (q->wh_ev2) {
+    ev_put(q->wh_ev2);
   }
   if (q->wh_stream) {
     (void)hipStreamDestroy(q->wh_stream);
@@ -10936,8 +11116,133 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
               q->wh_cand.push_back(i);
             }
           }
+          // candidates whose every ignored link leaves the source (or names
+          // no link): the first-hop form over one nested batch of the
+          // sources' neighbour rows (spf_whatif_firsthop_kernel); the rest
+          // keep the pull / heavy kernel
+          q->wh_pull_cand.clear();
+          if (!(desc->flags & kQueryNoFirstHop) && env_flag("OPENR_SPF_WHATIF_FIRSTHOP", 1)) {
+            const std::vector<uint32_t>& heads = g->col_orig.empty() ? g->col : g->col_orig;
+            std::unordered_map<uint32_t, uint32_t> hop_of;
+            std::vector<uint32_t> fh_q, fh_h, hop_s, hop_cnt, hop_off, hop_nodes;
+            std::vector<std::vector<uint32_t>> hop_links;
+            for (uint32_t i : q->wh_cand) {
+              const uint32_t s0 = desc->sources[i];
+              bool pure = true;
+              for (uint32_t j = desc->ignore_offsets[i]; j < desc->ignore_offsets[i + 1] && pure;
+                   ++j) {
+                const uint32_t l = desc->ignore_links[j];
+                bool at = l >= g->L;
+                for (uint32_t e = g->row[s0]; e < g->row[s0 + 1] && !at; ++e) {
+                  at = g->link[e] == l;
+                }
+                pure = at;
+              }
+              if (!pure) {
+                q->wh_pull_cand.push_back(i);
+                continue;
+              }
+              auto it = hop_of.find(s0);
+              if (it == hop_of.end()) {
+                std::vector<uint32_t> nb, links;
+                for (uint32_t e = g->row[s0]; e < g->row[s0 + 1]; ++e) {
+                  if (heads[e] != s0) {
+                    nb.push_back(heads[e]);
+                  }
+                  links.push_back(g->link[e]);
+                }
+                std::sort(nb.begin(), nb.end());
+                nb.erase(std::unique(nb.begin(), nb.end()), nb.end());
+                std::sort(links.begin(), links.end());
+                links.erase(std::unique(links.begin(), links.end()), links.end());
+                if (nb.empty()) {
+                  q->wh_pull_cand.push_back(i);
+                  continue;
+                }
+                it = hop_of.emplace(s0, (uint32_t)hop_s.size()).first;
+                hop_s.push_back(s0);
+                hop_cnt.push_back((uint32_t)nb.size());
+                hop_off.push_back((uint32_t)hop_nodes.size());
+                hop_nodes.insert(hop_nodes.end(), nb.begin(), nb.end());
+                hop_links.push_back(std::move(links));
+              }
+              fh_q.push_back(i);
+              fh_h.push_back(it->second);
+            }
+            std::vector<uint32_t> hop_row0;
+            if (!fh_q.empty()) {
+              // (a) the plain bit-parallel BFS with the source non-transit in
+              // its neighbours' batches (MsBfsArgs::blocked): each source's
+              // neighbours padded to whole 64-row batches
+              std::vector<uint32_t> hsrc, unit32; // unit32: blocked node per 32 rows
+              for (size_t h = 0; h < hop_s.size(); ++h) {
+                hop_row0.push_back((uint32_t)hsrc.size());
+                const uint32_t* nb = hop_nodes.data() + hop_off[h];
+                const uint32_t padded = (hop_cnt[h] + 63) / 64 * 64;
+                for (uint32_t k = 0; k < padded; ++k) {
+                  hsrc.push_back(nb[k < hop_cnt[h] ? k : 0]);
+                }
+                unit32.insert(unit32.end(), padded / 32, hop_s[h]);
+              }
+              spf_query_desc hd{};
+              hd.num_queries = (uint32_t)hsrc.size();
+              hd.sources = hsrc.data();
+              hd.flags = SPF_F_UNIT_METRIC | kQueryNoFirstHop;
+              if ((s = spf_query_create(g, &hd, &q->hop))) {
+                return bail(s);
+              }
+              spf_query* hq = q->hop;
+              if (hq->dist == DistPlan::MsBfs && hq->nh == NhPlan::None && !hq->zvars &&
+                  hq->nrows == hq->nq && (hq->ms_bits == 64 || hq->ms_bits == 32) &&
+                  env_flag("OPENR_SPF_WHATIF_FIRSTHOP_BLOCKED", 1)) {
+                std::vector<uint32_t> blk;
+                const uint32_t per = hq->ms_bits / 32;
+                for (size_t u = 0; u < unit32.size(); u += per) {
+                  blk.push_back(unit32[u]);
+                }
+                if ((s = dev_upload_q(&hq->d_ms_blocked, blk.data(), blk.size()))) {
+                  return bail(s);
+                }
+              } else {
+                // (b) any other plan: every link of the source ignored, rows
+                // unpadded
+                free_query(q->hop);
+                q->hop = nullptr;
+                hsrc.clear();
+                hop_row0.clear();
+                std::vector<uint32_t> hoff{0}, hign;
+                for (size_t h = 0; h < hop_s.size(); ++h) {
+                  hop_row0.push_back((uint32_t)hsrc.size());
+                  for (uint32_t k = 0; k < hop_cnt[h]; ++k) {
+                    hsrc.push_back(hop_nodes[hop_off[h] + k]);
+                    hign.insert(hign.end(), hop_links[h].begin(), hop_links[h].end());
+                    hoff.push_back((uint32_t)hign.size());
+                  }
+                }
+                hd.num_queries = (uint32_t)hsrc.size();
+                hd.sources = hsrc.data();
+                hd.ignore_offsets = hoff.data();
+                hd.ignore_links = hign.data();
+                if ((s = spf_query_create(g, &hd, &q->hop))) {
+                  return bail(s);
+                }
+              }
+              std::vector<uint32_t> pack;
+              for (const auto* v : {&fh_q, &fh_h, &hop_row0, &hop_cnt, &hop_off, &hop_nodes}) {
+                pack.insert(pack.end(), v->begin(), v->end());
+              }
+              if ((s = dev_upload_q(&q->d_fh, pack.data(), pack.size()))) {
+                return bail(s);
+              }
+              q->nfh = (uint32_t)fh_q.size();
+              q->nhop = (uint32_t)hop_row0.size();
+              q->nhop_nodes = (uint32_t)hop_nodes.size();
+            }
+          } else {
+            q->wh_pull_cand = q->wh_cand;
+          }
           q->wh_pull = g->d_sell != nullptr && env_flag("OPENR_SPF_WHATIF_PULL", 1);
-          for (uint32_t i : q->wh_cand) {
+          for (uint32_t i : q->wh_pull_cand) {
             if (desc->ignore_offsets[i + 1] - desc->ignore_offsets[i] > kWpIgnE / 2) {
               q->wh_pull = false;
             }
@@ -10947,20 +11252,27 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
             for (uint32_t i : q->wh_cand) {
               mark[i] = 1;
             }
-            if ((s = dev_upload_q(&q->d_wh_cand, q->wh_cand.data(), q->wh_cand.size())) ||
-                (s = dev_upload_q(&q->d_wh_mark, mark.data(), mark.size()))) {
+            if ((s = dev_upload_q(&q->d_wh_mark, mark.data(), mark.size()))) {
+              return bail(s);
+            }
+          }
+          if (!q->wh_pull_cand.empty()) {
+            if ((s = dev_upload_q(&q->d_wh_cand, q->wh_pull_cand.data(), q->wh_pull_cand.size()))) {
               return bail(s);
             }
             if (pool_malloc((void**)&q->d_wh_lstart,
-                            q->wh_cand.size() * ((size_t)g->V + 1) * 4) != hipSuccess) {
+                            q->wh_pull_cand.size() * ((size_t)g->V + 1) * 4) != hipSuccess) {
               return bail(fail(SPF_E_NOMEM, "what-if heavy level segments"));
             }
+          }
+          if (!q->wh_pull_cand.empty() || q->nfh) {
             // high priority: its two big-LDS workgroups must be placed before
             // the SSSP's hundreds fill every CU (they waited ~0.6 ms, r05an)
             int plo = 0, phi = 0;
             (void)hipDeviceGetStreamPriorityRange(&plo, &phi);
             if (hipStreamCreateWithPriority(&q->wh_stream, hipStreamNonBlocking, phi) != hipSuccess ||
-                ev_get(&q->wh_ev0) != hipSuccess || ev_get(&q->wh_ev1) != hipSuccess) {
+                ev_get(&q->wh_ev0) != hipSuccess || ev_get(&q->wh_ev1) != hipSuccess ||
+                ev_get(&q->wh_ev2) != hipSuccess) {
               return bail(fail(SPF_E_DEVICE, "what-if heavy stream"));
             }
           }
@@ -11356,6 +11668,7 @@ inline bool lvl_only(const spf_query* q) {
 
 int launch_msbfs(spf_query* q, bool unit) {
   spf_graph* g = q->g;
+  hipStream_t st = q->stream_override ? q->stream_override : g->stream;
   MsBfsArgs a;
   a.row = g->d_row;
   a.col = g->d_col;
@@ -11377,14 +11690,15 @@ int launch_msbfs(spf_query* q, bool unit) {
   a.nz = 0;
   a.lvl_only = lvl_only(q) ? 1u : 0u;
   a.norec = env_u32("OPENR_MS_NOREC", 0);
+  a.blocked = q->d_ms_blocked;
   q->ms_par ^= 1u;
   a.flags = q->d_flags + q->ms_par;
   a.flags_clear = q->d_flags + (q->ms_par ^ 1u);
   if (q->ms_ign) {
-    HIP_TRY(hipMemsetAsync(q->d_ms_mask, 0, (size_t)q->ms_nbatch * g->E * 8, g->stream));
-    HIP_TRY(hipMemsetAsync(q->d_ms_flag, 0, (size_t)q->ms_nbatch * q->ms_nfw * 4, g->stream));
+    HIP_TRY(hipMemsetAsync(q->d_ms_mask, 0, (size_t)q->ms_nbatch * g->E * 8, st));
+    HIP_TRY(hipMemsetAsync(q->d_ms_flag, 0, (size_t)q->ms_nbatch * q->ms_nfw * 4, st));
     if (q->nq) {
-      SPF_LAUNCH(spf_ms_ign_kernel, dim3(q->nq), dim3(256), 0, g->stream, q->d_ign_off,
+      SPF_LAUNCH(spf_ms_ign_kernel, dim3(q->nq), dim3(256), 0, st, q->d_ign_off,
                          q->d_ign, g->d_link_half, g->d_col, g->d_rev, g->L,
                          (uint32_t)q->ms_bits, g->E, q->ms_nfw, q->d_ms_mask, q->d_ms_flag);
       HIP_TRY(hipGetLastError());
@@ -11437,7 +11751,8 @@ int launch_msbfs(spf_query* q, bool unit) {
   // every rank size (N = 8 block: 0.122 vs 0.117 ms; with the row stores off
   // 0.122 vs 0.064 ms, profiles/r05u): a level's barrier, acquire and frontier
   // reload cost ~7 us against ~8 us of pull work split P ways
-  if (!gen && q->ms_bits == 64 && sell && q->zvars == 0 && g->V <= 8u * kMsThreads * 2u &&
+  if (!gen && !a.blocked && q->ms_bits == 64 && sell && q->zvars == 0 &&
+      g->V <= 8u * kMsThreads * 2u &&
       env_flag("OPENR_MS_COOP", 0)) {
     const uint32_t nbatch = (q->nrows + 63) / 64;
     const void* ck = (const void*)spf_msbfs_coop_kernel<8>;
@@ -11456,14 +11771,14 @@ int launch_msbfs(spf_query* q, bool unit) {
         const size_t xb = (size_t)nbatch * 2 * g->V * 8;
         const size_t need = xb + (size_t)nbatch * 4 + (size_t)nbatch * 2 * P * 4 + 16;
         if (q->d_coop && q->coop_bytes < need) {
-          HIP_TRY(hipStreamSynchronize(g->stream));
+          HIP_TRY(hipStreamSynchronize(st));
           pool_free(q->d_coop);
           q->d_coop = nullptr;
         }
         if (!q->d_coop) {
           HIP_TRY(pool_malloc(&q->d_coop, need));
           q->coop_bytes = need;
-          HIP_TRY(hipMemsetAsync(q->d_coop, 0, need, g->stream));
+          HIP_TRY(hipMemsetAsync(q->d_coop, 0, need, st));
         }
         MsCoopArgs c;
         c.a = a;
@@ -11472,11 +11787,11 @@ int launch_msbfs(spf_query* q, bool unit) {
         c.anyv = c.cnt + nbatch;
         c.err = c.anyv + (size_t)nbatch * 2 * P;
         c.P = P;
-        HIP_TRY(hipMemsetAsync(c.cnt, 0, (size_t)nbatch * 4, g->stream));
+        HIP_TRY(hipMemsetAsync(c.cnt, 0, (size_t)nbatch * 4, st));
         void* cargs[] = {&c};
         spf_note_launch("spf_msbfs_coop_kernel");
         const hipError_t le = hipLaunchCooperativeKernel(ck, dim3(nbatch * P), dim3(kMsThreads),
-                                                         cargs, (unsigned)clds, g->stream);
+                                                         cargs, (unsigned)clds, st);
         if (le == hipSuccess) {
           q->coop_p = P;
           return SPF_OK;
@@ -11498,7 +11813,7 @@ int launch_msbfs(spf_query* q, bool unit) {
     void* args[] = {&a};
     spf_note_launch("spf_msbfs_kernel");
     HIP_TRY(hipLaunchKernel(kern, dim3(q->grid), dim3(kMsThreads), args,
-                            q->lds_bytes, g->stream));
+                            q->lds_bytes, st));
     HIP_TRY(hipGetLastError());
   }
   if (q->zvars && q->d_zvar) {
@@ -11775,7 +12090,29 @@ int run_screen(spf_query* q) {
     return fail(SPF_E_UNSUPPORTED,
                 "what-if query: a half-edge went down alone since creation (recreate the query)");
   }
-  int s = run_plan(b);
+  if (!q->wh_cand.empty() && !((q->flags & SPF_F_UNIT_METRIC) || g->uniform)) {
+    // the source-link kernels compute levels x the uniform metric
+    return fail(SPF_E_UNSUPPORTED,
+                "what-if query: the metrics stopped being uniform since creation (recreate the query)");
+  }
+  int s = SPF_OK;
+  if (q->hop) {
+    // the first-hop rows: BFS levels from the sources' neighbours through
+    // every node but the source (independent of the baseline).  The blocked
+    // form runs on the side stream beside the baseline and the screen; the
+    // ignore-list form (its own mask kernel and memsets) on the graph stream
+    if (q->hop->d_ms_blocked && q->wh_stream) {
+      HIP_TRY(hipEventRecord(q->wh_ev2, g->stream));
+      HIP_TRY(hipStreamWaitEvent(q->wh_stream, q->wh_ev2, 0));
+      q->hop->stream_override = q->wh_stream;
+      q->wh_pending = true; // (the graph stream joins wh_ev1 after the SSSP launch)
+    }
+    s = run_plan(q->hop);
+    if (s != SPF_OK) {
+      return s;
+    }
+  }
+  s = run_plan(b);
   if (s != SPF_OK) {
     return s;
   }
@@ -11818,7 +12155,53 @@ int run_screen(spf_query* q) {
   }
   SPF_LAUNCH(spf_whatif_screen_kernel, dim3(q->nq), dim3(256), 0, g->stream, a);
   HIP_TRY(hipGetLastError());
-  if (q->repair && !q->wh_cand.empty()) {
+  if (q->repair && q->nfh) {
+    const spf_query* hq = q->hop;
+    WhatifHopArgs f{};
+    f.row = g->d_row;
+    f.col = g->d_col;
+    f.link = g->d_link;
+    f.slot = g->d_slot;
+    f.trbits = g->d_tr;
+    f.src = q->d_src;
+    f.ign_off = q->d_ign_off;
+    f.ign = q->d_ign;
+    f.skip = q->d_skip;
+    f.fh_q = q->d_fh;
+    f.fh_h = q->d_fh + q->nfh;
+    f.hop_row0 = q->d_fh + 2 * (size_t)q->nfh;
+    f.hop_cnt = f.hop_row0 + q->nhop;
+    f.hop_off = f.hop_cnt + q->nhop;
+    f.hop_nodes = f.hop_off + q->nhop;
+    f.rows = (const uint32_t*)hq->d_dist;
+    f.rows_pitch = hq->Vp;
+    f.dist_out = (uint32_t*)q->d_dist;
+    f.nh_out = q->d_nh;
+    f.nh_off = q->d_nh_off;
+    f.nh_w = q->d_nh_w;
+    f.V = g->V;
+    f.Vp = q->Vp;
+    f.scale = (q->flags & SPF_F_UNIT_METRIC) ? 1u : g->uniform;
+    f.want_nh = (q->flags & SPF_F_NEXTHOPS) ? 1u : 0u;
+    if (rows64(hq) || !hq->d_dist) {
+      return fail(SPF_E_INVALID, "internal: first-hop rows are not 32-bit distance rows");
+    }
+    // after the screen (skip) on the side stream, behind the hop rows
+    hipStream_t fs = g->stream;
+    if (q->wh_stream) {
+      HIP_TRY(hipEventRecord(q->wh_ev0, g->stream));
+      HIP_TRY(hipStreamWaitEvent(q->wh_stream, q->wh_ev0, 0));
+      fs = q->wh_stream;
+    }
+    SPF_LAUNCH(spf_whatif_firsthop_kernel, dim3(q->nfh, (g->V + kFhChunk - 1) / kFhChunk),
+               dim3(256), 0, fs, f);
+    HIP_TRY(hipGetLastError());
+    if (q->wh_stream && q->wh_pull_cand.empty()) {
+      HIP_TRY(hipEventRecord(q->wh_ev1, q->wh_stream));
+      q->wh_pending = true;
+    }
+  }
+  if (q->repair && !q->wh_pull_cand.empty()) {
     WhatifHeavyArgs h{};
     h.row = g->d_row;
     h.col = g->d_col;
@@ -11845,8 +12228,8 @@ int run_screen(spf_query* q) {
     h.link_half = g->d_link_half;
     h.L = g->L;
     if (env_flag("OPENR_SPF_WHATIF_STATS", 0)) {
-      HIP_TRY(hipMalloc((void**)&h.stats, 6 * q->wh_cand.size() * 8));
-      HIP_TRY(hipMemset(h.stats, 0, 6 * q->wh_cand.size() * 8));
+      HIP_TRY(hipMalloc((void**)&h.stats, 6 * q->wh_pull_cand.size() * 8));
+      HIP_TRY(hipMemset(h.stats, 0, 6 * q->wh_pull_cand.size() * 8));
     }
     const size_t lds = q->wh_pull ? ((size_t)g->V + (g->V + 31) / 32) * 4
                                   : (3 * (size_t)g->V + 1 + (g->V + 31) / 32) * 4;
@@ -11865,11 +12248,11 @@ int run_screen(spf_query* q) {
       HIP_TRY(hipStreamWaitEvent(q->wh_stream, q->wh_ev0, 0));
     }
     if (q->wh_pull) {
-      SPF_LAUNCH(spf_whatif_pull_kernel, dim3((uint32_t)q->wh_cand.size()), dim3(kWhThreads),
-                 lds, hstream, h);
+      SPF_LAUNCH(spf_whatif_pull_kernel, dim3((uint32_t)q->wh_pull_cand.size()),
+                 dim3(kWhThreads), lds, hstream, h);
     } else {
-      SPF_LAUNCH(spf_whatif_heavy_kernel, dim3((uint32_t)q->wh_cand.size()), dim3(kWhThreads),
-                 lds, hstream, h);
+      SPF_LAUNCH(spf_whatif_heavy_kernel, dim3((uint32_t)q->wh_pull_cand.size()),
+                 dim3(kWhThreads), lds, hstream, h);
     }
     HIP_TRY(hipGetLastError());
     if (side) {
@@ -11877,15 +12260,15 @@ int run_screen(spf_query* q) {
       q->wh_pending = true;
     }
     if (h.stats) {
-      std::vector<unsigned long long> hs(6 * q->wh_cand.size());
+      std::vector<unsigned long long> hs(6 * q->wh_pull_cand.size());
       HIP_TRY(hipStreamSynchronize(side ? q->wh_stream : g->stream));
       HIP_TRY(hipMemcpy(hs.data(), h.stats, hs.size() * 8, hipMemcpyDeviceToHost));
       HIP_TRY(hipFree(h.stats));
-      for (size_t i = 0; i < q->wh_cand.size(); ++i) {
+      for (size_t i = 0; i < q->wh_pull_cand.size(); ++i) {
         const unsigned long long* o = hs.data() + 6 * i;
         if (o[4]) {
           fprintf(stderr, "[whatif heavy] query %u: init %llu bfs %llu rows %llu masks %llu ticks "
-                  "(100 MHz), %llu levels, %llu reached\n", q->wh_cand[i], o[0], o[1], o[2], o[3],
+                  "(100 MHz), %llu levels, %llu reached\n", q->wh_pull_cand[i], o[0], o[1], o[2], o[3],
                   o[4], o[5]);
         }
       }

@@ -150,20 +150,25 @@ def test_repair_fabric_clos(gpu_ready, monkeypatch):
     g.close()
 
 
-@pytest.mark.parametrize("pull", ["1", "0"])
+@pytest.mark.parametrize("mode", ["firsthop", "pull", "queue"])
 @pytest.mark.parametrize("case", ["fabric", "uniform5"])
-def test_source_link_failures_heavy_kernel(gpu_ready, case, pull, monkeypatch):
+def test_source_link_failures_heavy_kernel(gpu_ready, case, mode, monkeypatch):
     """What-ifs that fail a link of the source itself on a uniform-metric
-    area (K is most of the graph) run on one 1,024-thread workgroup per
-    query: a BFS and a level-by-level next-hop pass, in pull form over the
-    sliced ELL (spf_whatif_pull_kernel, default) or over a BFS queue
+    area (K is most of the graph).  Queries whose every ignored link is at
+    the source take the first-hop form (spf_whatif_firsthop_kernel over one
+    nested batch of the source's neighbour rows, default); the others, and
+    all of them with OPENR_SPF_WHATIF_FIRSTHOP=0, run on one 1,024-thread
+    workgroup per query: a BFS and a level-by-level next-hop pass, in pull
+    form over the sliced ELL (spf_whatif_pull_kernel) or over a BFS queue
     (spf_whatif_heavy_kernel, OPENR_SPF_WHATIF_PULL=0).  Rows and masks
-    equal the same batch with neither (OPENR_SPF_WHATIF_HEAVY=0:
+    equal the same batch with none of them (OPENR_SPF_WHATIF_HEAVY=0:
     spf_sssp_kernel from scratch) and the DijkstraQ replay; parallel links
     of the source keep its neighbour bit."""
     monkeypatch.setenv("OPENR_SPF_MSBFS_IGN", "0")
-    monkeypatch.setenv("OPENR_SPF_WHATIF_PULL", pull)
-    kname = "spf_whatif_pull_kernel" if pull == "1" else "spf_whatif_heavy_kernel"
+    monkeypatch.setenv("OPENR_SPF_WHATIF_FIRSTHOP", "1" if mode == "firsthop" else "0")
+    monkeypatch.setenv("OPENR_SPF_WHATIF_PULL", "0" if mode == "queue" else "1")
+    kname = {"firsthop": "spf_whatif_firsthop_kernel", "pull": "spf_whatif_pull_kernel",
+             "queue": "spf_whatif_heavy_kernel"}[mode]
     rng = random.Random(306)
     if case == "fabric":
         topo = TP.fabric(1200)
@@ -192,6 +197,7 @@ def test_source_link_failures_heavy_kernel(gpu_ready, case, pull, monkeypatch):
     r = g.query(qs, flags, ignore=ign).run()
     monkeypatch.delenv("OPENR_SPF_WHATIF_HEAVY")
     assert kname not in r.kernels()
+    assert "spf_whatif_firsthop_kernel" not in r.kernels()
     for i in range(len(qs)):
         assert (q.dist(i) == r.dist(i)).all(), i
         assert (q.nexthops(i) == r.nexthops(i)).all(), i

@@ -178,6 +178,18 @@ __device__ __forceinline__ uint32_t grp_min(uint32_t x, int G) {
   return x;
 }
 
+// Lanes per node for a list of n nodes over a kBlock workgroup: the graph's
+// G (median degree), doubled while the whole list still runs in one pass
+// (round 6): a short list -- a what-if repair's K, an SSSP's first levels --
+// then walks a 84- or 190-edge row in 2-3 steps instead of 21-48 at G = 4
+// (the fabric's median degree), each step a dependent global-load trip
+__device__ __forceinline__ uint32_t lanes_for(uint32_t n, uint32_t G) {
+  while (G < 64 && kBlock / (2 * G) >= n) {
+    G <<= 1;
+  }
+  return G;
+}
+
 __device__ __forceinline__ uint64_t grp_or(uint64_t x, int G) {
   for (int o = G >> 1; o > 0; o >>= 1) {
     x |= (uint64_t)__shfl_xor((unsigned long long)x, o, G);
@@ -497,16 +509,29 @@ __device__ uint32_t whatif_repair_init(
     const SsspArgs& a, uint32_t src, uint32_t* dist, uint32_t* kb, uint32_t* okb,
     uint32_t* act, const uint32_t* tr, QT* queue, uint32_t* ctl, const uint32_t* ilist,
     uint32_t nign, const IgnSet& ig) {
-  const uint32_t tid = threadIdx.x, G = a.G, V = a.V, nbw = a.nbw;
-  const uint32_t lg = tid & (G - 1), grp = tid / G, ngrp = kBlock / G;
+  (void)act;
+  const uint32_t tid = threadIdx.x, V = a.V, nbw = a.nbw;
+  // K and ok grow as LDS worklists (round 6): |K| is a handful of nodes, and
+  // compacting the V-bit maps after every closure level (a block scan each)
+  // was most of this prologue.  K lists into queue[0 ..), ok into
+  // queue[V / 2 ..) (|ok| <= |K| <= V / 4 once the size check passed); the
+  // tails live in the control words the scans leave alone.
+  uint32_t* ktail = ctl + (kCtlWords - 2);
+  uint32_t* otail = ctl + (kCtlWords - 3);
+  QT* olist = queue + V / 2;
   auto usable = [&](uint32_t u) { return u == src || ((tr[u >> 5] >> (u & 31)) & 1u); };
   auto ignored = [&](uint32_t e) { return ig.has(a.link[e]); };
-  auto mark = [&](uint32_t* bm, uint32_t v) {
+  auto push = [&](uint32_t* bm, uint32_t* tail, QT* list, uint32_t v) {
     const uint32_t m = 1u << (v & 31);
     if (!(atomicOr(&bm[v >> 5], m) & m)) {
-      atomicOr(&act[v >> 5], m);
+      list[atomicAdd(tail, 1u)] = (QT)v; // each node once: at most V entries
     }
   };
+  if (tid == 0) {
+    *ktail = 0;
+    *otail = 0;
+  }
+  __syncthreads();
   // seeds: heads of tight ignored halves
   for (uint32_t i = tid; i < 2 * nign; i += kBlock) {
     const uint32_t l = ilist[i >> 1]; // the query's list (the LDS copy may be a hash set)
@@ -517,30 +542,30 @@ __device__ uint32_t whatif_repair_init(
     const uint32_t u = a.col[a.rev[e]], v = a.col[e];
     const uint32_t du = dist[u];
     if (du != kInf32 && usable(u) && du + (UNIT ? 1u : a.wout[e]) == dist[v]) {
-      mark(kb, v);
+      push(kb, ktail, queue, v);
     }
   }
   __syncthreads();
-  // K: closure over tight usable non-ignored edges
-  uint32_t ksize = 0;
+  // K: closure over tight usable non-ignored edges, level by level
+  uint32_t head = 0;
   for (;;) {
-    const uint32_t n = compact_bits<QT>(act, nbw, queue, ctl + 1);
-    __syncthreads();
-    ksize += n;
-    if (!n) {
-      break;
-    }
-    if (ksize * 4 > V) {
+    const uint32_t tail = *ktail;
+    __syncthreads(); // every lane has its tail before this level pushes
+    if (tail * 4 > V) {
       // K spans most of the graph (a failure next to the source): the
       // caller's run from scratch is cheaper than repairing it
       for (uint32_t w = tid; w < nbw; w += kBlock) {
         kb[w] = 0;
-        act[w] = 0;
       }
       __syncthreads();
       return kInf32;
     }
-    for (uint32_t i = grp; i < n; i += ngrp) {
+    if (head == tail) {
+      break;
+    }
+    const uint32_t G = lanes_for(tail - head, a.G);
+    const uint32_t lg = tid & (G - 1), grp = tid / G, ngrp = kBlock / G;
+    for (uint32_t i = head + grp; i < tail; i += ngrp) {
       const uint32_t u = queue[i];
       if (!usable(u)) {
         continue;
@@ -549,47 +574,49 @@ __device__ uint32_t whatif_repair_init(
       for (uint32_t e = a.row[u] + lg; e < a.row[u + 1]; e += G) {
         const uint32_t v = a.col[e];
         if (du + (UNIT ? 1u : a.wout[e]) == dist[v] && !bit_test(kb, v) && !ignored(e)) {
-          mark(kb, v);
+          push(kb, ktail, queue, v);
         }
       }
     }
+    head = tail;
     __syncthreads();
   }
+  const uint32_t nk = head;
   // ok seeds: K nodes with a tight usable non-ignored in-edge from outside K
-  // (K listed into the queue first: |K| is usually a handful of nodes)
-  for (uint32_t w = tid; w < nbw; w += kBlock) {
-    act[w] = kb[w];
-  }
-  __syncthreads();
-  const uint32_t nk = compact_bits<QT>(act, nbw, queue, ctl + 1);
-  __syncthreads();
-  for (uint32_t i = grp; i < nk; i += ngrp) {
-    const uint32_t v = queue[i];
-    const uint32_t dv = dist[v];
-    bool found = false;
-    for (uint32_t e = a.row[v] + lg; e < a.row[v + 1] && !found; e += G) {
-      const uint32_t u = a.col[e];
-      if (bit_test(kb, u) || !usable(u)) {
-        continue;
+  {
+    const uint32_t G = lanes_for(nk, a.G);
+    const uint32_t lg = tid & (G - 1), grp = tid / G, ngrp = kBlock / G;
+    for (uint32_t i = grp; i < nk; i += ngrp) {
+      const uint32_t v = queue[i];
+      const uint32_t dv = dist[v];
+      bool found = false;
+      for (uint32_t e = a.row[v] + lg; e < a.row[v + 1] && !found; e += G) {
+        const uint32_t u = a.col[e];
+        if (bit_test(kb, u) || !usable(u)) {
+          continue;
+        }
+        const uint32_t du = dist[u];
+        found = du != kInf32 && du + (UNIT ? 1u : a.win[e]) == dv && !ignored(e);
       }
-      const uint32_t du = dist[u];
-      found = du != kInf32 && du + (UNIT ? 1u : a.win[e]) == dv && !ignored(e);
-    }
-    found = grp_min(found ? 0u : 1u, (int)G) == 0;
-    if (found && lg == 0) {
-      mark(okb, v);
+      found = grp_min(found ? 0u : 1u, (int)G) == 0;
+      if (found && lg == 0) {
+        push(okb, otail, olist, v);
+      }
     }
   }
   __syncthreads();
   // ok: closure inside K over tight usable non-ignored edges
+  uint32_t oh = 0;
   for (;;) {
-    const uint32_t n = compact_bits<QT>(act, nbw, queue, ctl + 1);
+    const uint32_t ot = *otail;
     __syncthreads();
-    if (!n) {
+    if (oh == ot) {
       break;
     }
-    for (uint32_t i = grp; i < n; i += ngrp) {
-      const uint32_t u = queue[i];
+    const uint32_t G = lanes_for(ot - oh, a.G);
+    const uint32_t lg = tid & (G - 1), grp = tid / G, ngrp = kBlock / G;
+    for (uint32_t i = oh + grp; i < ot; i += ngrp) {
+      const uint32_t u = olist[i];
       if (!usable(u)) {
         continue;
       }
@@ -598,28 +625,29 @@ __device__ uint32_t whatif_repair_init(
         const uint32_t v = a.col[e];
         if (bit_test(kb, v) && !bit_test(okb, v) && du + (UNIT ? 1u : a.wout[e]) == dist[v] &&
             !ignored(e)) {
-          mark(okb, v);
+          push(okb, otail, olist, v);
         }
       }
     }
+    oh = ot;
     __syncthreads();
   }
-  // K \ ok reset; all of K queued for the PULL step
-  for (uint32_t w = tid; w < nbw; w += kBlock) {
-    uint32_t bad = kb[w] & ~okb[w];
-    act[w] = kb[w];
-    kb[w] = 0;
-    okb[w] = 0;
-    while (bad) {
-      const uint32_t k = __ffs(bad) - 1;
-      bad &= bad - 1;
-      dist[w * 32 + k] = kInf32;
+  // K \ ok reset; all of K (queue[0, nk)) goes to the PULL step
+  for (uint32_t i = tid; i < nk; i += kBlock) {
+    const uint32_t v = queue[i];
+    if (!bit_test(okb, v)) {
+      dist[v] = kInf32;
     }
   }
   __syncthreads();
-  const uint32_t n = compact_bits<QT>(act, nbw, queue, ctl + 1);
+  // the maps leave clear (only K's bits were set)
+  for (uint32_t i = tid; i < nk; i += kBlock) {
+    const uint32_t v = queue[i];
+    kb[v >> 5] = 0;
+    okb[v >> 5] = 0;
+  }
   __syncthreads();
-  return n;
+  return nk;
 }
 
 // WMAX: max next-hop words (0 = distances only).  UNIT: every hop costs 1.
@@ -787,6 +815,8 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
         pull_first = false; // the queue holds K: straight to the PULL step
       } else {
       // ---- PUSH: changed nodes mark the neighbours they can improve or tie
+      const uint32_t G = lanes_for(qlen, a.G);
+      const uint32_t lg = tid & (G - 1), grp = tid / G, ngrp = kBlock / G;
       for (uint32_t i = grp; i < qlen; i += ngrp) {
         const uint32_t u = queue[i];
         if (u != src && !((tr[u >> 5] >> (u & 31)) & 1u)) {
@@ -816,6 +846,8 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
       }
 
       // ---- PULL: marked nodes recompute (dist, next hops) from all in-edges
+      const uint32_t G = lanes_for(qlen, a.G);
+      const uint32_t lg = tid & (G - 1), grp = tid / G, ngrp = kBlock / G;
       for (uint32_t i = grp; i < qlen; i += ngrp) {
         const uint32_t v = queue[i];
         const uint32_t beg = a.row[v], end = a.row[v + 1];

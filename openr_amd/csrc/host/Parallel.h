@@ -214,10 +214,54 @@ void parallelFor(size_t n, unsigned threads, Fn&& fn, size_t chunk = 16) {
 // build records its shard counts in the RouteDb and the release reuses them.
 inline unsigned routeShards(size_t routes) { return hostThreads(routes, 64); }
 
-// fn(shard) for every shard in [0, shards), one shard per work item.
+// fn(shard) for every shard in [0, shards): shard s runs on pool worker s
+// (s = 0: the calling thread) in every section, not on whichever worker
+// claims it first, so releaseRouteDb frees each shard's routes on the very
+// thread (and malloc arena / tcache) that built them (round 6; with dynamic
+// claiming most frees crossed threads).  OPENR_SHARD_DYNAMIC=1: the old
+// dynamic hand-out.  The first exception (by shard) is rethrown after every
+// shard ran.
 template <class Fn>
 void parallelShards(unsigned shards, Fn&& fn) {
-  parallelFor(shards, shards, [&](size_t s, unsigned) { fn((unsigned)s); }, 1);
+  static const bool dynamic = [] {
+    const char* e = std::getenv("OPENR_SHARD_DYNAMIC");
+    return e && std::atoi(e) != 0;
+  }();
+  if (dynamic) {
+    parallelFor(shards, shards, [&](size_t s, unsigned) { fn((unsigned)s); }, 1);
+    return;
+  }
+  if (shards <= 1) {
+    for (unsigned s = 0; s < shards; ++s) {
+      fn(s);
+    }
+    return;
+  }
+  std::vector<std::exception_ptr> errors(shards);
+  auto body = [&](unsigned w) {
+    try {
+      fn(w);
+    } catch (...) {
+      errors[w] = std::current_exception();
+    }
+  };
+  const std::function<void(unsigned)> job(body);
+  if (!HostPool::get().run(shards, job)) {
+    std::vector<std::thread> pool;
+    pool.reserve(shards - 1);
+    for (unsigned w = 1; w < shards; ++w) {
+      pool.emplace_back(body, w);
+    }
+    body(0);
+    for (auto& t : pool) {
+      t.join();
+    }
+  }
+  for (auto& e : errors) {
+    if (e) {
+      std::rethrow_exception(e);
+    }
+  }
 }
 
 } // namespace openr

@@ -451,6 +451,10 @@ struct SsspArgs {
   // queries beyond the first gridDim.x are claimed from this counter (zeroed
   // per launch); nullptr: static stride
   uint32_t* qctr = nullptr;
+  // repair batches: [0] heavy count, [1] total, [2 ..] the queries to run,
+  // heavy (skip 2) first (spf_whatif_worklist_kernel); nullptr: every query
+  // is claimed and its skip flag tested (two passes)
+  const uint32_t* wl = nullptr;
   // OPENR_SPF_WHATIF_STATS: repaired / from-scratch queries, |K| total, PULL
   // rounds, and wall-clock ticks (100 MHz) of copy / init / rounds / output
   unsigned long long* stats = nullptr;
@@ -706,11 +710,15 @@ __global__ __launch_bounds__(kBlock) void spf_sssp_kernel(SsspArgs a) {
   // repair batches claim in two passes: first the queries whose failed link
   // leaves the source (skip == 2, the screen's mark: their K is most of the
   // graph and they run from scratch), then the rest (skip == 0)
-  const bool two_pass = rep && a.qctr;
-  const uint32_t nclaim = two_pass ? 2 * a.nq : a.nq;
+  // (with the work list every claim is a query to run: the screened ones
+  // no longer cost a claim -- one contended counter add and two barriers each)
+  const bool listed = rep && a.wl != nullptr;
+  const bool two_pass = rep && a.qctr && !listed;
+  const uint32_t nclaim = listed ? a.wl[1] : (two_pass ? 2 * a.nq : a.nq);
   for (uint32_t c = blockIdx.x; c < nclaim; c = next_query(c)) {
-    const uint32_t q = c < a.nq ? c : c - a.nq;
-    if (two_pass ? a.skip[q] != (c < a.nq ? 2u : 0u) : (a.skip && a.skip[q])) {
+    const uint32_t q = listed ? a.wl[2 + c] : (c < a.nq ? c : c - a.nq);
+    if (!listed &&
+        (two_pass ? a.skip[q] != (c < a.nq ? 2u : 0u) : (a.skip && a.skip[q]))) {
       continue; // uniform per block
     }
     const uint32_t src = a.src[q];
@@ -6160,6 +6168,36 @@ __global__ __launch_bounds__(kWhThreads) void spf_whatif_pull_kernel(WhatifHeavy
   }
 }
 
+// The repair SSSP's work list (round 6): the queries the screen left to it,
+// heavy ones (skip 2, run from scratch) first, then the repairs (skip 0),
+// compacted from the skip flags by one workgroup.  wl[0] = heavy count,
+// wl[1] = total, wl[2 ..] = queries.
+__global__ __launch_bounds__(1024) void spf_whatif_worklist_kernel(
+    const uint32_t* skip, uint32_t nq, uint32_t* wl) {
+  __shared__ uint32_t scan[32];
+  uint32_t base = 0;
+  for (uint32_t pass = 0; pass < 2; ++pass) {
+    const uint32_t want = pass == 0 ? 2u : 0u;
+    for (uint32_t b0 = 0; b0 < nq; b0 += 1024) {
+      const uint32_t q = b0 + threadIdx.x;
+      const uint32_t f = q < nq && skip[q] == want ? 1u : 0u;
+      uint32_t total = 0;
+      const uint32_t off = block_excl_scan<1024>(f, scan, &total);
+      if (f) {
+        wl[2 + base + off] = q;
+      }
+      base += total;
+      __syncthreads(); // scan[] is rewritten by the next chunk
+    }
+    if (pass == 0 && threadIdx.x == 0) {
+      wl[0] = base;
+    }
+  }
+  if (threadIdx.x == 0) {
+    wl[1] = base;
+  }
+}
+
 // Source-link failures, first-hop form (round 6, spf_whatif_firsthop_kernel,
 // OPENR_SPF_WHATIF_FIRSTHOP=0 keeps the pull kernel for them).  On a uniform
 // metric a shortest path from s never returns to s, so for a query q that
@@ -8258,6 +8296,7 @@ struct spf_query {
   uint64_t* d_nh = nullptr;
   uint64_t* d_key = nullptr; // wide plan settle keys (SPF_F_ORDER)
   uint32_t* d_qctr = nullptr; // dstep source-claim counter
+  uint32_t* d_wl = nullptr;   // repair work list (spf_whatif_worklist_kernel)
   uint32_t* d_big = nullptr;  // nh_levels: queries with more than kNsHeldMax mask words
   uint32_t* d_held_order = nullptr; // OPENR_NL_ORDER=1: XCD-contiguous held-kernel work order
   // the v2 next-hop pass (spf_nh_levels_v2_kernel, OPENR_NL_V2): solo / group
@@ -9008,7 +9047,7 @@ void free_query(spf_query* q) {
         q->d_dist, (void*)q->d_nh,
         (void*)q->d_lvl, (void*)q->d_flags, (void*)q->d_perm,
         (void*)q->d_slab, (void*)q->d_msd, (void*)q->d_base_of,
-        (void*)q->d_skip, (void*)q->d_key, (void*)q->d_qctr, (void*)q->d_scatter,
+        (void*)q->d_skip, (void*)q->d_key, (void*)q->d_qctr, (void*)q->d_wl, (void*)q->d_scatter,
         (void*)q->d_trace, (void*)q->d_big, (void*)q->d_held_order, (void*)q->d_zl,
         (void*)q->d_zvar, (void*)q->d_ms_mask, (void*)q->d_ms_flag,
         (void*)q->d_ovf, q->narrow ? (void*)q->d_nhb : nullptr, (void*)q->d_tcs, q->d_v2,
@@ -11122,6 +11161,10 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
         if (!q->d_qctr && pool_malloc((void**)&q->d_qctr, 4) != hipSuccess) {
           return bail(fail(SPF_E_NOMEM, "what-if claim counter"));
         }
+        if (env_flag("OPENR_SPF_WHATIF_WORKLIST", 1) &&
+            pool_malloc((void**)&q->d_wl, ((size_t)nq + 2) * 4) != hipSuccess) {
+          return bail(fail(SPF_E_NOMEM, "what-if work list"));
+        }
         // queries whose failed link leaves the source: their own BFS launch
         // on a uniform-metric area (spf_whatif_heavy_kernel)
         // (both kernels read v's out-edges as its in-edges: every half-edge
@@ -11376,6 +11419,12 @@ int launch_sssp(spf_query* q) {
     a.L = g->L;
     a.qctr = q->d_qctr;
     HIP_TRY(hipMemsetAsync(q->d_qctr, 0, 4, g->stream));
+    if (q->d_wl) {
+      SPF_LAUNCH(spf_whatif_worklist_kernel, dim3(1), dim3(1024), 0, g->stream, q->d_skip,
+                 q->nq, q->d_wl);
+      HIP_TRY(hipGetLastError());
+      a.wl = q->d_wl;
+    }
     if (env_flag("OPENR_SPF_WHATIF_STATS", 0)) {
       HIP_TRY(hipMalloc((void**)&a.stats, 8 * sizeof(unsigned long long)));
       HIP_TRY(hipMemsetAsync(a.stats, 0, 8 * sizeof(unsigned long long), g->stream));

@@ -1013,8 +1013,10 @@ def whatif_batch(world, rank, local, dist, steps=3, cpu_lines=True):
         "screened_queries": screened,
         "kernels_launched": launched,
         "roofline": {"bound": "hbm", "kernel": "what-if plan: " + " + ".join(launched),
-                     "note": "latency-bound: the per-area baseline SSSP runs on one workgroup before "
-                             "the batch can start", "algorithmic_bytes": int(alg),
+                     "note": "latency-bound: two dependent chains per area (baseline SSSP, screen, "
+                             "then the repair SSSP: one workgroup per query, ~40 us of dependent "
+                             "steps each on the fabric; DESIGN.md section 3)",
+                     "algorithmic_bytes": int(alg),
                      "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": wi_traffic,
                      "traffic_source": wi_src,

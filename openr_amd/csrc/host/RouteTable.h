@@ -54,9 +54,20 @@ class AllNodesRouteTable {
   // in this area, none of them by a border node; the announcers are the
   // in-area entries (for an interior node every other area's announcer is
   // unreachable, Decision.cpp:555-579)
+  // bgpColumns (round 6, AllAreasRouteTable without bgpUseIgpMetric): BGP
+  // prefixes on the device too.  With no IGP metric in the vector and every
+  // in-graph announcer reachable from every node, the metric-vector
+  // selection (runBestPathSelectionBgp, Decision.cpp:714-803) has the same
+  // winners for every node, so it runs once on the host and the kernel takes
+  // the winners (drained filter applied) as the column's announcers; a node
+  // among them gets no route (selectEcmpBgp :805-866).  bestPrefixEntry,
+  // bestArea and the loopback next hop are the selection's; doNotInstall =
+  // bgpDryRun.  A prefix with an announcer some node cannot reach stays on
+  // the host.  diff() refuses tables with BGP columns.
   AllNodesRouteTable(
       const LinkState& ls, const PrefixState& ps, bool enableV4 = true, bool computeLfa = false,
-      const std::unordered_set<std::string>* borderNodes = nullptr);
+      const std::unordered_set<std::string>* borderNodes = nullptr, bool bgpColumns = false,
+      bool bgpDryRun = false);
   ~AllNodesRouteTable();
   AllNodesRouteTable(const AllNodesRouteTable&) = delete;
   AllNodesRouteTable& operator=(const AllNodesRouteTable&) = delete;
@@ -93,6 +104,8 @@ class AllNodesRouteTable {
   const std::string& nodeName(uint32_t id) const { return names_.at(id); }
   // the unicast prefixes the kernel serves (routes() covers exactly these)
   const std::vector<thrift::IpPrefix>& prefixes() const { return prefixes_; }
+  // BGP prefixes among them (bgpColumns)
+  size_t numBgpPrefixes() const { return nbgp_; }
 
  private:
   struct Row {
@@ -116,6 +129,12 @@ class AllNodesRouteTable {
     uint32_t id;
     thrift::PrefixEntry entry;
   };
+  // a BGP column's host-side selection (bgpColumns)
+  struct BgpSel {
+    thrift::PrefixEntry bestEntry;
+    std::string bestArea;
+    std::optional<thrift::NextHopThrift> bestNexthop; // nullopt: no route anywhere
+  };
   std::string area_;
   bool enableV4_;
   bool lfa_;
@@ -125,6 +144,9 @@ class AllNodesRouteTable {
   std::vector<std::shared_ptr<Link>> halfLink_; // half-edge -> Link
   std::vector<thrift::IpPrefix> prefixes_;
   std::vector<std::vector<Announcer>> announcers_;
+  std::vector<std::optional<BgpSel>> bgp_; // per prefix (set: a BGP column)
+  size_t nbgp_{0};
+  bool bgpDryRun_{false};
   // node-label columns: column prefixes_.size() + k is owners_[k]
   struct LabelOwner {
     int32_t label;
@@ -176,6 +198,15 @@ class AllAreasRouteTable {
   size_t lastHostRoutes() const { return lastHost_; }
   bool isBorder(const std::string& node) const { return border_.count(node) > 0; }
   size_t numTables() const { return tables_.size(); }
+  // BGP prefixes the device tables serve (round 6; AllNodesRouteTable
+  // bgpColumns)
+  size_t numBgpDevicePrefixes() const {
+    size_t n = 0;
+    for (const auto& [_, t] : tables_) {
+      n += t->numBgpPrefixes();
+    }
+    return n;
+  }
 
  private:
   const std::unordered_map<std::string, LinkState>& areas_;

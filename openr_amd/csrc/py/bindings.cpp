@@ -353,6 +353,7 @@ PYBIND11_MODULE(_openr_spf, m) {
       .def_property_readonly("last_table_routes", &AllAreasRouteTable::lastTableRoutes)
       .def_property_readonly("last_host_routes", &AllAreasRouteTable::lastHostRoutes)
       .def_property_readonly("num_tables", &AllAreasRouteTable::numTables)
+      .def_property_readonly("bgp_device_prefixes", &AllAreasRouteTable::numBgpDevicePrefixes)
       .def("is_border", &AllAreasRouteTable::isBorder);
 
   py::class_<AllSourcesTable>(m, "AllSourcesTable")

@@ -393,5 +393,57 @@ def test_all_areas_route_table_equals_oracle(gpu_ready, seed, n_areas, bgp):
             table_routes += t.last_table_routes
             host_routes += t.last_host_routes
         assert table_routes > 0  # the device tables served the interior nodes
-        if n_areas > 1 or bgp:
-            assert host_routes > 0  # border nodes / BGP / SR-MPLS on the host
+        if n_areas > 1:
+            assert host_routes > 0  # border nodes / multi-area routes on the host
+
+
+def _bgp_network(seed, n_nodes=40, split=False):
+    """One area with BGP prefixes (RZ.random_network's metric-vector
+    entries).  split: two components joined by nothing, so BGP prefixes with
+    announcers on both sides are unreachable from some nodes."""
+    from tests import randomized as RZ
+
+    names, adj_dbs, prefix_dbs = RZ.random_network(seed, n_nodes=n_nodes, n_links=n_nodes * 3,
+                                                   bgp=True)
+    if split:
+        half = set(names[: n_nodes // 2])
+        for db in adj_dbs["0"]:
+            db.adjacencies = [a for a in db.adjacencies
+                              if (a.otherNodeName in half) == (db.thisNodeName in half)]
+    return names, adj_dbs, prefix_dbs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,dry,igp,split", [(11, False, False, False), (12, True, False, False),
+                                                 (13, False, True, False), (14, False, False, True),
+                                                 (15, True, False, True)])
+def test_all_areas_route_table_bgp_on_device(gpu_ready, seed, dry, igp, split):
+    """BGP prefixes (IP / SP_ECMP) in the device table (round 6): without the
+    IGP cost in the metric vector and with every announcer reachable from
+    every node, the metric-vector selection (runBestPathSelectionBgp,
+    Decision.cpp:714-803) has the same winners at every node, so it runs once
+    on the host and the winners are the column's announcers
+    (selectEcmpBgp :805-866: no route at a winner, bestPrefixEntry / loopback
+    next hop of the selection, doNotInstall = bgpDryRun).  Every node's
+    RouteDb equals the oracle's, with bgpDryRun, with bgpUseIgpMetric (BGP
+    then stays on the host) and on a split graph (prefixes some node cannot
+    reach stay on the host)."""
+    from oracle import _oracle_ref as O
+    import openr_amd._openr_spf as E
+    from tests import randomized as RZ
+
+    names, adj_dbs, prefix_dbs = _bgp_network(5200 + seed, split=split)
+    ea, ep = RZ.load(E, adj_dbs, prefix_dbs, seed)
+    oa, op = RZ.load(O, adj_dbs, prefix_dbs, seed)
+    for lfa in (False, True):
+        t = E.AllAreasRouteTable(ea, ep, True, lfa, dry, igp)
+        if igp:
+            assert t.bgp_device_prefixes == 0
+        elif not split:
+            assert t.bgp_device_prefixes > 0
+        for node in names:
+            os_ = O.SpfSolver(node, True, lfa, False, dry, igp)
+            want = os_.buildRouteDb(node, oa, op)
+            got = t.route_db(node)
+            assert got == want, (node, lfa)
+        assert t.num_tables == 1

@@ -41,6 +41,7 @@ for q in qs.values():
 torch.cuda.synchronize()
 for r in range(rounds):
     for mode, q in qs.items():
+        os.environ[env] = mode  # (switches read at launch, e.g. OPENR_NL_TILEW)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -51,6 +52,10 @@ for r in range(rounds):
         out[mode]["dist_ms"].append(sum(x[0] for x in h) / len(h))
         out[mode]["nh_ms"].append(sum(x[1] for x in h) / len(h))
 a, b = qs[modes[0]], qs[modes[1]]
+os.environ[env] = modes[0]
+a.run()
+os.environ[env] = modes[1]
+b.run()
 same = bool((a.fetch_nexthops(0, csr.num_nodes) == b.fetch_nexthops(0, csr.num_nodes)).all())
 res = {"env": env}
 res.update({env + "=" + k: {kk: round(float(np.median(v)), 4) for kk, v in d.items()} for k, d in out.items()})

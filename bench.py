@@ -839,6 +839,7 @@ def ksp2_route_db(topo, device, iters=2):
                      "decision.route_prefix_pool_us", "decision.route_merge_us",
                      "decision.route_label_us", "decision.route_release_us",
                      "decision.kth_trace_us", "decision.kth_memo_clear_us", "decision.kth2_trace_us",
+                     "decision.kth_todo_us", "decision.kth_lists_us", "decision.kth_fill_us",
                      "decision.kth2_base_us", "decision.ksp2_best_us", "decision.ksp2_paths_us",
                      "decision.ksp2_nexthops_us", "decision.ksp2_rest_us",
                      "decision.kth2_device_trace_us", "decision.kth2_device_traces",

@@ -2674,20 +2674,25 @@ std::vector<LinkState::Path> const& LinkState::getKthPaths(
 
 void LinkState::prefetchKthPaths(
     const std::string& src, const std::vector<std::string>& dests) const {
+  const auto tAll = std::chrono::steady_clock::now();
   auto& eng = engine();
   auto sid = eng.ids.find(src);
   if (sid == eng.ids.end()) {
     return;
   }
-  // destinations whose second pass is still to run
+  // destinations whose second pass is still to run: the name and memo
+  // lookups on the host pool (~230 ns each serially: 2.3 ms for the
+  // fabric's 9,975), then the duplicates dropped in order
   std::vector<std::pair<const std::string*, uint32_t>> todo;
   {
-    std::shared_lock<std::shared_mutex> rv(eng.viewMu);
-    std::unordered_set<uint32_t> seen;
-    for (const auto& d : dests) {
+    std::shared_lock<std::shared_mutex> rv(eng.viewMu); // (held for the workers too)
+    const size_t n = dests.size();
+    std::vector<uint32_t> idOf(n, ~0u); // ~0u: unknown node, or nothing to run
+    parallelFor(n, hostThreads(n, 256), [&](size_t i, unsigned) {
+      const auto& d = dests[i];
       auto did = eng.ids.find(d);
-      if (did == eng.ids.end() || !seen.insert(did->second).second) {
-        continue;
+      if (did == eng.ids.end()) {
+        return;
       }
       const KthKey k2{src, d, 2};
       KthStripe& stripe = kthStripe(k2);
@@ -2697,15 +2702,24 @@ void LinkState::prefetchKthPaths(
         known = stripe.ids.count(k2) > 0;
       }
       auto pf = eng.kthPrefetch.find({sid->second, did->second});
-      if (known || (pf != eng.kthPrefetch.end() && pf->second)) {
-        continue;
+      if (!known && !(pf != eng.kthPrefetch.end() && pf->second)) {
+        idOf[i] = did->second;
       }
-      todo.emplace_back(&d, did->second);
+    }, 64);
+    std::vector<uint8_t> seen(eng.names.size(), 0);
+    for (size_t i = 0; i < n; ++i) {
+      if (idOf[i] != ~0u && !seen[idOf[i]]) {
+        seen[idOf[i]] = 1;
+        todo.emplace_back(&dests[i], idOf[i]);
+      }
     }
   }
   if (todo.empty()) {
     return;
   }
+  Counters::add("decision.kth_todo_us", std::chrono::duration_cast<std::chrono::microseconds>(
+                                            std::chrono::steady_clock::now() - tAll)
+                                            .count());
   spfView(src, true); // every k = 1 trace reads the source's own SPF
   // k = 1 paths of every destination (independent traces over the same
   // row: host worker pool), then their links as the ignore lists
@@ -2744,10 +2758,14 @@ void LinkState::prefetchKthPaths(
     // runSpf each, LinkState.cpp:776-777); overflowed traces keep their row
     // for the host trace
     DeviceTraces tr;
+    const auto tDev = std::chrono::steady_clock::now();
     {
       std::lock_guard<std::mutex> dev(eng.devMu);
       tr = traceSecondPasses(eng, sources, dstIds, lists);
     }
+    const auto tFill = std::chrono::steady_clock::now();
+    Counters::add("decision.kth_lists_us",
+                  std::chrono::duration_cast<std::chrono::microseconds>(tDev - tTrace).count());
     traced = !tr.unsupported;
     if (!traced) {
       tr.count.clear();
@@ -2795,6 +2813,9 @@ void LinkState::prefetchKthPaths(
     }, 1);
     // one COUNT sample per SPF, as the per-entry add(1) of the fill
     Counters::addSamples("decision.spf_runs", filled.load(), filled.load());
+    Counters::add("decision.kth_fill_us", std::chrono::duration_cast<std::chrono::microseconds>(
+                                              std::chrono::steady_clock::now() - tFill)
+                                              .count());
     if (traced) {
       views = std::move(tr.rows);
       Counters::add("decision.kth2_device_traces", (int64_t)(tr.count.size() - overflowed));

@@ -1,6 +1,6 @@
 set -o pipefail
 # KSP2 todo lookups on the host pool: KSP2 goldens + bench breakdown
-D=gpurun_out/r06ae; mkdir -p $D
+D=gpurun_out/${TAG:-r06ae}; mkdir -p $D
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu -k "ksp2 or kth or trace" tests/ > $D/gpu_tests.log 2>&1 || { tail -40 $D/gpu_tests.log; exit 3; }
 tail -1 $D/gpu_tests.log
 timeout -k 10 400 python bench.py --no-wan --no-whatif --no-cpu-baseline --no-repair --steps 3 --warmup 1 > $D/b.json 2> $D/b.err || { tail -20 $D/b.err; exit 4; }

@@ -1563,6 +1563,8 @@ void SpfSolver::SpfSolverImpl::selectKsp2(
   // lookup in the adjacency databases per hop (same values: the engine's
   // metrics are the links' metrics, ksp2Labels_ the databases' labels)
   const bool byId = ksp2Fast_.ok && areaLinkStates.size() == 1;
+  // one next hop per path and area at most: no rehash while they go in
+  entry.nexthops.reserve(paths.size() * areaLinkStates.size());
   std::vector<std::pair<uint32_t, const thrift::PrefixEntry*>> destCache;
   for (const auto& path : paths) {
     if (path.size() == 0) {

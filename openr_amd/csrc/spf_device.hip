@@ -10636,7 +10636,13 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
           }
         }
       }
-      if (nq >= 32 || (nq + extra.size() >= 32 && env_flag("OPENR_SPF_MSBFS_FEW", 1))) {
+      // (and a small area, one node per MS-BFS thread, at any batch size: a
+      // RouteDb build's few sources on the 100-node grid take one MS-BFS
+      // workgroup and the level pass instead of one SSSP workgroup per
+      // source with next hops inline, 78.7 us, profiles/r06an;
+      // OPENR_SPF_MSBFS_SMALL=0 disables)
+      if (nq >= 32 || (nq + extra.size() >= 32 && env_flag("OPENR_SPF_MSBFS_FEW", 1)) ||
+          (V <= kMsThreads && env_flag("OPENR_SPF_MSBFS_SMALL", 1))) {
         rows_ok = true;
         helpers = std::move(extra);
       }
@@ -10811,7 +10817,7 @@ int spf_query_create(spf_graph* g, const spf_query_desc* desc, spf_query** out) 
   // many sources on a uniform metric: bit-parallel multi-source BFS
   // (OPENR_SPF_MSBFS=0 disables, =32 / =64 picks the batch width)
   if ((q->dist == DistPlan::BfsLds || q->dist == DistPlan::BfsGmem) &&
-      V <= kMsThreads * kMsMaxK && nq + helpers.size() >= 32) {
+      V <= kMsThreads * kMsMaxK && (nq + helpers.size() >= 32 || !helpers.empty())) {
     const char* env = getenv("OPENR_SPF_MSBFS");
     int width = env ? atoi(env) : 64;
     if (width == 64 && 2 * (size_t)V * 8 > kLdsLimit) {

@@ -80,8 +80,27 @@ struct LinkState::Engine {
   // never overwritten or leaked
   std::vector<spf_graph*> retired;
 
+  // the last batch's query (runBatch), rerun when the next batch asks for the
+  // same sources and flags with no ignore lists: transit bits are read at run
+  // time (spf_graph_set_transit keeps it), every other change of the graph
+  // (metric patches, link splices, a rebuild) drops it first.  A RouteDb
+  // build on a small area pays the plan, the allocations and the uploads of
+  // spf_query_create once instead of per build.
+  // (OPENR_LS_QUERY_CACHE=0 disables)
+  spf_query* lastQuery{nullptr};
+  std::vector<uint32_t> lastSources;
+  uint32_t lastFlags{0};
+  void dropQuery() {
+    if (lastQuery) {
+      spf_query_destroy(lastQuery);
+      lastQuery = nullptr;
+    }
+    lastSources.clear();
+  }
+
   // drop `graph`: freed now, or kept in `retired` if the ABI refuses
   void retireGraph() {
+    dropQuery();
     if (graph && spf_graph_destroy(graph) != SPF_OK) {
       retired.push_back(graph);
     }

@@ -629,16 +629,40 @@ std::vector<std::unique_ptr<SpfView>> runBatch(
     qd.ignore_offsets = ioff.data();
     qd.ignore_links = ilinks.data();
   }
+  const char* cacheEnv = std::getenv("OPENR_LS_QUERY_CACHE"); // (read per batch: A/B)
+  const bool cacheQuery = !(cacheEnv && std::atoi(cacheEnv) == 0);
+  const bool reuse = cacheQuery && !ignore;
   spf_query* q = nullptr;
-  int s = spf_query_create(eng.graph, &qd, &q);
-  if (s != SPF_OK) {
-    engineFailure("spf_query_create", s);
+  int s = SPF_OK;
+  if (reuse && eng.lastQuery && eng.lastFlags == flags && eng.lastSources == sources) {
+    q = eng.lastQuery;
+    Counters::add("decision.spf_query_reuses", 1);
+  } else {
+    if (reuse) {
+      eng.dropQuery();
+    }
+    if ((s = spf_query_create(eng.graph, &qd, &q)) != SPF_OK) {
+      engineFailure("spf_query_create", s);
+    }
   }
+  // a cached query outlives the batch; any other is destroyed on return
   struct Guard {
     spf_query* q;
-    ~Guard() { spf_query_destroy(q); }
-  } guard{q};
+    ~Guard() {
+      if (q) {
+        spf_query_destroy(q);
+      }
+    }
+  } guard{reuse ? nullptr : q};
+  if (reuse && !eng.lastQuery) {
+    eng.lastQuery = q;
+    eng.lastSources = sources;
+    eng.lastFlags = flags;
+  }
   if ((s = spf_query_run(q)) != SPF_OK || (s = spf_query_sync(q)) != SPF_OK) {
+    if (q == eng.lastQuery) {
+      eng.dropQuery();
+    }
     engineFailure("spf_query_run", s);
   }
   spf_query_elapsed_ms(q, &eng.lastMs);
@@ -1437,6 +1461,7 @@ void LinkState::patchMemo(
       for (size_t i = 0; i < edges.size(); ++i) {
         eng.metric[edges[i]] = metrics[i];
       }
+      eng.dropQuery(); // (plans read the metrics: uniform, widths, buckets)
       const int s = spf_graph_patch_metrics(
           eng.graph, (uint32_t)edges.size(), edges.data(), metrics.data());
       if (s != SPF_OK) {
@@ -1779,6 +1804,7 @@ bool LinkState::patchStructure(
   const auto tu = std::chrono::steady_clock::now();
   Counters::add("decision.graph_splice_us",
                 std::chrono::duration_cast<std::chrono::microseconds>(tu - t0).count());
+  eng.dropQuery(); // (the splice changes rows, neighbour lists and plans)
   if (spf_graph_update(eng.graph, &d) != SPF_OK) {
     // the handle is never nulled while the ABI still refuses to free it
     // (live queries): retireGraph keeps it for a later destroy

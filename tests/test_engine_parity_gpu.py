@@ -447,3 +447,59 @@ def test_ksp2_route_db_trace_step_budget(mods, seed, heavy, monkeypatch):
     c = E.get_counters()
     assert c.get("decision.spf_runs") == O.get_counters().get("decision.spf_runs")
     assert c.get("decision.kth2_device_overflows", 0) > 0
+
+
+@pytest.mark.parametrize("net", ["weighted", "uniform", "grid"])
+def test_same_node_rebuilds_reuse_query(mods, net):
+    """Rebuilding one node's RouteDb under churn: a batch with the same
+    sources and flags as the last one reruns the engine's cached query
+    (Engine::lastQuery; transit bits are read at run time) and every other
+    change of the graph -- a metric patch, a link overload splice -- drops it
+    first.  On a uniform metric the LFA batch (the node and its neighbours,
+    their neighbours as helper rows) takes the small-area MS-BFS plan.
+    Every build equals the oracle's, with and without the cache
+    (OPENR_LS_QUERY_CACHE=0).  On the 8x8 grid (the bench's configs[0]
+    loop: node drains elsewhere invalidate every row of the batch) the cache
+    must be hit."""
+    import os
+    import random
+
+    from openr_amd import topologies as TP
+
+    E, O = mods
+    if net == "grid":
+        topo = TP.grid(8)
+        names = topo.names
+        adj_dbs, prefix_dbs = {"0": topo.adj_dbs()}, topo.prefix_dbs()
+        me = "1"
+    else:
+        names, adj_dbs, prefix_dbs = RZ.random_network(
+            700, n_nodes=40, n_links=90, metric_range=(1, 1) if net == "uniform" else (1, 20))
+        me = names[0]
+    ea, ep = RZ.load(E, adj_dbs, prefix_dbs, 3)
+    oa, op = RZ.load(O, adj_dbs, prefix_dbs, 3)
+    es = E.SpfSolver(me, True, True)
+    os_ = O.SpfSolver(me, True, True)
+    rng = random.Random(5)
+    dbs = [copy.deepcopy(d) for d in adj_dbs["0"]]
+    E.reset_counters()
+    try:
+        for step in range(30):
+            os.environ["OPENR_LS_QUERY_CACHE"] = "0" if step % 8 == 7 else "1"
+            db = rng.choice(dbs)
+            kind = rng.random()
+            if kind < 0.7 or not db.adjacencies:
+                db.isOverloaded = not db.isOverloaded
+            elif kind < 0.88:
+                adj = rng.choice(db.adjacencies)
+                adj.metric = 1 if net != "weighted" and step % 3 else rng.randint(1, 20)
+            else:
+                adj = rng.choice(db.adjacencies)
+                adj.isOverloaded = not adj.isOverloaded
+            assert ea["0"].updateAdjacencyDatabase(db) == oa["0"].updateAdjacencyDatabase(db)
+            for _ in range(2):  # the second build of the same state hits the memo
+                assert es.buildRouteDb(me, ea, ep) == os_.buildRouteDb(me, oa, op), step
+    finally:
+        os.environ.pop("OPENR_LS_QUERY_CACHE", None)
+    if net == "grid":
+        assert E.get_counters().get("decision.spf_query_reuses", 0) > 0

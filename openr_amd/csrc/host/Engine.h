@@ -84,8 +84,8 @@ struct LinkState::Engine {
   // same sources and flags with no ignore lists: transit bits are read at run
   // time (spf_graph_set_transit keeps it), every other change of the graph
   // (metric patches, link splices, a rebuild) drops it first.  A RouteDb
-  // build on a small area pays the plan, the allocations and the uploads of
-  // spf_query_create once instead of per build.
+  // build on a small area (<= 4,096 nodes) pays the plan, the allocations
+  // and the uploads of spf_query_create once instead of per build.
   // (OPENR_LS_QUERY_CACHE=0 disables)
   spf_query* lastQuery{nullptr};
   std::vector<uint32_t> lastSources;

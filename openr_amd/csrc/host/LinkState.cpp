@@ -631,7 +631,9 @@ std::vector<std::unique_ptr<SpfView>> runBatch(
   }
   const char* cacheEnv = std::getenv("OPENR_LS_QUERY_CACHE"); // (read per batch: A/B)
   const bool cacheQuery = !(cacheEnv && std::atoi(cacheEnv) == 0);
-  const bool reuse = cacheQuery && !ignore;
+  // (small areas only: on the fabric the reuse bought nothing on the RouteDb
+  // loops and cost 4-6 ms on the KSP2 loop, A/B/A/B on one box, r06aw)
+  const bool reuse = cacheQuery && !ignore && eng.names.size() <= 4096;
   spf_query* q = nullptr;
   int s = SPF_OK;
   if (reuse && eng.lastQuery && eng.lastFlags == flags && eng.lastSources == sources) {

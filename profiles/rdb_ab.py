@@ -2,7 +2,9 @@
 on, and ksp2_route_db) under two settings of one environment switch, the
 settings interleaved so both see the same box:
 
-    python profiles/rdb_ab.py VAR OFF ON [rounds]
+    python profiles/rdb_ab.py VAR OFF ON [rounds] [ksp2]
+
+(with "ksp2" the KSP2 loop only)
 """
 import json
 import os
@@ -23,8 +25,11 @@ res = {a: [], b: []}
 for r in range(rounds):
     for val in (a, b):
         os.environ[var] = val
-        row = {"lfa": bench.route_db_rebuild_ms(topo, 0, lfa=True),
-               "plain": bench.route_db_rebuild_ms(topo, 0)}
+        if "ksp2" in sys.argv[5:]:
+            row = {"ksp2": bench.ksp2_route_db(topo, 0, iters=4)}
+        else:
+            row = {"lfa": bench.route_db_rebuild_ms(topo, 0, lfa=True),
+                   "plain": bench.route_db_rebuild_ms(topo, 0)}
         res[val].append({k: {kk: vv for kk, vv in v.items() if kk.endswith("ms_median")}
                          for k, v in row.items()})
         print(var, val, json.dumps(res[val][-1]), flush=True)

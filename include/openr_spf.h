@@ -243,6 +243,17 @@ uint32_t spf_query_row_stride(const spf_query* q);
  * caller materialises (NodeSpfResult::nextHops, LinkState.h:203-257). */
 int spf_query_fetch_nexthops(
     spf_query* q, uint32_t first, uint32_t count, uint64_t* dst);
+/* Both of the above into host memory with ONE synchronisation: the uint32
+ * distance rows of queries [first, first+count) into rows (row_pitch bytes
+ * apart; NULL skips them) and their next-hop masks into masks (the layout of
+ * spf_query_fetch_nexthops; NULL skips them).  Small batches (a RouteDb
+ * build's few sources: the node and its LFA neighbours, LinkState.cpp:
+ * 1220-1260's per-source getSpfResult) go through a pinned staging buffer,
+ * so the two transfers cost one round trip; larger ones take the two calls
+ * above.  Same errors as those. */
+int spf_query_fetch_host(
+    spf_query* q, uint32_t first, uint32_t count, uint32_t* rows, size_t row_pitch,
+    uint64_t* masks);
 /* getKthPaths' trace loop on the device (LinkState.cpp:776-786 over
  * traceOnePath, :398-419): for queries [first, first+count), repeated
  * traceOnePath from the query's source to dests[i] over the query's own

@@ -72,6 +72,7 @@ EXPORTED_SYMBOLS = (
     "spf_query_row_stride",
     "spf_query_fetch_rows",
     "spf_query_fetch_nexthops",
+    "spf_query_fetch_host",
     "spf_query_trace_paths",
     "spf_query_trace_fetch",
     "spf_graph_diff",
@@ -274,6 +275,7 @@ def load():
         "spf_query_row_stride": (u32, [vp]),
         "spf_query_fetch_rows": (C.c_int, [vp, u32, u32, vp, C.c_size_t, C.c_int]),
         "spf_query_fetch_nexthops": (C.c_int, [vp, u32, u32, pu64]),
+        "spf_query_fetch_host": (C.c_int, [vp, u32, u32, vp, C.c_size_t, vp]),
         "spf_query_trace_paths": (C.c_int, [vp, u32, u32, pu32, pu32, pu32]),
         "spf_query_trace_fetch": (C.c_int, [vp, pu32, pu32]),
         "spf_query_device_rows": (
@@ -719,6 +721,21 @@ class Query:
         _check(load().spf_query_fetch_nexthops(self.h, first, count, _p(out, C.c_uint64)),
                "fetch_nexthops")
         return out[:n]
+
+    def fetch_host(self, first: int, count: int, rows=True, masks=True):
+        """Rows and masks of queries [first, first+count) in one call
+        (spf_query_fetch_host): (rows [count, V] uint32 or None, masks as
+        fetch_nexthops or None)."""
+        V = self.graph.V
+        r = np.zeros((count, V), dtype=np.uint32) if rows else None
+        m = None
+        if masks:
+            n = sum(V * self.nh_words(i) for i in range(first, first + count))
+            m = np.zeros(max(n, 1), dtype=np.uint64)
+        _check(load().spf_query_fetch_host(
+            self.h, first, count, r.ctypes.data if rows else None, V * 4,
+            m.ctypes.data if masks else None), "fetch_host")
+        return r, (m[:n] if masks else None)
 
     def trace_paths(self, dests, first: int = 0):
         """getKthPaths' trace loop on the device (spf_query_trace_paths +

@@ -699,9 +699,6 @@ std::vector<std::unique_ptr<SpfView>> runBatch(
         eng.rowBlock = rows32;
       }
     }
-    if ((s = spf_query_fetch_rows(q, 0, nq, rows32->data(), (size_t)V * 4, 0)) != SPF_OK) {
-      engineFailure("spf_query_fetch_rows", s);
-    }
   }
   if (wantNextHops) {
     for (uint32_t i = 0; i < nq; ++i) {
@@ -710,9 +707,13 @@ std::vector<std::unique_ptr<SpfView>> runBatch(
     }
     if (nq > 1) {
       masks.resize(maskOff[nq]);
-      if ((s = spf_query_fetch_nexthops(q, 0, nq, masks.data())) != SPF_OK) {
-        engineFailure("spf_query_fetch_nexthops", s);
-      }
+    }
+  }
+  // rows and masks in one call: one synchronisation for both transfers
+  if (rows32 || !masks.empty()) {
+    if ((s = spf_query_fetch_host(q, 0, nq, rows32 ? rows32->data() : nullptr, (size_t)V * 4,
+                                  masks.empty() ? nullptr : masks.data())) != SPF_OK) {
+      engineFailure("spf_query_fetch_host", s);
     }
   }
   auto fill = [&](size_t i, unsigned) {

@@ -13242,6 +13242,108 @@ int spf_query_fetch_nexthops(
   return SPF_OK;
 }
 
+} // extern "C"
+
+namespace {
+// pinned host staging for spf_query_fetch_host: one buffer per process
+// (portable across devices), grown to the largest small request, never freed
+struct HostStage {
+  std::mutex mu;
+  uint8_t* p = nullptr;
+  size_t cap = 0;
+};
+HostStage& host_stage() {
+  static HostStage s;
+  return s;
+}
+constexpr size_t kHostStageMax = (size_t)4 << 20;
+} // namespace
+
+extern "C" {
+
+int spf_query_fetch_host(
+    spf_query* q, uint32_t first, uint32_t count, uint32_t* rows, size_t row_pitch,
+    uint64_t* masks) {
+  SPF_ABI_RANGE("spf_query_fetch_host");
+  if (!q) {
+    return fail(SPF_E_INVALID, "null argument");
+  }
+  if (!q->ran) {
+    return fail(SPF_E_INVALID, "query has not run");
+  }
+  if ((uint64_t)first + count > q->nq) {
+    return fail(SPF_E_INVALID, "row range out of bounds");
+  }
+  if (masks && !(q->flags & SPF_F_NEXTHOPS)) {
+    return fail(SPF_E_INVALID, "no next hops for this query");
+  }
+  if (rows && rows64(q)) {
+    return fail(SPF_E_UNSUPPORTED, "64-bit distance rows: use spf_query_dist");
+  }
+  const size_t V = q->g->V;
+  if (rows && row_pitch < V * 4) {
+    return fail(SPF_E_INVALID, "destination pitch < 4*V");
+  }
+  if (count == 0 || V == 0 || (!rows && !masks)) {
+    return SPF_OK;
+  }
+  const size_t rb = rows ? (((size_t)count * V * 4 + 255) & ~(size_t)255) : 0;
+  const uint64_t lo = masks ? q->nhb_off[first] : 0;
+  const uint64_t hi =
+      !masks ? 0 : (first + count < q->nq ? q->nhb_off[first + count] : q->nhb_total);
+  const size_t mb = (size_t)(hi - lo);
+  if (rb + mb > kHostStageMax || !env_flag("OPENR_SPF_FETCH_STAGE", 1)) {
+    if (rows) {
+      if (const int st = spf_query_fetch_rows(q, first, count, rows, row_pitch, 0)) {
+        return st;
+      }
+    }
+    return masks ? spf_query_fetch_nexthops(q, first, count, masks) : SPF_OK;
+  }
+  HostStage& hs = host_stage();
+  std::lock_guard<std::mutex> lk(hs.mu);
+  HIP_TRY(hipSetDevice(q->g->device));
+  if (hs.cap < rb + mb) {
+    if (hs.p) {
+      HIP_TRY(hipHostFree(hs.p));
+      hs.p = nullptr;
+      hs.cap = 0;
+    }
+    const size_t want = std::max<size_t>(rb + mb, (size_t)64 << 10);
+    HIP_TRY(hipHostMalloc((void**)&hs.p, want, hipHostMallocPortable));
+    hs.cap = want;
+  }
+  hipStream_t st = q->g->stream;
+  if (rows) {
+    HIP_TRY(hipMemcpy2DAsync(hs.p, V * 4, (const char*)q->d_dist + (size_t)first * q->Vp * 4,
+                             (size_t)q->Vp * 4, V * 4, count, hipMemcpyDeviceToHost, st));
+  }
+  if (mb) {
+    HIP_TRY(hipMemcpyAsync(hs.p + rb, q->d_nhb + lo, mb, hipMemcpyDeviceToHost, st));
+  }
+  HIP_TRY(hipStreamSynchronize(st));
+  if (rows) {
+    for (uint32_t i = 0; i < count; ++i) {
+      std::memcpy(reinterpret_cast<uint8_t*>(rows) + (size_t)i * row_pitch,
+                  hs.p + (size_t)i * V * 4, V * 4);
+    }
+  }
+  if (masks) {
+    uint64_t out = 0;
+    for (uint32_t i = first; i < first + count; ++i) {
+      const size_t n = V * q->nh_w[i];
+      const uint8_t* src = hs.p + rb + (q->nhb_off[i] - lo);
+      if (q->nh_b[i] >= 8) {
+        std::memcpy(masks + out, src, n * 8);
+      } else {
+        widen_masks(src, q->nh_b[i], V, masks + out);
+      }
+      out += n;
+    }
+  }
+  return SPF_OK;
+}
+
 uint32_t spf_query_row_stride(const spf_query* q) {
   if (!q) {
     return 0;

@@ -6,6 +6,7 @@ Covers: positive / unit / zero / negative (uint64 wrap) metrics, overloaded
 memory and exact kernels.  Bit-exact distances and next-hop sets.
 """
 
+import os
 import random
 
 import numpy as np
@@ -420,6 +421,24 @@ def test_bulk_fetch_matches_row_reads(gpu_ready):
         assert (flat[off : off + m.size] == m).all()
         off += m.size
     assert off == flat.size
+    # spf_query_fetch_host: both in one call, through the pinned staging
+    # buffer (small) and through the two plain calls (staging off), over a
+    # sub-range, rows or masks alone
+    for stage in ("1", "0"):
+        os.environ["OPENR_SPF_FETCH_STAGE"] = stage
+        try:
+            r2, f2 = q.fetch_host(0, len(srcs))
+            assert (r2 == rows).all() and (f2 == flat).all()
+            r3, f3 = q.fetch_host(5, 7)
+            lo = sum(q.nexthops(i).size for i in range(5))
+            assert (r3 == rows[5:12]).all()
+            assert (f3 == flat[lo : lo + f3.size]).all()
+            assert q.fetch_host(3, 2, masks=False)[1] is None
+            lo3 = sum(q.nexthops(i).size for i in range(3))
+            n3 = q.nexthops(3).size + q.nexthops(4).size
+            assert (q.fetch_host(3, 2, rows=False)[1] == flat[lo3 : lo3 + n3]).all()
+        finally:
+            os.environ.pop("OPENR_SPF_FETCH_STAGE", None)
     del g_query
 
 

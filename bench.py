@@ -1629,9 +1629,9 @@ def fabric_sharded(args, topo, world, rank, local, dist, cluster):
             "parallelism": f"contiguous source blocks over {world} GPUs inside the engine "
                            "(spf_table, RCCL cluster); rows stay on their owner GPU",
         },
-        "gteps_equivalent": {"value": round(V * E / (step_ms / 1000.0) / 1e9, 2),
-                             "note": "per-source-equivalent (sources x directed edges / step), "
-                                     "not a measured rate"},
+        "derived": {"gteps_equivalent": {
+            "value": round(V * E / (step_ms / 1000.0) / 1e9, 2),
+            "note": "per-source-equivalent (sources x directed edges / step), not a measured rate"}},
         "device_compute_ms": round(comp_ms, 4),
         "with_row_gather": {
             "what": "the same table with every GPU's uint32 distance rows all-gathered over xGMI "
@@ -1785,11 +1785,11 @@ def fabric_single(args, topo, world, rank, local, dist):
             "kernel": kname,
             "parallelism": "one table of every source on one GPU (N > 1 runs fabric_sharded)",
         },
-        "gteps_equivalent": {
+        "derived": {"gteps_equivalent": {
             "value": round(world * nsrc * E / (step_ms / 1000.0) / 1e9, 2),
             "note": "per-source-equivalent, not a measured rate: sources x directed edges per step "
                     "time (a textbook SSSP traverses every edge once); the bit-parallel BFS scans an "
-                    "edge once per level for 64 sources, so this counts shared scans, not traffic"},
+                    "edge once per level for 64 sources, so this counts shared scans, not traffic"}},
         "kernel_ms": round(kernel_ms, 4),
         "kernels": stages,
         "kernels_launched": launched,

@@ -12011,6 +12011,12 @@ int launch_nh_levels(spf_query* q, bool unit) {
       HIP_TRY(hipGetLastError());
     }
     const uint32_t skip = env_flag("OPENR_NL_WIDE", 1) ? q->nmid : 0;
+    // with no wide source left the kernel only serves a BFS deeper than 254
+    // levels, which a graph of at most 254 nodes cannot have: no launch (a
+    // small area's RouteDb batch, e.g. the 10x10 grid)
+    if (q->nbig == skip && g->V <= 254 && env_flag("OPENR_NL_SWAR_SKIP", 1)) {
+      return SPF_OK;
+    }
     const uint32_t grid = std::max<uint32_t>(q->nbig - skip, std::min<uint32_t>(q->nq, 1024));
     SPF_LAUNCH(spf_nh_levels_swar_kernel, dim3(grid), dim3(kNsThreads), 0, g->stream,
                        a, (const uint32_t*)q->d_big + skip, q->nbig - skip);
